@@ -1,0 +1,485 @@
+// host.cpp — the C ABI of libebpfemu.so (include/ebpf_emu.h): program load (the reference's
+// decoder, ins.rs), the load-time pre-decoder to device micro-ops, batch launch, and the
+// multi-GPU counter all-reduce over RCCL.
+//
+// This file has no interpreter: execution happens only in the gfx950 kernel (interp.hip).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/ebpf_emu.h"
+#include "launch.h"
+#include "uop.h"
+
+using namespace ebpfemu;
+
+namespace {
+
+// The reference's decoded Instruction (ins.rs:37-45); `code` kept as the raw opcode byte.
+struct RefInsn {
+  int32_t imm;
+  int64_t imm64;
+  int16_t off;
+  uint8_t src, dst, code;
+};
+
+constexpr int kMaxDevices = 64;
+
+uint64_t le64(const uint8_t* p) {
+  uint64_t v = 0;
+  for (int i = 7; i >= 0; i--) v = (v << 8) | p[i];
+  return v;
+}
+
+bool is_ls(uint8_t code) { return (code & 7) <= 3; }  // ins.rs:163
+
+// u64s_to_instructions (ins.rs:96-119) over the LE image; Instruction::from (ins.rs:121-132)
+// with the panics of Register::from (ins.rs:32), AOp/JOp::from (ins.rs:251,257) and
+// Mode::from (ins.rs:187; 0x80/0xa0 are invalid discriminants) turned into error codes.
+int decode_image(const uint8_t* code, size_t nbytes, std::vector<RefInsn>& out, size_t* bad) {
+  out.clear();
+  if (nbytes % 8) {
+    if (bad) *bad = nbytes / 8;
+    return EBPF_ELEN;
+  }
+  const size_t nw = nbytes / 8;
+  for (size_t i = 0; i < nw; i++) {
+    const uint64_t w = le64(code + 8 * i);
+    RefInsn ins;
+    ins.imm = (int32_t)(uint32_t)(w >> 32);
+    ins.imm64 = (int64_t)(w >> 32);
+    ins.off = (int16_t)(uint16_t)(w >> 16);
+    ins.src = (uint8_t)((w >> 12) & 0xf);
+    ins.dst = (uint8_t)((w >> 8) & 0xf);
+    ins.code = (uint8_t)w;
+    if (bad) *bad = i;
+    if (ins.src >= 12 || ins.dst >= 12) return EBPF_EREG;
+    const uint8_t cls = ins.code & 7;
+    if (cls >= 4) {
+      if ((ins.code >> 4) > 0xd) return EBPF_EOP;
+    } else {
+      const uint8_t mode = ins.code & 0xe0;
+      if (mode > 0xc0 || mode == 0x80 || mode == 0xa0) return EBPF_EMODE;
+      if (mode == 0x00) {  // wide: fold the next word (ins.rs:107-114)
+        if (++i >= nw) return EBPF_ELDDW;
+        int64_t sum;
+        if (__builtin_add_overflow((int64_t)(uint32_t)ins.imm, (int64_t)le64(code + 8 * i), &sum))
+          return EBPF_ELDDW_OVF;
+        ins.imm64 = sum;
+        ins.imm = 0;
+      }
+    }
+    out.push_back(ins);
+  }
+  return EBPF_OK;
+}
+
+Uop fault_uop(uint8_t status) {
+  Uop u{};
+  u.op = U_FAULT;
+  u.aux = status;
+  return u;
+}
+
+// Load-time lowering of one decoded instruction at index pc to a device micro-op
+// (the static half of emu.rs:48-451).
+Uop lower(const RefInsn& in, uint32_t pc) {
+  const uint8_t code = in.code, cls = code & 7;
+  Uop u{};
+  u.dst = in.dst;
+  u.src = in.src;
+  if (!is_ls(code)) {
+    const uint8_t op = code >> 4, source = (code >> 3) & 1;
+    // registers read before any op-specific behaviour (emu.rs:66-72,75,220): index 11 panics
+    if ((source && in.src >= 11) || in.dst >= 11) return fault_uop(EBPF_ST_INSN);
+    u.aux = source ? F_SRC : 0;
+    u.k = (int64_t)in.imm;  // `imm as i64`, emu.rs:67
+    if (!source) u.src = 0;
+    if (cls == 4 || cls == 7) {
+      const bool alu32 = cls == 4;
+      if (op == 13) {  // END (emu.rs:165-209)
+        u.aux = 0;
+        u.src = 0;
+        if (in.imm == 16) u.op = source ? U_BSWAP16 : U_ZX16;
+        else if (in.imm == 32) u.op = source ? U_BSWAP32 : U_ZX32;
+        else if (in.imm == 64) u.op = source ? U_BSWAP64 : U_NOP;
+        else return fault_uop(EBPF_ST_INSN);  // unreachable! emu.rs:206
+        return u;
+      }
+      u.op = (uint8_t)((alu32 ? U_ADD32 : U_ADD64) + op);
+      return u;
+    }
+    // JMP / JMP32 (emu.rs:218-304)
+    const uint32_t target = (pc + 1) + (uint32_t)(int32_t)in.off;  // wrapping_add_signed
+    u.x = (int32_t)target;
+    const bool j32 = cls == 6;
+    switch (op) {
+      case 0: u.op = U_JA; u.aux = 0; u.src = 0; return u;  // JA, also in JMP32 (Q26)
+      case 1: u.op = j32 ? U_JEQ32 : U_JEQ; return u;
+      case 2: case 6: u.op = j32 ? U_JGT32 : U_JGT; return u;   // JGT == JSGT (Q2)
+      case 3: case 7: u.op = j32 ? U_JGE32 : U_JGE; return u;
+      case 4: u.op = j32 ? U_JSET32 : U_JSET; return u;
+      case 5: u.op = j32 ? U_JNE32 : U_JNE; return u;
+      case 10: case 12: u.op = j32 ? U_JLT32 : U_JLT; return u;
+      case 11: case 13: u.op = j32 ? U_JLE32 : U_JLE; return u;
+      case 8:  // CALL
+        if (source) return fault_uop(EBPF_ST_INSN);          // callx: todo!() emu.rs:270
+        if (target == 0xFFFFFFFFu) return fault_uop(EBPF_ST_ARITH);  // pc + 1 overflow
+        u.op = U_CALL; u.aux = 0; u.src = 0;
+        return u;
+      case 9: u.op = U_EXIT; u.aux = 0; u.src = 0; return u;
+      default: return fault_uop(EBPF_ST_INSN);
+    }
+  }
+  // LS (emu.rs:311-444): src, r0 and dst are read first (emu.rs:320-322)
+  if (in.src >= 11 || in.dst >= 11) return fault_uop(EBPF_ST_INSN);
+  const uint8_t mode = code & 0xe0, size = code & 0x18;
+  const uint8_t w = size == 0x00 ? 4 : size == 0x08 ? 2 : size == 0x10 ? 1 : 8;
+  u.x = (int32_t)in.off;
+  if (cls == 0 || cls == 1) {
+    if (mode == 0x00) { u.op = U_LDIMM; u.k = in.imm64; u.src = 0; return u; }
+    if (mode == 0x60 && cls == 1) { u.op = U_LDX; u.aux = w; return u; }
+    return fault_uop(EBPF_ST_INSN);  // ABS/IND (:336), LD+MEM (:339), ATOMIC (:351)
+  }
+  if (mode == 0x60) {
+    u.aux = w;
+    if (cls == 2) { u.op = U_ST; u.k = in.imm64; u.src = 0; }  // zero-extended imm (Q8)
+    else u.op = U_STX;
+    return u;
+  }
+  if (mode == 0xc0) {  // ATOMIC (emu.rs:373-437), ST class behaves like STX here
+    u.op = U_ATOMIC;
+    u.aux = (uint8_t)((size == 0 ? F_ATOMIC32 : 0) | ((in.imm64 & 1) ? F_FETCH : 0));
+    const int64_t aop = in.imm64 & 0xfe;
+    const bool known = aop == 0x00 || aop == 0x40 || aop == 0x50 || aop == 0xa0 || aop == 0xe0 ||
+                       aop == 0xf0;
+    u.k = known ? aop : 0xff;  // unknown op faults only after the 8-byte read (emu.rs:375,421)
+    return u;
+  }
+  return fault_uop(EBPF_ST_INSN);  // ST/STX with IMM/ABS/IND (emu.rs:438)
+}
+
+int parse_hex_u64s(const char* hex, std::vector<uint8_t>& image) {
+  // hexs_to_u64s (ins.rs:60-74): trim, drop spaces, 16-digit chunks, u64::from_str_radix
+  std::string s(hex ? hex : "");
+  size_t b = 0, e = s.size();
+  while (b < e && isspace((unsigned char)s[b])) b++;
+  while (e > b && isspace((unsigned char)s[e - 1])) e--;
+  std::string t;
+  for (size_t i = b; i < e; i++)
+    if (s[i] != ' ') t.push_back(s[i]);
+  image.clear();
+  for (size_t i = 0; i < t.size(); i += 16) {
+    if (i + 16 > t.size()) return EBPF_ELEN;  // "invalid hex format for u64"
+    uint64_t v = 0;
+    for (size_t j = 0; j < 16; j++) {
+      const char c = t[i + j];
+      int d;
+      if (c >= '0' && c <= '9') d = c - '0';
+      else if (c >= 'a' && c <= 'f') d = c - 'a' + 10;
+      else if (c >= 'A' && c <= 'F') d = c - 'A' + 10;
+      else if (c == '+' && j == 0) continue;  // from_str_radix accepts a leading '+'
+      else return EBPF_EHEX;
+      v = (v << 4) | (uint64_t)d;
+    }
+    for (int k = 7; k >= 0; k--) image.push_back((uint8_t)(v >> (8 * k)));  // BE text -> LE image
+  }
+  return EBPF_OK;
+}
+
+struct DevWorkspace {
+  void* ptr = nullptr;
+  uint64_t bytes = 0;
+};
+
+std::mutex g_ws_mu;
+std::map<std::pair<int, void*>, DevWorkspace> g_ws;  // (device, stream) -> library scratch
+
+int device_of_current() {
+  int d = 0;
+  hipGetDevice(&d);
+  return d;
+}
+
+}  // namespace
+
+struct ebpf_prog {
+  std::vector<RefInsn> insns;
+  std::vector<Uop> uops;
+  int tier = 0;
+  std::mutex mu;
+  Uop* dev_uops[kMaxDevices] = {};
+};
+
+extern "C" {
+
+void ebpf_batch_init(ebpf_batch* b) {
+  if (!b) return;
+  std::memset(b, 0, sizeof *b);
+  b->mem_size = EBPF_DEFAULT_MEM;
+  b->r10 = EBPF_DEFAULT_R10;
+  b->max_steps = EBPF_DEFAULT_STEPS;
+}
+
+int ebpf_prog_load(const uint8_t* code, size_t nbytes, ebpf_prog** out, size_t* bad_word) {
+  if (!out || (!code && nbytes)) return EBPF_EINVAL;
+  *out = nullptr;
+  std::vector<RefInsn> insns;
+  int rc = decode_image(code, nbytes, insns, bad_word);
+  if (rc) return rc;
+  if (insns.size() > EBPF_MAX_INSNS) return EBPF_ETOOBIG;
+  ebpf_prog* p = new (std::nothrow) ebpf_prog;
+  if (!p) return EBPF_ENOMEM;
+  p->insns = std::move(insns);
+  p->uops.reserve(p->insns.size());
+  for (size_t i = 0; i < p->insns.size(); i++) {
+    Uop u = lower(p->insns[i], (uint32_t)i);
+    if (u.op == U_FAULT) { u.dst = 0; u.src = 0; }  // the kernel never indexes a bad register
+    if (u.op == U_ST || u.op == U_STX || u.op == U_ATOMIC || u.op == U_CALL) p->tier = 1;
+    p->uops.push_back(u);
+  }
+  *out = p;
+  return EBPF_OK;
+}
+
+int ebpf_prog_load_hex(const char* hex, ebpf_prog** out, size_t* bad_word) {
+  std::vector<uint8_t> image;
+  int rc = parse_hex_u64s(hex, image);
+  if (rc) {
+    if (bad_word) *bad_word = 0;
+    return rc;
+  }
+  return ebpf_prog_load(image.data(), image.size(), out, bad_word);
+}
+
+void ebpf_prog_free(ebpf_prog* p) {
+  if (!p) return;
+  int cur = device_of_current();
+  for (int d = 0; d < kMaxDevices; d++) {
+    if (p->dev_uops[d]) {
+      hipSetDevice(d);
+      hipFree(p->dev_uops[d]);
+    }
+  }
+  hipSetDevice(cur);
+  delete p;
+}
+
+size_t ebpf_prog_len(const ebpf_prog* p) { return p ? p->insns.size() : 0; }
+
+int ebpf_prog_insn(const ebpf_prog* p, size_t i, int32_t* imm, int64_t* imm64, int16_t* off,
+                   uint8_t* src, uint8_t* dst, uint8_t* code) {
+  if (!p || i >= p->insns.size()) return EBPF_EINVAL;
+  const RefInsn& r = p->insns[i];
+  if (imm) *imm = r.imm;
+  if (imm64) *imm64 = r.imm64;
+  if (off) *off = r.off;
+  if (src) *src = r.src;
+  if (dst) *dst = r.dst;
+  if (code) *code = r.code;
+  return EBPF_OK;
+}
+
+int ebpf_prog_tier(const ebpf_prog* p) { return p ? p->tier : -1; }
+
+int ebpf_prog_upload(ebpf_prog* p, int device) {
+  if (!p || device < 0 || device >= kMaxDevices) return EBPF_EINVAL;
+  std::lock_guard<std::mutex> lk(p->mu);
+  if (p->dev_uops[device]) return EBPF_OK;
+  int cur = device_of_current();
+  if (hipSetDevice(device) != hipSuccess) return EBPF_EHIP;
+  const size_t bytes = std::max<size_t>(1, p->uops.size()) * sizeof(Uop);
+  Uop* d = nullptr;
+  int rc = EBPF_OK;
+  if (hipMalloc(&d, bytes) != hipSuccess) rc = EBPF_EHIP;
+  else if (!p->uops.empty() &&
+           hipMemcpy(d, p->uops.data(), p->uops.size() * sizeof(Uop), hipMemcpyHostToDevice) !=
+               hipSuccess)
+    rc = EBPF_EHIP;
+  if (rc == EBPF_OK) p->dev_uops[device] = d;
+  else if (d) hipFree(d);
+  hipSetDevice(cur);
+  return rc;
+}
+
+uint64_t ebpf_workspace_bytes(const ebpf_prog* p, const ebpf_batch* b, int device) {
+  if (!p || !b) return 0;
+  uint64_t bytes = kWsSlotsOff;
+  if (p->tier == 1) {
+    int cur = device_of_current();
+    hipSetDevice(device);
+    int grid = 0;
+    interp_grid(p->tier, (uint32_t)p->uops.size(), (b->n + 63) / 64, &grid);
+    hipSetDevice(cur);
+    bytes += (uint64_t)grid * kWavesPerBlock * tier1_slot_bytes(b->mem_size);
+  }
+  return bytes;
+}
+
+static int check_batch(const ebpf_batch* b) {
+  if (!b) return EBPF_EINVAL;
+  if (b->mem_size < 8 || b->mem_size % 8 || b->mem_size > (1u << 24)) return EBPF_EINVAL;
+  if (b->max_steps == 0) return EBPF_EINVAL;
+  if (b->n && !b->frames) return EBPF_EINVAL;
+  if (!b->offsets && b->stride == 0 && !b->lens) return EBPF_EINVAL;
+  if (b->flags != 0) return EBPF_EINVAL;
+  return EBPF_OK;
+}
+
+int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* b, const ebpf_batch_out* out,
+                   ebpf_stream_t stream) {
+  if (!p || !out) return EBPF_EINVAL;
+  int rc = check_batch(b);
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  int device = 0;
+  if (s) {
+    if (hipStreamGetDevice(s, &device) != hipSuccess) return EBPF_EHIP;
+  } else {
+    device = device_of_current();
+  }
+  if (b->n == 0) return EBPF_OK;
+  rc = ebpf_prog_upload(p, device);
+  if (rc) return rc;
+  int cur = device_of_current();
+  if (cur != device) hipSetDevice(device);
+
+  const uint64_t n_tiles = (b->n + 63) / 64;
+  int grid = 0;
+  if (interp_grid(p->tier, (uint32_t)p->uops.size(), n_tiles, &grid) != 0) {
+    if (cur != device) hipSetDevice(cur);
+    return EBPF_EHIP;
+  }
+  // scratch: caller-provided or library-owned per (device, stream)
+  uint64_t need = ebpf_workspace_bytes(p, b, device);
+  uint8_t* ws = (uint8_t*)b->workspace;
+  if (ws && b->workspace_bytes < need) {
+    if (cur != device) hipSetDevice(cur);
+    return EBPF_EINVAL;
+  }
+  if (!ws) {
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    DevWorkspace& w = g_ws[{device, (void*)s}];
+    if (w.bytes < need) {
+      if (w.ptr) {
+        hipStreamSynchronize(s);
+        hipFree(w.ptr);
+        w.ptr = nullptr;
+        w.bytes = 0;
+      }
+      if (hipMalloc(&w.ptr, need) != hipSuccess) {
+        if (cur != device) hipSetDevice(cur);
+        return EBPF_ENOMEM;
+      }
+      if (hipMemset(w.ptr, 0, kWsSlotsOff) != hipSuccess) {  // ticket + shards start at zero
+        if (cur != device) hipSetDevice(cur);
+        return EBPF_EHIP;
+      }
+      w.bytes = need;
+    }
+    ws = (uint8_t*)w.ptr;
+  }
+  LaunchArgs a{};
+  a.prog = p->dev_uops[device];
+  a.n_uops = (uint32_t)p->uops.size();
+  a.mem_size = b->mem_size;
+  a.frames = b->frames;
+  a.offsets = b->offsets;
+  a.lens = b->lens;
+  a.stride = b->stride;
+  a.n = b->n;
+  a.r10 = b->r10;
+  a.max_steps = b->max_steps;
+  a.verdict = out->verdict;
+  a.r0 = out->r0;
+  a.status = out->status;
+  a.counters = out->counters;
+  a.ticket = (uint32_t*)ws;
+  a.shards = (uint64_t*)(ws + kWsShardsOff);
+  a.image_ws = ws + kWsSlotsOff;
+  a.n_tiles = n_tiles;
+  a.init_regs = b->init_regs;
+  a.mem_out = out->mem;
+  a.regs_out = out->regs;
+  hipError_t e = launch_interp(p->tier, a, grid, s);
+  if (cur != device) hipSetDevice(cur);
+  return e == hipSuccess ? EBPF_OK : EBPF_EHIP;
+}
+
+int ebpf_run_batch_multi(ebpf_prog* p, int nshards, const int* devices, const ebpf_batch* batches,
+                         const ebpf_batch_out* outs, ebpf_stream_t const* streams) {
+  if (!p || nshards <= 0 || nshards > kMaxDevices || !devices || !batches || !outs || !streams)
+    return EBPF_EINVAL;
+  for (int s = 0; s < nshards; s++)
+    if (!outs[s].counters || !streams[s]) return EBPF_EINVAL;
+  int cur = device_of_current();
+  // per-shard launches: independent, no data-path exchange
+  for (int s = 0; s < nshards; s++) {
+    if (hipSetDevice(devices[s]) != hipSuccess) return EBPF_EHIP;
+    hipMemsetAsync(outs[s].counters, 0, EBPF_NCOUNTERS * sizeof(uint64_t),
+                   (hipStream_t)streams[s]);
+    int rc = ebpf_run_batch(p, &batches[s], &outs[s], streams[s]);
+    if (rc) { hipSetDevice(cur); return rc; }
+  }
+  // the one exchange step: sum the counters across GPUs over RCCL / xGMI
+  static std::mutex mu;
+  static std::map<std::vector<int>, std::vector<ncclComm_t>> comms;
+  std::vector<int> key(devices, devices + nshards);
+  std::vector<ncclComm_t>* cs;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = comms.find(key);
+    if (it == comms.end()) {
+      std::vector<ncclComm_t> c(nshards);
+      if (ncclCommInitAll(c.data(), nshards, devices) != ncclSuccess) {
+        hipSetDevice(cur);
+        return EBPF_ERCCL;
+      }
+      it = comms.emplace(key, std::move(c)).first;
+    }
+    cs = &it->second;
+  }
+  if (ncclGroupStart() != ncclSuccess) { hipSetDevice(cur); return EBPF_ERCCL; }
+  for (int s = 0; s < nshards; s++) {
+    hipSetDevice(devices[s]);
+    if (ncclAllReduce(outs[s].counters, outs[s].counters, EBPF_NCOUNTERS, ncclUint64, ncclSum,
+                      (*cs)[s], (hipStream_t)streams[s]) != ncclSuccess) {
+      ncclGroupEnd();
+      hipSetDevice(cur);
+      return EBPF_ERCCL;
+    }
+  }
+  int rc = ncclGroupEnd() == ncclSuccess ? EBPF_OK : EBPF_ERCCL;
+  hipSetDevice(cur);
+  return rc;
+}
+
+const char* ebpf_strerror(int err) {
+  switch (err) {
+    case EBPF_OK: return "ok";
+    case EBPF_EINVAL: return "invalid argument";
+    case EBPF_ELEN: return "invalid hex format for u64";  // ins.rs:67
+    case EBPF_EREG: return "register index >= 12 (ins.rs:32)";
+    case EBPF_EOP: return "ALU/JMP operation > 0xd (ins.rs:251,257)";
+    case EBPF_EMODE: return "invalid load/store mode (ins.rs:187)";
+    case EBPF_ELDDW: return "wide instruction without second word (ins.rs:112)";
+    case EBPF_ELDDW_OVF: return "wide immediate overflows i64 (ins.rs:112)";
+    case EBPF_EHEX: return "invalid hex digit";
+    case EBPF_ENOMEM: return "out of device memory";
+    case EBPF_EHIP: return "HIP runtime error";
+    case EBPF_ETOOBIG: return "program too large";
+    case EBPF_ERCCL: return "RCCL error";
+    default: return "unknown error";
+  }
+}
+
+const char* ebpf_version(void) { return "ebpfemu 0.1 gfx950"; }
+
+}  // extern "C"

@@ -1,0 +1,561 @@
+// interp.hip — the batched eBPF/XDP interpreter for MI355X (gfx950 / CDNA4).
+//
+// Replaces the reference's fetch-decode-execute loop (src/emu.rs:48-458) and flat memory
+// (src/mmu.rs:1-31). One lane interprets the program over one packet; one wave64 holds 64
+// packets (a "tile"). Design:
+//   * the pre-decoded micro-op table (uop.h) is staged ONCE per workgroup in LDS; a fetch is a
+//     wave-uniform LDS broadcast read whose fields go to SGPRs (readfirstlane), so dispatch is a
+//     scalar branch and register indices are scalar (s_set_gpr_idx VGPR indexing, no scratch);
+//   * re-convergence by min-pc: lanes whose pc equals the wave's minimum pc execute the step;
+//     the all-lanes-agree case is one readfirstlane + one compare-ballot, the divergent case a
+//     DPP wave-min. Lanes that are done (exit, fall-off, fault) park at pc = 0xFFFFFFFF;
+//   * memory tier 0 (programs without stores/calls): the first 64 bytes of each packet are
+//     staged in a padded per-lane LDS window with coalesced 16-byte HBM loads (4 lanes per
+//     packet, 16 packets per wave instruction); reads beyond it go to HBM with dword-aligned
+//     loads, bytes past the packet read as zero, exactly as the reference's zeroed image does;
+//   * memory tier 1 (stores, atomics or calls present): each lane owns a lane-interleaved copy
+//     of the reference's whole memory image plus a frame stack in device scratch;
+//   * every mmu.rs bounds check is inlined; faults become per-packet status codes.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/ebpf_emu.h"
+#include "launch.h"
+#include "uop.h"
+
+namespace ebpfemu {
+
+__device__ __forceinline__ uint32_t rfl(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+
+// Minimum over the 64 lanes (all lanes active) — DPP row shifts + row broadcasts (gfx9 DPP).
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x111, 0xf, 0xf, false));
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x112, 0xf, 0xf, false));
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x114, 0xf, 0xf, false));
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x118, 0xf, 0xf, false));
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x142, 0xa, 0xf, false));
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x143, 0xc, 0xf, false));
+  return __builtin_amdgcn_readlane(v, 63);
+}
+
+__device__ __forceinline__ uint64_t wmask(uint32_t w) {
+  return w >= 8 ? ~0ull : ((1ull << (8 * w)) - 1);
+}
+
+__device__ __forceinline__ uint32_t bswap32(uint32_t v) { return __builtin_bswap32(v); }
+
+// Bytes [a, a+w) of a packet at `base` whose length is len, with a < len; bytes at or past len
+// read as zero (the zeroed image, main.rs:16). Only dwords holding at least one packet byte
+// are loaded, so no access leaves the page of a valid byte.
+__device__ __forceinline__ uint64_t pkt_read(const uint8_t* base, uint32_t a, uint32_t w,
+                                             uint32_t len) {
+  if (w == 1) return base[a];
+  const uintptr_t p = (uintptr_t)base + a;
+  const uintptr_t end = (uintptr_t)base + len;
+  const uint32_t* p4 = (const uint32_t*)(p & ~(uintptr_t)3);
+  const uint32_t s = (uint32_t)(p & 3);
+  const uint32_t d0 = p4[0];
+  const uint32_t d1 = ((uintptr_t)(p4 + 1) < end) ? p4[1] : 0u;
+  uint64_t v = __builtin_amdgcn_alignbyte(d1, d0, s);
+  if (w == 8) {
+    const uint32_t d2 = ((uintptr_t)(p4 + 2) < end) ? p4[2] : 0u;
+    v |= (uint64_t)__builtin_amdgcn_alignbyte(d2, d1, s) << 32;
+  }
+  const uint32_t valid = len - a;
+  if (valid < w) v &= wmask(valid);
+  return v & wmask(w);
+}
+
+// Bytes [a, a+w) of the lane's LDS window (a + w <= kWin).
+__device__ __forceinline__ uint64_t win_read(const uint8_t* win, uint32_t a, uint32_t w) {
+  const uint32_t* p = (const uint32_t*)(win + (a & ~3u));
+  const uint32_t s = a & 3;
+  const uint32_t d0 = p[0], d1 = p[1];
+  uint64_t v = __builtin_amdgcn_alignbyte(d1, d0, s);
+  if (w == 8) v |= (uint64_t)__builtin_amdgcn_alignbyte(p[2], d1, s) << 32;
+  return v & wmask(w);
+}
+
+// ---- tier-1 image: lane-interleaved dwords, dword d of this lane at img[d * 64] ----
+__device__ __forceinline__ uint64_t img_read(const uint32_t* img, uint32_t a, uint32_t w) {
+  const uint32_t* p = img + (size_t)(a >> 2) * kWave;
+  const uint32_t s = a & 3;
+  const uint32_t d0 = p[0];
+  const uint32_t d1 = (s + w > 4) ? p[kWave] : 0u;
+  uint64_t v = __builtin_amdgcn_alignbyte(d1, d0, s);
+  if (w == 8) {
+    const uint32_t d2 = s ? p[2 * kWave] : 0u;
+    v |= (uint64_t)__builtin_amdgcn_alignbyte(d2, d1, s) << 32;
+  }
+  return v & wmask(w);
+}
+
+__device__ __forceinline__ void img_write(uint32_t* img, uint32_t a, uint32_t w, uint64_t v) {
+  uint32_t* p = img + (size_t)(a >> 2) * kWave;
+  const uint32_t s = a & 3;
+  if (w == 1) {
+    ((uint8_t*)p)[s] = (uint8_t)v;
+    return;
+  }
+  const uint64_t m = wmask(w);
+  const uint64_t vm = v & m;
+  const uint64_t m01 = m << (8 * s), v01 = vm << (8 * s);
+  const uint32_t mlo = (uint32_t)m01, mhi = (uint32_t)(m01 >> 32);
+  if (mlo) p[0] = (p[0] & ~mlo) | (uint32_t)v01;
+  if (mhi) p[kWave] = (p[kWave] & ~mhi) | (uint32_t)(v01 >> 32);
+  if (s && w == 8) {
+    const uint32_t m2 = (uint32_t)(m >> (64 - 8 * s)), v2 = (uint32_t)(vm >> (64 - 8 * s));
+    p[2 * kWave] = (p[2 * kWave] & ~m2) | v2;
+  }
+}
+
+template <int TIER>
+__global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint32_t nu = a.n_uops;
+  const bool lds_prog = nu <= (uint32_t)kMaxLdsUops;
+  const uint32_t prog_bytes = lds_prog ? nu * (uint32_t)sizeof(Uop) : 0u;
+  Uop* sprog = (Uop*)smem;
+  uint8_t* windows = smem + prog_bytes;
+
+  // stage the program once per workgroup (emu.instructions, emu.rs:24)
+  if (lds_prog) {
+    const uint4* src = (const uint4*)a.prog;
+    uint4* dst = (uint4*)sprog;
+    for (uint32_t i = threadIdx.x; i < nu; i += kBlock) dst[i] = src[i];
+  }
+  __syncthreads();
+
+  const uint32_t lane = threadIdx.x & (kWave - 1);
+  const uint32_t wv = threadIdx.x / kWave;
+  uint8_t* const wave_win = windows + (size_t)wv * kWave * kWinStride;
+  uint8_t* const my_win = wave_win + (size_t)lane * kWinStride;
+  const uint64_t wave_slot = (uint64_t)blockIdx.x * kWavesPerBlock + wv;
+  const uint64_t total_waves = (uint64_t)gridDim.x * kWavesPerBlock;
+  const uint32_t mem_size = a.mem_size;
+  const uint32_t max_steps = (uint32_t)(a.max_steps > 0xFFFFFFFFull ? 0xFFFFFFFFull : a.max_steps);
+
+  uint32_t* const img = TIER == 1
+      ? (uint32_t*)(a.image_ws + wave_slot * tier1_slot_bytes(mem_size)) + lane
+      : nullptr;
+  uint32_t* const cstack = TIER == 1 ? img + (size_t)(mem_size / 4) * kWave : nullptr;
+
+  uint64_t cnt[7] = {0, 0, 0, 0, 0, 0, 0};  // wave-uniform verdict buckets + faults
+  uint64_t retired = 0;                     // per lane
+
+  for (uint64_t tile = wave_slot; tile < a.n_tiles; tile += total_waves) {
+    const uint64_t pkt = tile * kWave + lane;
+    const bool valid = pkt < a.n;
+    const uint8_t* base = nullptr;
+    uint32_t len = 0;
+    if (valid) {
+      base = a.frames + (a.offsets ? (uint64_t)a.offsets[pkt] : pkt * a.stride);
+      len = a.lens ? (uint32_t)a.lens[pkt]
+                   : (uint32_t)(a.stride > 0xFFFFFFFFull ? 0xFFFFFFFFull : a.stride);
+    }
+
+    if (TIER == 0) {
+      // ---- stage the header window: coalesced when every packet base is 16-byte aligned ----
+      const bool aligned16 = ((uintptr_t)base & 15) == 0;
+      if (ballot(valid && !aligned16) == 0) {
+        const uint32_t c = lane & 3;
+        uint4 q[4];
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int j = r * 16 + (int)(lane >> 2);
+          const uint64_t bj = (uint64_t)__shfl((long long)(uintptr_t)base, j);
+          const uint32_t lj = (uint32_t)__shfl((int)len, j);
+          q[r] = make_uint4(0, 0, 0, 0);
+          if (c * 16 < min(lj, (uint32_t)kWin)) q[r] = *(const uint4*)(bj + c * 16);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int j = r * 16 + (int)(lane >> 2);
+          const uint32_t lj = (uint32_t)__shfl((int)len, j);
+          uint32_t d[4] = {q[r].x, q[r].y, q[r].z, q[r].w};
+          uint32_t* wdst = (uint32_t*)(wave_win + (size_t)j * kWinStride + c * 16);
+#pragma unroll
+          for (int e = 0; e < 4; e++) {
+            const uint32_t off = c * 16 + e * 4;  // bytes at or past len read as zero
+            uint32_t v = d[e];
+            if (off >= lj) v = 0;
+            else if (lj - off < 4) v &= (uint32_t)wmask(lj - off);
+            wdst[e] = v;
+          }
+        }
+      } else {
+        // per-lane path for unaligned packet bases
+        uint32_t* wdst = (uint32_t*)my_win;
+        const uint32_t m = valid ? min(len, (uint32_t)kWin) : 0u;
+        for (uint32_t d = 0; d < kWin / 4; d++)
+          wdst[d] = (d * 4 < m) ? (uint32_t)pkt_read(base, d * 4, 4, len) : 0u;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+
+    // ---- Emu::default() + main.rs:14-31 register/memory layout ----
+    uint64_t r[11];
+    if (a.init_regs) {  // caller-set Emu.state.regs (emu.rs:14-17)
+#pragma unroll
+      for (int i = 0; i < 11; i++) r[i] = a.init_regs[i];
+    } else {            // main.rs:28-31
+#pragma unroll
+      for (int i = 0; i < 11; i++) r[i] = 0;
+      r[2] = len;
+      r[10] = a.r10;
+    }
+    uint32_t pc = valid ? 0u : PC_DONE;
+    uint32_t st = EBPF_ST_OK;
+    uint32_t nsteps = 0;
+    uint32_t csp = 0;
+    if (valid && len > mem_size) {  // main.rs:20-21 index panic
+      st = EBPF_ST_BADPKT;
+      pc = PC_DONE;
+    }
+    if (TIER == 1) {
+      const uint32_t md = mem_size / 4;
+      const uint32_t m = (pc != PC_DONE) ? len : 0u;
+      for (uint32_t d = 0; d < md; d++)
+        img[(size_t)d * kWave] = (d * 4 < m) ? (uint32_t)pkt_read(base, d * 4, 4, len) : 0u;
+    }
+
+    // ---- Emu::run (emu.rs:452-458) with min-pc re-convergence ----
+    uint32_t wsteps = 0;
+    for (;;) {
+      uint32_t pcs = rfl(pc);
+      if (ballot(pc != pcs) != 0) pcs = wave_min_u32(pc);
+      if (pcs >= nu) break;  // every lane exited, fell off the end or faulted
+      if (++wsteps > max_steps) {  // exact per-lane budget only once it can bind
+        if (pc == pcs && nsteps >= max_steps) {
+          st = EBPF_ST_STEPS;
+          pc = PC_DONE;
+        }
+        if (ballot(pc == pcs) == 0) continue;
+      }
+      // fetch (wave-uniform): emu.rs:49
+      uint32_t w0, w1, w2, w3;
+      if (lds_prog) {
+        const uint4 q = *(const uint4*)(sprog + pcs);
+        w0 = rfl(q.x); w1 = rfl(q.y); w2 = rfl(q.z); w3 = rfl(q.w);
+      } else {
+        const uint4 q = *(const uint4*)(a.prog + pcs);
+        w0 = rfl(q.x); w1 = rfl(q.y); w2 = rfl(q.z); w3 = rfl(q.w);
+      }
+      const uint32_t op = w0 & 0xff, dst = (w0 >> 8) & 0xff, src = (w0 >> 16) & 0xff;
+      const uint32_t aux = w0 >> 24;
+      const uint32_t x = w1;
+      const uint64_t k = (uint64_t)w2 | ((uint64_t)w3 << 32);
+
+      if (pc == pcs) {
+        nsteps++;
+        pc = pcs + 1;  // emu.rs:63
+        const uint64_t A = r[dst];
+        const uint64_t S = r[src];
+        const uint64_t B = (aux & F_SRC) ? S : k;
+        const uint32_t a32 = (uint32_t)A, b32 = (uint32_t)B;
+        uint64_t R = A;
+        bool fault = false;
+        uint32_t fst = 0;
+        switch (op) {
+          // ---- ALU64 ----
+          case U_ADD64: R = A + B; break;
+          case U_SUB64: R = A - B; break;
+          case U_MUL64: R = A * B; break;
+          case U_DIV64: R = B ? A / B : 0; break;
+          case U_OR64: R = A | B; break;
+          case U_AND64: R = A & B; break;
+          case U_LSH64: R = A << (b32 & 63); break;
+          case U_RSH64: R = A >> (b32 & 63); break;
+          case U_NEG64: R = 0 - A; break;
+          case U_MOD64: R = B ? A % B : A; break;
+          case U_XOR64: R = A ^ B; break;
+          case U_MOV64: R = B; break;
+          case U_ARSH64: {  // rotate, then multiply by the sign (Q4, emu.rs:142-164)
+            const uint32_t sh = b32 & 63;
+            const uint64_t rot = sh ? ((A >> sh) | (A << (64 - sh))) : A;
+            if ((int64_t)A < 0) {
+              if (rot == 0x8000000000000000ull) { fault = true; fst = EBPF_ST_ARITH; }
+              R = 0 - rot;
+            } else {
+              R = rot;
+            }
+            break;
+          }
+          // ---- ALU32 (Q6/Q25) ----
+          case U_ADD32: R = (uint32_t)(a32 + b32); break;
+          case U_SUB32: R = (uint32_t)(a32 - b32); break;
+          case U_MUL32: R = (uint32_t)(a32 * b32); break;
+          case U_DIV32: R = b32 ? a32 / b32 : 0u; break;
+          case U_OR32: R = a32 | b32; break;
+          case U_AND32: R = a32 & b32; break;
+          case U_LSH32: R = (uint32_t)(a32 << (b32 & 31)); break;
+          case U_RSH32: R = a32 >> (b32 & 31); break;
+          case U_NEG32: R = (uint32_t)(0u - a32); break;
+          case U_MOD32: R = b32 ? a32 % b32 : a32; break;
+          case U_XOR32: R = a32 ^ b32; break;
+          case U_MOV32: R = b32; break;
+          case U_ARSH32: {
+            const uint32_t rot = __builtin_amdgcn_alignbit(a32, a32, b32 & 31);
+            R = (int32_t)a32 < 0 ? (uint32_t)(0u - rot) : rot;
+            break;
+          }
+          // ---- END (Q7) ----
+          case U_ZX16: R = A & 0xffffull; break;
+          case U_ZX32: R = A & 0xffffffffull; break;
+          case U_NOP: break;
+          case U_BSWAP16: R = ((A & 0xff) << 8) | ((A >> 8) & 0xff); break;
+          case U_BSWAP32: R = bswap32(a32); break;
+          case U_BSWAP64: R = ((uint64_t)bswap32(a32) << 32) | bswap32((uint32_t)(A >> 32)); break;
+          // ---- JMP: signed orderings (Q2) ----
+          case U_JA: pc = x; break;
+          case U_JEQ: if (A == B) pc = x; break;
+          case U_JGT: if ((int64_t)A > (int64_t)B) pc = x; break;
+          case U_JGE: if ((int64_t)A >= (int64_t)B) pc = x; break;
+          case U_JSET: if (A & B) pc = x; break;
+          case U_JNE: if (A != B) pc = x; break;
+          case U_JLT: if ((int64_t)A < (int64_t)B) pc = x; break;
+          case U_JLE: if ((int64_t)A <= (int64_t)B) pc = x; break;
+          // ---- JMP32: sign-extended low words (Q3) ----
+          case U_JEQ32: if (a32 == b32) pc = x; break;
+          case U_JGT32: if ((int32_t)a32 > (int32_t)b32) pc = x; break;
+          case U_JGE32: if ((int32_t)a32 >= (int32_t)b32) pc = x; break;
+          case U_JSET32: if (a32 & b32) pc = x; break;  // == (sext(a) & sext(b)) != 0
+          case U_JNE32: if (a32 != b32) pc = x; break;
+          case U_JLT32: if ((int32_t)a32 < (int32_t)b32) pc = x; break;
+          case U_JLE32: if ((int32_t)a32 <= (int32_t)b32) pc = x; break;
+          case U_CALL:  // emu.rs:265-272
+            if (TIER == 1) {
+              if (csp >= (uint32_t)kCallDepth) {
+                fault = true;
+                fst = EBPF_ST_CALLDEPTH;
+              } else {
+                cstack[(size_t)csp * kWave] = x + 1;
+                csp++;
+                pc = x;
+              }
+            } else {
+              fault = true;  // unreachable: the loader routes calls to tier 1
+              fst = EBPF_ST_INSN;
+            }
+            break;
+          case U_EXIT:  // emu.rs:273-279
+            if (TIER == 1 && csp > 0) {
+              csp--;
+              pc = cstack[(size_t)csp * kWave];
+            } else {
+              pc = PC_DONE;
+            }
+            break;
+          // ---- loads / stores (emu.rs:311-444) ----
+          case U_LDIMM: R = k; break;
+          case U_LDX: {
+            int64_t sum;
+            const bool ovf = __builtin_add_overflow((int64_t)S, (int64_t)(int32_t)x, &sum);
+            const uint64_t ua = (uint64_t)sum;
+            if (ovf || ua >= mem_size) { fault = true; fst = EBPF_ST_MEM; }
+            else if (ua + aux > mem_size) { fault = true; fst = EBPF_ST_MEM_UB; }
+            else {
+              const uint32_t a0 = (uint32_t)ua;
+              uint64_t v;
+              if (TIER == 1) v = img_read(img, a0, aux);
+              else if (a0 + aux <= (uint32_t)kWin) v = win_read(my_win, a0, aux);
+              else if (a0 >= len) v = 0;
+              else v = pkt_read(base, a0, aux, len);
+              const uint64_t m = wmask(aux);
+              R = (A & ~m) | v;  // upper bytes preserved (Q1)
+            }
+            break;
+          }
+          case U_ST:
+          case U_STX: {
+            if (TIER == 1) {
+              int64_t sum;
+              const bool ovf = __builtin_add_overflow((int64_t)A, (int64_t)(int32_t)x, &sum);
+              const uint64_t ua = (uint64_t)sum;
+              if (ovf || ua >= mem_size) { fault = true; fst = EBPF_ST_MEM; }
+              else if (ua + aux > mem_size) { fault = true; fst = EBPF_ST_MEM_UB; }
+              else img_write(img, (uint32_t)ua, aux, op == U_ST ? k : S);
+            } else {
+              fault = true;
+              fst = EBPF_ST_INSN;
+            }
+            break;
+          }
+          case U_ATOMIC: {  // emu.rs:373-437
+            if (TIER == 1) {
+              int64_t sum;
+              const bool ovf = __builtin_add_overflow((int64_t)A, (int64_t)(int32_t)x, &sum);
+              const uint64_t ua = (uint64_t)sum;
+              if (ovf || ua >= mem_size || ua + 8 > mem_size) { fault = true; fst = EBPF_ST_MEM; break; }
+              uint64_t orig = img_read(img, (uint32_t)ua, 8);
+              const bool fetch = aux & F_FETCH;
+              const bool is32 = aux & F_ATOMIC32;
+              uint64_t bak = fetch ? orig : 0;
+              uint64_t high = 0, sv = S, r0v = r[0];
+              if (is32) {
+                sv = (uint32_t)sv;
+                high = orig >> 32;
+                orig = (uint32_t)orig;
+                r0v = (uint32_t)r0v;
+                bak = (uint32_t)bak;
+              }
+              if (k == 0x00) {
+                int64_t t;
+                if (__builtin_add_overflow((int64_t)orig, (int64_t)sv, &t)) {
+                  fault = true; fst = EBPF_ST_ARITH; break;
+                }
+                orig = (uint64_t)t;
+              } else if (k == 0x40) orig |= sv;
+              else if (k == 0x50) orig &= sv;
+              else if (k == 0xa0) orig ^= sv;
+              else if (k == 0xe0) { bak = orig; orig = sv; }
+              else if (k == 0xf0) {
+                if (orig == r0v) orig = sv;
+                r[0] = bak;
+              } else { fault = true; fst = EBPF_ST_INSN; break; }
+              int64_t t;
+              if (__builtin_add_overflow((int64_t)orig, (int64_t)(high << 32), &t)) {
+                fault = true; fst = EBPF_ST_ARITH; break;
+              }
+              img_write(img, (uint32_t)ua, 8, (uint64_t)t);
+              if (fetch) r[src] = bak;
+            } else {
+              fault = true;
+              fst = EBPF_ST_INSN;
+            }
+            break;
+          }
+          default:  // U_FAULT
+            fault = true;
+            fst = aux;
+            break;
+        }
+        if (fault) {
+          st = fst;
+          pc = PC_DONE;
+          nsteps--;  // the faulting instruction does not retire
+        } else {
+          r[dst] = R;  // single write-back; ST/STX/ATOMIC rewrite the dst snapshot (Q14)
+        }
+      }
+    }
+
+    // ---- outputs: r0 (main.rs:43), status, verdict (xdp.rs:3-9), final image ----
+    const uint64_t r0v = r[0];
+    if (a.mem_out && valid) {
+      uint32_t* mo = (uint32_t*)(a.mem_out + pkt * (uint64_t)mem_size);
+      const uint32_t m = min(len, mem_size);
+      for (uint32_t d = 0; d < mem_size / 4; d++) {
+        uint32_t v;
+        if (TIER == 1) v = img[(size_t)d * kWave];
+        else if (d * 4 < (uint32_t)kWin) v = ((const uint32_t*)my_win)[d];
+        else v = (d * 4 < m) ? (uint32_t)pkt_read(base, d * 4, 4, len) : 0u;
+        mo[d] = v;
+      }
+    }
+    if (a.regs_out && valid) {
+#pragma unroll
+      for (int i = 0; i < 11; i++) a.regs_out[pkt * 11 + i] = r[i];
+    }
+    if (valid) {
+      if (a.r0) a.r0[pkt] = r0v;
+      if (a.status) a.status[pkt] = (uint8_t)st;
+      if (a.verdict) a.verdict[pkt] = st ? (uint8_t)EBPF_VERDICT_FAULT
+                                         : (r0v < 5 ? (uint8_t)r0v : (uint8_t)EBPF_VERDICT_OTHER);
+    }
+    const bool okv = valid && st == EBPF_ST_OK;
+#pragma unroll
+    for (int b = 0; b < 5; b++) cnt[b] += __builtin_popcountll(ballot(okv && r0v == (uint64_t)b));
+    cnt[5] += __builtin_popcountll(ballot(okv && r0v >= 5));
+    cnt[6] += __builtin_popcountll(ballot(valid && st != EBPF_ST_OK));
+    retired += valid ? nsteps : 0u;
+  }
+
+  // ---- counters: workgroup sum -> sharded device atomics -> the last workgroup folds the
+  //      shards into the caller's counters (one launch per batch, no finalize kernel) ----
+  for (int off = 32; off >= 1; off >>= 1) retired += (uint64_t)__shfl_xor((long long)retired, off);
+  __syncthreads();  // all waves are done with their windows: reuse LDS
+  uint64_t* red = (uint64_t*)smem;
+  if (lane == 0) {
+#pragma unroll
+    for (int b = 0; b < 7; b++) red[wv * 8 + b] = cnt[b];
+    red[wv * 8 + 7] = retired;
+  }
+  __syncthreads();
+  if (a.counters == nullptr) return;
+  __shared__ uint32_t last_flag;
+  if (threadIdx.x < 8) {
+    uint64_t s = 0;
+#pragma unroll
+    for (int w = 0; w < kWavesPerBlock; w++) s += red[w * 8 + threadIdx.x];
+    if (s)
+      __hip_atomic_fetch_add(&a.shards[(blockIdx.x % kCounterShards) * 8 + threadIdx.x], s,
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (threadIdx.x < kWave) {  // wave 0: its shard atomics are performed before the ticket
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    if (threadIdx.x == 0) {
+      const uint32_t t = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_ACQ_REL,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+      last_flag = (t == gridDim.x - 1);
+    }
+  }
+  __syncthreads();
+  if (!last_flag) return;
+  // last workgroup: read-and-clear every shard with device-scope atomics (coherent across XCDs)
+  uint64_t* fold = (uint64_t*)smem;
+  if (threadIdx.x < kCounterShards * 8 / 2) {
+    uint64_t v = 0;
+    for (int i = threadIdx.x; i < kCounterShards * 8; i += kCounterShards * 8 / 2)
+      v += __hip_atomic_exchange(&a.shards[i], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    fold[threadIdx.x] = v;  // entry i holds counter i % 8
+  }
+  __syncthreads();
+  if (threadIdx.x < 8) {
+    uint64_t t = 0;
+    for (int i = threadIdx.x; i < kCounterShards * 8 / 2; i += 8) t += fold[i];
+    if (t) atomicAdd((unsigned long long*)&a.counters[threadIdx.x], (unsigned long long)t);
+  }
+  if (threadIdx.x == 0) __hip_atomic_exchange(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+static uint32_t lds_bytes_for(uint32_t n_uops) {
+  const uint32_t prog = n_uops <= (uint32_t)kMaxLdsUops ? n_uops * (uint32_t)sizeof(Uop) : 0u;
+  uint32_t win = kBlock * kWinStride;
+  if (win < kWavesPerBlock * 8 * 8) win = kWavesPerBlock * 8 * 8;
+  return prog + win;
+}
+
+int interp_grid(int tier, uint32_t n_uops, uint64_t n_tiles, int* grid_out) {
+  const uint64_t want = (n_tiles + kWavesPerBlock - 1) / kWavesPerBlock;
+  if (tier == 0) {  // one tile per wave; the dispatcher load-balances divergent tiles
+    *grid_out = (int)(want ? (want < (1u << 30) ? want : (1u << 30)) : 1);
+    return 0;
+  }
+  int dev = 0, cus = 256, per_cu = 8;
+  if (hipGetDevice(&dev) != hipSuccess) return -1;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return -1;
+  const uint32_t lds = lds_bytes_for(n_uops);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, interp_kernel<1>, kBlock, lds) !=
+          hipSuccess || per_cu < 1)
+    per_cu = 1;
+  if (per_cu > 4) per_cu = 4;  // bounds the tier-1 image scratch
+  const uint64_t cap = (uint64_t)cus * (uint64_t)per_cu;
+  *grid_out = (int)(want < cap ? (want ? want : 1) : cap);
+  return 0;
+}
+
+hipError_t launch_interp(int tier, const LaunchArgs& a, int grid, hipStream_t stream) {
+  const uint32_t lds = lds_bytes_for(a.n_uops);
+  if (tier == 1)
+    hipLaunchKernelGGL(interp_kernel<1>, dim3(grid), dim3(kBlock), lds, stream, a);
+  else
+    hipLaunchKernelGGL(interp_kernel<0>, dim3(grid), dim3(kBlock), lds, stream, a);
+  return hipGetLastError();
+}
+
+}  // namespace ebpfemu

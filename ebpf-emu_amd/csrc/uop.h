@@ -1,0 +1,56 @@
+// uop.h — device micro-op format produced by the host pre-decoder (decode.cpp) and
+// interpreted by the gfx950 kernel (interp.hip).
+//
+// One 16-byte micro-op per DECODED reference instruction (a wide lddw is one entry, as
+// ins.rs:107-116 folds it), so jump targets keep the reference's decoded-entry indexing
+// (quirk Q9). Everything that can be resolved at load time is: operand source, ALU width,
+// the sign-extended immediate, absolute jump targets, static runtime faults (reg 11, END imm,
+// callx, illegal mode/class combinations). The kernel therefore never indexes register 11.
+#pragma once
+#include <stdint.h>
+
+namespace ebpfemu {
+
+struct alignas(16) Uop {
+  uint8_t op;   // UopKind
+  uint8_t dst;  // 0..10
+  uint8_t src;  // 0..10
+  uint8_t aux;  // kind-specific: F_SRC, access width, atomic flags, fault status
+  int32_t x;    // jump/call target (u32 bits) or memory offset (sign-extended i16)
+  int64_t k;    // immediate: sign-extended imm (ALU/JMP), imm64 (LDIMM), zext imm (ST), atomic op
+};
+static_assert(sizeof(Uop) == 16, "Uop must be 16 bytes");
+
+enum UopAux : uint8_t {
+  F_SRC = 1,        // ALU/JMP: operand is regs[src] (code bit 3), else k
+  F_ATOMIC32 = 2,   // ATOMIC: 32-bit form (size bits == 0, emu.rs:382)
+  F_FETCH = 4,      // ATOMIC: imm & 1 (emu.rs:376)
+};
+
+enum UopKind : uint8_t {
+  // ALU64 (emu.rs:80-209, class ALU64): dst = f(dst, b)
+  U_ADD64 = 0, U_SUB64, U_MUL64, U_DIV64, U_OR64, U_AND64, U_LSH64, U_RSH64, U_NEG64, U_MOD64,
+  U_XOR64, U_MOV64, U_ARSH64,
+  // ALU32 (class ALU, operands truncated to u32 before and after, emu.rs:76-79,214-216)
+  U_ADD32, U_SUB32, U_MUL32, U_DIV32, U_OR32, U_AND32, U_LSH32, U_RSH32, U_NEG32, U_MOD32,
+  U_XOR32, U_MOV32, U_ARSH32,
+  // END (emu.rs:165-209), either ALU class (Q7)
+  U_ZX16, U_ZX32, U_NOP, U_BSWAP16, U_BSWAP32, U_BSWAP64,
+  // JMP: all orderings signed (Q2); 32-bit forms compare sign-extended low words (Q3)
+  U_JA, U_JEQ, U_JGT, U_JGE, U_JSET, U_JNE, U_JLT, U_JLE,
+  U_JEQ32, U_JGT32, U_JGE32, U_JSET32, U_JNE32, U_JLT32, U_JLE32,
+  U_CALL,   // pc = x; push x + 1 (emu.rs:265-272)
+  U_EXIT,   // pop or stop (emu.rs:273-279)
+  // load/store
+  U_LDIMM,  // dst = k (emu.rs:332-334)
+  U_LDX,    // low aux bytes of dst <- mem[src + x] (Q1, emu.rs:341-349)
+  U_ST,     // mem[dst + x] <- low aux bytes of k (Q8)
+  U_STX,    // mem[dst + x] <- low aux bytes of src
+  U_ATOMIC, // 8-byte RMW at dst + x; k = imm & 0xfe (or 0xff = unknown -> fault after the read)
+  U_FAULT,  // aux = EBPF_ST_* raised when executed
+  U_NKINDS
+};
+
+constexpr uint32_t PC_DONE = 0xFFFFFFFFu;
+
+}  // namespace ebpfemu

@@ -1,0 +1,102 @@
+"""ctypes binding of libebpfemu.so (include/ebpf_emu.h).
+
+The product path: every execution goes through the gfx950 kernel inside libebpfemu.so. There
+is no Python or CPU fallback; if the library is missing this module raises at import time of
+`lib()`.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libebpfemu.so")
+
+# ---- constants mirrored from include/ebpf_emu.h ----
+EBPF_OK = 0
+EBPF_EINVAL, EBPF_ELEN, EBPF_EREG, EBPF_EOP, EBPF_EMODE = -1, -2, -3, -4, -5
+EBPF_ELDDW, EBPF_ELDDW_OVF, EBPF_EHEX, EBPF_ENOMEM, EBPF_EHIP = -6, -7, -8, -9, -10
+EBPF_ETOOBIG, EBPF_ERCCL = -11, -12
+
+ST_OK, ST_MEM, ST_MEM_UB, ST_INSN, ST_ARITH, ST_STEPS, ST_CALLDEPTH, ST_BADPKT = range(8)
+STATUS_NAMES = ["OK", "MEM", "MEM_UB", "INSN", "ARITH", "STEPS", "CALLDEPTH", "BADPKT"]
+VERDICT_OTHER, VERDICT_FAULT = 0xFE, 0xFF
+NCOUNTERS = 8
+DEFAULT_MEM, DEFAULT_R10, DEFAULT_STEPS = 1024, 512, 1 << 22
+MAX_CALL_DEPTH = 64
+
+EXPORTS = ["ebpf_batch_init", "ebpf_prog_load", "ebpf_prog_load_hex", "ebpf_prog_free",
+           "ebpf_prog_len", "ebpf_prog_insn", "ebpf_prog_tier", "ebpf_workspace_bytes",
+           "ebpf_prog_upload", "ebpf_run_batch", "ebpf_run_batch_multi", "ebpf_strerror",
+           "ebpf_version"]
+
+
+class Batch(ctypes.Structure):  # ebpf_batch
+    _fields_ = [("frames", ctypes.c_void_p), ("offsets", ctypes.c_void_p),
+                ("lens", ctypes.c_void_p), ("stride", ctypes.c_uint64), ("n", ctypes.c_uint64),
+                ("mem_size", ctypes.c_uint32), ("flags", ctypes.c_uint32),
+                ("r10", ctypes.c_uint64), ("max_steps", ctypes.c_uint64),
+                ("workspace", ctypes.c_void_p), ("workspace_bytes", ctypes.c_uint64),
+                ("init_regs", ctypes.c_void_p)]
+
+
+class BatchOut(ctypes.Structure):  # ebpf_batch_out
+    _fields_ = [("verdict", ctypes.c_void_p), ("r0", ctypes.c_void_p), ("status", ctypes.c_void_p),
+                ("counters", ctypes.c_void_p), ("mem", ctypes.c_void_p), ("regs", ctypes.c_void_p)]
+
+
+class EbpfError(RuntimeError):
+    def __init__(self, code: int, what: str = "", word: int | None = None):
+        self.code = code
+        self.word = word
+        msg = f"{what}: {strerror(code)} ({code})" if what else f"{strerror(code)} ({code})"
+        if word is not None:
+            msg += f" at word {word}"
+        super().__init__(msg)
+
+
+_LIB = None
+
+
+def lib():
+    """Load libebpfemu.so (built by __graft_entry__.build() / `make -C ebpf-emu_amd`)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is missing: build it with `make -C ebpf-emu_amd` "
+                          "(there is no CPU fallback)")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, sz, u64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64
+    L.ebpf_batch_init.argtypes = [ctypes.POINTER(Batch)]
+    L.ebpf_batch_init.restype = None
+    L.ebpf_prog_load.argtypes = [ctypes.c_char_p, sz, ctypes.POINTER(vp), ctypes.POINTER(sz)]
+    L.ebpf_prog_load_hex.argtypes = [ctypes.c_char_p, ctypes.POINTER(vp), ctypes.POINTER(sz)]
+    L.ebpf_prog_free.argtypes = [vp]
+    L.ebpf_prog_free.restype = None
+    L.ebpf_prog_len.argtypes = [vp]
+    L.ebpf_prog_len.restype = sz
+    L.ebpf_prog_insn.argtypes = [vp, sz, ctypes.POINTER(ctypes.c_int32),
+                                 ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int16),
+                                 ctypes.POINTER(ctypes.c_uint8), ctypes.POINTER(ctypes.c_uint8),
+                                 ctypes.POINTER(ctypes.c_uint8)]
+    L.ebpf_prog_tier.argtypes = [vp]
+    L.ebpf_workspace_bytes.argtypes = [vp, ctypes.POINTER(Batch), ctypes.c_int]
+    L.ebpf_workspace_bytes.restype = u64
+    L.ebpf_prog_upload.argtypes = [vp, ctypes.c_int]
+    L.ebpf_run_batch.argtypes = [vp, ctypes.POINTER(Batch), ctypes.POINTER(BatchOut), vp]
+    L.ebpf_run_batch_multi.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+                                       ctypes.POINTER(Batch), ctypes.POINTER(BatchOut),
+                                       ctypes.POINTER(vp)]
+    L.ebpf_strerror.argtypes = [ctypes.c_int]
+    L.ebpf_strerror.restype = ctypes.c_char_p
+    L.ebpf_version.restype = ctypes.c_char_p
+    _LIB = L
+    return L
+
+
+def strerror(code: int) -> str:
+    try:
+        return lib().ebpf_strerror(code).decode()
+    except ImportError:
+        return "error"

@@ -1,0 +1,156 @@
+"""Program / batch API: load once, run(packets) -> verdicts on the GPU.
+
+This is the batched form of the reference's per-packet composite
+    Emu::default(); mmu = Mmu{1 KiB, packet at [0,len)}; regs r1=0,r2=len,r10=512; emu.run();
+    verdict = emu.state.regs[0]                    (main.rs:14-43, emu.rs:30-45,452-458)
+over device-resident frames. Device memory and streams come from PyTorch (plumbing only); the
+work is one launch of the gfx950 kernel in libebpfemu.so per batch.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+from . import _lib
+from .ins import DecodeError, _decoded, load_image
+
+
+@dataclass
+class BatchResult:
+    verdict: object = None   # torch.uint8 [n]
+    r0: object = None        # torch.int64 [n] (u64 bits)
+    status: object = None    # torch.uint8 [n]
+    counters: object = None  # torch.int64 [8] (u64 bits), accumulated
+    mem: object = None       # torch.uint8 [n, mem_size]
+    regs: object = None      # torch.int64 [n, 11]
+
+
+def _ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+class Program:
+    """A loaded eBPF program (ebpf_prog_load). Immutable; shareable across devices."""
+
+    def __init__(self, image: bytes):
+        self._h = load_image(bytes(image))
+        self.image = bytes(image)
+
+    @classmethod
+    def from_hex(cls, hx: str) -> "Program":
+        L = _lib.lib()
+        h = ctypes.c_void_p()
+        bad = ctypes.c_size_t(0)
+        rc = L.ebpf_prog_load_hex(hx.encode(), ctypes.byref(h), ctypes.byref(bad))
+        if rc != 0:
+            raise DecodeError(rc, bad.value)
+        self = cls.__new__(cls)
+        self._h = h
+        self.image = None
+        return self
+
+    def __len__(self) -> int:
+        return _lib.lib().ebpf_prog_len(self._h)
+
+    @property
+    def tier(self) -> int:
+        return _lib.lib().ebpf_prog_tier(self._h)
+
+    @property
+    def instructions(self):
+        return _decoded(self._h)
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            _lib.lib().ebpf_prog_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def upload(self, device: int) -> None:
+        rc = _lib.lib().ebpf_prog_upload(self._h, device)
+        if rc:
+            raise _lib.EbpfError(rc, "ebpf_prog_upload")
+
+    def make_batch(self, frames, n: int | None = None, stride: int = 0, offsets=None, lens=None,
+                   mem_size: int = _lib.DEFAULT_MEM, r10: int = _lib.DEFAULT_R10,
+                   max_steps: int = _lib.DEFAULT_STEPS, init_regs=None,
+                   workspace=None) -> _lib.Batch:
+        b = _lib.Batch()
+        _lib.lib().ebpf_batch_init(ctypes.byref(b))
+        if n is None:
+            n = offsets.numel() if offsets is not None else frames.numel() // max(stride, 1)
+        b.frames = frames.data_ptr()
+        b.offsets = offsets.data_ptr() if offsets is not None else None
+        b.lens = lens.data_ptr() if lens is not None else None
+        b.stride = stride
+        b.n = n
+        b.mem_size = mem_size
+        b.r10 = r10 & ((1 << 64) - 1)
+        b.max_steps = max_steps
+        b.init_regs = init_regs.data_ptr() if init_regs is not None else None
+        if workspace is not None:
+            b.workspace = workspace.data_ptr()
+            b.workspace_bytes = workspace.numel() * workspace.element_size()
+        return b
+
+    def workspace_bytes(self, batch: _lib.Batch, device: int) -> int:
+        return int(_lib.lib().ebpf_workspace_bytes(self._h, ctypes.byref(batch), device))
+
+    def launch(self, batch: _lib.Batch, out: _lib.BatchOut, stream=None) -> None:
+        """Raw asynchronous launch on `stream` (a torch.cuda.Stream or None = current)."""
+        import torch
+
+        s = stream if stream is not None else torch.cuda.current_stream()
+        rc = _lib.lib().ebpf_run_batch(self._h, ctypes.byref(batch), ctypes.byref(out),
+                                       ctypes.c_void_p(s.cuda_stream))
+        if rc:
+            raise _lib.EbpfError(rc, "ebpf_run_batch")
+
+    def run(self, frames, n: int | None = None, stride: int = 0, offsets=None, lens=None,
+            mem_size: int = _lib.DEFAULT_MEM, r10: int = _lib.DEFAULT_R10,
+            max_steps: int = _lib.DEFAULT_STEPS, init_regs=None, verdict: bool = True,
+            r0: bool = False, status: bool = False, counters=None, mem: bool = False,
+            regs: bool = False, stream=None) -> BatchResult:
+        """Run the program over a device-resident batch; returns device tensors.
+
+        frames: torch.uint8 CUDA tensor. Layout: packet i at frames[i*stride:] (stride layout,
+        len = lens[i] or stride) or at frames[offsets[i]:] (offsets: torch.int32 / uint32 bits,
+        lens: torch.int16/uint16 bits). counters: an optional torch.int64 [8] tensor to add to.
+        """
+        import torch
+
+        dev = frames.device
+        b = self.make_batch(frames, n, stride, offsets, lens, mem_size, r10, max_steps, init_regs)
+        n = b.n
+        res = BatchResult()
+        if verdict:
+            res.verdict = torch.empty(n, dtype=torch.uint8, device=dev)
+        if r0:
+            res.r0 = torch.empty(n, dtype=torch.int64, device=dev)
+        if status:
+            res.status = torch.empty(n, dtype=torch.uint8, device=dev)
+        if mem:
+            res.mem = torch.empty((n, mem_size), dtype=torch.uint8, device=dev)
+        if regs:
+            res.regs = torch.empty((n, 11), dtype=torch.int64, device=dev)
+        res.counters = counters
+        out = _lib.BatchOut()
+        out.verdict = res.verdict.data_ptr() if verdict else None
+        out.r0 = res.r0.data_ptr() if r0 else None
+        out.status = res.status.data_ptr() if status else None
+        out.counters = counters.data_ptr() if counters is not None else None
+        out.mem = res.mem.data_ptr() if mem else None
+        out.regs = res.regs.data_ptr() if regs else None
+        with torch.cuda.device(dev):
+            self.launch(b, out, stream)
+        return res
+
+
+def u64(t):
+    """torch.int64 tensor of u64 bit patterns -> list of Python ints in [0, 2**64)."""
+    return [int(v) & ((1 << 64) - 1) for v in t.tolist()]

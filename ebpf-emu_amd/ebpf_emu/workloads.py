@@ -1,0 +1,152 @@
+"""Synthetic XDP workloads of BASELINE.json configs 2-5.
+
+Frames: seeded (numpy PCG64, seed 0x5EED0000 + config id) Ethernet frames. EtherType IPv4
+(90 %), IPv6 (5 %), ARP (5 %); IPv4 IHL 5 (95 %) or 6 with 4 option bytes (5 %); protocol TCP
+(45 %), UDP (45 %), ICMP (10 %); ~25 % of UDP flows to port 53; random addresses, ports and
+payload. Fixed 64-byte frames use the stride layout; mixed 64 / 1500-byte frames use
+offsets + lengths with every frame starting on a 64-byte boundary (a NIC-ring-like layout).
+
+Programs (hand-assembled: the container's LLVM has no BPF target). Jump offsets follow the
+reference's decoded-entry indexing (asm.py).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .asm import assemble
+
+SEED_BASE = 0x5EED0000
+
+# config 2: XDP_DROP-all, 3 instructions, touches the frame
+DROP_ALL = """
+    ldxb r3, [r1+0]
+    mov r0, 1
+    exit
+"""
+
+# config 3/4: IPv4 5-tuple parse -> PASS (2) / DROP (1), 32 instructions.
+# Loads are little-endian (the reference's memcpy into an i64, emu.rs:341-349), so big-endian
+# header fields are compared byte-swapped or converted with be16 (END, emu.rs:165-209).
+FIVE_TUPLE = """
+    mov r0, 2                 # default XDP_PASS
+    jlt r2, 34, out           # shorter than Ethernet + IPv4 header
+    ldxh r3, [r1+12]          # EtherType
+    jne r3, 0x0008, out       # 0x0800 read little-endian
+    ldxb r4, [r1+14]          # version / IHL
+    and r4, 0x0f
+    lsh r4, 2                 # IHL * 4
+    jlt r4, 20, drop          # malformed header
+    ldxb r5, [r1+23]          # protocol
+    ldxw r6, [r1+26]          # saddr (first octet in the low byte)
+    ldxw r7, [r1+30]          # daddr
+    mov r8, r1
+    add r8, r4                # r8 + 14 = L4 header
+    jeq r5, 1, icmp
+    jeq r5, 17, udp
+    jne r5, 6, out
+    ldxh r9, [r8+16]          # TCP dport
+    be16 r9
+    jge r9, 1024, out         # only well-known ports are filtered
+    and r6, 0xff
+    jeq r6, 10, drop          # 10.0.0.0/8 -> well-known TCP port: drop
+    ja out
+udp:
+    ldxh r9, [r8+16]          # UDP dport
+    be16 r9
+    jeq r9, 53, drop          # DNS: drop
+    ja out
+icmp:
+    and r7, 0xf0
+    jeq r7, 0xe0, drop        # ICMP to 224.0.0.0/4: drop
+    ja out
+drop:
+    mov r0, 1                 # XDP_DROP
+out:
+    exit
+"""
+
+# config 5: per-byte checksum loop, ~6 instructions per byte, then fold + parity.
+CHECKSUM = """
+    mov r0, 0
+    mov r3, 0
+    jge r3, r2, done
+loop:
+    mov r4, r1
+    add r4, r3
+    ldxb r5, [r4+0]
+    add r0, r5
+    add r3, 1
+    jlt r3, r2, loop
+done:
+    mov r6, r0
+    rsh r6, 8
+    xor r0, r6
+    and r0, 1
+    add r0, 1                 # DROP (1) or PASS (2) by parity
+    exit
+"""
+
+PROGRAMS = {"drop": DROP_ALL, "5tuple": FIVE_TUPLE, "checksum": CHECKSUM}
+
+
+def program(name: str) -> bytes:
+    return assemble(PROGRAMS[name])
+
+
+def _headers(rng: np.random.Generator, n: int, frame_len: np.ndarray, buf: np.ndarray,
+             starts: np.ndarray) -> None:
+    """Write Ethernet/IPv4/L4 headers into buf at starts (frames already hold random bytes)."""
+    u = rng.random(n)
+    ethertype = np.where(u < 0.90, 0x0800, np.where(u < 0.95, 0x86DD, 0x0806)).astype(np.uint16)
+    ihl = np.where(rng.random(n) < 0.95, 5, 6).astype(np.uint8)
+    p = rng.random(n)
+    proto = np.where(p < 0.45, 6, np.where(p < 0.90, 17, 1)).astype(np.uint8)
+    dport = rng.integers(0, 65536, n, dtype=np.uint32).astype(np.uint16)
+    dns = (proto == 17) & (rng.random(n) < 0.25)
+    dport[dns] = 53
+    low = (proto == 6) & (rng.random(n) < 0.30)
+    dport[low] = rng.integers(0, 1024, int(low.sum()), dtype=np.uint32).astype(np.uint16)
+    saddr0 = rng.integers(0, 256, n, dtype=np.uint32).astype(np.uint8)
+    ten = rng.random(n) < 0.20
+    saddr0[ten] = 10
+
+    def put(off, vals):
+        idx = starts + off
+        ok = off < frame_len
+        buf[idx[ok]] = vals[ok]
+
+    put(12, (ethertype >> 8).astype(np.uint8))
+    put(13, (ethertype & 0xFF).astype(np.uint8))
+    put(14, (0x40 | ihl).astype(np.uint8))
+    put(23, proto)
+    put(26, saddr0)
+    l4 = 14 + ihl.astype(np.int64) * 4
+    for k, v in ((2, dport >> 8), (3, dport & 0xFF)):
+        idx = starts + l4 + k
+        ok = (l4 + k) < frame_len
+        buf[idx[ok]] = v.astype(np.uint8)[ok]
+
+
+def frames_fixed(n: int, frame: int = 64, config_id: int = 3) -> np.ndarray:
+    """n fixed-size frames, stride layout: uint8[n * frame]."""
+    rng = np.random.Generator(np.random.PCG64(SEED_BASE + config_id))
+    buf = rng.integers(0, 256, n * frame, dtype=np.uint8)
+    starts = np.arange(n, dtype=np.int64) * frame
+    _headers(rng, n, np.full(n, frame, dtype=np.int64), buf, starts)
+    return buf
+
+
+def frames_mixed(n: int, small: int = 64, large: int = 1500, align: int = 64,
+                 config_id: int = 5):
+    """Mixed 64/1500-byte frames (50/50 by seeded coin): (buf uint8, offsets uint32, lens uint16)."""
+    rng = np.random.Generator(np.random.PCG64(SEED_BASE + config_id))
+    lens = np.where(rng.random(n) < 0.5, small, large).astype(np.int64)
+    slots = (lens + align - 1) // align * align
+    offsets = np.zeros(n, dtype=np.int64)
+    offsets[1:] = np.cumsum(slots)[:-1]
+    total = int(offsets[-1] + slots[-1]) if n else 0
+    if total >= 1 << 32:
+        raise ValueError("mixed batch exceeds the u32 offset range")
+    buf = rng.integers(0, 256, total, dtype=np.uint8)
+    _headers(rng, n, lens, buf, offsets)
+    return buf, offsets.astype(np.uint32), lens.astype(np.uint16)

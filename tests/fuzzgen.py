@@ -1,0 +1,115 @@
+"""Seeded random program / packet generator for differential tests (test infrastructure).
+
+Programs mix every instruction class the reference decodes: ALU/ALU64 (all 14 ops, imm and
+register sources, END widths incl. invalid ones), JMP/JMP32 (forward and occasional backward
+offsets, so some programs loop into the step budget), LDX/ST/STX/ATOMIC around the packet, the
+stack and the image end, wide lddw of edge values, CALL/EXIT, register 11 and a few opcodes that
+fault at run time. `valid_only=False` also produces load-time rejects.
+"""
+from __future__ import annotations
+
+import random
+
+from ebpf_emu.asm import encode
+
+EDGE = [0, 1, 2, 7, 0x7F, 0x80, 0xFF, 0x100, 0x7FFF, 0x8000, 0xFFFF, 0x7FFFFFFF, 0x80000000,
+        0xFFFFFFFF, 0x100000000, 0x7FFFFFFFFFFFFFFF, 0x8000000000000000, 0xFFFFFFFFFFFFFFFF,
+        0xFFFFFFFF00000000, 0x0000000100000001, 512, 504, 1016, 1020, 1023, 1024]
+IMM_EDGE = [0, 1, -1, 2, 7, 8, 16, 31, 32, 33, 63, 64, 65, -4, 0x7FFFFFFF, -0x80000000, 0x11, 53,
+            1024, 1020, 1023, 100]
+ATOMIC_IMMS = [0x00, 0x01, 0x40, 0x41, 0x50, 0x51, 0xA0, 0xA1, 0xE1, 0xF1, 0xE0, 0xF0, 0x10, 0x100]
+
+
+def _reg(rng, allow11=0.01):
+    if rng.random() < allow11:
+        return 11
+    return rng.randrange(11)
+
+
+def _imm(rng):
+    if rng.random() < 0.6:
+        return rng.choice(IMM_EDGE)
+    return rng.randrange(-(1 << 31), 1 << 31)
+
+
+def _mem_ref(rng):
+    """(base register, offset) aimed at the packet, the stack or the image edges."""
+    k = rng.random()
+    if k < 0.45:
+        return 1, rng.randrange(-2, 72)
+    if k < 0.8:
+        return 10, -rng.randrange(1, 64)
+    if k < 0.9:
+        return 1, rng.choice([1016, 1017, 1020, 1021, 1023, 1024, 2000, -8])
+    return rng.randrange(11), rng.randrange(-64, 64)
+
+
+def gen_program(rng: random.Random, n: int | None = None, valid_only: bool = True,
+                allow_loops: bool = True) -> bytes:
+    n = n or rng.randrange(3, 40)
+    words: list[bytes] = []
+    # seed registers with edge values so arithmetic corners are reached
+    for r in rng.sample([0, 3, 4, 5, 6, 7, 8, 9], rng.randrange(0, 4)):
+        v = rng.choice(EDGE)
+        words.append(encode(0x18, r, 0, 0, v & 0xFFFFFFFF) + encode(0, 0, 0, 0, v >> 32))
+    while len(words) < n:
+        k = rng.random()
+        dst, src = _reg(rng), _reg(rng)
+        if k < 0.40:  # ALU / ALU64
+            cls = rng.choice([0x04, 0x07])
+            op = rng.randrange(14)
+            srcbit = rng.choice([0, 0x08])
+            if op == 13:
+                imm = rng.choice([16, 32, 64, 16, 32, 64, 8, 0])
+                words.append(encode((op << 4) | srcbit | cls, dst, 0, 0, imm))
+            else:
+                words.append(encode((op << 4) | srcbit | cls, dst, src, 0, _imm(rng)))
+        elif k < 0.60:  # JMP / JMP32
+            cls = rng.choice([0x05, 0x06])
+            op = rng.choice([0, 1, 2, 3, 4, 5, 6, 7, 10, 11, 12, 13])
+            remaining = max(1, n - len(words))
+            off = rng.randrange(0, remaining + 2)
+            if allow_loops and rng.random() < 0.05:
+                off = -rng.randrange(1, 4)
+            words.append(encode((op << 4) | rng.choice([0, 0x08]) | cls, dst, src, off, _imm(rng)))
+        elif k < 0.72:  # LDX
+            base, off = _mem_ref(rng)
+            size = rng.choice([0x00, 0x08, 0x10, 0x18])
+            words.append(encode(0x61 | size, dst, base, off))
+        elif k < 0.80:  # ST / STX
+            base, off = _mem_ref(rng)
+            size = rng.choice([0x00, 0x08, 0x10, 0x18])
+            if rng.random() < 0.5:
+                words.append(encode(0x62 | size, base, 0, off, _imm(rng)))
+            else:
+                words.append(encode(0x63 | size, base, src, off))
+        elif k < 0.86:  # ATOMIC
+            base, off = (10, -8 * rng.randrange(1, 6)) if rng.random() < 0.8 else _mem_ref(rng)
+            size = rng.choice([0x00, 0x18, 0x18, 0x08])
+            cls = 0x03 if rng.random() < 0.9 else 0x02
+            words.append(encode(0xC0 | size | cls, base, src, off, rng.choice(ATOMIC_IMMS)))
+        elif k < 0.90:  # lddw
+            v = rng.choice(EDGE) if rng.random() < 0.7 else rng.getrandbits(64)
+            words.append(encode(0x18, dst, 0, 0, v & 0xFFFFFFFF) + encode(0, 0, 0, 0, v >> 32))
+        elif k < 0.93:  # CALL / EXIT
+            if rng.random() < 0.5:
+                words.append(encode(0x85, 0, 0, rng.randrange(0, 4)))
+            else:
+                words.append(encode(0x95))
+        elif k < 0.96:  # run-time faults
+            words.append(rng.choice([encode(0x20, 0, 0, 0, 0), encode(0x60, 0, 1, 0),
+                                     encode(0xD9, 0, 1, 0), encode(0x8D, 0, 1, 0),
+                                     encode(0x1A, 0, 0, 0, 0) + bytes(8)]))
+        else:  # mov
+            words.append(encode(0xB7 | rng.choice([0, 0x08]), dst, src, 0, _imm(rng)))
+        if not valid_only and rng.random() < 0.02:
+            words.append(rng.choice([encode(0xE7), encode(0x81, 0, 1), encode(0xB7, 12, 0),
+                                     encode(0xE1, 0, 1)]))
+    if rng.random() < 0.9:
+        words.append(encode(0x95))
+    return b"".join(words)
+
+
+def gen_packet(rng: random.Random, max_len: int = 80) -> bytes:
+    n = rng.choice([0, 1, 2, 5, 14, 34, 60, 63, 64, 65, rng.randrange(0, max_len + 1)])
+    return bytes(rng.getrandbits(8) for _ in range(n))
