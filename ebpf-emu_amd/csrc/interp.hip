@@ -224,10 +224,19 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
 
     // ---- Emu::run (emu.rs:452-458) with min-pc re-convergence ----
     uint32_t wsteps = 0;
+    // Termination guard: every iteration retires >= 1 lane-step and a lane retires at most
+    // max_steps, so 64 * max_steps + 64 iterations bound a correct run; the guard only turns a
+    // re-convergence bug into EBPF_ST_STEPS instead of a hung wave.
+    uint64_t witer = 0;
+    const uint64_t witer_cap = (uint64_t)kWave * max_steps + kWave;
     for (;;) {
       uint32_t pcs = rfl(pc);
       if (ballot(pc != pcs) != 0) pcs = wave_min_u32(pc);
       if (pcs >= nu) break;  // every lane exited, fell off the end or faulted
+      if (++witer > witer_cap) {
+        if (pc != PC_DONE) { st = EBPF_ST_STEPS; pc = PC_DONE; }
+        break;
+      }
       if (++wsteps > max_steps) {  // exact per-lane budget only once it can bind
         if (pc == pcs && nsteps >= max_steps) {
           st = EBPF_ST_STEPS;
