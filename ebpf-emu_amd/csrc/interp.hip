@@ -110,17 +110,16 @@ __device__ __forceinline__ void img_write(uint32_t* img, uint32_t a, uint32_t w,
   }
 }
 
-template <int TIER>
+template <int TIER, bool LDSP>
 __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t nu = a.n_uops;
-  const bool lds_prog = nu <= (uint32_t)kMaxLdsUops;
-  const uint32_t prog_bytes = lds_prog ? nu * (uint32_t)sizeof(Uop) : 0u;
+  const uint32_t prog_bytes = LDSP ? nu * (uint32_t)sizeof(Uop) : 0u;
   Uop* sprog = (Uop*)smem;
   uint8_t* windows = smem + prog_bytes;
 
   // stage the program once per workgroup (emu.instructions, emu.rs:24)
-  if (lds_prog) {
+  if (LDSP) {
     const uint4* src = (const uint4*)a.prog;
     uint4* dst = (uint4*)sprog;
     for (uint32_t i = threadIdx.x; i < nu; i += kBlock) dst[i] = src[i];
@@ -223,12 +222,17 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
     }
 
     // ---- Emu::run (emu.rs:452-458) with min-pc re-convergence ----
+    // Each iteration executes the instruction at the wave's minimum pc for the lanes parked
+    // there ("act"). The step is computed by all lanes and COMMITTED through selects on act,
+    // so the eBPF register file (22 VGPRs, indexed by the scalar dst/src via s_set_gpr_idx)
+    // is never inside divergent control flow; only memory accesses are predicated on act.
     uint32_t wsteps = 0;
     // Termination guard: every iteration retires >= 1 lane-step and a lane retires at most
     // max_steps, so 64 * max_steps + 64 iterations bound a correct run; the guard only turns a
     // re-convergence bug into EBPF_ST_STEPS instead of a hung wave.
-    uint64_t witer = 0;
-    const uint64_t witer_cap = (uint64_t)kWave * max_steps + kWave;
+    uint32_t witer = 0;
+    const uint64_t cap64 = (uint64_t)kWave * max_steps + kWave;
+    const uint32_t witer_cap = cap64 > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)cap64;
     for (;;) {
       uint32_t pcs = rfl(pc);
       if (ballot(pc != pcs) != 0) pcs = wave_min_u32(pc);
@@ -238,218 +242,215 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
         break;
       }
       if (++wsteps > max_steps) {  // exact per-lane budget only once it can bind
-        if (pc == pcs && nsteps >= max_steps) {
-          st = EBPF_ST_STEPS;
-          pc = PC_DONE;
-        }
-        if (ballot(pc == pcs) == 0) continue;
+        const bool over = pc == pcs && nsteps >= max_steps;
+        st = over ? EBPF_ST_STEPS : st;
+        pc = over ? PC_DONE : pc;  // an iteration with no active lane commits nothing
       }
       // fetch (wave-uniform): emu.rs:49
-      uint32_t w0, w1, w2, w3;
-      if (lds_prog) {
-        const uint4 q = *(const uint4*)(sprog + pcs);
-        w0 = rfl(q.x); w1 = rfl(q.y); w2 = rfl(q.z); w3 = rfl(q.w);
-      } else {
-        const uint4 q = *(const uint4*)(a.prog + pcs);
-        w0 = rfl(q.x); w1 = rfl(q.y); w2 = rfl(q.z); w3 = rfl(q.w);
-      }
+      uint4 q;
+      if (LDSP) q = *(const uint4*)(sprog + pcs);
+      else q = *(const uint4*)(a.prog + pcs);
+      const uint32_t w0 = rfl(q.x), x = rfl(q.y), w2 = rfl(q.z), w3 = rfl(q.w);
       const uint32_t op = w0 & 0xff, dst = (w0 >> 8) & 0xff, src = (w0 >> 16) & 0xff;
       const uint32_t aux = w0 >> 24;
-      const uint32_t x = w1;
       const uint64_t k = (uint64_t)w2 | ((uint64_t)w3 << 32);
 
-      if (pc == pcs) {
-        nsteps++;
-        pc = pcs + 1;  // emu.rs:63
-        const uint64_t A = r[dst];
-        const uint64_t S = r[src];
-        const uint64_t B = (aux & F_SRC) ? S : k;
-        const uint32_t a32 = (uint32_t)A, b32 = (uint32_t)B;
-        uint64_t R = A;
-        bool fault = false;
-        uint32_t fst = 0;
-        switch (op) {
-          // ---- ALU64 ----
-          case U_ADD64: R = A + B; break;
-          case U_SUB64: R = A - B; break;
-          case U_MUL64: R = A * B; break;
-          case U_DIV64: R = B ? A / B : 0; break;
-          case U_OR64: R = A | B; break;
-          case U_AND64: R = A & B; break;
-          case U_LSH64: R = A << (b32 & 63); break;
-          case U_RSH64: R = A >> (b32 & 63); break;
-          case U_NEG64: R = 0 - A; break;
-          case U_MOD64: R = B ? A % B : A; break;
-          case U_XOR64: R = A ^ B; break;
-          case U_MOV64: R = B; break;
-          case U_ARSH64: {  // rotate, then multiply by the sign (Q4, emu.rs:142-164)
-            const uint32_t sh = b32 & 63;
-            const uint64_t rot = sh ? ((A >> sh) | (A << (64 - sh))) : A;
-            if ((int64_t)A < 0) {
-              if (rot == 0x8000000000000000ull) { fault = true; fst = EBPF_ST_ARITH; }
-              R = 0 - rot;
-            } else {
-              R = rot;
+      const bool act = pc == pcs;
+      const uint64_t A = r[dst];
+      const uint64_t S = r[src];
+      const uint64_t B = (aux & F_SRC) ? S : k;
+      const uint32_t a32 = (uint32_t)A, b32 = (uint32_t)B;
+      uint64_t R = A;             // dst value to commit
+      uint32_t npc = pcs + 1;     // emu.rs:63
+      bool fault = false;
+      uint32_t fst = 0;
+      bool w_r0 = false, w_src = false;  // atomic side writes (emu.rs:418,435)
+      uint64_t side = 0;
+      switch (op) {
+        // ---- ALU64 ----
+        case U_ADD64: R = A + B; break;
+        case U_SUB64: R = A - B; break;
+        case U_MUL64: R = A * B; break;
+        case U_DIV64: R = B ? A / B : 0; break;
+        case U_OR64: R = A | B; break;
+        case U_AND64: R = A & B; break;
+        case U_LSH64: R = A << (b32 & 63); break;
+        case U_RSH64: R = A >> (b32 & 63); break;
+        case U_NEG64: R = 0 - A; break;
+        case U_MOD64: R = B ? A % B : A; break;
+        case U_XOR64: R = A ^ B; break;
+        case U_MOV64: R = B; break;
+        case U_ARSH64: {  // rotate, then multiply by the sign (Q4, emu.rs:142-164)
+          const uint32_t sh = b32 & 63;
+          const uint64_t rot = sh ? ((A >> sh) | (A << (64 - sh))) : A;
+          const bool neg = (int64_t)A < 0;
+          fault = neg && rot == 0x8000000000000000ull;  // i64::MIN * -1 (emu.rs:162)
+          fst = EBPF_ST_ARITH;
+          R = neg ? 0 - rot : rot;
+          break;
+        }
+        // ---- ALU32 (Q6/Q25) ----
+        case U_ADD32: R = (uint32_t)(a32 + b32); break;
+        case U_SUB32: R = (uint32_t)(a32 - b32); break;
+        case U_MUL32: R = (uint32_t)(a32 * b32); break;
+        case U_DIV32: R = b32 ? a32 / b32 : 0u; break;
+        case U_OR32: R = a32 | b32; break;
+        case U_AND32: R = a32 & b32; break;
+        case U_LSH32: R = (uint32_t)(a32 << (b32 & 31)); break;
+        case U_RSH32: R = a32 >> (b32 & 31); break;
+        case U_NEG32: R = (uint32_t)(0u - a32); break;
+        case U_MOD32: R = b32 ? a32 % b32 : a32; break;
+        case U_XOR32: R = a32 ^ b32; break;
+        case U_MOV32: R = b32; break;
+        case U_ARSH32: {
+          const uint32_t rot = __builtin_amdgcn_alignbit(a32, a32, b32 & 31);
+          R = (int32_t)a32 < 0 ? (uint32_t)(0u - rot) : rot;
+          break;
+        }
+        // ---- END (Q7) ----
+        case U_ZX16: R = A & 0xffffull; break;
+        case U_ZX32: R = A & 0xffffffffull; break;
+        case U_NOP: break;
+        case U_BSWAP16: R = ((A & 0xff) << 8) | ((A >> 8) & 0xff); break;
+        case U_BSWAP32: R = bswap32(a32); break;
+        case U_BSWAP64: R = ((uint64_t)bswap32(a32) << 32) | bswap32((uint32_t)(A >> 32)); break;
+        // ---- JMP: signed orderings (Q2) ----
+        case U_JA: npc = x; break;
+        case U_JEQ: npc = A == B ? x : npc; break;
+        case U_JGT: npc = (int64_t)A > (int64_t)B ? x : npc; break;
+        case U_JGE: npc = (int64_t)A >= (int64_t)B ? x : npc; break;
+        case U_JSET: npc = (A & B) ? x : npc; break;
+        case U_JNE: npc = A != B ? x : npc; break;
+        case U_JLT: npc = (int64_t)A < (int64_t)B ? x : npc; break;
+        case U_JLE: npc = (int64_t)A <= (int64_t)B ? x : npc; break;
+        // ---- JMP32: sign-extended low words (Q3) ----
+        case U_JEQ32: npc = a32 == b32 ? x : npc; break;
+        case U_JGT32: npc = (int32_t)a32 > (int32_t)b32 ? x : npc; break;
+        case U_JGE32: npc = (int32_t)a32 >= (int32_t)b32 ? x : npc; break;
+        case U_JSET32: npc = (a32 & b32) ? x : npc; break;  // == (sext(a) & sext(b)) != 0
+        case U_JNE32: npc = a32 != b32 ? x : npc; break;
+        case U_JLT32: npc = (int32_t)a32 < (int32_t)b32 ? x : npc; break;
+        case U_JLE32: npc = (int32_t)a32 <= (int32_t)b32 ? x : npc; break;
+        case U_CALL:  // emu.rs:265-272
+          if (TIER == 1) {
+            fault = csp >= (uint32_t)kCallDepth;
+            fst = EBPF_ST_CALLDEPTH;
+            if (act && !fault) {
+              cstack[(size_t)csp * kWave] = x + 1;
+              csp++;
             }
-            break;
+            npc = x;
+          } else {
+            fault = true;  // unreachable: the loader routes calls to tier 1
+            fst = EBPF_ST_INSN;
           }
-          // ---- ALU32 (Q6/Q25) ----
-          case U_ADD32: R = (uint32_t)(a32 + b32); break;
-          case U_SUB32: R = (uint32_t)(a32 - b32); break;
-          case U_MUL32: R = (uint32_t)(a32 * b32); break;
-          case U_DIV32: R = b32 ? a32 / b32 : 0u; break;
-          case U_OR32: R = a32 | b32; break;
-          case U_AND32: R = a32 & b32; break;
-          case U_LSH32: R = (uint32_t)(a32 << (b32 & 31)); break;
-          case U_RSH32: R = a32 >> (b32 & 31); break;
-          case U_NEG32: R = (uint32_t)(0u - a32); break;
-          case U_MOD32: R = b32 ? a32 % b32 : a32; break;
-          case U_XOR32: R = a32 ^ b32; break;
-          case U_MOV32: R = b32; break;
-          case U_ARSH32: {
-            const uint32_t rot = __builtin_amdgcn_alignbit(a32, a32, b32 & 31);
-            R = (int32_t)a32 < 0 ? (uint32_t)(0u - rot) : rot;
-            break;
+          break;
+        case U_EXIT:  // emu.rs:273-279
+          npc = PC_DONE;
+          if (TIER == 1 && act && csp > 0) {
+            csp--;
+            npc = cstack[(size_t)csp * kWave];
           }
-          // ---- END (Q7) ----
-          case U_ZX16: R = A & 0xffffull; break;
-          case U_ZX32: R = A & 0xffffffffull; break;
-          case U_NOP: break;
-          case U_BSWAP16: R = ((A & 0xff) << 8) | ((A >> 8) & 0xff); break;
-          case U_BSWAP32: R = bswap32(a32); break;
-          case U_BSWAP64: R = ((uint64_t)bswap32(a32) << 32) | bswap32((uint32_t)(A >> 32)); break;
-          // ---- JMP: signed orderings (Q2) ----
-          case U_JA: pc = x; break;
-          case U_JEQ: if (A == B) pc = x; break;
-          case U_JGT: if ((int64_t)A > (int64_t)B) pc = x; break;
-          case U_JGE: if ((int64_t)A >= (int64_t)B) pc = x; break;
-          case U_JSET: if (A & B) pc = x; break;
-          case U_JNE: if (A != B) pc = x; break;
-          case U_JLT: if ((int64_t)A < (int64_t)B) pc = x; break;
-          case U_JLE: if ((int64_t)A <= (int64_t)B) pc = x; break;
-          // ---- JMP32: sign-extended low words (Q3) ----
-          case U_JEQ32: if (a32 == b32) pc = x; break;
-          case U_JGT32: if ((int32_t)a32 > (int32_t)b32) pc = x; break;
-          case U_JGE32: if ((int32_t)a32 >= (int32_t)b32) pc = x; break;
-          case U_JSET32: if (a32 & b32) pc = x; break;  // == (sext(a) & sext(b)) != 0
-          case U_JNE32: if (a32 != b32) pc = x; break;
-          case U_JLT32: if ((int32_t)a32 < (int32_t)b32) pc = x; break;
-          case U_JLE32: if ((int32_t)a32 <= (int32_t)b32) pc = x; break;
-          case U_CALL:  // emu.rs:265-272
-            if (TIER == 1) {
-              if (csp >= (uint32_t)kCallDepth) {
-                fault = true;
-                fst = EBPF_ST_CALLDEPTH;
-              } else {
-                cstack[(size_t)csp * kWave] = x + 1;
-                csp++;
-                pc = x;
-              }
-            } else {
-              fault = true;  // unreachable: the loader routes calls to tier 1
-              fst = EBPF_ST_INSN;
-            }
-            break;
-          case U_EXIT:  // emu.rs:273-279
-            if (TIER == 1 && csp > 0) {
-              csp--;
-              pc = cstack[(size_t)csp * kWave];
-            } else {
-              pc = PC_DONE;
-            }
-            break;
-          // ---- loads / stores (emu.rs:311-444) ----
-          case U_LDIMM: R = k; break;
-          case U_LDX: {
+          break;
+        // ---- loads / stores (emu.rs:311-444) ----
+        case U_LDIMM: R = k; break;
+        case U_LDX: {
+          int64_t sum;
+          const bool ovf = __builtin_add_overflow((int64_t)S, (int64_t)(int32_t)x, &sum);
+          const uint64_t ua = (uint64_t)sum;
+          const bool oob = ovf || ua >= mem_size;
+          const bool ub = !oob && ua + aux > mem_size;
+          fault = oob || ub;
+          fst = oob ? EBPF_ST_MEM : EBPF_ST_MEM_UB;
+          const uint32_t a0 = (uint32_t)ua;
+          uint64_t v = 0;
+          if (act && !fault) {
+            if (TIER == 1) v = img_read(img, a0, aux);
+            else if (a0 + aux <= (uint32_t)kWin) v = win_read(my_win, a0, aux);
+            else if (a0 < len) v = pkt_read(base, a0, aux, len);
+          }
+          const uint64_t m = wmask(aux);
+          R = (A & ~m) | v;  // upper bytes preserved (Q1)
+          break;
+        }
+        case U_ST:
+        case U_STX: {
+          if (TIER == 1) {
             int64_t sum;
-            const bool ovf = __builtin_add_overflow((int64_t)S, (int64_t)(int32_t)x, &sum);
+            const bool ovf = __builtin_add_overflow((int64_t)A, (int64_t)(int32_t)x, &sum);
             const uint64_t ua = (uint64_t)sum;
-            if (ovf || ua >= mem_size) { fault = true; fst = EBPF_ST_MEM; }
-            else if (ua + aux > mem_size) { fault = true; fst = EBPF_ST_MEM_UB; }
-            else {
-              const uint32_t a0 = (uint32_t)ua;
-              uint64_t v;
-              if (TIER == 1) v = img_read(img, a0, aux);
-              else if (a0 + aux <= (uint32_t)kWin) v = win_read(my_win, a0, aux);
-              else if (a0 >= len) v = 0;
-              else v = pkt_read(base, a0, aux, len);
-              const uint64_t m = wmask(aux);
-              R = (A & ~m) | v;  // upper bytes preserved (Q1)
-            }
-            break;
-          }
-          case U_ST:
-          case U_STX: {
-            if (TIER == 1) {
-              int64_t sum;
-              const bool ovf = __builtin_add_overflow((int64_t)A, (int64_t)(int32_t)x, &sum);
-              const uint64_t ua = (uint64_t)sum;
-              if (ovf || ua >= mem_size) { fault = true; fst = EBPF_ST_MEM; }
-              else if (ua + aux > mem_size) { fault = true; fst = EBPF_ST_MEM_UB; }
-              else img_write(img, (uint32_t)ua, aux, op == U_ST ? k : S);
-            } else {
-              fault = true;
-              fst = EBPF_ST_INSN;
-            }
-            break;
-          }
-          case U_ATOMIC: {  // emu.rs:373-437
-            if (TIER == 1) {
-              int64_t sum;
-              const bool ovf = __builtin_add_overflow((int64_t)A, (int64_t)(int32_t)x, &sum);
-              const uint64_t ua = (uint64_t)sum;
-              if (ovf || ua >= mem_size || ua + 8 > mem_size) { fault = true; fst = EBPF_ST_MEM; break; }
-              uint64_t orig = img_read(img, (uint32_t)ua, 8);
-              const bool fetch = aux & F_FETCH;
-              const bool is32 = aux & F_ATOMIC32;
-              uint64_t bak = fetch ? orig : 0;
-              uint64_t high = 0, sv = S, r0v = r[0];
-              if (is32) {
-                sv = (uint32_t)sv;
-                high = orig >> 32;
-                orig = (uint32_t)orig;
-                r0v = (uint32_t)r0v;
-                bak = (uint32_t)bak;
-              }
-              if (k == 0x00) {
-                int64_t t;
-                if (__builtin_add_overflow((int64_t)orig, (int64_t)sv, &t)) {
-                  fault = true; fst = EBPF_ST_ARITH; break;
-                }
-                orig = (uint64_t)t;
-              } else if (k == 0x40) orig |= sv;
-              else if (k == 0x50) orig &= sv;
-              else if (k == 0xa0) orig ^= sv;
-              else if (k == 0xe0) { bak = orig; orig = sv; }
-              else if (k == 0xf0) {
-                if (orig == r0v) orig = sv;
-                r[0] = bak;
-              } else { fault = true; fst = EBPF_ST_INSN; break; }
-              int64_t t;
-              if (__builtin_add_overflow((int64_t)orig, (int64_t)(high << 32), &t)) {
-                fault = true; fst = EBPF_ST_ARITH; break;
-              }
-              img_write(img, (uint32_t)ua, 8, (uint64_t)t);
-              if (fetch) r[src] = bak;
-            } else {
-              fault = true;
-              fst = EBPF_ST_INSN;
-            }
-            break;
-          }
-          default:  // U_FAULT
+            const bool oob = ovf || ua >= mem_size;
+            const bool ub = !oob && ua + aux > mem_size;
+            fault = oob || ub;
+            fst = oob ? EBPF_ST_MEM : EBPF_ST_MEM_UB;
+            if (act && !fault) img_write(img, (uint32_t)ua, aux, op == U_ST ? k : S);
+          } else {
             fault = true;
-            fst = aux;
-            break;
+            fst = EBPF_ST_INSN;
+          }
+          break;
         }
-        if (fault) {
-          st = fst;
-          pc = PC_DONE;
-          nsteps--;  // the faulting instruction does not retire
-        } else {
-          r[dst] = R;  // single write-back; ST/STX/ATOMIC rewrite the dst snapshot (Q14)
+        case U_ATOMIC: {  // emu.rs:373-437
+          if (TIER == 1) {
+            int64_t sum;
+            const bool ovf = __builtin_add_overflow((int64_t)A, (int64_t)(int32_t)x, &sum);
+            const uint64_t ua = (uint64_t)sum;
+            fault = ovf || ua >= mem_size || ua + 8 > mem_size;
+            fst = EBPF_ST_MEM;
+            const bool go = act && !fault;
+            uint64_t orig = go ? img_read(img, (uint32_t)ua, 8) : 0;
+            const bool fetch = aux & F_FETCH;
+            const bool is32 = aux & F_ATOMIC32;
+            uint64_t bak = fetch ? orig : 0;
+            uint64_t high = 0, sv = S, r0v = r[0];
+            if (is32) {
+              sv = (uint32_t)sv;
+              high = orig >> 32;
+              orig = (uint32_t)orig;
+              r0v = (uint32_t)r0v;
+              bak = (uint32_t)bak;
+            }
+            bool f2 = false;
+            uint32_t fst2 = EBPF_ST_ARITH;
+            if (k == 0x00) {
+              int64_t t;
+              f2 = __builtin_add_overflow((int64_t)orig, (int64_t)sv, &t);
+              orig = (uint64_t)t;
+            } else if (k == 0x40) orig |= sv;
+            else if (k == 0x50) orig &= sv;
+            else if (k == 0xa0) orig ^= sv;
+            else if (k == 0xe0) { bak = orig; orig = sv; }
+            else if (k == 0xf0) {
+              if (orig == r0v) orig = sv;
+              w_r0 = true;
+            } else { f2 = true; fst2 = EBPF_ST_INSN; }
+            int64_t t;
+            const bool f3 = __builtin_add_overflow((int64_t)orig, (int64_t)(high << 32), &t);
+            if (!fault && (f2 || f3)) { fault = true; fst = f2 ? fst2 : EBPF_ST_ARITH; }
+            if (act && !fault) img_write(img, (uint32_t)ua, 8, (uint64_t)t);
+            w_src = fetch;
+            side = bak;
+          } else {
+            fault = true;
+            fst = EBPF_ST_INSN;
+          }
+          break;
         }
+        default:  // U_FAULT
+          fault = true;
+          fst = aux;
+          break;
       }
+      // ---- commit (active lanes only) ----
+      const bool ok = act && !fault;
+      if (TIER == 1) {
+        if (w_r0) r[0] = ok ? side : r[0];      // cmpxchg: regs[0] = old (emu.rs:418)
+        if (w_src) r[src] = ok ? side : r[src];  // fetch: regs[src] = old (emu.rs:435)
+      }
+      r[dst] = ok ? R : A;  // dst snapshot write-back for ST/STX/ATOMIC (Q14, emu.rs:443)
+      nsteps += ok ? 1u : 0u;
+      st = (act && fault) ? fst : st;
+      pc = act ? (fault ? PC_DONE : npc) : pc;
     }
 
     // ---- outputs: r0 (main.rs:43), status, verdict (xdp.rs:3-9), final image ----
@@ -549,8 +550,10 @@ int interp_grid(int tier, uint32_t n_uops, uint64_t n_tiles, int* grid_out) {
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return -1;
   const uint32_t lds = lds_bytes_for(n_uops);
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, interp_kernel<1>, kBlock, lds) !=
-          hipSuccess || per_cu < 1)
+  hipError_t e = n_uops <= (uint32_t)kMaxLdsUops
+      ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, interp_kernel<1, true>, kBlock, lds)
+      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, interp_kernel<1, false>, kBlock, lds);
+  if (e != hipSuccess || per_cu < 1)
     per_cu = 1;
   if (per_cu > 4) per_cu = 4;  // bounds the tier-1 image scratch
   const uint64_t cap = (uint64_t)cus * (uint64_t)per_cu;
@@ -560,10 +563,15 @@ int interp_grid(int tier, uint32_t n_uops, uint64_t n_tiles, int* grid_out) {
 
 hipError_t launch_interp(int tier, const LaunchArgs& a, int grid, hipStream_t stream) {
   const uint32_t lds = lds_bytes_for(a.n_uops);
-  if (tier == 1)
-    hipLaunchKernelGGL(interp_kernel<1>, dim3(grid), dim3(kBlock), lds, stream, a);
+  const bool ldsp = a.n_uops <= (uint32_t)kMaxLdsUops;
+  if (tier == 1 && ldsp)
+    hipLaunchKernelGGL((interp_kernel<1, true>), dim3(grid), dim3(kBlock), lds, stream, a);
+  else if (tier == 1)
+    hipLaunchKernelGGL((interp_kernel<1, false>), dim3(grid), dim3(kBlock), lds, stream, a);
+  else if (ldsp)
+    hipLaunchKernelGGL((interp_kernel<0, true>), dim3(grid), dim3(kBlock), lds, stream, a);
   else
-    hipLaunchKernelGGL(interp_kernel<0>, dim3(grid), dim3(kBlock), lds, stream, a);
+    hipLaunchKernelGGL((interp_kernel<0, false>), dim3(grid), dim3(kBlock), lds, stream, a);
   return hipGetLastError();
 }
 
