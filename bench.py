@@ -45,6 +45,7 @@ def parse():
     ap.add_argument("--pool-mib", type=int, default=512, help="min bytes of distinct batches")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0=skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, affinity)")
+    ap.add_argument("--no-counters", action="store_true", help="A/B: verdicts only")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC traffic summary (profiles/*.json) to report as roofline.traffic")
     return ap.parse_args()
@@ -111,7 +112,7 @@ def main():
         descs.append(bd)
     out = _lib.BatchOut()
     out.verdict = verdict.data_ptr()
-    out.counters = counters.data_ptr()
+    out.counters = None if args.no_counters else counters.data_ptr()
     stream = torch.cuda.current_stream(dev)
 
     def step(i):
@@ -149,7 +150,8 @@ def main():
 
     cnt = [int(c) & ((1 << 64) - 1) for c in counters.cpu().tolist()]
     total_pkts = n * args.steps * world
-    assert sum(cnt[:7]) == total_pkts, (cnt, total_pkts)  # every packet has exactly one verdict
+    if not args.no_counters:
+        assert sum(cnt[:7]) == total_pkts, (cnt, total_pkts)  # every packet: exactly one verdict
     mpps = total_pkts / elapsed / 1e6
     achieved_gbs = algo_bytes / (kern_avg_ms * 1e-3) / 1e9
 

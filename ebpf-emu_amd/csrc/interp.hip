@@ -497,18 +497,22 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
   __syncthreads();
   if (a.counters == nullptr) return;
   __shared__ uint32_t last_flag;
-  if (threadIdx.x < 8) {
-    uint64_t s = 0;
+  if (threadIdx.x < kWave) {  // wave 0
+    // Shard adds are RETURNING device-scope atomics; waiting for their return values
+    // (vmcnt(0)) means they are performed at the coherence point before this workgroup's
+    // ticket add is issued ("8-byte agent atomics on both sides", MI355X_MICROARCH.md): no
+    // cache write-back fence is needed because no plain stores are handed off.
+    uint64_t old = 0;
+    if (threadIdx.x < 8) {
+      uint64_t s = 0;
 #pragma unroll
-    for (int w = 0; w < kWavesPerBlock; w++) s += red[w * 8 + threadIdx.x];
-    if (s)
-      __hip_atomic_fetch_add(&a.shards[(blockIdx.x % kCounterShards) * 8 + threadIdx.x], s,
-                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  if (threadIdx.x < kWave) {  // wave 0: its shard atomics are performed before the ticket
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      for (int w = 0; w < kWavesPerBlock; w++) s += red[w * 8 + threadIdx.x];
+      old = __hip_atomic_fetch_add(&a.shards[(blockIdx.x % kCounterShards) * 8 + threadIdx.x], s,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::"v"(old) : "memory");
     if (threadIdx.x == 0) {
-      const uint32_t t = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_ACQ_REL,
+      const uint32_t t = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED,
                                                 __HIP_MEMORY_SCOPE_AGENT);
       last_flag = (t == gridDim.x - 1);
     }
