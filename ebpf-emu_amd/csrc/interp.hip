@@ -39,6 +39,47 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
   return __builtin_amdgcn_readlane(v, 63);
 }
 
+// Explicit global (address space 1) accesses: pointers carried in LaunchArgs would otherwise be
+// generic and lower to flat_* instructions (which also count against lgkmcnt).
+typedef __attribute__((address_space(1))) const uint8_t g_u8;
+typedef __attribute__((address_space(1))) const uint32_t g_u32;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const u32x4 g_u4;
+__device__ __forceinline__ uint32_t gld8(uintptr_t p) { return *(g_u8*)p; }
+__device__ __forceinline__ uint32_t gld32(uintptr_t p) { return *(g_u32*)p; }
+__device__ __forceinline__ uint4 gld128(uintptr_t p) {
+  const u32x4 v = *(g_u4*)p;
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+// Set of pcs at which some lane of the wave is parked, for programs of up to 64 * NW micro-ops:
+// the next pc to run is its lowest member (s_ff1), replacing a per-step wave-wide min.
+template <int NW>
+struct PcSet {
+  uint64_t w[NW > 0 ? NW : 1];
+  __device__ __forceinline__ void init(bool any) {
+#pragma unroll
+    for (int i = 0; i < (NW > 0 ? NW : 1); i++) w[i] = 0;
+    if (any) w[0] = 1;  // every lane starts at pc 0
+  }
+  __device__ __forceinline__ uint32_t first() const {
+#pragma unroll
+    for (int i = 0; i < NW; i++)
+      if (w[i]) return (uint32_t)(i * 64 + __builtin_ctzll(w[i]));
+    return PC_DONE;
+  }
+  __device__ __forceinline__ void add(uint32_t p) {
+#pragma unroll
+    for (int i = 0; i < NW; i++)
+      if ((p >> 6) == (uint32_t)i) w[i] |= 1ull << (p & 63);
+  }
+  __device__ __forceinline__ void del(uint32_t p) {
+#pragma unroll
+    for (int i = 0; i < NW; i++)
+      if ((p >> 6) == (uint32_t)i) w[i] &= ~(1ull << (p & 63));
+  }
+};
+
 __device__ __forceinline__ uint64_t wmask(uint32_t w) {
   return w >= 8 ? ~0ull : ((1ull << (8 * w)) - 1);
 }
@@ -50,16 +91,16 @@ __device__ __forceinline__ uint32_t bswap32(uint32_t v) { return __builtin_bswap
 // are loaded, so no access leaves the page of a valid byte.
 __device__ __forceinline__ uint64_t pkt_read(const uint8_t* base, uint32_t a, uint32_t w,
                                              uint32_t len) {
-  if (w == 1) return base[a];
+  if (w == 1) return gld8((uintptr_t)base + a);
   const uintptr_t p = (uintptr_t)base + a;
   const uintptr_t end = (uintptr_t)base + len;
-  const uint32_t* p4 = (const uint32_t*)(p & ~(uintptr_t)3);
+  const uintptr_t p4 = p & ~(uintptr_t)3;
   const uint32_t s = (uint32_t)(p & 3);
-  const uint32_t d0 = p4[0];
-  const uint32_t d1 = ((uintptr_t)(p4 + 1) < end) ? p4[1] : 0u;
+  const uint32_t d0 = gld32(p4);
+  const uint32_t d1 = (p4 + 4 < end) ? gld32(p4 + 4) : 0u;
   uint64_t v = __builtin_amdgcn_alignbyte(d1, d0, s);
   if (w == 8) {
-    const uint32_t d2 = ((uintptr_t)(p4 + 2) < end) ? p4[2] : 0u;
+    const uint32_t d2 = (p4 + 8 < end) ? gld32(p4 + 8) : 0u;
     v |= (uint64_t)__builtin_amdgcn_alignbyte(d2, d1, s) << 32;
   }
   const uint32_t valid = len - a;
@@ -110,7 +151,7 @@ __device__ __forceinline__ void img_write(uint32_t* img, uint32_t a, uint32_t w,
   }
 }
 
-template <int TIER, bool LDSP>
+template <int TIER, bool LDSP, int NW>
 __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t nu = a.n_uops;
@@ -166,7 +207,7 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
           const uint64_t bj = (uint64_t)__shfl((long long)(uintptr_t)base, j);
           const uint32_t lj = (uint32_t)__shfl((int)len, j);
           q[r] = make_uint4(0, 0, 0, 0);
-          if (c * 16 < min(lj, (uint32_t)kWin)) q[r] = *(const uint4*)(bj + c * 16);
+          if (c * 16 < min(lj, (uint32_t)kWin)) q[r] = gld128((uintptr_t)(bj + c * 16));
         }
 #pragma unroll
         for (int r = 0; r < 4; r++) {
@@ -233,9 +274,16 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
     uint32_t witer = 0;
     const uint64_t cap64 = (uint64_t)kWave * max_steps + kWave;
     const uint32_t witer_cap = cap64 > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)cap64;
+    PcSet<NW> live;
+    if (NW > 0) live.init(nu > 0 && ballot(pc == 0) != 0);
     for (;;) {
-      uint32_t pcs = rfl(pc);
-      if (ballot(pc != pcs) != 0) pcs = wave_min_u32(pc);
+      uint32_t pcs;
+      if (NW > 0) {
+        pcs = live.first();
+      } else {
+        pcs = rfl(pc);
+        if (ballot(pc != pcs) != 0) pcs = wave_min_u32(pc);
+      }
       if (pcs >= nu) break;  // every lane exited, fell off the end or faulted
       if (++witer > witer_cap) {
         if (pc != PC_DONE) { st = EBPF_ST_STEPS; pc = PC_DONE; }
@@ -450,7 +498,22 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
       r[dst] = ok ? R : A;  // dst snapshot write-back for ST/STX/ATOMIC (Q14, emu.rs:443)
       nsteps += ok ? 1u : 0u;
       st = (act && fault) ? fst : st;
-      pc = act ? (fault ? PC_DONE : npc) : pc;
+      pc = act ? (fault || npc >= nu ? PC_DONE : npc) : pc;
+      if (NW > 0) {  // successors of this step: pcs + 1, the jump/call target, popped returns
+        live.del(pcs);
+        const uint32_t f = pcs + 1;
+        if (f < nu && ballot(act && pc == f) != 0) live.add(f);
+        const bool jumps = op >= U_JA && op <= U_CALL;
+        if (jumps && x < nu && x != f && ballot(act && pc == x) != 0) live.add(x);
+        if (TIER == 1 && op == U_EXIT) {
+          uint64_t m = ballot(act && pc < nu);
+          while (m) {
+            const uint32_t p = __builtin_amdgcn_readlane(pc, __builtin_ctzll(m));
+            live.add(p);
+            m &= ~ballot(pc == p);
+          }
+        }
+      }
     }
 
     // ---- outputs: r0 (main.rs:43), status, verdict (xdp.rs:3-9), final image ----
@@ -543,6 +606,19 @@ static uint32_t lds_bytes_for(uint32_t n_uops) {
   return prog + win;
 }
 
+// Kernel variant for a program: tier (memory model), LDS-staged program, scheduler width.
+template <int TIER>
+static const void* variant(uint32_t n_uops) {
+  if (n_uops <= 64) return (const void*)interp_kernel<TIER, true, 1>;
+  if (n_uops <= 256) return (const void*)interp_kernel<TIER, true, 4>;
+  if (n_uops <= (uint32_t)kMaxLdsUops) return (const void*)interp_kernel<TIER, true, 0>;
+  return (const void*)interp_kernel<TIER, false, 0>;
+}
+
+static const void* kernel_for(int tier, uint32_t n_uops) {
+  return tier == 1 ? variant<1>(n_uops) : variant<0>(n_uops);
+}
+
 int interp_grid(int tier, uint32_t n_uops, uint64_t n_tiles, int* grid_out) {
   const uint64_t want = (n_tiles + kWavesPerBlock - 1) / kWavesPerBlock;
   if (tier == 0) {  // one tile per wave; the dispatcher load-balances divergent tiles
@@ -554,10 +630,9 @@ int interp_grid(int tier, uint32_t n_uops, uint64_t n_tiles, int* grid_out) {
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return -1;
   const uint32_t lds = lds_bytes_for(n_uops);
-  hipError_t e = n_uops <= (uint32_t)kMaxLdsUops
-      ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, interp_kernel<1, true>, kBlock, lds)
-      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, interp_kernel<1, false>, kBlock, lds);
-  if (e != hipSuccess || per_cu < 1)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel_for(tier, n_uops), kBlock,
+                                                   lds) != hipSuccess ||
+      per_cu < 1)
     per_cu = 1;
   if (per_cu > 4) per_cu = 4;  // bounds the tier-1 image scratch
   const uint64_t cap = (uint64_t)cus * (uint64_t)per_cu;
@@ -567,16 +642,8 @@ int interp_grid(int tier, uint32_t n_uops, uint64_t n_tiles, int* grid_out) {
 
 hipError_t launch_interp(int tier, const LaunchArgs& a, int grid, hipStream_t stream) {
   const uint32_t lds = lds_bytes_for(a.n_uops);
-  const bool ldsp = a.n_uops <= (uint32_t)kMaxLdsUops;
-  if (tier == 1 && ldsp)
-    hipLaunchKernelGGL((interp_kernel<1, true>), dim3(grid), dim3(kBlock), lds, stream, a);
-  else if (tier == 1)
-    hipLaunchKernelGGL((interp_kernel<1, false>), dim3(grid), dim3(kBlock), lds, stream, a);
-  else if (ldsp)
-    hipLaunchKernelGGL((interp_kernel<0, true>), dim3(grid), dim3(kBlock), lds, stream, a);
-  else
-    hipLaunchKernelGGL((interp_kernel<0, false>), dim3(grid), dim3(kBlock), lds, stream, a);
-  return hipGetLastError();
+  void* args[] = {(void*)&a};
+  return hipLaunchKernel(kernel_for(tier, a.n_uops), dim3(grid), dim3(kBlock), args, lds, stream);
 }
 
 }  // namespace ebpfemu

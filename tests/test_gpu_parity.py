@@ -124,6 +124,32 @@ def test_fuzz_wave_divergence(cuda, oracle_mod, seed):
     assert tiers == {0, 1}
 
 
+@pytest.mark.parametrize("pad", [70, 300, 5000])
+def test_program_size_variants(cuda, oracle_mod, pad):
+    """Programs past 64 / 256 micro-ops (wider pc-set scheduler, DPP wave-min scheduler) and past
+    4096 (micro-ops fetched from global memory instead of LDS): a `ja` over `pad` never-executed
+    instructions, then a fuzzed program; some programs also jump back into the padding."""
+    from ebpf_emu.asm import encode
+
+    rng = random.Random(77 + pad)
+    filler = b"".join(encode(0xB7, rng.randrange(10), 0, 0, rng.randrange(100)) for _ in range(pad))
+    n_ok = 0
+    for it in range(25):
+        body = gen_program(rng)
+        try:
+            oracle_mod.Program(body)
+        except oracle_mod.OracleDecodeError:
+            continue
+        img = encode(0x05, 0, 0, pad) + filler + body
+        if it % 5 == 0:  # re-enter the padding from the end of the program
+            img += encode(0x05, 0, 0, -(len(img) // 8) + 1 + rng.randrange(pad))
+        pkts = [gen_packet(rng) for _ in range(70)]
+        got = _run_full(img, pkts, cuda)
+        _check_against_oracle(oracle_mod, img, pkts, got, tag=f"pad {pad} it {it}")
+        n_ok += 1
+    assert n_ok >= 15
+
+
 def test_layouts_and_alignment(cuda, oracle_mod):
     """Stride and offsets layouts, 16-byte-aligned (coalesced staging) and misaligned (per-lane
     staging) packet bases, packets shorter/longer than the 64-byte LDS window."""
