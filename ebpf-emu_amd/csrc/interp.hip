@@ -19,6 +19,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <map>
+#include <mutex>
+#include <tuple>
+
 #include "../../include/ebpf_emu.h"
 #include "launch.h"
 #include "uop.h"
@@ -151,6 +155,75 @@ __device__ __forceinline__ void img_write(uint32_t* img, uint32_t a, uint32_t w,
   }
 }
 
+// ---- tier-0 header-window pipeline ----
+// Per-lane packet metadata as loaded (offset word, length); the packet base is formed only
+// where it is used, so the offsets load can be issued two tiles ahead without a stall.
+struct MetaRaw {
+  uint32_t off;
+  uint32_t len;
+};
+
+__device__ __forceinline__ MetaRaw load_meta(const LaunchArgs& a, uint64_t tile, uint32_t lane) {
+  MetaRaw m{0, 0};
+  const uint64_t pkt = tile * kWave + lane;
+  if (tile < a.n_tiles && pkt < a.n) {
+    if (a.offsets) m.off = a.offsets[pkt];
+    m.len = a.lens ? (uint32_t)a.lens[pkt]
+                   : (uint32_t)(a.stride > 0xFFFFFFFFull ? 0xFFFFFFFFull : a.stride);
+  }
+  return m;
+}
+
+__device__ __forceinline__ uintptr_t pkt_base(const LaunchArgs& a, uint64_t tile, uint32_t lane,
+                                              const MetaRaw& m) {
+  const uint64_t pkt = tile * kWave + lane;
+  return (uintptr_t)a.frames + (a.offsets ? (uint64_t)m.off : pkt * a.stride);
+}
+
+// Wave-uniform: every valid packet base of the tile is 16-byte aligned (coalesced staging).
+__device__ __forceinline__ bool tile_coalescible(const LaunchArgs& a, uint64_t tile, uint32_t lane,
+                                                 const MetaRaw& m) {
+  const bool valid = tile * kWave + lane < a.n;
+  return ballot(valid && (pkt_base(a, tile, lane, m) & 15) != 0) == 0;
+}
+
+// Issue the 16-byte loads of a tile's 64 header windows: lane l loads 16 bytes (chunk l % 4) of
+// packet 16 r + l / 4 in round r, so each wave instruction reads 16 packets x 64 contiguous bytes.
+__device__ __forceinline__ void issue_window(const LaunchArgs& a, uint64_t tile, uint32_t lane,
+                                             const MetaRaw& m, uint4 q[4]) {
+  const uint32_t c = lane & 3;
+  const uintptr_t base = pkt_base(a, tile, lane, m);
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const int j = r * 16 + (int)(lane >> 2);
+    const uint64_t bj = (uint64_t)__shfl((long long)base, j);
+    const uint32_t lj = (uint32_t)__shfl((int)m.len, j);
+    q[r] = make_uint4(0, 0, 0, 0);
+    if (c * 16 < min(lj, (uint32_t)kWin)) q[r] = gld128((uintptr_t)(bj + c * 16));
+  }
+}
+
+// Write the loaded chunks to the packets' LDS windows; bytes at or past len read as zero.
+__device__ __forceinline__ void commit_window(uint8_t* wave_win, uint32_t lane, const MetaRaw& m,
+                                              const uint4 q[4]) {
+  const uint32_t c = lane & 3;
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const int j = r * 16 + (int)(lane >> 2);
+    const uint32_t lj = (uint32_t)__shfl((int)m.len, j);
+    const uint32_t d[4] = {q[r].x, q[r].y, q[r].z, q[r].w};
+    uint32_t* wdst = (uint32_t*)(wave_win + (size_t)j * kWinStride + c * 16);
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+      const uint32_t off = c * 16 + e * 4;
+      uint32_t v = d[e];
+      if (off >= lj) v = 0;
+      else if (lj - off < 4) v &= (uint32_t)wmask(lj - off);
+      wdst[e] = v;
+    }
+  }
+}
+
 template <int TIER, bool LDSP, int NW>
 __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -184,48 +257,31 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
   uint64_t cnt[7] = {0, 0, 0, 0, 0, 0, 0};  // wave-uniform verdict buckets + faults
   uint64_t retired = 0;                     // per lane
 
+  // Tier 0 software pipeline: while tile t is interpreted, the header windows of tile t + W are
+  // in flight to registers and the metadata of tile t + 2W is being loaded (W = total waves).
+  MetaRaw m_cur = load_meta(a, wave_slot, lane);
+  MetaRaw m_nxt = load_meta(a, wave_slot + total_waves, lane);
+  bool co_cur = false;
+  uint4 q_cur[4];
+  if (TIER == 0 && wave_slot < a.n_tiles) {
+    co_cur = tile_coalescible(a, wave_slot, lane, m_cur);
+    if (co_cur) issue_window(a, wave_slot, lane, m_cur, q_cur);
+  }
+
   for (uint64_t tile = wave_slot; tile < a.n_tiles; tile += total_waves) {
     const uint64_t pkt = tile * kWave + lane;
     const bool valid = pkt < a.n;
-    const uint8_t* base = nullptr;
-    uint32_t len = 0;
-    if (valid) {
-      base = a.frames + (a.offsets ? (uint64_t)a.offsets[pkt] : pkt * a.stride);
-      len = a.lens ? (uint32_t)a.lens[pkt]
-                   : (uint32_t)(a.stride > 0xFFFFFFFFull ? 0xFFFFFFFFull : a.stride);
-    }
+    const uint32_t len = m_cur.len;
+    const uint8_t* base = valid ? (const uint8_t*)pkt_base(a, tile, lane, m_cur) : nullptr;
 
+    bool co_nxt = false;
+    uint4 q_nxt[4];
+    MetaRaw m_nn{0, 0};
     if (TIER == 0) {
-      // ---- stage the header window: coalesced when every packet base is 16-byte aligned ----
-      const bool aligned16 = ((uintptr_t)base & 15) == 0;
-      if (ballot(valid && !aligned16) == 0) {
-        const uint32_t c = lane & 3;
-        uint4 q[4];
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-          const int j = r * 16 + (int)(lane >> 2);
-          const uint64_t bj = (uint64_t)__shfl((long long)(uintptr_t)base, j);
-          const uint32_t lj = (uint32_t)__shfl((int)len, j);
-          q[r] = make_uint4(0, 0, 0, 0);
-          if (c * 16 < min(lj, (uint32_t)kWin)) q[r] = gld128((uintptr_t)(bj + c * 16));
-        }
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-          const int j = r * 16 + (int)(lane >> 2);
-          const uint32_t lj = (uint32_t)__shfl((int)len, j);
-          uint32_t d[4] = {q[r].x, q[r].y, q[r].z, q[r].w};
-          uint32_t* wdst = (uint32_t*)(wave_win + (size_t)j * kWinStride + c * 16);
-#pragma unroll
-          for (int e = 0; e < 4; e++) {
-            const uint32_t off = c * 16 + e * 4;  // bytes at or past len read as zero
-            uint32_t v = d[e];
-            if (off >= lj) v = 0;
-            else if (lj - off < 4) v &= (uint32_t)wmask(lj - off);
-            wdst[e] = v;
-          }
-        }
-      } else {
-        // per-lane path for unaligned packet bases
+      // ---- stage this tile's header windows ----
+      if (co_cur) {
+        commit_window(wave_win, lane, m_cur, q_cur);
+      } else {  // per-lane path for unaligned packet bases
         uint32_t* wdst = (uint32_t*)my_win;
         const uint32_t m = valid ? min(len, (uint32_t)kWin) : 0u;
         for (uint32_t d = 0; d < kWin / 4; d++)
@@ -234,6 +290,13 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      // ---- prefetch the next tile's windows and the metadata after it ----
+      const uint64_t tn = tile + total_waves;
+      if (tn < a.n_tiles) {
+        co_nxt = tile_coalescible(a, tn, lane, m_nxt);
+        if (co_nxt) issue_window(a, tn, lane, m_nxt, q_nxt);
+      }
+      m_nn = load_meta(a, tn + total_waves, lane);
     }
 
     // ---- Emu::default() + main.rs:14-31 register/memory layout ----
@@ -545,6 +608,16 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
     cnt[5] += __builtin_popcountll(ballot(okv && r0v >= 5));
     cnt[6] += __builtin_popcountll(ballot(valid && st != EBPF_ST_OK));
     retired += valid ? nsteps : 0u;
+    if (TIER == 0) {
+      m_cur = m_nxt;
+      m_nxt = m_nn;
+      co_cur = co_nxt;
+#pragma unroll
+      for (int r = 0; r < 4; r++) q_cur[r] = q_nxt[r];
+    } else {
+      m_cur = m_nxt;
+      m_nxt = load_meta(a, tile + 2 * total_waves, lane);
+    }
   }
 
   // ---- counters: workgroup sum -> sharded device atomics -> the last workgroup folds the
@@ -620,23 +693,35 @@ static const void* kernel_for(int tier, uint32_t n_uops) {
 }
 
 int interp_grid(int tier, uint32_t n_uops, uint64_t n_tiles, int* grid_out) {
-  const uint64_t want = (n_tiles + kWavesPerBlock - 1) / kWavesPerBlock;
-  if (tier == 0) {  // one tile per wave; the dispatcher load-balances divergent tiles
-    *grid_out = (int)(want ? (want < (1u << 30) ? want : (1u << 30)) : 1);
-    return 0;
-  }
-  int dev = 0, cus = 256, per_cu = 8;
+  int dev = 0, cus = 256, per_cu = 1;
   if (hipGetDevice(&dev) != hipSuccess) return -1;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return -1;
   const uint32_t lds = lds_bytes_for(n_uops);
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel_for(tier, n_uops), kBlock,
-                                                   lds) != hipSuccess ||
-      per_cu < 1)
-    per_cu = 1;
-  if (per_cu > 4) per_cu = 4;  // bounds the tier-1 image scratch
-  const uint64_t cap = (uint64_t)cus * (uint64_t)per_cu;
-  *grid_out = (int)(want < cap ? (want ? want : 1) : cap);
+  const void* k = kernel_for(tier, n_uops);
+  {
+    static std::mutex mu;
+    static std::map<std::tuple<int, const void*, uint32_t>, int> cache;
+    std::lock_guard<std::mutex> lk(mu);
+    auto key = std::make_tuple(dev, k, lds);
+    auto it = cache.find(key);
+    if (it != cache.end()) {
+      per_cu = it->second;
+    } else {
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kBlock, lds) != hipSuccess ||
+          per_cu < 1)
+        per_cu = 1;
+      cache[key] = per_cu;
+    }
+  }
+  if (tier == 1 && per_cu > 4) per_cu = 4;  // bounds the tier-1 image scratch
+  // Persistent waves, each owning the same number of tiles (+-1): k = ceil(tiles / resident
+  // waves), then just enough waves for k tiles each.
+  const uint64_t resident = (uint64_t)cus * (uint64_t)per_cu * kWavesPerBlock;
+  const uint64_t tiles = n_tiles ? n_tiles : 1;
+  const uint64_t per_wave = (tiles + resident - 1) / resident;
+  const uint64_t waves = (tiles + per_wave - 1) / per_wave;
+  *grid_out = (int)((waves + kWavesPerBlock - 1) / kWavesPerBlock);
   return 0;
 }
 
