@@ -9,10 +9,12 @@
 //   * re-convergence by min-pc: lanes whose pc equals the wave's minimum pc execute the step;
 //     the all-lanes-agree case is one readfirstlane + one compare-ballot, the divergent case a
 //     DPP wave-min. Lanes that are done (exit, fall-off, fault) park at pc = 0xFFFFFFFF;
-//   * memory tier 0 (programs without stores/calls): the first 64 bytes of each packet are
-//     staged in a padded per-lane LDS window with coalesced 16-byte HBM loads (4 lanes per
-//     packet, 16 packets per wave instruction); reads beyond it go to HBM with dword-aligned
-//     loads, bytes past the packet read as zero, exactly as the reference's zeroed image does;
+//   * memory tier 0 (programs without stores/calls): the first 64 bytes of each packet (its
+//     "header window") are copied HBM -> LDS by LDS-DMA (global_load_lds_dwordx4: 16 packets x
+//     64 contiguous bytes per wave instruction, no VGPR destination), double-buffered so that
+//     the windows of the wave's next tile land while the current tile is interpreted; reads
+//     beyond the window go to HBM with dword-aligned loads; bytes past the packet read as
+//     zero, exactly as the reference's zeroed image does;
 //   * memory tier 1 (stores, atomics or calls present): each lane owns a lane-interleaved copy
 //     of the reference's whole memory image plus a frame stack in device scratch;
 //   * every mmu.rs bounds check is inlined; faults become per-packet status codes.
@@ -112,14 +114,57 @@ __device__ __forceinline__ uint64_t pkt_read(const uint8_t* base, uint32_t a, ui
   return v & wmask(w);
 }
 
-// Bytes [a, a+w) of the lane's LDS window (a + w <= kWin).
-__device__ __forceinline__ uint64_t win_read(const uint8_t* win, uint32_t a, uint32_t w) {
-  const uint32_t* p = (const uint32_t*)(win + (a & ~3u));
-  const uint32_t s = a & 3;
-  const uint32_t d0 = p[0], d1 = p[1];
+// Header window layout (per wave, per buffer): packet j's 64 bytes at j * 64, its 16-byte
+// chunk c stored at chunk slot c ^ swz(j), swz(j) = (j >> 2) & 3. The XOR is applied on the
+// DMA's SOURCE addresses (the LDS side of an LDS-DMA is lane-linear), and spreads the 16 packets
+// of each ds_read_b128 lane group over all 16 four-bank groups.
+__device__ __forceinline__ uint32_t win_swz(uint32_t j) { return (j >> 2) & 3; }
+
+// LDS byte offset of logical window byte b (multiple of 4) of the packet whose window starts at
+// pw (swz = win_swz of that packet).
+__device__ __forceinline__ uint32_t win_off(uint32_t b, uint32_t swz) {
+  return ((((b >> 4) ^ swz) << 4) | (b & 15)) & 63;
+}
+
+// Bytes [a, a+w) of the lane's window, a < len, a + w <= kWin; bytes at or past len are 0.
+__device__ __forceinline__ uint64_t win_read(const uint8_t* pw, uint32_t swz, uint32_t a, uint32_t w,
+                                             uint32_t len) {
+  const uint32_t b0 = a & ~3u, s = a & 3;
+  const uint32_t d0 = *(const uint32_t*)(pw + win_off(b0, swz));
+  const uint32_t d1 = *(const uint32_t*)(pw + win_off(b0 + 4, swz));  // in-window wrap if unused
   uint64_t v = __builtin_amdgcn_alignbyte(d1, d0, s);
-  if (w == 8) v |= (uint64_t)__builtin_amdgcn_alignbyte(p[2], d1, s) << 32;
+  if (w == 8) {
+    const uint32_t d2 = *(const uint32_t*)(pw + win_off(b0 + 8, swz));
+    v |= (uint64_t)__builtin_amdgcn_alignbyte(d2, d1, s) << 32;
+  }
+  const uint32_t valid = len - a;
+  if (valid < w) v &= wmask(valid);
   return v & wmask(w);
+}
+
+// ---- LDS-DMA (global_load_lds_*): lane i's `size` bytes land at lds_dst + i * size ----
+// Hand-written per MI355X guide §5.7: M0 is written in the same statement that reads it, and the
+// transfer is invisible to hipcc's s_waitcnt bookkeeping, so completion is waited for explicitly
+// (dma_wait) before the wave reads the buffer.
+__device__ __forceinline__ void dma_x4(uintptr_t gsrc, uint32_t lds_dst) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
+}
+__device__ __forceinline__ void dma_x1(uintptr_t gsrc, uint32_t lds_dst) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
+}
+__device__ __forceinline__ void dma_u16(uintptr_t gsrc, uint32_t lds_dst) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_ushort %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
+}
+__device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return rfl((uint32_t)(uintptr_t)(__attribute__((address_space(3))) const void*)p);
 }
 
 // ---- tier-1 image: lane-interleaved dwords, dword d of this lane at img[d * 64] ----
@@ -156,72 +201,64 @@ __device__ __forceinline__ void img_write(uint32_t* img, uint32_t a, uint32_t w,
 }
 
 // ---- tier-0 header-window pipeline ----
-// Per-lane packet metadata as loaded (offset word, length); the packet base is formed only
-// where it is used, so the offsets load can be issued two tiles ahead without a stall.
-struct MetaRaw {
-  uint32_t off;
-  uint32_t len;
+// Per-wave LDS region: win[2][64 packets][64 B] + meta_off[2][64] u32 + meta_len[2][64] u16.
+constexpr uint32_t kWinBytes = kWave * kWin;                       // one buffer, 4 KiB
+constexpr uint32_t kWaveLds0 = 2 * kWinBytes + 2 * kWave * 4 + 2 * kWave * 2;  // 8.75 KiB
+
+struct WaveLds {
+  uint8_t* win;        // [2][kWinBytes]
+  uint32_t* meta_off;  // [2][64]
+  uint16_t* meta_len;  // [2][64]
 };
 
-__device__ __forceinline__ MetaRaw load_meta(const LaunchArgs& a, uint64_t tile, uint32_t lane) {
-  MetaRaw m{0, 0};
-  const uint64_t pkt = tile * kWave + lane;
-  if (tile < a.n_tiles && pkt < a.n) {
-    if (a.offsets) m.off = a.offsets[pkt];
-    m.len = a.lens ? (uint32_t)a.lens[pkt]
-                   : (uint32_t)(a.stride > 0xFFFFFFFFull ? 0xFFFFFFFFull : a.stride);
-  }
-  return m;
+__device__ __forceinline__ uint32_t stride_len(const LaunchArgs& a) {
+  return (uint32_t)(a.stride > 0xFFFFFFFFull ? 0xFFFFFFFFull : a.stride);
 }
 
-__device__ __forceinline__ uintptr_t pkt_base(const LaunchArgs& a, uint64_t tile, uint32_t lane,
-                                              const MetaRaw& m) {
-  const uint64_t pkt = tile * kWave + lane;
-  return (uintptr_t)a.frames + (a.offsets ? (uint64_t)m.off : pkt * a.stride);
+// DMA the offsets / lengths of tile t into meta buffer b (lanes past the batch read a dummy).
+__device__ __forceinline__ void dma_meta(const LaunchArgs& a, const WaveLds& L, uint32_t b,
+                                         uint64_t t, uint32_t lane) {
+  const uint64_t pkt = t * kWave + lane;
+  const bool ok = t < a.n_tiles && pkt < a.n;
+  if (a.offsets)
+    dma_x1(ok ? (uintptr_t)(a.offsets + pkt) : (uintptr_t)a.prog, lds_addr(L.meta_off + b * kWave));
+  if (a.lens)
+    dma_u16(ok ? (uintptr_t)(a.lens + pkt) : (uintptr_t)a.prog, lds_addr(L.meta_len + b * kWave));
 }
 
-// Wave-uniform: every valid packet base of the tile is 16-byte aligned (coalesced staging).
-__device__ __forceinline__ bool tile_coalescible(const LaunchArgs& a, uint64_t tile, uint32_t lane,
-                                                 const MetaRaw& m) {
-  const bool valid = tile * kWave + lane < a.n;
-  return ballot(valid && (pkt_base(a, tile, lane, m) & 15) != 0) == 0;
+// Packet j of tile t, from meta buffer b: base address and length (0 for j past the batch).
+__device__ __forceinline__ void meta_of(const LaunchArgs& a, const WaveLds& L, uint32_t b,
+                                        uint64_t t, uint32_t j, uintptr_t& base, uint32_t& len) {
+  const uint64_t pkt = t * kWave + j;
+  const bool ok = pkt < a.n;
+  base = (uintptr_t)a.frames + (a.offsets ? (uint64_t)L.meta_off[b * kWave + j] : pkt * a.stride);
+  len = ok ? (a.lens ? (uint32_t)L.meta_len[b * kWave + j] : stride_len(a)) : 0u;
 }
 
-// Issue the 16-byte loads of a tile's 64 header windows: lane l loads 16 bytes (chunk l % 4) of
-// packet 16 r + l / 4 in round r, so each wave instruction reads 16 packets x 64 contiguous bytes.
-__device__ __forceinline__ void issue_window(const LaunchArgs& a, uint64_t tile, uint32_t lane,
-                                             const MetaRaw& m, uint4 q[4]) {
-  const uint32_t c = lane & 3;
-  const uintptr_t base = pkt_base(a, tile, lane, m);
+// DMA tile t's 64 header windows into window buffer b: round r moves packets 16r..16r+15, lane l
+// filling chunk slot (l & 3) of packet 16r + l/4 from logical chunk (l & 3) ^ swz. Chunks wholly
+// past the packet's end read a dummy address instead (never a byte past a valid 16-byte chunk).
+__device__ __forceinline__ void dma_window(const LaunchArgs& a, const WaveLds& L, uint32_t b,
+                                           uint64_t t, uint32_t lane) {
 #pragma unroll
   for (int r = 0; r < 4; r++) {
-    const int j = r * 16 + (int)(lane >> 2);
-    const uint64_t bj = (uint64_t)__shfl((long long)base, j);
-    const uint32_t lj = (uint32_t)__shfl((int)m.len, j);
-    q[r] = make_uint4(0, 0, 0, 0);
-    if (c * 16 < min(lj, (uint32_t)kWin)) q[r] = gld128((uintptr_t)(bj + c * 16));
+    const uint32_t j = r * 16 + (lane >> 2);
+    uintptr_t bj;
+    uint32_t lj;
+    meta_of(a, L, b, t, j, bj, lj);
+    const uint32_t c = (lane & 3) ^ win_swz(j);
+    const uintptr_t src = (c * 16 < lj) ? bj + c * 16 : (uintptr_t)a.prog;
+    dma_x4(src, lds_addr(L.win + b * kWinBytes + r * 1024));
   }
 }
 
-// Write the loaded chunks to the packets' LDS windows; bytes at or past len read as zero.
-__device__ __forceinline__ void commit_window(uint8_t* wave_win, uint32_t lane, const MetaRaw& m,
-                                              const uint4 q[4]) {
-  const uint32_t c = lane & 3;
+// Synchronous per-lane staging for tiles whose packet bases are not all 16-byte aligned.
+__device__ __forceinline__ void stage_window_lane(uint8_t* pw, uint32_t swz, const uint8_t* base,
+                                                  uint32_t len, bool valid) {
+  const uint32_t m = valid ? min(len, (uint32_t)kWin) : 0u;
 #pragma unroll
-  for (int r = 0; r < 4; r++) {
-    const int j = r * 16 + (int)(lane >> 2);
-    const uint32_t lj = (uint32_t)__shfl((int)m.len, j);
-    const uint32_t d[4] = {q[r].x, q[r].y, q[r].z, q[r].w};
-    uint32_t* wdst = (uint32_t*)(wave_win + (size_t)j * kWinStride + c * 16);
-#pragma unroll
-    for (int e = 0; e < 4; e++) {
-      const uint32_t off = c * 16 + e * 4;
-      uint32_t v = d[e];
-      if (off >= lj) v = 0;
-      else if (lj - off < 4) v &= (uint32_t)wmask(lj - off);
-      wdst[e] = v;
-    }
-  }
+  for (uint32_t bo = 0; bo < (uint32_t)kWin; bo += 4)
+    *(uint32_t*)(pw + win_off(bo, swz)) = (bo < m) ? (uint32_t)pkt_read(base, bo, 4, len) : 0u;
 }
 
 template <int TIER, bool LDSP, int NW>
@@ -230,7 +267,7 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
   const uint32_t nu = a.n_uops;
   const uint32_t prog_bytes = LDSP ? nu * (uint32_t)sizeof(Uop) : 0u;
   Uop* sprog = (Uop*)smem;
-  uint8_t* windows = smem + prog_bytes;
+  uint8_t* const wave_region = smem + prog_bytes;  // tier 0: kWaveLds0 per wave
 
   // stage the program once per workgroup (emu.instructions, emu.rs:24)
   if (LDSP) {
@@ -242,8 +279,11 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
 
   const uint32_t lane = threadIdx.x & (kWave - 1);
   const uint32_t wv = threadIdx.x / kWave;
-  uint8_t* const wave_win = windows + (size_t)wv * kWave * kWinStride;
-  uint8_t* const my_win = wave_win + (size_t)lane * kWinStride;
+  WaveLds L;
+  L.win = wave_region + (size_t)wv * kWaveLds0;
+  L.meta_off = (uint32_t*)(L.win + 2 * kWinBytes);
+  L.meta_len = (uint16_t*)(L.meta_off + 2 * kWave);
+  const uint32_t my_swz = win_swz(lane);
   const uint64_t wave_slot = (uint64_t)blockIdx.x * kWavesPerBlock + wv;
   const uint64_t total_waves = (uint64_t)gridDim.x * kWavesPerBlock;
   const uint32_t mem_size = a.mem_size;
@@ -257,46 +297,54 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
   uint64_t cnt[7] = {0, 0, 0, 0, 0, 0, 0};  // wave-uniform verdict buckets + faults
   uint64_t retired = 0;                     // per lane
 
-  // Tier 0 software pipeline: while tile t is interpreted, the header windows of tile t + W are
-  // in flight to registers and the metadata of tile t + 2W is being loaded (W = total waves).
-  MetaRaw m_cur = load_meta(a, wave_slot, lane);
-  MetaRaw m_nxt = load_meta(a, wave_slot + total_waves, lane);
-  bool co_cur = false;
-  uint4 q_cur[4];
+  // Tier 0 pipeline (W = total waves, buffers alternate per tile of this wave): at the top of
+  // tile t the windows of t (buffer b) and the metadata of t + W (buffer b ^ 1) have landed; the
+  // wave then DMAs the windows of t + W into buffer b ^ 1 and the metadata of t + 2W into buffer
+  // b, and interprets t while both are in flight.
+  uint32_t b = 0;
+  bool co_cur = false;  // tile t's windows were DMA'd (all packet bases 16-byte aligned)
   if (TIER == 0 && wave_slot < a.n_tiles) {
-    co_cur = tile_coalescible(a, wave_slot, lane, m_cur);
-    if (co_cur) issue_window(a, wave_slot, lane, m_cur, q_cur);
+    dma_meta(a, L, 0, wave_slot, lane);
+    dma_wait();
+    uintptr_t mb;
+    uint32_t ml;
+    meta_of(a, L, 0, wave_slot, lane, mb, ml);
+    co_cur = ballot(ml != 0 && (mb & 15) != 0) == 0;
+    if (co_cur) dma_window(a, L, 0, wave_slot, lane);
+    if (wave_slot + total_waves < a.n_tiles) dma_meta(a, L, 1, wave_slot + total_waves, lane);
   }
 
   for (uint64_t tile = wave_slot; tile < a.n_tiles; tile += total_waves) {
     const uint64_t pkt = tile * kWave + lane;
     const bool valid = pkt < a.n;
-    const uint32_t len = m_cur.len;
-    const uint8_t* base = valid ? (const uint8_t*)pkt_base(a, tile, lane, m_cur) : nullptr;
-
-    bool co_nxt = false;
-    uint4 q_nxt[4];
-    MetaRaw m_nn{0, 0};
+    const uint8_t* base = nullptr;
+    uint32_t len = 0;
+    uint8_t* const my_win = L.win + b * kWinBytes + lane * kWin;
     if (TIER == 0) {
-      // ---- stage this tile's header windows ----
-      if (co_cur) {
-        commit_window(wave_win, lane, m_cur, q_cur);
-      } else {  // per-lane path for unaligned packet bases
-        uint32_t* wdst = (uint32_t*)my_win;
-        const uint32_t m = valid ? min(len, (uint32_t)kWin) : 0u;
-        for (uint32_t d = 0; d < kWin / 4; d++)
-          wdst[d] = (d * 4 < m) ? (uint32_t)pkt_read(base, d * 4, 4, len) : 0u;
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      // ---- prefetch the next tile's windows and the metadata after it ----
+      dma_wait();  // windows of this tile + metadata of the next one
+      uintptr_t mb;
+      uint32_t ml;
+      meta_of(a, L, b, tile, lane, mb, ml);
+      base = (const uint8_t*)mb;
+      len = valid ? ml : 0u;
+      if (!co_cur) stage_window_lane(my_win, my_swz, base, len, valid);
+      // next tile: its metadata is in buffer b ^ 1
       const uint64_t tn = tile + total_waves;
+      bool co_nxt = false;
       if (tn < a.n_tiles) {
-        co_nxt = tile_coalescible(a, tn, lane, m_nxt);
-        if (co_nxt) issue_window(a, tn, lane, m_nxt, q_nxt);
+        uintptr_t nb;
+        uint32_t nl;
+        meta_of(a, L, b ^ 1, tn, lane, nb, nl);
+        co_nxt = ballot(nl != 0 && (nb & 15) != 0) == 0;
+        if (co_nxt) dma_window(a, L, b ^ 1, tn, lane);
       }
-      m_nn = load_meta(a, tn + total_waves, lane);
+      // the metadata reads of buffer b above have returned before the DMA may overwrite it
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (tn + total_waves < a.n_tiles) dma_meta(a, L, b, tn + total_waves, lane);
+      co_cur = co_nxt;
+    } else if (valid) {
+      base = a.frames + (a.offsets ? (uint64_t)a.offsets[pkt] : pkt * a.stride);
+      len = a.lens ? (uint32_t)a.lens[pkt] : stride_len(a);
     }
 
     // ---- Emu::default() + main.rs:14-31 register/memory layout ----
@@ -477,8 +525,9 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
           uint64_t v = 0;
           if (act && !fault) {
             if (TIER == 1) v = img_read(img, a0, aux);
-            else if (a0 + aux <= (uint32_t)kWin) v = win_read(my_win, a0, aux);
-            else if (a0 < len) v = pkt_read(base, a0, aux, len);
+            else if (a0 >= len) v = 0;
+            else if (a0 + aux <= (uint32_t)kWin) v = win_read(my_win, my_swz, a0, aux, len);
+            else v = pkt_read(base, a0, aux, len);
           }
           const uint64_t m = wmask(aux);
           R = (A & ~m) | v;  // upper bytes preserved (Q1)
@@ -587,8 +636,9 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
       for (uint32_t d = 0; d < mem_size / 4; d++) {
         uint32_t v;
         if (TIER == 1) v = img[(size_t)d * kWave];
-        else if (d * 4 < (uint32_t)kWin) v = ((const uint32_t*)my_win)[d];
-        else v = (d * 4 < m) ? (uint32_t)pkt_read(base, d * 4, 4, len) : 0u;
+        else if (d * 4 >= m) v = 0u;
+        else if (d * 4 < (uint32_t)kWin) v = (uint32_t)win_read(my_win, my_swz, d * 4, 4, len);
+        else v = (uint32_t)pkt_read(base, d * 4, 4, len);
         mo[d] = v;
       }
     }
@@ -608,17 +658,9 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
     cnt[5] += __builtin_popcountll(ballot(okv && r0v >= 5));
     cnt[6] += __builtin_popcountll(ballot(valid && st != EBPF_ST_OK));
     retired += valid ? nsteps : 0u;
-    if (TIER == 0) {
-      m_cur = m_nxt;
-      m_nxt = m_nn;
-      co_cur = co_nxt;
-#pragma unroll
-      for (int r = 0; r < 4; r++) q_cur[r] = q_nxt[r];
-    } else {
-      m_cur = m_nxt;
-      m_nxt = load_meta(a, tile + 2 * total_waves, lane);
-    }
+    b ^= 1;
   }
+  if (TIER == 0) dma_wait();  // no LDS-DMA may still target this workgroup's LDS at exit
 
   // ---- counters: workgroup sum -> sharded device atomics -> the last workgroup folds the
   //      shards into the caller's counters (one launch per batch, no finalize kernel) ----
@@ -672,11 +714,11 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
   if (threadIdx.x == 0) __hip_atomic_exchange(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-static uint32_t lds_bytes_for(uint32_t n_uops) {
+static uint32_t lds_bytes_for(int tier, uint32_t n_uops) {
   const uint32_t prog = n_uops <= (uint32_t)kMaxLdsUops ? n_uops * (uint32_t)sizeof(Uop) : 0u;
-  uint32_t win = kBlock * kWinStride;
-  if (win < kWavesPerBlock * 8 * 8) win = kWavesPerBlock * 8 * 8;
-  return prog + win;
+  uint32_t rest = tier == 0 ? kWavesPerBlock * kWaveLds0 : 0u;
+  if (rest < kWavesPerBlock * 8 * 8) rest = kWavesPerBlock * 8 * 8;  // counter reduction scratch
+  return prog + rest;
 }
 
 // Kernel variant for a program: tier (memory model), LDS-staged program, scheduler width.
@@ -697,7 +739,7 @@ int interp_grid(int tier, uint32_t n_uops, uint64_t n_tiles, int* grid_out) {
   if (hipGetDevice(&dev) != hipSuccess) return -1;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return -1;
-  const uint32_t lds = lds_bytes_for(n_uops);
+  const uint32_t lds = lds_bytes_for(tier, n_uops);
   const void* k = kernel_for(tier, n_uops);
   {
     static std::mutex mu;
@@ -726,7 +768,7 @@ int interp_grid(int tier, uint32_t n_uops, uint64_t n_tiles, int* grid_out) {
 }
 
 hipError_t launch_interp(int tier, const LaunchArgs& a, int grid, hipStream_t stream) {
-  const uint32_t lds = lds_bytes_for(a.n_uops);
+  const uint32_t lds = lds_bytes_for(tier, a.n_uops);
   void* args[] = {(void*)&a};
   return hipLaunchKernel(kernel_for(tier, a.n_uops), dim3(grid), dim3(kBlock), args, lds, stream);
 }
