@@ -328,20 +328,6 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
       base = (const uint8_t*)mb;
       len = valid ? ml : 0u;
       if (!co_cur) stage_window_lane(my_win, my_swz, base, len, valid);
-      // next tile: its metadata is in buffer b ^ 1
-      const uint64_t tn = tile + total_waves;
-      bool co_nxt = false;
-      if (tn < a.n_tiles) {
-        uintptr_t nb;
-        uint32_t nl;
-        meta_of(a, L, b ^ 1, tn, lane, nb, nl);
-        co_nxt = ballot(nl != 0 && (nb & 15) != 0) == 0;
-        if (co_nxt) dma_window(a, L, b ^ 1, tn, lane);
-      }
-      // the metadata reads of buffer b above have returned before the DMA may overwrite it
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (tn + total_waves < a.n_tiles) dma_meta(a, L, b, tn + total_waves, lane);
-      co_cur = co_nxt;
     } else if (valid) {
       base = a.frames + (a.offsets ? (uint64_t)a.offsets[pkt] : pkt * a.stride);
       len = a.lens ? (uint32_t)a.lens[pkt] : stride_len(a);
@@ -371,6 +357,28 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
       const uint32_t m = (pc != PC_DONE) ? len : 0u;
       for (uint32_t d = 0; d < md; d++)
         img[(size_t)d * kWave] = (d * 4 < m) ? (uint32_t)pkt_read(base, d * 4, 4, len) : 0u;
+    }
+
+    if (TIER == 0) {
+      // vmcnt(0) as a builtin: hipcc's wait-count pass then knows that none of ITS loads (e.g.
+      // init_regs into the register file) is pending, so it puts no wait at the interpreter's
+      // indexed register accesses -- such a wait would also drain the LDS-DMA issued next,
+      // which hipcc does not see.
+      __builtin_amdgcn_s_waitcnt(0x0F70);
+      // next tile of this wave: its metadata is in buffer b ^ 1
+      const uint64_t tn = tile + total_waves;
+      bool co_nxt = false;
+      if (tn < a.n_tiles) {
+        uintptr_t nb;
+        uint32_t nl;
+        meta_of(a, L, b ^ 1, tn, lane, nb, nl);
+        co_nxt = ballot(nl != 0 && (nb & 15) != 0) == 0;
+        if (co_nxt) dma_window(a, L, b ^ 1, tn, lane);
+      }
+      // the metadata reads of buffer b (top of this tile) returned before the DMA overwrites it
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (tn + total_waves < a.n_tiles) dma_meta(a, L, b, tn + total_waves, lane);
+      co_cur = co_nxt;
     }
 
     // ---- Emu::run (emu.rs:452-458) with min-pc re-convergence ----
