@@ -42,6 +42,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", choices=sorted(CONFIGS), default="5tuple")
     ap.add_argument("--packets", type=int, default=1 << 20, help="packets per batch per GPU")
+    ap.add_argument("--total-packets", type=int, default=0,
+                    help="strong scaling: one global batch of this many packets (BASELINE config 4"
+                         " = 100000000), sharded over the ranks in seeded 1Mi-packet chunks")
     ap.add_argument("--pool-mib", type=int, default=512, help="min bytes of distinct batches")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0=skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, affinity)")
@@ -75,12 +78,26 @@ def main():
     prog = Program(img)
     prog.upload(local)
 
-    # ---- synthetic device-resident batches (rank-distinct seeds) ----
+    # ---- synthetic device-resident batches ----
+    from ebpf_emu import dist as D
+
     mixed = args.config == "checksum"
     batches = []
     pool_bytes = 0
+    if args.total_packets:
+        # strong scaling: this rank's contiguous shard of a global batch of seeded chunks
+        assert not mixed, "--total-packets is defined for the 64-byte-frame configs"
+        sizes = D.chunk_sizes(args.total_packets, 1 << 20)
+        mine = D.shard_chunks(len(sizes), world, rank)
+        n = sum(sizes[k] for k in mine)
+        buf = np.concatenate([W.frames_fixed(sizes[k], 64, cfg_idx + 1 + 100 * k) for k in mine])
+        batches.append(dict(frames=torch.from_numpy(buf).to(dev)))
+        algo_bytes = n * (64 + 1)
+        pool_bytes = buf.nbytes
     k = 0
-    while True:
+    while not args.total_packets:
+        # weak scaling: a pool of distinct batches per rank (rank-distinct seeds), larger than
+        # the Infinity Cache so that every step streams from HBM
         cid = cfg_idx + 1 + 1000 * rank + 100 * k
         if mixed:
             buf, offs, lens = W.frames_mixed(n, config_id=cid)
@@ -97,7 +114,7 @@ def main():
         if pool_bytes >= args.pool_mib * (1 << 20) or k >= 16:
             break
     mem_size, r10 = (2048, 2048) if mixed else (1024, 512)
-    verdict = torch.empty(n, dtype=torch.uint8, device=dev)
+    verdict = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
     counters = torch.zeros(8, dtype=torch.int64, device=dev)
 
     from ebpf_emu import _lib
@@ -134,8 +151,7 @@ def main():
         starts[i].record(stream)
         step(i)
         ends[i].record(stream)
-    if world > 1:  # the one exchange step: per-verdict counters over RCCL / xGMI
-        dist.all_reduce(counters)
+    D.reduce_counters(counters)  # the one exchange step: per-verdict counters, RCCL / xGMI
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -149,7 +165,7 @@ def main():
     kern_avg_ms = sum(kern_ms) / len(kern_ms)
 
     cnt = [int(c) & ((1 << 64) - 1) for c in counters.cpu().tolist()]
-    total_pkts = n * args.steps * world
+    total_pkts = (args.total_packets or n * world) * args.steps
     if not args.no_counters:
         assert sum(cnt[:7]) == total_pkts, (cnt, total_pkts)  # every packet: exactly one verdict
     mpps = total_pkts / elapsed / 1e6
@@ -175,7 +191,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed * 1e3 / args.steps, 5),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.total_packets else "weak",
             "vs_baseline": None,
             "dtype": "int64",
             "data": "synthetic (seeded Ethernet/IPv4 frames, device-resident, pool > Infinity Cache)",
@@ -183,6 +199,7 @@ def main():
                 "workload": desc,
                 "baseline_config": cfg_idx,
                 "packets_per_step_per_gpu": n,
+                "global_batch": args.total_packets or n * world,
                 "frame_bytes": "64/1500 mixed" if mixed else 64,
                 "program_insns": len(prog),
                 "mem_size": mem_size,
