@@ -338,3 +338,13 @@ def test_emem_cli_kats(cuda):
     r = subprocess.run([emem, ""], input="71 10 00 04 00 00 00 00 95 00 00 00 00 00 00 00\n",
                        capture_output=True, text=True, timeout=120)  # ldxb r0, [r1+1024] -> panic
     assert r.returncode == 101
+
+
+def test_conformance_runner(cuda):
+    """The `.data` runner over the reference-derived vectors, through the GPU path."""
+    import os
+
+    from ebpf_emu.conformance import main
+
+    d = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "conformance")
+    assert main([d]) == 0

@@ -67,3 +67,24 @@ def test_from_str_radix_plus_sign():
     assert hexs_to_u8s("+f0a") == [0x0F, 0x0A]
     with pytest.raises(HexError):
         hexs_to_u8s("zz")
+
+
+def test_conformance_data_parser():
+    """bpf_conformance `.data` parsing (asm and raw forms) agrees with the oracle's answers."""
+    import glob
+    import os
+
+    import oracle
+
+    from ebpf_emu.conformance import parse_data
+
+    d = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "conformance")
+    files = sorted(glob.glob(os.path.join(d, "*.data")))
+    assert len(files) >= 9
+    for f in files:
+        v = parse_data(open(f).read(), os.path.basename(f))
+        st, r0, _ = oracle.Program(v.program).run_packet(v.memory, 1024, 512, 100000)
+        if v.expect_error:
+            assert st != 0, f
+        else:
+            assert st == 0 and r0 == v.result, (f, st, hex(r0))
