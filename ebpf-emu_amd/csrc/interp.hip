@@ -142,7 +142,7 @@ __device__ __forceinline__ uint64_t win_read(const uint8_t* pw, uint32_t swz, ui
   return v & wmask(w);
 }
 
-// ---- LDS-DMA (global_load_lds_*): lane i's `size` bytes land at lds_dst + i * size ----
+// ---- LDS-DMA (global_load_lds_*): lane i's data lands at lds_dst + i * max(size, 4) ----
 // Hand-written per MI355X guide §5.7: M0 is written in the same statement that reads it, and the
 // transfer is invisible to hipcc's s_waitcnt bookkeeping, so completion is waited for explicitly
 // (dma_wait) before the wave reads the buffer.
@@ -201,14 +201,16 @@ __device__ __forceinline__ void img_write(uint32_t* img, uint32_t a, uint32_t w,
 }
 
 // ---- tier-0 header-window pipeline ----
-// Per-wave LDS region: win[2][64 packets][64 B] + meta_off[2][64] u32 + meta_len[2][64] u16.
-constexpr uint32_t kWinBytes = kWave * kWin;                       // one buffer, 4 KiB
-constexpr uint32_t kWaveLds0 = 2 * kWinBytes + 2 * kWave * 4 + 2 * kWave * 2;  // 8.75 KiB
+// Per-wave LDS region: win[2][64 packets][64 B] + meta_off[2][64] u32 + meta_len[2][64] u32.
+// (A sub-dword LDS-DMA such as global_load_lds_ushort still fills one zero-extended DWORD slot
+// per lane, so the 16-bit lengths land in 4-byte slots.)
+constexpr uint32_t kWinBytes = kWave * kWin;                          // one buffer, 4 KiB
+constexpr uint32_t kWaveLds0 = 2 * kWinBytes + 2 * kWave * 4 + 2 * kWave * 4;  // 9 KiB
 
 struct WaveLds {
   uint8_t* win;        // [2][kWinBytes]
   uint32_t* meta_off;  // [2][64]
-  uint16_t* meta_len;  // [2][64]
+  uint32_t* meta_len;  // [2][64], low 16 bits
 };
 
 __device__ __forceinline__ uint32_t stride_len(const LaunchArgs& a) {
@@ -232,7 +234,7 @@ __device__ __forceinline__ void meta_of(const LaunchArgs& a, const WaveLds& L, u
   const uint64_t pkt = t * kWave + j;
   const bool ok = pkt < a.n;
   base = (uintptr_t)a.frames + (a.offsets ? (uint64_t)L.meta_off[b * kWave + j] : pkt * a.stride);
-  len = ok ? (a.lens ? (uint32_t)L.meta_len[b * kWave + j] : stride_len(a)) : 0u;
+  len = ok ? (a.lens ? (L.meta_len[b * kWave + j] & 0xffffu) : stride_len(a)) : 0u;
 }
 
 // DMA tile t's 64 header windows into window buffer b: round r moves packets 16r..16r+15, lane l
@@ -282,7 +284,7 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
   WaveLds L;
   L.win = wave_region + (size_t)wv * kWaveLds0;
   L.meta_off = (uint32_t*)(L.win + 2 * kWinBytes);
-  L.meta_len = (uint16_t*)(L.meta_off + 2 * kWave);
+  L.meta_len = L.meta_off + 2 * kWave;
   const uint32_t my_swz = win_swz(lane);
   const uint64_t wave_slot = (uint64_t)blockIdx.x * kWavesPerBlock + wv;
   const uint64_t total_waves = (uint64_t)gridDim.x * kWavesPerBlock;
