@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
 #include <map>
 #include <mutex>
 #include <tuple>
@@ -61,28 +62,34 @@ __device__ __forceinline__ uint4 gld128(uintptr_t p) {
 // Set of pcs at which some lane of the wave is parked, for programs of up to 64 * NW micro-ops:
 // the next pc to run is its lowest member (s_ff1), replacing a per-step wave-wide min.
 template <int NW>
-struct PcSet {
-  uint64_t w[NW > 0 ? NW : 1];
+struct PcSet {  // NW in {0 (unused), 1, 4}; words are named scalars (SGPRs), never an array
+  uint64_t w0, w1, w2, w3;
   __device__ __forceinline__ void init(bool any) {
-#pragma unroll
-    for (int i = 0; i < (NW > 0 ? NW : 1); i++) w[i] = 0;
-    if (any) w[0] = 1;  // every lane starts at pc 0
+    w0 = any ? 1ull : 0ull;  // every lane starts at pc 0
+    w1 = w2 = w3 = 0;
   }
   __device__ __forceinline__ uint32_t first() const {
-#pragma unroll
-    for (int i = 0; i < NW; i++)
-      if (w[i]) return (uint32_t)(i * 64 + __builtin_ctzll(w[i]));
+    if (w0) return (uint32_t)__builtin_ctzll(w0);
+    if (NW > 1) {
+      if (w1) return 64u + (uint32_t)__builtin_ctzll(w1);
+      if (w2) return 128u + (uint32_t)__builtin_ctzll(w2);
+      if (w3) return 192u + (uint32_t)__builtin_ctzll(w3);
+    }
     return PC_DONE;
   }
   __device__ __forceinline__ void add(uint32_t p) {
-#pragma unroll
-    for (int i = 0; i < NW; i++)
-      if ((p >> 6) == (uint32_t)i) w[i] |= 1ull << (p & 63);
+    const uint64_t bit = 1ull << (p & 63);
+    if (NW == 1 || p < 64) w0 |= bit;
+    else if (p < 128) w1 |= bit;
+    else if (p < 192) w2 |= bit;
+    else w3 |= bit;
   }
   __device__ __forceinline__ void del(uint32_t p) {
-#pragma unroll
-    for (int i = 0; i < NW; i++)
-      if ((p >> 6) == (uint32_t)i) w[i] &= ~(1ull << (p & 63));
+    const uint64_t bit = ~(1ull << (p & 63));
+    if (NW == 1 || p < 64) w0 &= bit;
+    else if (p < 128) w1 &= bit;
+    else if (p < 192) w2 &= bit;
+    else w3 &= bit;
   }
 };
 
@@ -205,7 +212,11 @@ __device__ __forceinline__ void img_write(uint32_t* img, uint32_t a, uint32_t w,
 // (A sub-dword LDS-DMA such as global_load_lds_ushort still fills one zero-extended DWORD slot
 // per lane, so the 16-bit lengths land in 4-byte slots.)
 constexpr uint32_t kWinBytes = kWave * kWin;                          // one buffer, 4 KiB
-constexpr uint32_t kWaveLds0 = 2 * kWinBytes + 2 * kWave * 4 + 2 * kWave * 4;  // 9 KiB
+constexpr uint32_t kMetaBytes = 2 * kWave * 4 + 2 * kWave * 4;             // 1 KiB
+// per-wave LDS bytes: double-buffered windows (DB) or one window buffer
+__host__ __device__ constexpr uint32_t wave_lds0(bool db) {
+  return (db ? 2 : 1) * kWinBytes + kMetaBytes;
+}
 
 struct WaveLds {
   uint8_t* win;        // [2][kWinBytes]
@@ -237,20 +248,21 @@ __device__ __forceinline__ void meta_of(const LaunchArgs& a, const WaveLds& L, u
   len = ok ? (a.lens ? (L.meta_len[b * kWave + j] & 0xffffu) : stride_len(a)) : 0u;
 }
 
-// DMA tile t's 64 header windows into window buffer b: round r moves packets 16r..16r+15, lane l
-// filling chunk slot (l & 3) of packet 16r + l/4 from logical chunk (l & 3) ^ swz. Chunks wholly
-// past the packet's end read a dummy address instead (never a byte past a valid 16-byte chunk).
-__device__ __forceinline__ void dma_window(const LaunchArgs& a, const WaveLds& L, uint32_t b,
-                                           uint64_t t, uint32_t lane) {
+// DMA tile t's 64 header windows (metadata in buffer mb) into window buffer wb: round r moves
+// packets 16r..16r+15, lane l filling chunk slot (l & 3) of packet 16r + l/4 from logical chunk
+// (l & 3) ^ swz. Chunks wholly past the packet's end read a dummy address instead (never a byte
+// past a valid 16-byte chunk).
+__device__ __forceinline__ void dma_window(const LaunchArgs& a, const WaveLds& L, uint32_t mb,
+                                           uint32_t wb, uint64_t t, uint32_t lane) {
 #pragma unroll
   for (int r = 0; r < 4; r++) {
     const uint32_t j = r * 16 + (lane >> 2);
     uintptr_t bj;
     uint32_t lj;
-    meta_of(a, L, b, t, j, bj, lj);
+    meta_of(a, L, mb, t, j, bj, lj);
     const uint32_t c = (lane & 3) ^ win_swz(j);
     const uintptr_t src = (c * 16 < lj) ? bj + c * 16 : (uintptr_t)a.prog;
-    dma_x4(src, lds_addr(L.win + b * kWinBytes + r * 1024));
+    dma_x4(src, lds_addr(L.win + wb * kWinBytes + r * 1024));
   }
 }
 
@@ -263,13 +275,24 @@ __device__ __forceinline__ void stage_window_lane(uint8_t* pw, uint32_t swz, con
     *(uint32_t*)(pw + win_off(bo, swz)) = (bo < m) ? (uint32_t)pkt_read(base, bo, 4, len) : 0u;
 }
 
-template <int TIER, bool LDSP, int NW>
+// The eBPF register file r0..r10 (emu.rs:15), as two 11-entry u32 arrays (low and high words):
+// each maps to an 11-VGPR tuple indexed with s_set_gpr_idx by the scalar register number, where a
+// uint64_t[11] would occupy a 32-VGPR tuple (10 registers wasted).
+#define RF_GET(i) ((uint64_t)rlo[i] | ((uint64_t)rhi[i] << 32))
+#define RF_SET(i, v)                     \
+  do {                                   \
+    const uint64_t v_ = (v);             \
+    rlo[i] = (uint32_t)v_;               \
+    rhi[i] = (uint32_t)(v_ >> 32);       \
+  } while (0)
+
+template <int TIER, bool LDSP, int NW, bool DB>
 __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t nu = a.n_uops;
   const uint32_t prog_bytes = LDSP ? nu * (uint32_t)sizeof(Uop) : 0u;
   Uop* sprog = (Uop*)smem;
-  uint8_t* const wave_region = smem + prog_bytes;  // tier 0: kWaveLds0 per wave
+  uint8_t* const wave_region = smem + prog_bytes;  // tier 0: wave_lds0(DB) per wave
 
   // stage the program once per workgroup (emu.instructions, emu.rs:24)
   if (LDSP) {
@@ -282,8 +305,8 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
   const uint32_t lane = threadIdx.x & (kWave - 1);
   const uint32_t wv = threadIdx.x / kWave;
   WaveLds L;
-  L.win = wave_region + (size_t)wv * kWaveLds0;
-  L.meta_off = (uint32_t*)(L.win + 2 * kWinBytes);
+  L.win = wave_region + (size_t)wv * wave_lds0(DB);
+  L.meta_off = (uint32_t*)(L.win + (DB ? 2 : 1) * kWinBytes);
   L.meta_len = L.meta_off + 2 * kWave;
   const uint32_t my_swz = win_swz(lane);
   const uint64_t wave_slot = (uint64_t)blockIdx.x * kWavesPerBlock + wv;
@@ -299,21 +322,25 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
   uint64_t cnt[7] = {0, 0, 0, 0, 0, 0, 0};  // wave-uniform verdict buckets + faults
   uint64_t retired = 0;                     // per lane
 
-  // Tier 0 pipeline (W = total waves, buffers alternate per tile of this wave): at the top of
-  // tile t the windows of t (buffer b) and the metadata of t + W (buffer b ^ 1) have landed; the
-  // wave then DMAs the windows of t + W into buffer b ^ 1 and the metadata of t + 2W into buffer
-  // b, and interprets t while both are in flight.
+  // Tier 0 pipeline (W = total waves; buffers alternate per tile of this wave).
+  //  DB (double-buffered windows): at the top of tile t the windows of t (buffer b) and the
+  //  metadata of t + W (buffer b ^ 1) have landed; the wave DMAs the windows of t + W into buffer
+  //  b ^ 1 and the metadata of t + 2W into buffer b, and interprets t while both are in flight.
+  //  !DB (one window buffer, half the LDS, more resident waves): the windows of t are DMA'd and
+  //  waited for at the top of t; only the metadata of t + W is in flight during t.
   uint32_t b = 0;
   bool co_cur = false;  // tile t's windows were DMA'd (all packet bases 16-byte aligned)
   if (TIER == 0 && wave_slot < a.n_tiles) {
     dma_meta(a, L, 0, wave_slot, lane);
     dma_wait();
-    uintptr_t mb;
-    uint32_t ml;
-    meta_of(a, L, 0, wave_slot, lane, mb, ml);
-    co_cur = ballot(ml != 0 && (mb & 15) != 0) == 0;
-    if (co_cur) dma_window(a, L, 0, wave_slot, lane);
-    if (wave_slot + total_waves < a.n_tiles) dma_meta(a, L, 1, wave_slot + total_waves, lane);
+    if (DB) {
+      uintptr_t mb;
+      uint32_t ml;
+      meta_of(a, L, 0, wave_slot, lane, mb, ml);
+      co_cur = ballot(ml != 0 && (mb & 15) != 0) == 0;
+      if (co_cur) dma_window(a, L, 0, 0, wave_slot, lane);
+      if (wave_slot + total_waves < a.n_tiles) dma_meta(a, L, 1, wave_slot + total_waves, lane);
+    }
   }
 
   for (uint64_t tile = wave_slot; tile < a.n_tiles; tile += total_waves) {
@@ -321,14 +348,21 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
     const bool valid = pkt < a.n;
     const uint8_t* base = nullptr;
     uint32_t len = 0;
-    uint8_t* const my_win = L.win + b * kWinBytes + lane * kWin;
+    uint8_t* const my_win = L.win + (DB ? b : 0u) * kWinBytes + lane * kWin;
     if (TIER == 0) {
-      dma_wait();  // windows of this tile + metadata of the next one
+      dma_wait();  // DB: windows of this tile + metadata of the next; !DB: this tile's metadata
       uintptr_t mb;
       uint32_t ml;
       meta_of(a, L, b, tile, lane, mb, ml);
       base = (const uint8_t*)mb;
       len = valid ? ml : 0u;
+      if (!DB) {
+        co_cur = ballot(valid && ml != 0 && (mb & 15) != 0) == 0;
+        if (co_cur) {
+          dma_window(a, L, b, 0, tile, lane);
+          dma_wait();
+        }
+      }
       if (!co_cur) stage_window_lane(my_win, my_swz, base, len, valid);
     } else if (valid) {
       base = a.frames + (a.offsets ? (uint64_t)a.offsets[pkt] : pkt * a.stride);
@@ -336,15 +370,15 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
     }
 
     // ---- Emu::default() + main.rs:14-31 register/memory layout ----
-    uint64_t r[11];
+    uint32_t rlo[11], rhi[11];
     if (a.init_regs) {  // caller-set Emu.state.regs (emu.rs:14-17)
 #pragma unroll
-      for (int i = 0; i < 11; i++) r[i] = a.init_regs[i];
+      for (int i = 0; i < 11; i++) RF_SET(i, a.init_regs[i]);
     } else {            // main.rs:28-31
 #pragma unroll
-      for (int i = 0; i < 11; i++) r[i] = 0;
-      r[2] = len;
-      r[10] = a.r10;
+      for (int i = 0; i < 11; i++) RF_SET(i, 0);
+      RF_SET(2, len);
+      RF_SET(10, a.r10);
     }
     uint32_t pc = valid ? 0u : PC_DONE;
     uint32_t st = EBPF_ST_OK;
@@ -367,20 +401,24 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
       // indexed register accesses -- such a wait would also drain the LDS-DMA issued next,
       // which hipcc does not see.
       __builtin_amdgcn_s_waitcnt(0x0F70);
-      // next tile of this wave: its metadata is in buffer b ^ 1
       const uint64_t tn = tile + total_waves;
-      bool co_nxt = false;
-      if (tn < a.n_tiles) {
-        uintptr_t nb;
-        uint32_t nl;
-        meta_of(a, L, b ^ 1, tn, lane, nb, nl);
-        co_nxt = ballot(nl != 0 && (nb & 15) != 0) == 0;
-        if (co_nxt) dma_window(a, L, b ^ 1, tn, lane);
+      if (DB) {
+        // next tile of this wave: its metadata is in buffer b ^ 1
+        bool co_nxt = false;
+        if (tn < a.n_tiles) {
+          uintptr_t nb;
+          uint32_t nl;
+          meta_of(a, L, b ^ 1, tn, lane, nb, nl);
+          co_nxt = ballot(nl != 0 && (nb & 15) != 0) == 0;
+          if (co_nxt) dma_window(a, L, b ^ 1, b ^ 1, tn, lane);
+        }
+        // the metadata reads of buffer b (top of this tile) returned before the DMA overwrites it
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (tn + total_waves < a.n_tiles) dma_meta(a, L, b, tn + total_waves, lane);
+        co_cur = co_nxt;
+      } else if (tn < a.n_tiles) {
+        dma_meta(a, L, b ^ 1, tn, lane);  // lands while this tile is interpreted
       }
-      // the metadata reads of buffer b (top of this tile) returned before the DMA overwrites it
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (tn + total_waves < a.n_tiles) dma_meta(a, L, b, tn + total_waves, lane);
-      co_cur = co_nxt;
     }
 
     // ---- Emu::run (emu.rs:452-458) with min-pc re-convergence ----
@@ -425,8 +463,8 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
       const uint64_t k = (uint64_t)w2 | ((uint64_t)w3 << 32);
 
       const bool act = pc == pcs;
-      const uint64_t A = r[dst];
-      const uint64_t S = r[src];
+      const uint64_t A = RF_GET(dst);
+      const uint64_t S = RF_GET(src);
       const uint64_t B = (aux & F_SRC) ? S : k;
       const uint32_t a32 = (uint32_t)A, b32 = (uint32_t)B;
       uint64_t R = A;             // dst value to commit
@@ -572,7 +610,7 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
             const bool fetch = aux & F_FETCH;
             const bool is32 = aux & F_ATOMIC32;
             uint64_t bak = fetch ? orig : 0;
-            uint64_t high = 0, sv = S, r0v = r[0];
+            uint64_t high = 0, sv = S, r0v = RF_GET(0);
             if (is32) {
               sv = (uint32_t)sv;
               high = orig >> 32;
@@ -614,10 +652,10 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
       // ---- commit (active lanes only) ----
       const bool ok = act && !fault;
       if (TIER == 1) {
-        if (w_r0) r[0] = ok ? side : r[0];      // cmpxchg: regs[0] = old (emu.rs:418)
-        if (w_src) r[src] = ok ? side : r[src];  // fetch: regs[src] = old (emu.rs:435)
+        if (w_r0) RF_SET(0, ok ? side : RF_GET(0));        // cmpxchg: regs[0] = old (emu.rs:418)
+        if (w_src) RF_SET(src, ok ? side : RF_GET(src));  // fetch: regs[src] = old (emu.rs:435)
       }
-      r[dst] = ok ? R : A;  // dst snapshot write-back for ST/STX/ATOMIC (Q14, emu.rs:443)
+      RF_SET(dst, ok ? R : A);  // dst snapshot write-back for ST/STX/ATOMIC (Q14, emu.rs:443)
       nsteps += ok ? 1u : 0u;
       st = (act && fault) ? fst : st;
       pc = act ? (fault || npc >= nu ? PC_DONE : npc) : pc;
@@ -639,7 +677,7 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
     }
 
     // ---- outputs: r0 (main.rs:43), status, verdict (xdp.rs:3-9), final image ----
-    const uint64_t r0v = r[0];
+    const uint64_t r0v = RF_GET(0);
     if (a.mem_out && valid) {
       uint32_t* mo = (uint32_t*)(a.mem_out + pkt * (uint64_t)mem_size);
       const uint32_t m = min(len, mem_size);
@@ -654,7 +692,7 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
     }
     if (a.regs_out && valid) {
 #pragma unroll
-      for (int i = 0; i < 11; i++) a.regs_out[pkt * 11 + i] = r[i];
+      for (int i = 0; i < 11; i++) a.regs_out[pkt * 11 + i] = RF_GET(i);
     }
     if (valid) {
       if (a.r0) a.r0[pkt] = r0v;
@@ -724,24 +762,30 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
   if (threadIdx.x == 0) __hip_atomic_exchange(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+static bool g_db = [] {  // tier-0 window double-buffering (EBPFEMU_TIER0_DB=0|1 for A/B runs)
+  const char* e = getenv("EBPFEMU_TIER0_DB");
+  return e ? e[0] == '1' : false;
+}();
+
 static uint32_t lds_bytes_for(int tier, uint32_t n_uops) {
   const uint32_t prog = n_uops <= (uint32_t)kMaxLdsUops ? n_uops * (uint32_t)sizeof(Uop) : 0u;
-  uint32_t rest = tier == 0 ? kWavesPerBlock * kWaveLds0 : 0u;
+  uint32_t rest = tier == 0 ? kWavesPerBlock * wave_lds0(g_db) : 0u;
   if (rest < kWavesPerBlock * 8 * 8) rest = kWavesPerBlock * 8 * 8;  // counter reduction scratch
   return prog + rest;
 }
 
 // Kernel variant for a program: tier (memory model), LDS-staged program, scheduler width.
-template <int TIER>
+template <int TIER, bool DB>
 static const void* variant(uint32_t n_uops) {
-  if (n_uops <= 64) return (const void*)interp_kernel<TIER, true, 1>;
-  if (n_uops <= 256) return (const void*)interp_kernel<TIER, true, 4>;
-  if (n_uops <= (uint32_t)kMaxLdsUops) return (const void*)interp_kernel<TIER, true, 0>;
-  return (const void*)interp_kernel<TIER, false, 0>;
+  if (n_uops <= 64) return (const void*)interp_kernel<TIER, true, 1, DB>;
+  if (n_uops <= 256) return (const void*)interp_kernel<TIER, true, 4, DB>;
+  if (n_uops <= (uint32_t)kMaxLdsUops) return (const void*)interp_kernel<TIER, true, 0, DB>;
+  return (const void*)interp_kernel<TIER, false, 0, DB>;
 }
 
 static const void* kernel_for(int tier, uint32_t n_uops) {
-  return tier == 1 ? variant<1>(n_uops) : variant<0>(n_uops);
+  if (tier == 1) return variant<1, false>(n_uops);
+  return g_db ? variant<0, true>(n_uops) : variant<0, false>(n_uops);
 }
 
 int interp_grid(int tier, uint32_t n_uops, uint64_t n_tiles, int* grid_out) {
