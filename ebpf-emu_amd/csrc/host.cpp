@@ -214,6 +214,7 @@ struct ebpf_prog {
   std::vector<RefInsn> insns;
   std::vector<Uop> uops;
   int tier = 0;
+  bool tiny = false;  // straight-line and <= kTinyUops: persistent grid (see interp_grid)
   std::mutex mu;
   Uop* dev_uops[kMaxDevices] = {};
 };
@@ -244,6 +245,11 @@ int ebpf_prog_load(const uint8_t* code, size_t nbytes, ebpf_prog** out, size_t* 
     if (u.op == U_FAULT) { u.dst = 0; u.src = 0; }  // the kernel never indexes a bad register
     if (u.op == U_ST || u.op == U_STX || u.op == U_ATOMIC || u.op == U_CALL) p->tier = 1;
     p->uops.push_back(u);
+  }
+  p->tiny = p->uops.size() <= kTinyUops;
+  for (size_t i = 0; i < p->uops.size(); i++) {
+    const Uop& u = p->uops[i];
+    if (u.op >= U_JA && u.op <= U_CALL && (uint32_t)u.x <= (uint32_t)i) p->tiny = false;
   }
   *out = p;
   return EBPF_OK;
@@ -316,7 +322,7 @@ uint64_t ebpf_workspace_bytes(const ebpf_prog* p, const ebpf_batch* b, int devic
     int cur = device_of_current();
     hipSetDevice(device);
     int grid = 0;
-    interp_grid(p->tier, (uint32_t)p->uops.size(), (b->n + 63) / 64, &grid);
+    interp_grid(p->tier, (uint32_t)p->uops.size(), p->tiny, (b->n + 63) / 64, &grid);
     hipSetDevice(cur);
     bytes += (uint64_t)grid * kWavesPerBlock * tier1_slot_bytes(b->mem_size);
   }
@@ -353,7 +359,7 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* b, const ebpf_batch_out* out,
 
   const uint64_t n_tiles = (b->n + 63) / 64;
   int grid = 0;
-  if (interp_grid(p->tier, (uint32_t)p->uops.size(), n_tiles, &grid) != 0) {
+  if (interp_grid(p->tier, (uint32_t)p->uops.size(), p->tiny, n_tiles, &grid) != 0) {
     if (cur != device) hipSetDevice(cur);
     return EBPF_EHIP;
   }
@@ -378,7 +384,7 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* b, const ebpf_batch_out* out,
         if (cur != device) hipSetDevice(cur);
         return EBPF_ENOMEM;
       }
-      if (hipMemset(w.ptr, 0, kWsSlotsOff) != hipSuccess) {  // ticket + shards start at zero
+      if (hipMemset(w.ptr, 0, kWsSlotsOff) != hipSuccess) {  // counter shards start at zero
         if (cur != device) hipSetDevice(cur);
         return EBPF_EHIP;
       }
@@ -401,7 +407,6 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* b, const ebpf_batch_out* out,
   a.r0 = out->r0;
   a.status = out->status;
   a.counters = out->counters;
-  a.ticket = (uint32_t*)ws;
   a.shards = (uint64_t*)(ws + kWsShardsOff);
   a.image_ws = ws + kWsSlotsOff;
   a.n_tiles = n_tiles;

@@ -710,9 +710,11 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
   }
   if (TIER == 0) dma_wait();  // no LDS-DMA may still target this workgroup's LDS at exit
 
-  // ---- counters: workgroup sum -> sharded device atomics -> the last workgroup folds the
-  //      shards into the caller's counters (one launch per batch, no finalize kernel) ----
+  // ---- counters: workgroup sum -> non-returning sharded device atomics. Nothing waits on
+  //      them: the workgroup retires at once and fold_counters (next on the stream) folds the
+  //      shards into the caller's counters. ----
   for (int off = 32; off >= 1; off >>= 1) retired += (uint64_t)__shfl_xor((long long)retired, off);
+  if (a.counters == nullptr) return;
   __syncthreads();  // all waves are done with their windows: reuse LDS
   uint64_t* red = (uint64_t*)smem;
   if (lane == 0) {
@@ -721,45 +723,30 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
     red[wv * 8 + 7] = retired;
   }
   __syncthreads();
-  if (a.counters == nullptr) return;
-  __shared__ uint32_t last_flag;
-  if (threadIdx.x < kWave) {  // wave 0
-    // Shard adds are RETURNING device-scope atomics; waiting for their return values
-    // (vmcnt(0)) means they are performed at the coherence point before this workgroup's
-    // ticket add is issued ("8-byte agent atomics on both sides", MI355X_MICROARCH.md): no
-    // cache write-back fence is needed because no plain stores are handed off.
-    uint64_t old = 0;
-    if (threadIdx.x < 8) {
-      uint64_t s = 0;
+  if (threadIdx.x < 8) {
+    uint64_t s = 0;
 #pragma unroll
-      for (int w = 0; w < kWavesPerBlock; w++) s += red[w * 8 + threadIdx.x];
-      old = __hip_atomic_fetch_add(&a.shards[(blockIdx.x % kCounterShards) * 8 + threadIdx.x], s,
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::"v"(old) : "memory");
-    if (threadIdx.x == 0) {
-      const uint32_t t = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT);
-      last_flag = (t == gridDim.x - 1);
-    }
+    for (int w = 0; w < kWavesPerBlock; w++) s += red[w * 8 + threadIdx.x];
+    // blockIdx -> XCD is round-robin, so shard (blockIdx % 64) is only ever hit from one XCD
+    if (s) __hip_atomic_fetch_add(&a.shards[(blockIdx.x % kCounterShards) * 8 + threadIdx.x], s,
+                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  __syncthreads();
-  if (!last_flag) return;
-  // last workgroup: read-and-clear every shard with device-scope atomics (coherent across XCDs)
-  uint64_t* fold = (uint64_t*)smem;
-  if (threadIdx.x < kCounterShards * 8 / 2) {
-    uint64_t v = 0;
-    for (int i = threadIdx.x; i < kCounterShards * 8; i += kCounterShards * 8 / 2)
-      v += __hip_atomic_exchange(&a.shards[i], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    fold[threadIdx.x] = v;  // entry i holds counter i % 8
-  }
+}
+
+// One workgroup: read-and-clear every shard (device-scope atomics, coherent across XCDs) and
+// add the per-counter sums into the caller's counters. Stream order after interp_kernel makes
+// every shard add visible here; the shards are left zeroed for the next batch.
+__global__ __launch_bounds__(kCounterShards * 8) void fold_counters(uint64_t* shards,
+                                                                     uint64_t* counters) {
+  __shared__ uint64_t fold[kCounterShards * 8];
+  fold[threadIdx.x] =
+      __hip_atomic_exchange(&shards[threadIdx.x], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   if (threadIdx.x < 8) {
     uint64_t t = 0;
-    for (int i = threadIdx.x; i < kCounterShards * 8 / 2; i += 8) t += fold[i];
-    if (t) atomicAdd((unsigned long long*)&a.counters[threadIdx.x], (unsigned long long)t);
+    for (int i = threadIdx.x; i < kCounterShards * 8; i += 8) t += fold[i];
+    if (t) atomicAdd((unsigned long long*)&counters[threadIdx.x], (unsigned long long)t);
   }
-  if (threadIdx.x == 0) __hip_atomic_exchange(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 static bool g_db = [] {  // tier-0 window double-buffering (EBPFEMU_TIER0_DB=0|1 for A/B runs)
@@ -788,7 +775,14 @@ static const void* kernel_for(int tier, uint32_t n_uops) {
   return g_db ? variant<0, true>(n_uops) : variant<0, false>(n_uops);
 }
 
-int interp_grid(int tier, uint32_t n_uops, uint64_t n_tiles, int* grid_out) {
+// Grid policy override for A/B runs: EBPFEMU_GRID=balanced|full|tiles (default: per program).
+static int g_grid = [] {
+  const char* e = getenv("EBPFEMU_GRID");
+  if (!e) return -1;
+  return e[0] == 'f' ? 1 : e[0] == 't' ? 2 : 0;
+}();
+
+int interp_grid(int tier, uint32_t n_uops, bool tiny, uint64_t n_tiles, int* grid_out) {
   int dev = 0, cus = 256, per_cu = 1;
   if (hipGetDevice(&dev) != hipSuccess) return -1;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
@@ -811,12 +805,20 @@ int interp_grid(int tier, uint32_t n_uops, uint64_t n_tiles, int* grid_out) {
     }
   }
   if (tier == 1 && per_cu > 4) per_cu = 4;  // bounds the tier-1 image scratch
-  // Persistent waves, each owning the same number of tiles (+-1): k = ceil(tiles / resident
-  // waves), then just enough waves for k tiles each.
   const uint64_t resident = (uint64_t)cus * (uint64_t)per_cu * kWavesPerBlock;
   const uint64_t tiles = n_tiles ? n_tiles : 1;
-  const uint64_t per_wave = (tiles + resident - 1) / resident;
-  const uint64_t waves = (tiles + per_wave - 1) / per_wave;
+  uint64_t waves;
+  const int policy = g_grid >= 0 ? g_grid : tier == 1 ? 0 : tiny ? 1 : 2;
+  if (policy == 1) {
+    waves = tiles < resident ? tiles : resident;  // every resident slot, grid-stride
+  } else if (policy == 2 && tier == 0) {
+    waves = tiles;  // one tile per wave, hardware dispatch
+  } else {
+    // Persistent waves, each owning the same number of tiles (+-1): k = ceil(tiles / resident
+    // waves), then just enough waves for k tiles each.
+    const uint64_t per_wave = (tiles + resident - 1) / resident;
+    waves = (tiles + per_wave - 1) / per_wave;
+  }
   *grid_out = (int)((waves + kWavesPerBlock - 1) / kWavesPerBlock);
   return 0;
 }
@@ -824,7 +826,14 @@ int interp_grid(int tier, uint32_t n_uops, uint64_t n_tiles, int* grid_out) {
 hipError_t launch_interp(int tier, const LaunchArgs& a, int grid, hipStream_t stream) {
   const uint32_t lds = lds_bytes_for(tier, a.n_uops);
   void* args[] = {(void*)&a};
-  return hipLaunchKernel(kernel_for(tier, a.n_uops), dim3(grid), dim3(kBlock), args, lds, stream);
+  hipError_t e =
+      hipLaunchKernel(kernel_for(tier, a.n_uops), dim3(grid), dim3(kBlock), args, lds, stream);
+  if (e != hipSuccess || a.counters == nullptr) return e;
+  uint64_t* shards = a.shards;
+  uint64_t* counters = a.counters;
+  void* fargs[] = {(void*)&shards, (void*)&counters};
+  return hipLaunchKernel((const void*)fold_counters, dim3(1), dim3(kCounterShards * 8), fargs, 0,
+                         stream);
 }
 
 }  // namespace ebpfemu

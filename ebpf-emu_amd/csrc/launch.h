@@ -15,7 +15,7 @@ constexpr int kWinStride = kWin + 4;  // padded per-lane LDS stride: 17 dwords, 
 constexpr int kMaxLdsUops = 4096;     // programs up to this many micro-ops are staged in LDS
 constexpr int kCallDepth = 64;        // EBPF_MAX_CALL_DEPTH
 constexpr int kCounterShards = 64;    // device-atomic counter shards (spread contention)
-// workspace layout: [ticket u32 | pad to 256][shards u64[64][8]][tier-1 wave slots]
+// workspace layout: [reserved 256 B][shards u64[64][8]][tier-1 wave slots]
 constexpr uint64_t kWsShardsOff = 256;
 constexpr uint64_t kWsSlotsOff = 256 + kCounterShards * 8 * 8;
 
@@ -34,7 +34,6 @@ struct LaunchArgs {
   uint64_t* r0;
   uint8_t* status;
   uint64_t* counters;   // optional caller counters [8] (added to)
-  uint32_t* ticket;     // workspace: workgroups finished (reset by the last one)
   uint64_t* shards;     // workspace: [kCounterShards][8] partial counters (left zeroed)
   uint8_t* image_ws;    // tier 1: per-wave-slot images + call stacks
   uint64_t n_tiles;     // ceil(n / 64)
@@ -48,10 +47,16 @@ __host__ __device__ inline uint64_t tier1_slot_bytes(uint32_t mem_size) {
   return (uint64_t)(mem_size / 4 + kCallDepth) * kWave * 4;
 }
 
-// Persistent grid size for a tier / LDS footprint on the current device.
-int interp_grid(int tier, uint32_t n_uops, uint64_t n_tiles, int* grid_out);
+// Programs this short with no back edge do a fixed, tiny amount of work per tile.
+constexpr uint32_t kTinyUops = 8;
 
-// Enqueue the interpreter (one kernel; counters folded in by its last workgroup).
+// Grid size on the current device. Tier 0: one tile (64 packets) per wave, so the hardware
+// dispatcher balances divergent tiles, except `tiny` programs, which get every resident wave
+// slot once (grid-stride) so per-workgroup fixed costs are paid once per slot. Tier 1:
+// balanced persistent waves (bounds the per-wave image scratch).
+int interp_grid(int tier, uint32_t n_uops, bool tiny, uint64_t n_tiles, int* grid_out);
+
+// Enqueue the interpreter, then (when counters are requested) fold_counters on the same stream.
 hipError_t launch_interp(int tier, const LaunchArgs& a, int grid, hipStream_t stream);
 
 }  // namespace ebpfemu

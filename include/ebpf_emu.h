@@ -84,8 +84,9 @@ typedef struct ebpf_batch {
   uint64_t r10;             /* initial r10 (stack top) */
   uint64_t max_steps;       /* per-packet step budget, 1..; faults EBPF_ST_STEPS beyond */
   void* workspace;          /* optional device scratch of ebpf_workspace_bytes() bytes, ZEROED before its
-                               first use and then reused as is (the kernel leaves its counter
-                               shards and ticket at zero); NULL => library-owned per (device, stream) */
+                               first use and then reused as is (each batch leaves its counter
+                               shards at zero); one workspace per stream; NULL => library-owned
+                               per (device, stream) */
   uint64_t workspace_bytes;
   const uint64_t* init_regs; /* optional device u64[11]: initial r0..r10 for every packet, replacing
                                 the main.rs layout (Emu.state.regs set by the caller, emu.rs:14-17) */
@@ -127,7 +128,7 @@ int ebpf_prog_insn(const ebpf_prog* prog, size_t i, int32_t* imm, int64_t* imm64
  * no calls), 1 = general per-packet image in device workspace. */
 int ebpf_prog_tier(const ebpf_prog* prog);
 
-/* Device scratch a batch needs (counter shards + ticket; tier 1 adds per-wave memory images). */
+/* Device scratch a batch needs (counter shards; tier 1 adds per-wave memory images). */
 uint64_t ebpf_workspace_bytes(const ebpf_prog* prog, const ebpf_batch* batch, int device);
 
 /* Copy the device micro-op table to `device` now (otherwise done on first run there).
@@ -136,7 +137,8 @@ int ebpf_prog_upload(ebpf_prog* prog, int device);
 
 /* Run a batch on the device owning `stream` (NULL = the current device's null stream).
  * Replaces, per packet, Emu::default() + Mmu setup + Emu::run() + reading state.regs[0]
- * (main.rs:14-43, emu.rs:30-45,452-458). Asynchronous, stream-ordered. */
+ * (main.rs:14-43, emu.rs:30-45,452-458). Asynchronous, stream-ordered: one interpreter
+ * kernel, plus a one-workgroup counter fold kernel when out->counters is set. */
 int ebpf_run_batch(ebpf_prog* prog, const ebpf_batch* batch, const ebpf_batch_out* out,
                    ebpf_stream_t stream);
 
