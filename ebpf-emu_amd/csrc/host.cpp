@@ -7,6 +7,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdint>
 #include <cstring>
 #include <map>
@@ -215,9 +216,48 @@ struct ebpf_prog {
   std::vector<Uop> uops;
   int tier = 0;
   bool tiny = false;  // straight-line and <= kTinyUops: persistent grid (see interp_grid)
+  std::vector<DUop> duops;  // tier 0, forward jumps only, <= kMaxDagUops: dag_kernel's table
   std::mutex mu;
   Uop* dev_uops[kMaxDevices] = {};
+  DUop* dev_duops[kMaxDevices] = {};
 };
+
+// EBPFEMU_NO_DAG=1 runs every tier-0 program on interp_kernel (A/B runs, differential tests).
+static const bool g_no_dag = [] {
+  const char* e = getenv("EBPFEMU_NO_DAG");
+  return e && e[0] == '1';
+}();
+
+// Width mask of an access of w bytes.
+static uint64_t width_mask(uint32_t w) { return w >= 8 ? ~0ull : ((1ull << (8 * w)) - 1); }
+
+// dag_kernel's table: every per-step quantity that depends only on the micro-op (uop.h DUop).
+static std::vector<DUop> build_dag(const std::vector<Uop>& uops) {
+  const uint32_t n = (uint32_t)uops.size();
+  std::vector<DUop> d(n);
+  auto bit = [&](uint32_t pc) -> uint64_t { return pc < n && n <= 64 ? 1ull << pc : 0ull; };
+  for (uint32_t i = 0; i < n; i++) {
+    const Uop& u = uops[i];
+    DUop& o = d[i];
+    std::memset(&o, 0, sizeof o);
+    o.op = u.op;
+    o.aux = u.aux;
+    o.doff = (uint32_t)u.dst * kRegStride;
+    o.soff = (uint32_t)u.src * kRegStride;
+    o.npc = i + 1 < n ? i + 1 : PC_DONE;
+    o.nbit = bit(i + 1);
+    o.k = (uint64_t)u.k;
+    if (u.op >= U_JA && u.op <= U_JLE32) {
+      const uint32_t t = (uint32_t)u.x;
+      o.x = t < n ? t : PC_DONE;
+      o.tbit = bit(t);
+    } else {
+      o.x = (uint32_t)u.x;
+    }
+    if (u.op == U_LDX) o.k = width_mask(u.aux);
+  }
+  return d;
+}
 
 extern "C" {
 
@@ -246,11 +286,14 @@ int ebpf_prog_load(const uint8_t* code, size_t nbytes, ebpf_prog** out, size_t* 
     if (u.op == U_ST || u.op == U_STX || u.op == U_ATOMIC || u.op == U_CALL) p->tier = 1;
     p->uops.push_back(u);
   }
-  p->tiny = p->uops.size() <= kTinyUops;
+  bool forward = true;  // no back edge: every lane's pc only grows (a DAG)
   for (size_t i = 0; i < p->uops.size(); i++) {
     const Uop& u = p->uops[i];
-    if (u.op >= U_JA && u.op <= U_CALL && (uint32_t)u.x <= (uint32_t)i) p->tiny = false;
+    if (u.op >= U_JA && u.op <= U_CALL && (uint32_t)u.x <= (uint32_t)i) forward = false;
   }
+  p->tiny = forward && p->uops.size() <= kTinyUops;
+  if (forward && p->tier == 0 && !p->uops.empty() && p->uops.size() <= kMaxDagUops)
+    p->duops = build_dag(p->uops);
   *out = p;
   return EBPF_OK;
 }
@@ -269,9 +312,10 @@ void ebpf_prog_free(ebpf_prog* p) {
   if (!p) return;
   int cur = device_of_current();
   for (int d = 0; d < kMaxDevices; d++) {
-    if (p->dev_uops[d]) {
+    if (p->dev_uops[d] || p->dev_duops[d]) {
       hipSetDevice(d);
-      hipFree(p->dev_uops[d]);
+      if (p->dev_uops[d]) hipFree(p->dev_uops[d]);
+      if (p->dev_duops[d]) hipFree(p->dev_duops[d]);
     }
   }
   hipSetDevice(cur);
@@ -295,6 +339,8 @@ int ebpf_prog_insn(const ebpf_prog* p, size_t i, int32_t* imm, int64_t* imm64, i
 
 int ebpf_prog_tier(const ebpf_prog* p) { return p ? p->tier : -1; }
 
+int ebpf_prog_forward_only(const ebpf_prog* p) { return p ? (p->duops.empty() ? 0 : 1) : -1; }
+
 int ebpf_prog_upload(ebpf_prog* p, int device) {
   if (!p || device < 0 || device >= kMaxDevices) return EBPF_EINVAL;
   std::lock_guard<std::mutex> lk(p->mu);
@@ -309,8 +355,20 @@ int ebpf_prog_upload(ebpf_prog* p, int device) {
            hipMemcpy(d, p->uops.data(), p->uops.size() * sizeof(Uop), hipMemcpyHostToDevice) !=
                hipSuccess)
     rc = EBPF_EHIP;
-  if (rc == EBPF_OK) p->dev_uops[device] = d;
-  else if (d) hipFree(d);
+  DUop* dd = nullptr;
+  if (rc == EBPF_OK && !p->duops.empty()) {
+    if (hipMalloc(&dd, p->duops.size() * sizeof(DUop)) != hipSuccess ||
+        hipMemcpy(dd, p->duops.data(), p->duops.size() * sizeof(DUop), hipMemcpyHostToDevice) !=
+            hipSuccess)
+      rc = EBPF_EHIP;
+  }
+  if (rc == EBPF_OK) {
+    p->dev_uops[device] = d;
+    p->dev_duops[device] = dd;
+  } else {
+    if (d) hipFree(d);
+    if (dd) hipFree(dd);
+  }
   hipSetDevice(cur);
   return rc;
 }
@@ -335,7 +393,7 @@ static int check_batch(const ebpf_batch* b) {
   if (b->max_steps == 0) return EBPF_EINVAL;
   if (b->n && !b->frames) return EBPF_EINVAL;
   if (!b->offsets && b->stride == 0 && !b->lens) return EBPF_EINVAL;
-  if (b->flags != 0) return EBPF_EINVAL;
+  if (b->flags & ~EBPF_BATCH_GENERIC) return EBPF_EINVAL;
   return EBPF_OK;
 }
 
@@ -358,8 +416,13 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* b, const ebpf_batch_out* out,
   if (cur != device) hipSetDevice(device);
 
   const uint64_t n_tiles = (b->n + 63) / 64;
+  // dag_kernel needs no step budget: a lane of a forward-only program retires <= n_uops steps
+  const int kind = (p->dev_duops[device] && b->max_steps >= p->uops.size() && !g_no_dag &&
+                    !(b->flags & EBPF_BATCH_GENERIC))
+                       ? kKindDag
+                       : p->tier;
   int grid = 0;
-  if (interp_grid(p->tier, (uint32_t)p->uops.size(), p->tiny, n_tiles, &grid) != 0) {
+  if (interp_grid(kind, (uint32_t)p->uops.size(), p->tiny, n_tiles, &grid) != 0) {
     if (cur != device) hipSetDevice(cur);
     return EBPF_EHIP;
   }
@@ -394,6 +457,7 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* b, const ebpf_batch_out* out,
   }
   LaunchArgs a{};
   a.prog = p->dev_uops[device];
+  a.dprog = p->dev_duops[device];
   a.n_uops = (uint32_t)p->uops.size();
   a.mem_size = b->mem_size;
   a.frames = b->frames;
@@ -413,7 +477,7 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* b, const ebpf_batch_out* out,
   a.init_regs = b->init_regs;
   a.mem_out = out->mem;
   a.regs_out = out->regs;
-  hipError_t e = launch_interp(p->tier, a, grid, s);
+  hipError_t e = launch_interp(kind, a, grid, s);
   if (cur != device) hipSetDevice(cur);
   return e == hipSuccess ? EBPF_OK : EBPF_EHIP;
 }

@@ -275,6 +275,33 @@ __device__ __forceinline__ void stage_window_lane(uint8_t* pw, uint32_t swz, con
     *(uint32_t*)(pw + win_off(bo, swz)) = (bo < m) ? (uint32_t)pkt_read(base, bo, 4, len) : 0u;
 }
 
+// ---- counters: workgroup sum -> non-returning sharded device atomics. Nothing waits on them:
+//      the workgroup retires at once and fold_counters (next on the stream) folds the shards
+//      into the caller's counters. cnt[] is wave-uniform, retired per lane. Reuses LDS (smem),
+//      so every wave of the workgroup must be done with its LDS data. ----
+__device__ __forceinline__ void flush_counters(const LaunchArgs& a, const uint64_t (&cnt)[7],
+                                               uint64_t retired, uint8_t* smem, uint32_t lane,
+                                               uint32_t wv) {
+  for (int off = 32; off >= 1; off >>= 1) retired += (uint64_t)__shfl_xor((long long)retired, off);
+  if (a.counters == nullptr) return;
+  __syncthreads();
+  uint64_t* red = (uint64_t*)smem;
+  if (lane == 0) {
+#pragma unroll
+    for (int b = 0; b < 7; b++) red[wv * 8 + b] = cnt[b];
+    red[wv * 8 + 7] = retired;
+  }
+  __syncthreads();
+  if (threadIdx.x < 8) {
+    uint64_t s = 0;
+#pragma unroll
+    for (int w = 0; w < kWavesPerBlock; w++) s += red[w * 8 + threadIdx.x];
+    // blockIdx -> XCD is round-robin, so shard (blockIdx % 64) is only ever hit from one XCD
+    if (s) __hip_atomic_fetch_add(&a.shards[(blockIdx.x % kCounterShards) * 8 + threadIdx.x], s,
+                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // The eBPF register file r0..r10 (emu.rs:15), as two 11-entry u32 arrays (low and high words):
 // each maps to an 11-VGPR tuple indexed with s_set_gpr_idx by the scalar register number, where a
 // uint64_t[11] would occupy a 32-VGPR tuple (10 registers wasted).
@@ -710,27 +737,279 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
   }
   if (TIER == 0) dma_wait();  // no LDS-DMA may still target this workgroup's LDS at exit
 
-  // ---- counters: workgroup sum -> non-returning sharded device atomics. Nothing waits on
-  //      them: the workgroup retires at once and fold_counters (next on the stream) folds the
-  //      shards into the caller's counters. ----
-  for (int off = 32; off >= 1; off >>= 1) retired += (uint64_t)__shfl_xor((long long)retired, off);
-  if (a.counters == nullptr) return;
-  __syncthreads();  // all waves are done with their windows: reuse LDS
-  uint64_t* red = (uint64_t*)smem;
-  if (lane == 0) {
+  flush_counters(a, cnt, retired, smem, lane, wv);
+}
+
+// ============================================================================================
+// dag_kernel — tier-0 programs whose jumps all go forward (the verifier-era XDP shape), run with
+// max_steps >= n_uops. Same semantics as interp_kernel<0, ...> (bit-exact, tested against each
+// other and the oracle), shaped around the CU's ONE scalar unit, which interp_kernel saturates:
+//   * the register file lives in LDS ([11][64] u64 per wave), so a register access is a VALU
+//     address add + ds_read/ds_write instead of an s_set_gpr_idx_on/off pair per 32-bit half;
+//   * the micro-op is ONE s_load_dwordx16 of a DUop whose fields are pre-scaled on the host
+//     (register byte offsets, next pc, jump target, pc-set bits), so no readfirstlane/bit-field
+//     extraction;
+//   * lanes only move forward, so no step budget can bind (a lane retires <= n_uops steps) and
+//     the scheduler is just "lowest pc with a parked lane" over a pc set whose every member has
+//     a lane parked at it: no step counters, no termination guard, no empty iterations.
+// Each step is computed by all lanes and committed through selects on `act`, as in
+// interp_kernel, so uniform state (the pc set) is never written under divergent control flow.
+// ============================================================================================
+constexpr uint32_t kRegBytes = 11 * kRegStride;                           // 5.5 KiB per wave
+constexpr uint32_t kDagMetaBytes = 2 * kWave * 4;                         // offsets + lengths
+constexpr uint32_t kDagWaveLds = kRegBytes + kWinBytes + kDagMetaBytes;  // 10 KiB per wave
+
+typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
+
+// One DUop (64 B) from the device table into SGPRs.
+__device__ __forceinline__ u32x16 load_duop(const DUop* prog, uint32_t pc) {
+  u32x16 v;
+  asm("s_load_dwordx16 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)"
+      : "=s"(v) : "s"(prog), "s"(pc * (uint32_t)sizeof(DUop)));
+  return v;
+}
+
+__device__ __forceinline__ uint64_t rget(const uint8_t* rl, uint32_t off) {
+  return *(const uint64_t*)(rl + off);
+}
+__device__ __forceinline__ void rset(uint8_t* rl, uint32_t off, uint64_t v) {
+  *(uint64_t*)(rl + off) = v;
+}
+
+template <int NW>
+__global__ __launch_bounds__(kBlock) void dag_kernel(LaunchArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint32_t lane = threadIdx.x & (kWave - 1);
+  const uint32_t wv = threadIdx.x / kWave;
+  uint8_t* const wreg = smem + wv * kDagWaveLds;
+  uint8_t* const rl = wreg + lane * 8;  // this lane's regs[0]; regs[r] at + r * kRegStride
+  WaveLds L;
+  L.win = wreg + kRegBytes;
+  L.meta_off = (uint32_t*)(L.win + kWinBytes);
+  L.meta_len = L.meta_off + kWave;
+  const uint32_t my_swz = win_swz(lane);
+  uint8_t* const my_win = L.win + lane * kWin;
+  const uint64_t wave_slot = (uint64_t)blockIdx.x * kWavesPerBlock + wv;
+  const uint64_t total_waves = (uint64_t)gridDim.x * kWavesPerBlock;
+  const uint32_t mem_size = a.mem_size;
+
+  uint64_t cnt[7] = {0, 0, 0, 0, 0, 0, 0};
+  uint64_t retired = 0;
+
+  for (uint64_t tile = wave_slot; tile < a.n_tiles; tile += total_waves) {
+    const uint64_t pkt = tile * kWave + lane;
+    const bool valid = pkt < a.n;
+    // ---- header windows (as interp_kernel's single-buffered tier 0) ----
+    dma_meta(a, L, 0, tile, lane);
+    dma_wait();
+    uintptr_t mb;
+    uint32_t ml;
+    meta_of(a, L, 0, tile, lane, mb, ml);
+    const uint8_t* const base = (const uint8_t*)mb;
+    const uint32_t len = valid ? ml : 0u;
+    const bool co = ballot(valid && ml != 0 && (mb & 15) != 0) == 0;
+    if (co) dma_window(a, L, 0, 0, tile, lane);
+
+    // ---- Emu::default() + main.rs:14-31 register layout (or caller-set regs) ----
+    if (a.init_regs) {
 #pragma unroll
-    for (int b = 0; b < 7; b++) red[wv * 8 + b] = cnt[b];
-    red[wv * 8 + 7] = retired;
-  }
-  __syncthreads();
-  if (threadIdx.x < 8) {
-    uint64_t s = 0;
+      for (int i = 0; i < 11; i++) rset(rl, i * kRegStride, a.init_regs[i]);
+    } else {
 #pragma unroll
-    for (int w = 0; w < kWavesPerBlock; w++) s += red[w * 8 + threadIdx.x];
-    // blockIdx -> XCD is round-robin, so shard (blockIdx % 64) is only ever hit from one XCD
-    if (s) __hip_atomic_fetch_add(&a.shards[(blockIdx.x % kCounterShards) * 8 + threadIdx.x], s,
-                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int i = 0; i < 11; i++)
+        rset(rl, i * kRegStride, i == 2 ? (uint64_t)len : i == 10 ? a.r10 : 0ull);
+    }
+    uint32_t lpc = valid ? 0u : PC_DONE;
+    uint32_t st = EBPF_ST_OK;
+    uint32_t nsteps = 0;
+    if (valid && len > mem_size) {  // main.rs:20-21 index panic
+      st = EBPF_ST_BADPKT;
+      lpc = PC_DONE;
+    }
+    if (co) dma_wait();
+    else stage_window_lane(my_win, my_swz, base, len, valid);
+
+    // ---- Emu::run (emu.rs:452-458): lowest parked pc first ----
+    PcSet<NW> live;
+    live.init(ballot(lpc == 0) != 0);
+    for (;;) {
+      const uint32_t P = live.first();
+      if (P == PC_DONE) break;
+      live.del(P);
+      const u32x16 q = load_duop(a.dprog, P);
+      const uint32_t op = q[0], aux = q[1], doff = q[2], soff = q[3], npc = q[4], x = q[5];
+      const uint64_t k = (uint64_t)q[8] | ((uint64_t)q[9] << 32);
+      const uint64_t nbit = (uint64_t)q[10] | ((uint64_t)q[11] << 32);
+      const uint64_t tbit = (uint64_t)q[12] | ((uint64_t)q[13] << 32);
+      const bool act = lpc == P;
+      const uint64_t A = rget(rl, doff);
+      const uint64_t S = rget(rl, soff);
+      const uint64_t B = (aux & F_SRC) ? S : k;
+      const uint32_t a32 = (uint32_t)A, b32 = (uint32_t)B;
+      uint64_t R;
+      bool cnd;
+      switch (op) {
+        // ---- ALU64 ----
+        case U_ADD64: R = A + B; goto alu;
+        case U_SUB64: R = A - B; goto alu;
+        case U_MUL64: R = A * B; goto alu;
+        case U_DIV64: R = B ? A / B : 0; goto alu;
+        case U_OR64: R = A | B; goto alu;
+        case U_AND64: R = A & B; goto alu;
+        case U_LSH64: R = A << (b32 & 63); goto alu;
+        case U_RSH64: R = A >> (b32 & 63); goto alu;
+        case U_NEG64: R = 0 - A; goto alu;
+        case U_MOD64: R = B ? A % B : A; goto alu;
+        case U_XOR64: R = A ^ B; goto alu;
+        case U_MOV64: R = B; goto alu;
+        case U_ARSH64: {  // rotate, then multiply by the sign (Q4, emu.rs:142-164)
+          const uint32_t sh = b32 & 63;
+          const uint64_t rot = sh ? ((A >> sh) | (A << (64 - sh))) : A;
+          const bool neg = (int64_t)A < 0;
+          const bool fault = neg && rot == 0x8000000000000000ull;  // i64::MIN * -1 (emu.rs:162)
+          R = neg ? 0 - rot : rot;
+          const bool ok = act && !fault;
+          rset(rl, doff, ok ? R : A);
+          st = (act && fault) ? (uint32_t)EBPF_ST_ARITH : st;
+          lpc = act ? (fault ? PC_DONE : npc) : lpc;
+          nsteps += ok ? 1u : 0u;
+          if (ballot(ok) != 0) {
+            if (NW == 1) live.w0 |= nbit;
+            else if (npc != PC_DONE) live.add(npc);
+          }
+          continue;
+        }
+        // ---- ALU32 (Q6/Q25) ----
+        case U_ADD32: R = (uint32_t)(a32 + b32); goto alu;
+        case U_SUB32: R = (uint32_t)(a32 - b32); goto alu;
+        case U_MUL32: R = (uint32_t)(a32 * b32); goto alu;
+        case U_DIV32: R = b32 ? a32 / b32 : 0u; goto alu;
+        case U_OR32: R = a32 | b32; goto alu;
+        case U_AND32: R = a32 & b32; goto alu;
+        case U_LSH32: R = (uint32_t)(a32 << (b32 & 31)); goto alu;
+        case U_RSH32: R = a32 >> (b32 & 31); goto alu;
+        case U_NEG32: R = (uint32_t)(0u - a32); goto alu;
+        case U_MOD32: R = b32 ? a32 % b32 : a32; goto alu;
+        case U_XOR32: R = a32 ^ b32; goto alu;
+        case U_MOV32: R = b32; goto alu;
+        case U_ARSH32: {
+          const uint32_t rot = __builtin_amdgcn_alignbit(a32, a32, b32 & 31);
+          R = (int32_t)a32 < 0 ? (uint32_t)(0u - rot) : rot;
+          goto alu;
+        }
+        // ---- END (Q7) ----
+        case U_ZX16: R = A & 0xffffull; goto alu;
+        case U_ZX32: R = A & 0xffffffffull; goto alu;
+        case U_NOP: R = A; goto alu;
+        case U_BSWAP16: R = ((A & 0xff) << 8) | ((A >> 8) & 0xff); goto alu;
+        case U_BSWAP32: R = bswap32(a32); goto alu;
+        case U_BSWAP64: R = ((uint64_t)bswap32(a32) << 32) | bswap32((uint32_t)(A >> 32)); goto alu;
+        case U_LDIMM: R = k; goto alu;
+        // ---- JMP: signed orderings (Q2); JMP32 on sign-extended low words (Q3) ----
+        case U_JA: cnd = true; goto jump;
+        case U_JEQ: cnd = A == B; goto jump;
+        case U_JGT: cnd = (int64_t)A > (int64_t)B; goto jump;
+        case U_JGE: cnd = (int64_t)A >= (int64_t)B; goto jump;
+        case U_JSET: cnd = (A & B) != 0; goto jump;
+        case U_JNE: cnd = A != B; goto jump;
+        case U_JLT: cnd = (int64_t)A < (int64_t)B; goto jump;
+        case U_JLE: cnd = (int64_t)A <= (int64_t)B; goto jump;
+        case U_JEQ32: cnd = a32 == b32; goto jump;
+        case U_JGT32: cnd = (int32_t)a32 > (int32_t)b32; goto jump;
+        case U_JGE32: cnd = (int32_t)a32 >= (int32_t)b32; goto jump;
+        case U_JSET32: cnd = (a32 & b32) != 0; goto jump;
+        case U_JNE32: cnd = a32 != b32; goto jump;
+        case U_JLT32: cnd = (int32_t)a32 < (int32_t)b32; goto jump;
+        case U_JLE32: cnd = (int32_t)a32 <= (int32_t)b32; goto jump;
+        case U_EXIT:  // emu.rs:273-279 with an empty frame stack: stop
+          lpc = act ? PC_DONE : lpc;
+          nsteps += act ? 1u : 0u;
+          continue;
+        case U_LDX: {  // emu.rs:341-349 + mmu.rs bounds (Q1 upper bytes kept, Q20 first byte)
+          int64_t sum;
+          const bool ovf = __builtin_add_overflow((int64_t)S, (int64_t)(int32_t)x, &sum);
+          const uint64_t ua = (uint64_t)sum;
+          const bool oob = ovf || ua >= mem_size;
+          const bool ub = !oob && ua + aux > mem_size;
+          const bool fault = oob || ub;
+          const uint32_t a0 = (uint32_t)ua;
+          const bool ok = act && !fault;
+          const bool in_pkt = a0 < len;
+          const bool in_win = a0 + aux <= (uint32_t)kWin;
+          // the window read is harmless for every lane (address kept inside the window)
+          uint64_t v = win_read(my_win, my_swz, in_win ? a0 : 0u, aux, len);
+          v = (in_pkt && in_win) ? v : 0ull;
+          const bool far = ok && in_pkt && !in_win;
+          if (ballot(far) != 0) {
+            if (far) v = pkt_read(base, a0, aux, len);
+          }
+          R = (A & ~k) | v;  // k = width mask
+          rset(rl, doff, ok ? R : A);
+          st = (act && fault) ? (oob ? (uint32_t)EBPF_ST_MEM : (uint32_t)EBPF_ST_MEM_UB) : st;
+          lpc = act ? (fault ? PC_DONE : npc) : lpc;
+          nsteps += ok ? 1u : 0u;
+          if (ballot(ok) != 0) {
+            if (NW == 1) live.w0 |= nbit;
+            else if (npc != PC_DONE) live.add(npc);
+          }
+          continue;
+        }
+        default:  // U_FAULT (static faults; tier-1 kinds never reach this kernel)
+          st = act ? (op == U_FAULT ? aux : (uint32_t)EBPF_ST_INSN) : st;
+          lpc = act ? PC_DONE : lpc;
+          continue;
+      }
+    alu:
+      rset(rl, doff, act ? R : A);
+      lpc = act ? npc : lpc;
+      nsteps += act ? 1u : 0u;
+      if (NW == 1) live.w0 |= nbit;
+      else if (npc != PC_DONE) live.add(npc);
+      continue;
+    jump: {
+      const uint64_t tk = ballot(act && cnd), nt = ballot(act && !cnd);
+      lpc = act ? (cnd ? x : npc) : lpc;
+      nsteps += act ? 1u : 0u;
+      if (NW == 1) {
+        live.w0 |= (tk ? tbit : 0ull) | (nt ? nbit : 0ull);
+      } else {
+        if (tk && x != PC_DONE) live.add(x);
+        if (nt && npc != PC_DONE) live.add(npc);
+      }
+    }
+    }
+
+    // ---- outputs: r0 (main.rs:43), status, verdict (xdp.rs:3-9), final image/registers ----
+    const uint64_t r0v = rget(rl, 0);
+    if (a.mem_out && valid) {
+      uint32_t* mo = (uint32_t*)(a.mem_out + pkt * (uint64_t)mem_size);
+      const uint32_t m = min(len, mem_size);
+      for (uint32_t d = 0; d < mem_size / 4; d++) {
+        uint32_t v;
+        if (d * 4 >= m) v = 0u;
+        else if (d * 4 < (uint32_t)kWin) v = (uint32_t)win_read(my_win, my_swz, d * 4, 4, len);
+        else v = (uint32_t)pkt_read(base, d * 4, 4, len);
+        mo[d] = v;
+      }
+    }
+    if (a.regs_out && valid) {
+#pragma unroll
+      for (int i = 0; i < 11; i++) a.regs_out[pkt * 11 + i] = rget(rl, i * kRegStride);
+    }
+    if (valid) {
+      if (a.r0) a.r0[pkt] = r0v;
+      if (a.status) a.status[pkt] = (uint8_t)st;
+      if (a.verdict) a.verdict[pkt] = st ? (uint8_t)EBPF_VERDICT_FAULT
+                                         : (r0v < 5 ? (uint8_t)r0v : (uint8_t)EBPF_VERDICT_OTHER);
+    }
+    const bool okv = valid && st == EBPF_ST_OK;
+#pragma unroll
+    for (int b = 0; b < 5; b++) cnt[b] += __builtin_popcountll(ballot(okv && r0v == (uint64_t)b));
+    cnt[5] += __builtin_popcountll(ballot(okv && r0v >= 5));
+    cnt[6] += __builtin_popcountll(ballot(valid && st != EBPF_ST_OK));
+    retired += valid ? nsteps : 0u;
   }
+  flush_counters(a, cnt, retired, smem, lane, wv);
 }
 
 // One workgroup: read-and-clear every shard (device-scope atomics, coherent across XCDs) and
@@ -754,9 +1033,10 @@ static bool g_db = [] {  // tier-0 window double-buffering (EBPFEMU_TIER0_DB=0|1
   return e ? e[0] == '1' : false;
 }();
 
-static uint32_t lds_bytes_for(int tier, uint32_t n_uops) {
+static uint32_t lds_bytes_for(int kind, uint32_t n_uops) {
+  if (kind == kKindDag) return kWavesPerBlock * kDagWaveLds;  // program is fetched by SMEM
   const uint32_t prog = n_uops <= (uint32_t)kMaxLdsUops ? n_uops * (uint32_t)sizeof(Uop) : 0u;
-  uint32_t rest = tier == 0 ? kWavesPerBlock * wave_lds0(g_db) : 0u;
+  uint32_t rest = kind == kKindTier0 ? kWavesPerBlock * wave_lds0(g_db) : 0u;
   if (rest < kWavesPerBlock * 8 * 8) rest = kWavesPerBlock * 8 * 8;  // counter reduction scratch
   return prog + rest;
 }
@@ -770,8 +1050,10 @@ static const void* variant(uint32_t n_uops) {
   return (const void*)interp_kernel<TIER, false, 0, DB>;
 }
 
-static const void* kernel_for(int tier, uint32_t n_uops) {
-  if (tier == 1) return variant<1, false>(n_uops);
+static const void* kernel_for(int kind, uint32_t n_uops) {
+  if (kind == kKindDag)
+    return n_uops <= 64 ? (const void*)dag_kernel<1> : (const void*)dag_kernel<4>;
+  if (kind == kKindTier1) return variant<1, false>(n_uops);
   return g_db ? variant<0, true>(n_uops) : variant<0, false>(n_uops);
 }
 
@@ -782,13 +1064,13 @@ static int g_grid = [] {
   return e[0] == 'f' ? 1 : e[0] == 't' ? 2 : 0;
 }();
 
-int interp_grid(int tier, uint32_t n_uops, bool tiny, uint64_t n_tiles, int* grid_out) {
+int interp_grid(int kind, uint32_t n_uops, bool tiny, uint64_t n_tiles, int* grid_out) {
   int dev = 0, cus = 256, per_cu = 1;
   if (hipGetDevice(&dev) != hipSuccess) return -1;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return -1;
-  const uint32_t lds = lds_bytes_for(tier, n_uops);
-  const void* k = kernel_for(tier, n_uops);
+  const uint32_t lds = lds_bytes_for(kind, n_uops);
+  const void* k = kernel_for(kind, n_uops);
   {
     static std::mutex mu;
     static std::map<std::tuple<int, const void*, uint32_t>, int> cache;
@@ -804,14 +1086,14 @@ int interp_grid(int tier, uint32_t n_uops, bool tiny, uint64_t n_tiles, int* gri
       cache[key] = per_cu;
     }
   }
-  if (tier == 1 && per_cu > 4) per_cu = 4;  // bounds the tier-1 image scratch
+  if (kind == kKindTier1 && per_cu > 4) per_cu = 4;  // bounds the tier-1 image scratch
   const uint64_t resident = (uint64_t)cus * (uint64_t)per_cu * kWavesPerBlock;
   const uint64_t tiles = n_tiles ? n_tiles : 1;
   uint64_t waves;
-  const int policy = g_grid >= 0 ? g_grid : tier == 1 ? 0 : tiny ? 1 : 2;
+  const int policy = g_grid >= 0 ? g_grid : kind == kKindTier1 ? 0 : tiny ? 1 : 2;
   if (policy == 1) {
     waves = tiles < resident ? tiles : resident;  // every resident slot, grid-stride
-  } else if (policy == 2 && tier == 0) {
+  } else if (policy == 2 && kind != kKindTier1) {
     waves = tiles;  // one tile per wave, hardware dispatch
   } else {
     // Persistent waves, each owning the same number of tiles (+-1): k = ceil(tiles / resident
@@ -823,11 +1105,11 @@ int interp_grid(int tier, uint32_t n_uops, bool tiny, uint64_t n_tiles, int* gri
   return 0;
 }
 
-hipError_t launch_interp(int tier, const LaunchArgs& a, int grid, hipStream_t stream) {
-  const uint32_t lds = lds_bytes_for(tier, a.n_uops);
+hipError_t launch_interp(int kind, const LaunchArgs& a, int grid, hipStream_t stream) {
+  const uint32_t lds = lds_bytes_for(kind, a.n_uops);
   void* args[] = {(void*)&a};
   hipError_t e =
-      hipLaunchKernel(kernel_for(tier, a.n_uops), dim3(grid), dim3(kBlock), args, lds, stream);
+      hipLaunchKernel(kernel_for(kind, a.n_uops), dim3(grid), dim3(kBlock), args, lds, stream);
   if (e != hipSuccess || a.counters == nullptr) return e;
   uint64_t* shards = a.shards;
   uint64_t* counters = a.counters;

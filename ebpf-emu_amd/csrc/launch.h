@@ -19,8 +19,14 @@ constexpr int kCounterShards = 64;    // device-atomic counter shards (spread co
 constexpr uint64_t kWsShardsOff = 256;
 constexpr uint64_t kWsSlotsOff = 256 + kCounterShards * 8 * 8;
 
+// Kernel kinds: the two memory tiers of interp_kernel, and dag_kernel (tier-0 programs whose
+// jumps all go forward, run with max_steps >= n_uops so no step budget can bind).
+enum KernelKind : int { kKindTier0 = 0, kKindTier1 = 1, kKindDag = 2 };
+constexpr uint32_t kMaxDagUops = 256;
+
 struct LaunchArgs {
   const Uop* prog;      // device micro-ops
+  const DUop* dprog;    // device DAG micro-ops (kKindDag)
   uint32_t n_uops;
   uint32_t mem_size;
   const uint8_t* frames;
@@ -50,13 +56,13 @@ __host__ __device__ inline uint64_t tier1_slot_bytes(uint32_t mem_size) {
 // Programs this short with no back edge do a fixed, tiny amount of work per tile.
 constexpr uint32_t kTinyUops = 8;
 
-// Grid size on the current device. Tier 0: one tile (64 packets) per wave, so the hardware
+// Grid size on the current device. Tier 0 and DAG: one tile (64 packets) per wave, so the hardware
 // dispatcher balances divergent tiles, except `tiny` programs, which get every resident wave
 // slot once (grid-stride) so per-workgroup fixed costs are paid once per slot. Tier 1:
 // balanced persistent waves (bounds the per-wave image scratch).
-int interp_grid(int tier, uint32_t n_uops, bool tiny, uint64_t n_tiles, int* grid_out);
+int interp_grid(int kind, uint32_t n_uops, bool tiny, uint64_t n_tiles, int* grid_out);
 
 // Enqueue the interpreter, then (when counters are requested) fold_counters on the same stream.
-hipError_t launch_interp(int tier, const LaunchArgs& a, int grid, hipStream_t stream);
+hipError_t launch_interp(int kind, const LaunchArgs& a, int grid, hipStream_t stream);
 
 }  // namespace ebpfemu

@@ -53,4 +53,25 @@ enum UopKind : uint8_t {
 
 constexpr uint32_t PC_DONE = 0xFFFFFFFFu;
 
+// Per-lane register file of the DAG kernel in LDS: regs[r] of lane l at r * kRegStride + l * 8.
+constexpr uint32_t kRegStride = 64 * 8;
+
+// Micro-op of the DAG kernel (tier-0 programs whose jumps all go forward, dag_kernel in
+// interp.hip): a Uop with everything the kernel would otherwise compute per step resolved at
+// load time, fetched by ONE scalar load (s_load_dwordx16) straight into SGPRs.
+struct alignas(64) DUop {
+  uint32_t op;    // UopKind
+  uint32_t aux;   // as Uop::aux
+  uint32_t doff;  // dst * kRegStride
+  uint32_t soff;  // src * kRegStride
+  uint32_t npc;   // pc + 1, or PC_DONE when that falls off the end (a normal stop, emu.rs:452)
+  uint32_t x;     // jump target (PC_DONE past the end) or LDX offset (sign-extended i16)
+  uint32_t pad0, pad1;
+  uint64_t k;     // immediate (ALU/JMP/LDIMM); LDX: mask of the access width's low bytes
+  uint64_t nbit;  // 1 << npc in the pc set of programs of <= 64 micro-ops (0 for PC_DONE)
+  uint64_t tbit;  // 1 << x likewise, for jumps
+  uint64_t pad2;
+};
+static_assert(sizeof(DUop) == 64, "DUop must be 64 bytes");
+
 }  // namespace ebpfemu

@@ -23,10 +23,12 @@ STATUS_NAMES = ["OK", "MEM", "MEM_UB", "INSN", "ARITH", "STEPS", "CALLDEPTH", "B
 VERDICT_OTHER, VERDICT_FAULT = 0xFE, 0xFF
 NCOUNTERS = 8
 DEFAULT_MEM, DEFAULT_R10, DEFAULT_STEPS = 1024, 512, 1 << 22
+BATCH_GENERIC = 1  # ebpf_batch.flags: EBPF_BATCH_GENERIC
 MAX_CALL_DEPTH = 64
 
 EXPORTS = ["ebpf_batch_init", "ebpf_prog_load", "ebpf_prog_load_hex", "ebpf_prog_free",
-           "ebpf_prog_len", "ebpf_prog_insn", "ebpf_prog_tier", "ebpf_workspace_bytes",
+           "ebpf_prog_len", "ebpf_prog_insn", "ebpf_prog_tier", "ebpf_prog_forward_only",
+           "ebpf_workspace_bytes",
            "ebpf_prog_upload", "ebpf_run_batch", "ebpf_run_batch_multi", "ebpf_strerror",
            "ebpf_version"]
 
@@ -81,6 +83,7 @@ def lib():
                                  ctypes.POINTER(ctypes.c_uint8), ctypes.POINTER(ctypes.c_uint8),
                                  ctypes.POINTER(ctypes.c_uint8)]
     L.ebpf_prog_tier.argtypes = [vp]
+    L.ebpf_prog_forward_only.argtypes = [vp]
     L.ebpf_workspace_bytes.argtypes = [vp, ctypes.POINTER(Batch), ctypes.c_int]
     L.ebpf_workspace_bytes.restype = u64
     L.ebpf_prog_upload.argtypes = [vp, ctypes.c_int]

@@ -57,6 +57,11 @@ class Program:
         return _lib.lib().ebpf_prog_tier(self._h)
 
     @property
+    def forward_only(self) -> bool:
+        """True when batches run on the forward-jump fast path (max_steps >= len(self))."""
+        return bool(_lib.lib().ebpf_prog_forward_only(self._h))
+
+    @property
     def instructions(self):
         return _decoded(self._h)
 
@@ -79,7 +84,7 @@ class Program:
     def make_batch(self, frames, n: int | None = None, stride: int = 0, offsets=None, lens=None,
                    mem_size: int = _lib.DEFAULT_MEM, r10: int = _lib.DEFAULT_R10,
                    max_steps: int = _lib.DEFAULT_STEPS, init_regs=None,
-                   workspace=None) -> _lib.Batch:
+                   workspace=None, generic: bool = False) -> _lib.Batch:
         b = _lib.Batch()
         _lib.lib().ebpf_batch_init(ctypes.byref(b))
         if n is None:
@@ -93,6 +98,7 @@ class Program:
         b.r10 = r10 & ((1 << 64) - 1)
         b.max_steps = max_steps
         b.init_regs = init_regs.data_ptr() if init_regs is not None else None
+        b.flags = _lib.BATCH_GENERIC if generic else 0
         if workspace is not None:
             b.workspace = workspace.data_ptr()
             b.workspace_bytes = workspace.numel() * workspace.element_size()
@@ -115,17 +121,19 @@ class Program:
             mem_size: int = _lib.DEFAULT_MEM, r10: int = _lib.DEFAULT_R10,
             max_steps: int = _lib.DEFAULT_STEPS, init_regs=None, verdict: bool = True,
             r0: bool = False, status: bool = False, counters=None, mem: bool = False,
-            regs: bool = False, stream=None) -> BatchResult:
+            regs: bool = False, stream=None, generic: bool = False) -> BatchResult:
         """Run the program over a device-resident batch; returns device tensors.
 
         frames: torch.uint8 CUDA tensor. Layout: packet i at frames[i*stride:] (stride layout,
         len = lens[i] or stride) or at frames[offsets[i]:] (offsets: torch.int32 / uint32 bits,
         lens: torch.int16/uint16 bits). counters: an optional torch.int64 [8] tensor to add to.
+        generic: run on the general interpreter even if the forward-jump fast path applies.
         """
         import torch
 
         dev = frames.device
-        b = self.make_batch(frames, n, stride, offsets, lens, mem_size, r10, max_steps, init_regs)
+        b = self.make_batch(frames, n, stride, offsets, lens, mem_size, r10, max_steps, init_regs,
+                            generic=generic)
         n = b.n
         res = BatchResult()
         if verdict:

@@ -66,6 +66,9 @@ typedef struct ihipStream_t* ebpf_stream_t; /* == hipStream_t */
 
 #define EBPF_MAX_INSNS      65536  /* decoded instructions per program */
 #define EBPF_MAX_CALL_DEPTH 64
+/* ebpf_batch.flags: run on the general interpreter even when the program qualifies for the
+ * forward-jump fast path (differential testing; results are identical by contract). */
+#define EBPF_BATCH_GENERIC 1u
 #define EBPF_DEFAULT_MEM    1024   /* main.rs:16 */
 #define EBPF_DEFAULT_R10    512    /* main.rs:31 */
 #define EBPF_DEFAULT_STEPS  (1ull << 22)
@@ -80,7 +83,7 @@ typedef struct ebpf_batch {
   uint64_t stride;          /* bytes between packets in the stride layout */
   uint64_t n;               /* packets */
   uint32_t mem_size;        /* bytes of the per-packet memory image (multiple of 8, >= 8) */
-  uint32_t flags;           /* reserved, 0 */
+  uint32_t flags;           /* 0, or EBPF_BATCH_GENERIC */
   uint64_t r10;             /* initial r10 (stack top) */
   uint64_t max_steps;       /* per-packet step budget, 1..; faults EBPF_ST_STEPS beyond */
   void* workspace;          /* optional device scratch of ebpf_workspace_bytes() bytes, ZEROED before its
@@ -127,6 +130,11 @@ int ebpf_prog_insn(const ebpf_prog* prog, size_t i, int32_t* imm, int64_t* imm64
 /* Memory tier the device path uses for this program: 0 = read-only packet window (no stores,
  * no calls), 1 = general per-packet image in device workspace. */
 int ebpf_prog_tier(const ebpf_prog* prog);
+
+/* 1 when the program (memory tier 0, every jump forward, <= 256 micro-ops) runs on the
+ * forward-jump fast path -- for batches with max_steps >= its length and without
+ * EBPF_BATCH_GENERIC -- else 0; -1 for NULL. */
+int ebpf_prog_forward_only(const ebpf_prog* prog);
 
 /* Device scratch a batch needs (counter shards; tier 1 adds per-wave memory images). */
 uint64_t ebpf_workspace_bytes(const ebpf_prog* prog, const ebpf_batch* batch, int device);

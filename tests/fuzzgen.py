@@ -45,7 +45,9 @@ def _mem_ref(rng):
 
 
 def gen_program(rng: random.Random, n: int | None = None, valid_only: bool = True,
-                allow_loops: bool = True) -> bytes:
+                allow_loops: bool = True, tier0: bool = False) -> bytes:
+    """tier0=True: no ST/STX/ATOMIC/CALL (the read-only memory tier); with allow_loops=False
+    every jump goes forward, i.e. the program qualifies for the forward-jump fast path."""
     n = n or rng.randrange(3, 40)
     words: list[bytes] = []
     # seed registers with edge values so arithmetic corners are reached
@@ -76,6 +78,8 @@ def gen_program(rng: random.Random, n: int | None = None, valid_only: bool = Tru
             base, off = _mem_ref(rng)
             size = rng.choice([0x00, 0x08, 0x10, 0x18])
             words.append(encode(0x61 | size, dst, base, off))
+        elif k < 0.80 and tier0:
+            continue
         elif k < 0.80:  # ST / STX
             base, off = _mem_ref(rng)
             size = rng.choice([0x00, 0x08, 0x10, 0x18])
@@ -83,6 +87,8 @@ def gen_program(rng: random.Random, n: int | None = None, valid_only: bool = Tru
                 words.append(encode(0x62 | size, base, 0, off, _imm(rng)))
             else:
                 words.append(encode(0x63 | size, base, src, off))
+        elif k < 0.86 and tier0:
+            continue
         elif k < 0.86:  # ATOMIC
             base, off = (10, -8 * rng.randrange(1, 6)) if rng.random() < 0.8 else _mem_ref(rng)
             size = rng.choice([0x00, 0x18, 0x18, 0x08])
@@ -92,7 +98,7 @@ def gen_program(rng: random.Random, n: int | None = None, valid_only: bool = Tru
             v = rng.choice(EDGE) if rng.random() < 0.7 else rng.getrandbits(64)
             words.append(encode(0x18, dst, 0, 0, v & 0xFFFFFFFF) + encode(0, 0, 0, 0, v >> 32))
         elif k < 0.93:  # CALL / EXIT
-            if rng.random() < 0.5:
+            if rng.random() < 0.5 and not tier0:
                 words.append(encode(0x85, 0, 0, rng.randrange(0, 4)))
             else:
                 words.append(encode(0x95))

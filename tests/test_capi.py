@@ -75,6 +75,30 @@ def test_tier_selection(product_lib):
     assert tier("call +0\nexit") == 1
 
 
+def test_forward_only_selection(product_lib):
+    """The forward-jump fast path: tier 0, every jump target after the jump, <= 256 micro-ops."""
+    from ebpf_emu import workloads as W
+    from ebpf_emu.asm import assemble
+    from ebpf_emu.ins import load_image
+
+    def fwd(img):
+        h = load_image(img)
+        t = product_lib.ebpf_prog_forward_only(h)
+        product_lib.ebpf_prog_free(h)
+        return t
+
+    assert fwd(W.program("5tuple")) == 1
+    assert fwd(W.program("drop")) == 1
+    assert fwd(W.program("checksum")) == 0                      # loops
+    assert fwd(assemble("ja +0\nexit")) == 1                   # target = next insn
+    assert fwd(assemble("ja -1\nexit")) == 0                   # jump to itself
+    assert fwd(assemble("jeq r1, 0, +5\nexit")) == 1           # target past the end
+    assert fwd(assemble("stb [r10-1], 1\nexit")) == 0          # tier 1
+    assert fwd(assemble("mov r0, 0\n" * 255 + "exit")) == 1    # 256 micro-ops
+    assert fwd(assemble("mov r0, 0\n" * 256 + "exit")) == 0
+    assert product_lib.ebpf_prog_forward_only(None) == -1
+
+
 def test_invalid_arguments_fail_before_any_device_call(product_lib):
     from ebpf_emu import _lib
     from ebpf_emu.asm import assemble

@@ -51,7 +51,8 @@ def _stage(pkts, dev, stride=None, offsets_layout=False, misalign=0, align=1):
     return frames, dict(n=len(pkts), stride=stride, lens=ln)
 
 
-def _run_full(prog_img, pkts, dev, mem_size=1024, r10=512, max_steps=STEPS, **layout):
+def _run_full(prog_img, pkts, dev, mem_size=1024, r10=512, max_steps=STEPS, generic=False,
+              **layout):
     from ebpf_emu import Program
 
     torch = _torch()
@@ -59,12 +60,12 @@ def _run_full(prog_img, pkts, dev, mem_size=1024, r10=512, max_steps=STEPS, **la
     frames, kw = _stage(pkts, dev, **layout)
     cnt = torch.zeros(8, dtype=torch.int64, device=dev)
     res = prog.run(frames, mem_size=mem_size, r10=r10, max_steps=max_steps, verdict=True, r0=True,
-                   status=True, mem=True, regs=True, counters=cnt, **kw)
+                   status=True, mem=True, regs=True, counters=cnt, generic=generic, **kw)
     torch.cuda.synchronize()
     out = dict(status=res.status.cpu().numpy(), r0=res.r0.cpu().numpy().view(np.uint64),
                verdict=res.verdict.cpu().numpy(), regs=res.regs.cpu().numpy().view(np.uint64),
                mem=res.mem.cpu().numpy(), counters=cnt.cpu().numpy().view(np.uint64),
-               tier=prog.tier)
+               tier=prog.tier, fast=prog.forward_only and not generic and max_steps >= len(prog))
     prog.close()
     return out
 
@@ -122,6 +123,77 @@ def test_fuzz_wave_divergence(cuda, oracle_mod, seed):
         tiers.add(got["tier"])
         _check_against_oracle(oracle_mod, img, pkts, got, tag=f"seed {seed} it {it}")
     assert tiers == {0, 1}
+
+
+_OUT_KEYS = ("status", "r0", "verdict", "regs", "mem", "counters")
+
+
+def _same_outputs(a, b, ctx):
+    for key in _OUT_KEYS:
+        assert np.array_equal(a[key], b[key]), f"{ctx}: {key} differs"
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_forward_only_fast_path_fuzz(cuda, oracle_mod, seed):
+    """Forward-only tier-0 programs (the dag_kernel fast path) over diverging packets: every
+    output bit-identical to the general interpreter on the same batch (EBPF_BATCH_GENERIC) and
+    to the oracle."""
+    rng = random.Random(9000 + seed)
+    n_fast = 0
+    for it in range(50):
+        img = gen_program(rng, allow_loops=False, tier0=True)
+        try:
+            oracle_mod.Program(img)
+        except oracle_mod.OracleDecodeError:
+            continue
+        pkts = [gen_packet(rng) for _ in range(rng.choice([64, 65, 100, 130]))]
+        got = _run_full(img, pkts, cuda)
+        assert got["fast"], img.hex()
+        n_fast += 1
+        ref = _run_full(img, pkts, cuda, generic=True)
+        _same_outputs(got, ref, f"seed {seed} it {it} prog {img.hex()}")
+        _check_against_oracle(oracle_mod, img, pkts, got, tag=f"seed {seed} it {it}")
+    assert n_fast >= 35
+
+
+@pytest.mark.parametrize("pad", [40, 120, 230])
+def test_forward_only_wide_pc_set(cuda, oracle_mod, pad):
+    """Fast-path programs past 64 micro-ops (four-word pc set): forward jumps over `pad` filler
+    instructions, some of which are executed by the lanes that take the other branch."""
+    from ebpf_emu.asm import assemble
+
+    rng = random.Random(77 + pad)
+    for it in range(6):
+        body = gen_program(rng, n=20, allow_loops=False, tier0=True)
+        head = assemble(f"ldxb r3, [r1+0]\njgt r3, 127, +{pad}\n" + "add r0, 3\n" * pad)
+        img = head + body
+        try:
+            oracle_mod.Program(img)
+        except oracle_mod.OracleDecodeError:
+            continue
+        pkts = [gen_packet(rng) for _ in range(97)]
+        got = _run_full(img, pkts, cuda)
+        assert got["fast"]
+        _same_outputs(got, _run_full(img, pkts, cuda, generic=True), f"pad {pad} it {it}")
+        _check_against_oracle(oracle_mod, img, pkts, got, tag=f"pad {pad} it {it}")
+
+
+def test_forward_only_step_budget_falls_back(cuda, oracle_mod):
+    """max_steps below the program length can bind, so the batch runs on the general
+    interpreter: same statuses as the oracle with that budget."""
+    from ebpf_emu.asm import assemble
+
+    img = assemble("mov r0, 1\n" * 10 + "exit")
+    pkts = [bytes(range(n)) for n in (0, 5, 64, 70)]
+    for budget in (1, 5, 10, 11, 12):
+        got = _run_full(img, pkts, cuda, max_steps=budget)
+        assert got["fast"] == (budget >= 11)
+        op = oracle_mod.Program(img)
+        for i, p in enumerate(pkts):
+            st, regs, mem, steps = op.run_full(p, 1024, 512, budget)
+            assert got["status"][i] == st, (budget, i)
+            if st == 0:
+                assert [int(v) for v in got["regs"][i]] == regs
 
 
 @pytest.mark.parametrize("pad", [70, 300, 5000])

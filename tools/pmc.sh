@@ -14,6 +14,9 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" \
            "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS" \
            "GRBM_GUI_ACTIVE SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU_INT64 TCC_HIT_sum TCC_MISS_sum"; do
   i=$((i+1))
-  timeout -k 10 240 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d "$out/p$i" -o run -- python3 "$root/bench.py" --steps 20 --warmup 3 --cpu-seconds 0 "$@" > "$out/p$i.log" 2>&1 || { echo "pass $i ($grp) failed rc=$?"; tail -5 "$out/p$i.log"; }
+  timeout -k 10 240 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d "$out/p$i" -o run -- python3 "$root/bench.py" --steps 20 --warmup 3 --cpu-seconds 0 "$@" > "$out/p$i.log" 2>&1 || {
+    rc=$?; echo "pass $i ($grp) failed rc=$rc"; tail -5 "$out/p$i.log"
+    [ $rc -ge 124 ] && exit $rc  # timeout / abort / fault: nothing more on the GPU
+  }
 done
 ls -R "$out" | head -50
