@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "../../include/ebpf_emu.h"
+#include "dag_asm.h"
 #include "launch.h"
 #include "uop.h"
 
@@ -216,10 +217,12 @@ struct ebpf_prog {
   std::vector<Uop> uops;
   int tier = 0;
   bool tiny = false;  // straight-line and <= kTinyUops: persistent grid (see interp_grid)
-  std::vector<DUop> duops;  // tier 0, forward jumps only, <= kMaxDagUops: dag_kernel's table
+  std::vector<DUop> duops;   // tier 0, forward jumps only, <= kMaxDagUops: dag_kernel's table
+  std::vector<DUop> duopsk;  // the same with constant-address loads resolved (no init_regs)
   std::mutex mu;
   Uop* dev_uops[kMaxDevices] = {};
   DUop* dev_duops[kMaxDevices] = {};
+  DUop* dev_duopsk[kMaxDevices] = {};
 };
 
 // EBPFEMU_NO_DAG=1 runs every tier-0 program on interp_kernel (A/B runs, differential tests).
@@ -232,6 +235,54 @@ static const bool g_no_dag = [] {
 static uint64_t width_mask(uint32_t w) { return w >= 8 ? ~0ull : ((1ull << (8 * w)) - 1); }
 
 // dag_kernel's table: every per-step quantity that depends only on the micro-op (uop.h DUop).
+// The asm loop's handler for a (canonical) micro-op, and the immediate it consumes (d16-17).
+static uint32_t asm_handler(uint32_t op, uint32_t aux, uint64_t k, uint64_t& imm) {
+  const bool reg = aux & F_SRC;
+  imm = k;
+  auto pick = [&](uint32_t h_imm, uint32_t h_reg) { return reg ? h_reg : h_imm; };
+  switch (op) {
+    case U_EXIT: return H_EXIT;
+    case U_LDIMM: return H_MOV64_IMM;
+    case U_MOV64: return pick(H_MOV64_IMM, H_MOV64_REG);
+    case U_ADD64: return pick(H_ADD64_IMM, H_ADD64_REG);
+    case U_SUB64:
+      if (!reg) imm = 0 - k;  // a - k == a + (-k) mod 2^64
+      return pick(H_ADD64_IMM, H_SUB64_REG);
+    case U_AND64: return pick(H_AND64_IMM, H_AND64_REG);
+    case U_OR64: return pick(H_OR64_IMM, H_OR64_REG);
+    case U_XOR64: return pick(H_XOR64_IMM, H_XOR64_REG);
+    case U_LSH64: imm = k & 63; return pick(H_LSH64_IMM, H_LSH64_REG);
+    case U_RSH64: imm = k & 63; return pick(H_RSH64_IMM, H_RSH64_REG);
+    case U_MOV32: imm = (uint32_t)k; return pick(H_MOV32_IMM, H_MOV32_REG);
+    case U_ADD32: return pick(H_ADD32_IMM, H_ADD32_REG);
+    case U_SUB32:
+      if (!reg) imm = (uint32_t)(0u - (uint32_t)k);
+      return pick(H_ADD32_IMM, H_SUB32_REG);
+    case U_AND32: return pick(H_AND32_IMM, H_AND32_REG);
+    case U_OR32: return pick(H_OR32_IMM, H_OR32_REG);
+    case U_XOR32: return pick(H_XOR32_IMM, H_XOR32_REG);
+    case U_LSH32: imm = k & 31; return pick(H_LSH32_IMM, H_LSH32_REG);
+    case U_RSH32: imm = k & 31; return pick(H_RSH32_IMM, H_RSH32_REG);
+    case U_ZX16: return H_ZX16;
+    case U_ZX32: return H_ZX32;
+    case U_NOP: return H_NOP;
+    case U_BSWAP16: return H_BSWAP16;
+    case U_BSWAP32: return H_BSWAP32;
+    case U_BSWAP64: return H_BSWAP64;
+    case U_JA: return H_JA;
+    case U_JEQ: return pick(H_JEQ_IMM, H_JEQ_REG);
+    case U_JGT: return pick(H_JGT_IMM, H_JGT_REG);
+    case U_JLT: return pick(H_JLT_IMM, H_JLT_REG);
+    case U_JSET: return pick(H_JSET_IMM, H_JSET_REG);
+    case U_JEQ32: return pick(H_JEQ32_IMM, H_JEQ32_REG);
+    case U_JGT32: return pick(H_JGT32_IMM, H_JGT32_REG);
+    case U_JLT32: return pick(H_JLT32_IMM, H_JLT32_REG);
+    case U_JSET32: return pick(H_JSET32_IMM, H_JSET32_REG);
+    case U_LDX: imm = k; return H_LDX;  // k: the sign-extended offset (set by the caller)
+    default: return H_SLOW;  // MUL/DIV/MOD/NEG/ARSH, static faults: the C++ step
+  }
+}
+
 static std::vector<DUop> build_dag(const std::vector<Uop>& uops) {
   const uint32_t n = (uint32_t)uops.size();
   std::vector<DUop> d(n);
@@ -240,8 +291,7 @@ static std::vector<DUop> build_dag(const std::vector<Uop>& uops) {
     const Uop& u = uops[i];
     DUop& o = d[i];
     std::memset(&o, 0, sizeof o);
-    o.op = u.op;
-    o.aux = u.aux;
+    uint32_t op = u.op;
     o.doff = (uint32_t)u.dst * kRegStride;
     o.soff = (uint32_t)u.src * kRegStride;
     o.npc = i + 1 < n ? i + 1 : PC_DONE;
@@ -251,10 +301,121 @@ static std::vector<DUop> build_dag(const std::vector<Uop>& uops) {
       const uint32_t t = (uint32_t)u.x;
       o.x = t < n ? t : PC_DONE;
       o.tbit = bit(t);
+      // canonical conditions: "jump if not C" = "jump if C" with the two successors swapped
+      switch (u.op) {
+        case U_JNE: op = U_JEQ; break;
+        case U_JGE: op = U_JLT; break;
+        case U_JLE: op = U_JGT; break;
+        case U_JNE32: op = U_JEQ32; break;
+        case U_JGE32: op = U_JLT32; break;
+        case U_JLE32: op = U_JGT32; break;
+        default: break;
+      }
+      if (op != u.op) {
+        std::swap(o.x, o.npc);
+        std::swap(o.tbit, o.nbit);
+      }
     } else {
       o.x = (uint32_t)u.x;
     }
-    if (u.op == U_LDX) o.k = width_mask(u.aux);
+    o.opaux = op | ((uint32_t)u.aux << 8);
+    if (u.op == U_LDX) {
+      o.k = width_mask(u.aux);
+      o.width = u.aux;
+    }
+    const uint64_t kk = u.op == U_LDX ? (uint64_t)(int64_t)u.x : (uint64_t)u.k;
+    o.hoff = asm_handler(op, u.aux, kk, o.imm) * DAG_SLOT;
+  }
+  return d;
+}
+
+// Load-time constant propagation over a forward-only program, from the main.rs:28-31 register
+// layout (r1 = 0 = the packet's image address, r0 and r3..r9 = 0; r2 = len and r10 are
+// per-batch). Every LDX whose base register holds one known constant on all paths into it
+// becomes U_LDXK with its address resolved, so the kernel neither reads that register nor
+// waits on it before reading the packet window. Only used for batches without init_regs.
+static std::vector<DUop> fold_const_loads(const std::vector<Uop>& uops, std::vector<DUop> d) {
+  const uint32_t n = (uint32_t)uops.size();
+  struct Regs {
+    bool reached = false;
+    bool known[11] = {};
+    uint64_t v[11] = {};
+  };
+  std::vector<Regs> in(n + 1);
+  in[0].reached = true;
+  for (int r = 0; r < 11; r++) in[0].known[r] = (r != 2 && r != 10);
+  auto flow = [&](uint32_t to, const Regs& s) {
+    if (to >= n) return;
+    Regs& t = in[to];
+    if (!t.reached) {
+      t = s;
+      return;
+    }
+    for (int r = 0; r < 11; r++)
+      if (t.known[r] && !(s.known[r] && s.v[r] == t.v[r])) t.known[r] = false;
+  };
+  for (uint32_t i = 0; i < n; i++) {
+    if (!in[i].reached) continue;
+    const Uop& u = uops[i];
+    Regs s = in[i];
+    const bool src = u.aux & F_SRC;
+    if (u.op == U_LDX && s.known[u.src]) {
+      int64_t a;
+      DUop& o = d[i];
+      if (__builtin_add_overflow((int64_t)s.v[u.src], (int64_t)u.x, &a)) {
+        o.opaux = U_FAULT | (EBPF_ST_MEM << 8);  // address overflow: emu.rs:344 debug panic
+        o.hoff = H_SLOW * DAG_SLOT;
+      } else {
+        const uint64_t ua = (uint64_t)a;
+        o.opaux = U_LDXK | ((uint32_t)u.aux << 8);
+        o.addr = ua;
+        o.hoff = H_SLOW * DAG_SLOT;
+        // inside the header window (ua < kWin first: ua + width must not wrap): the asm loop
+        // reads it; an address past the window or the image runs in the C++ step
+        if (ua < (uint64_t)kWin && ua + u.aux <= (uint64_t)kWin) {
+          o.end = (uint32_t)ua + u.aux;
+          const uint32_t b0 = (uint32_t)ua & ~3u;
+          for (uint32_t w = 0; w < 3; w++) {
+            const uint32_t b = std::min(b0 + 4 * w, (uint32_t)kWin - 4);  // unused dwords: any
+            o.win[2 * w] = b & 0x30;
+            o.win[2 * w + 1] = b & 15;
+          }
+          o.hoff = H_LDXK * DAG_SLOT;
+        }
+      }
+    }
+    switch (u.op) {
+      case U_JA: case U_JEQ: case U_JGT: case U_JGE: case U_JSET: case U_JNE: case U_JLT:
+      case U_JLE: case U_JEQ32: case U_JGT32: case U_JGE32: case U_JSET32: case U_JNE32:
+      case U_JLT32: case U_JLE32:
+        flow((uint32_t)u.x, s);
+        if (u.op != U_JA) flow(i + 1, s);
+        continue;
+      case U_EXIT: case U_FAULT:
+        continue;
+      case U_MOV64:
+        s.known[u.dst] = !src || s.known[u.src];
+        s.v[u.dst] = src ? s.v[u.src] : (uint64_t)u.k;
+        break;
+      case U_MOV32:
+        s.known[u.dst] = !src || s.known[u.src];
+        s.v[u.dst] = (uint32_t)(src ? s.v[u.src] : (uint64_t)u.k);
+        break;
+      case U_LDIMM:
+        s.known[u.dst] = true;
+        s.v[u.dst] = (uint64_t)u.k;
+        break;
+      case U_ADD64:
+        s.known[u.dst] = s.known[u.dst] && (!src || s.known[u.src]);
+        s.v[u.dst] += src ? s.v[u.src] : (uint64_t)u.k;  // wrapping, emu.rs:81-83
+        break;
+      case U_NOP:
+        break;
+      default:  // every other micro-op of tier 0 writes dst with a value not tracked here
+        s.known[u.dst] = false;
+        break;
+    }
+    flow(i + 1, s);
   }
   return d;
 }
@@ -292,8 +453,10 @@ int ebpf_prog_load(const uint8_t* code, size_t nbytes, ebpf_prog** out, size_t* 
     if (u.op >= U_JA && u.op <= U_CALL && (uint32_t)u.x <= (uint32_t)i) forward = false;
   }
   p->tiny = forward && p->uops.size() <= kTinyUops;
-  if (forward && p->tier == 0 && !p->uops.empty() && p->uops.size() <= kMaxDagUops)
+  if (forward && p->tier == 0 && !p->uops.empty() && p->uops.size() <= kMaxDagUops) {
     p->duops = build_dag(p->uops);
+    p->duopsk = fold_const_loads(p->uops, p->duops);
+  }
   *out = p;
   return EBPF_OK;
 }
@@ -316,6 +479,7 @@ void ebpf_prog_free(ebpf_prog* p) {
       hipSetDevice(d);
       if (p->dev_uops[d]) hipFree(p->dev_uops[d]);
       if (p->dev_duops[d]) hipFree(p->dev_duops[d]);
+      if (p->dev_duopsk[d]) hipFree(p->dev_duopsk[d]);
     }
   }
   hipSetDevice(cur);
@@ -355,19 +519,28 @@ int ebpf_prog_upload(ebpf_prog* p, int device) {
            hipMemcpy(d, p->uops.data(), p->uops.size() * sizeof(Uop), hipMemcpyHostToDevice) !=
                hipSuccess)
     rc = EBPF_EHIP;
-  DUop* dd = nullptr;
-  if (rc == EBPF_OK && !p->duops.empty()) {
-    if (hipMalloc(&dd, p->duops.size() * sizeof(DUop)) != hipSuccess ||
-        hipMemcpy(dd, p->duops.data(), p->duops.size() * sizeof(DUop), hipMemcpyHostToDevice) !=
-            hipSuccess)
+  // dag_kernel tables, each with one zeroed padding entry past the end (the kernel prefetches
+  // the micro-op after each one)
+  auto put = [&](const std::vector<DUop>& t, DUop** dst) {
+    const size_t nb = t.size() * sizeof(DUop);
+    if (rc != EBPF_OK || t.empty()) return;
+    if (hipMalloc(dst, nb + sizeof(DUop)) != hipSuccess ||
+        hipMemset(*dst, 0, nb + sizeof(DUop)) != hipSuccess ||
+        hipMemcpy(*dst, t.data(), nb, hipMemcpyHostToDevice) != hipSuccess)
       rc = EBPF_EHIP;
-  }
+  };
+  DUop* dd = nullptr;
+  DUop* ddk = nullptr;
+  put(p->duops, &dd);
+  put(p->duopsk, &ddk);
   if (rc == EBPF_OK) {
     p->dev_uops[device] = d;
     p->dev_duops[device] = dd;
+    p->dev_duopsk[device] = ddk;
   } else {
     if (d) hipFree(d);
     if (dd) hipFree(dd);
+    if (ddk) hipFree(ddk);
   }
   hipSetDevice(cur);
   return rc;
@@ -457,7 +630,8 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* b, const ebpf_batch_out* out,
   }
   LaunchArgs a{};
   a.prog = p->dev_uops[device];
-  a.dprog = p->dev_duops[device];
+  // constant-address loads are resolved for the main.rs register layout only
+  a.dprog = b->init_regs ? p->dev_duops[device] : p->dev_duopsk[device];
   a.n_uops = (uint32_t)p->uops.size();
   a.mem_size = b->mem_size;
   a.frames = b->frames;

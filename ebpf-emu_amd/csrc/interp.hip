@@ -27,6 +27,7 @@
 #include <tuple>
 
 #include "../../include/ebpf_emu.h"
+#include "dag_asm.h"
 #include "launch.h"
 #include "uop.h"
 
@@ -263,6 +264,27 @@ __device__ __forceinline__ void dma_window(const LaunchArgs& a, const WaveLds& L
     const uint32_t c = (lane & 3) ^ win_swz(j);
     const uintptr_t src = (c * 16 < lj) ? bj + c * 16 : (uintptr_t)a.prog;
     dma_x4(src, lds_addr(L.win + wb * kWinBytes + r * 1024));
+  }
+}
+
+// Stride layout with 16-byte aligned slots of >= kWin bytes: every packet's whole window is
+// inside its slot (the C ABI requires n * stride bytes of frames), so tile t's windows can be
+// DMA'd without its lengths -- i.e. in the same HBM round trip as the lengths. Bytes past a
+// packet's length are masked when read.
+__device__ __forceinline__ bool stride_windows(const LaunchArgs& a) {
+  return a.offsets == nullptr && a.stride >= (uint64_t)kWin &&
+         (((uintptr_t)a.frames | (uintptr_t)a.stride) & 15) == 0;
+}
+__device__ __forceinline__ void dma_window_stride(const LaunchArgs& a, uint8_t* win, uint64_t t,
+                                                  uint32_t lane) {
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const uint32_t j = r * 16 + (lane >> 2);
+    const uint64_t pkt = t * kWave + j;
+    const uint32_t c = (lane & 3) ^ win_swz(j);
+    const uintptr_t src =
+        pkt < a.n ? (uintptr_t)a.frames + pkt * a.stride + c * 16 : (uintptr_t)a.prog;
+    dma_x4(src, lds_addr(win + r * 1024));
   }
 }
 
@@ -761,12 +783,37 @@ constexpr uint32_t kDagWaveLds = kRegBytes + kWinBytes + kDagMetaBytes;  // 10 K
 
 typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
 
-// One DUop (64 B) from the device table into SGPRs.
+// The first 16 dwords of a DUop (the fields the C++ step reads) from the device table.
 __device__ __forceinline__ u32x16 load_duop(const DUop* prog, uint32_t pc) {
   u32x16 v;
-  asm("s_load_dwordx16 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)"
+  asm volatile("s_load_dwordx16 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)"
       : "=s"(v) : "s"(prog), "s"(pc * (uint32_t)sizeof(DUop)));
   return v;
+}
+
+// The hand-written interpreter loop (dag_loop.inc, generated by gen_dag_loop.py; contract in its
+// header). Runs until every lane is done (returns PC_DONE) or the lowest live pc holds a
+// micro-op it leaves to the C++ step (returns that pc, already removed from `live`). Programs of
+// <= 64 micro-ops (one-word pc set). exec is the whole wave at entry and is restored at exit.
+__device__ __forceinline__ uint32_t dag_loop_asm(uint64_t& live, uint32_t& lpc, uint32_t& nsteps,
+                                                 const DUop* prog, uint32_t rl, uint32_t win,
+                                                 uint32_t swz16, uint32_t len, uint32_t mem_size) {
+  uint32_t P;
+  // hipcc's divergence analysis cannot prove the pc set uniform across the C++ step's control
+  // flow; it is (every update is a ballot or an SGPR), so re-assert that at the boundary
+  live = (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)live) |
+         ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(live >> 32)) << 32);
+  asm volatile(
+#include "dag_loop.inc"
+      : [live] "+s"(live), [lpc] "+v"(lpc), [nst] "+v"(nsteps), [P] "=&s"(P)
+      : [prog] "s"(prog), [rl] "v"(rl), [win] "v"(win), [swz] "v"(swz16), [len] "v"(len),
+        [mem] "s"(mem_size)
+      : "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71", "s72", "s73", "s74", "s75",
+        "s76", "s77", "s78", "s79", "s80", "s81", "s82", "s83", "s84", "s85", "s86", "s87",
+        "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95", "s96", "s97", "s98", "s99",
+        "s62", "s63", "v80", "v81", "v82", "v83", "v84", "v85", "v86", "v87", "v88", "v89",
+        "v90", "v91", "v92", "v93", "v94", "v95", "vcc", "scc", "memory");
+  return P;
 }
 
 __device__ __forceinline__ uint64_t rget(const uint8_t* rl, uint32_t off) {
@@ -776,7 +823,7 @@ __device__ __forceinline__ void rset(uint8_t* rl, uint32_t off, uint64_t v) {
   *(uint64_t*)(rl + off) = v;
 }
 
-template <int NW>
+template <int NW, int V = 11>
 __global__ __launch_bounds__(kBlock) void dag_kernel(LaunchArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t lane = threadIdx.x & (kWave - 1);
@@ -799,16 +846,19 @@ __global__ __launch_bounds__(kBlock) void dag_kernel(LaunchArgs a) {
   for (uint64_t tile = wave_slot; tile < a.n_tiles; tile += total_waves) {
     const uint64_t pkt = tile * kWave + lane;
     const bool valid = pkt < a.n;
-    // ---- header windows (as interp_kernel's single-buffered tier 0) ----
+    // ---- header windows: with stride slots, windows and lengths in one round trip; else as
+    //      interp_kernel's single-buffered tier 0 (lengths/offsets first) ----
+    const bool sw = (V & 1) && stride_windows(a);
     dma_meta(a, L, 0, tile, lane);
+    if (sw) dma_window_stride(a, L.win, tile, lane);
     dma_wait();
     uintptr_t mb;
     uint32_t ml;
     meta_of(a, L, 0, tile, lane, mb, ml);
     const uint8_t* const base = (const uint8_t*)mb;
     const uint32_t len = valid ? ml : 0u;
-    const bool co = ballot(valid && ml != 0 && (mb & 15) != 0) == 0;
-    if (co) dma_window(a, L, 0, 0, tile, lane);
+    const bool co = sw || ballot(valid && ml != 0 && (mb & 15) != 0) == 0;
+    if (co && !sw) dma_window(a, L, 0, 0, tile, lane);
 
     // ---- Emu::default() + main.rs:14-31 register layout (or caller-set regs) ----
     if (a.init_regs) {
@@ -826,26 +876,45 @@ __global__ __launch_bounds__(kBlock) void dag_kernel(LaunchArgs a) {
       st = EBPF_ST_BADPKT;
       lpc = PC_DONE;
     }
-    if (co) dma_wait();
-    else stage_window_lane(my_win, my_swz, base, len, valid);
+    if (co) {
+      if (!sw) dma_wait();
+    } else {
+      stage_window_lane(my_win, my_swz, base, len, valid);
+    }
 
     // ---- Emu::run (emu.rs:452-458): lowest parked pc first ----
     PcSet<NW> live;
     live.init(ballot(lpc == 0) != 0);
+    const uint32_t rl_lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)rl;
+    const uint32_t win_lds =
+        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)my_win;
     for (;;) {
-      const uint32_t P = live.first();
-      if (P == PC_DONE) break;
-      live.del(P);
+      uint32_t P;
+      if (NW == 1 && (V & 8)) {
+        // the common micro-ops run in the hand-written loop; it returns here for the others
+        P = dag_loop_asm(live.w0, lpc, nsteps, a.dprog, rl_lds, win_lds, my_swz << 4, len,
+                         mem_size);
+        if (P == PC_DONE) break;
+      } else {
+        P = live.first();
+        if (P == PC_DONE) break;
+        live.del(P);
+      }
       const u32x16 q = load_duop(a.dprog, P);
-      const uint32_t op = q[0], aux = q[1], doff = q[2], soff = q[3], npc = q[4], x = q[5];
-      const uint64_t k = (uint64_t)q[8] | ((uint64_t)q[9] << 32);
-      const uint64_t nbit = (uint64_t)q[10] | ((uint64_t)q[11] << 32);
-      const uint64_t tbit = (uint64_t)q[12] | ((uint64_t)q[13] << 32);
+      const uint32_t op = q[1] & 0xff, aux = q[1] >> 8, doff = q[2], soff = q[3], npc = q[4];
+      const uint32_t x = q[5];
+      const uint64_t k = (uint64_t)q[6] | ((uint64_t)q[7] << 32);
+      const uint64_t nbit = (uint64_t)q[8] | ((uint64_t)q[9] << 32);
+      const uint64_t tbit = (uint64_t)q[10] | ((uint64_t)q[11] << 32);
       const bool act = lpc == P;
       const uint64_t A = rget(rl, doff);
       const uint64_t S = rget(rl, soff);
-      const uint64_t B = (aux & F_SRC) ? S : k;
-      const uint32_t a32 = (uint32_t)A, b32 = (uint32_t)B;
+      // operand B and the low words are formed inside each handler, after the dispatch, so the
+      // register reads above are in flight while the scalar unit walks the dispatch tree
+      const uint64_t Bearly = (V & 2) ? 0ull : ((aux & F_SRC) ? S : k);
+#define B ((V & 2) ? ((aux & F_SRC) ? S : k) : Bearly)
+#define a32 ((uint32_t)A)
+#define b32 ((uint32_t)B)
       uint64_t R;
       bool cnd;
       switch (op) {
@@ -905,22 +974,17 @@ __global__ __launch_bounds__(kBlock) void dag_kernel(LaunchArgs a) {
         case U_BSWAP32: R = bswap32(a32); goto alu;
         case U_BSWAP64: R = ((uint64_t)bswap32(a32) << 32) | bswap32((uint32_t)(A >> 32)); goto alu;
         case U_LDIMM: R = k; goto alu;
-        // ---- JMP: signed orderings (Q2); JMP32 on sign-extended low words (Q3) ----
+        // ---- JMP: signed orderings (Q2); JMP32 on sign-extended low words (Q3). The host
+        //      rewrote JNE/JGE/JLE as JEQ/JLT/JGT with swapped successors (build_dag). ----
         case U_JA: cnd = true; goto jump;
         case U_JEQ: cnd = A == B; goto jump;
         case U_JGT: cnd = (int64_t)A > (int64_t)B; goto jump;
-        case U_JGE: cnd = (int64_t)A >= (int64_t)B; goto jump;
         case U_JSET: cnd = (A & B) != 0; goto jump;
-        case U_JNE: cnd = A != B; goto jump;
         case U_JLT: cnd = (int64_t)A < (int64_t)B; goto jump;
-        case U_JLE: cnd = (int64_t)A <= (int64_t)B; goto jump;
         case U_JEQ32: cnd = a32 == b32; goto jump;
         case U_JGT32: cnd = (int32_t)a32 > (int32_t)b32; goto jump;
-        case U_JGE32: cnd = (int32_t)a32 >= (int32_t)b32; goto jump;
         case U_JSET32: cnd = (a32 & b32) != 0; goto jump;
-        case U_JNE32: cnd = a32 != b32; goto jump;
         case U_JLT32: cnd = (int32_t)a32 < (int32_t)b32; goto jump;
-        case U_JLE32: cnd = (int32_t)a32 <= (int32_t)b32; goto jump;
         case U_EXIT:  // emu.rs:273-279 with an empty frame stack: stop
           lpc = act ? PC_DONE : lpc;
           nsteps += act ? 1u : 0u;
@@ -954,11 +1018,36 @@ __global__ __launch_bounds__(kBlock) void dag_kernel(LaunchArgs a) {
           }
           continue;
         }
+        case U_LDXK: {  // LDX at a load-time constant address (host.cpp fold_const_loads)
+          const uint64_t ua = (uint64_t)q[12] | ((uint64_t)q[13] << 32);
+          const bool oob = ua >= mem_size;
+          if (oob || ua + aux > mem_size) {  // uniform: every active lane faults alike
+            st = act ? (oob ? (uint32_t)EBPF_ST_MEM : (uint32_t)EBPF_ST_MEM_UB) : st;
+            lpc = act ? PC_DONE : lpc;
+            continue;
+          }
+          const uint32_t a0 = (uint32_t)ua;
+          uint64_t v = 0;
+          if (a0 + aux <= (uint32_t)kWin) {
+            v = win_read(my_win, my_swz, a0, aux, len);
+            v = a0 < len ? v : 0ull;
+          } else {
+            const bool far = act && a0 < len;
+            if (ballot(far) != 0) {
+              if (far) v = pkt_read(base, a0, aux, len);
+            }
+          }
+          R = (A & ~k) | v;
+          goto alu;
+        }
         default:  // U_FAULT (static faults; tier-1 kinds never reach this kernel)
           st = act ? (op == U_FAULT ? aux : (uint32_t)EBPF_ST_INSN) : st;
           lpc = act ? PC_DONE : lpc;
           continue;
       }
+#undef B
+#undef a32
+#undef b32
     alu:
       rset(rl, doff, act ? R : A);
       lpc = act ? npc : lpc;
@@ -1050,9 +1139,19 @@ static const void* variant(uint32_t n_uops) {
   return (const void*)interp_kernel<TIER, false, 0, DB>;
 }
 
+// A/B switch (EBPFEMU_DAG_VARIANT): dag_kernel feature bits -- 1 windows and lengths in one
+// DMA round trip, 2 operand B formed after the dispatch, 8 the hand-written loop
+static int g_dag_variant = [] {
+  const char* e = getenv("EBPFEMU_DAG_VARIANT");
+  return e ? atoi(e) : 11;
+}();
+
 static const void* kernel_for(int kind, uint32_t n_uops) {
-  if (kind == kKindDag)
-    return n_uops <= 64 ? (const void*)dag_kernel<1> : (const void*)dag_kernel<4>;
+  if (kind == kKindDag) {
+    if (n_uops > 64) return (const void*)dag_kernel<4, 3>;
+    // 11: the hand-written loop + the C++ step for the rest (default); 3: the C++ step only
+    return g_dag_variant == 3 ? (const void*)dag_kernel<1, 3> : (const void*)dag_kernel<1, 11>;
+  }
   if (kind == kKindTier1) return variant<1, false>(n_uops);
   return g_db ? variant<0, true>(n_uops) : variant<0, false>(n_uops);
 }

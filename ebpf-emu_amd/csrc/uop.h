@@ -48,7 +48,10 @@ enum UopKind : uint8_t {
   U_STX,    // mem[dst + x] <- low aux bytes of src
   U_ATOMIC, // 8-byte RMW at dst + x; k = imm & 0xfe (or 0xff = unknown -> fault after the read)
   U_FAULT,  // aux = EBPF_ST_* raised when executed
-  U_NKINDS
+  U_NKINDS,
+  // dag_kernel only: LDX whose base register holds the same known constant on every path
+  // (load-time dataflow, default register layout); DUop::addr = that constant + offset
+  U_LDXK = U_NKINDS
 };
 
 constexpr uint32_t PC_DONE = 0xFFFFFFFFu;
@@ -58,20 +61,28 @@ constexpr uint32_t kRegStride = 64 * 8;
 
 // Micro-op of the DAG kernel (tier-0 programs whose jumps all go forward, dag_kernel in
 // interp.hip): a Uop with everything the kernel would otherwise compute per step resolved at
-// load time, fetched by ONE scalar load (s_load_dwordx16) straight into SGPRs.
-struct alignas(64) DUop {
-  uint32_t op;    // UopKind
-  uint32_t aux;   // as Uop::aux
-  uint32_t doff;  // dst * kRegStride
-  uint32_t soff;  // src * kRegStride
-  uint32_t npc;   // pc + 1, or PC_DONE when that falls off the end (a normal stop, emu.rs:452)
-  uint32_t x;     // jump target (PC_DONE past the end) or LDX offset (sign-extended i16)
-  uint32_t pad0, pad1;
-  uint64_t k;     // immediate (ALU/JMP/LDIMM); LDX: mask of the access width's low bytes
-  uint64_t nbit;  // 1 << npc in the pc set of programs of <= 64 micro-ops (0 for PC_DONE)
-  uint64_t tbit;  // 1 << x likewise, for jumps
-  uint64_t pad2;
+// load time, fetched by scalar loads straight into SGPRs. Dword i lands in s[64 + i] of the
+// hand-written loop (dag_asm.h); the C++ step reads the first 16 dwords.
+struct alignas(128) DUop {
+  uint32_t hoff;    // d0: asm handler slot offset (dag_asm.h id * DAG_SLOT)
+  uint32_t opaux;   // d1: UopKind | aux << 8
+  uint32_t doff;    // d2: dst * kRegStride
+  uint32_t soff;    // d3: src * kRegStride
+  uint32_t npc;     // d4: pc + 1, or PC_DONE when that falls off the end (a normal stop)
+  uint32_t x;       // d5: jump target (PC_DONE past the end) or LDX offset (sign-extended i16)
+  uint64_t k;       // d6-7: immediate (ALU/JMP/LDIMM); LDX/LDXK: mask of the access width
+  uint64_t nbit;    // d8-9: 1 << npc in the pc set of programs of <= 64 micro-ops (0: PC_DONE)
+  uint64_t tbit;    // d10-11: 1 << x likewise, for jumps
+  uint64_t addr;    // d12-13: U_LDXK: the absolute image address
+  uint32_t width;   // d14: LDX/LDXK access width
+  uint32_t end;     // d15: U_LDXK: addr + width (scalar bounds check)
+  // ---- asm-only operands (the C++ step never reads these) ----
+  uint64_t imm;     // d16-17: the immediate as the handler consumes it (negated for SUB, masked
+                    //         shift count); H_LDX: the sign-extended offset
+  uint32_t win[6];  // d18-23: H_LDXK window dwords i = 0..2 of the access: {chunk bits (b & 0x30),
+                    //         byte-in-chunk (b & 15)} of dword address b, for the lane swizzle
+  uint32_t pad[8];
 };
-static_assert(sizeof(DUop) == 64, "DUop must be 64 bytes");
+static_assert(sizeof(DUop) == 128, "DUop must be 128 bytes");
 
 }  // namespace ebpfemu

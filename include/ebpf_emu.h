@@ -80,7 +80,8 @@ typedef struct ebpf_batch {
   const uint8_t* frames;    /* packet bytes */
   const uint32_t* offsets;  /* packet i at frames + offsets[i]; NULL => frames + i*stride */
   const uint16_t* lens;     /* packet i length; NULL => stride */
-  uint64_t stride;          /* bytes between packets in the stride layout */
+  uint64_t stride;          /* bytes between packets in the stride layout, where frames must hold
+                               n * stride bytes (every slot whole, as in a ring of fixed slots) */
   uint64_t n;               /* packets */
   uint32_t mem_size;        /* bytes of the per-packet memory image (multiple of 8, >= 8) */
   uint32_t flags;           /* 0, or EBPF_BATCH_GENERIC */

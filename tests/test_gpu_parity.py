@@ -178,6 +178,38 @@ def test_forward_only_wide_pc_set(cuda, oracle_mod, pad):
         _check_against_oracle(oracle_mod, img, pkts, got, tag=f"pad {pad} it {it}")
 
 
+CONST_LOAD_PROGRAMS = [
+    "mov r1, 8\nldxb r0, [r1+2]\nexit",                                   # rebased constant
+    "jeq r2, 60, +2\nmov r1, 4\nja +1\nmov r1, 6\nldxb r0, [r1+0]\nexit",  # join, differs
+    "jeq r2, 60, +2\nmov r1, 4\nja +1\nmov r1, 4\nldxh r0, [r1+1]\nexit",  # join, agrees
+    "lddw r1, 0x7fffffffffffffff\nldxb r0, [r1+1]\nexit",                # static overflow
+    "add r1, 20\nldxw r0, [r1+3]\nexit",                                  # add on a constant
+    "mov r1, r2\nldxb r0, [r1-1]\nexit",                                  # per-lane: not folded
+    "ldxdw r0, [r1+60]\nldxb r3, [r1+70]\nadd r0, r3\nexit",               # past the window
+    "ldxb r0, [r1+1023]\nldxh r3, [r1+1023]\nexit",                         # image end, tail UB
+    "ldxb r0, [r1-1]\nexit",                                               # negative address
+    "mov32 r1, -1\nldxb r0, [r1+0]\nexit",                                # zero-extended mov32
+    "ldxw r1, [r1+0]\nldxb r0, [r1+0]\nexit",                             # base from a load
+]
+
+
+def test_forward_only_constant_address_loads(cuda, oracle_mod):
+    """Loads whose base register is a load-time constant (resolved addresses on the fast path)
+    at the edges of the dataflow: joins, overflow, window/image ends, non-constant bases."""
+    from ebpf_emu.asm import assemble
+
+    rng = random.Random(5)
+    pkts = [bytes(rng.getrandbits(8) for _ in range(n))
+            for n in (0, 1, 3, 14, 60, 63, 64, 65, 70, 71, 200, 1024)]
+    pkts += [gen_packet(rng) for _ in range(60)]
+    for src in CONST_LOAD_PROGRAMS:
+        img = assemble(src)
+        got = _run_full(img, pkts, cuda)
+        assert got["fast"], src
+        _same_outputs(got, _run_full(img, pkts, cuda, generic=True), src)
+        _check_against_oracle(oracle_mod, img, pkts, got, tag=src)
+
+
 def test_forward_only_step_budget_falls_back(cuda, oracle_mod):
     """max_steps below the program length can bind, so the batch runs on the general
     interpreter: same statuses as the oracle with that budget."""
