@@ -215,7 +215,11 @@ def main():
                 "traffic": traffic,
                 "algo_bytes_per_launch": algo_bytes,
                 "kernel_avg_us": round(kern_avg_ms * 1e3, 3),
-                "kernel": "ebpfemu::interp_kernel<0>",
+                # HIP events bracket one whole batch: the interpreter kernel plus, with counters,
+                # the one-workgroup fold_counters kernel (rocprofv3 lists both)
+                "kernel": ("ebpfemu::dag_kernel" if prog.forward_only
+                           else f"ebpfemu::interp_kernel<{prog.tier}>")
+                          + ("" if args.no_counters else " + ebpfemu::fold_counters"),
             },
             "counters": {"drop": cnt[1], "pass": cnt[2], "other": cnt[5], "faults": cnt[6],
                          "insns_retired": cnt[7]},
