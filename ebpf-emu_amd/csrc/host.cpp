@@ -322,7 +322,15 @@ static std::vector<DUop> build_dag(const std::vector<Uop>& uops) {
     if (u.op == U_LDX) {
       o.k = width_mask(u.aux);
       o.width = u.aux;
+      o.kmask = o.k;
     }
+    // the hand-written loop's half
+    o.dst2 = 2u * u.dst;
+    o.src2 = 2u * u.src;
+    o.anpc = o.npc;
+    o.ax = o.x;
+    o.anbit = o.nbit;
+    o.atbit = o.tbit;
     const uint64_t kk = u.op == U_LDX ? (uint64_t)(int64_t)u.x : (uint64_t)u.k;
     o.hoff = asm_handler(op, u.aux, kk, o.imm) * DAG_SLOT;
   }
@@ -369,6 +377,7 @@ static std::vector<DUop> fold_const_loads(const std::vector<Uop>& uops, std::vec
         const uint64_t ua = (uint64_t)a;
         o.opaux = U_LDXK | ((uint32_t)u.aux << 8);
         o.addr = ua;
+        o.a0 = (uint32_t)ua;
         o.hoff = H_SLOW * DAG_SLOT;
         // inside the header window (ua < kWin first: ua + width must not wrap): the asm loop
         // reads it; an address past the window or the image runs in the C++ step

@@ -783,11 +783,11 @@ constexpr uint32_t kDagWaveLds = kRegBytes + kWinBytes + kDagMetaBytes;  // 10 K
 
 typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
 
-// The first 16 dwords of a DUop (the fields the C++ step reads) from the device table.
+// The C++ step's half of a DUop (dwords 32..47) from the device table.
 __device__ __forceinline__ u32x16 load_duop(const DUop* prog, uint32_t pc) {
   u32x16 v;
   asm volatile("s_load_dwordx16 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)"
-      : "=s"(v) : "s"(prog), "s"(pc * (uint32_t)sizeof(DUop)));
+      : "=s"(v) : "s"(prog), "s"(pc * (uint32_t)sizeof(DUop) + (uint32_t)offsetof(DUop, opaux)));
   return v;
 }
 
@@ -811,8 +811,10 @@ __device__ __forceinline__ uint32_t dag_loop_asm(uint64_t& live, uint32_t& lpc, 
       : "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71", "s72", "s73", "s74", "s75",
         "s76", "s77", "s78", "s79", "s80", "s81", "s82", "s83", "s84", "s85", "s86", "s87",
         "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95", "s96", "s97", "s98", "s99",
-        "s62", "s63", "v80", "v81", "v82", "v83", "v84", "v85", "v86", "v87", "v88", "v89",
-        "v90", "v91", "v92", "v93", "v94", "v95", "vcc", "scc", "memory");
+        "s62", "s63", "v82", "v83", "v84", "v85", "v86", "v87", "v88", "v89", "v90", "v91",
+        "v92", "v93", "v94", "v95", "v96", "v97", "v98", "v99", "v100", "v101", "v102", "v103",
+        "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111", "v112", "v113", "v114",
+        "v115", "v116", "v117", "vcc", "scc", "memory");
   return P;
 }
 
@@ -901,8 +903,8 @@ __global__ __launch_bounds__(kBlock) void dag_kernel(LaunchArgs a) {
         live.del(P);
       }
       const u32x16 q = load_duop(a.dprog, P);
-      const uint32_t op = q[1] & 0xff, aux = q[1] >> 8, doff = q[2], soff = q[3], npc = q[4];
-      const uint32_t x = q[5];
+      const uint32_t op = q[0] & 0xff, aux = q[0] >> 8, doff = q[1], soff = q[2], npc = q[3];
+      const uint32_t x = q[4];
       const uint64_t k = (uint64_t)q[6] | ((uint64_t)q[7] << 32);
       const uint64_t nbit = (uint64_t)q[8] | ((uint64_t)q[9] << 32);
       const uint64_t tbit = (uint64_t)q[10] | ((uint64_t)q[11] << 32);
@@ -1019,7 +1021,7 @@ __global__ __launch_bounds__(kBlock) void dag_kernel(LaunchArgs a) {
           continue;
         }
         case U_LDXK: {  // LDX at a load-time constant address (host.cpp fold_const_loads)
-          const uint64_t ua = (uint64_t)q[12] | ((uint64_t)q[13] << 32);
+          const uint64_t ua = (uint64_t)q[12] | ((uint64_t)q[13] << 32);  // DUop::addr
           const bool oob = ua >= mem_size;
           if (oob || ua + aux > mem_size) {  // uniform: every active lane faults alike
             st = act ? (oob ? (uint32_t)EBPF_ST_MEM : (uint32_t)EBPF_ST_MEM_UB) : st;

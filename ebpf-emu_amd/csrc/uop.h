@@ -7,6 +7,7 @@
 // the sign-extended immediate, absolute jump targets, static runtime faults (reg 11, END imm,
 // callx, illegal mode/class combinations). The kernel therefore never indexes register 11.
 #pragma once
+#include <stddef.h>
 #include <stdint.h>
 
 namespace ebpfemu {
@@ -61,28 +62,41 @@ constexpr uint32_t kRegStride = 64 * 8;
 
 // Micro-op of the DAG kernel (tier-0 programs whose jumps all go forward, dag_kernel in
 // interp.hip): a Uop with everything the kernel would otherwise compute per step resolved at
-// load time, fetched by scalar loads straight into SGPRs. Dword i lands in s[64 + i] of the
-// hand-written loop (dag_asm.h); the C++ step reads the first 16 dwords.
-struct alignas(128) DUop {
-  uint32_t hoff;    // d0: asm handler slot offset (dag_asm.h id * DAG_SLOT)
-  uint32_t opaux;   // d1: UopKind | aux << 8
-  uint32_t doff;    // d2: dst * kRegStride
-  uint32_t soff;    // d3: src * kRegStride
-  uint32_t npc;     // d4: pc + 1, or PC_DONE when that falls off the end (a normal stop)
-  uint32_t x;       // d5: jump target (PC_DONE past the end) or LDX offset (sign-extended i16)
-  uint64_t k;       // d6-7: immediate (ALU/JMP/LDIMM); LDX/LDXK: mask of the access width
-  uint64_t nbit;    // d8-9: 1 << npc in the pc set of programs of <= 64 micro-ops (0: PC_DONE)
-  uint64_t tbit;    // d10-11: 1 << x likewise, for jumps
-  uint64_t addr;    // d12-13: U_LDXK: the absolute image address
-  uint32_t width;   // d14: LDX/LDXK access width
-  uint32_t end;     // d15: U_LDXK: addr + width (scalar bounds check)
-  // ---- asm-only operands (the C++ step never reads these) ----
-  uint64_t imm;     // d16-17: the immediate as the handler consumes it (negated for SUB, masked
+// load time, fetched by scalar loads straight into SGPRs. Two independent halves: dwords 0..23
+// for the hand-written loop (dword i lands in s[64 + i], dag_asm.h / gen_dag_loop.py) and dwords
+// 32..47 for the C++ step.
+struct alignas(256) DUop {
+  // ---- the hand-written loop ----
+  uint32_t hoff;    // d0: handler slot offset (dag_asm.h id * DAG_SLOT)
+  uint32_t dst2;    // d1: 2 * dst (register pair index in the loop's VGPR register file)
+  uint32_t src2;    // d2: 2 * src
+  uint32_t anpc;    // d3: pc + 1, or PC_DONE (canonical jumps: the not-taken successor)
+  uint32_t ax;      // d4: jump target, or PC_DONE past the end
+  uint32_t a0;      // d5: H_LDXK: the image address
+  uint64_t kmask;   // d6-7: H_LDX/H_LDXK: mask of the access width's low bytes
+  uint64_t anbit;   // d8-9: 1 << anpc (0 for PC_DONE)
+  uint64_t atbit;   // d10-11: 1 << ax
+  uint64_t imm;     // d12-13: the immediate as the handler consumes it (negated for SUB, masked
                     //         shift count); H_LDX: the sign-extended offset
-  uint32_t win[6];  // d18-23: H_LDXK window dwords i = 0..2 of the access: {chunk bits (b & 0x30),
+  uint32_t width;   // d14: H_LDX/H_LDXK access width
+  uint32_t end;     // d15: H_LDXK: a0 + width (scalar bounds check)
+  uint32_t win[6];  // d16-21: H_LDXK window dwords i = 0..2 of the access: {chunk bits (b & 0x30),
                     //         byte-in-chunk (b & 15)} of dword address b, for the lane swizzle
-  uint32_t pad[8];
+  uint32_t apad[10];
+  // ---- the C++ step (d32..47) ----
+  uint32_t opaux;   // UopKind | aux << 8
+  uint32_t doff;    // dst * kRegStride (LDS register file)
+  uint32_t soff;    // src * kRegStride
+  uint32_t npc;     // pc + 1, or PC_DONE when that falls off the end (a normal stop)
+  uint32_t x;       // jump target (PC_DONE past the end) or LDX offset (sign-extended i16)
+  uint32_t cpad;
+  uint64_t k;       // immediate (ALU/JMP/LDIMM); LDX/LDXK: mask of the access width
+  uint64_t nbit;    // 1 << npc in the pc set of programs of <= 64 micro-ops (0 for PC_DONE)
+  uint64_t tbit;    // 1 << x likewise, for jumps
+  uint64_t addr;    // U_LDXK: the absolute image address
+  uint32_t cpad2[16];
 };
-static_assert(sizeof(DUop) == 128, "DUop must be 128 bytes");
+static_assert(sizeof(DUop) == 256, "DUop must be 256 bytes");
+static_assert(offsetof(DUop, opaux) == 128, "the C++ half starts at dword 32");
 
 }  // namespace ebpfemu
