@@ -64,4 +64,26 @@
 #define H_JSET32_REG 54
 #define H_LDXK 55         // constant address inside the header window
 #define H_LDX 56          // register base: window fast path, anything else bails to C++
-#define H_COUNT 57
+// handled by the self-contained tile loop only (dag_tile.inc); the hybrid loop hands them to
+// its C++ step
+#define H_MUL64_IMM 57
+#define H_MUL64_REG 58
+#define H_MUL32_IMM 59
+#define H_MUL32_REG 60
+#define H_NEG64 61
+#define H_NEG32 62
+#define H_ARSH64_IMM 63
+#define H_ARSH64_REG 64
+#define H_ARSH32_IMM 65
+#define H_ARSH32_REG 66
+#define H_DIV64_IMM 67
+#define H_DIV64_REG 68
+#define H_MOD64_IMM 69
+#define H_MOD64_REG 70
+#define H_DIV32_IMM 71
+#define H_DIV32_REG 72
+#define H_MOD32_IMM 73
+#define H_MOD32_REG 74
+#define H_FAULT 75        // static fault: status in the immediate
+#define H_LDXK_FAR 76     // constant address not inside the header window
+#define H_COUNT 77

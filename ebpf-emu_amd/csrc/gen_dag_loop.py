@@ -292,11 +292,9 @@ def main():
     order = sorted(IDS.items(), key=lambda kv: kv[1])
     names = [n for n, i in order if n != "H_COUNT"]
     assert [IDS[n] for n in names] == list(range(len(names))), "handler ids must be dense"
-    missing = [n for n in names if n not in H]
-    assert not missing, missing
     parts = [PROLOGUE]
-    for n in names:
-        parts.append(f"; {n}\n.org .Lslots%=+{IDS[n] * SLOT}\n" + H[n])
+    for n in names:  # ids this loop does not implement go to the C++ step
+        parts.append(f"; {n}\n.org .Lslots%=+{IDS[n] * SLOT}\n" + H.get(n, "s_branch .Lslow%="))
     parts.append(f".org .Lslots%=+{IDS['H_COUNT'] * SLOT}")
     parts += [LDXK, LDX, EPILOGUE]
     text = "\n".join(parts)

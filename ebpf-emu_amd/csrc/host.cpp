@@ -279,7 +279,19 @@ static uint32_t asm_handler(uint32_t op, uint32_t aux, uint64_t k, uint64_t& imm
     case U_JLT32: return pick(H_JLT32_IMM, H_JLT32_REG);
     case U_JSET32: return pick(H_JSET32_IMM, H_JSET32_REG);
     case U_LDX: imm = k; return H_LDX;  // k: the sign-extended offset (set by the caller)
-    default: return H_SLOW;  // MUL/DIV/MOD/NEG/ARSH, static faults: the C++ step
+    // the self-contained tile loop only (the hybrid loop hands these to its C++ step)
+    case U_MUL64: return pick(H_MUL64_IMM, H_MUL64_REG);
+    case U_MUL32: imm = (uint32_t)k; return pick(H_MUL32_IMM, H_MUL32_REG);
+    case U_NEG64: return H_NEG64;
+    case U_NEG32: return H_NEG32;
+    case U_ARSH64: imm = k & 63; return pick(H_ARSH64_IMM, H_ARSH64_REG);
+    case U_ARSH32: imm = k & 31; return pick(H_ARSH32_IMM, H_ARSH32_REG);
+    case U_DIV64: return pick(H_DIV64_IMM, H_DIV64_REG);
+    case U_MOD64: return pick(H_MOD64_IMM, H_MOD64_REG);
+    case U_DIV32: imm = (uint32_t)k; return pick(H_DIV32_IMM, H_DIV32_REG);
+    case U_MOD32: imm = (uint32_t)k; return pick(H_MOD32_IMM, H_MOD32_REG);
+    case U_FAULT: imm = aux; return H_FAULT;  // aux: the status it raises
+    default: return H_SLOW;
   }
 }
 
@@ -370,19 +382,22 @@ static std::vector<DUop> fold_const_loads(const std::vector<Uop>& uops, std::vec
     if (u.op == U_LDX && s.known[u.src]) {
       int64_t a;
       DUop& o = d[i];
-      if (__builtin_add_overflow((int64_t)s.v[u.src], (int64_t)u.x, &a)) {
-        o.opaux = U_FAULT | (EBPF_ST_MEM << 8);  // address overflow: emu.rs:344 debug panic
-        o.hoff = H_SLOW * DAG_SLOT;
+      const bool ovf = __builtin_add_overflow((int64_t)s.v[u.src], (int64_t)u.x, &a);
+      if (ovf || (uint64_t)a > 0xFFFFFFF0ull) {
+        // address overflow (emu.rs:344 debug panic) or past any image (mem_size <= 2^24)
+        o.opaux = U_FAULT | (EBPF_ST_MEM << 8);
+        o.hoff = H_FAULT * DAG_SLOT;
+        o.imm = EBPF_ST_MEM;
       } else {
         const uint64_t ua = (uint64_t)a;
         o.opaux = U_LDXK | ((uint32_t)u.aux << 8);
         o.addr = ua;
         o.a0 = (uint32_t)ua;
-        o.hoff = H_SLOW * DAG_SLOT;
+        o.end = (uint32_t)ua + u.aux;
+        o.hoff = H_LDXK_FAR * DAG_SLOT;  // outside the window: global loads (tile loop only)
         // inside the header window (ua < kWin first: ua + width must not wrap): the asm loop
         // reads it; an address past the window or the image runs in the C++ step
         if (ua < (uint64_t)kWin && ua + u.aux <= (uint64_t)kWin) {
-          o.end = (uint32_t)ua + u.aux;
           const uint32_t b0 = (uint32_t)ua & ~3u;
           for (uint32_t w = 0; w < 3; w++) {
             const uint32_t b = std::min(b0 + 4 * w, (uint32_t)kWin - 4);  // unused dwords: any

@@ -1103,6 +1103,117 @@ __global__ __launch_bounds__(kBlock) void dag_kernel(LaunchArgs a) {
   flush_counters(a, cnt, retired, smem, lane, wv);
 }
 
+// ============================================================================================
+// dag_tile_kernel — the forward-only fast path with the whole tile interpreted by one hand-written
+// asm statement (dag_tile.inc, generated by gen_dag_tile.py: register file in VGPRs, every
+// tier-0 micro-op, mmu.rs faults, reads inside and past the header window). LDS holds only the
+// header windows and their metadata: 4.5 KiB per wave.
+// ============================================================================================
+constexpr uint32_t kTileWaveLds = kWinBytes + kDagMetaBytes;
+
+// Interprets this tile; returns r0 (and stores the register file to regs_out when rflag).
+__device__ __forceinline__ uint64_t dag_tile_asm(uint64_t live, uint32_t& lpc, uint32_t& nsteps,
+                                                 uint32_t& st, const LaunchArgs& a, uint32_t win,
+                                                 uint32_t swz16, uint32_t len, uint64_t base,
+                                                 uint64_t raddr, uint32_t vok) {
+  uint32_t r0l, r0h;
+  live = (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)live) |
+         ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(live >> 32)) << 32);
+  const uint32_t r10l = (uint32_t)a.r10, r10h = (uint32_t)(a.r10 >> 32);
+  const uint32_t rflag = __builtin_amdgcn_readfirstlane(a.regs_out != nullptr ? 1u : 0u);
+  asm volatile(
+#include "dag_tile.inc"
+      : [live] "+s"(live), [lpc] "+v"(lpc), [nst] "+v"(nsteps), [st] "+v"(st), [r0l] "=&v"(r0l),
+        [r0h] "=&v"(r0h)
+      : [prog] "s"(a.dprog), [mem] "s"(a.mem_size), [r10l] "s"(r10l), [r10h] "s"(r10h),
+        [initp] "s"(a.init_regs), [rflag] "s"(rflag), [win] "v"(win), [swz] "v"(swz16),
+        [len] "v"(len), [base] "v"(base), [raddr] "v"(raddr), [vok] "v"(vok)
+      : "s52", "s53", "s54", "s55", "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71", "s72", "s73", "s74", "s75", "s76", "s77", "s78", "s79", "s80", "s81", "s82", "s83", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95", "s96", "s97", "s98", "s99", "v16", "v17", "v18", "v19", "v20", "v21", "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32", "v33", "v34", "v35", "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", "v56", "v57", "v58", "v59", "v60", "v61", "v62", "v63", "vcc", "scc", "memory");
+  return (uint64_t)r0l | ((uint64_t)r0h << 32);
+}
+
+__global__ __launch_bounds__(kBlock, 5) void dag_tile_kernel(LaunchArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint32_t lane = threadIdx.x & (kWave - 1);
+  const uint32_t wv = threadIdx.x / kWave;
+  WaveLds L;
+  L.win = smem + wv * kTileWaveLds;
+  L.meta_off = (uint32_t*)(L.win + kWinBytes);
+  L.meta_len = L.meta_off + kWave;
+  const uint32_t my_swz = win_swz(lane);
+  uint8_t* const my_win = L.win + lane * kWin;
+  const uint32_t win_lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)my_win;
+  const uint64_t wave_slot = (uint64_t)blockIdx.x * kWavesPerBlock + wv;
+  const uint64_t total_waves = (uint64_t)gridDim.x * kWavesPerBlock;
+  const uint32_t mem_size = a.mem_size;
+
+  uint64_t cnt[7] = {0, 0, 0, 0, 0, 0, 0};
+  uint64_t retired = 0;
+
+  for (uint64_t tile = wave_slot; tile < a.n_tiles; tile += total_waves) {
+    const uint64_t pkt = tile * kWave + lane;
+    const bool valid = pkt < a.n;
+    // ---- header windows (as dag_kernel) ----
+    const bool sw = stride_windows(a);
+    dma_meta(a, L, 0, tile, lane);
+    if (sw) dma_window_stride(a, L.win, tile, lane);
+    dma_wait();
+    uintptr_t mb;
+    uint32_t ml;
+    meta_of(a, L, 0, tile, lane, mb, ml);
+    const uint8_t* const base = (const uint8_t*)mb;
+    const uint32_t len = valid ? ml : 0u;
+    const bool co = sw || ballot(valid && ml != 0 && (mb & 15) != 0) == 0;
+    if (co) {
+      if (!sw) {
+        dma_window(a, L, 0, 0, tile, lane);
+        dma_wait();
+      }
+    } else {
+      stage_window_lane(my_win, my_swz, base, len, valid);
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // the window's LDS writes / metadata reads: done
+
+    uint32_t lpc = valid ? 0u : PC_DONE;
+    uint32_t st = EBPF_ST_OK;
+    uint32_t nsteps = 0;
+    if (valid && len > mem_size) {  // main.rs:20-21 index panic
+      st = EBPF_ST_BADPKT;
+      lpc = PC_DONE;
+    }
+    const uint64_t live = ballot(lpc == 0) != 0 ? 1ull : 0ull;
+    const uint64_t raddr = a.regs_out ? (uint64_t)(uintptr_t)(a.regs_out + pkt * 11) : 0ull;
+    const uint64_t r0v = dag_tile_asm(live, lpc, nsteps, st, a, win_lds, my_swz << 4, len,
+                                      (uint64_t)(uintptr_t)base, raddr, valid ? 1u : 0u);
+
+    // ---- outputs: r0 (main.rs:43), status, verdict (xdp.rs:3-9), final image ----
+    if (a.mem_out && valid) {
+      uint32_t* mo = (uint32_t*)(a.mem_out + pkt * (uint64_t)mem_size);
+      const uint32_t m = min(len, mem_size);
+      for (uint32_t d = 0; d < mem_size / 4; d++) {
+        uint32_t v;
+        if (d * 4 >= m) v = 0u;
+        else if (d * 4 < (uint32_t)kWin) v = (uint32_t)win_read(my_win, my_swz, d * 4, 4, len);
+        else v = (uint32_t)pkt_read(base, d * 4, 4, len);
+        mo[d] = v;
+      }
+    }
+    if (valid) {
+      if (a.r0) a.r0[pkt] = r0v;
+      if (a.status) a.status[pkt] = (uint8_t)st;
+      if (a.verdict) a.verdict[pkt] = st ? (uint8_t)EBPF_VERDICT_FAULT
+                                         : (r0v < 5 ? (uint8_t)r0v : (uint8_t)EBPF_VERDICT_OTHER);
+    }
+    const bool okv = valid && st == EBPF_ST_OK;
+#pragma unroll
+    for (int b = 0; b < 5; b++) cnt[b] += __builtin_popcountll(ballot(okv && r0v == (uint64_t)b));
+    cnt[5] += __builtin_popcountll(ballot(okv && r0v >= 5));
+    cnt[6] += __builtin_popcountll(ballot(valid && st != EBPF_ST_OK));
+    retired += valid ? nsteps : 0u;
+  }
+  flush_counters(a, cnt, retired, smem, lane, wv);
+}
+
 // One workgroup: read-and-clear every shard (device-scope atomics, coherent across XCDs) and
 // add the per-counter sums into the caller's counters. Stream order after interp_kernel makes
 // every shard add visible here; the shards are left zeroed for the next batch.
@@ -1124,8 +1235,17 @@ static bool g_db = [] {  // tier-0 window double-buffering (EBPFEMU_TIER0_DB=0|1
   return e ? e[0] == '1' : false;
 }();
 
+// A/B switch (EBPFEMU_DAG_VARIANT): 19 dag_tile_kernel (default); dag_kernel feature bits -- 1
+// windows and lengths in one DMA round trip, 2 operand B formed after the dispatch, 8 the
+// hand-written loop with the C++ step for the micro-ops it leaves
+static int g_dag_variant = [] {
+  const char* e = getenv("EBPFEMU_DAG_VARIANT");
+  return e ? atoi(e) : 19;
+}();
+
 static uint32_t lds_bytes_for(int kind, uint32_t n_uops) {
-  if (kind == kKindDag) return kWavesPerBlock * kDagWaveLds;  // program is fetched by SMEM
+  if (kind == kKindDag)  // the program is fetched by SMEM
+    return kWavesPerBlock * (n_uops <= 64 && g_dag_variant == 19 ? kTileWaveLds : kDagWaveLds);
   const uint32_t prog = n_uops <= (uint32_t)kMaxLdsUops ? n_uops * (uint32_t)sizeof(Uop) : 0u;
   uint32_t rest = kind == kKindTier0 ? kWavesPerBlock * wave_lds0(g_db) : 0u;
   if (rest < kWavesPerBlock * 8 * 8) rest = kWavesPerBlock * 8 * 8;  // counter reduction scratch
@@ -1141,18 +1261,16 @@ static const void* variant(uint32_t n_uops) {
   return (const void*)interp_kernel<TIER, false, 0, DB>;
 }
 
-// A/B switch (EBPFEMU_DAG_VARIANT): dag_kernel feature bits -- 1 windows and lengths in one
-// DMA round trip, 2 operand B formed after the dispatch, 8 the hand-written loop
-static int g_dag_variant = [] {
-  const char* e = getenv("EBPFEMU_DAG_VARIANT");
-  return e ? atoi(e) : 11;
-}();
+
 
 static const void* kernel_for(int kind, uint32_t n_uops) {
   if (kind == kKindDag) {
     if (n_uops > 64) return (const void*)dag_kernel<4, 3>;
-    // 11: the hand-written loop + the C++ step for the rest (default); 3: the C++ step only
-    return g_dag_variant == 3 ? (const void*)dag_kernel<1, 3> : (const void*)dag_kernel<1, 11>;
+    // 19: the self-contained tile loop (default); 11: the hand-written loop with a C++ step
+    // for the rest; 3: the C++ step only
+    if (g_dag_variant == 3) return (const void*)dag_kernel<1, 3>;
+    if (g_dag_variant == 11) return (const void*)dag_kernel<1, 11>;
+    return (const void*)dag_tile_kernel;
   }
   if (kind == kKindTier1) return variant<1, false>(n_uops);
   return g_db ? variant<0, true>(n_uops) : variant<0, false>(n_uops);
