@@ -215,11 +215,10 @@ def main():
                 "traffic": traffic,
                 "algo_bytes_per_launch": algo_bytes,
                 "kernel_avg_us": round(kern_avg_ms * 1e3, 3),
-                # HIP events bracket one whole batch: the interpreter kernel plus, with counters,
-                # the one-workgroup fold_counters kernel (rocprofv3 lists both)
+                # HIP events bracket one whole batch: one interpreter launch (with counters, its
+                # last workgroup folds the per-shard sums into them)
                 "kernel": (("ebpfemu::dag_tile_kernel" if len(prog) <= 64 else "ebpfemu::dag_kernel")
-                           if prog.forward_only else f"ebpfemu::interp_kernel<{prog.tier}>")
-                          + ("" if args.no_counters else " + ebpfemu::fold_counters"),
+                           if prog.forward_only else f"ebpfemu::interp_kernel<{prog.tier}>"),
             },
             "counters": {"drop": cnt[1], "pass": cnt[2], "other": cnt[5], "faults": cnt[6],
                          "insns_retired": cnt[7]},

@@ -1,0 +1,834 @@
+#!/usr/bin/env python3
+"""Generates tile.inc + tile_ids.h: the gfx950 interpreter of one tile (64 packets, one per lane)
+of a forward-only tier-0 program, as ONE inline-asm statement (tile_kernel in interp.hip).
+
+What the statement does, between the C++ header-window DMA and the counter ballots:
+  * prologue: per-lane packet address / length (FIXED stride layout, or the LDS metadata the
+    C++ prologue DMA'd), validity, the main.rs:14-31 register layout (or the caller's
+    init_regs), the ST_BADPKT check (main.rs:20-21), the pc set;
+  * the interpreter: the lowest pc with a parked lane runs next ("min-pc" re-convergence,
+    forward jumps only, so each pc runs at most once per tile). Dispatch = one s_load_dwordx16
+    of the micro-op (uop.h TUop, 64 bytes) + s_setpc into fixed 256-byte handler slots;
+    exec is narrowed to the lanes parked at the pc (v_cmpx) and results are committed under it;
+  * basic-block chaining: a micro-op whose successor is not a block start (no jump lands there)
+    has a chained form that loads its successor and jumps straight to it, skipping the pc-set
+    update and the min-pc search; only block-ending micro-ops touch the pc set;
+  * register file r0..r10 in v[0:21], accessed IN PLACE under s_set_gpr_idx (the dst/src
+    register is scalar: dst2/src2 of the micro-op);
+  * every tier-0 micro-op kind (ALU incl. MUL, DIV/MOD by a bit-serial divider, NEG, the
+    reference's ARSH with its overflow fault; END; canonical jumps; LDX with the mmu.rs bounds
+    checks, reads in the LDS header window and past it; static faults);
+  * epilogue: verdict / r0 / status / final registers stored for the valid lanes; outputs the
+    lane's counter bucket (0..4 r0, 5 other, 6 fault, 7 not a packet) and retired steps.
+The DONE sentinel: bit 63 of the pc set is always set and micro-op 63 is the DONE handler, so
+the min-pc search needs no empty-set test (programs of <= 63 micro-ops).
+
+Only SALU/VALU/DS/SMEM, VGPR index mode and plain global loads/stores on VGPR addresses: no
+readlane, DPP, trans, SDWA or VALU-written SGPRs feeding VMEM, so no gfx950 software wait states
+are needed inside (MI355X guide §5.7 item 2); M0 is saved on entry and restored on exit.
+
+  python3 gen_tile.py           # writes tile.inc and tile_ids.h next to this file
+  python3 gen_tile.py --clobbers
+"""
+import os
+import re
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+IDS_OLD = {m.group(1): int(m.group(2)) for m in re.finditer(
+    r"#define (H_\w+) (\d+)", open(os.path.join(HERE, "dag_asm.h")).read())}
+SLOT = 256
+
+# status codes (include/ebpf_emu.h)
+ST_MEM, ST_MEM_UB, ST_INSN, ST_ARITH, ST_BADPKT = 1, 2, 3, 4, 7
+
+NVGPR = 56  # v[0:55] belong to the statement (clobbered)
+# s[33:70] belong to the statement: within the 72 SGPRs of 8 waves per SIMD, and clear of s32 (the
+# ABI stack pointer). The micro-op is s[36:51] (s_load_dwordx16 needs a 4-aligned destination).
+UB = 36
+
+
+def u(i, n=1):
+    return f"s{UB + i}" if n == 1 else f"s[{UB + i}:{UB + i + n - 1}]"
+
+
+M = {
+    # TUop, dword i in s[UB + i] (uop.h)
+    "HOFF": u(0), "DST2": u(1), "SRC2": u(2), "NPC": u(3), "X": u(4), "A0": u(5),
+    "KML": u(6), "KMH": u(7), "NBIT": u(8, 2), "TBIT": u(10, 2),
+    "IMM": u(12, 2), "IMML": u(12), "IMMH": u(13), "WID": u(14), "END": u(15),
+    "UOP": u(0, 16),
+    # LDXK window dwords (overlaying fields LDXK does not use)
+    "W0": u(2), "W1": u(4), "W2": u(10), "W3": u(11), "W4": u(12), "W5": u(13),
+    # divider: its mode lives in the (dead after dispatch) handler offset
+    "MODE": u(0),
+    # prologue / epilogue scratch inside the micro-op registers
+    "KFR": u(0, 2), "KST": u(2, 2), "KSTL": u(2), "KSTH": u(3), "KN": u(4, 2),
+    "KOFF": u(6, 2), "KLEN": u(8, 2), "KINIT": u(10, 2), "KR10": u(12, 2),
+    "KR10L": u(12), "KR10H": u(13),
+    "EV": u(0, 2), "ER0": u(2, 2), "EST": u(4, 2), "ERG": u(6, 2),
+    "KMEM": "s33", "T3": "s34", "CNT": "s34", "M0S": "s35",
+    "LIVE": "s[52:53]", "PROG": "s[54:55]", "PROGL": "s54", "PROGH": "s55",
+    "SLOTB": "s[56:57]", "SLOTBL": "s56", "SLOTBH": "s57", "VM": "s[58:59]",
+    "T0": "s[60:61]", "T1": "s[62:63]", "T4": "s[64:65]", "T5": "s[66:67]", "T7": "s[68:69]",
+    "PCOFF": "s70",
+    # the jump target and the dispatcher's pc use temporaries dead at that point
+    "JT": "s[60:61]", "JTL": "s60", "JTH": "s61", "P": "s62",
+    # every wave of the kernel is full: the statement runs with exec = all 64 lanes
+    "EXEC0": "-1",
+    # VGPRs: the register file r_i = v[2i : 2i+1] is v[0:21]
+    "RF": "v[0:1]", "RF0": "v0", "RF1": "v1",
+    "A": "v[22:23]", "AL": "v22", "AH": "v23",
+    "S": "v[24:25]", "SL": "v24", "SH": "v25",
+    "R": "v[26:27]", "RL": "v26", "RH": "v27",
+    "LPC": "v28", "NST": "v29", "ST": "v30", "LEN": "v31",
+    "BASE": "v[32:33]", "BASEL": "v32", "BASEH": "v33", "WIN": "v34", "SWZ": "v35",
+}
+for i in range(20):
+    M[f"t{i}"] = f"v{36 + i}"
+for i in range(0, 20, 2):
+    M[f"T{i}{i + 1}"] = f"v[{36 + i}:{37 + i}]"
+M.update({"WD0": M["t13"], "WD1": M["t14"], "WD2": M["t15"], "SHF": M["t16"], "LENM": M["t17"]})
+SGPRS = list(range(33, 71))
+
+
+def F(text):
+    """Substitute {NAME} register names (the asm's own %[..] operands and %= are untouched)."""
+    return re.sub(r"\{(\w+)\}", lambda m: M[m.group(1)], text)
+
+
+def on(modes, idx="{DST2}"):
+    return f"s_set_gpr_idx_on {idx}, gpr_idx({modes})"
+
+
+OFF = "s_set_gpr_idx_off"
+READ_A = f"{on('SRC0')}\nv_mov_b64 {{A}}, {{RF}}\n{OFF}"
+READ_S = f"{on('SRC0', '{SRC2}')}\nv_mov_b64 {{S}}, {{RF}}\n{OFF}"
+WRITE_R = f"{on('DST')}\nv_mov_b64 {{RF}}, {{R}}\n{OFF}"
+WRITE_R32 = f"{on('DST')}\nv_mov_b32 {{RF0}}, {{RL}}\nv_mov_b32 {{RF1}}, 0\n{OFF}"
+STEP = "v_add_u32 {NST}, 1, {NST}"
+
+# Find the lowest parked pc (bit 63 = the DONE sentinel), fetch its micro-op, narrow exec to the
+# lanes parked there, jump to its handler.
+DISPATCH = """s_mov_b64 exec, {EXEC0}
+s_ff1_i32_b64 {P}, {LIVE}
+s_bitset0_b64 {LIVE}, {P}
+s_lshl_b32 {PCOFF}, {P}, 6
+s_load_dwordx16 {UOP}, {PROG}, {PCOFF}
+v_cmpx_eq_u32 vcc, {P}, {LPC}
+s_waitcnt lgkmcnt(0)
+s_add_u32 {JTL}, {SLOTBL}, {HOFF}
+s_addc_u32 {JTH}, {SLOTBH}, 0
+s_setpc_b64 {JT}"""
+
+# Chained successor: same lanes, next micro-op.
+CHAIN = """s_add_u32 {PCOFF}, {PCOFF}, 64
+s_load_dwordx16 {UOP}, {PROG}, {PCOFF}
+s_waitcnt lgkmcnt(0)
+s_add_u32 {JTL}, {SLOTBL}, {HOFF}
+s_addc_u32 {JTH}, {SLOTBH}, 0
+s_setpc_b64 {JT}"""
+
+# Block end of a non-jump: park the lanes at npc.
+END_N = "v_mov_b32 {LPC}, {NPC}\ns_or_b64 {LIVE}, {LIVE}, {NBIT}\n" + DISPATCH
+
+# Block end of a conditional jump: vcc = taken lanes among the active ones.
+JTAIL = """v_mov_b32 {t0}, {X}
+v_mov_b32 {t1}, {NPC}
+v_cndmask_b32 {LPC}, {t1}, {t0}, vcc
+s_cmp_lg_u64 vcc, 0
+s_cselect_b64 {T0}, {TBIT}, 0
+s_andn2_b64 {T1}, exec, vcc
+s_cselect_b64 {T1}, {NBIT}, 0
+s_or_b64 {LIVE}, {LIVE}, {T0}
+s_or_b64 {LIVE}, {LIVE}, {T1}
+""" + DISPATCH
+
+
+def fault_split(tag, status):
+    """vcc = faulting lanes among the active ones: they stop with `status`; exec continues with
+    the others (to the dispatcher when there are none)."""
+    return f"""s_mov_b64 {{T4}}, exec
+s_and_b64 exec, {{T4}}, vcc
+s_cbranch_scc0 .Lnf_{tag}%=
+v_mov_b32 {{ST}}, {status}
+v_mov_b32 {{LPC}}, -1
+.Lnf_{tag}%=:
+s_andn2_b64 exec, {{T4}}, vcc
+s_cbranch_scc0 .Ldisp%="""
+
+
+# ---- handler bodies (without their tail): ALU-like kinds get a chained and a block-end form ----
+def inplace64(op):
+    return f"{on('SRC1,DST')}\n{op} {{RF0}}, {{IMML}}, {{RF0}}\n{op} {{RF1}}, {{IMMH}}, {{RF1}}\n{OFF}"
+
+
+def inplace64r(op):
+    return f"{READ_S}\n{on('SRC1,DST')}\n{op} {{RF0}}, {{SL}}, {{RF0}}\n{op} {{RF1}}, {{SH}}, {{RF1}}\n{OFF}"
+
+
+def inplace32(op, reg=False):
+    b = "{SL}" if reg else "{IMML}"
+    pre = READ_S + "\n" if reg else ""
+    return f"{pre}{on('SRC1,DST')}\n{op} {{RF0}}, {b}, {{RF0}}\nv_mov_b32 {{RF1}}, 0\n{OFF}"
+
+
+def mul64(reg):
+    bl, bh = ("{SL}", "{SH}") if reg else ("{IMML}", "{IMMH}")
+    pre = READ_A + "\n" + (READ_S + "\n" if reg else "")
+    return pre + f"""v_mul_lo_u32 {{RL}}, {{AL}}, {bl}
+v_mul_hi_u32 {{t0}}, {{AL}}, {bl}
+v_mul_lo_u32 {{t1}}, {{AL}}, {bh}
+v_mul_lo_u32 {{t2}}, {{AH}}, {bl}
+v_add3_u32 {{RH}}, {{t0}}, {{t1}}, {{t2}}
+{WRITE_R}"""
+
+
+def arsh64(reg):
+    sh = "{SL}" if reg else "{IMML}"
+    pre = READ_A + "\n" + (READ_S + "\n" if reg else "")
+    tag = "arsh64r" if reg else "arsh64i"
+    return pre + f"""v_lshrrev_b64 {{T01}}, {sh}, {{A}}
+v_sub_u32_e64 {{t2}}, 64, {sh}
+v_lshlrev_b64 {{T23}}, {{t2}}, {{A}}
+v_or_b32 {{t0}}, {{t0}}, {{t2}}
+v_or_b32 {{t1}}, {{t1}}, {{t3}}
+v_sub_co_u32_e64 {{t4}}, {{T5}}, 0, {{t0}}
+v_subb_co_u32_e64 {{t5}}, {{T5}}, 0, {{t1}}, {{T5}}
+v_cmp_gt_i32 vcc, 0, {{AH}}
+v_cndmask_b32 {{RL}}, {{t0}}, {{t4}}, vcc
+v_cndmask_b32 {{RH}}, {{t1}}, {{t5}}, vcc
+v_cmp_eq_u32_e64 {{T0}}, 0, {{t0}}
+s_mov_b32 {{T3}}, 0x80000000
+v_cmp_eq_u32_e64 {{T1}}, {{T3}}, {{t1}}
+s_and_b64 {{T0}}, {{T0}}, {{T1}}
+s_and_b64 vcc, vcc, {{T0}}
+{fault_split(tag, ST_ARITH)}
+{WRITE_R}"""
+
+
+def arsh32(reg):
+    sh = "{SL}" if reg else "{IMML}"
+    pre = READ_A + "\n" + (READ_S + "\n" if reg else "")
+    return pre + f"""v_alignbit_b32 {{t0}}, {{AL}}, {{AL}}, {sh}
+v_sub_u32 {{t1}}, 0, {{t0}}
+v_cmp_gt_i32 vcc, 0, {{AL}}
+v_cndmask_b32 {{RL}}, {{t0}}, {{t1}}, vcc
+{WRITE_R32}"""
+
+
+def divmod_setup(mod, w64, reg):
+    """Dividend -> T45, divisor -> T67, original dividend -> T1011 (the result of a division by
+    zero for MOD); MODE = 1 for MOD. 32-bit forms: zero-extended low words (Q6). The divider
+    (out of line) writes dst and returns through MODE bit 1 (chained) to the right tail."""
+    bl, bh = ("{SL}", "{SH}") if reg else ("{IMML}", "{IMMH}")
+    pre = READ_A + "\n" + (READ_S + "\n" if reg else "")
+    ah = "{AH}" if w64 else "0"
+    bh = bh if w64 else "0"
+    return pre + f"""v_mov_b32 {{t4}}, {{AL}}
+v_mov_b32 {{t5}}, {ah}
+v_mov_b32 {{t6}}, {bl}
+v_mov_b32 {{t7}}, {bh}
+v_mov_b32 {{t10}}, {{AL}}
+v_mov_b32 {{t11}}, {ah}
+s_mov_b32 {{MODE}}, {1 if mod else 0}"""
+
+
+def jump(cmp, reg, pre=""):
+    return (READ_S + "\n" if reg else "") + f"{pre}{cmp}"
+
+
+# name -> (body, kind): kind "alu" (chained + end forms), "jump" (end form, JTAIL), "term"
+# (complete: ends itself), "ool" (body jumps out of line; the out-of-line code ends with the
+# form's tail)
+H = {
+    "H_EXIT": ("v_mov_b32 {LPC}, -1\n" + STEP + "\n" + DISPATCH, "term"),
+    "H_FAULT": ("v_mov_b32 {ST}, {IMML}\nv_mov_b32 {LPC}, -1\n" + DISPATCH, "term"),
+    "H_SLOW": (f"v_mov_b32 {{ST}}, {ST_INSN}\nv_mov_b32 {{LPC}}, -1\n" + DISPATCH, "term"),
+    "H_MOV64_IMM": (f"{on('DST')}\nv_mov_b32 {{RF0}}, {{IMML}}\nv_mov_b32 {{RF1}}, {{IMMH}}\n{OFF}", "alu"),
+    "H_MOV64_REG": (f"{READ_S}\n{on('DST')}\nv_mov_b64 {{RF}}, {{S}}\n{OFF}", "alu"),
+    "H_ADD64_IMM": (f"{on('SRC0,DST')}\nv_lshl_add_u64 {{RF}}, {{RF}}, 0, {{IMM}}\n{OFF}", "alu"),
+    "H_ADD64_REG": (f"{READ_S}\n{on('SRC0,DST')}\nv_lshl_add_u64 {{RF}}, {{RF}}, 0, {{S}}\n{OFF}", "alu"),
+    "H_SUB64_REG": (f"{READ_S}\n{on('SRC0,DST')}\nv_sub_co_u32 {{RF0}}, vcc, {{RF0}}, {{SL}}\n"
+                    f"v_subb_co_u32 {{RF1}}, vcc, {{RF1}}, {{SH}}, vcc\n{OFF}", "alu"),
+    "H_AND64_IMM": (inplace64("v_and_b32"), "alu"), "H_AND64_REG": (inplace64r("v_and_b32"), "alu"),
+    "H_OR64_IMM": (inplace64("v_or_b32"), "alu"), "H_OR64_REG": (inplace64r("v_or_b32"), "alu"),
+    "H_XOR64_IMM": (inplace64("v_xor_b32"), "alu"), "H_XOR64_REG": (inplace64r("v_xor_b32"), "alu"),
+    # the hardware uses bits [5:0] / [4:0] of the shift count: the reference's masks (Q20)
+    "H_LSH64_IMM": (f"{on('SRC1,DST')}\nv_lshlrev_b64 {{RF}}, {{IMML}}, {{RF}}\n{OFF}", "alu"),
+    "H_LSH64_REG": (f"{READ_S}\n{on('SRC1,DST')}\nv_lshlrev_b64 {{RF}}, {{SL}}, {{RF}}\n{OFF}", "alu"),
+    "H_RSH64_IMM": (f"{on('SRC1,DST')}\nv_lshrrev_b64 {{RF}}, {{IMML}}, {{RF}}\n{OFF}", "alu"),
+    "H_RSH64_REG": (f"{READ_S}\n{on('SRC1,DST')}\nv_lshrrev_b64 {{RF}}, {{SL}}, {{RF}}\n{OFF}", "alu"),
+    "H_MOV32_IMM": (f"{on('DST')}\nv_mov_b32 {{RF0}}, {{IMML}}\nv_mov_b32 {{RF1}}, 0\n{OFF}", "alu"),
+    "H_MOV32_REG": (f"{READ_S}\n{on('DST')}\nv_mov_b32 {{RF0}}, {{SL}}\nv_mov_b32 {{RF1}}, 0\n{OFF}", "alu"),
+    "H_ADD32_IMM": (inplace32("v_add_u32"), "alu"),
+    "H_ADD32_REG": (inplace32("v_add_u32", True), "alu"),
+    "H_SUB32_REG": (inplace32("v_subrev_u32", True), "alu"),  # dst - src
+    "H_AND32_IMM": (inplace32("v_and_b32"), "alu"),
+    "H_AND32_REG": (inplace32("v_and_b32", True), "alu"),
+    "H_OR32_IMM": (inplace32("v_or_b32"), "alu"),
+    "H_OR32_REG": (inplace32("v_or_b32", True), "alu"),
+    "H_XOR32_IMM": (inplace32("v_xor_b32"), "alu"),
+    "H_XOR32_REG": (inplace32("v_xor_b32", True), "alu"),
+    "H_LSH32_IMM": (inplace32("v_lshlrev_b32"), "alu"),
+    "H_LSH32_REG": (inplace32("v_lshlrev_b32", True), "alu"),
+    "H_RSH32_IMM": (inplace32("v_lshrrev_b32"), "alu"),
+    "H_RSH32_REG": (inplace32("v_lshrrev_b32", True), "alu"),
+    "H_ZX16": (f"{on('SRC1,DST')}\nv_and_b32 {{RF0}}, 0xffff, {{RF0}}\nv_mov_b32 {{RF1}}, 0\n{OFF}", "alu"),
+    "H_ZX32": (f"{on('DST')}\nv_mov_b32 {{RF1}}, 0\n{OFF}", "alu"),
+    "H_NOP": ("", "alu"),
+    # v_perm_b32 selector bytes: 0..3 pick bytes of src1, 0x0c gives 0x00
+    "H_BSWAP16": (f"s_mov_b32 {{T3}}, 0x0c0c0001\n{on('SRC0,SRC1,DST')}\n"
+                  f"v_perm_b32 {{RF0}}, {{RF0}}, {{RF0}}, {{T3}}\nv_mov_b32 {{RF1}}, 0\n{OFF}", "alu"),
+    "H_BSWAP32": (f"s_mov_b32 {{T3}}, 0x00010203\n{on('SRC0,SRC1,DST')}\n"
+                  f"v_perm_b32 {{RF0}}, {{RF0}}, {{RF0}}, {{T3}}\nv_mov_b32 {{RF1}}, 0\n{OFF}", "alu"),
+    "H_BSWAP64": (f"""{READ_A}
+s_mov_b32 {{T3}}, 0x00010203
+v_perm_b32 {{RL}}, {{AH}}, {{AH}}, {{T3}}
+v_perm_b32 {{RH}}, {{AL}}, {{AL}}, {{T3}}
+{WRITE_R}""", "alu"),
+    "H_MUL64_IMM": (mul64(False), "alu"), "H_MUL64_REG": (mul64(True), "alu"),
+    "H_MUL32_IMM": (f"{READ_A}\nv_mul_lo_u32 {{RL}}, {{AL}}, {{IMML}}\n{WRITE_R32}", "alu"),
+    "H_MUL32_REG": (f"{READ_A}\n{READ_S}\nv_mul_lo_u32 {{RL}}, {{AL}}, {{SL}}\n{WRITE_R32}", "alu"),
+    "H_NEG64": (f"{on('SRC0,SRC1,DST')}\nv_sub_co_u32 {{RF0}}, vcc, 0, {{RF0}}\n"
+                f"v_subb_co_u32 {{RF1}}, vcc, 0, {{RF1}}, vcc\n{OFF}", "alu"),
+    "H_NEG32": (f"{on('SRC1,DST')}\nv_sub_u32 {{RF0}}, 0, {{RF0}}\nv_mov_b32 {{RF1}}, 0\n{OFF}", "alu"),
+    "H_ARSH64_IMM": (arsh64(False), "alu"), "H_ARSH64_REG": (arsh64(True), "alu"),
+    "H_ARSH32_IMM": (arsh32(False), "alu"), "H_ARSH32_REG": (arsh32(True), "alu"),
+    "H_DIV64_IMM": (divmod_setup(False, True, False), "div"),
+    "H_DIV64_REG": (divmod_setup(False, True, True), "div"),
+    "H_MOD64_IMM": (divmod_setup(True, True, False), "div"),
+    "H_MOD64_REG": (divmod_setup(True, True, True), "div"),
+    "H_DIV32_IMM": (divmod_setup(False, False, False), "div"),
+    "H_DIV32_REG": (divmod_setup(False, False, True), "div"),
+    "H_MOD32_IMM": (divmod_setup(True, False, False), "div"),
+    "H_MOD32_REG": (divmod_setup(True, False, True), "div"),
+    "H_JA": ("v_mov_b32 {LPC}, {X}\n" + STEP + "\ns_or_b64 {LIVE}, {LIVE}, {TBIT}\n" + DISPATCH, "term"),
+    # jumps: vcc = condition over the active lanes; x / npc, tbit / nbit already canonical
+    "H_JEQ_IMM": (jump(f"{on('SRC1')}\nv_cmp_eq_u64 vcc, {{IMM}}, {{RF}}\n{OFF}", False), "jump"),
+    "H_JEQ_REG": (jump(f"{on('SRC1')}\nv_cmp_eq_u64 vcc, {{S}}, {{RF}}\n{OFF}", True), "jump"),
+    "H_JGT_IMM": (jump(f"{on('SRC1')}\nv_cmp_lt_i64 vcc, {{IMM}}, {{RF}}\n{OFF}", False), "jump"),  # k < A
+    "H_JGT_REG": (jump(f"{on('SRC1')}\nv_cmp_lt_i64 vcc, {{S}}, {{RF}}\n{OFF}", True), "jump"),
+    "H_JLT_IMM": (jump(f"{on('SRC1')}\nv_cmp_gt_i64 vcc, {{IMM}}, {{RF}}\n{OFF}", False), "jump"),  # k > A
+    "H_JLT_REG": (jump(f"{on('SRC1')}\nv_cmp_gt_i64 vcc, {{S}}, {{RF}}\n{OFF}", True), "jump"),
+    "H_JSET_IMM": (jump("v_cmp_ne_u32 vcc, 0, {t0}", False,
+                        f"{on('SRC1')}\nv_and_b32 {{t0}}, {{IMML}}, {{RF0}}\nv_and_b32 {{t1}}, {{IMMH}}, {{RF1}}\n{OFF}\n"
+                        "v_or_b32 {t0}, {t0}, {t1}\n"), "jump"),
+    "H_JSET_REG": (jump("v_cmp_ne_u32 vcc, 0, {t0}", True,
+                        f"{on('SRC1')}\nv_and_b32 {{t0}}, {{SL}}, {{RF0}}\nv_and_b32 {{t1}}, {{SH}}, {{RF1}}\n{OFF}\n"
+                        "v_or_b32 {t0}, {t0}, {t1}\n"), "jump"),
+    # JMP32: signed compares of the low words == compares of the sign-extended words (Q3)
+    "H_JEQ32_IMM": (jump(f"{on('SRC1')}\nv_cmp_eq_u32 vcc, {{IMML}}, {{RF0}}\n{OFF}", False), "jump"),
+    "H_JEQ32_REG": (jump(f"{on('SRC1')}\nv_cmp_eq_u32 vcc, {{SL}}, {{RF0}}\n{OFF}", True), "jump"),
+    "H_JGT32_IMM": (jump(f"{on('SRC1')}\nv_cmp_lt_i32 vcc, {{IMML}}, {{RF0}}\n{OFF}", False), "jump"),
+    "H_JGT32_REG": (jump(f"{on('SRC1')}\nv_cmp_lt_i32 vcc, {{SL}}, {{RF0}}\n{OFF}", True), "jump"),
+    "H_JLT32_IMM": (jump(f"{on('SRC1')}\nv_cmp_gt_i32 vcc, {{IMML}}, {{RF0}}\n{OFF}", False), "jump"),
+    "H_JLT32_REG": (jump(f"{on('SRC1')}\nv_cmp_gt_i32 vcc, {{SL}}, {{RF0}}\n{OFF}", True), "jump"),
+    "H_JSET32_IMM": (jump("v_cmp_ne_u32 vcc, 0, {t0}", False,
+                          f"{on('SRC1')}\nv_and_b32 {{t0}}, {{IMML}}, {{RF0}}\n{OFF}\n"), "jump"),
+    "H_JSET32_REG": (jump("v_cmp_ne_u32 vcc, 0, {t0}", True,
+                          f"{on('SRC1')}\nv_and_b32 {{t0}}, {{SL}}, {{RF0}}\n{OFF}\n"), "jump"),
+    "H_LDXK": ("ldxk", "ool"),
+    "H_LDXK_FAR": ("ldxkfar", "ool"),
+    "H_LDX": ("ldx", "ool"),
+}
+DONE = "H_DONE"
+
+
+def window_addr(dst, b):
+    """LDS address of window dword b (VGPR, a multiple of 4) of this lane: the 16-byte chunk
+    (b & 0x30) is XOR-swizzled per lane (interp.hip win_off)."""
+    return f"""v_and_b32 {{t18}}, 48, {b}
+v_xor_b32 {{t18}}, {{t18}}, {{SWZ}}
+v_and_b32 {{t19}}, 15, {b}
+v_add3_u32 {dst}, {{WIN}}, {{t18}}, {{t19}}"""
+
+
+def window_tail(a0, shift):
+    """{WD0..2} = the three dwords at (a0 & ~3) (LDS reads or global loads in flight), byte
+    shift in `shift`; mask to the access width (k), zero the bytes at or past len (the zeroed
+    image, main.rs:16; never the case in the FIXED layout, where every packet is >= 64 bytes
+    long), merge into the old dst value (upper bytes kept, Q1) and commit."""
+    return f""".if %[fixed] == 0
+v_sub_u32_e64 {{LENM}}, {{LEN}}, {a0}
+v_cmp_lt_u32 vcc, {a0}, {{LEN}}
+v_cndmask_b32 {{LENM}}, 0, {{LENM}}, vcc
+v_min_u32 {{LENM}}, 8, {{LENM}}
+v_lshlrev_b32 {{LENM}}, 3, {{LENM}}
+v_sub_u32 {{LENM}}, 64, {{LENM}}
+.endif
+{WAIT}
+v_alignbyte_b32 {{RL}}, {{WD1}}, {{WD0}}, {shift}
+v_alignbyte_b32 {{RH}}, {{WD2}}, {{WD1}}, {shift}
+.if %[fixed] == 0
+v_and_b32 {{RL}}, {{KML}}, {{RL}}
+v_and_b32 {{RH}}, {{KMH}}, {{RH}}
+v_lshlrev_b64 {{R}}, {{LENM}}, {{R}}
+v_lshrrev_b64 {{R}}, {{LENM}}, {{R}}
+v_cndmask_b32 {{RL}}, 0, {{RL}}, vcc
+v_cndmask_b32 {{RH}}, 0, {{RH}}, vcc
+.endif
+{on('SRC2,DST')}
+v_bfi_b32 {{RF0}}, {{KML}}, {{RL}}, {{RF0}}
+v_bfi_b32 {{RF1}}, {{KMH}}, {{RH}}, {{RF1}}
+{OFF}"""
+
+
+WAIT = "s_waitcnt lgkmcnt(0)"
+
+
+def far_read(a0v, tag, save="{T0}"):
+    """Current exec = lanes reading packet bytes outside the window (a0v < len): {WD0..2} =
+    the dwords at (a0 & ~3) + 0/4/8, each loaded only if it holds a packet byte (pkt_read in
+    interp.hip: no access leaves the page of a valid byte), else 0."""
+    return f"""v_and_b32 {{t10}}, -4, {a0v}
+v_mov_b32 {{t11}}, 0
+v_lshl_add_u64 {{T89}}, {{BASE}}, 0, {{T1011}}
+global_load_dword {{WD0}}, {{T89}}, off
+v_mov_b32 {{WD1}}, 0
+v_mov_b32 {{WD2}}, 0
+s_mov_b64 {save}, exec
+v_add_u32 {{t12}}, 4, {{t10}}
+v_cmp_lt_u32 vcc, {{t12}}, {{LEN}}
+s_and_b64 exec, {save}, vcc
+s_cbranch_scc0 .Lfa_{tag}%=
+global_load_dword {{WD1}}, {{T89}}, off offset:4
+.Lfa_{tag}%=:
+s_mov_b64 exec, {save}
+v_add_u32 {{t12}}, 8, {{t10}}
+v_cmp_lt_u32 vcc, {{t12}}, {{LEN}}
+s_and_b64 exec, {save}, vcc
+s_cbranch_scc0 .Lfb_{tag}%=
+global_load_dword {{WD2}}, {{T89}}, off offset:8
+.Lfb_{tag}%=:
+s_mov_b64 exec, {save}
+s_waitcnt vmcnt(0)"""
+
+
+def ldxk(sfx):
+    """LDXK: constant address a0 = A0 inside the window, end = END; window dword i at chunk bits
+    W[2i] (xor'ed with the lane swizzle), byte-in-chunk W[2i + 1]."""
+    return f""".Lldxk{sfx}%=:
+s_cmp_gt_u32 {{END}}, {{KMEM}}
+s_cbranch_scc1 .Lkfault%=
+v_xor_b32 {{WD0}}, {{W0}}, {{SWZ}}
+v_add3_u32 {{WD0}}, {{WIN}}, {{WD0}}, {{W1}}
+v_xor_b32 {{WD1}}, {{W2}}, {{SWZ}}
+v_add3_u32 {{WD1}}, {{WIN}}, {{WD1}}, {{W3}}
+v_xor_b32 {{WD2}}, {{W4}}, {{SWZ}}
+v_add3_u32 {{WD2}}, {{WIN}}, {{WD2}}, {{W5}}
+ds_read_b32 {{WD0}}, {{WD0}}
+ds_read_b32 {{WD1}}, {{WD1}}
+ds_read_b32 {{WD2}}, {{WD2}}
+s_and_b32 {{T3}}, {{A0}}, 3
+{window_tail("{A0}", "{T3}")}
+{STEP}
+{TAILS[sfx]}"""
+
+
+# a fault of a constant-address load hits every active lane alike (mmu.rs:13-30)
+KFAULT = f""".Lkfault%=:
+s_cmp_ge_u32 {{A0}}, {{KMEM}}
+s_cselect_b32 {{T3}}, {ST_MEM}, {ST_MEM_UB}
+v_mov_b32 {{ST}}, {{T3}}
+v_mov_b32 {{LPC}}, -1
+.Ldisp%=:
+{DISPATCH}"""
+
+
+def ldxkfar(sfx):
+    """LDXK outside the window: a0 < 2^32 (the host faults larger constants statically)."""
+    return f""".Lldxkfar{sfx}%=:
+s_cmp_gt_u32 {{END}}, {{KMEM}}
+s_cbranch_scc1 .Lkfault%=
+v_mov_b32 {{t7}}, {{A0}}
+v_mov_b32 {{WD0}}, 0
+v_mov_b32 {{WD1}}, 0
+v_mov_b32 {{WD2}}, 0
+s_mov_b64 {{T7}}, exec
+v_cmp_lt_u32 vcc, {{A0}}, {{LEN}}
+s_and_b64 exec, {{T7}}, vcc
+s_cbranch_scc0 .Lkf_none{sfx}%=
+{far_read("{t7}", "kf" + sfx)}
+.Lkf_none{sfx}%=:
+s_mov_b64 exec, {{T7}}
+s_and_b32 {{T3}}, {{A0}}, 3
+{window_tail_ldx("{A0}", "{T3}")}
+{STEP}
+{TAILS[sfx]}"""
+
+
+def ldx(sfx):
+    """LDX: address = S + sext(off) (IMM), mmu.rs bounds per lane: signed overflow or addr >= mem
+    -> ST_MEM, addr + width > mem -> ST_MEM_UB (emu.rs:344, mmu.rs:13-30); then the window
+    (addr + width <= 64), or the packet bytes past it, or zeros past the packet."""
+    return f""".Lldx{sfx}%=:
+{READ_S}
+v_lshl_add_u64 {{T01}}, {{S}}, 0, {{IMM}}
+v_xor_b32 {{t2}}, {{SH}}, {{t1}}
+v_xor_b32 {{t3}}, {{IMMH}}, {{t1}}
+v_and_b32 {{t2}}, {{t2}}, {{t3}}
+v_cmp_gt_i32_e64 {{T0}}, 0, {{t2}}
+v_cmp_ne_u32_e64 {{T1}}, 0, {{t1}}
+s_or_b64 {{T0}}, {{T0}}, {{T1}}
+v_cmp_le_u32_e64 {{T1}}, {{KMEM}}, {{t0}}
+s_or_b64 {{T0}}, {{T0}}, {{T1}}
+v_add_u32 {{t4}}, {{WID}}, {{t0}}
+v_cmp_lt_u32_e64 {{T1}}, {{KMEM}}, {{t4}}
+s_andn2_b64 {{T1}}, {{T1}}, {{T0}}
+s_or_b64 vcc, {{T0}}, {{T1}}
+v_cndmask_b32_e64 {{t5}}, {ST_MEM_UB}, {ST_MEM}, {{T0}}
+{fault_split("ldx" + sfx, "{t5}")}
+v_cmp_lt_u32_e64 {{T1}}, 64, {{t4}}
+v_cndmask_b32_e64 {{t6}}, {{t0}}, 0, {{T1}}
+v_and_b32 {{t6}}, -4, {{t6}}
+{window_addr("{WD0}", "{t6}")}
+v_add_u32 {{t7}}, 4, {{t6}}
+v_min_u32 {{t7}}, 60, {{t7}}
+{window_addr("{WD1}", "{t7}")}
+v_add_u32 {{t7}}, 8, {{t6}}
+v_min_u32 {{t7}}, 60, {{t7}}
+{window_addr("{WD2}", "{t7}")}
+ds_read_b32 {{WD0}}, {{WD0}}
+ds_read_b32 {{WD1}}, {{WD1}}
+ds_read_b32 {{WD2}}, {{WD2}}
+v_cmp_lt_u32_e64 {{T0}}, {{t0}}, {{LEN}}
+s_and_b64 {{T7}}, {{T1}}, {{T0}}
+s_cbranch_scc0 .Lldx_near{sfx}%=
+{WAIT}
+s_mov_b64 {{T5}}, exec
+s_mov_b64 exec, {{T7}}
+{far_read("{t0}", "ldx" + sfx)}
+s_mov_b64 exec, {{T5}}
+.Lldx_near{sfx}%=:
+v_and_b32 {{SHF}}, 3, {{t0}}
+{window_tail_ldx("{t0}", "{SHF}")}
+{STEP}
+{TAILS[sfx]}"""
+
+
+def window_tail_ldx(a0, shift):
+    """As window_tail, but the bytes may come from far_read (past the window), where the bytes
+    past len must be zeroed in every layout."""
+    return f"""v_sub_u32_e64 {{LENM}}, {{LEN}}, {a0}
+v_cmp_lt_u32 vcc, {a0}, {{LEN}}
+v_cndmask_b32 {{LENM}}, 0, {{LENM}}, vcc
+v_min_u32 {{LENM}}, 8, {{LENM}}
+v_lshlrev_b32 {{LENM}}, 3, {{LENM}}
+v_sub_u32 {{LENM}}, 64, {{LENM}}
+{WAIT}
+v_alignbyte_b32 {{RL}}, {{WD1}}, {{WD0}}, {shift}
+v_alignbyte_b32 {{RH}}, {{WD2}}, {{WD1}}, {shift}
+v_and_b32 {{RL}}, {{KML}}, {{RL}}
+v_and_b32 {{RH}}, {{KMH}}, {{RH}}
+v_lshlrev_b64 {{R}}, {{LENM}}, {{R}}
+v_lshrrev_b64 {{R}}, {{LENM}}, {{R}}
+v_cndmask_b32 {{RL}}, 0, {{RL}}, vcc
+v_cndmask_b32 {{RH}}, 0, {{RH}}, vcc
+{on('SRC2,DST')}
+v_bfi_b32 {{RF0}}, {{KML}}, {{RL}}, {{RF0}}
+v_bfi_b32 {{RF1}}, {{KMH}}, {{RH}}, {{RF1}}
+{OFF}"""
+
+
+# bit-serial restoring division: T45 dividend, T67 divisor -> T01 quotient, T23 remainder;
+# division by zero: DIV -> 0, MOD -> dividend (T1011) (emu.rs:90-100,126-135, Q5)
+def divmod(sfx):
+    return f""".Ldivmod{sfx}%=:
+v_mov_b32 {{t0}}, 0
+v_mov_b32 {{t1}}, 0
+v_mov_b32 {{t2}}, 0
+v_mov_b32 {{t3}}, 0
+s_mov_b32 {{CNT}}, 64
+.Ldivloop{sfx}%=:
+v_lshlrev_b64 {{T23}}, 1, {{T23}}
+v_lshrrev_b32 {{t8}}, 31, {{t5}}
+v_or_b32 {{t2}}, {{t2}}, {{t8}}
+v_lshlrev_b64 {{T45}}, 1, {{T45}}
+v_lshlrev_b64 {{T01}}, 1, {{T01}}
+v_cmp_ge_u64 vcc, {{T23}}, {{T67}}
+v_sub_co_u32_e64 {{t8}}, {{T5}}, {{t2}}, {{t6}}
+v_subb_co_u32_e64 {{t9}}, {{T5}}, {{t3}}, {{t7}}, {{T5}}
+v_cndmask_b32 {{t2}}, {{t2}}, {{t8}}, vcc
+v_cndmask_b32 {{t3}}, {{t3}}, {{t9}}, vcc
+v_cndmask_b32_e64 {{t8}}, 0, 1, vcc
+v_or_b32 {{t0}}, {{t0}}, {{t8}}
+s_sub_u32 {{CNT}}, {{CNT}}, 1
+s_cmp_lg_u32 {{CNT}}, 0
+s_cbranch_scc1 .Ldivloop{sfx}%=
+v_cmp_eq_u64 vcc, 0, {{T67}}
+s_cmp_eq_u32 {{MODE}}, 0
+s_cbranch_scc0 .Lmodres{sfx}%=
+v_cndmask_b32_e64 {{RL}}, {{t0}}, 0, vcc
+v_cndmask_b32_e64 {{RH}}, {{t1}}, 0, vcc
+s_branch .Ldivend{sfx}%=
+.Lmodres{sfx}%=:
+v_cndmask_b32 {{RL}}, {{t2}}, {{t10}}, vcc
+v_cndmask_b32 {{RH}}, {{t3}}, {{t11}}, vcc
+.Ldivend{sfx}%=:
+{WRITE_R}
+{STEP}
+{TAILS[sfx]}"""
+
+
+TAILS = {"c": CHAIN, "e": END_N}
+
+# ---- prologue / epilogue ----
+# %[ka]: the kernel-argument segment (LaunchArgs at offset 0; LA_* offsets are "i" operands);
+# %[tile]: the tile index (64-bit SGPR pair); %[winb]: this wave's window region (LDS byte
+# address); %[metab]: this wave's metadata region (offsets u32[64], lengths u32[64]).
+PROLOGUE = """s_mov_b32 {M0S}, m0
+s_load_dwordx2 {PROG}, %[ka], %[o_tprog]
+s_load_dwordx2 {KFR}, %[ka], %[o_frames]
+s_load_dwordx2 {KST}, %[ka], %[o_stride]
+s_load_dwordx2 {KN}, %[ka], %[o_n]
+s_load_dword {KMEM}, %[ka], %[o_mem]
+.if %[fixed] == 0
+s_load_dwordx2 {KOFF}, %[ka], %[o_offsets]
+s_load_dwordx2 {KLEN}, %[ka], %[o_lens]
+.endif
+s_load_dwordx2 {KINIT}, %[ka], %[o_init]
+s_load_dwordx2 {KR10}, %[ka], %[o_r10]
+v_mbcnt_lo_u32_b32 {t0}, -1, 0
+v_mbcnt_hi_u32_b32 {t0}, -1, {t0}
+s_lshl_b64 {T0}, %[tile], 6
+v_mov_b32 {t1}, 0
+v_lshl_add_u64 {T23}, {T01}, 0, {T0}
+.if %[fixed] == 0
+v_lshlrev_b32 {t5}, 2, {t0}
+v_add_u32 {t5}, %[metab], {t5}
+ds_read_b32 {t6}, {t5}
+ds_read_b32 {t7}, {t5} offset:256
+.endif
+s_waitcnt lgkmcnt(0)
+.if %[fixed]
+; the tile's header windows HBM -> LDS (as dma_window_stride in interp.hip): round r moves
+; packets 16r..16r+15, lane l filling chunk slot (l & 3) of packet 16r + l/4 from logical
+; chunk (l & 3) ^ ((l >> 4) & 3); lanes past the batch read the micro-op table instead
+v_lshrrev_b32 {t4}, 2, {t0}
+v_mov_b32 {t5}, 0
+v_lshl_add_u64 {T45}, {T45}, 0, {T0}
+v_and_b32 {t6}, 3, {t0}
+v_bfe_u32 {t7}, {t0}, 4, 2
+v_xor_b32 {t6}, {t6}, {t7}
+v_lshlrev_b32 {t6}, 4, {t6}
+v_mov_b32 {t7}, 0
+v_mov_b32 {t10}, {KSTL}
+v_mad_u64_u32 {T89}, {T4}, {t4}, {t10}, {KFR}
+v_mul_lo_u32 {t11}, {t5}, {KSTL}
+v_mul_lo_u32 {t12}, {t4}, {KSTH}
+v_add3_u32 {t9}, {t9}, {t11}, {t12}
+v_lshl_add_u64 {T89}, {T89}, 0, {T67}
+s_lshl_b64 {T1}, {KST}, 4
+v_mov_b32 {t10}, {PROGL}
+v_mov_b32 {t11}, {PROGH}
+""" + "\n".join(f"""v_cmp_gt_u64 vcc, {{KN}}, {{T45}}
+v_cndmask_b32 {{t12}}, {{t10}}, {{t8}}, vcc
+v_cndmask_b32 {{t13}}, {{t11}}, {{t9}}, vcc
+s_add_u32 m0, %[winb], {1024 * r}
+s_nop 0
+global_load_lds_dwordx4 {{T1213}}, off
+v_lshl_add_u64 {{T45}}, {{T45}}, 0, 16
+v_lshl_add_u64 {{T89}}, {{T89}}, 0, {{T1}}""" for r in range(4)) + """
+s_waitcnt vmcnt(0)
+.endif
+v_cmp_gt_u64 vcc, {KN}, {T23}
+s_and_b64 {VM}, vcc, exec
+s_cmp_gt_u32 {KSTH}, 0
+s_cselect_b32 {T3}, -1, {KSTL}
+v_mov_b32 {LEN}, {T3}
+v_mov_b32 {t4}, {KSTL}
+v_mad_u64_u32 {BASE}, {T4}, {t2}, {t4}, {KFR}
+v_mul_lo_u32 {t4}, {t3}, {KSTL}
+v_mul_lo_u32 {t9}, {t2}, {KSTH}
+v_add3_u32 {BASEH}, {BASEH}, {t4}, {t9}
+.if %[fixed] == 0
+s_cmp_lg_u64 {KOFF}, 0
+s_cbranch_scc0 .Lnooff%=
+v_mov_b32 {t8}, {t6}
+v_mov_b32 {t9}, 0
+v_lshl_add_u64 {BASE}, {KFR}, 0, {T89}
+.Lnooff%=:
+s_cmp_lg_u64 {KLEN}, 0
+s_cbranch_scc0 .Lnolen%=
+v_and_b32 {LEN}, 0xffff, {t7}
+.Lnolen%=:
+.endif
+v_cndmask_b32 {LEN}, 0, {LEN}, vcc
+v_lshlrev_b32 {WIN}, 6, {t0}
+v_add_u32 {WIN}, %[winb], {WIN}
+v_lshrrev_b32 {SWZ}, 2, {t0}
+v_and_b32 {SWZ}, 3, {SWZ}
+v_lshlrev_b32 {SWZ}, 4, {SWZ}
+v_mov_b32 {NST}, 0
+v_mov_b32 {ST}, 0
+v_mov_b32 {LPC}, -1
+v_cmp_lt_u32 {T0}, {KMEM}, {LEN}
+s_and_b64 {T0}, {T0}, {VM}
+s_andn2_b64 {T1}, {VM}, {T0}
+s_mov_b64 exec, {T0}
+v_mov_b32 {ST}, 7
+s_mov_b64 exec, {T1}
+v_mov_b32 {LPC}, 0
+s_mov_b64 exec, {EXEC0}
+s_cmp_lg_u64 {T1}, 0
+s_cselect_b64 {LIVE}, 1, 0
+s_bitset1_b64 {LIVE}, 63
+s_cmp_lg_u64 {KINIT}, 0
+s_cbranch_scc1 .Linitc%=
+""" + "\n".join(f"v_mov_b32 v{i}, 0" for i in range(22) if i not in (4, 20, 21)) + """
+v_mov_b32 v4, {LEN}
+v_mov_b32 v20, {KR10L}
+v_mov_b32 v21, {KR10H}
+s_branch .Linitd%=
+.Linitc%=:
+s_mov_b64 {T5}, {KINIT}
+s_load_dwordx16 {UOP}, {T5}, 0x0
+s_waitcnt lgkmcnt(0)
+""" + "\n".join(f"v_mov_b32 v{i}, s{UB + i}" for i in range(16)) + """
+s_load_dwordx4 s[36:39], {T5}, 0x40
+s_load_dwordx2 s[40:41], {T5}, 0x50
+s_waitcnt lgkmcnt(0)
+""" + "\n".join(f"v_mov_b32 v{16 + i}, s{UB + i}" for i in range(6)) + """
+.Linitd%=:
+s_getpc_b64 {SLOTB}
+.Lpc%=:
+s_add_u32 {SLOTBL}, {SLOTBL}, .Lslots%=-.Lpc%=
+s_addc_u32 {SLOTBH}, {SLOTBH}, 0
+""" + DISPATCH + """
+.p2align 8
+.Lslots%=:"""
+
+# bucket: 0..4 r0, 5 r0 >= 5, 6 fault, 7 not a packet; stores of the valid lanes
+EPILOGUE = """.Ldone%=:
+s_mov_b64 exec, {EXEC0}
+v_cmp_gt_u64 vcc, 5, {RF}
+v_cndmask_b32 %[bkt], 5, {RF0}, vcc
+v_cmp_ne_u32 vcc, 0, {ST}
+v_cndmask_b32_e64 %[bkt], %[bkt], 6, vcc
+v_cndmask_b32_e64 %[bkt], 7, %[bkt], {VM}
+v_cndmask_b32_e64 %[nst], 0, {NST}, {VM}
+s_mov_b64 exec, {VM}
+s_cmp_lg_u64 exec, 0
+s_cbranch_scc0 .Lend%=
+v_mbcnt_lo_u32_b32 {t0}, -1, 0
+v_mbcnt_hi_u32_b32 {t0}, -1, {t0}
+s_lshl_b64 {T0}, %[tile], 6
+v_mov_b32 {t1}, 0
+v_lshl_add_u64 {T23}, {T01}, 0, {T0}
+s_load_dwordx2 {EV}, %[ka], %[o_verdict]
+s_load_dwordx2 {ER0}, %[ka], %[o_r0]
+s_load_dwordx2 {EST}, %[ka], %[o_status]
+s_load_dwordx2 {ERG}, %[ka], %[o_regs]
+s_waitcnt lgkmcnt(0)
+s_cmp_lg_u64 {EV}, 0
+s_cbranch_scc0 .Lnov%=
+v_cmp_gt_u32 vcc, 5, %[bkt]
+v_mov_b32 {t5}, 0xfe
+v_cndmask_b32 {t4}, {t5}, {RF0}, vcc
+v_cmp_ne_u32 vcc, 6, %[bkt]
+v_mov_b32 {t5}, 0xff
+v_cndmask_b32 {t4}, {t5}, {t4}, vcc
+v_lshl_add_u64 {T67}, {T23}, 0, {EV}
+global_store_byte {T67}, {t4}, off
+.Lnov%=:
+s_cmp_lg_u64 {ER0}, 0
+s_cbranch_scc0 .Lnor%=
+v_lshlrev_b64 {T67}, 3, {T23}
+v_lshl_add_u64 {T67}, {T67}, 0, {ER0}
+global_store_dwordx2 {T67}, {RF}, off
+.Lnor%=:
+s_cmp_lg_u64 {EST}, 0
+s_cbranch_scc0 .Lnos%=
+v_lshl_add_u64 {T67}, {T23}, 0, {EST}
+global_store_byte {T67}, {ST}, off
+.Lnos%=:
+s_cmp_lg_u64 {ERG}, 0
+s_cbranch_scc0 .Lend%=
+v_mov_b32 {t6}, 88
+v_mad_u64_u32 {T89}, {T4}, {t2}, {t6}, {ERG}
+v_mul_lo_u32 {t6}, {t3}, {t6}
+v_add_u32 {t9}, {t9}, {t6}
+""" + "\n".join(f"global_store_dwordx2 {{T89}}, v[{2 * r}:{2 * r + 1}], off offset:{8 * r}"
+                for r in range(11)) + """
+.Lend%=:
+s_mov_b64 exec, {EXEC0}
+s_mov_b32 m0, {M0S}"""
+
+
+def handler_table():
+    """Handler names in slot order and their id: every "alu"/"div"/"ool" kind has a chained (_C)
+    and a block-end (_E) form; the others one form (_E); then DONE."""
+    out = []
+    for n, (body, kind) in H.items():
+        if kind in ("alu", "div", "ool"):
+            out.append((n + "_C", n, "c"))
+        out.append((n + "_E", n, "e"))
+    out.append((DONE, DONE, "e"))
+    return out
+
+
+def main():
+    table = handler_table()
+    parts = [PROLOGUE]
+    ool = []
+    for idx, (name, base, sfx) in enumerate(table):
+        if base == DONE:
+            code = "s_branch .Ldone%="
+        else:
+            body, kind = H[base]
+            if kind == "term":
+                code = body
+            elif kind == "jump":
+                code = body + "\n" + STEP + "\n" + JTAIL
+            elif kind == "alu":
+                code = (body + "\n" if body else "") + STEP + "\n" + TAILS[sfx]
+            elif kind == "div":
+                code = body + f"\ns_branch .Ldivmod{sfx}%="
+            else:  # ool
+                code = f"s_branch .L{body}{sfx}%="
+        code = re.sub(r"\.L(nf_\w+?)%=", lambda m: f".L{m.group(1)}_{idx}%=", code)
+        parts.append(f"; {name}\n.org .Lslots%=+{idx * SLOT}\n" + code)
+    parts.append(f".org .Lslots%=+{len(table) * SLOT}")
+    for sfx in ("c", "e"):
+        parts += [ldxk(sfx), ldxkfar(sfx), ldx(sfx), divmod(sfx)]
+    parts += [KFAULT, EPILOGUE]
+    text = F("\n".join(parts))
+    assert "{" not in text, "unsubstituted register name: " + text[text.index("{"):][:40]
+    out = ["// GENERATED by gen_tile.py -- do not edit. One inline-asm statement (tile_kernel).",
+           "// clang-format off"]
+    for line in text.splitlines():
+        out.append('"' + line.replace("\\", "\\\\").replace('"', '\\"') + '\\n"')
+    out.append("// clang-format on")
+    with open(os.path.join(HERE, "tile.inc"), "w") as f:
+        f.write("\n".join(out) + "\n")
+    # ids: T_<base>_C / T_<base>_E (byte offsets = id * TILE_SLOT)
+    ids = ["// GENERATED by gen_tile.py -- do not edit. Handler slots of tile.inc (uop.h TUop::hoff",
+           "// = id * TILE_SLOT). Chained (_C) forms continue with the next micro-op; block-end (_E)",
+           "// forms update the pc set and dispatch.",
+           "#pragma once", f"#define TILE_SLOT {SLOT}", f"#define TILE_NVGPR {NVGPR}"]
+    for idx, (name, base, sfx) in enumerate(table):
+        ids.append(f"#define T{name[1:]} {idx}")
+    ids.append(f"#define T_COUNT {len(table)}")
+    # old (dag_asm.h) id -> tile ids, for the host's table builder
+    c_map, e_map = [], []
+    for n in sorted(IDS_OLD, key=lambda k: IDS_OLD[k]):
+        if n == "H_COUNT":
+            continue
+        e = f"T{n[1:]}_E"
+        c = f"T{n[1:]}_C" if any(t[0] == n + "_C" for t in table) else e
+        c_map.append(c)
+        e_map.append(e)
+    ids.append("// indexed by dag_asm.h H_* ids")
+    ids.append("static const short kTileIdChained[] = {" + ", ".join(c_map) + "};")
+    ids.append("static const short kTileIdEnd[] = {" + ", ".join(e_map) + "};")
+    with open(os.path.join(HERE, "tile_ids.h"), "w") as f:
+        f.write("\n".join(ids) + "\n")
+
+
+if __name__ == "__main__":
+    import sys
+    if len(sys.argv) > 1 and sys.argv[1] == "--clobbers":
+        print(", ".join(f'"s{s}"' for s in SGPRS) + ", " +
+              ", ".join(f'"v{v}"' for v in range(NVGPR)))
+    else:
+        main()

@@ -17,6 +17,7 @@
 
 #include "../../include/ebpf_emu.h"
 #include "dag_asm.h"
+#include "tile_ids.h"
 #include "launch.h"
 #include "uop.h"
 
@@ -223,6 +224,9 @@ struct ebpf_prog {
   Uop* dev_uops[kMaxDevices] = {};
   DUop* dev_duops[kMaxDevices] = {};
   DUop* dev_duopsk[kMaxDevices] = {};
+  std::vector<TUop> tuops, tuopsk;  // tile_kernel's tables (<= 63 micro-ops), from duops / duopsk
+  TUop* dev_tuops[kMaxDevices] = {};
+  TUop* dev_tuopsk[kMaxDevices] = {};
 };
 
 // EBPFEMU_NO_DAG=1 runs every tier-0 program on interp_kernel (A/B runs, differential tests).
@@ -347,6 +351,49 @@ static std::vector<DUop> build_dag(const std::vector<Uop>& uops) {
     o.hoff = asm_handler(op, u.aux, kk, o.imm) * DAG_SLOT;
   }
   return d;
+}
+
+// tile_kernel's table (uop.h TUop) from the DUop table. A micro-op whose successor no jump can
+// reach (and that is not itself a jump, exit or fault) gets the CHAINED handler form: the tile loop
+// runs its successor next on the same lanes without touching the pc set (basic-block chaining).
+static std::vector<TUop> build_tile(const std::vector<Uop>& uops, const std::vector<DUop>& d) {
+  const uint32_t n = (uint32_t)uops.size();
+  std::vector<TUop> t(kTileUops);
+  std::memset(t.data(), 0, t.size() * sizeof(TUop));
+  std::vector<char> start(n + 1, 0);  // block starts: 0, jump targets, successors of block ends
+  start[0] = 1;
+  for (uint32_t i = 0; i < n; i++) {
+    const uint32_t h = d[i].hoff / DAG_SLOT;
+    const bool is_jump = uops[i].op >= U_JA && uops[i].op <= U_JLE32;
+    if (is_jump && (uint32_t)uops[i].x < n) start[(uint32_t)uops[i].x] = 1;
+    if (is_jump || h == H_EXIT || h == H_FAULT || h == H_SLOW) start[i + 1] = 1;
+  }
+  for (uint32_t i = 0; i < n; i++) {
+    const DUop& o = d[i];
+    TUop& u = t[i];
+    const uint32_t h = o.hoff / DAG_SLOT;
+    const bool chained = i + 1 < n && !start[i + 1];
+    u.hoff = (uint32_t)(chained ? kTileIdChained[h] : kTileIdEnd[h]) * TILE_SLOT;
+    u.dst2 = o.dst2;
+    u.src2 = o.src2;
+    u.npc = o.anpc;
+    u.x = o.ax;
+    u.a0 = o.a0;
+    u.kmask = o.kmask;
+    u.nbit = o.anbit;
+    u.tbit = o.atbit;
+    u.imm = o.imm;
+    u.width = o.width;
+    u.end = o.end;
+    if (h == H_LDXK) {  // window dwords in the fields LDXK does not use
+      u.src2 = o.win[0];
+      u.x = o.win[1];
+      u.tbit = (uint64_t)o.win[2] | ((uint64_t)o.win[3] << 32);
+      u.imm = (uint64_t)o.win[4] | ((uint64_t)o.win[5] << 32);
+    }
+  }
+  t[kTileUops - 1].hoff = T_DONE * TILE_SLOT;
+  return t;
 }
 
 // Load-time constant propagation over a forward-only program, from the main.rs:28-31 register
@@ -480,6 +527,10 @@ int ebpf_prog_load(const uint8_t* code, size_t nbytes, ebpf_prog** out, size_t* 
   if (forward && p->tier == 0 && !p->uops.empty() && p->uops.size() <= kMaxDagUops) {
     p->duops = build_dag(p->uops);
     p->duopsk = fold_const_loads(p->uops, p->duops);
+    if (p->uops.size() < kTileUops) {
+      p->tuops = build_tile(p->uops, p->duops);
+      p->tuopsk = build_tile(p->uops, p->duopsk);
+    }
   }
   *out = p;
   return EBPF_OK;
@@ -504,6 +555,8 @@ void ebpf_prog_free(ebpf_prog* p) {
       if (p->dev_uops[d]) hipFree(p->dev_uops[d]);
       if (p->dev_duops[d]) hipFree(p->dev_duops[d]);
       if (p->dev_duopsk[d]) hipFree(p->dev_duopsk[d]);
+      if (p->dev_tuops[d]) hipFree(p->dev_tuops[d]);
+      if (p->dev_tuopsk[d]) hipFree(p->dev_tuopsk[d]);
     }
   }
   hipSetDevice(cur);
@@ -553,18 +606,30 @@ int ebpf_prog_upload(ebpf_prog* p, int device) {
         hipMemcpy(*dst, t.data(), nb, hipMemcpyHostToDevice) != hipSuccess)
       rc = EBPF_EHIP;
   };
+  auto putt = [&](const std::vector<TUop>& t, TUop** dst) {
+    const size_t nb = t.size() * sizeof(TUop);
+    if (rc != EBPF_OK || t.empty()) return;
+    if (hipMalloc(dst, nb) != hipSuccess ||
+        hipMemcpy(*dst, t.data(), nb, hipMemcpyHostToDevice) != hipSuccess)
+      rc = EBPF_EHIP;
+  };
   DUop* dd = nullptr;
   DUop* ddk = nullptr;
+  TUop* td = nullptr;
+  TUop* tdk = nullptr;
   put(p->duops, &dd);
   put(p->duopsk, &ddk);
+  putt(p->tuops, &td);
+  putt(p->tuopsk, &tdk);
   if (rc == EBPF_OK) {
     p->dev_uops[device] = d;
     p->dev_duops[device] = dd;
     p->dev_duopsk[device] = ddk;
+    p->dev_tuops[device] = td;
+    p->dev_tuopsk[device] = tdk;
   } else {
-    if (d) hipFree(d);
-    if (dd) hipFree(dd);
-    if (ddk) hipFree(ddk);
+    for (void* q : {(void*)d, (void*)dd, (void*)ddk, (void*)td, (void*)tdk})
+      if (q) hipFree(q);
   }
   hipSetDevice(cur);
   return rc;
@@ -656,6 +721,7 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* b, const ebpf_batch_out* out,
   a.prog = p->dev_uops[device];
   // constant-address loads are resolved for the main.rs register layout only
   a.dprog = b->init_regs ? p->dev_duops[device] : p->dev_duopsk[device];
+  a.tprog = b->init_regs ? p->dev_tuops[device] : p->dev_tuopsk[device];
   a.n_uops = (uint32_t)p->uops.size();
   a.mem_size = b->mem_size;
   a.frames = b->frames;
@@ -670,6 +736,7 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* b, const ebpf_batch_out* out,
   a.status = out->status;
   a.counters = out->counters;
   a.shards = (uint64_t*)(ws + kWsShardsOff);
+  a.tickets = (uint32_t*)(ws + kWsTicketsOff);
   a.image_ws = ws + kWsSlotsOff;
   a.n_tiles = n_tiles;
   a.init_regs = b->init_regs;

@@ -34,6 +34,9 @@
 namespace ebpfemu {
 
 __device__ __forceinline__ uint32_t rfl(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t rfl64(uint64_t v) {
+  return (uint64_t)rfl((uint32_t)v) | ((uint64_t)rfl((uint32_t)(v >> 32)) << 32);
+}
 __device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 
 // Minimum over the 64 lanes (all lanes active) — DPP row shifts + row broadcasts (gfx9 DPP).
@@ -297,31 +300,89 @@ __device__ __forceinline__ void stage_window_lane(uint8_t* pw, uint32_t swz, con
     *(uint32_t*)(pw + win_off(bo, swz)) = (bo < m) ? (uint32_t)pkt_read(base, bo, 4, len) : 0u;
 }
 
-// ---- counters: workgroup sum -> non-returning sharded device atomics. Nothing waits on them:
-//      the workgroup retires at once and fold_counters (next on the stream) folds the shards
-//      into the caller's counters. cnt[] is wave-uniform, retired per lane. Reuses LDS (smem),
-//      so every wave of the workgroup must be done with its LDS data. ----
+// ---- counters ----
+// Per-workgroup accumulator in static LDS (separate from each kernel's dynamic LDS, which other
+// waves may still be using when one wave finishes). Zeroed by counters_init() at kernel start.
+struct WgCounters {
+  uint64_t acc[8];
+  uint32_t arrived;
+};
+__device__ __forceinline__ WgCounters* wg_counters() {
+  __shared__ WgCounters c;
+  return &c;
+}
+// Every kernel calls this first; the barrier makes the zeroed accumulator visible to all waves.
+__device__ __forceinline__ void counters_init() {
+  WgCounters* w = wg_counters();
+  if (threadIdx.x < 8) w->acc[threadIdx.x] = 0;
+  if (threadIdx.x == 0) w->arrived = 0;
+  __syncthreads();
+}
+
+// Per-wave counter epilogue; no workgroup barrier, so a finished wave retires at once.
+//   * each wave adds its sums to the workgroup accumulator in LDS and takes an LDS arrival ticket;
+//   * the workgroup's last wave adds the sums to shard (blockIdx % 64) with agent-scope 8-byte
+//     atomics (blockIdx -> XCD is round-robin, so a shard is only ever hit from one XCD);
+//   * a two-level device ticket then finds the last workgroup of the launch: ticket[g] counts the
+//     workgroups of shard g (<= grid/64 + 1 arrivals per word, far below the ~88/us one device
+//     word sustains, MI355X guide "dequeue"/"fanin"), and the last of shard g adds one to
+//     ticket[64]; the 64th of those folds the 64 shards into the caller's counters and leaves
+//     shards and tickets at zero for the next batch.
+// Ordering is "8-byte agent atomics on both sides" (MI355X guide, hand-off valid forms): the shard
+// adds are drained with s_waitcnt vmcnt(0) before the ticket add and the folder reads the shards
+// with agent-scope atomic exchanges, so no L2 write-back fence is needed. cnt[] is wave-uniform,
+// retired per lane.
 __device__ __forceinline__ void flush_counters(const LaunchArgs& a, const uint64_t (&cnt)[7],
-                                               uint64_t retired, uint8_t* smem, uint32_t lane,
-                                               uint32_t wv) {
+                                               uint64_t retired, uint8_t*, uint32_t lane,
+                                               uint32_t) {
   for (int off = 32; off >= 1; off >>= 1) retired += (uint64_t)__shfl_xor((long long)retired, off);
   if (a.counters == nullptr) return;
-  __syncthreads();
-  uint64_t* red = (uint64_t*)smem;
+  WgCounters* w = wg_counters();
+  uint64_t mine = retired;
+#pragma unroll
+  for (int b = 0; b < 7; b++) mine = lane == (uint32_t)b ? cnt[b] : mine;
+  if (lane < 8 && mine) atomicAdd((unsigned long long*)&w->acc[lane], (unsigned long long)mine);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  uint32_t old = 0;
+  if (lane == 0) old = atomicAdd(&w->arrived, 1u);
+  old = __builtin_amdgcn_readfirstlane(old);
+  if (old != (uint32_t)kWavesPerBlock - 1) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  // the workgroup's last wave
+  const uint32_t g = blockIdx.x % kCounterShards;
+  if (lane < 8) {
+    const uint64_t s = w->acc[lane];
+    if (s) __hip_atomic_fetch_add(&a.shards[g * 8 + lane], s, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (a.fold_kernel) return;  // fold_counters runs next on the stream
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every shard add performed
+  uint32_t is_last = 0;
   if (lane == 0) {
-#pragma unroll
-    for (int b = 0; b < 7; b++) red[wv * 8 + b] = cnt[b];
-    red[wv * 8 + 7] = retired;
+    const uint32_t grid = gridDim.x;
+    const uint32_t members = (grid - g + kCounterShards - 1) / kCounterShards;
+    const uint32_t groups = grid < (uint32_t)kCounterShards ? grid : (uint32_t)kCounterShards;
+    if (__hip_atomic_fetch_add(&a.tickets[g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+        members - 1) {
+      __hip_atomic_store(&a.tickets[g], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (__hip_atomic_fetch_add(&a.tickets[kCounterShards], 1u, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT) == groups - 1) {
+        __hip_atomic_store(&a.tickets[kCounterShards], 0u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        is_last = 1;
+      }
+    }
   }
-  __syncthreads();
-  if (threadIdx.x < 8) {
-    uint64_t s = 0;
+  if (__builtin_amdgcn_readfirstlane(is_last) == 0) return;
+  // the launch's last workgroup: read-and-clear the 512 shard words (lane l: words l + 64k, all
+  // of counter l % 8), sum across the lanes of each counter, add to the caller's counters
+  uint64_t v = 0;
 #pragma unroll
-    for (int w = 0; w < kWavesPerBlock; w++) s += red[w * 8 + threadIdx.x];
-    // blockIdx -> XCD is round-robin, so shard (blockIdx % 64) is only ever hit from one XCD
-    if (s) __hip_atomic_fetch_add(&a.shards[(blockIdx.x % kCounterShards) * 8 + threadIdx.x], s,
-                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  for (uint32_t k = 0; k < kCounterShards * 8 / kWave; k++)
+    v += __hip_atomic_exchange(&a.shards[lane + k * kWave], 0ull, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+  for (int off = 8; off < kWave; off <<= 1) v += (uint64_t)__shfl_xor((long long)v, off);
+  if (lane < 8 && v) atomicAdd((unsigned long long*)&a.counters[lane], (unsigned long long)v);
 }
 
 // The eBPF register file r0..r10 (emu.rs:15), as two 11-entry u32 arrays (low and high words):
@@ -337,6 +398,7 @@ __device__ __forceinline__ void flush_counters(const LaunchArgs& a, const uint64
 
 template <int TIER, bool LDSP, int NW, bool DB>
 __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
+  counters_init();
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t nu = a.n_uops;
   const uint32_t prog_bytes = LDSP ? nu * (uint32_t)sizeof(Uop) : 0u;
@@ -827,6 +889,7 @@ __device__ __forceinline__ void rset(uint8_t* rl, uint32_t off, uint64_t v) {
 
 template <int NW, int V = 11>
 __global__ __launch_bounds__(kBlock) void dag_kernel(LaunchArgs a) {
+  counters_init();
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t lane = threadIdx.x & (kWave - 1);
   const uint32_t wv = threadIdx.x / kWave;
@@ -1132,7 +1195,12 @@ __device__ __forceinline__ uint64_t dag_tile_asm(uint64_t live, uint32_t& lpc, u
   return (uint64_t)r0l | ((uint64_t)r0h << 32);
 }
 
+// FIXED: the stride layout with 16-byte aligned slots of >= 64 bytes, no lens array (every packet
+// is `stride` bytes) and no final-image output -- the shape of a NIC ring of fixed slots. Its tile
+// needs no packet metadata at all: the windows are DMA'd straight from pkt * stride.
+template <bool FIXED>
 __global__ __launch_bounds__(kBlock, 5) void dag_tile_kernel(LaunchArgs a) {
+  counters_init();
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t lane = threadIdx.x & (kWave - 1);
   const uint32_t wv = threadIdx.x / kWave;
@@ -1153,24 +1221,33 @@ __global__ __launch_bounds__(kBlock, 5) void dag_tile_kernel(LaunchArgs a) {
   for (uint64_t tile = wave_slot; tile < a.n_tiles; tile += total_waves) {
     const uint64_t pkt = tile * kWave + lane;
     const bool valid = pkt < a.n;
-    // ---- header windows (as dag_kernel) ----
-    const bool sw = stride_windows(a);
-    dma_meta(a, L, 0, tile, lane);
-    if (sw) dma_window_stride(a, L.win, tile, lane);
-    dma_wait();
-    uintptr_t mb;
-    uint32_t ml;
-    meta_of(a, L, 0, tile, lane, mb, ml);
-    const uint8_t* const base = (const uint8_t*)mb;
-    const uint32_t len = valid ? ml : 0u;
-    const bool co = sw || ballot(valid && ml != 0 && (mb & 15) != 0) == 0;
-    if (co) {
-      if (!sw) {
-        dma_window(a, L, 0, 0, tile, lane);
-        dma_wait();
-      }
+    const uint8_t* base;
+    uint32_t len;
+    if (FIXED) {
+      dma_window_stride(a, L.win, tile, lane);
+      base = a.frames + pkt * a.stride;
+      len = valid ? stride_len(a) : 0u;
+      dma_wait();
     } else {
-      stage_window_lane(my_win, my_swz, base, len, valid);
+      // ---- header windows (as dag_kernel) ----
+      const bool sw = stride_windows(a);
+      dma_meta(a, L, 0, tile, lane);
+      if (sw) dma_window_stride(a, L.win, tile, lane);
+      dma_wait();
+      uintptr_t mb;
+      uint32_t ml;
+      meta_of(a, L, 0, tile, lane, mb, ml);
+      base = (const uint8_t*)mb;
+      len = valid ? ml : 0u;
+      const bool co = sw || ballot(valid && ml != 0 && (mb & 15) != 0) == 0;
+      if (co) {
+        if (!sw) {
+          dma_window(a, L, 0, 0, tile, lane);
+          dma_wait();
+        }
+      } else {
+        stage_window_lane(my_win, my_swz, base, len, valid);
+      }
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);  // the window's LDS writes / metadata reads: done
 
@@ -1187,7 +1264,7 @@ __global__ __launch_bounds__(kBlock, 5) void dag_tile_kernel(LaunchArgs a) {
                                       (uint64_t)(uintptr_t)base, raddr, valid ? 1u : 0u);
 
     // ---- outputs: r0 (main.rs:43), status, verdict (xdp.rs:3-9), final image ----
-    if (a.mem_out && valid) {
+    if (!FIXED && a.mem_out && valid) {
       uint32_t* mo = (uint32_t*)(a.mem_out + pkt * (uint64_t)mem_size);
       const uint32_t m = min(len, mem_size);
       for (uint32_t d = 0; d < mem_size / 4; d++) {
@@ -1214,9 +1291,114 @@ __global__ __launch_bounds__(kBlock, 5) void dag_tile_kernel(LaunchArgs a) {
   flush_counters(a, cnt, retired, smem, lane, wv);
 }
 
-// One workgroup: read-and-clear every shard (device-scope atomics, coherent across XCDs) and
-// add the per-counter sums into the caller's counters. Stream order after interp_kernel makes
-// every shard add visible here; the shards are left zeroed for the next batch.
+// ============================================================================================
+// tile_kernel -- the forward-only fast path for programs of <= 63 micro-ops. The C++ part only
+// moves each tile's header windows HBM -> LDS (LDS-DMA) and turns the per-lane counter bucket
+// into ballots; everything in between is ONE hand-written asm statement (tile.inc, generated by
+// gen_tile.py): per-lane packet address/length, the register file in VGPRs with in-place indexed
+// access, min-pc dispatch with basic-block chaining, every tier-0 micro-op, mmu.rs faults, and the
+// verdict / r0 / status / register outputs. No per-lane C++ value lives across the statement, so
+// the kernel fits 64 VGPRs: 8 waves per SIMD.
+// FIXED: the stride layout with 16-byte aligned slots of >= 64 bytes, no lens array and no
+// final-image output (a NIC ring of fixed slots): no packet metadata at all.
+// ============================================================================================
+template <bool FIXED>
+__global__ __launch_bounds__(kBlock, 8) void tile_kernel(LaunchArgs a) {
+  counters_init();
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint32_t wv = rfl(threadIdx.x / kWave);  // wave-uniform: keeps LDS addresses scalar
+  WaveLds L;
+  L.win = smem + wv * kTileWaveLds;
+  L.meta_off = (uint32_t*)(L.win + kWinBytes);
+  L.meta_len = L.meta_off + kWave;
+  const uint32_t winb = lds_addr(L.win);
+  const uint32_t metab = lds_addr(L.meta_off);
+  const uint64_t wave_slot = (uint64_t)blockIdx.x * kWavesPerBlock + wv;
+  const uint64_t total_waves = (uint64_t)gridDim.x * kWavesPerBlock;
+  const auto ka = __builtin_amdgcn_kernarg_segment_ptr();
+
+  uint32_t cnt[7] = {0, 0, 0, 0, 0, 0, 0};  // per wave: < 2^32 packets
+  uint32_t retired = 0;                      // per lane: <= 63 steps per tile
+
+  for (uint64_t tile = wave_slot; tile < a.n_tiles; tile += total_waves) {
+    // the lane index is re-derived inside the loop (volatile: not hoistable), so no per-lane
+    // address of the window DMA stays live across the asm statement
+    if (!FIXED) {  // (FIXED: the asm statement DMAs the windows itself)
+      uint32_t lane;
+      asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+      const uint64_t pkt = tile * kWave + lane;
+      const bool valid = pkt < a.n;
+      const bool sw = stride_windows(a);
+      dma_meta(a, L, 0, tile, lane);
+      if (sw) dma_window_stride(a, L.win, tile, lane);
+      dma_wait();
+      uintptr_t mb;
+      uint32_t ml;
+      meta_of(a, L, 0, tile, lane, mb, ml);
+      const bool co = sw || ballot(valid && ml != 0 && (mb & 15) != 0) == 0;
+      if (co) {
+        if (!sw) {
+          dma_window(a, L, 0, 0, tile, lane);
+          dma_wait();
+        }
+      } else {
+        stage_window_lane(L.win + lane * kWin, win_swz(lane), (const uint8_t*)mb,
+                          valid ? ml : 0u, valid);
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // the window's LDS writes / metadata reads: done
+    }
+    const uint64_t t = rfl64(tile);
+    uint32_t bkt, nst;
+    asm volatile(
+#include "tile.inc"
+        : [bkt] "=&v"(bkt), [nst] "=&v"(nst)
+        : [ka] "s"(ka), [tile] "s"(t), [winb] "s"(winb), [metab] "s"(metab),
+          [fixed] "i"(FIXED ? 1 : 0), [o_tprog] "i"(offsetof(LaunchArgs, tprog)),
+          [o_frames] "i"(offsetof(LaunchArgs, frames)), [o_stride] "i"(offsetof(LaunchArgs, stride)),
+          [o_n] "i"(offsetof(LaunchArgs, n)), [o_mem] "i"(offsetof(LaunchArgs, mem_size)),
+          [o_offsets] "i"(offsetof(LaunchArgs, offsets)), [o_lens] "i"(offsetof(LaunchArgs, lens)),
+          [o_init] "i"(offsetof(LaunchArgs, init_regs)), [o_r10] "i"(offsetof(LaunchArgs, r10)),
+          [o_verdict] "i"(offsetof(LaunchArgs, verdict)), [o_r0] "i"(offsetof(LaunchArgs, r0)),
+          [o_status] "i"(offsetof(LaunchArgs, status)), [o_regs] "i"(offsetof(LaunchArgs, regs_out))
+        : "s33", "s34", "s35", "s36", "s37", "s38", "s39", "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53", "s54", "s55", "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15", "v16", "v17", "v18", "v19", "v20", "v21", "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32", "v33", "v34", "v35", "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", "vcc", "scc", "memory");
+
+    // ---- final image (Emu.state.mmu.memory): the window, then the packet, then zeros ----
+    if (!FIXED && a.mem_out) {
+      uint32_t ln;
+      asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+      const uint64_t pk = tile * kWave + ln;
+      if (pk < a.n) {
+        uintptr_t mb;
+        uint32_t ml;
+        meta_of(a, L, 0, tile, ln, mb, ml);
+        const uint32_t len = ml;
+        const uint8_t* base = (const uint8_t*)mb;
+        const uint32_t mem_size = a.mem_size;
+        uint32_t* mo = (uint32_t*)(a.mem_out + pk * (uint64_t)mem_size);
+        const uint32_t m = min(len, mem_size);
+        for (uint32_t d = 0; d < mem_size / 4; d++) {
+          uint32_t v;
+          if (d * 4 >= m) v = 0u;
+          else if (d * 4 < (uint32_t)kWin) v = (uint32_t)win_read(L.win + ln * kWin, win_swz(ln), d * 4, 4, len);
+          else v = (uint32_t)pkt_read(base, d * 4, 4, len);
+          mo[d] = v;
+        }
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < 7; b++) cnt[b] += __builtin_popcountll(ballot(bkt == (uint32_t)b));
+    retired += nst;
+  }
+  uint64_t cnt64[7];
+#pragma unroll
+  for (int b = 0; b < 7; b++) cnt64[b] = cnt[b];
+  uint32_t ln;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+  flush_counters(a, cnt64, retired, smem, ln, wv);
+}
+
+// Folds the shards into the caller's counters (EBPFEMU_FOLD=kernel A/B mode): one workgroup,
+// launched after the interpreter on the same stream.
 __global__ __launch_bounds__(kCounterShards * 8) void fold_counters(uint64_t* shards,
                                                                      uint64_t* counters) {
   __shared__ uint64_t fold[kCounterShards * 8];
@@ -1229,6 +1411,16 @@ __global__ __launch_bounds__(kCounterShards * 8) void fold_counters(uint64_t* sh
     if (t) atomicAdd((unsigned long long*)&counters[threadIdx.x], (unsigned long long)t);
   }
 }
+
+// A/B switches: EBPFEMU_FOLD=kernel (separate fold kernel), EBPFEMU_FIXED=0 (no lean variant)
+static bool g_fold_kernel = [] {
+  const char* e = getenv("EBPFEMU_FOLD");
+  return e && e[0] == 'k';
+}();
+static bool g_fixed = [] {
+  const char* e = getenv("EBPFEMU_FIXED");
+  return !e || e[0] != '0';
+}();
 
 static bool g_db = [] {  // tier-0 window double-buffering (EBPFEMU_TIER0_DB=0|1 for A/B runs)
   const char* e = getenv("EBPFEMU_TIER0_DB");
@@ -1243,12 +1435,18 @@ static int g_dag_variant = [] {
   return e ? atoi(e) : 19;
 }();
 
+// A/B knob (EBPFEMU_LDS_PAD=bytes): extra dynamic LDS per workgroup, to lower occupancy on purpose.
+static uint32_t g_lds_pad = [] {
+  const char* e = getenv("EBPFEMU_LDS_PAD");
+  return e ? (uint32_t)atoi(e) : 0u;
+}();
+
 static uint32_t lds_bytes_for(int kind, uint32_t n_uops) {
   if (kind == kKindDag)  // the program is fetched by SMEM
-    return kWavesPerBlock * (n_uops <= 64 && g_dag_variant == 19 ? kTileWaveLds : kDagWaveLds);
+    return g_lds_pad +
+           kWavesPerBlock * (n_uops <= 64 && g_dag_variant == 19 ? kTileWaveLds : kDagWaveLds);
   const uint32_t prog = n_uops <= (uint32_t)kMaxLdsUops ? n_uops * (uint32_t)sizeof(Uop) : 0u;
   uint32_t rest = kind == kKindTier0 ? kWavesPerBlock * wave_lds0(g_db) : 0u;
-  if (rest < kWavesPerBlock * 8 * 8) rest = kWavesPerBlock * 8 * 8;  // counter reduction scratch
   return prog + rest;
 }
 
@@ -1263,14 +1461,24 @@ static const void* variant(uint32_t n_uops) {
 
 
 
-static const void* kernel_for(int kind, uint32_t n_uops) {
+// The tile kernel's lean variant serves the fixed-slot stride layout without image output.
+static bool fixed_layout(const LaunchArgs* a) {
+  return g_fixed && a && a->offsets == nullptr && a->lens == nullptr && a->mem_out == nullptr &&
+         a->stride >= (uint64_t)kWin && (((uintptr_t)a->frames | (uintptr_t)a->stride) & 15) == 0;
+}
+
+static const void* kernel_for(int kind, uint32_t n_uops, const LaunchArgs* a = nullptr) {
   if (kind == kKindDag) {
     if (n_uops > 64) return (const void*)dag_kernel<4, 3>;
     // 19: the self-contained tile loop (default); 11: the hand-written loop with a C++ step
     // for the rest; 3: the C++ step only
     if (g_dag_variant == 3) return (const void*)dag_kernel<1, 3>;
     if (g_dag_variant == 11) return (const void*)dag_kernel<1, 11>;
-    return (const void*)dag_tile_kernel;
+    if (n_uops < kTileUops && g_dag_variant == 19)
+      return fixed_layout(a) ? (const void*)tile_kernel<true> : (const void*)tile_kernel<false>;
+    if (g_dag_variant == 20)  // the previous self-contained tile loop (A/B)
+      return fixed_layout(a) ? (const void*)dag_tile_kernel<true> : (const void*)dag_tile_kernel<false>;
+    return (const void*)dag_kernel<1, 3>;
   }
   if (kind == kKindTier1) return variant<1, false>(n_uops);
   return g_db ? variant<0, true>(n_uops) : variant<0, false>(n_uops);
@@ -1326,10 +1534,12 @@ int interp_grid(int kind, uint32_t n_uops, bool tiny, uint64_t n_tiles, int* gri
 
 hipError_t launch_interp(int kind, const LaunchArgs& a, int grid, hipStream_t stream) {
   const uint32_t lds = lds_bytes_for(kind, a.n_uops);
-  void* args[] = {(void*)&a};
+  LaunchArgs b = a;
+  b.fold_kernel = g_fold_kernel ? 1u : 0u;
+  void* bargs[] = {(void*)&b};
   hipError_t e =
-      hipLaunchKernel(kernel_for(kind, a.n_uops), dim3(grid), dim3(kBlock), args, lds, stream);
-  if (e != hipSuccess || a.counters == nullptr) return e;
+      hipLaunchKernel(kernel_for(kind, a.n_uops, &a), dim3(grid), dim3(kBlock), bargs, lds, stream);
+  if (e != hipSuccess || a.counters == nullptr || !g_fold_kernel) return e;
   uint64_t* shards = a.shards;
   uint64_t* counters = a.counters;
   void* fargs[] = {(void*)&shards, (void*)&counters};

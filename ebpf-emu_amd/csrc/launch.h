@@ -15,9 +15,11 @@ constexpr int kWinStride = kWin + 4;  // padded per-lane LDS stride: 17 dwords, 
 constexpr int kMaxLdsUops = 4096;     // programs up to this many micro-ops are staged in LDS
 constexpr int kCallDepth = 64;        // EBPF_MAX_CALL_DEPTH
 constexpr int kCounterShards = 64;    // device-atomic counter shards (spread contention)
-// workspace layout: [reserved 256 B][shards u64[64][8]][tier-1 wave slots]
-constexpr uint64_t kWsShardsOff = 256;
-constexpr uint64_t kWsSlotsOff = 256 + kCounterShards * 8 * 8;
+// workspace layout: [arrival tickets u32[64 + 1], padded to 512 B][shards u64[64][8]]
+// [tier-1 wave slots]; tickets and shards are zero between batches
+constexpr uint64_t kWsTicketsOff = 0;
+constexpr uint64_t kWsShardsOff = 512;
+constexpr uint64_t kWsSlotsOff = kWsShardsOff + kCounterShards * 8 * 8;
 
 // Kernel kinds: the two memory tiers of interp_kernel, and dag_kernel (tier-0 programs whose
 // jumps all go forward, run with max_steps >= n_uops so no step budget can bind).
@@ -27,6 +29,7 @@ constexpr uint32_t kMaxDagUops = 256;
 struct LaunchArgs {
   const Uop* prog;      // device micro-ops
   const DUop* dprog;    // device DAG micro-ops (kKindDag)
+  const TUop* tprog;    // device tile micro-ops (kKindDag, <= 63 micro-ops), else null
   uint32_t n_uops;
   uint32_t mem_size;
   const uint8_t* frames;
@@ -41,11 +44,13 @@ struct LaunchArgs {
   uint8_t* status;
   uint64_t* counters;   // optional caller counters [8] (added to)
   uint64_t* shards;     // workspace: [kCounterShards][8] partial counters (left zeroed)
+  uint32_t* tickets;    // workspace: [kCounterShards] per-shard arrivals + [1] shard arrivals
   uint8_t* image_ws;    // tier 1: per-wave-slot images + call stacks
   uint64_t n_tiles;     // ceil(n / 64)
   const uint64_t* init_regs;  // optional [11] initial registers (else main.rs layout)
   uint8_t* mem_out;           // optional [n][mem_size] final images
   uint64_t* regs_out;         // optional [n][11] final registers
+  uint32_t fold_kernel;       // 1: shards are folded by fold_counters after the launch (A/B)
 };
 
 // Bytes of tier-1 scratch per wave slot: lane-interleaved image dwords + call stack.
@@ -62,7 +67,7 @@ constexpr uint32_t kTinyUops = 8;
 // balanced persistent waves (bounds the per-wave image scratch).
 int interp_grid(int kind, uint32_t n_uops, bool tiny, uint64_t n_tiles, int* grid_out);
 
-// Enqueue the interpreter, then (when counters are requested) fold_counters on the same stream.
+// Enqueue the interpreter on `stream`; with counters, its last workgroup folds the shards into them.
 hipError_t launch_interp(int kind, const LaunchArgs& a, int grid, hipStream_t stream);
 
 }  // namespace ebpfemu

@@ -147,7 +147,7 @@ int ebpf_prog_upload(ebpf_prog* prog, int device);
 /* Run a batch on the device owning `stream` (NULL = the current device's null stream).
  * Replaces, per packet, Emu::default() + Mmu setup + Emu::run() + reading state.regs[0]
  * (main.rs:14-43, emu.rs:30-45,452-458). Asynchronous, stream-ordered: one interpreter
- * kernel, plus a one-workgroup counter fold kernel when out->counters is set. */
+ * kernel; with out->counters, its last workgroup folds the per-shard sums into them. */
 int ebpf_run_batch(ebpf_prog* prog, const ebpf_batch* batch, const ebpf_batch_out* out,
                    ebpf_stream_t stream);
 

@@ -1,2 +1,2 @@
-P="cd /tmp && export TMPDIR=/tmp && rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof5 -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 50 --warmup 5 --cpu-seconds 0"
-bash tools/gpu_session.sh "tests|400|python -m pytest tests -m gpu -q" "bench|300|python bench.py" "bd|120|python bench.py --config drop --cpu-seconds 0" "bc|120|python bench.py --config checksum --cpu-seconds 0" "prof5|240|$P" "pmc5|600|bash tools/pmc.sh t5 --config 5tuple"
+B="python bench.py --cpu-seconds 0 --steps 100"
+bash tools/gpu_session.sh "tests|300|python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread" "b5|120|$B" "bd|120|$B --config drop" "b5old|120|EBPFEMU_DAG_VARIANT=20 EBPFEMU_FIXED=0 EBPFEMU_FOLD=kernel $B" "bdold|120|EBPFEMU_DAG_VARIANT=20 EBPFEMU_FIXED=0 EBPFEMU_FOLD=kernel $B --config drop"
