@@ -57,8 +57,11 @@ M = {
     "KML": u(6), "KMH": u(7), "NBIT": u(8, 2), "TBIT": u(10, 2),
     "IMM": u(12, 2), "IMML": u(12), "IMMH": u(13), "WID": u(14), "END": u(15),
     "UOP": u(0, 16),
-    # LDXK window dwords (overlaying fields LDXK does not use)
-    "W0": u(2), "W1": u(4), "W2": u(10), "W3": u(11), "W4": u(12), "W5": u(13),
+    # LDXK: byte offsets of the window dwords (a0 & ~3) + 0/4/8 (clamped to 60), the end address,
+    # the bit shift of a one-dword access; steps to take back on a fault (REMK for LDXK, REMX for
+    # LDX and ARSH64); BLEN: the length of the basic block this micro-op starts (retired steps)
+    "W0": u(2), "W1": u(10), "W2": u(11), "KEND": u(4), "KSHIFT": u(12), "REMK": u(14),
+    "REMX": u(5), "BLEN": u(15),
     # divider: its mode lives in the (dead after dispatch) handler offset
     "MODE": u(0),
     # prologue / epilogue scratch inside the micro-op registers
@@ -105,7 +108,7 @@ READ_A = f"{on('SRC0')}\nv_mov_b64 {{A}}, {{RF}}\n{OFF}"
 READ_S = f"{on('SRC0', '{SRC2}')}\nv_mov_b64 {{S}}, {{RF}}\n{OFF}"
 WRITE_R = f"{on('DST')}\nv_mov_b64 {{RF}}, {{R}}\n{OFF}"
 WRITE_R32 = f"{on('DST')}\nv_mov_b32 {{RF0}}, {{RL}}\nv_mov_b32 {{RF1}}, 0\n{OFF}"
-STEP = "v_add_u32 {NST}, 1, {NST}"
+STEP = ""  # steps are counted per basic block at dispatch (BLEN); faults take back REM
 
 # Find the lowest parked pc (bit 63 = the DONE sentinel), fetch its micro-op, narrow exec to the
 # lanes parked there, jump to its handler.
@@ -116,6 +119,7 @@ s_lshl_b32 {PCOFF}, {P}, 6
 s_load_dwordx16 {UOP}, {PROG}, {PCOFF}
 v_cmpx_eq_u32 vcc, {P}, {LPC}
 s_waitcnt lgkmcnt(0)
+v_add_u32 {NST}, {BLEN}, {NST}
 s_add_u32 {JTL}, {SLOTBL}, {HOFF}
 s_addc_u32 {JTH}, {SLOTBH}, 0
 s_setpc_b64 {JT}"""
@@ -144,14 +148,16 @@ s_or_b64 {LIVE}, {LIVE}, {T1}
 """ + DISPATCH
 
 
-def fault_split(tag, status):
-    """vcc = faulting lanes among the active ones: they stop with `status`; exec continues with
-    the others (to the dispatcher when there are none)."""
+def fault_split(tag, status, rem):
+    """vcc = faulting lanes among the active ones: they stop with `status` (the steps of their
+    block from this micro-op on, `rem`, are not retired); exec continues with the others (to the
+    dispatcher when there are none)."""
     return f"""s_mov_b64 {{T4}}, exec
 s_and_b64 exec, {{T4}}, vcc
 s_cbranch_scc0 .Lnf_{tag}%=
 v_mov_b32 {{ST}}, {status}
 v_mov_b32 {{LPC}}, -1
+v_subrev_u32 {{NST}}, {rem}, {{NST}}
 .Lnf_{tag}%=:
 s_andn2_b64 exec, {{T4}}, vcc
 s_cbranch_scc0 .Ldisp%="""
@@ -202,7 +208,7 @@ s_mov_b32 {{T3}}, 0x80000000
 v_cmp_eq_u32_e64 {{T1}}, {{T3}}, {{t1}}
 s_and_b64 {{T0}}, {{T0}}, {{T1}}
 s_and_b64 vcc, vcc, {{T0}}
-{fault_split(tag, ST_ARITH)}
+{fault_split(tag, ST_ARITH, "{REMX}")}
 {WRITE_R}"""
 
 
@@ -242,8 +248,8 @@ def jump(cmp, reg, pre=""):
 # form's tail)
 H = {
     "H_EXIT": ("v_mov_b32 {LPC}, -1\n" + STEP + "\n" + DISPATCH, "term"),
-    "H_FAULT": ("v_mov_b32 {ST}, {IMML}\nv_mov_b32 {LPC}, -1\n" + DISPATCH, "term"),
-    "H_SLOW": (f"v_mov_b32 {{ST}}, {ST_INSN}\nv_mov_b32 {{LPC}}, -1\n" + DISPATCH, "term"),
+    "H_FAULT": ("v_mov_b32 {ST}, {IMML}\nv_mov_b32 {LPC}, -1\nv_subrev_u32 {NST}, 1, {NST}\n" + DISPATCH, "term"),
+    "H_SLOW": (f"v_mov_b32 {{ST}}, {ST_INSN}\nv_mov_b32 {{LPC}}, -1\nv_subrev_u32 {{NST}}, 1, {{NST}}\n" + DISPATCH, "term"),
     "H_MOV64_IMM": (f"{on('DST')}\nv_mov_b32 {{RF0}}, {{IMML}}\nv_mov_b32 {{RF1}}, {{IMMH}}\n{OFF}", "alu"),
     "H_MOV64_REG": (f"{READ_S}\n{on('DST')}\nv_mov_b64 {{RF}}, {{S}}\n{OFF}", "alu"),
     "H_ADD64_IMM": (f"{on('SRC0,DST')}\nv_lshl_add_u64 {{RF}}, {{RF}}, 0, {{IMM}}\n{OFF}", "alu"),
@@ -328,6 +334,8 @@ v_perm_b32 {{RH}}, {{AL}}, {{AL}}, {{T3}}
     "H_JSET32_REG": (jump("v_cmp_ne_u32 vcc, 0, {t0}", True,
                           f"{on('SRC1')}\nv_and_b32 {{t0}}, {{SL}}, {{RF0}}\n{OFF}\n"), "jump"),
     "H_LDXK": ("ldxk", "ool"),
+    "H_LDXK1": ("ldxk1", "ool"),
+    "H_LDXK2": ("ldxk2", "ool"),
     "H_LDXK_FAR": ("ldxkfar", "ool"),
     "H_LDX": ("ldx", "ool"),
 }
@@ -335,12 +343,10 @@ DONE = "H_DONE"
 
 
 def window_addr(dst, b):
-    """LDS address of window dword b (VGPR, a multiple of 4) of this lane: the 16-byte chunk
-    (b & 0x30) is XOR-swizzled per lane (interp.hip win_off)."""
-    return f"""v_and_b32 {{t18}}, 48, {b}
-v_xor_b32 {{t18}}, {{t18}}, {{SWZ}}
-v_and_b32 {{t19}}, 15, {b}
-v_add3_u32 {dst}, {{WIN}}, {{t18}}, {{t19}}"""
+    """LDS address of window dword b (a multiple of 4) of this lane: the 16-byte chunk bits
+    (b & 0x30) are XOR-swizzled per lane (interp.hip win_off); SWZ has only bits 4-5 set, so
+    the address is (b ^ SWZ) + WIN."""
+    return f"v_xad_u32 {dst}, {{SWZ}}, {b}, {{WIN}}"
 
 
 def window_tail(a0, shift):
@@ -404,18 +410,73 @@ s_mov_b64 exec, {save}
 s_waitcnt vmcnt(0)"""
 
 
+def kcheck():
+    return "s_cmp_gt_u32 {KEND}, {KMEM}\ns_cbranch_scc1 .Lkfault%="
+
+
+def ldxk1(sfx):
+    """LDXK, the access inside one window dword (a0 % 4 + width <= 4): shift it down, zero the
+    bytes at or past len (not in the FIXED layout, where packets are >= 64 bytes), merge into the
+    low word of dst (upper bytes kept, Q1; the high word is untouched)."""
+    return f""".Lldxk1{sfx}%=:
+{kcheck()}
+{window_addr("{WD0}", "{W0}")}
+ds_read_b32 {{WD0}}, {{WD0}}
+.if %[fixed] == 0
+v_subrev_u32 {{LENM}}, {{A0}}, {{LEN}}
+v_min_u32 {{LENM}}, 4, {{LENM}}
+v_lshlrev_b32 {{LENM}}, 3, {{LENM}}
+v_sub_u32 {{LENM}}, 32, {{LENM}}
+.endif
+{WAIT}
+v_lshrrev_b32 {{RL}}, {{KSHIFT}}, {{WD0}}
+.if %[fixed] == 0
+v_lshlrev_b32 {{RL}}, {{LENM}}, {{RL}}
+v_lshrrev_b32 {{RL}}, {{LENM}}, {{RL}}
+v_cmp_lt_u32 vcc, {{A0}}, {{LEN}}
+v_cndmask_b32 {{RL}}, 0, {{RL}}, vcc
+.endif
+{on('SRC2,DST')}
+v_bfi_b32 {{RF0}}, {{KML}}, {{RL}}, {{RF0}}
+{OFF}
+{TAILS[sfx]}"""
+
+
+def ldxk2(sfx):
+    """LDXK, a width <= 4 access spanning two window dwords."""
+    return f""".Lldxk2{sfx}%=:
+{kcheck()}
+{window_addr("{WD0}", "{W0}")}
+{window_addr("{WD1}", "{W1}")}
+ds_read_b32 {{WD0}}, {{WD0}}
+ds_read_b32 {{WD1}}, {{WD1}}
+.if %[fixed] == 0
+v_subrev_u32 {{LENM}}, {{A0}}, {{LEN}}
+v_min_u32 {{LENM}}, 4, {{LENM}}
+v_lshlrev_b32 {{LENM}}, 3, {{LENM}}
+v_sub_u32 {{LENM}}, 32, {{LENM}}
+.endif
+{WAIT}
+v_alignbyte_b32 {{RL}}, {{WD1}}, {{WD0}}, {{A0}}
+.if %[fixed] == 0
+v_lshlrev_b32 {{RL}}, {{LENM}}, {{RL}}
+v_lshrrev_b32 {{RL}}, {{LENM}}, {{RL}}
+v_cmp_lt_u32 vcc, {{A0}}, {{LEN}}
+v_cndmask_b32 {{RL}}, 0, {{RL}}, vcc
+.endif
+{on('SRC2,DST')}
+v_bfi_b32 {{RF0}}, {{KML}}, {{RL}}, {{RF0}}
+{OFF}
+{TAILS[sfx]}"""
+
+
 def ldxk(sfx):
-    """LDXK: constant address a0 = A0 inside the window, end = END; window dword i at chunk bits
-    W[2i] (xor'ed with the lane swizzle), byte-in-chunk W[2i + 1]."""
+    """LDXK, general (8-byte) form: constant address a0 = A0 inside the window, end = KEND."""
     return f""".Lldxk{sfx}%=:
-s_cmp_gt_u32 {{END}}, {{KMEM}}
-s_cbranch_scc1 .Lkfault%=
-v_xor_b32 {{WD0}}, {{W0}}, {{SWZ}}
-v_add3_u32 {{WD0}}, {{WIN}}, {{WD0}}, {{W1}}
-v_xor_b32 {{WD1}}, {{W2}}, {{SWZ}}
-v_add3_u32 {{WD1}}, {{WIN}}, {{WD1}}, {{W3}}
-v_xor_b32 {{WD2}}, {{W4}}, {{SWZ}}
-v_add3_u32 {{WD2}}, {{WIN}}, {{WD2}}, {{W5}}
+{kcheck()}
+{window_addr("{WD0}", "{W0}")}
+{window_addr("{WD1}", "{W1}")}
+{window_addr("{WD2}", "{W2}")}
 ds_read_b32 {{WD0}}, {{WD0}}
 ds_read_b32 {{WD1}}, {{WD1}}
 ds_read_b32 {{WD2}}, {{WD2}}
@@ -431,6 +492,7 @@ s_cmp_ge_u32 {{A0}}, {{KMEM}}
 s_cselect_b32 {{T3}}, {ST_MEM}, {ST_MEM_UB}
 v_mov_b32 {{ST}}, {{T3}}
 v_mov_b32 {{LPC}}, -1
+v_subrev_u32 {{NST}}, {{REMK}}, {{NST}}
 .Ldisp%=:
 {DISPATCH}"""
 
@@ -438,7 +500,7 @@ v_mov_b32 {{LPC}}, -1
 def ldxkfar(sfx):
     """LDXK outside the window: a0 < 2^32 (the host faults larger constants statically)."""
     return f""".Lldxkfar{sfx}%=:
-s_cmp_gt_u32 {{END}}, {{KMEM}}
+s_cmp_gt_u32 {{KEND}}, {{KMEM}}
 s_cbranch_scc1 .Lkfault%=
 v_mov_b32 {{t7}}, {{A0}}
 v_mov_b32 {{WD0}}, 0
@@ -458,26 +520,21 @@ s_and_b32 {{T3}}, {{A0}}, 3
 
 
 def ldx(sfx):
-    """LDX: address = S + sext(off) (IMM), mmu.rs bounds per lane: signed overflow or addr >= mem
-    -> ST_MEM, addr + width > mem -> ST_MEM_UB (emu.rs:344, mmu.rs:13-30); then the window
-    (addr + width <= 64), or the packet bytes past it, or zeros past the packet."""
+    """LDX: address = S + sext(off) (IMM), mmu.rs bounds per lane: the high word != 0 (every
+    signed-overflowing sum has one too: emu.rs:344's panic, ST_MEM like the reference's slice
+    panic) or addr >= mem -> ST_MEM; addr + width > mem -> ST_MEM_UB (mmu.rs:13-30); then the
+    window (addr + width <= 64), or the packet bytes past it, or zeros past the packet."""
     return f""".Lldx{sfx}%=:
 {READ_S}
 v_lshl_add_u64 {{T01}}, {{S}}, 0, {{IMM}}
-v_xor_b32 {{t2}}, {{SH}}, {{t1}}
-v_xor_b32 {{t3}}, {{IMMH}}, {{t1}}
-v_and_b32 {{t2}}, {{t2}}, {{t3}}
-v_cmp_gt_i32_e64 {{T0}}, 0, {{t2}}
-v_cmp_ne_u32_e64 {{T1}}, 0, {{t1}}
-s_or_b64 {{T0}}, {{T0}}, {{T1}}
+v_cmp_ne_u32_e64 {{T0}}, 0, {{t1}}
 v_cmp_le_u32_e64 {{T1}}, {{KMEM}}, {{t0}}
 s_or_b64 {{T0}}, {{T0}}, {{T1}}
 v_add_u32 {{t4}}, {{WID}}, {{t0}}
-v_cmp_lt_u32_e64 {{T1}}, {{KMEM}}, {{t4}}
-s_andn2_b64 {{T1}}, {{T1}}, {{T0}}
-s_or_b64 vcc, {{T0}}, {{T1}}
+v_cmp_lt_u32_e64 vcc, {{KMEM}}, {{t4}}
+s_or_b64 vcc, vcc, {{T0}}
 v_cndmask_b32_e64 {{t5}}, {ST_MEM_UB}, {ST_MEM}, {{T0}}
-{fault_split("ldx" + sfx, "{t5}")}
+{fault_split("ldx" + sfx, "{t5}", "{REMX}")}
 v_cmp_lt_u32_e64 {{T1}}, 64, {{t4}}
 v_cndmask_b32_e64 {{t6}}, {{t0}}, 0, {{T1}}
 v_and_b32 {{t6}}, -4, {{t6}}
@@ -507,23 +564,29 @@ v_and_b32 {{SHF}}, 3, {{t0}}
 
 
 def window_tail_ldx(a0, shift):
-    """As window_tail, but the bytes may come from far_read (past the window), where the bytes
-    past len must be zeroed in every layout."""
-    return f"""v_sub_u32_e64 {{LENM}}, {{LEN}}, {a0}
+    """As window_tail for a register-based address, whose bytes may also come from far_read.
+    Bytes past len read as zero (main.rs:16): in the FIXED layout every packet is >= 64 bytes
+    and a multiple of 16 long, so window bytes are packet bytes and far_read's whole-dword
+    selection already zeroes the rest; otherwise mask them."""
+    return f""".if %[fixed] == 0
+v_sub_u32_e64 {{LENM}}, {{LEN}}, {a0}
 v_cmp_lt_u32 vcc, {a0}, {{LEN}}
 v_cndmask_b32 {{LENM}}, 0, {{LENM}}, vcc
 v_min_u32 {{LENM}}, 8, {{LENM}}
 v_lshlrev_b32 {{LENM}}, 3, {{LENM}}
 v_sub_u32 {{LENM}}, 64, {{LENM}}
+.endif
 {WAIT}
 v_alignbyte_b32 {{RL}}, {{WD1}}, {{WD0}}, {shift}
 v_alignbyte_b32 {{RH}}, {{WD2}}, {{WD1}}, {shift}
+.if %[fixed] == 0
 v_and_b32 {{RL}}, {{KML}}, {{RL}}
 v_and_b32 {{RH}}, {{KMH}}, {{RH}}
 v_lshlrev_b64 {{R}}, {{LENM}}, {{R}}
 v_lshrrev_b64 {{R}}, {{LENM}}, {{R}}
 v_cndmask_b32 {{RL}}, 0, {{RL}}, vcc
 v_cndmask_b32 {{RH}}, 0, {{RH}}, vcc
+.endif
 {on('SRC2,DST')}
 v_bfi_b32 {{RF0}}, {{KML}}, {{RL}}, {{RF0}}
 v_bfi_b32 {{RF1}}, {{KMH}}, {{RH}}, {{RF1}}
@@ -675,8 +738,9 @@ s_cselect_b64 {LIVE}, 1, 0
 s_bitset1_b64 {LIVE}, 63
 s_cmp_lg_u64 {KINIT}, 0
 s_cbranch_scc1 .Linitc%=
-""" + "\n".join(f"v_mov_b32 v{i}, 0" for i in range(22) if i not in (4, 20, 21)) + """
+""" + "\n".join(f"v_mov_b64 v[{i}:{i + 1}], 0" for i in range(0, 20, 2) if i != 4) + """
 v_mov_b32 v4, {LEN}
+v_mov_b32 v5, 0
 v_mov_b32 v20, {KR10L}
 v_mov_b32 v21, {KR10H}
 s_branch .Linitd%=
@@ -790,7 +854,7 @@ def main():
         parts.append(f"; {name}\n.org .Lslots%=+{idx * SLOT}\n" + code)
     parts.append(f".org .Lslots%=+{len(table) * SLOT}")
     for sfx in ("c", "e"):
-        parts += [ldxk(sfx), ldxkfar(sfx), ldx(sfx), divmod(sfx)]
+        parts += [ldxk(sfx), ldxk1(sfx), ldxk2(sfx), ldxkfar(sfx), ldx(sfx), divmod(sfx)]
     parts += [KFAULT, EPILOGUE]
     text = F("\n".join(parts))
     assert "{" not in text, "unsubstituted register name: " + text[text.index("{"):][:40]

@@ -360,20 +360,27 @@ static std::vector<TUop> build_tile(const std::vector<Uop>& uops, const std::vec
   const uint32_t n = (uint32_t)uops.size();
   std::vector<TUop> t(kTileUops);
   std::memset(t.data(), 0, t.size() * sizeof(TUop));
-  std::vector<char> start(n + 1, 0);  // block starts: 0, jump targets, successors of block ends
+  // block starts: 0, jump targets, successors of block-ending micro-ops
+  std::vector<char> start(n + 1, 0);
   start[0] = 1;
+  std::vector<char> term(n, 0);  // jumps, exits, faults: always the end of their block
   for (uint32_t i = 0; i < n; i++) {
     const uint32_t h = d[i].hoff / DAG_SLOT;
     const bool is_jump = uops[i].op >= U_JA && uops[i].op <= U_JLE32;
     if (is_jump && (uint32_t)uops[i].x < n) start[(uint32_t)uops[i].x] = 1;
-    if (is_jump || h == H_EXIT || h == H_FAULT || h == H_SLOW) start[i + 1] = 1;
+    term[i] = is_jump || h == H_EXIT || h == H_FAULT || h == H_SLOW;
+    if (term[i]) start[i + 1] = 1;
   }
+  // rem[i]: micro-ops from i to the end of its block (steps not retired when i faults);
+  // blen[i] = rem[i] for a block start (the steps its lanes retire unless one faults)
+  std::vector<uint32_t> rem(n + 1, 0);
+  for (uint32_t i = n; i-- > 0;) rem[i] = (term[i] || start[i + 1]) ? 1 : rem[i + 1] + 1;
   for (uint32_t i = 0; i < n; i++) {
     const DUop& o = d[i];
     TUop& u = t[i];
-    const uint32_t h = o.hoff / DAG_SLOT;
-    const bool chained = i + 1 < n && !start[i + 1];
-    u.hoff = (uint32_t)(chained ? kTileIdChained[h] : kTileIdEnd[h]) * TILE_SLOT;
+    uint32_t h = o.hoff / DAG_SLOT;
+    const bool chained = !term[i] && i + 1 < n && !start[i + 1];
+    uint32_t id = chained ? kTileIdChained[h] : kTileIdEnd[h];
     u.dst2 = o.dst2;
     u.src2 = o.src2;
     u.npc = o.anpc;
@@ -384,13 +391,26 @@ static std::vector<TUop> build_tile(const std::vector<Uop>& uops, const std::vec
     u.tbit = o.atbit;
     u.imm = o.imm;
     u.width = o.width;
-    u.end = o.end;
-    if (h == H_LDXK) {  // window dwords in the fields LDXK does not use
-      u.src2 = o.win[0];
-      u.x = o.win[1];
-      u.tbit = (uint64_t)o.win[2] | ((uint64_t)o.win[3] << 32);
-      u.imm = (uint64_t)o.win[4] | ((uint64_t)o.win[5] << 32);
+    u.blen = start[i] ? rem[i] : 0;
+    if (h == H_LDX || h == H_ARSH64_IMM || h == H_ARSH64_REG) u.a0 = rem[i];  // REMX
+    if (h == H_LDXK || h == H_LDXK_FAR) {
+      const uint32_t a0 = o.a0, w = o.end - o.a0;
+      u.x = o.end;      // KEND
+      u.width = rem[i]; // REMK
+      if (h == H_LDXK) {
+        const uint32_t b0 = a0 & ~3u;
+        u.src2 = b0;                                     // W0
+        const uint32_t b1 = std::min(b0 + 4, (uint32_t)kWin - 4), b2 = std::min(b0 + 8, (uint32_t)kWin - 4);
+        u.tbit = (uint64_t)b1 | ((uint64_t)b2 << 32);    // W1, W2
+        if ((a0 & 3) + w <= 4) {
+          id = chained ? T_LDXK1_C : T_LDXK1_E;
+          u.imm = (a0 & 3) * 8;                          // KSHIFT
+        } else if (w <= 4) {
+          id = chained ? T_LDXK2_C : T_LDXK2_E;
+        }
+      }
     }
+    u.hoff = id * TILE_SLOT;
   }
   t[kTileUops - 1].hoff = T_DONE * TILE_SLOT;
   return t;

@@ -1412,11 +1412,17 @@ __global__ __launch_bounds__(kCounterShards * 8) void fold_counters(uint64_t* sh
   }
 }
 
-// A/B switches: EBPFEMU_FOLD=kernel (separate fold kernel), EBPFEMU_FIXED=0 (no lean variant)
-static bool g_fold_kernel = [] {
+// Counter fold: fold_counters after the launch, or the launch's last workgroup (two-level arrival
+// ticket). In-kernel, the last wave of every workgroup waits for its shard adds before its ticket
+// while holding the workgroup's LDS, so it only pays with few workgroups: the tile kernel's
+// balanced persistent grid (5-tuple, 1 Mi packets, one MI355X: 30.3 us in-kernel vs 31.1 us with
+// fold_counters; one tile per wave: 36.9 vs 32.2). Default: in-kernel for tile_kernel, the fold
+// kernel otherwise. EBPFEMU_FOLD=kernel|inkernel forces one for A/B runs.
+static int g_fold_mode = [] {
   const char* e = getenv("EBPFEMU_FOLD");
-  return e && e[0] == 'k';
+  return !e ? -1 : e[0] == 'i' ? 0 : 1;
 }();
+// A/B: EBPFEMU_FIXED=0 disables the fixed-slot variants
 static bool g_fixed = [] {
   const char* e = getenv("EBPFEMU_FIXED");
   return !e || e[0] != '0';
@@ -1461,6 +1467,11 @@ static const void* variant(uint32_t n_uops) {
 
 
 
+// Programs that run on tile_kernel.
+static bool tile_kernel_for(int kind, uint32_t n_uops) {
+  return kind == kKindDag && n_uops < kTileUops && g_dag_variant == 19;
+}
+
 // The tile kernel's lean variant serves the fixed-slot stride layout without image output.
 static bool fixed_layout(const LaunchArgs* a) {
   return g_fixed && a && a->offsets == nullptr && a->lens == nullptr && a->mem_out == nullptr &&
@@ -1474,7 +1485,7 @@ static const void* kernel_for(int kind, uint32_t n_uops, const LaunchArgs* a = n
     // for the rest; 3: the C++ step only
     if (g_dag_variant == 3) return (const void*)dag_kernel<1, 3>;
     if (g_dag_variant == 11) return (const void*)dag_kernel<1, 11>;
-    if (n_uops < kTileUops && g_dag_variant == 19)
+    if (tile_kernel_for(kind, n_uops))
       return fixed_layout(a) ? (const void*)tile_kernel<true> : (const void*)tile_kernel<false>;
     if (g_dag_variant == 20)  // the previous self-contained tile loop (A/B)
       return fixed_layout(a) ? (const void*)dag_tile_kernel<true> : (const void*)dag_tile_kernel<false>;
@@ -1517,7 +1528,10 @@ int interp_grid(int kind, uint32_t n_uops, bool tiny, uint64_t n_tiles, int* gri
   const uint64_t resident = (uint64_t)cus * (uint64_t)per_cu * kWavesPerBlock;
   const uint64_t tiles = n_tiles ? n_tiles : 1;
   uint64_t waves;
-  const int policy = g_grid >= 0 ? g_grid : kind == kKindTier1 ? 0 : tiny ? 1 : 2;
+  // tile_kernel: balanced persistent waves (few workgroups: cheap in-kernel counter fold)
+  const int policy = g_grid >= 0 ? g_grid
+                     : kind == kKindTier1 || tile_kernel_for(kind, n_uops) ? 0
+                     : tiny ? 1 : 2;
   if (policy == 1) {
     waves = tiles < resident ? tiles : resident;  // every resident slot, grid-stride
   } else if (policy == 2 && kind != kKindTier1) {
@@ -1535,11 +1549,14 @@ int interp_grid(int kind, uint32_t n_uops, bool tiny, uint64_t n_tiles, int* gri
 hipError_t launch_interp(int kind, const LaunchArgs& a, int grid, hipStream_t stream) {
   const uint32_t lds = lds_bytes_for(kind, a.n_uops);
   LaunchArgs b = a;
-  b.fold_kernel = g_fold_kernel ? 1u : 0u;
+  // (tiny programs: the fold kernel measured 20.4 vs 23.8 us in-kernel for drop-all)
+  const bool fold_kernel =
+      g_fold_mode >= 0 ? g_fold_mode == 1 : !tile_kernel_for(kind, a.n_uops) || a.n_uops <= kTinyUops;
+  b.fold_kernel = fold_kernel ? 1u : 0u;
   void* bargs[] = {(void*)&b};
   hipError_t e =
       hipLaunchKernel(kernel_for(kind, a.n_uops, &a), dim3(grid), dim3(kBlock), bargs, lds, stream);
-  if (e != hipSuccess || a.counters == nullptr || !g_fold_kernel) return e;
+  if (e != hipSuccess || a.counters == nullptr || !fold_kernel) return e;
   uint64_t* shards = a.shards;
   uint64_t* counters = a.counters;
   void* fargs[] = {(void*)&shards, (void*)&counters};

@@ -104,17 +104,17 @@ static_assert(sizeof(DUop) == 256, "DUop must be 256 bytes");
 struct alignas(64) TUop {
   uint32_t hoff;   // d0: handler slot offset (tile_ids.h id * TILE_SLOT): chained or block-end form
   uint32_t dst2;   // d1: 2 * dst
-  uint32_t src2;   // d2: 2 * src; LDXK: window dword 0 chunk bits
+  uint32_t src2;   // d2: 2 * src; LDXK: byte offset of window dword 0 (a0 & ~3)
   uint32_t npc;    // d3: pc + 1, or PC_DONE (canonical jumps: the not-taken successor)
-  uint32_t x;      // d4: jump target, or PC_DONE past the end; LDXK: window dword 0 byte
-  uint32_t a0;     // d5: LDXK: the image address
+  uint32_t x;      // d4: jump target, or PC_DONE past the end; LDXK: a0 + width
+  uint32_t a0;     // d5: LDXK: the image address; LDX / ARSH64: steps not retired on a fault
   uint64_t kmask;  // d6-7: LDX/LDXK: mask of the access width's low bytes
   uint64_t nbit;   // d8-9: 1 << npc (0 for PC_DONE)
-  uint64_t tbit;   // d10-11: 1 << x; LDXK: window dword 1 {chunk bits, byte}
+  uint64_t tbit;   // d10-11: 1 << x; LDXK: byte offsets of window dwords 1, 2
   uint64_t imm;    // d12-13: the immediate as the handler consumes it; LDX: the offset;
-                   //         LDXK: window dword 2 {chunk bits, byte}
-  uint32_t width;  // d14: LDX access width
-  uint32_t end;    // d15: LDXK: a0 + width
+                   //         one-dword LDXK: the bit shift (a0 % 4) * 8
+  uint32_t width;  // d14: LDX access width; LDXK: steps not retired on a fault
+  uint32_t blen;   // d15: block start: length of its basic block (steps retired at dispatch)
 };
 static_assert(sizeof(TUop) == 64, "TUop must be 64 bytes");
 constexpr uint32_t kTileUops = 64;   // table entries (63 micro-ops + the DONE sentinel)

@@ -1,2 +1,2 @@
 B="python bench.py --cpu-seconds 0 --steps 100"
-bash tools/gpu_session.sh "tests|300|python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread" "b5|120|$B" "bd|120|$B --config drop" "b5old|120|EBPFEMU_DAG_VARIANT=20 EBPFEMU_FIXED=0 EBPFEMU_FOLD=kernel $B" "bdold|120|EBPFEMU_DAG_VARIANT=20 EBPFEMU_FIXED=0 EBPFEMU_FOLD=kernel $B --config drop"
+bash tools/gpu_session.sh "tests|300|python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread" "b5|120|$B" "bd|120|$B --config drop" "b5k|120|EBPFEMU_FOLD=kernel $B"
