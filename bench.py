@@ -217,8 +217,7 @@ def main():
                 "kernel_avg_us": round(kern_avg_ms * 1e3, 3),
                 # HIP events bracket one whole batch: one interpreter launch (with counters, its
                 # last workgroup folds the per-shard sums into them)
-                "kernel": (("ebpfemu::dag_tile_kernel" if len(prog) <= 64 else "ebpfemu::dag_kernel")
-                           if prog.forward_only else f"ebpfemu::interp_kernel<{prog.tier}>"),
+                "kernel": kernel_name(prog),
             },
             "counters": {"drop": cnt[1], "pass": cnt[2], "other": cnt[5], "faults": cnt[6],
                          "insns_retired": cnt[7]},
@@ -228,6 +227,15 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def kernel_name(prog):
+    """The kernel ebpf_run_batch picks for this program (interp.hip kernel_for)."""
+    if prog.tier == 0 and len(prog) <= 62:
+        return "ebpfemu::tile_kernel<" + ("forward" if prog.forward_only else "loops") + ">"
+    if prog.forward_only:
+        return "ebpfemu::dag_kernel"
+    return f"ebpfemu::interp_kernel<{prog.tier}>"
 
 
 def cpu_baseline(args, img, batch0, mixed, n, mem_size, r10):

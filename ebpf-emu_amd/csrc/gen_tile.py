@@ -74,13 +74,17 @@ M = {
     "SLOTB": "s[56:57]", "SLOTBL": "s56", "SLOTBH": "s57", "VM": "s[58:59]",
     "T0": "s[60:61]", "T1": "s[62:63]", "T4": "s[64:65]", "T5": "s[66:67]", "T7": "s[68:69]",
     "PCOFF": "s70",
+    # loop mode: the step budget (max_steps, clamped to 32 bits)
+    "MAXS": "s71",
     # the jump target and the dispatcher's pc use temporaries dead at that point
     "JT": "s[60:61]", "JTL": "s60", "JTH": "s61", "P": "s62",
     # every wave of the kernel is full: the statement runs with exec = all 64 lanes
     "EXEC0": "-1",
     # VGPRs: the register file r_i = v[2i : 2i+1] is v[0:21]
     "RF": "v[0:1]", "RF0": "v0", "RF1": "v1",
-    "A": "v[22:23]", "AL": "v22", "AH": "v23",
+    "A": "v[54:55]", "AL": "v54", "AH": "v55",
+    # loop mode: the packet offset of this lane's 64-byte LDS window (refilled on demand)
+    "WB": "v22",
     "S": "v[24:25]", "SL": "v24", "SH": "v25",
     "R": "v[26:27]", "RL": "v26", "RH": "v27",
     "LPC": "v28", "NST": "v29", "ST": "v30", "LEN": "v31",
@@ -91,7 +95,7 @@ for i in range(20):
 for i in range(0, 20, 2):
     M[f"T{i}{i + 1}"] = f"v[{36 + i}:{37 + i}]"
 M.update({"WD0": M["t13"], "WD1": M["t14"], "WD2": M["t15"], "SHF": M["t16"], "LENM": M["t17"]})
-SGPRS = list(range(33, 71))
+SGPRS = list(range(33, 72))
 
 
 def F(text):
@@ -120,6 +124,10 @@ s_load_dwordx16 {UOP}, {PROG}, {PCOFF}
 v_cmpx_eq_u32 vcc, {P}, {LPC}
 s_waitcnt lgkmcnt(0)
 v_add_u32 {NST}, {BLEN}, {NST}
+.if %[loops]
+v_cmp_lt_u32 vcc, {MAXS}, {NST}
+s_cbranch_vccnz .Lbudget%=
+.endif
 s_add_u32 {JTL}, {SLOTBL}, {HOFF}
 s_addc_u32 {JTH}, {SLOTBH}, 0
 s_setpc_b64 {JT}"""
@@ -486,6 +494,38 @@ s_and_b32 {{T3}}, {{A0}}, 3
 {TAILS[sfx]}"""
 
 
+# Step budget (loop mode). Block mode: some lane could run out of budget inside this block --
+# restart the tile in exact mode (the one-micro-op-per-block table: a dispatch is one step), where
+# the budget is checked before every step as the reference's max_steps (oracle: ST_STEPS when
+# steps == max_steps before an instruction). Bit 62 of the pc set marks exact mode (entry 62 of
+# every table is a second DONE sentinel). The restart re-reads the window from the packet where
+# refills are possible (WB = -64: no byte is in the window) and keeps it otherwise (never refilled).
+BUDGET = f""".Lbudget%=:
+s_bitcmp1_b64 {{LIVE}}, 62
+s_cbranch_scc1 .Lbexact%=
+s_load_dwordx2 {{PROG}}, %[ka], %[o_tprog_exact]
+s_mov_b64 exec, -1
+s_mov_b64 {{LIVE}}, 0
+s_bitset1_b64 {{LIVE}}, 62
+s_cmp_eq_u32 %[aligned], 0
+s_cbranch_scc1 .Lbkeep%=
+v_mov_b32 {{WB}}, -64
+.Lbkeep%=:
+s_waitcnt lgkmcnt(0)
+s_branch .Lreinit%=
+.Lbexact%=:
+s_mov_b64 {{T4}}, exec
+s_mov_b64 exec, vcc
+v_mov_b32 {{ST}}, 5
+v_mov_b32 {{LPC}}, -1
+v_subrev_u32 {{NST}}, 1, {{NST}}
+s_andn2_b64 exec, {{T4}}, vcc
+s_cbranch_scc0 .Ldisp%=
+s_add_u32 {{JTL}}, {{SLOTBL}}, {{HOFF}}
+s_addc_u32 {{JTH}}, {{SLOTBH}}, 0
+s_setpc_b64 {{JT}}"""
+
+
 # a fault of a constant-address load hits every active lane alike (mmu.rs:13-30)
 KFAULT = f""".Lkfault%=:
 s_cmp_ge_u32 {{A0}}, {{KMEM}}
@@ -560,6 +600,81 @@ s_mov_b64 exec, {{T5}}
 v_and_b32 {{SHF}}, 3, {{t0}}
 {window_tail_ldx("{t0}", "{SHF}")}
 {STEP}
+{TAILS[sfx]}"""
+
+
+def ldx_loop(sfx):
+    """LDX in loop mode: the lane's 64-byte LDS window holds packet bytes [WB, WB + 64). An access
+    outside it (that needs packet bytes, a < len) refills it from WB = a & ~15 with four 16-byte
+    loads (chunks wholly past the packet are skipped: their bytes read as zero anyway) -- when
+    every packet base of the tile is 16-byte aligned (%[aligned]), so that no 16-byte load
+    leaves the page of a packet byte; otherwise such lanes read the packet dwords directly
+    (far_read). Bounds and faults as ldx()."""
+    return f""".Lldxl{sfx}%=:
+{READ_S}
+v_lshl_add_u64 {{T01}}, {{S}}, 0, {{IMM}}
+v_cmp_ne_u32_e64 {{T0}}, 0, {{t1}}
+v_cmp_le_u32_e64 {{T1}}, {{KMEM}}, {{t0}}
+s_or_b64 {{T0}}, {{T0}}, {{T1}}
+v_add_u32 {{t4}}, {{WID}}, {{t0}}
+v_cmp_lt_u32_e64 vcc, {{KMEM}}, {{t4}}
+s_or_b64 vcc, vcc, {{T0}}
+v_cndmask_b32_e64 {{t5}}, {ST_MEM_UB}, {ST_MEM}, {{T0}}
+{fault_split("ldxl" + sfx, "{t5}", "{REMX}")}
+v_sub_u32 {{t6}}, {{t0}}, {{WB}}
+s_sub_u32 {{T3}}, 64, {{WID}}
+v_cmp_lt_u32_e64 {{T1}}, {{T3}}, {{t6}}
+v_cmp_lt_u32_e64 {{T0}}, {{t0}}, {{LEN}}
+s_and_b64 {{T7}}, {{T1}}, {{T0}}
+s_cbranch_scc0 .Lldxl_win{sfx}%=
+s_cmp_eq_u32 %[aligned], 0
+s_cbranch_scc1 .Lldxl_win{sfx}%=
+s_mov_b64 {{T5}}, exec
+s_mov_b64 exec, {{T7}}
+v_and_b32 {{WB}}, -16, {{t0}}
+v_mov_b32 {{t7}}, 0
+v_mov_b32 {{t6}}, {{WB}}
+v_lshl_add_u64 {{T67}}, {{BASE}}, 0, {{T67}}
+""" + "\n".join(f"""v_add_u32 {{t1}}, {16 * c}, {{WB}}
+v_cmp_lt_u32 vcc, {{t1}}, {{LEN}}
+s_and_b64 exec, {{T7}}, vcc
+global_load_dwordx4 {reg}, {{T67}}, off offset:{16 * c}""" for c, reg in
+               enumerate(("v[44:47]", "v[48:51]", "v[52:55]", "v[38:41]"))) + f"""
+s_mov_b64 exec, {{T7}}
+s_waitcnt vmcnt(0)
+""" + "\n".join(f"""v_xad_u32 {{t1}}, {{SWZ}}, {16 * c}, {{WIN}}
+ds_write_b128 {{t1}}, {reg}""" for c, reg in
+                 enumerate(("v[44:47]", "v[48:51]", "v[52:55]", "v[38:41]"))) + f"""
+s_waitcnt lgkmcnt(0)
+s_mov_b64 exec, {{T5}}
+.Lldxl_win{sfx}%=:
+v_sub_u32 {{t6}}, {{t0}}, {{WB}}
+v_and_b32 {{t6}}, -4, {{t6}}
+v_min_u32 {{t6}}, 60, {{t6}}
+{window_addr("{WD0}", "{t6}")}
+v_add_u32 {{t7}}, 4, {{t6}}
+v_min_u32 {{t7}}, 60, {{t7}}
+{window_addr("{WD1}", "{t7}")}
+v_add_u32 {{t7}}, 8, {{t6}}
+v_min_u32 {{t7}}, 60, {{t7}}
+{window_addr("{WD2}", "{t7}")}
+ds_read_b32 {{WD0}}, {{WD0}}
+ds_read_b32 {{WD1}}, {{WD1}}
+ds_read_b32 {{WD2}}, {{WD2}}
+v_sub_u32 {{t6}}, {{t0}}, {{WB}}
+s_sub_u32 {{T3}}, 64, {{WID}}
+v_cmp_lt_u32_e64 {{T1}}, {{T3}}, {{t6}}
+v_cmp_lt_u32_e64 {{T0}}, {{t0}}, {{LEN}}
+s_and_b64 {{T7}}, {{T1}}, {{T0}}
+s_cbranch_scc0 .Lldxl_near{sfx}%=
+{WAIT}
+s_mov_b64 {{T5}}, exec
+s_mov_b64 exec, {{T7}}
+{far_read("{t0}", "ldxl" + sfx)}
+s_mov_b64 exec, {{T5}}
+.Lldxl_near{sfx}%=:
+v_and_b32 {{SHF}}, 3, {{t0}}
+{window_tail_ldx("{t0}", "{SHF}")}
 {TAILS[sfx]}"""
 
 
@@ -640,6 +755,7 @@ TAILS = {"c": CHAIN, "e": END_N}
 # %[tile]: the tile index (64-bit SGPR pair); %[winb]: this wave's window region (LDS byte
 # address); %[metab]: this wave's metadata region (offsets u32[64], lengths u32[64]).
 PROLOGUE = """s_mov_b32 {M0S}, m0
+s_mov_b64 {LIVE}, 0
 s_load_dwordx2 {PROG}, %[ka], %[o_tprog]
 s_load_dwordx2 {KFR}, %[ka], %[o_frames]
 s_load_dwordx2 {KST}, %[ka], %[o_stride]
@@ -649,8 +765,6 @@ s_load_dword {KMEM}, %[ka], %[o_mem]
 s_load_dwordx2 {KOFF}, %[ka], %[o_offsets]
 s_load_dwordx2 {KLEN}, %[ka], %[o_lens]
 .endif
-s_load_dwordx2 {KINIT}, %[ka], %[o_init]
-s_load_dwordx2 {KR10}, %[ka], %[o_r10]
 v_mbcnt_lo_u32_b32 {t0}, -1, 0
 v_mbcnt_hi_u32_b32 {t0}, -1, {t0}
 s_lshl_b64 {T0}, %[tile], 6
@@ -722,6 +836,14 @@ v_add_u32 {WIN}, %[winb], {WIN}
 v_lshrrev_b32 {SWZ}, 2, {t0}
 v_and_b32 {SWZ}, 3, {SWZ}
 v_lshlrev_b32 {SWZ}, 4, {SWZ}
+.if %[loops]
+s_load_dwordx2 {T5}, %[ka], %[o_maxs]
+v_mov_b32 {WB}, 0
+s_waitcnt lgkmcnt(0)
+s_cmp_lg_u32 s67, 0
+s_cselect_b32 {MAXS}, -1, s66
+.endif
+.Lreinit%=:
 v_mov_b32 {NST}, 0
 v_mov_b32 {ST}, 0
 v_mov_b32 {LPC}, -1
@@ -734,8 +856,12 @@ s_mov_b64 exec, {T1}
 v_mov_b32 {LPC}, 0
 s_mov_b64 exec, {EXEC0}
 s_cmp_lg_u64 {T1}, 0
-s_cselect_b64 {LIVE}, 1, 0
+s_cselect_b64 {T0}, 1, 0
+s_or_b64 {LIVE}, {LIVE}, {T0}
 s_bitset1_b64 {LIVE}, 63
+s_load_dwordx2 {KINIT}, %[ka], %[o_init]
+s_load_dwordx2 {KR10}, %[ka], %[o_r10]
+s_waitcnt lgkmcnt(0)
 s_cmp_lg_u64 {KINIT}, 0
 s_cbranch_scc1 .Linitc%=
 """ + "\n".join(f"v_mov_b64 v[{i}:{i + 1}], 0" for i in range(0, 20, 2) if i != 4) + """
@@ -848,14 +974,17 @@ def main():
                 code = (body + "\n" if body else "") + STEP + "\n" + TAILS[sfx]
             elif kind == "div":
                 code = body + f"\ns_branch .Ldivmod{sfx}%="
+            elif body == "ldx":  # ool, two modes
+                code = f".if %[loops]\ns_branch .Lldxl{sfx}%=\n.else\ns_branch .Lldx{sfx}%=\n.endif"
             else:  # ool
                 code = f"s_branch .L{body}{sfx}%="
         code = re.sub(r"\.L(nf_\w+?)%=", lambda m: f".L{m.group(1)}_{idx}%=", code)
         parts.append(f"; {name}\n.org .Lslots%=+{idx * SLOT}\n" + code)
     parts.append(f".org .Lslots%=+{len(table) * SLOT}")
     for sfx in ("c", "e"):
-        parts += [ldxk(sfx), ldxk1(sfx), ldxk2(sfx), ldxkfar(sfx), ldx(sfx), divmod(sfx)]
-    parts += [KFAULT, EPILOGUE]
+        parts += [ldxk(sfx), ldxk1(sfx), ldxk2(sfx), ldxkfar(sfx), ldx(sfx), ldx_loop(sfx),
+                  divmod(sfx)]
+    parts += [KFAULT, ".if %[loops]", BUDGET, ".endif", EPILOGUE]
     text = F("\n".join(parts))
     assert "{" not in text, "unsubstituted register name: " + text[text.index("{"):][:40]
     out = ["// GENERATED by gen_tile.py -- do not edit. One inline-asm statement (tile_kernel).",

@@ -224,10 +224,20 @@ struct ebpf_prog {
   Uop* dev_uops[kMaxDevices] = {};
   DUop* dev_duops[kMaxDevices] = {};
   DUop* dev_duopsk[kMaxDevices] = {};
-  std::vector<TUop> tuops, tuopsk;  // tile_kernel's tables (<= 63 micro-ops), from duops / duopsk
+  std::vector<TUop> tuops, tuopsk;  // tile_kernel's tables (forward-only, <= 62 micro-ops)
   TUop* dev_tuops[kMaxDevices] = {};
   TUop* dev_tuopsk[kMaxDevices] = {};
+  // tile_kernel in loop mode (any tier-0 program of <= 62 micro-ops): block and exact tables
+  std::vector<TUop> ltuops, ltuopsx;
+  TUop* dev_ltuops[kMaxDevices] = {};
+  TUop* dev_ltuopsx[kMaxDevices] = {};
 };
+
+// A/B: EBPFEMU_NO_LOOP=1 runs loop programs on the general interpreter (interp_kernel).
+static const bool g_no_loop = [] {
+  const char* e = getenv("EBPFEMU_NO_LOOP");
+  return e && e[0] == '1';
+}();
 
 // EBPFEMU_NO_DAG=1 runs every tier-0 program on interp_kernel (A/B runs, differential tests).
 static const bool g_no_dag = [] {
@@ -356,7 +366,9 @@ static std::vector<DUop> build_dag(const std::vector<Uop>& uops) {
 // tile_kernel's table (uop.h TUop) from the DUop table. A micro-op whose successor no jump can
 // reach (and that is not itself a jump, exit or fault) gets the CHAINED handler form: the tile loop
 // runs its successor next on the same lanes without touching the pc set (basic-block chaining).
-static std::vector<TUop> build_tile(const std::vector<Uop>& uops, const std::vector<DUop>& d) {
+// exact: every micro-op its own block (the loop mode's exact-budget table).
+static std::vector<TUop> build_tile(const std::vector<Uop>& uops, const std::vector<DUop>& d,
+                                    bool exact = false) {
   const uint32_t n = (uint32_t)uops.size();
   std::vector<TUop> t(kTileUops);
   std::memset(t.data(), 0, t.size() * sizeof(TUop));
@@ -368,7 +380,7 @@ static std::vector<TUop> build_tile(const std::vector<Uop>& uops, const std::vec
     const uint32_t h = d[i].hoff / DAG_SLOT;
     const bool is_jump = uops[i].op >= U_JA && uops[i].op <= U_JLE32;
     if (is_jump && (uint32_t)uops[i].x < n) start[(uint32_t)uops[i].x] = 1;
-    term[i] = is_jump || h == H_EXIT || h == H_FAULT || h == H_SLOW;
+    term[i] = exact || is_jump || h == H_EXIT || h == H_FAULT || h == H_SLOW;
     if (term[i]) start[i + 1] = 1;
   }
   // rem[i]: micro-ops from i to the end of its block (steps not retired when i faults);
@@ -413,6 +425,7 @@ static std::vector<TUop> build_tile(const std::vector<Uop>& uops, const std::vec
     u.hoff = id * TILE_SLOT;
   }
   t[kTileUops - 1].hoff = T_DONE * TILE_SLOT;
+  t[kTileUops - 2].hoff = T_DONE * TILE_SLOT;  // exact-mode marker bit (loop mode)
   return t;
 }
 
@@ -547,10 +560,15 @@ int ebpf_prog_load(const uint8_t* code, size_t nbytes, ebpf_prog** out, size_t* 
   if (forward && p->tier == 0 && !p->uops.empty() && p->uops.size() <= kMaxDagUops) {
     p->duops = build_dag(p->uops);
     p->duopsk = fold_const_loads(p->uops, p->duops);
-    if (p->uops.size() < kTileUops) {
+    if (p->uops.size() <= kTileMaxUops) {
       p->tuops = build_tile(p->uops, p->duops);
       p->tuopsk = build_tile(p->uops, p->duopsk);
     }
+  }
+  if (p->tier == 0 && !p->uops.empty() && p->uops.size() <= kTileMaxUops) {
+    const std::vector<DUop> d = p->duops.empty() ? build_dag(p->uops) : p->duops;
+    p->ltuops = build_tile(p->uops, d);
+    p->ltuopsx = build_tile(p->uops, d, true);
   }
   *out = p;
   return EBPF_OK;
@@ -577,6 +595,8 @@ void ebpf_prog_free(ebpf_prog* p) {
       if (p->dev_duopsk[d]) hipFree(p->dev_duopsk[d]);
       if (p->dev_tuops[d]) hipFree(p->dev_tuops[d]);
       if (p->dev_tuopsk[d]) hipFree(p->dev_tuopsk[d]);
+      if (p->dev_ltuops[d]) hipFree(p->dev_ltuops[d]);
+      if (p->dev_ltuopsx[d]) hipFree(p->dev_ltuopsx[d]);
     }
   }
   hipSetDevice(cur);
@@ -637,18 +657,24 @@ int ebpf_prog_upload(ebpf_prog* p, int device) {
   DUop* ddk = nullptr;
   TUop* td = nullptr;
   TUop* tdk = nullptr;
+  TUop* tl = nullptr;
+  TUop* tlx = nullptr;
   put(p->duops, &dd);
   put(p->duopsk, &ddk);
   putt(p->tuops, &td);
   putt(p->tuopsk, &tdk);
+  putt(p->ltuops, &tl);
+  putt(p->ltuopsx, &tlx);
   if (rc == EBPF_OK) {
     p->dev_uops[device] = d;
     p->dev_duops[device] = dd;
     p->dev_duopsk[device] = ddk;
     p->dev_tuops[device] = td;
     p->dev_tuopsk[device] = tdk;
+    p->dev_ltuops[device] = tl;
+    p->dev_ltuopsx[device] = tlx;
   } else {
-    for (void* q : {(void*)d, (void*)dd, (void*)ddk, (void*)td, (void*)tdk})
+    for (void* q : {(void*)d, (void*)dd, (void*)ddk, (void*)td, (void*)tdk, (void*)tl, (void*)tlx})
       if (q) hipFree(q);
   }
   hipSetDevice(cur);
@@ -699,10 +725,11 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* b, const ebpf_batch_out* out,
 
   const uint64_t n_tiles = (b->n + 63) / 64;
   // dag_kernel needs no step budget: a lane of a forward-only program retires <= n_uops steps
-  const int kind = (p->dev_duops[device] && b->max_steps >= p->uops.size() && !g_no_dag &&
-                    !(b->flags & EBPF_BATCH_GENERIC))
-                       ? kKindDag
-                       : p->tier;
+  // the tile kernel in loop mode: loops, or a step budget that can bind (exact budget)
+  const bool generic = g_no_dag || (b->flags & EBPF_BATCH_GENERIC);
+  const int kind = (p->dev_duops[device] && b->max_steps >= p->uops.size() && !generic) ? kKindDag
+                   : (p->dev_ltuops[device] && !generic && !g_no_loop)            ? kKindLoop
+                                                                                   : p->tier;
   int grid = 0;
   if (interp_grid(kind, (uint32_t)p->uops.size(), p->tiny, n_tiles, &grid) != 0) {
     if (cur != device) hipSetDevice(cur);
@@ -741,7 +768,9 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* b, const ebpf_batch_out* out,
   a.prog = p->dev_uops[device];
   // constant-address loads are resolved for the main.rs register layout only
   a.dprog = b->init_regs ? p->dev_duops[device] : p->dev_duopsk[device];
-  a.tprog = b->init_regs ? p->dev_tuops[device] : p->dev_tuopsk[device];
+  a.tprog = kind == kKindLoop ? p->dev_ltuops[device]
+           : b->init_regs      ? p->dev_tuops[device] : p->dev_tuopsk[device];
+  a.tprog_exact = p->dev_ltuopsx[device];
   a.n_uops = (uint32_t)p->uops.size();
   a.mem_size = b->mem_size;
   a.frames = b->frames;

@@ -1302,7 +1302,7 @@ __global__ __launch_bounds__(kBlock, 5) void dag_tile_kernel(LaunchArgs a) {
 // FIXED: the stride layout with 16-byte aligned slots of >= 64 bytes, no lens array and no
 // final-image output (a NIC ring of fixed slots): no packet metadata at all.
 // ============================================================================================
-template <bool FIXED>
+template <bool FIXED, bool LOOPS>
 __global__ __launch_bounds__(kBlock, 8) void tile_kernel(LaunchArgs a) {
   counters_init();
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -1323,6 +1323,7 @@ __global__ __launch_bounds__(kBlock, 8) void tile_kernel(LaunchArgs a) {
   for (uint64_t tile = wave_slot; tile < a.n_tiles; tile += total_waves) {
     // the lane index is re-derived inside the loop (volatile: not hoistable), so no per-lane
     // address of the window DMA stays live across the asm statement
+    uint32_t aligned = 1;  // every packet base of the tile 16-byte aligned (loop-mode refills)
     if (!FIXED) {  // (FIXED: the asm statement DMAs the windows itself)
       uint32_t lane;
       asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
@@ -1336,6 +1337,7 @@ __global__ __launch_bounds__(kBlock, 8) void tile_kernel(LaunchArgs a) {
       uint32_t ml;
       meta_of(a, L, 0, tile, lane, mb, ml);
       const bool co = sw || ballot(valid && ml != 0 && (mb & 15) != 0) == 0;
+      aligned = co ? 1u : 0u;
       if (co) {
         if (!sw) {
           dma_window(a, L, 0, 0, tile, lane);
@@ -1353,14 +1355,17 @@ __global__ __launch_bounds__(kBlock, 8) void tile_kernel(LaunchArgs a) {
 #include "tile.inc"
         : [bkt] "=&v"(bkt), [nst] "=&v"(nst)
         : [ka] "s"(ka), [tile] "s"(t), [winb] "s"(winb), [metab] "s"(metab),
-          [fixed] "i"(FIXED ? 1 : 0), [o_tprog] "i"(offsetof(LaunchArgs, tprog)),
+          [fixed] "i"(FIXED ? 1 : 0), [loops] "i"(LOOPS ? 1 : 0), [aligned] "s"(rfl(aligned)),
+          [o_tprog] "i"(offsetof(LaunchArgs, tprog)),
+          [o_tprog_exact] "i"(offsetof(LaunchArgs, tprog_exact)),
+          [o_maxs] "i"(offsetof(LaunchArgs, max_steps)),
           [o_frames] "i"(offsetof(LaunchArgs, frames)), [o_stride] "i"(offsetof(LaunchArgs, stride)),
           [o_n] "i"(offsetof(LaunchArgs, n)), [o_mem] "i"(offsetof(LaunchArgs, mem_size)),
           [o_offsets] "i"(offsetof(LaunchArgs, offsets)), [o_lens] "i"(offsetof(LaunchArgs, lens)),
           [o_init] "i"(offsetof(LaunchArgs, init_regs)), [o_r10] "i"(offsetof(LaunchArgs, r10)),
           [o_verdict] "i"(offsetof(LaunchArgs, verdict)), [o_r0] "i"(offsetof(LaunchArgs, r0)),
           [o_status] "i"(offsetof(LaunchArgs, status)), [o_regs] "i"(offsetof(LaunchArgs, regs_out))
-        : "s33", "s34", "s35", "s36", "s37", "s38", "s39", "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53", "s54", "s55", "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15", "v16", "v17", "v18", "v19", "v20", "v21", "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32", "v33", "v34", "v35", "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", "vcc", "scc", "memory");
+        : "s33", "s34", "s35", "s36", "s37", "s38", "s39", "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53", "s54", "s55", "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71", "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15", "v16", "v17", "v18", "v19", "v20", "v21", "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32", "v33", "v34", "v35", "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", "vcc", "scc", "memory");
 
     // ---- final image (Emu.state.mmu.memory): the window, then the packet, then zeros ----
     if (!FIXED && a.mem_out) {
@@ -1379,7 +1384,8 @@ __global__ __launch_bounds__(kBlock, 8) void tile_kernel(LaunchArgs a) {
         for (uint32_t d = 0; d < mem_size / 4; d++) {
           uint32_t v;
           if (d * 4 >= m) v = 0u;
-          else if (d * 4 < (uint32_t)kWin) v = (uint32_t)win_read(L.win + ln * kWin, win_swz(ln), d * 4, 4, len);
+          else if (!LOOPS && d * 4 < (uint32_t)kWin)  // (loop mode may have moved the window)
+            v = (uint32_t)win_read(L.win + ln * kWin, win_swz(ln), d * 4, 4, len);
           else v = (uint32_t)pkt_read(base, d * 4, 4, len);
           mo[d] = v;
         }
@@ -1448,9 +1454,12 @@ static uint32_t g_lds_pad = [] {
 }();
 
 static uint32_t lds_bytes_for(int kind, uint32_t n_uops) {
+  if (kind == kKindLoop) return g_lds_pad + kWavesPerBlock * kTileWaveLds;
   if (kind == kKindDag)  // the program is fetched by SMEM
     return g_lds_pad +
-           kWavesPerBlock * (n_uops <= 64 && g_dag_variant == 19 ? kTileWaveLds : kDagWaveLds);
+           kWavesPerBlock * ((n_uops <= kTileMaxUops && g_dag_variant == 19) ||
+                                     (n_uops <= 64 && g_dag_variant == 20)
+                                 ? kTileWaveLds : kDagWaveLds);
   const uint32_t prog = n_uops <= (uint32_t)kMaxLdsUops ? n_uops * (uint32_t)sizeof(Uop) : 0u;
   uint32_t rest = kind == kKindTier0 ? kWavesPerBlock * wave_lds0(g_db) : 0u;
   return prog + rest;
@@ -1467,9 +1476,9 @@ static const void* variant(uint32_t n_uops) {
 
 
 
-// Programs that run on tile_kernel.
+// Programs that run on tile_kernel (kKindLoop always does).
 static bool tile_kernel_for(int kind, uint32_t n_uops) {
-  return kind == kKindDag && n_uops < kTileUops && g_dag_variant == 19;
+  return kind == kKindLoop || (kind == kKindDag && n_uops <= kTileMaxUops && g_dag_variant == 19);
 }
 
 // The tile kernel's lean variant serves the fixed-slot stride layout without image output.
@@ -1486,11 +1495,13 @@ static const void* kernel_for(int kind, uint32_t n_uops, const LaunchArgs* a = n
     if (g_dag_variant == 3) return (const void*)dag_kernel<1, 3>;
     if (g_dag_variant == 11) return (const void*)dag_kernel<1, 11>;
     if (tile_kernel_for(kind, n_uops))
-      return fixed_layout(a) ? (const void*)tile_kernel<true> : (const void*)tile_kernel<false>;
+      return fixed_layout(a) ? (const void*)tile_kernel<true, false>
+                             : (const void*)tile_kernel<false, false>;
     if (g_dag_variant == 20)  // the previous self-contained tile loop (A/B)
       return fixed_layout(a) ? (const void*)dag_tile_kernel<true> : (const void*)dag_tile_kernel<false>;
     return (const void*)dag_kernel<1, 3>;
   }
+  if (kind == kKindLoop) return (const void*)tile_kernel<false, true>;
   if (kind == kKindTier1) return variant<1, false>(n_uops);
   return g_db ? variant<0, true>(n_uops) : variant<0, false>(n_uops);
 }
@@ -1530,6 +1541,7 @@ int interp_grid(int kind, uint32_t n_uops, bool tiny, uint64_t n_tiles, int* gri
   uint64_t waves;
   // tile_kernel: balanced persistent waves (few workgroups: cheap in-kernel counter fold)
   const int policy = g_grid >= 0 ? g_grid
+                     : kind == kKindLoop ? 2  // divergent tiles: one per wave
                      : kind == kKindTier1 || tile_kernel_for(kind, n_uops) ? 0
                      : tiny ? 1 : 2;
   if (policy == 1) {
@@ -1550,8 +1562,9 @@ hipError_t launch_interp(int kind, const LaunchArgs& a, int grid, hipStream_t st
   const uint32_t lds = lds_bytes_for(kind, a.n_uops);
   LaunchArgs b = a;
   // (tiny programs: the fold kernel measured 20.4 vs 23.8 us in-kernel for drop-all)
-  const bool fold_kernel =
-      g_fold_mode >= 0 ? g_fold_mode == 1 : !tile_kernel_for(kind, a.n_uops) || a.n_uops <= kTinyUops;
+  const bool fold_kernel = g_fold_mode >= 0 ? g_fold_mode == 1
+                           : kind != kKindDag || !tile_kernel_for(kind, a.n_uops) ||
+                                 a.n_uops <= kTinyUops;
   b.fold_kernel = fold_kernel ? 1u : 0u;
   void* bargs[] = {(void*)&b};
   hipError_t e =

@@ -23,13 +23,14 @@ constexpr uint64_t kWsSlotsOff = kWsShardsOff + kCounterShards * 8 * 8;
 
 // Kernel kinds: the two memory tiers of interp_kernel, and dag_kernel (tier-0 programs whose
 // jumps all go forward, run with max_steps >= n_uops so no step budget can bind).
-enum KernelKind : int { kKindTier0 = 0, kKindTier1 = 1, kKindDag = 2 };
+enum KernelKind : int { kKindTier0 = 0, kKindTier1 = 1, kKindDag = 2, kKindLoop = 3 };
 constexpr uint32_t kMaxDagUops = 256;
 
 struct LaunchArgs {
   const Uop* prog;      // device micro-ops
   const DUop* dprog;    // device DAG micro-ops (kKindDag)
-  const TUop* tprog;    // device tile micro-ops (kKindDag, <= 63 micro-ops), else null
+  const TUop* tprog;    // device tile micro-ops (kKindDag / kKindLoop, <= 62 micro-ops), else null
+  const TUop* tprog_exact;  // kKindLoop: the one-micro-op-per-block table (exact step budget)
   uint32_t n_uops;
   uint32_t mem_size;
   const uint8_t* frames;

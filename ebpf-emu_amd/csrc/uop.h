@@ -100,7 +100,7 @@ static_assert(sizeof(DUop) == 256, "DUop must be 256 bytes");
 
 // Micro-op of the tile interpreter (tile_kernel in interp.hip, tile.inc generated by gen_tile.py):
 // one s_load_dwordx16 per dispatch, dword i in s[64 + i]. Built from the DUop of the same pc
-// (build_tile in host.cpp); entry 63 of every table is the DONE sentinel.
+// (build_tile in host.cpp); entries 62 and 63 of every table are DONE sentinels.
 struct alignas(64) TUop {
   uint32_t hoff;   // d0: handler slot offset (tile_ids.h id * TILE_SLOT): chained or block-end form
   uint32_t dst2;   // d1: 2 * dst
@@ -117,7 +117,8 @@ struct alignas(64) TUop {
   uint32_t blen;   // d15: block start: length of its basic block (steps retired at dispatch)
 };
 static_assert(sizeof(TUop) == 64, "TUop must be 64 bytes");
-constexpr uint32_t kTileUops = 64;   // table entries (63 micro-ops + the DONE sentinel)
+constexpr uint32_t kTileUops = 64;     // table entries: micro-ops, then the DONE sentinels 62, 63
+constexpr uint32_t kTileMaxUops = 62;  // programs the tile kernels run
 static_assert(offsetof(DUop, opaux) == 128, "the C++ half starts at dword 32");
 
 }  // namespace ebpfemu

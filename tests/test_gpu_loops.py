@@ -1,0 +1,123 @@
+"""Loop mode of the tile interpreter (tile_kernel<..., LOOPS>, csrc/gen_tile.py): programs with back
+edges, or with a step budget that can bind, on MI355X. Bit-exact against the C oracle with the
+same budget (status of every packet; registers and image of every completing packet; counters
+including retired steps), and identical in every output to the general interpreter
+(EBPF_BATCH_GENERIC). Covers the two things loop mode adds:
+  * the exact step budget: a lane that would run out inside a basic block restarts the tile in
+    one-micro-op-per-block mode (emu.rs:452-458 has no limit; ST_STEPS is this build's);
+  * the refillable per-lane LDS window: loads past the first 64 bytes, forward, backward and
+    strided, in 16-byte aligned (refills) and misaligned (direct packet reads) layouts."""
+import random
+
+import pytest
+
+from test_gpu_parity import _check_against_oracle, _run_full, _same_outputs
+
+pytestmark = pytest.mark.gpu
+
+# r0 = sum of the packet bytes, forward (workloads.CHECKSUM without the fold)
+FORWARD_SUM = """
+    mov r0, 0
+    mov r3, 0
+    jge r3, r2, done
+loop:
+    mov r4, r1
+    add r4, r3
+    ldxb r5, [r4+0]
+    add r0, r5
+    add r3, 1
+    jlt r3, r2, loop
+done:
+    exit
+"""
+
+# backward scan of 16-bit words (every refill moves the window down)
+BACKWARD_WORDS = """
+    mov r0, 0
+    mov r3, r2
+loop:
+    jlt r3, 2, done
+    sub r3, 2
+    mov r4, r1
+    add r4, r3
+    ldxh r5, [r4+0]
+    xor r0, r5
+    lsh r0, 1
+    ja loop
+done:
+    exit
+"""
+
+# strided 4- and 8-byte reads (r3 = i * 37 mod len), some reading past len (zeros) or past the
+# image end (ST_MEM / ST_MEM_UB faults on the lanes whose packets make them do so)
+STRIDED = """
+    mov r0, 0
+    mov r3, 0
+    mov r6, 0
+loop:
+    jge r6, 40, done
+    add r6, 1
+    add r3, 37
+    mov r7, r3
+    mod r7, r2
+    mov r4, r1
+    add r4, r7
+    ldxw r5, [r4+0]
+    add r0, r5
+    ldxdw r5, [r4+3]
+    xor r0, r5
+    jset r5, 0x100, far
+    ja loop
+far:
+    ldxb r5, [r4+1000]
+    add r0, r5
+    ja loop
+done:
+    exit
+"""
+
+LOOP_PROGRAMS = [FORWARD_SUM, BACKWARD_WORDS, STRIDED]
+
+
+def _packets(rng, n):
+    lens = [0, 1, 2, 3, 15, 16, 17, 63, 64, 65, 100, 127, 128, 300, 700, 1000]
+    return [bytes(rng.getrandbits(8) for _ in range(rng.choice(lens))) for _ in range(n)]
+
+
+@pytest.mark.parametrize("layout", [dict(), dict(offsets_layout=True, align=16),
+                                    dict(offsets_layout=True, misalign=3)])
+def test_loop_programs_layouts(cuda, oracle_mod, layout):
+    from ebpf_emu.asm import assemble
+
+    rng = random.Random(11)
+    pkts = _packets(rng, 150)
+    for src in LOOP_PROGRAMS:
+        img = assemble(src)
+        got = _run_full(img, pkts, cuda, **layout)
+        _check_against_oracle(oracle_mod, img, pkts, got, tag=f"{layout} {src[:40]}")
+        _same_outputs(got, _run_full(img, pkts, cuda, generic=True, **layout), src)
+
+
+@pytest.mark.parametrize("budget", [1, 2, 3, 5, 6, 7, 8, 13, 50, 101, 997])
+def test_loop_step_budget_exact(cuda, oracle_mod, budget):
+    """Budgets that bind at every position of the loop body, for lanes of different lengths in
+    one tile: ST_STEPS exactly where the oracle stops (and faults before the budget win)."""
+    from ebpf_emu.asm import assemble
+
+    rng = random.Random(budget)
+    pkts = _packets(rng, 100)
+    for src in LOOP_PROGRAMS:
+        img = assemble(src)
+        got = _run_full(img, pkts, cuda, max_steps=budget, offsets_layout=True, align=16)
+        op = oracle_mod.Program(img)
+        retired = 0
+        for i, p in enumerate(pkts):
+            st, regs, mem, steps = op.run_full(p, 1024, 512, budget)
+            assert got["status"][i] == st, (budget, i, src[:40])
+            if st == 0:
+                assert [int(v) for v in got["regs"][i]] == regs, (budget, i)
+            retired += steps
+        assert int(got["counters"][7]) == retired, budget
+        gen = _run_full(img, pkts, cuda, max_steps=budget, offsets_layout=True, align=16,
+                        generic=True)
+        _same_outputs(got, gen, f"budget {budget}")
