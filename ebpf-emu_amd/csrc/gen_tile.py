@@ -905,6 +905,18 @@ v_mbcnt_hi_u32_b32 {t0}, -1, {t0}
 s_lshl_b64 {T0}, %[tile], 6
 v_mov_b32 {t1}, 0
 v_lshl_add_u64 {T23}, {T01}, 0, {T0}
+.if %[loops]
+s_load_dwordx2 {T1}, %[ka], %[o_perm]
+s_waitcnt lgkmcnt(0)
+s_cmp_lg_u64 {T1}, 0
+s_cbranch_scc0 .Lnoperm%=
+v_lshlrev_b64 {T45}, 2, {T23}
+v_lshl_add_u64 {T45}, {T45}, 0, {T1}
+global_load_dword {t2}, {T45}, off
+v_mov_b32 {t3}, 0
+s_waitcnt vmcnt(0)
+.Lnoperm%=:
+.endif
 s_load_dwordx2 {EV}, %[ka], %[o_verdict]
 s_load_dwordx2 {ER0}, %[ka], %[o_r0]
 s_load_dwordx2 {EST}, %[ka], %[o_status]

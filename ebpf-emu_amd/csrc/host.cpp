@@ -233,6 +233,14 @@ struct ebpf_prog {
   TUop* dev_ltuopsx[kMaxDevices] = {};
 };
 
+// Length-binned lane packing for the loop-mode tile kernel (EBPFEMU_BIN=0|1 forces it off/on;
+// default: offsets + lens layouts of >= kBinMinPackets packets).
+static const int g_bin = [] {
+  const char* e = getenv("EBPFEMU_BIN");
+  return e ? (e[0] == '1' ? 1 : 0) : -1;
+}();
+constexpr uint64_t kBinMinPackets = 16384;
+
 // A/B: EBPFEMU_NO_LOOP=1 runs loop programs on the general interpreter (interp_kernel).
 static const bool g_no_loop = [] {
   const char* e = getenv("EBPFEMU_NO_LOOP");
@@ -681,9 +689,16 @@ int ebpf_prog_upload(ebpf_prog* p, int device) {
   return rc;
 }
 
+// Whether a loop-mode batch runs in length-binned order.
+static bool use_binning(const ebpf_prog* p, const ebpf_batch* b) {
+  if (p->ltuops.empty() || !b->offsets || !b->lens || (b->flags & EBPF_BATCH_GENERIC)) return false;
+  return g_bin >= 0 ? g_bin == 1 : b->n >= kBinMinPackets;
+}
+
 uint64_t ebpf_workspace_bytes(const ebpf_prog* p, const ebpf_batch* b, int device) {
   if (!p || !b) return 0;
   uint64_t bytes = kWsSlotsOff;
+  if (use_binning(p, b)) bytes += b->n * 4;  // the binned packet order
   if (p->tier == 1) {
     int cur = device_of_current();
     hipSetDevice(device);
@@ -791,6 +806,14 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* b, const ebpf_batch_out* out,
   a.init_regs = b->init_regs;
   a.mem_out = out->mem;
   a.regs_out = out->regs;
+  if (kind == kKindLoop && use_binning(p, b)) {
+    a.perm = (const uint32_t*)(ws + kWsSlotsOff);
+    a.bin_counts = (uint32_t*)(ws + kWsBinCountsOff);
+    if (launch_binning(b->lens, b->n, a.bin_counts, (uint32_t*)a.perm, s) != hipSuccess) {
+      if (cur != device) hipSetDevice(cur);
+      return EBPF_EHIP;
+    }
+  }
   hipError_t e = launch_interp(kind, a, grid, s);
   if (cur != device) hipSetDevice(cur);
   return e == hipSuccess ? EBPF_OK : EBPF_EHIP;

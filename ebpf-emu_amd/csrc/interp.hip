@@ -1292,6 +1292,64 @@ __global__ __launch_bounds__(kBlock, 5) void dag_tile_kernel(LaunchArgs a) {
 }
 
 // ============================================================================================
+// Length-binned lane packing (loop mode, offsets + lens layouts). Lanes of a tile run until its
+// longest packet is done, so a tile mixing 64- and 1500-byte frames idles half its lanes in a
+// per-byte loop. A counting sort by class ceil(len / 128) (capped) groups similar lengths:
+// bin_hist counts the classes (per-workgroup LDS histogram, one device atomic per class per
+// workgroup), bin_scatter reserves each workgroup's range per class and writes the indices.
+// The order within a class is arbitrary; every output stays indexed by the original packet.
+// ============================================================================================
+constexpr int kBinBlock = 1024;
+
+__device__ __forceinline__ uint32_t bin_class(uint32_t len) {
+  const uint32_t c = (len + 127) >> 7;
+  return c < (uint32_t)kBinClasses ? c : (uint32_t)kBinClasses - 1;
+}
+
+__global__ __launch_bounds__(kBinBlock) void bin_hist(const uint16_t* lens, uint64_t n,
+                                                      uint32_t* bins) {
+  __shared__ uint32_t h[kBinClasses];
+  if (threadIdx.x < kBinClasses) h[threadIdx.x] = 0;
+  __syncthreads();
+  for (uint64_t i = (uint64_t)blockIdx.x * kBinBlock + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * kBinBlock)
+    atomicAdd(&h[bin_class(lens[i])], 1u);
+  __syncthreads();
+  if (threadIdx.x < kBinClasses && h[threadIdx.x]) atomicAdd(&bins[threadIdx.x], h[threadIdx.x]);
+}
+
+__global__ __launch_bounds__(kBinBlock) void bin_scatter(const uint16_t* lens, uint64_t n,
+                                                         uint32_t* bins, uint32_t* perm) {
+  __shared__ uint32_t h[kBinClasses], base[kBinClasses];
+  const uint32_t t = threadIdx.x;
+  if (t < kBinClasses) h[t] = 0;
+  __syncthreads();
+  for (uint64_t i = (uint64_t)blockIdx.x * kBinBlock + t; i < n; i += (uint64_t)gridDim.x * kBinBlock)
+    atomicAdd(&h[bin_class(lens[i])], 1u);
+  __syncthreads();
+  if (t < kBinClasses) {
+    uint32_t start = 0;  // exclusive prefix of the global class counts
+    for (int c = 0; c < (int)t; c++) start += bins[c];
+    base[t] = start + (h[t] ? atomicAdd(&bins[kBinClasses + t], h[t]) : 0u);
+    h[t] = 0;
+  }
+  __syncthreads();
+  for (uint64_t i = (uint64_t)blockIdx.x * kBinBlock + t; i < n; i += (uint64_t)gridDim.x * kBinBlock) {
+    const uint32_t c = bin_class(lens[i]);
+    perm[base[c] + atomicAdd(&h[c], 1u)] = (uint32_t)i;
+  }
+}
+
+hipError_t launch_binning(const uint16_t* lens, uint64_t n, uint32_t* bins, uint32_t* perm,
+                          hipStream_t stream) {
+  uint64_t g = (n + 4ull * kBinBlock - 1) / (4ull * kBinBlock);  // ~4 packets per thread
+  const int grid = (int)(g < 1 ? 1 : g > 1024 ? 1024 : g);
+  hipLaunchKernelGGL(bin_hist, dim3(grid), dim3(kBinBlock), 0, stream, lens, n, bins);
+  hipLaunchKernelGGL(bin_scatter, dim3(grid), dim3(kBinBlock), 0, stream, lens, n, bins, perm);
+  return hipGetLastError();
+}
+
+// ============================================================================================
 // tile_kernel -- the forward-only fast path for programs of <= 63 micro-ops. The C++ part only
 // moves each tile's header windows HBM -> LDS (LDS-DMA) and turns the per-lane counter bucket
 // into ballots; everything in between is ONE hand-written asm statement (tile.inc, generated by
@@ -1305,6 +1363,9 @@ __global__ __launch_bounds__(kBlock, 5) void dag_tile_kernel(LaunchArgs a) {
 template <bool FIXED, bool LOOPS>
 __global__ __launch_bounds__(kBlock, 8) void tile_kernel(LaunchArgs a) {
   counters_init();
+  // the length bins of this batch were consumed by bin_scatter (earlier on the stream): re-zero
+  if (LOOPS && a.perm && blockIdx.x == 0 && threadIdx.x < 2 * kBinClasses)
+    a.bin_counts[threadIdx.x] = 0;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t wv = rfl(threadIdx.x / kWave);  // wave-uniform: keeps LDS addresses scalar
   WaveLds L;
@@ -1330,7 +1391,15 @@ __global__ __launch_bounds__(kBlock, 8) void tile_kernel(LaunchArgs a) {
       const uint64_t pkt = tile * kWave + lane;
       const bool valid = pkt < a.n;
       const bool sw = stride_windows(a);
-      dma_meta(a, L, 0, tile, lane);
+      if (LOOPS && a.perm) {  // length-binned order: gather this tile's packet metadata
+        const uint64_t src = valid ? (uint64_t)a.perm[pkt] : 0ull;
+        if (a.offsets)
+          dma_x1(valid ? (uintptr_t)(a.offsets + src) : (uintptr_t)a.prog, lds_addr(L.meta_off));
+        if (a.lens)
+          dma_u16(valid ? (uintptr_t)(a.lens + src) : (uintptr_t)a.prog, lds_addr(L.meta_len));
+      } else {
+        dma_meta(a, L, 0, tile, lane);
+      }
       if (sw) dma_window_stride(a, L.win, tile, lane);
       dma_wait();
       uintptr_t mb;
@@ -1358,7 +1427,7 @@ __global__ __launch_bounds__(kBlock, 8) void tile_kernel(LaunchArgs a) {
           [fixed] "i"(FIXED ? 1 : 0), [loops] "i"(LOOPS ? 1 : 0), [aligned] "s"(rfl(aligned)),
           [o_tprog] "i"(offsetof(LaunchArgs, tprog)),
           [o_tprog_exact] "i"(offsetof(LaunchArgs, tprog_exact)),
-          [o_maxs] "i"(offsetof(LaunchArgs, max_steps)),
+          [o_maxs] "i"(offsetof(LaunchArgs, max_steps)), [o_perm] "i"(offsetof(LaunchArgs, perm)),
           [o_frames] "i"(offsetof(LaunchArgs, frames)), [o_stride] "i"(offsetof(LaunchArgs, stride)),
           [o_n] "i"(offsetof(LaunchArgs, n)), [o_mem] "i"(offsetof(LaunchArgs, mem_size)),
           [o_offsets] "i"(offsetof(LaunchArgs, offsets)), [o_lens] "i"(offsetof(LaunchArgs, lens)),
@@ -1371,8 +1440,9 @@ __global__ __launch_bounds__(kBlock, 8) void tile_kernel(LaunchArgs a) {
     if (!FIXED && a.mem_out) {
       uint32_t ln;
       asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
-      const uint64_t pk = tile * kWave + ln;
-      if (pk < a.n) {
+      const uint64_t slot = tile * kWave + ln;
+      const uint64_t pk = slot < a.n && LOOPS && a.perm ? (uint64_t)a.perm[slot] : slot;
+      if (slot < a.n) {
         uintptr_t mb;
         uint32_t ml;
         meta_of(a, L, 0, tile, ln, mb, ml);

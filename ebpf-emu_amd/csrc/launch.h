@@ -15,9 +15,13 @@ constexpr int kWinStride = kWin + 4;  // padded per-lane LDS stride: 17 dwords, 
 constexpr int kMaxLdsUops = 4096;     // programs up to this many micro-ops are staged in LDS
 constexpr int kCallDepth = 64;        // EBPF_MAX_CALL_DEPTH
 constexpr int kCounterShards = 64;    // device-atomic counter shards (spread contention)
-// workspace layout: [arrival tickets u32[64 + 1], padded to 512 B][shards u64[64][8]]
-// [tier-1 wave slots]; tickets and shards are zero between batches
+// workspace layout: [arrival tickets u32[64 + 1] | length-bin counts u32[16] @384 | bin cursors
+// u32[16] @448, 512 B][shards u64[64][8]][tier-1 wave slots, or the length-binned packet order
+// u32[n]]; tickets, bin counts/cursors and shards are zero between batches
 constexpr uint64_t kWsTicketsOff = 0;
+constexpr uint64_t kWsBinCountsOff = 384;
+constexpr uint64_t kWsBinCursorOff = 448;
+constexpr int kBinClasses = 16;  // packets are binned by ceil(len / 128), capped
 constexpr uint64_t kWsShardsOff = 512;
 constexpr uint64_t kWsSlotsOff = kWsShardsOff + kCounterShards * 8 * 8;
 
@@ -52,6 +56,8 @@ struct LaunchArgs {
   uint8_t* mem_out;           // optional [n][mem_size] final images
   uint64_t* regs_out;         // optional [n][11] final registers
   uint32_t fold_kernel;       // 1: shards are folded by fold_counters after the launch (A/B)
+  const uint32_t* perm;       // loop mode: packet index of tile slot i (length-binned), else null
+  uint32_t* bin_counts;       // with perm: bin counts + cursors, zeroed again by the tile kernel
 };
 
 // Bytes of tier-1 scratch per wave slot: lane-interleaved image dwords + call stack.
@@ -67,6 +73,12 @@ constexpr uint32_t kTinyUops = 8;
 // slot once (grid-stride) so per-workgroup fixed costs are paid once per slot. Tier 1:
 // balanced persistent waves (bounds the per-wave image scratch).
 int interp_grid(int kind, uint32_t n_uops, bool tiny, uint64_t n_tiles, int* grid_out);
+
+// Length-binned lane packing for the loop-mode tile kernel (offsets + lens layouts): fills
+// perm[n] with the packet indices grouped by ceil(len / 128), so a tile's lanes run loops of
+// similar trip counts. Two kernels on `stream` (histogram, scatter); bins start zeroed.
+hipError_t launch_binning(const uint16_t* lens, uint64_t n, uint32_t* bins, uint32_t* perm,
+                          hipStream_t stream);
 
 // Enqueue the interpreter on `stream`; with counters, its last workgroup folds the shards into them.
 hipError_t launch_interp(int kind, const LaunchArgs& a, int grid, hipStream_t stream);

@@ -121,3 +121,41 @@ def test_loop_step_budget_exact(cuda, oracle_mod, budget):
         gen = _run_full(img, pkts, cuda, max_steps=budget, offsets_layout=True, align=16,
                         generic=True)
         _same_outputs(got, gen, f"budget {budget}")
+
+
+@pytest.mark.parametrize("layout", [dict(offsets_layout=True, align=64),
+                                    dict(offsets_layout=True, misalign=5)])
+def test_length_binned_batches(cuda, oracle_mod, layout):
+    """Batches of >= 16384 packets in the offsets + lens layout run in length-binned order
+    (bin_hist / bin_scatter): every output still at its packet's index, identical to the general
+    interpreter, and counters equal to the oracle's."""
+    import numpy as np
+
+    from ebpf_emu.asm import assemble
+    from ebpf_emu import workloads as W
+
+    rng = random.Random(77)
+    pkts = [bytes(rng.getrandbits(8) for _ in range(rng.choice([0, 14, 64, 65, 200, 600, 1500])))
+            for _ in range(20000)]
+    for src in (W.CHECKSUM, FORWARD_SUM):
+        img = assemble(src)
+        got = _run_full(img, pkts, cuda, mem_size=2048, r10=2048, **layout)
+        gen = _run_full(img, pkts, cuda, mem_size=2048, r10=2048, generic=True, **layout)
+        _same_outputs(got, gen, f"{layout} {src[:30]}")
+        (frames, n), kw = _oracle_batch(pkts)
+        r0, st, cnt = oracle_mod.Program(img).run_batch(frames, n, mem_size=2048, r10=2048,
+                                                        threads=8, **kw)
+        assert np.array_equal(got["status"], st)
+        assert list(got["counters"]) == [int(c) for c in cnt]
+
+
+def _oracle_batch(pkts):
+    import numpy as np
+
+    buf = b"".join(pkts) + bytes(16)
+    offs, pos = [], 0
+    for p in pkts:
+        offs.append(pos)
+        pos += len(p)
+    return (np.frombuffer(buf, dtype=np.uint8), len(pkts)), dict(
+        offsets=np.array(offs, dtype=np.uint32), lens=np.array([len(p) for p in pkts], dtype=np.uint16))
