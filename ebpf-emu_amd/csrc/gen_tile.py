@@ -346,6 +346,7 @@ v_perm_b32 {{RH}}, {{AL}}, {{AL}}, {{T3}}
     "H_LDXK2": ("ldxk2", "ool"),
     "H_LDXK_FAR": ("ldxkfar", "ool"),
     "H_LDX": ("ldx", "ool"),
+    "H_LDX1": ("ldx1", "ool"),
 }
 DONE = "H_DONE"
 
@@ -678,6 +679,90 @@ v_and_b32 {{SHF}}, 3, {{t0}}
 {TAILS[sfx]}"""
 
 
+def refill(tag):
+    """Loop mode: exec = lanes whose access needs packet bytes outside their window (T7), tile
+    aligned: WB = a & ~15, four 16-byte loads of [WB, WB + 64) (chunks wholly past the packet
+    skipped), written to the lane's LDS window. Clobbers t1..t19 except t0 (the address)."""
+    return f"""s_mov_b64 {{T5}}, exec
+s_mov_b64 exec, {{T7}}
+v_and_b32 {{WB}}, -16, {{t0}}
+v_mov_b32 {{t7}}, 0
+v_mov_b32 {{t6}}, {{WB}}
+v_lshl_add_u64 {{T67}}, {{BASE}}, 0, {{T67}}
+""" + "\n".join(f"""v_add_u32 {{t1}}, {16 * c}, {{WB}}
+v_cmp_lt_u32 vcc, {{t1}}, {{LEN}}
+s_and_b64 exec, {{T7}}, vcc
+global_load_dwordx4 {reg}, {{T67}}, off offset:{16 * c}""" for c, reg in
+                 enumerate(("v[44:47]", "v[48:51]", "v[52:55]", "v[38:41]"))) + f"""
+s_mov_b64 exec, {{T7}}
+s_waitcnt vmcnt(0)
+""" + "\n".join(f"""v_xad_u32 {{t1}}, {{SWZ}}, {16 * c}, {{WIN}}
+ds_write_b128 {{t1}}, {reg}""" for c, reg in
+                 enumerate(("v[44:47]", "v[48:51]", "v[52:55]", "v[38:41]"))) + f"""
+s_waitcnt lgkmcnt(0)
+s_mov_b64 exec, {{T5}}"""
+
+
+def ldx1(sfx, loop):
+    """LDX of one byte (ldxb), register-based address: one window dword. a = S + sext(off);
+    the high word != 0 or a >= mem -> ST_MEM (for one byte, a + 1 > mem is a >= mem; emu.rs:344,
+    mmu.rs:23-30). Window bytes from LDS (loop mode: the window at WB, refilled as in
+    ldx_loop), packet bytes past it from HBM (the dword holding byte a), bytes at or past len
+    read as zero (main.rs:16); merged into the low byte of dst (Q1)."""
+    lab = f"ldx1{'l' if loop else ''}{sfx}"
+    win = "v_sub_u32 {t6}, {t0}, {WB}" if loop else "v_mov_b32 {t6}, {t0}"
+    out = f""".L{lab}%=:
+{READ_S}
+v_lshl_add_u64 {{T01}}, {{S}}, 0, {{IMM}}
+v_cmp_ne_u32_e64 {{T0}}, 0, {{t1}}
+v_cmp_le_u32_e64 {{T1}}, {{KMEM}}, {{t0}}
+s_or_b64 vcc, {{T0}}, {{T1}}
+{fault_split(lab, ST_MEM, "{REMX}")}
+{win}
+v_cmp_lt_u32_e64 {{T0}}, {{t0}}, {{LEN}}
+v_cmp_le_u32_e64 {{T1}}, 64, {{t6}}
+s_and_b64 {{T7}}, {{T1}}, {{T0}}
+"""
+    if loop:
+        out += f"""s_cbranch_scc0 .L{lab}_win%=
+s_cmp_eq_u32 %[aligned], 0
+s_cbranch_scc1 .L{lab}_win%=
+{refill(lab)}
+v_sub_u32 {{t6}}, {{t0}}, {{WB}}
+v_cmp_le_u32_e64 {{T1}}, 64, {{t6}}
+v_cmp_lt_u32_e64 {{T0}}, {{t0}}, {{LEN}}
+s_and_b64 {{T7}}, {{T1}}, {{T0}}
+.L{lab}_win%=:
+"""
+    out += f"""v_and_b32 {{t6}}, -4, {{t6}}
+v_min_u32 {{t6}}, 60, {{t6}}
+{window_addr("{WD0}", "{t6}")}
+ds_read_b32 {{WD0}}, {{WD0}}
+s_and_b64 {{T7}}, {{T7}}, exec
+s_cbranch_scc0 .L{lab}_near%=
+{WAIT}
+s_mov_b64 {{T5}}, exec
+s_mov_b64 exec, {{T7}}
+v_and_b32 {{t10}}, -4, {{t0}}
+v_mov_b32 {{t11}}, 0
+v_lshl_add_u64 {{T89}}, {{BASE}}, 0, {{T1011}}
+global_load_dword {{WD0}}, {{T89}}, off
+s_waitcnt vmcnt(0)
+s_mov_b64 exec, {{T5}}
+.L{lab}_near%=:
+v_and_b32 {{SHF}}, 3, {{t0}}
+v_lshlrev_b32 {{SHF}}, 3, {{SHF}}
+{WAIT}
+v_bfe_u32 {{RL}}, {{WD0}}, {{SHF}}, 8
+v_cmp_lt_u32 vcc, {{t0}}, {{LEN}}
+v_cndmask_b32 {{RL}}, 0, {{RL}}, vcc
+{on('SRC2,DST')}
+v_bfi_b32 {{RF0}}, {{KML}}, {{RL}}, {{RF0}}
+{OFF}
+{TAILS[sfx]}"""
+    return out
+
+
 def window_tail_ldx(a0, shift):
     """As window_tail for a register-based address, whose bytes may also come from far_read.
     Bytes past len read as zero (main.rs:16): in the FIXED layout every packet is >= 64 bytes
@@ -988,6 +1073,8 @@ def main():
                 code = body + f"\ns_branch .Ldivmod{sfx}%="
             elif body == "ldx":  # ool, two modes
                 code = f".if %[loops]\ns_branch .Lldxl{sfx}%=\n.else\ns_branch .Lldx{sfx}%=\n.endif"
+            elif body == "ldx1":
+                code = f".if %[loops]\ns_branch .Lldx1l{sfx}%=\n.else\ns_branch .Lldx1{sfx}%=\n.endif"
             else:  # ool
                 code = f"s_branch .L{body}{sfx}%="
         code = re.sub(r"\.L(nf_\w+?)%=", lambda m: f".L{m.group(1)}_{idx}%=", code)
@@ -995,7 +1082,7 @@ def main():
     parts.append(f".org .Lslots%=+{len(table) * SLOT}")
     for sfx in ("c", "e"):
         parts += [ldxk(sfx), ldxk1(sfx), ldxk2(sfx), ldxkfar(sfx), ldx(sfx), ldx_loop(sfx),
-                  divmod(sfx)]
+                  ldx1(sfx, False), ".if %[loops]", ldx1(sfx, True), ".endif", divmod(sfx)]
     parts += [KFAULT, ".if %[loops]", BUDGET, ".endif", EPILOGUE]
     text = F("\n".join(parts))
     assert "{" not in text, "unsubstituted register name: " + text[text.index("{"):][:40]

@@ -413,6 +413,7 @@ static std::vector<TUop> build_tile(const std::vector<Uop>& uops, const std::vec
     u.width = o.width;
     u.blen = start[i] ? rem[i] : 0;
     if (h == H_LDX || h == H_ARSH64_IMM || h == H_ARSH64_REG) u.a0 = rem[i];  // REMX
+    if (h == H_LDX && o.width == 1) id = chained ? T_LDX1_C : T_LDX1_E;  // one byte: one dword
     if (h == H_LDXK || h == H_LDXK_FAR) {
       const uint32_t a0 = o.a0, w = o.end - o.a0;
       u.x = o.end;      // KEND
