@@ -141,16 +141,19 @@ def main():
     counters.zero_()
 
     # ---- timed region: barrier + sync on both sides, K steps, max over ranks ----
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    # HIP events on the launch stream: one pair around the K back-to-back batches (a batch =
+    # every launch of one ebpf_run_batch), so the per-batch time includes the dispatch gaps
+    # between launches but no event packets between them
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    ev0.record(stream)
     for i in range(args.steps):
-        starts[i].record(stream)
         step(i)
-        ends[i].record(stream)
+    ev1.record(stream)
     D.reduce_counters(counters)  # the one exchange step: per-verdict counters, RCCL / xGMI
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -161,8 +164,7 @@ def main():
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-    kern_ms = [s.elapsed_time(e) for s, e in zip(starts, ends)]
-    kern_avg_ms = sum(kern_ms) / len(kern_ms)
+    kern_avg_ms = ev0.elapsed_time(ev1) / args.steps
 
     cnt = [int(c) & ((1 << 64) - 1) for c in counters.cpu().tolist()]
     total_pkts = (args.total_packets or n * world) * args.steps
