@@ -868,6 +868,43 @@ int ebpf_run_batch_multi(ebpf_prog* p, int nshards, const int* devices, const eb
   return rc;
 }
 
+int ebpf_pcap_index(const uint8_t* buf, size_t nbytes, uint32_t* offsets, uint16_t* lens,
+                    size_t cap, size_t* n, uint32_t* linktype) {
+  if (!buf || !n || (cap && (!offsets || !lens))) return EBPF_EINVAL;
+  *n = 0;
+  if (nbytes < 24) return EBPF_EPCAP;
+  auto rd32 = [&](size_t at, bool swap) {
+    uint32_t v;
+    std::memcpy(&v, buf + at, 4);
+    return swap ? __builtin_bswap32(v) : v;
+  };
+  const uint32_t magic = rd32(0, false);
+  bool swap;
+  if (magic == 0xa1b2c3d4u || magic == 0xa1b23c4du) swap = false;       // micro / nanosecond
+  else if (magic == 0xd4c3b2a1u || magic == 0x4d3cb2a1u) swap = true;   // written byte-swapped
+  else return EBPF_EPCAP;
+  if (linktype) *linktype = rd32(20, swap) & 0x0fffffffu;  // upper bits: FCS flags
+  if (nbytes > 0xFFFFFFFFull) return EBPF_ETOOBIG;
+  size_t at = 24, count = 0;
+  int rc = EBPF_OK;
+  while (at < nbytes) {
+    if (nbytes - at < 16) return EBPF_EPCAP;  // truncated record header
+    const uint32_t incl = rd32(at + 8, swap);
+    if (incl > nbytes - at - 16) return EBPF_EPCAP;  // truncated packet data
+    if (incl > 0xFFFF) return EBPF_ETOOBIG;
+    if (count < cap) {
+      offsets[count] = (uint32_t)(at + 16);
+      lens[count] = (uint16_t)incl;
+    } else if (cap) {
+      rc = EBPF_EINVAL;
+    }
+    count++;
+    at += 16 + (size_t)incl;
+  }
+  *n = count;
+  return rc;
+}
+
 const char* ebpf_strerror(int err) {
   switch (err) {
     case EBPF_OK: return "ok";
@@ -883,6 +920,7 @@ const char* ebpf_strerror(int err) {
     case EBPF_EHIP: return "HIP runtime error";
     case EBPF_ETOOBIG: return "program too large";
     case EBPF_ERCCL: return "RCCL error";
+    case EBPF_EPCAP: return "not a classic pcap capture, or a truncated record";
     default: return "unknown error";
   }
 }

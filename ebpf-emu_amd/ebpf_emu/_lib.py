@@ -16,7 +16,7 @@ LIB_PATH = os.path.join(_HERE, "libebpfemu.so")
 EBPF_OK = 0
 EBPF_EINVAL, EBPF_ELEN, EBPF_EREG, EBPF_EOP, EBPF_EMODE = -1, -2, -3, -4, -5
 EBPF_ELDDW, EBPF_ELDDW_OVF, EBPF_EHEX, EBPF_ENOMEM, EBPF_EHIP = -6, -7, -8, -9, -10
-EBPF_ETOOBIG, EBPF_ERCCL = -11, -12
+EBPF_ETOOBIG, EBPF_ERCCL, EBPF_EPCAP = -11, -12, -13
 
 ST_OK, ST_MEM, ST_MEM_UB, ST_INSN, ST_ARITH, ST_STEPS, ST_CALLDEPTH, ST_BADPKT = range(8)
 STATUS_NAMES = ["OK", "MEM", "MEM_UB", "INSN", "ARITH", "STEPS", "CALLDEPTH", "BADPKT"]
@@ -29,8 +29,8 @@ MAX_CALL_DEPTH = 64
 EXPORTS = ["ebpf_batch_init", "ebpf_prog_load", "ebpf_prog_load_hex", "ebpf_prog_free",
            "ebpf_prog_len", "ebpf_prog_insn", "ebpf_prog_tier", "ebpf_prog_forward_only",
            "ebpf_workspace_bytes",
-           "ebpf_prog_upload", "ebpf_run_batch", "ebpf_run_batch_multi", "ebpf_strerror",
-           "ebpf_version"]
+           "ebpf_prog_upload", "ebpf_run_batch", "ebpf_run_batch_multi", "ebpf_pcap_index",
+           "ebpf_strerror", "ebpf_version"]
 
 
 class Batch(ctypes.Structure):  # ebpf_batch
@@ -91,6 +91,8 @@ def lib():
     L.ebpf_run_batch_multi.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
                                        ctypes.POINTER(Batch), ctypes.POINTER(BatchOut),
                                        ctypes.POINTER(vp)]
+    L.ebpf_pcap_index.argtypes = [vp, sz, vp, vp, sz, ctypes.POINTER(sz),
+                                  ctypes.POINTER(ctypes.c_uint32)]
     L.ebpf_strerror.argtypes = [ctypes.c_int]
     L.ebpf_strerror.restype = ctypes.c_char_p
     L.ebpf_version.restype = ctypes.c_char_p

@@ -37,6 +37,7 @@ typedef struct ihipStream_t* ebpf_stream_t; /* == hipStream_t */
 #define EBPF_EHIP          (-10) /* a HIP runtime call failed */
 #define EBPF_ETOOBIG       (-11) /* program beyond the device limit (EBPF_MAX_INSNS) */
 #define EBPF_ERCCL         (-12) /* an RCCL call failed */
+#define EBPF_EPCAP         (-13) /* not a classic pcap capture, or a truncated record */
 
 /* ---- per-packet status (u8) ---- */
 #define EBPF_ST_OK          0  /* exit with empty frame stack or pc past the end (emu.rs:49,277) */
@@ -158,6 +159,20 @@ int ebpf_run_batch(ebpf_prog* prog, const ebpf_batch* batch, const ebpf_batch_ou
 int ebpf_run_batch_multi(ebpf_prog* prog, int nshards, const int* devices,
                          const ebpf_batch* batches, const ebpf_batch_out* outs,
                          ebpf_stream_t const* streams);
+
+/* Host ingestion (the path starts in host memory, "a pcap buffer or NIC ring").
+ * Index a classic libpcap capture held in host memory (magic a1b2c3d4 / a1b23c4d, either byte
+ * order): offsets[i] / lens[i] = the byte offset and captured length of record i's packet
+ * within buf. A device copy of the same bytes plus these arrays is an offsets + lens batch, so
+ * the capture runs unmodified (no repacking). Records are indexed in file order; at most cap of
+ * them (offsets/lens may be NULL with cap 0 to count). *n receives the number of records in
+ * the buffer, *linktype the capture's link type (1 = Ethernet). Returns EBPF_EPCAP for a bad
+ * header or a truncated record, EBPF_ETOOBIG for a record longer than 65535 bytes or a buffer
+ * past 4 GiB (u32 offsets: index such a capture in pieces), EBPF_EINVAL when more than cap
+ * records exist (the first cap are indexed). The reference reads its packet from argv
+ * (main.rs:14-22); this replaces that per-packet input for whole captures. */
+int ebpf_pcap_index(const uint8_t* buf, size_t nbytes, uint32_t* offsets, uint16_t* lens,
+                    size_t cap, size_t* n, uint32_t* linktype);
 
 /* Human-readable message for an EBPF_E* code. */
 const char* ebpf_strerror(int err);

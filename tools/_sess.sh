@@ -1,2 +1,1 @@
-B="python bench.py --cpu-seconds 0 --steps 100"
-bash tools/gpu_session.sh "tests|300|python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread" "b5|120|$B" "bd|120|$B --config drop" "b5k|120|EBPFEMU_FOLD=kernel $B"
+bash tools/gpu_session.sh "pcap|300|python tools/e2e_bench.py --pcap" "pcapc|300|python tools/e2e_bench.py --pcap --chunk 4194304"

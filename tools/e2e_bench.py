@@ -23,7 +23,13 @@ def main():
     ap.add_argument("--packets", type=int, default=16 << 20)
     ap.add_argument("--chunk", type=int, default=1 << 20)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--pcap", action="store_true",
+                    help="the packets as one classic pcap capture (16-byte record headers between "
+                         "the frames), through ebpf_emu.pcap.Capture: index, chunked H2D, kernel, "
+                         "verdict D2H")
     args = ap.parse_args()
+    if args.pcap:
+        return pcap_e2e(args)
 
     import numpy as np
     import torch
@@ -108,6 +114,49 @@ def main():
         "h2d_only_mpps": round(n / res["h2d_only"] / 1e6, 1),
         "h2d_only_GBps": round(n * 64 / res["h2d_only"] / 1e9, 2),
         "kernel_only_mpps": round(n / res["kernel_only"] / 1e6, 1),
+    }))
+
+
+def pcap_e2e(args):
+    """End to end from a capture in host memory: the capture's bytes (frames + record headers)
+    cross PCIe as they are; offsets / lengths come from ebpf_pcap_index."""
+    import numpy as np
+    import torch
+
+    from ebpf_emu import Program, pcap
+    from ebpf_emu import workloads as W
+
+    n, c = args.packets, args.chunk
+    one = W.frames_fixed(c, 64, 3).reshape(c, 64)
+    # the capture: 24-byte header, then n records of 16 + 64 bytes (distinct rolled copies)
+    rec = np.zeros((n, 80), dtype=np.uint8)
+    hdr = np.frombuffer(pcap.to_bytes([bytes(64)])[24:40], dtype=np.uint8)
+    rec[:, :16] = hdr
+    for i in range(n // c):
+        rec[i * c:(i + 1) * c, 16:] = np.roll(one, i, axis=0)
+    buf = np.concatenate([np.frombuffer(pcap.to_bytes([])[:24], dtype=np.uint8), rec.reshape(-1)])
+    t0 = time.perf_counter()
+    cap = pcap.Capture(buf)
+    t_stage = time.perf_counter() - t0
+    prog = Program(W.program(args.config))
+    prog.upload(0)
+    cap.run(prog, packets_per_chunk=c)
+    best = 1e9
+    for _ in range(args.reps):
+        t0 = time.perf_counter()
+        verdict, counters = cap.run(prog, packets_per_chunk=c)
+        best = min(best, time.perf_counter() - t0)
+    # parity spot check: chunk 0's verdicts against a device-resident fixed-slot run
+    dev = torch.device("cuda", 0)
+    ref = prog.run(torch.from_numpy(rec[:c, 16:].reshape(-1).copy()).to(dev), n=c, stride=64)
+    torch.cuda.synchronize(dev)
+    assert torch.equal(ref.verdict.cpu(), verdict[:c]), "pcap verdicts differ"
+    print(json.dumps({
+        "config": args.config, "source": "pcap capture in pinned host memory", "packets": n,
+        "chunk": c, "frame_bytes": 64, "capture_bytes": int(buf.nbytes),
+        "e2e_mpps": round(n / best / 1e6, 1),
+        "e2e_GBps_h2d": round(buf.nbytes / best / 1e9, 2),
+        "index_and_pin_s": round(t_stage, 3),
     }))
 
 
