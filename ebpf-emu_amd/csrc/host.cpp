@@ -690,15 +690,30 @@ int ebpf_prog_upload(ebpf_prog* p, int device) {
   return rc;
 }
 
-// Whether a loop-mode batch runs in length-binned order.
+// Whether a loop-mode batch runs in length-binned order (an xdp_md batch is staged as offsets +
+// lens).
 static bool use_binning(const ebpf_prog* p, const ebpf_batch* b) {
-  if (p->ltuops.empty() || !b->offsets || !b->lens || (b->flags & EBPF_BATCH_GENERIC)) return false;
+  const bool ol = (b->offsets && b->lens) || (b->flags & EBPF_BATCH_XDP_MD);
+  if (p->ltuops.empty() || !ol || (b->flags & EBPF_BATCH_GENERIC)) return false;
   return g_bin >= 0 ? g_bin == 1 : b->n >= kBinMinPackets;
+}
+
+static uint64_t align16(uint64_t v) { return (v + 15) & ~15ull; }
+
+// xdp_md staging region (at the end of the workspace): offsets u32[n], lengths u16[n], then the
+// images, each in a 16-byte aligned slot of at most round16(min(8 + max len, mem_size)) bytes.
+static uint64_t xdp_image_bytes(const ebpf_batch* b) {
+  const uint64_t maxlen = b->lens ? 0xFFFFull : std::min<uint64_t>(b->stride, 0xFFFFull);
+  return b->n * align16(std::min<uint64_t>(maxlen + 8, b->mem_size)) + 64;
+}
+static uint64_t xdp_region_bytes(const ebpf_batch* b) {
+  return align16(b->n * 4) + align16(b->n * 2) + xdp_image_bytes(b);
 }
 
 uint64_t ebpf_workspace_bytes(const ebpf_prog* p, const ebpf_batch* b, int device) {
   if (!p || !b) return 0;
-  uint64_t bytes = kWsSlotsOff;
+  const uint64_t x = (b->flags & EBPF_BATCH_XDP_MD) ? xdp_region_bytes(b) : 0;
+  uint64_t bytes = kWsSlotsOff + x;
   if (use_binning(p, b)) bytes += b->n * 4;  // the binned packet order
   if (p->tier == 1) {
     int cur = device_of_current();
@@ -708,7 +723,7 @@ uint64_t ebpf_workspace_bytes(const ebpf_prog* p, const ebpf_batch* b, int devic
     hipSetDevice(cur);
     bytes += (uint64_t)grid * kWavesPerBlock * tier1_slot_bytes(b->mem_size);
   }
-  return bytes;
+  return bytes;  // (the xdp_md region, when present, is the last x bytes)
 }
 
 static int check_batch(const ebpf_batch* b) {
@@ -717,14 +732,17 @@ static int check_batch(const ebpf_batch* b) {
   if (b->max_steps == 0) return EBPF_EINVAL;
   if (b->n && !b->frames) return EBPF_EINVAL;
   if (!b->offsets && b->stride == 0 && !b->lens) return EBPF_EINVAL;
-  if (b->flags & ~EBPF_BATCH_GENERIC) return EBPF_EINVAL;
+  if (b->flags & ~(EBPF_BATCH_GENERIC | EBPF_BATCH_XDP_MD)) return EBPF_EINVAL;
+  if ((b->flags & EBPF_BATCH_XDP_MD) &&
+      (b->mem_size > 65528 || xdp_image_bytes(b) > 0xFFFFFFFFull))
+    return EBPF_EINVAL;  // 8 + len must fit the u16 lengths; staged offsets are u32
   return EBPF_OK;
 }
 
-int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* b, const ebpf_batch_out* out,
+int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* bin, const ebpf_batch_out* out,
                    ebpf_stream_t stream) {
   if (!p || !out) return EBPF_EINVAL;
-  int rc = check_batch(b);
+  int rc = check_batch(bin);
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
   int device = 0;
@@ -733,7 +751,9 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* b, const ebpf_batch_out* out,
   } else {
     device = device_of_current();
   }
-  if (b->n == 0) return EBPF_OK;
+  if (bin->n == 0) return EBPF_OK;
+  ebpf_batch staged = *bin;  // an xdp_md batch runs as the staged offsets + lens batch
+  const ebpf_batch* b = bin;
   rc = ebpf_prog_upload(p, device);
   if (rc) return rc;
   int cur = device_of_current();
@@ -752,7 +772,7 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* b, const ebpf_batch_out* out,
     return EBPF_EHIP;
   }
   // scratch: caller-provided or library-owned per (device, stream)
-  uint64_t need = ebpf_workspace_bytes(p, b, device);
+  uint64_t need = ebpf_workspace_bytes(p, bin, device);
   uint8_t* ws = (uint8_t*)b->workspace;
   if (ws && b->workspace_bytes < need) {
     if (cur != device) hipSetDevice(cur);
@@ -779,6 +799,25 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* b, const ebpf_batch_out* out,
       w.bytes = need;
     }
     ws = (uint8_t*)w.ptr;
+  }
+  if (bin->flags & EBPF_BATCH_XDP_MD) {
+    uint8_t* x = ws + need - xdp_region_bytes(bin);
+    uint32_t* doffs = (uint32_t*)x;
+    uint16_t* dlens = (uint16_t*)(x + align16(bin->n * 4));
+    uint8_t* dst = x + align16(bin->n * 4) + align16(bin->n * 2);
+    unsigned long long* cursor = (unsigned long long*)(ws + kWsXdpCursorOff);
+    if (hipMemsetAsync(cursor, 0, 8, s) != hipSuccess ||
+        launch_xdp_stage(bin->frames, bin->offsets, bin->lens, bin->stride, bin->n, bin->mem_size,
+                         dst, doffs, dlens, cursor, s) != hipSuccess) {
+      if (cur != device) hipSetDevice(cur);
+      return EBPF_EHIP;
+    }
+    staged.frames = dst;
+    staged.offsets = doffs;
+    staged.lens = dlens;
+    staged.stride = 0;
+    staged.flags &= ~EBPF_BATCH_XDP_MD;
+    b = &staged;
   }
   LaunchArgs a{};
   a.prog = p->dev_uops[device];

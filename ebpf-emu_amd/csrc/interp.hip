@@ -1350,6 +1350,71 @@ hipError_t launch_binning(const uint16_t* lens, uint64_t n, uint32_t* bins, uint
 }
 
 // ============================================================================================
+// xdp_md calling convention (xdp.rs:16-20): image i = [u32 data = 8][u32 data_end = 8 + len]
+// [packet bytes] -- the bytes main.rs would be handed for a standard XDP program. One workgroup
+// stages 256 packets: it sizes their 16-byte aligned slots, reserves its range with one device
+// atomic (workgroups pack in arrival order; every packet keeps its index through the offsets),
+// then copies packet by packet with all 256 threads (coalesced bytes). An image longer than
+// mem_size is not copied: its length alone makes the batch fault it ST_BADPKT (main.rs:20-21).
+// ============================================================================================
+__global__ __launch_bounds__(256) void xdp_stage(const uint8_t* frames, const uint32_t* offsets,
+                                                 const uint16_t* lens, uint64_t stride, uint64_t n,
+                                                 uint32_t mem_size, uint8_t* dst, uint32_t* doffs,
+                                                 uint16_t* dlens, unsigned long long* cursor) {
+  __shared__ uint32_t pre[256], cp[256], len_s[256];
+  __shared__ const uint8_t* src_s[256];
+  __shared__ unsigned long long base;
+  const uint32_t t = threadIdx.x;
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + t;
+  uint32_t len = 0, copy = 0, slot = 0;
+  if (i < n) {
+    len = lens ? lens[i] : (uint32_t)(stride < 0xFFFF ? stride : 0xFFFF);
+    copy = len + 8 <= mem_size ? len + 8 : 0u;
+    slot = ((copy ? copy : 8u) + 15u) & ~15u;
+    src_s[t] = frames + (offsets ? (uint64_t)offsets[i] : i * stride);
+  }
+  cp[t] = copy;
+  len_s[t] = len;
+  pre[t] = slot;
+  __syncthreads();
+  for (uint32_t d = 1; d < 256; d <<= 1) {  // inclusive scan of the slot sizes
+    const uint32_t v = t >= d ? pre[t - d] : 0u;
+    __syncthreads();
+    pre[t] += v;
+    __syncthreads();
+  }
+  if (t == 255) base = atomicAdd(cursor, (unsigned long long)pre[255]);
+  __syncthreads();
+  const uint32_t excl = pre[t] - slot;
+  if (i < n) {
+    doffs[i] = (uint32_t)(base + excl);
+    dlens[i] = (uint16_t)(len + 8 < 0xFFFF ? len + 8 : 0xFFFF);
+  }
+  __syncthreads();
+  const uint32_t count = (uint32_t)min((uint64_t)256, n - (uint64_t)blockIdx.x * 256);
+  for (uint32_t j = 0; j < count; j++) {
+    const uint32_t c = cp[j];
+    if (c == 0) continue;
+    uint8_t* o = dst + base + (pre[j] - (((c + 15u) & ~15u)));
+    const uint8_t* src = src_s[j];
+    const uint32_t data_end = 8 + len_s[j];
+    for (uint32_t b = t; b < c; b += 256)
+      o[b] = b < 4 ? (uint8_t)(8u >> (8 * b)) : b < 8 ? (uint8_t)(data_end >> (8 * (b - 4)))
+                                                     : src[b - 8];
+  }
+}
+
+hipError_t launch_xdp_stage(const uint8_t* frames, const uint32_t* offsets, const uint16_t* lens,
+                            uint64_t stride, uint64_t n, uint32_t mem_size, uint8_t* dst,
+                            uint32_t* doffs, uint16_t* dlens, unsigned long long* cursor,
+                            hipStream_t stream) {
+  const uint64_t grid = (n + 255) / 256;
+  hipLaunchKernelGGL(xdp_stage, dim3((unsigned)grid), dim3(256), 0, stream, frames, offsets, lens,
+                     stride, n, mem_size, dst, doffs, dlens, cursor);
+  return hipGetLastError();
+}
+
+// ============================================================================================
 // tile_kernel -- the forward-only fast path for programs of <= 63 micro-ops. The C++ part only
 // moves each tile's header windows HBM -> LDS (LDS-DMA) and turns the per-lane counter bucket
 // into ballots; everything in between is ONE hand-written asm statement (tile.inc, generated by

@@ -22,6 +22,7 @@ constexpr uint64_t kWsTicketsOff = 0;
 constexpr uint64_t kWsBinCountsOff = 384;
 constexpr uint64_t kWsBinCursorOff = 448;
 constexpr int kBinClasses = 16;  // packets are binned by ceil(len / 128), capped
+constexpr uint64_t kWsXdpCursorOff = 320;  // u64: bytes staged by xdp_stage (reset per batch)
 constexpr uint64_t kWsShardsOff = 512;
 constexpr uint64_t kWsSlotsOff = kWsShardsOff + kCounterShards * 8 * 8;
 
@@ -79,6 +80,15 @@ int interp_grid(int kind, uint32_t n_uops, bool tiny, uint64_t n_tiles, int* gri
 // similar trip counts. Two kernels on `stream` (histogram, scatter); bins start zeroed.
 hipError_t launch_binning(const uint16_t* lens, uint64_t n, uint32_t* bins, uint32_t* perm,
                           hipStream_t stream);
+
+// xdp_md calling convention: stage image i = [xdp_md {8, 8 + len}][packet][...] for every packet
+// into dst (16-byte aligned slots, packed in workgroup order); writes the staged offsets and
+// lengths (8 + len). Images longer than mem_size are not copied (the batch faults them
+// ST_BADPKT from the length alone). cursor: a zeroed u64.
+hipError_t launch_xdp_stage(const uint8_t* frames, const uint32_t* offsets, const uint16_t* lens,
+                            uint64_t stride, uint64_t n, uint32_t mem_size, uint8_t* dst,
+                            uint32_t* doffs, uint16_t* dlens, unsigned long long* cursor,
+                            hipStream_t stream);
 
 // Enqueue the interpreter on `stream`; with counters, its last workgroup folds the shards into them.
 hipError_t launch_interp(int kind, const LaunchArgs& a, int grid, hipStream_t stream);

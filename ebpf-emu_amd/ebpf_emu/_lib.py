@@ -24,6 +24,7 @@ VERDICT_OTHER, VERDICT_FAULT = 0xFE, 0xFF
 NCOUNTERS = 8
 DEFAULT_MEM, DEFAULT_R10, DEFAULT_STEPS = 1024, 512, 1 << 22
 BATCH_GENERIC = 1  # ebpf_batch.flags: EBPF_BATCH_GENERIC
+BATCH_XDP_MD = 2   # ebpf_batch.flags: EBPF_BATCH_XDP_MD (the xdp_md calling convention)
 MAX_CALL_DEPTH = 64
 
 EXPORTS = ["ebpf_batch_init", "ebpf_prog_load", "ebpf_prog_load_hex", "ebpf_prog_free",

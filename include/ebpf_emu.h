@@ -70,6 +70,14 @@ typedef struct ihipStream_t* ebpf_stream_t; /* == hipStream_t */
 /* ebpf_batch.flags: run on the general interpreter even when the program qualifies for the
  * forward-jump fast path (differential testing; results are identical by contract). */
 #define EBPF_BATCH_GENERIC 1u
+/* ebpf_batch.flags: the xdp_md calling convention (xdp.rs:16-20, struct xdp_md { u32 data;
+ * u32 data_end; }). Each packet's memory image becomes [xdp_md][packet][zeros]: data = 8,
+ * data_end = 8 + len at image offsets 0 and 4, the packet at offset 8, so r1 (= 0) is the ctx
+ * pointer, standard XDP programs run unchanged, and r2 = 8 + len (main.rs:18-29 gives r2 the
+ * image length). This is exactly the image the reference executes when main.rs is handed the
+ * ctx-prefixed bytes. The library stages the images in the workspace (a device copy of the
+ * packets), then runs the batch as usual. Requires mem_size <= 65528. */
+#define EBPF_BATCH_XDP_MD  2u
 #define EBPF_DEFAULT_MEM    1024   /* main.rs:16 */
 #define EBPF_DEFAULT_R10    512    /* main.rs:31 */
 #define EBPF_DEFAULT_STEPS  (1ull << 22)
@@ -85,7 +93,7 @@ typedef struct ebpf_batch {
                                n * stride bytes (every slot whole, as in a ring of fixed slots) */
   uint64_t n;               /* packets */
   uint32_t mem_size;        /* bytes of the per-packet memory image (multiple of 8, >= 8) */
-  uint32_t flags;           /* 0, or EBPF_BATCH_GENERIC */
+  uint32_t flags;           /* 0, or EBPF_BATCH_GENERIC | EBPF_BATCH_XDP_MD */
   uint64_t r10;             /* initial r10 (stack top) */
   uint64_t max_steps;       /* per-packet step budget, 1..; faults EBPF_ST_STEPS beyond */
   void* workspace;          /* optional device scratch of ebpf_workspace_bytes() bytes, ZEROED before its
