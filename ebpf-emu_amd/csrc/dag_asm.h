@@ -1,8 +1,6 @@
-// dag_asm.h — handler numbering of the forward-only fast path's hand-written interpreter loop
-// (dag_loop_asm in interp.hip). The host (build_dag) stores handler_id * DAG_SLOT in DUop::hoff;
-// the loop jumps to slot_base + hoff with s_setpc. Plain #defines: the asm text stringifies them
-// into `.org` directives, and an overfull 128-byte slot is an assembler error, never a silent
-// mis-dispatch.
+// dag_asm.h -- handler numbering of the forward-only micro-op table (host.cpp build_dag stores
+// handler_id * DAG_SLOT in DUop::hoff). gen_tile.py reads these ids and emits the tile kernel's
+// chained / block-end slots for each (tile_ids.h), and build_tile maps DUop::hoff to them.
 #pragma once
 
 #define DAG_SLOT 128
@@ -64,8 +62,7 @@
 #define H_JSET32_REG 54
 #define H_LDXK 55         // constant address inside the header window
 #define H_LDX 56          // register base: window fast path, anything else bails to C++
-// handled by the self-contained tile loop only (dag_tile.inc); the hybrid loop hands them to
-// its C++ step
+// (more kinds; the tile kernel handles every id)
 #define H_MUL64_IMM 57
 #define H_MUL64_REG 58
 #define H_MUL32_IMM 59

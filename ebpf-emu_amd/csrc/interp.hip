@@ -853,33 +853,6 @@ __device__ __forceinline__ u32x16 load_duop(const DUop* prog, uint32_t pc) {
   return v;
 }
 
-// The hand-written interpreter loop (dag_loop.inc, generated by gen_dag_loop.py; contract in its
-// header). Runs until every lane is done (returns PC_DONE) or the lowest live pc holds a
-// micro-op it leaves to the C++ step (returns that pc, already removed from `live`). Programs of
-// <= 64 micro-ops (one-word pc set). exec is the whole wave at entry and is restored at exit.
-__device__ __forceinline__ uint32_t dag_loop_asm(uint64_t& live, uint32_t& lpc, uint32_t& nsteps,
-                                                 const DUop* prog, uint32_t rl, uint32_t win,
-                                                 uint32_t swz16, uint32_t len, uint32_t mem_size) {
-  uint32_t P;
-  // hipcc's divergence analysis cannot prove the pc set uniform across the C++ step's control
-  // flow; it is (every update is a ballot or an SGPR), so re-assert that at the boundary
-  live = (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)live) |
-         ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(live >> 32)) << 32);
-  asm volatile(
-#include "dag_loop.inc"
-      : [live] "+s"(live), [lpc] "+v"(lpc), [nst] "+v"(nsteps), [P] "=&s"(P)
-      : [prog] "s"(prog), [rl] "v"(rl), [win] "v"(win), [swz] "v"(swz16), [len] "v"(len),
-        [mem] "s"(mem_size)
-      : "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71", "s72", "s73", "s74", "s75",
-        "s76", "s77", "s78", "s79", "s80", "s81", "s82", "s83", "s84", "s85", "s86", "s87",
-        "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95", "s96", "s97", "s98", "s99",
-        "s62", "s63", "v82", "v83", "v84", "v85", "v86", "v87", "v88", "v89", "v90", "v91",
-        "v92", "v93", "v94", "v95", "v96", "v97", "v98", "v99", "v100", "v101", "v102", "v103",
-        "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111", "v112", "v113", "v114",
-        "v115", "v116", "v117", "vcc", "scc", "memory");
-  return P;
-}
-
 __device__ __forceinline__ uint64_t rget(const uint8_t* rl, uint32_t off) {
   return *(const uint64_t*)(rl + off);
 }
@@ -887,7 +860,7 @@ __device__ __forceinline__ void rset(uint8_t* rl, uint32_t off, uint64_t v) {
   *(uint64_t*)(rl + off) = v;
 }
 
-template <int NW, int V = 11>
+template <int NW>
 __global__ __launch_bounds__(kBlock) void dag_kernel(LaunchArgs a) {
   counters_init();
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -913,7 +886,7 @@ __global__ __launch_bounds__(kBlock) void dag_kernel(LaunchArgs a) {
     const bool valid = pkt < a.n;
     // ---- header windows: with stride slots, windows and lengths in one round trip; else as
     //      interp_kernel's single-buffered tier 0 (lengths/offsets first) ----
-    const bool sw = (V & 1) && stride_windows(a);
+    const bool sw = stride_windows(a);
     dma_meta(a, L, 0, tile, lane);
     if (sw) dma_window_stride(a, L.win, tile, lane);
     dma_wait();
@@ -950,21 +923,10 @@ __global__ __launch_bounds__(kBlock) void dag_kernel(LaunchArgs a) {
     // ---- Emu::run (emu.rs:452-458): lowest parked pc first ----
     PcSet<NW> live;
     live.init(ballot(lpc == 0) != 0);
-    const uint32_t rl_lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)rl;
-    const uint32_t win_lds =
-        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)my_win;
     for (;;) {
-      uint32_t P;
-      if (NW == 1 && (V & 8)) {
-        // the common micro-ops run in the hand-written loop; it returns here for the others
-        P = dag_loop_asm(live.w0, lpc, nsteps, a.dprog, rl_lds, win_lds, my_swz << 4, len,
-                         mem_size);
-        if (P == PC_DONE) break;
-      } else {
-        P = live.first();
-        if (P == PC_DONE) break;
-        live.del(P);
-      }
+      const uint32_t P = live.first();
+      if (P == PC_DONE) break;
+      live.del(P);
       const u32x16 q = load_duop(a.dprog, P);
       const uint32_t op = q[0] & 0xff, aux = q[0] >> 8, doff = q[1], soff = q[2], npc = q[3];
       const uint32_t x = q[4];
@@ -976,8 +938,7 @@ __global__ __launch_bounds__(kBlock) void dag_kernel(LaunchArgs a) {
       const uint64_t S = rget(rl, soff);
       // operand B and the low words are formed inside each handler, after the dispatch, so the
       // register reads above are in flight while the scalar unit walks the dispatch tree
-      const uint64_t Bearly = (V & 2) ? 0ull : ((aux & F_SRC) ? S : k);
-#define B ((V & 2) ? ((aux & F_SRC) ? S : k) : Bearly)
+#define B ((aux & F_SRC) ? S : k)
 #define a32 ((uint32_t)A)
 #define b32 ((uint32_t)B)
       uint64_t R;
@@ -1167,131 +1128,6 @@ __global__ __launch_bounds__(kBlock) void dag_kernel(LaunchArgs a) {
 }
 
 // ============================================================================================
-// dag_tile_kernel — the forward-only fast path with the whole tile interpreted by one hand-written
-// asm statement (dag_tile.inc, generated by gen_dag_tile.py: register file in VGPRs, every
-// tier-0 micro-op, mmu.rs faults, reads inside and past the header window). LDS holds only the
-// header windows and their metadata: 4.5 KiB per wave.
-// ============================================================================================
-constexpr uint32_t kTileWaveLds = kWinBytes + kDagMetaBytes;
-
-// Interprets this tile; returns r0 (and stores the register file to regs_out when rflag).
-__device__ __forceinline__ uint64_t dag_tile_asm(uint64_t live, uint32_t& lpc, uint32_t& nsteps,
-                                                 uint32_t& st, const LaunchArgs& a, uint32_t win,
-                                                 uint32_t swz16, uint32_t len, uint64_t base,
-                                                 uint64_t raddr, uint32_t vok) {
-  uint32_t r0l, r0h;
-  live = (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)live) |
-         ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(live >> 32)) << 32);
-  const uint32_t r10l = (uint32_t)a.r10, r10h = (uint32_t)(a.r10 >> 32);
-  const uint32_t rflag = __builtin_amdgcn_readfirstlane(a.regs_out != nullptr ? 1u : 0u);
-  asm volatile(
-#include "dag_tile.inc"
-      : [live] "+s"(live), [lpc] "+v"(lpc), [nst] "+v"(nsteps), [st] "+v"(st), [r0l] "=&v"(r0l),
-        [r0h] "=&v"(r0h)
-      : [prog] "s"(a.dprog), [mem] "s"(a.mem_size), [r10l] "s"(r10l), [r10h] "s"(r10h),
-        [initp] "s"(a.init_regs), [rflag] "s"(rflag), [win] "v"(win), [swz] "v"(swz16),
-        [len] "v"(len), [base] "v"(base), [raddr] "v"(raddr), [vok] "v"(vok)
-      : "s52", "s53", "s54", "s55", "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71", "s72", "s73", "s74", "s75", "s76", "s77", "s78", "s79", "s80", "s81", "s82", "s83", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95", "s96", "s97", "s98", "s99", "v16", "v17", "v18", "v19", "v20", "v21", "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32", "v33", "v34", "v35", "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", "v56", "v57", "v58", "v59", "v60", "v61", "v62", "v63", "vcc", "scc", "memory");
-  return (uint64_t)r0l | ((uint64_t)r0h << 32);
-}
-
-// FIXED: the stride layout with 16-byte aligned slots of >= 64 bytes, no lens array (every packet
-// is `stride` bytes) and no final-image output -- the shape of a NIC ring of fixed slots. Its tile
-// needs no packet metadata at all: the windows are DMA'd straight from pkt * stride.
-template <bool FIXED>
-__global__ __launch_bounds__(kBlock, 5) void dag_tile_kernel(LaunchArgs a) {
-  counters_init();
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const uint32_t lane = threadIdx.x & (kWave - 1);
-  const uint32_t wv = threadIdx.x / kWave;
-  WaveLds L;
-  L.win = smem + wv * kTileWaveLds;
-  L.meta_off = (uint32_t*)(L.win + kWinBytes);
-  L.meta_len = L.meta_off + kWave;
-  const uint32_t my_swz = win_swz(lane);
-  uint8_t* const my_win = L.win + lane * kWin;
-  const uint32_t win_lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)my_win;
-  const uint64_t wave_slot = (uint64_t)blockIdx.x * kWavesPerBlock + wv;
-  const uint64_t total_waves = (uint64_t)gridDim.x * kWavesPerBlock;
-  const uint32_t mem_size = a.mem_size;
-
-  uint64_t cnt[7] = {0, 0, 0, 0, 0, 0, 0};
-  uint64_t retired = 0;
-
-  for (uint64_t tile = wave_slot; tile < a.n_tiles; tile += total_waves) {
-    const uint64_t pkt = tile * kWave + lane;
-    const bool valid = pkt < a.n;
-    const uint8_t* base;
-    uint32_t len;
-    if (FIXED) {
-      dma_window_stride(a, L.win, tile, lane);
-      base = a.frames + pkt * a.stride;
-      len = valid ? stride_len(a) : 0u;
-      dma_wait();
-    } else {
-      // ---- header windows (as dag_kernel) ----
-      const bool sw = stride_windows(a);
-      dma_meta(a, L, 0, tile, lane);
-      if (sw) dma_window_stride(a, L.win, tile, lane);
-      dma_wait();
-      uintptr_t mb;
-      uint32_t ml;
-      meta_of(a, L, 0, tile, lane, mb, ml);
-      base = (const uint8_t*)mb;
-      len = valid ? ml : 0u;
-      const bool co = sw || ballot(valid && ml != 0 && (mb & 15) != 0) == 0;
-      if (co) {
-        if (!sw) {
-          dma_window(a, L, 0, 0, tile, lane);
-          dma_wait();
-        }
-      } else {
-        stage_window_lane(my_win, my_swz, base, len, valid);
-      }
-    }
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // the window's LDS writes / metadata reads: done
-
-    uint32_t lpc = valid ? 0u : PC_DONE;
-    uint32_t st = EBPF_ST_OK;
-    uint32_t nsteps = 0;
-    if (valid && len > mem_size) {  // main.rs:20-21 index panic
-      st = EBPF_ST_BADPKT;
-      lpc = PC_DONE;
-    }
-    const uint64_t live = ballot(lpc == 0) != 0 ? 1ull : 0ull;
-    const uint64_t raddr = a.regs_out ? (uint64_t)(uintptr_t)(a.regs_out + pkt * 11) : 0ull;
-    const uint64_t r0v = dag_tile_asm(live, lpc, nsteps, st, a, win_lds, my_swz << 4, len,
-                                      (uint64_t)(uintptr_t)base, raddr, valid ? 1u : 0u);
-
-    // ---- outputs: r0 (main.rs:43), status, verdict (xdp.rs:3-9), final image ----
-    if (!FIXED && a.mem_out && valid) {
-      uint32_t* mo = (uint32_t*)(a.mem_out + pkt * (uint64_t)mem_size);
-      const uint32_t m = min(len, mem_size);
-      for (uint32_t d = 0; d < mem_size / 4; d++) {
-        uint32_t v;
-        if (d * 4 >= m) v = 0u;
-        else if (d * 4 < (uint32_t)kWin) v = (uint32_t)win_read(my_win, my_swz, d * 4, 4, len);
-        else v = (uint32_t)pkt_read(base, d * 4, 4, len);
-        mo[d] = v;
-      }
-    }
-    if (valid) {
-      if (a.r0) a.r0[pkt] = r0v;
-      if (a.status) a.status[pkt] = (uint8_t)st;
-      if (a.verdict) a.verdict[pkt] = st ? (uint8_t)EBPF_VERDICT_FAULT
-                                         : (r0v < 5 ? (uint8_t)r0v : (uint8_t)EBPF_VERDICT_OTHER);
-    }
-    const bool okv = valid && st == EBPF_ST_OK;
-#pragma unroll
-    for (int b = 0; b < 5; b++) cnt[b] += __builtin_popcountll(ballot(okv && r0v == (uint64_t)b));
-    cnt[5] += __builtin_popcountll(ballot(okv && r0v >= 5));
-    cnt[6] += __builtin_popcountll(ballot(valid && st != EBPF_ST_OK));
-    retired += valid ? nsteps : 0u;
-  }
-  flush_counters(a, cnt, retired, smem, lane, wv);
-}
-
-// ============================================================================================
 // Length-binned lane packing (loop mode, offsets + lens layouts). Lanes of a tile run until its
 // longest packet is done, so a tile mixing 64- and 1500-byte frames idles half its lanes in a
 // per-byte loop. A counting sort by class ceil(len / 128) (capped) groups similar lengths:
@@ -1425,6 +1261,8 @@ hipError_t launch_xdp_stage(const uint8_t* frames, const uint32_t* offsets, cons
 // FIXED: the stride layout with 16-byte aligned slots of >= 64 bytes, no lens array and no
 // final-image output (a NIC ring of fixed slots): no packet metadata at all.
 // ============================================================================================
+constexpr uint32_t kTileWaveLds = kWinBytes + kDagMetaBytes;  // window + metadata, 4.5 KiB
+
 template <bool FIXED, bool LOOPS>
 __global__ __launch_bounds__(kBlock, 8) void tile_kernel(LaunchArgs a) {
   counters_init();
@@ -1574,12 +1412,10 @@ static bool g_db = [] {  // tier-0 window double-buffering (EBPFEMU_TIER0_DB=0|1
   return e ? e[0] == '1' : false;
 }();
 
-// A/B switch (EBPFEMU_DAG_VARIANT): 19 dag_tile_kernel (default); dag_kernel feature bits -- 1
-// windows and lengths in one DMA round trip, 2 operand B formed after the dispatch, 8 the
-// hand-written loop with the C++ step for the micro-ops it leaves
-static int g_dag_variant = [] {
-  const char* e = getenv("EBPFEMU_DAG_VARIANT");
-  return e ? atoi(e) : 19;
+// A/B switch: EBPFEMU_NO_TILE=1 runs forward-only programs on dag_kernel instead of tile_kernel.
+static bool g_no_tile = [] {
+  const char* e = getenv("EBPFEMU_NO_TILE");
+  return e && e[0] == '1';
 }();
 
 // A/B knob (EBPFEMU_LDS_PAD=bytes): extra dynamic LDS per workgroup, to lower occupancy on purpose.
@@ -1592,9 +1428,7 @@ static uint32_t lds_bytes_for(int kind, uint32_t n_uops) {
   if (kind == kKindLoop) return g_lds_pad + kWavesPerBlock * kTileWaveLds;
   if (kind == kKindDag)  // the program is fetched by SMEM
     return g_lds_pad +
-           kWavesPerBlock * ((n_uops <= kTileMaxUops && g_dag_variant == 19) ||
-                                     (n_uops <= 64 && g_dag_variant == 20)
-                                 ? kTileWaveLds : kDagWaveLds);
+           kWavesPerBlock * (n_uops <= kTileMaxUops && !g_no_tile ? kTileWaveLds : kDagWaveLds);
   const uint32_t prog = n_uops <= (uint32_t)kMaxLdsUops ? n_uops * (uint32_t)sizeof(Uop) : 0u;
   uint32_t rest = kind == kKindTier0 ? kWavesPerBlock * wave_lds0(g_db) : 0u;
   return prog + rest;
@@ -1613,7 +1447,7 @@ static const void* variant(uint32_t n_uops) {
 
 // Programs that run on tile_kernel (kKindLoop always does).
 static bool tile_kernel_for(int kind, uint32_t n_uops) {
-  return kind == kKindLoop || (kind == kKindDag && n_uops <= kTileMaxUops && g_dag_variant == 19);
+  return kind == kKindLoop || (kind == kKindDag && n_uops <= kTileMaxUops && !g_no_tile);
 }
 
 // The tile kernel's lean variant serves the fixed-slot stride layout without image output.
@@ -1624,17 +1458,10 @@ static bool fixed_layout(const LaunchArgs* a) {
 
 static const void* kernel_for(int kind, uint32_t n_uops, const LaunchArgs* a = nullptr) {
   if (kind == kKindDag) {
-    if (n_uops > 64) return (const void*)dag_kernel<4, 3>;
-    // 19: the self-contained tile loop (default); 11: the hand-written loop with a C++ step
-    // for the rest; 3: the C++ step only
-    if (g_dag_variant == 3) return (const void*)dag_kernel<1, 3>;
-    if (g_dag_variant == 11) return (const void*)dag_kernel<1, 11>;
     if (tile_kernel_for(kind, n_uops))
       return fixed_layout(a) ? (const void*)tile_kernel<true, false>
                              : (const void*)tile_kernel<false, false>;
-    if (g_dag_variant == 20)  // the previous self-contained tile loop (A/B)
-      return fixed_layout(a) ? (const void*)dag_tile_kernel<true> : (const void*)dag_tile_kernel<false>;
-    return (const void*)dag_kernel<1, 3>;
+    return n_uops > 64 ? (const void*)dag_kernel<4> : (const void*)dag_kernel<1>;
   }
   if (kind == kKindLoop) return (const void*)tile_kernel<false, true>;
   if (kind == kKindTier1) return variant<1, false>(n_uops);

@@ -62,9 +62,9 @@ constexpr uint32_t kRegStride = 64 * 8;
 
 // Micro-op of the DAG kernel (tier-0 programs whose jumps all go forward, dag_kernel in
 // interp.hip): a Uop with everything the kernel would otherwise compute per step resolved at
-// load time, fetched by scalar loads straight into SGPRs. Two independent halves: dwords 0..23
-// for the hand-written loop (dword i lands in s[64 + i], dag_asm.h / gen_dag_loop.py) and dwords
-// 32..47 for the C++ step.
+// load time, fetched by scalar loads straight into SGPRs. Two halves: dwords 0..23 hold the
+// hand-written handlers' view (dag_asm.h ids, from which build_tile makes the tile kernel's TUop)
+// and dwords 32..47 dag_kernel's C++ step.
 struct alignas(256) DUop {
   // ---- the hand-written loop ----
   uint32_t hoff;    // d0: handler slot offset (dag_asm.h id * DAG_SLOT)
