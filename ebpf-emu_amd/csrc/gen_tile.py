@@ -891,7 +891,31 @@ s_nop 0
 global_load_lds_dwordx4 {{T1213}}, off
 v_lshl_add_u64 {{T45}}, {{T45}}, 0, 16
 v_lshl_add_u64 {{T89}}, {{T89}}, 0, {{T1}}""" for r in range(4)) + """
+; prefetch the wave's next tile (%[ntile]; %[pf] = 0: none) into L2 / the Infinity Cache while
+; this one is interpreted: one dword of every packet, landing in the 512 B of LDS metadata the
+; FIXED layout does not use; the windows wait for all but this youngest load
+s_cmp_eq_u32 %[pf], 0
+s_cbranch_scc1 .Lnopf%=
+v_mov_b32 {t4}, {t0}
+v_mov_b32 {t5}, 0
+s_lshl_b64 {T1}, %[ntile], 6
+v_lshl_add_u64 {T45}, {T45}, 0, {T1}
+v_cmp_gt_u64 vcc, {KN}, {T45}
+v_mov_b32 {t12}, {KSTL}
+v_mad_u64_u32 {T89}, {T4}, {t4}, {t12}, {KFR}
+v_mul_lo_u32 {t12}, {t5}, {KSTL}
+v_mul_lo_u32 {t13}, {t4}, {KSTH}
+v_add3_u32 {t9}, {t9}, {t12}, {t13}
+v_cndmask_b32 {t12}, {t10}, {t8}, vcc
+v_cndmask_b32 {t13}, {t11}, {t9}, vcc
+s_mov_b32 m0, %[metab]
+s_nop 0
+global_load_lds_dword {T1213}, off
+s_waitcnt vmcnt(1)
+s_branch .Lpfd%=
+.Lnopf%=:
 s_waitcnt vmcnt(0)
+.Lpfd%=:
 .endif
 v_cmp_gt_u64 vcc, {KN}, {T23}
 s_and_b64 {VM}, vcc, exec
