@@ -767,7 +767,9 @@ def window_tail_ldx(a0, shift):
     """As window_tail for a register-based address, whose bytes may also come from far_read.
     Bytes past len read as zero (main.rs:16): in the FIXED layout every packet is >= 64 bytes
     and a multiple of 16 long, so window bytes are packet bytes and far_read's whole-dword
-    selection already zeroes the rest; otherwise mask them."""
+    selection zeroes the rest of a read that starts inside the packet; a read that starts at or
+    past len (whose registers still hold the window bytes at 0) is zeroed whole. Otherwise mask
+    them byte by byte."""
     return f""".if %[fixed] == 0
 v_sub_u32_e64 {{LENM}}, {{LEN}}, {a0}
 v_cmp_lt_u32 vcc, {a0}, {{LEN}}
@@ -784,6 +786,10 @@ v_and_b32 {{RL}}, {{KML}}, {{RL}}
 v_and_b32 {{RH}}, {{KMH}}, {{RH}}
 v_lshlrev_b64 {{R}}, {{LENM}}, {{R}}
 v_lshrrev_b64 {{R}}, {{LENM}}, {{R}}
+v_cndmask_b32 {{RL}}, 0, {{RL}}, vcc
+v_cndmask_b32 {{RH}}, 0, {{RH}}, vcc
+.else
+v_cmp_lt_u32 vcc, {a0}, {{LEN}}
 v_cndmask_b32 {{RL}}, 0, {{RL}}, vcc
 v_cndmask_b32 {{RH}}, 0, {{RH}}, vcc
 .endif
@@ -833,7 +839,7 @@ v_cndmask_b32 {{RH}}, {{t3}}, {{t11}}, vcc
 {TAILS[sfx]}"""
 
 
-TAILS = {"c": CHAIN, "e": END_N}
+TAILS = {"c": CHAIN, "e": END_N, "j": ""}
 
 # ---- prologue / epilogue ----
 # %[ka]: the kernel-argument segment (LaunchArgs at offset 0; LA_* offsets are "i" operands);
@@ -989,7 +995,9 @@ s_load_dwordx2 s[40:41], {T5}, 0x50
 s_waitcnt lgkmcnt(0)
 """ + "\n".join(f"v_mov_b32 v{16 + i}, s{UB + i}" for i in range(6)) + """
 .Linitd%=:
-s_getpc_b64 {SLOTB}
+"""
+# the interpreter's dispatch entry: handler slots follow the statement's prologue
+SLOTS_HEAD = """s_getpc_b64 {SLOTB}
 .Lpc%=:
 s_add_u32 {SLOTBL}, {SLOTBL}, .Lslots%=-.Lpc%=
 s_addc_u32 {SLOTBH}, {SLOTBH}, 0
@@ -1066,6 +1074,131 @@ s_mov_b64 exec, {EXEC0}
 s_mov_b32 m0, {M0S}"""
 
 
+# ---- JIT templates (jit.cpp): the same handler bodies, compiled per program ----
+# A compiled program is straight-line code over its micro-ops in pc order (forward jumps only):
+# exec holds the lanes running the current basic block; lanes that jump park at the target with
+# LPC = target, and each jump target's entry adds them back (LPC == pc), so the lowest pc runs
+# first exactly as in the interpreter's min-pc dispatch. The handler bodies are those above with
+#   * every s_set_gpr_idx region rewritten to direct register operands: @D<k>@ / @D<a>:<b>@ (dst
+#     register pair 2*dst + k) and @S..@ (src), filled in by the compiler per micro-op;
+#   * the micro-op's fields (s37..s51, TUop dwords 1..15) as tokens @K<d>@ / @K<a>:<b>@: inline
+#     constants where the value is one, else an s_mov into the same SGPR before the micro-op;
+#   * labels unique per micro-op (@U@), the dispatcher replaced by the next block entry (@NEXT@),
+#     and tails by @JTAIL@ (conditional jump), @JA@, @EXIT@.
+GPRIDX_OF = {M["DST2"]: "D", M["SRC2"]: "S"}
+
+
+def _direct_operands(line, idx, roles):
+    """One VALU line of an s_set_gpr_idx region: the VGPR operands in the enabled roles get the
+    index (VGPR index mode adds it to those operands only, never to SGPR or constant ones)."""
+    mn, rest = line.split(None, 1)
+    ops = [o.strip() for o in rest.split(",")]
+    if mn.startswith("v_cmp"):
+        slots = ["SDST", "SRC0", "SRC1"]
+    elif "_co_" in mn:
+        slots = ["DST", "SDST", "SRC0", "SRC1", "SRC2"]
+    else:
+        slots = ["DST", "SRC0", "SRC1", "SRC2"]
+    assert len(ops) <= len(slots), line
+    out = []
+    for slot, o in zip(slots, ops):
+        if slot in roles:
+            m1 = re.fullmatch(r"v(\d+)", o)
+            m2 = re.fullmatch(r"v\[(\d+):(\d+)\]", o)
+            if m1:
+                o = f"@{idx}{m1.group(1)}@"
+            elif m2:
+                o = f"@{idx}{m2.group(1)}:{m2.group(2)}@"
+        out.append(o)
+    return f"{mn} " + ", ".join(out)
+
+
+def jit_text(raw):
+    """A handler body (register names substituted) -> JIT template text."""
+    out, mode = [], None
+    for line in raw.split("\n"):
+        m = re.match(r"s_set_gpr_idx_on (\S+), gpr_idx\(([A-Z0-9,]+)\)$", line.strip())
+        if m:
+            mode = (GPRIDX_OF[m.group(1)], set(m.group(2).split(",")))
+            continue
+        if line.strip() == "s_set_gpr_idx_off":
+            mode = None
+            continue
+        if mode and line.startswith("v_"):
+            line = _direct_operands(line, *mode)
+        out.append(line)
+    assert mode is None
+    t = "\n".join(out)
+    t = t.replace(".Ldisp%=", "@NEXT@").replace(".Lkfault%=", ".Lkf@U@")
+    t = re.sub(r"\.L(\w+)%=", r".L\1@U@", t)
+    assert "%=" not in t, t
+
+    def field(m):
+        a = int(m.group(1)) - UB
+        if m.group(2) is None:
+            return f"@K{a}@" if 1 <= a <= 15 else m.group(0)
+        b = int(m.group(2)) - UB
+        return f"@K{a}:{b}@" if 1 <= a and b <= 15 else m.group(0)
+    t = re.sub(r"\bs\[(\d+):(\d+)\]", lambda m: field(m) if int(m.group(1)) >= UB else m.group(0), t)
+    t = re.sub(r"\bs(\d+)\b", lambda m: (f"@K{int(m.group(1)) - UB}@"
+                                         if UB + 1 <= int(m.group(1)) <= UB + 15 else m.group(0)), t)
+    assert "s_set_gpr_idx" not in t and "s_setpc" not in t and "s_load_dwordx16" not in t, t
+    return t
+
+
+# a constant-address load outside the image: every active lane faults alike (KFAULT above)
+KFAULT_JIT = f""".Lkf@U@:
+s_cmp_ge_u32 {{A0}}, {{KMEM}}
+s_cselect_b32 {{T3}}, {ST_MEM}, {ST_MEM_UB}
+v_mov_b32 {{ST}}, {{T3}}
+v_subrev_u32 {{NST}}, {{REMK}}, {{NST}}
+s_mov_b64 exec, 0
+s_branch @NEXT@"""
+
+JIT_TERM = {
+    "H_EXIT": "@EXIT@",
+    "H_JA": "@JA@",
+    "H_FAULT": "v_mov_b32 {ST}, {IMML}\nv_subrev_u32 {NST}, 1, {NST}\n@EXIT@",
+    "H_SLOW": f"v_mov_b32 {{ST}}, {ST_INSN}\nv_subrev_u32 {{NST}}, 1, {{NST}}\n@EXIT@",
+}
+JIT_OOL = {"ldxk": ldxk, "ldxk1": ldxk1, "ldxk2": ldxk2, "ldxkfar": ldxkfar, "ldx": ldx}
+
+
+def jit_template(base):
+    """(main, out-of-line) JIT template text of handler `base`."""
+    if base == DONE:
+        return "", ""
+    body, kind = H[base]
+    if kind == "term":
+        raw = JIT_TERM[base]
+    elif kind == "jump":
+        raw = body + "\n@JTAIL@"
+    elif kind == "alu":
+        raw = body
+    elif kind == "div":
+        raw = body + "\n" + divmod("j")
+    elif body == "ldx1":
+        raw = ldx1("j", False)
+    else:
+        raw = JIT_OOL[body]("j")
+    main = jit_text(F(raw))
+    ool = jit_text(F(KFAULT_JIT)) if ".Lkf@U@" in main else ""
+    return main, ool
+
+
+def cstr(text):
+    return "\n".join('"' + ln.replace("\\", "\\\\").replace('"', '\\"') + '\\n"'
+                     for ln in text.splitlines()) or '""'
+
+
+# The template kernel's statement: the prologue, a marker the compiler fills in at load time, the
+# epilogue. The marker line carries the statement's label number and operand registers.
+JIT_STATEMENT = PROLOGUE + """
+; JIT N=%= fixed=%[fixed] loops=%[loops] aligned=%[aligned]
+;@@JIT@@
+""" + EPILOGUE
+
+
 def handler_table():
     """Handler names in slot order and their id: every "alu"/"div"/"ool" kind has a chained (_C)
     and a block-end (_E) form; the others one form (_E); then DONE."""
@@ -1080,8 +1213,7 @@ def handler_table():
 
 def main():
     table = handler_table()
-    parts = [PROLOGUE]
-    ool = []
+    parts = [PROLOGUE + SLOTS_HEAD]
     for idx, (name, base, sfx) in enumerate(table):
         if base == DONE:
             code = "s_branch .Ldone%="
@@ -1139,6 +1271,21 @@ def main():
     ids.append("static const short kTileIdEnd[] = {" + ", ".join(e_map) + "};")
     with open(os.path.join(HERE, "tile_ids.h"), "w") as f:
         f.write("\n".join(ids) + "\n")
+    # JIT: the template kernel's statement and the per-handler templates, indexed by tile id
+    text = F(JIT_STATEMENT)
+    assert "{" not in text
+    with open(os.path.join(HERE, "tile_jit.inc"), "w") as f:
+        f.write("// GENERATED by gen_tile.py -- do not edit. The JIT template kernel's statement.\n"
+                "// clang-format off\n" + cstr(text) + "\n// clang-format on\n")
+    out = ["// GENERATED by gen_tile.py -- do not edit. Per-handler JIT templates (jit.cpp), indexed",
+           "// by tile id (tile_ids.h): {main text, out-of-line text}.", "#pragma once",
+           "// clang-format off", "static const char* const kJitTemplates[T_COUNT][2] = {"]
+    for idx, (name, base, sfx) in enumerate(table):
+        main_t, ool_t = jit_template(base)
+        out.append(f"// {name}\n{{{cstr(main_t)},\n{cstr(ool_t)}}},")
+    out += ["};", "// clang-format on"]
+    with open(os.path.join(HERE, "jit_tmpl.h"), "w") as f:
+        f.write("\n".join(out) + "\n")
 
 
 if __name__ == "__main__":

@@ -19,6 +19,7 @@
 #include "dag_asm.h"
 #include "tile_ids.h"
 #include "launch.h"
+#include "jit.h"
 #include "uop.h"
 
 using namespace ebpfemu;
@@ -231,7 +232,39 @@ struct ebpf_prog {
   std::vector<TUop> ltuops, ltuopsx;
   TUop* dev_ltuops[kMaxDevices] = {};
   TUop* dev_ltuopsx[kMaxDevices] = {};
+  // the compiled program (jit.cpp), per variant of tuops / tuopsk: code object, and its module on
+  // each device. jit_state: 0 not compiled yet, 1 compiled, 2 not a compiled program, < 0 failed
+  int jit_state = 0;
+  std::vector<char> jit_co[2];
+  std::string jit_asm[2];
+  std::string jit_err;
+  hipModule_t jit_mod[kMaxDevices][2] = {};
+  JitFns jit_fn[kMaxDevices][2];
 };
+
+// EBPFEMU_NO_JIT=1: forward-only programs run on the tile interpreter (A/B runs).
+static const bool g_no_jit = [] {
+  const char* e = getenv("EBPFEMU_NO_JIT");
+  return e && e[0] == '1';
+}();
+
+// Compile both table variants (caller holds p->mu). Returns the C ABI code of ebpf_prog_compile.
+static int jit_compile_locked(ebpf_prog* p) {
+  if (p->jit_state == 0) {
+    if (g_no_jit || p->tuops.empty() || p->tuopsk.empty()) {
+      p->jit_state = 2;
+    } else {
+      p->jit_state = 1;
+      for (int v = 0; v < 2 && p->jit_state == 1; v++)
+        if (!jit_compile(p->uops, v ? p->tuopsk : p->tuops, p->jit_co[v], &p->jit_err,
+                         &p->jit_asm[v]))
+          p->jit_state = EBPF_EJIT;
+      if (p->jit_state == EBPF_EJIT && getenv("EBPFEMU_JIT_VERBOSE"))
+        fprintf(stderr, "ebpfemu: program compiler: %s\n", p->jit_err.c_str());
+    }
+  }
+  return p->jit_state == 1 ? 1 : p->jit_state == 2 ? 0 : p->jit_state;
+}
 
 // Length-binned lane packing for the loop-mode tile kernel (EBPFEMU_BIN=0|1 forces it off/on;
 // default: offsets + lens layouts of >= kBinMinPackets packets).
@@ -607,6 +640,11 @@ void ebpf_prog_free(ebpf_prog* p) {
       if (p->dev_ltuops[d]) hipFree(p->dev_ltuops[d]);
       if (p->dev_ltuopsx[d]) hipFree(p->dev_ltuopsx[d]);
     }
+    for (int v = 0; v < 2; v++)
+      if (p->jit_mod[d][v]) {
+        hipSetDevice(d);
+        (void)hipModuleUnload(p->jit_mod[d][v]);
+      }
   }
   hipSetDevice(cur);
   delete p;
@@ -630,6 +668,26 @@ int ebpf_prog_insn(const ebpf_prog* p, size_t i, int32_t* imm, int64_t* imm64, i
 int ebpf_prog_tier(const ebpf_prog* p) { return p ? p->tier : -1; }
 
 int ebpf_prog_forward_only(const ebpf_prog* p) { return p ? (p->duops.empty() ? 0 : 1) : -1; }
+
+int ebpf_prog_compile(ebpf_prog* p) {
+  if (!p) return EBPF_EINVAL;
+  std::lock_guard<std::mutex> lk(p->mu);
+  return jit_compile_locked(p);
+}
+
+int ebpf_prog_jit_asm(ebpf_prog* p, int variant, char* buf, size_t cap, size_t* len) {
+  if (!p || variant < 0 || variant > 1) return EBPF_EINVAL;
+  std::lock_guard<std::mutex> lk(p->mu);
+  if (jit_compile_locked(p) != 1) return EBPF_EINVAL;
+  const std::string& a = p->jit_asm[variant];
+  if (len) *len = a.size();
+  if (buf && cap) {
+    const size_t k = std::min(cap - 1, a.size());
+    std::memcpy(buf, a.data(), k);
+    buf[k] = 0;
+  }
+  return EBPF_OK;
+}
 
 int ebpf_prog_upload(ebpf_prog* p, int device) {
   if (!p || device < 0 || device >= kMaxDevices) return EBPF_EINVAL;
@@ -674,6 +732,11 @@ int ebpf_prog_upload(ebpf_prog* p, int device) {
   putt(p->tuopsk, &tdk);
   putt(p->ltuops, &tl);
   putt(p->ltuopsx, &tlx);
+  // the compiled program's modules on this device (a compiler failure leaves the interpreter)
+  if (rc == EBPF_OK && jit_compile_locked(p) == 1) {
+    for (int v = 0; v < 2 && rc == EBPF_OK; v++)
+      if (!jit_load(p->jit_co[v], &p->jit_mod[device][v], &p->jit_fn[device][v])) rc = EBPF_EHIP;
+  }
   if (rc == EBPF_OK) {
     p->dev_uops[device] = d;
     p->dev_duops[device] = dd;
@@ -732,7 +795,7 @@ static int check_batch(const ebpf_batch* b) {
   if (b->max_steps == 0) return EBPF_EINVAL;
   if (b->n && !b->frames) return EBPF_EINVAL;
   if (!b->offsets && b->stride == 0 && !b->lens) return EBPF_EINVAL;
-  if (b->flags & ~(EBPF_BATCH_GENERIC | EBPF_BATCH_XDP_MD)) return EBPF_EINVAL;
+  if (b->flags & ~(EBPF_BATCH_GENERIC | EBPF_BATCH_XDP_MD | EBPF_BATCH_NO_JIT)) return EBPF_EINVAL;
   if ((b->flags & EBPF_BATCH_XDP_MD) &&
       (b->mem_size > 65528 || xdp_image_bytes(b) > 0xFFFFFFFFull))
     return EBPF_EINVAL;  // 8 + len must fit the u16 lengths; staged offsets are u32
@@ -854,7 +917,11 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* bin, const ebpf_batch_out* ou
       return EBPF_EHIP;
     }
   }
-  hipError_t e = launch_interp(kind, a, grid, s);
+  // the compiled program, where it applies (tile-kernel programs; same tables, same results)
+  const JitFns* jit = nullptr;
+  if (kind == kKindDag && !(b->flags & EBPF_BATCH_NO_JIT) && p->jit_mod[device][0])
+    jit = &p->jit_fn[device][b->init_regs ? 0 : 1];
+  hipError_t e = launch_interp(kind, a, grid, s, jit);
   if (cur != device) hipSetDevice(cur);
   return e == hipSuccess ? EBPF_OK : EBPF_EHIP;
 }

@@ -1127,6 +1127,7 @@ __global__ __launch_bounds__(kBlock) void dag_kernel(LaunchArgs a) {
   flush_counters(a, cnt, retired, smem, lane, wv);
 }
 
+#ifndef EBPFEMU_JIT_TEMPLATE  // (the JIT template build: the tile kernels only)
 // ============================================================================================
 // Length-binned lane packing (loop mode, offsets + lens layouts). Lanes of a tile run until its
 // longest packet is done, so a tile mixing 64- and 1500-byte frames idles half its lanes in a
@@ -1250,6 +1251,8 @@ hipError_t launch_xdp_stage(const uint8_t* frames, const uint32_t* offsets, cons
   return hipGetLastError();
 }
 
+#endif  // EBPFEMU_JIT_TEMPLATE
+
 // ============================================================================================
 // tile_kernel -- the forward-only fast path for programs of <= 63 micro-ops. The C++ part only
 // moves each tile's header windows HBM -> LDS (LDS-DMA) and turns the per-lane counter bucket
@@ -1264,8 +1267,26 @@ hipError_t launch_xdp_stage(const uint8_t* frames, const uint32_t* offsets, cons
 constexpr uint32_t kTileWaveLds = kWinBytes + kDagMetaBytes;  // window + metadata, 4.5 KiB
 
 
-template <bool FIXED, bool LOOPS>
-__global__ __launch_bounds__(kBlock, 8) void tile_kernel(LaunchArgs a) {
+#define TILE_ASM_OPERANDS \
+        : [bkt] "=&v"(bkt), [nst] "=&v"(nst) \
+        : [ka] "s"(ka), [tile] "s"(t), [winb] "s"(winb), [metab] "s"(metab), \
+          [fixed] "i"(FIXED ? 1 : 0), [loops] "i"(LOOPS ? 1 : 0), [aligned] "s"(rfl(aligned)), \
+          [pf] "s"(rfl(pf)), [ntile] "s"(nt), \
+          [o_tprog] "i"(offsetof(LaunchArgs, tprog)), \
+          [o_tprog_exact] "i"(offsetof(LaunchArgs, tprog_exact)), \
+          [o_maxs] "i"(offsetof(LaunchArgs, max_steps)), [o_perm] "i"(offsetof(LaunchArgs, perm)), \
+          [o_frames] "i"(offsetof(LaunchArgs, frames)), [o_stride] "i"(offsetof(LaunchArgs, stride)), \
+          [o_n] "i"(offsetof(LaunchArgs, n)), [o_mem] "i"(offsetof(LaunchArgs, mem_size)), \
+          [o_offsets] "i"(offsetof(LaunchArgs, offsets)), [o_lens] "i"(offsetof(LaunchArgs, lens)), \
+          [o_init] "i"(offsetof(LaunchArgs, init_regs)), [o_r10] "i"(offsetof(LaunchArgs, r10)), \
+          [o_verdict] "i"(offsetof(LaunchArgs, verdict)), [o_r0] "i"(offsetof(LaunchArgs, r0)), \
+          [o_status] "i"(offsetof(LaunchArgs, status)), [o_regs] "i"(offsetof(LaunchArgs, regs_out)) \
+        : "s33", "s34", "s35", "s36", "s37", "s38", "s39", "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53", "s54", "s55", "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71", "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15", "v16", "v17", "v18", "v19", "v20", "v21", "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32", "v33", "v34", "v35", "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", "vcc", "scc", "memory"
+
+// JIT: the statement of the compiled-program template kernels (tile_jit.inc; jit.cpp fills in the
+// program's code at load time).
+template <bool FIXED, bool LOOPS, bool JIT>
+__device__ __forceinline__ void tile_body(LaunchArgs& a) {
   counters_init();
   // the length bins of this batch were consumed by bin_scatter (earlier on the stream): re-zero
   if (LOOPS && a.perm && blockIdx.x == 0 && threadIdx.x < 2 * kBinClasses)
@@ -1326,22 +1347,15 @@ __global__ __launch_bounds__(kBlock, 8) void tile_kernel(LaunchArgs a) {
     const uint64_t nt = t + total_waves;  // this wave's next tile (prefetched in FIXED mode)
     const uint32_t pf = a.tile_prefetch && nt < a.n_tiles ? 1u : 0u;
     uint32_t bkt, nst;
-    asm volatile(
+    if constexpr (JIT) {
+      asm volatile(
+#include "tile_jit.inc"
+          TILE_ASM_OPERANDS);
+    } else {
+      asm volatile(
 #include "tile.inc"
-        : [bkt] "=&v"(bkt), [nst] "=&v"(nst)
-        : [ka] "s"(ka), [tile] "s"(t), [winb] "s"(winb), [metab] "s"(metab),
-          [fixed] "i"(FIXED ? 1 : 0), [loops] "i"(LOOPS ? 1 : 0), [aligned] "s"(rfl(aligned)),
-          [pf] "s"(rfl(pf)), [ntile] "s"(nt),
-          [o_tprog] "i"(offsetof(LaunchArgs, tprog)),
-          [o_tprog_exact] "i"(offsetof(LaunchArgs, tprog_exact)),
-          [o_maxs] "i"(offsetof(LaunchArgs, max_steps)), [o_perm] "i"(offsetof(LaunchArgs, perm)),
-          [o_frames] "i"(offsetof(LaunchArgs, frames)), [o_stride] "i"(offsetof(LaunchArgs, stride)),
-          [o_n] "i"(offsetof(LaunchArgs, n)), [o_mem] "i"(offsetof(LaunchArgs, mem_size)),
-          [o_offsets] "i"(offsetof(LaunchArgs, offsets)), [o_lens] "i"(offsetof(LaunchArgs, lens)),
-          [o_init] "i"(offsetof(LaunchArgs, init_regs)), [o_r10] "i"(offsetof(LaunchArgs, r10)),
-          [o_verdict] "i"(offsetof(LaunchArgs, verdict)), [o_r0] "i"(offsetof(LaunchArgs, r0)),
-          [o_status] "i"(offsetof(LaunchArgs, status)), [o_regs] "i"(offsetof(LaunchArgs, regs_out))
-        : "s33", "s34", "s35", "s36", "s37", "s38", "s39", "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53", "s54", "s55", "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71", "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15", "v16", "v17", "v18", "v19", "v20", "v21", "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32", "v33", "v34", "v35", "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", "vcc", "scc", "memory");
+          TILE_ASM_OPERANDS);
+    }
 
     // ---- final image (Emu.state.mmu.memory): the window, then the packet, then zeros ----
     if (!FIXED && a.mem_out) {
@@ -1380,6 +1394,24 @@ __global__ __launch_bounds__(kBlock, 8) void tile_kernel(LaunchArgs a) {
   asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
   flush_counters(a, cnt64, retired, smem, ln, wv);
 }
+
+#ifndef EBPFEMU_JIT_TEMPLATE
+template <bool FIXED, bool LOOPS>
+__global__ __launch_bounds__(kBlock, 8) void tile_kernel(LaunchArgs a) {
+  tile_body<FIXED, LOOPS, false>(a);
+}
+#else
+// The JIT template kernels (build/tile_jit.s, embedded in the library): jit.cpp inserts each
+// program's compiled code at the marker of their statement and assembles the result.
+extern "C" __global__ __launch_bounds__(kBlock, 8) void ebpf_tile_jit_fixed(LaunchArgs a) {
+  tile_body<true, false, true>(a);
+}
+extern "C" __global__ __launch_bounds__(kBlock, 8) void ebpf_tile_jit_var(LaunchArgs a) {
+  tile_body<false, false, true>(a);
+}
+#endif
+
+#ifndef EBPFEMU_JIT_TEMPLATE
 
 // Folds the shards into the caller's counters (EBPFEMU_FOLD=kernel A/B mode): one workgroup,
 // launched after the interpreter on the same stream.
@@ -1533,7 +1565,8 @@ int interp_grid(int kind, uint32_t n_uops, bool tiny, uint64_t n_tiles, int* gri
   return 0;
 }
 
-hipError_t launch_interp(int kind, const LaunchArgs& a, int grid, hipStream_t stream) {
+hipError_t launch_interp(int kind, const LaunchArgs& a, int grid, hipStream_t stream,
+                         const JitFns* jit) {
   const uint32_t lds = lds_bytes_for(kind, a.n_uops);
   LaunchArgs b = a;
   b.tile_prefetch = g_tile_prefetch ? 1u : 0u;
@@ -1543,8 +1576,13 @@ hipError_t launch_interp(int kind, const LaunchArgs& a, int grid, hipStream_t st
                                  a.n_uops <= kTinyUops;
   b.fold_kernel = fold_kernel ? 1u : 0u;
   void* bargs[] = {(void*)&b};
-  hipError_t e =
-      hipLaunchKernel(kernel_for(kind, a.n_uops, &a), dim3(grid), dim3(kBlock), bargs, lds, stream);
+  hipError_t e;
+  if (jit && kind == kKindDag && tile_kernel_for(kind, a.n_uops))  // the compiled program
+    e = hipModuleLaunchKernel(fixed_layout(&a) ? jit->fixed : jit->var, grid, 1, 1, kBlock, 1, 1,
+                              lds, stream, bargs, nullptr);
+  else
+    e = hipLaunchKernel(kernel_for(kind, a.n_uops, &a), dim3(grid), dim3(kBlock), bargs, lds,
+                        stream);
   if (e != hipSuccess || a.counters == nullptr || !fold_kernel) return e;
   uint64_t* shards = a.shards;
   uint64_t* counters = a.counters;
@@ -1552,5 +1590,7 @@ hipError_t launch_interp(int kind, const LaunchArgs& a, int grid, hipStream_t st
   return hipLaunchKernel((const void*)fold_counters, dim3(1), dim3(kCounterShards * 8), fargs, 0,
                          stream);
 }
+
+#endif  // EBPFEMU_JIT_TEMPLATE
 
 }  // namespace ebpfemu

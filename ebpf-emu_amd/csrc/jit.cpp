@@ -1,0 +1,401 @@
+// jit.cpp — compiles a forward-only eBPF program into gfx950 code for the tile kernel.
+//
+// The tile interpreter (gen_tile.py -> tile.inc) spends most of its issue slots on interpretation:
+// a scalar load of every micro-op and a wait for it, the pc-set search, the jump into the handler
+// slot, and s_set_gpr_idx pairs around every register access. For a program that runs on the
+// tile kernel (tier 0, forward jumps only, <= 62 micro-ops, the reference's whole XDP use case),
+// all of that is known at load time. This compiler emits the program as straight-line code in pc
+// order, built from the very same handler bodies (gen_tile.py -> jit_tmpl.h):
+//   * register operands direct (v[2r : 2r+1] for eBPF register r), no index mode;
+//   * micro-op fields as inline constants where they are one, else an s_mov into the SGPR the
+//     handler reads;
+//   * min-pc re-convergence without a pc set: exec holds the lanes running the current block;
+//     a jump parks its leaving lanes at the target (LPC = target) and every jump target's entry
+//     re-admits the lanes parked there, so blocks run in pc order as the interpreter runs them
+//     (forward jumps only: each block once per tile);
+//   * retired steps counted per block as before (TUop::blen), faults taking back the rest.
+// The code is inserted into the assembly of the template kernels (interp.hip built with
+// EBPFEMU_JIT_TEMPLATE, embedded as kJitTemplateAsm: the tile kernel's C++ prologue, the
+// statement's prologue and epilogue around a marker), assembled and linked in process with
+// amd_comgr, and loaded with hipModuleLoadData. Results are bit-identical to the interpreter's
+// (the same instruction sequences); tests/test_gpu_jit.py checks both against the oracle.
+#include "jit.h"
+
+#include <amd_comgr/amd_comgr.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <set>
+#include <string>
+#include <vector>
+
+#include "jit_template.h"  // build/: kJitTemplateAsm
+#include "tile_ids.h"
+#include "jit_tmpl.h"
+
+namespace ebpfemu {
+
+namespace {
+
+constexpr uint32_t kFieldSgpr = 36;  // TUop dword d lives in s[36 + d] (gen_tile.py UB)
+
+struct Marker {
+  size_t begin = 0, end = 0;  // the marker line ";@@JIT@@" (replaced)
+  std::string n;              // the statement's %= number
+  std::string fixed = "0";
+  std::string aligned;
+};
+
+bool inline_const(int64_t v) { return v >= -16 && v <= 64; }
+
+std::string hex32(uint32_t v) {
+  char b[16];
+  snprintf(b, sizeof b, "0x%x", v);
+  return b;
+}
+
+std::string vreg(uint32_t base, uint32_t a) { return "v" + std::to_string(base + a); }
+std::string vpair(uint32_t base, uint32_t a, uint32_t b) {
+  return "v[" + std::to_string(base + a) + ":" + std::to_string(base + b) + "]";
+}
+
+// Find the markers of the template kernels' statements.
+bool find_markers(const std::string& s, std::vector<Marker>& out) {
+  size_t pos = 0;
+  while ((pos = s.find("; JIT N=", pos)) != std::string::npos) {
+    Marker m;
+    const size_t eol = s.find('\n', pos);
+    const std::string line = s.substr(pos, eol - pos);
+    auto field = [&](const char* key) {
+      const size_t k = line.find(key);
+      if (k == std::string::npos) return std::string();
+      const size_t v = k + strlen(key);
+      return line.substr(v, line.find(' ', v) - v);
+    };
+    m.n = field("N=");
+    m.fixed = field("fixed=");
+    m.aligned = field("aligned=");
+    const size_t mk = s.find(";@@JIT@@", eol);
+    if (mk == std::string::npos || m.n.empty()) return false;
+    m.begin = mk;
+    m.end = s.find('\n', mk);
+    out.push_back(m);
+    pos = m.end;
+  }
+  return !out.empty();
+}
+
+struct Compiler {
+  const std::vector<Uop>& uops;
+  const std::vector<TUop>& t;
+  uint32_t n;
+  std::vector<char> start, target;
+  std::string err;
+
+  Compiler(const std::vector<Uop>& u, const std::vector<TUop>& tt)
+      : uops(u), t(tt), n((uint32_t)u.size()) {
+    start.assign(n + 1, 0);
+    target.assign(n + 1, 0);
+    target[0] = 1;
+    for (uint32_t i = 0; i < n; i++) {
+      if (t[i].blen) start[i] = 1;
+      const Uop& o = uops[i];
+      if (o.op >= U_JA && o.op <= U_JLE32) {
+        const uint32_t x = t[i].x;  // the canonical taken target (PC_DONE past the end)
+        const uint32_t np = t[i].npc;
+        if (x < n) target[x] = 1;
+        if (np < n && np != i + 1) target[np] = 1;
+      }
+    }
+    start[n] = 1;
+  }
+
+  uint32_t next_start(uint32_t i) const {
+    uint32_t j = i + 1;
+    while (j < n && !start[j]) j++;
+    return j;
+  }
+
+  // park the lanes of `mask` ("vcc" or "exec") at pc x (x >= n: they are done, their last
+  // entry's LPC is below every later entry)
+  static std::string park(const std::string& lpc_val, bool done) {
+    return done ? std::string() : "v_mov_b32 v28, " + lpc_val + "\n";
+  }
+
+  // Conditional jump tail: vcc = taken among the active lanes.
+  std::string jtail(uint32_t i) const {
+    const uint32_t x = t[i].x, np = t[i].npc;
+    const bool x_next = x == i + 1, n_next = np == i + 1;
+    const bool x_done = x >= n, n_done = np >= n;
+    if (x_next && n_next) return "";
+    std::string s = "s_mov_b64 s[64:65], exec\n";
+    if (n_next) {  // taken lanes leave
+      s += "s_mov_b64 exec, vcc\n" + park(std::to_string(x), x_done) +
+           "s_andn2_b64 exec, s[64:65], vcc\n";
+    } else if (x_next) {  // not-taken lanes leave
+      s += "s_andn2_b64 exec, s[64:65], vcc\n" + park(std::to_string(np), n_done) +
+           "s_mov_b64 exec, vcc\n";
+    } else {  // both leave
+      s += "s_mov_b64 exec, vcc\n" + park(std::to_string(x), x_done) +
+           "s_andn2_b64 exec, s[64:65], vcc\n" + park(std::to_string(np), n_done) +
+           "s_mov_b64 exec, 0\n";
+    }
+    return s;
+  }
+
+  std::string ja(uint32_t i) const {
+    const uint32_t x = t[i].x;
+    if (x == i + 1) return "";
+    return park(std::to_string(x), x >= n) + "s_mov_b64 exec, 0\n";
+  }
+
+  // Expand the tokens of one template text for micro-op i.
+  bool expand(const char* tmpl, uint32_t i, const Marker& m, const std::string& P,
+              std::set<uint32_t>& sg, std::string& out) {
+    const TUop& u = t[i];
+    const uint32_t* w = (const uint32_t*)&u;
+    const std::string lab = P + "u" + std::to_string(i);
+    const std::string next = ".L" + P + "b" + std::to_string(next_start(i));
+    std::string text(tmpl);
+    size_t ls = 0;
+    while (ls < text.size()) {
+      size_t le = text.find('\n', ls);
+      if (le == std::string::npos) le = text.size();
+      const std::string line = text.substr(ls, le - ls);
+      ls = le + 1;
+      const bool salu = line.compare(0, 2, "s_") == 0;
+      int literals = 0;
+      std::string o;
+      size_t p = 0;
+      while (p < line.size()) {
+        const size_t a = line.find('@', p);
+        if (a == std::string::npos) {
+          o += line.substr(p);
+          break;
+        }
+        const size_t b = line.find('@', a + 1);
+        if (b == std::string::npos) {
+          err = "unterminated token: " + line;
+          return false;
+        }
+        o += line.substr(p, a - p);
+        const std::string tok = line.substr(a + 1, b - a - 1);
+        p = b + 1;
+        if (tok == "U") {
+          o += lab;
+        } else if (tok == "NEXT") {
+          o += next;
+        } else if (tok == "JTAIL") {
+          o += jtail(i);
+        } else if (tok == "JA") {
+          o += ja(i);
+        } else if (tok == "EXIT") {
+          o += "s_mov_b64 exec, 0\n";
+        } else if (tok[0] == 'D' || tok[0] == 'S') {
+          const uint32_t base = tok[0] == 'D' ? u.dst2 : u.src2;
+          if (base > 20) {
+            err = "register index out of range";
+            return false;
+          }
+          const size_t c = tok.find(':');
+          if (c == std::string::npos)
+            o += vreg(base, (uint32_t)std::stoul(tok.substr(1)));
+          else
+            o += vpair(base, (uint32_t)std::stoul(tok.substr(1, c - 1)),
+                       (uint32_t)std::stoul(tok.substr(c + 1)));
+        } else if (tok[0] == 'K') {
+          const size_t c = tok.find(':');
+          if (c == std::string::npos) {
+            const uint32_t d = (uint32_t)std::stoul(tok.substr(1));
+            const uint32_t v = w[d];
+            if (inline_const((int32_t)v)) {
+              o += std::to_string((int32_t)v);
+            } else if (salu && literals == 0) {
+              o += hex32(v);
+              literals++;
+            } else {
+              sg.insert(d);
+              o += "s" + std::to_string(kFieldSgpr + d);
+            }
+          } else {
+            const uint32_t d0 = (uint32_t)std::stoul(tok.substr(1, c - 1));
+            const uint32_t d1 = (uint32_t)std::stoul(tok.substr(c + 1));
+            const int64_t v = (int64_t)((uint64_t)w[d0] | ((uint64_t)w[d1] << 32));
+            if (d1 == d0 + 1 && inline_const(v)) {
+              o += std::to_string(v);
+            } else {
+              for (uint32_t d = d0; d <= d1; d++) sg.insert(d);
+              o += "s[" + std::to_string(kFieldSgpr + d0) + ":" + std::to_string(kFieldSgpr + d1) +
+                   "]";
+            }
+          }
+        } else {
+          err = "unknown token @" + tok + "@";
+          return false;
+        }
+      }
+      // the statement's own operands
+      for (const auto& kv : {std::make_pair(std::string("%[fixed]"), m.fixed),
+                             std::make_pair(std::string("%[loops]"), std::string("0")),
+                             std::make_pair(std::string("%[aligned]"), m.aligned)}) {
+        size_t q;
+        while ((q = o.find(kv.first)) != std::string::npos) o.replace(q, kv.first.size(), kv.second);
+      }
+      if (o.find("%[") != std::string::npos) {
+        err = "unresolved operand: " + o;
+        return false;
+      }
+      out += o;
+      if (!o.empty() && o.back() != '\n') out += '\n';
+    }
+    return true;
+  }
+
+  // The program's code for the statement behind marker m.
+  bool body(const Marker& m, std::string& out) {
+    const std::string P = "J" + m.n + "_";
+    std::string main = "; compiled eBPF program: " + std::to_string(n) + " micro-ops\n"
+                       "s_mov_b64 exec, 0\n";
+    std::string ool;
+    for (uint32_t i = 0; i < n; i++) {
+      if (start[i]) {
+        main += ".L" + P + "b" + std::to_string(i) + ":\n";
+        if (target[i])
+          main += "s_mov_b64 s[64:65], exec\ns_mov_b64 exec, -1\nv_cmp_eq_u32 vcc, " +
+                  std::to_string(i) + ", v28\ns_or_b64 exec, s[64:65], vcc\n";
+        main += "s_cbranch_execz .L" + P + "b" + std::to_string(next_start(i)) + "\n";
+        main += "v_add_u32 v29, " + std::to_string(t[i].blen) + ", v29\n";
+      }
+      const uint32_t id = t[i].hoff / TILE_SLOT;
+      if (id >= (uint32_t)T_COUNT || id == (uint32_t)T_DONE) {
+        err = "bad handler id";
+        return false;
+      }
+      std::set<uint32_t> sg;
+      std::string mt, ot;
+      if (!expand(kJitTemplates[id][0], i, m, P, sg, mt)) return false;
+      if (!expand(kJitTemplates[id][1], i, m, P, sg, ot)) return false;
+      const uint32_t* w = (const uint32_t*)&t[i];
+      for (uint32_t d : sg)
+        main += "s_mov_b32 s" + std::to_string(kFieldSgpr + d) + ", " + hex32(w[d]) + "\n";
+      main += mt;
+      ool += ot;
+    }
+    main += ".L" + P + "b" + std::to_string(n) + ":\n";
+    if (!ool.empty()) main += "s_branch .Ldone" + m.n + "\n" + ool;
+    out = main;
+    return true;
+  }
+};
+
+#define COMGR_OK(x) ((x) == AMD_COMGR_STATUS_SUCCESS)
+
+std::string comgr_log(amd_comgr_data_set_t set) {
+  size_t nl = 0;
+  std::string all;
+  if (!COMGR_OK(amd_comgr_action_data_count(set, AMD_COMGR_DATA_KIND_LOG, &nl))) return all;
+  for (size_t i = 0; i < nl; i++) {
+    amd_comgr_data_t l;
+    if (!COMGR_OK(amd_comgr_action_data_get_data(set, AMD_COMGR_DATA_KIND_LOG, i, &l))) continue;
+    size_t sz = 0;
+    amd_comgr_get_data(l, &sz, nullptr);
+    std::string b(sz, '\0');
+    amd_comgr_get_data(l, &sz, &b[0]);
+    all += b;
+    amd_comgr_release_data(l);
+  }
+  return all;
+}
+
+// .s -> relocatable -> executable code object, in process.
+bool assemble(const std::string& src, std::vector<char>& co, std::string* err) {
+  amd_comgr_data_t d{};
+  amd_comgr_data_set_t in{}, rel{}, exe{};
+  amd_comgr_action_info_t ai{};
+  bool ok = COMGR_OK(amd_comgr_create_data(AMD_COMGR_DATA_KIND_SOURCE, &d)) &&
+            COMGR_OK(amd_comgr_set_data(d, src.size(), src.data())) &&
+            COMGR_OK(amd_comgr_set_data_name(d, "ebpf_jit.s")) &&
+            COMGR_OK(amd_comgr_create_data_set(&in)) && COMGR_OK(amd_comgr_create_data_set(&rel)) &&
+            COMGR_OK(amd_comgr_create_data_set(&exe)) && COMGR_OK(amd_comgr_data_set_add(in, d)) &&
+            COMGR_OK(amd_comgr_create_action_info(&ai)) &&
+            COMGR_OK(amd_comgr_action_info_set_isa_name(ai, "amdgcn-amd-amdhsa--gfx950")) &&
+            COMGR_OK(amd_comgr_action_info_set_language(ai, AMD_COMGR_LANGUAGE_NONE)) &&
+            COMGR_OK(amd_comgr_action_info_set_logging(ai, true));
+  if (ok && !COMGR_OK(amd_comgr_do_action(AMD_COMGR_ACTION_ASSEMBLE_SOURCE_TO_RELOCATABLE, ai, in,
+                                          rel))) {
+    ok = false;
+    if (err) *err = "assembler: " + comgr_log(rel);
+  }
+  if (ok && !COMGR_OK(amd_comgr_do_action(AMD_COMGR_ACTION_LINK_RELOCATABLE_TO_EXECUTABLE, ai, rel,
+                                          exe))) {
+    ok = false;
+    if (err) *err = "linker: " + comgr_log(exe);
+  }
+  if (ok) {
+    amd_comgr_data_t e;
+    size_t sz = 0;
+    ok = COMGR_OK(amd_comgr_action_data_get_data(exe, AMD_COMGR_DATA_KIND_EXECUTABLE, 0, &e));
+    if (ok) {
+      amd_comgr_get_data(e, &sz, nullptr);
+      co.resize(sz);
+      ok = COMGR_OK(amd_comgr_get_data(e, &sz, co.data()));
+      amd_comgr_release_data(e);
+    }
+    if (!ok && err) *err = "no executable";
+  }
+  if (ai.handle) amd_comgr_destroy_action_info(ai);
+  if (exe.handle) amd_comgr_destroy_data_set(exe);
+  if (rel.handle) amd_comgr_destroy_data_set(rel);
+  if (in.handle) amd_comgr_destroy_data_set(in);
+  if (d.handle) amd_comgr_release_data(d);
+  return ok;
+}
+
+}  // namespace
+
+bool jit_compile(const std::vector<Uop>& uops, const std::vector<TUop>& t,
+                 std::vector<char>& code_object, std::string* err, std::string* asm_out) {
+  if (uops.empty() || uops.size() > kTileMaxUops || t.size() < uops.size()) {
+    if (err) *err = "not a tile program";
+    return false;
+  }
+  const std::string tmpl(kJitTemplateAsm);
+  std::vector<Marker> marks;
+  if (!find_markers(tmpl, marks)) {
+    if (err) *err = "template markers not found";
+    return false;
+  }
+  Compiler c(uops, t);
+  std::string src;
+  size_t at = 0;
+  for (const Marker& m : marks) {
+    std::string b;
+    if (!c.body(m, b)) {
+      if (err) *err = c.err;
+      return false;
+    }
+    src += tmpl.substr(at, m.begin - at);
+    src += b;
+    at = m.end;
+  }
+  src += tmpl.substr(at);
+  if (asm_out) *asm_out = src;
+  return assemble(src, code_object, err);
+}
+
+bool jit_load(const std::vector<char>& co, hipModule_t* mod, JitFns* fns) {
+  hipModule_t m = nullptr;
+  if (hipModuleLoadData(&m, co.data()) != hipSuccess) return false;
+  JitFns f;
+  if (hipModuleGetFunction(&f.fixed, m, "ebpf_tile_jit_fixed") != hipSuccess ||
+      hipModuleGetFunction(&f.var, m, "ebpf_tile_jit_var") != hipSuccess) {
+    (void)hipModuleUnload(m);
+    return false;
+  }
+  *mod = m;
+  *fns = f;
+  return true;
+}
+
+}  // namespace ebpfemu

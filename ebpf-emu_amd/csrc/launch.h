@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "jit.h"
 #include "uop.h"
 
 namespace ebpfemu {
@@ -92,6 +93,8 @@ hipError_t launch_xdp_stage(const uint8_t* frames, const uint32_t* offsets, cons
                             hipStream_t stream);
 
 // Enqueue the interpreter on `stream`; with counters, its last workgroup folds the shards into them.
-hipError_t launch_interp(int kind, const LaunchArgs& a, int grid, hipStream_t stream);
+// jit: the program's compiled kernels, launched instead of the tile interpreter where it would run.
+hipError_t launch_interp(int kind, const LaunchArgs& a, int grid, hipStream_t stream,
+                         const JitFns* jit = nullptr);
 
 }  // namespace ebpfemu

@@ -16,7 +16,7 @@ LIB_PATH = os.path.join(_HERE, "libebpfemu.so")
 EBPF_OK = 0
 EBPF_EINVAL, EBPF_ELEN, EBPF_EREG, EBPF_EOP, EBPF_EMODE = -1, -2, -3, -4, -5
 EBPF_ELDDW, EBPF_ELDDW_OVF, EBPF_EHEX, EBPF_ENOMEM, EBPF_EHIP = -6, -7, -8, -9, -10
-EBPF_ETOOBIG, EBPF_ERCCL, EBPF_EPCAP = -11, -12, -13
+EBPF_ETOOBIG, EBPF_ERCCL, EBPF_EPCAP, EBPF_EJIT = -11, -12, -13, -14
 
 ST_OK, ST_MEM, ST_MEM_UB, ST_INSN, ST_ARITH, ST_STEPS, ST_CALLDEPTH, ST_BADPKT = range(8)
 STATUS_NAMES = ["OK", "MEM", "MEM_UB", "INSN", "ARITH", "STEPS", "CALLDEPTH", "BADPKT"]
@@ -25,11 +25,12 @@ NCOUNTERS = 8
 DEFAULT_MEM, DEFAULT_R10, DEFAULT_STEPS = 1024, 512, 1 << 22
 BATCH_GENERIC = 1  # ebpf_batch.flags: EBPF_BATCH_GENERIC
 BATCH_XDP_MD = 2   # ebpf_batch.flags: EBPF_BATCH_XDP_MD (the xdp_md calling convention)
+BATCH_NO_JIT = 4   # ebpf_batch.flags: EBPF_BATCH_NO_JIT (the tile interpreter, not the compiled program)
 MAX_CALL_DEPTH = 64
 
 EXPORTS = ["ebpf_batch_init", "ebpf_prog_load", "ebpf_prog_load_hex", "ebpf_prog_free",
            "ebpf_prog_len", "ebpf_prog_insn", "ebpf_prog_tier", "ebpf_prog_forward_only",
-           "ebpf_workspace_bytes",
+           "ebpf_workspace_bytes", "ebpf_prog_compile", "ebpf_prog_jit_asm",
            "ebpf_prog_upload", "ebpf_run_batch", "ebpf_run_batch_multi", "ebpf_pcap_index",
            "ebpf_strerror", "ebpf_version"]
 
@@ -85,6 +86,8 @@ def lib():
                                  ctypes.POINTER(ctypes.c_uint8)]
     L.ebpf_prog_tier.argtypes = [vp]
     L.ebpf_prog_forward_only.argtypes = [vp]
+    L.ebpf_prog_compile.argtypes = [vp]
+    L.ebpf_prog_jit_asm.argtypes = [vp, ctypes.c_int, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
     L.ebpf_workspace_bytes.argtypes = [vp, ctypes.POINTER(Batch), ctypes.c_int]
     L.ebpf_workspace_bytes.restype = u64
     L.ebpf_prog_upload.argtypes = [vp, ctypes.c_int]

@@ -61,6 +61,26 @@ class Program:
         """True when batches run on the forward-jump fast path (max_steps >= len(self))."""
         return bool(_lib.lib().ebpf_prog_forward_only(self._h))
 
+    def compile(self) -> bool:
+        """Compile to gfx950 code now (ebpf_prog_compile): True if this is a compiled program
+        (tier 0, forward jumps only, <= 62 micro-ops), False if it runs interpreted."""
+        rc = _lib.lib().ebpf_prog_compile(self._h)
+        if rc < 0:
+            raise _lib.EbpfError(rc, "ebpf_prog_compile")
+        return rc == 1
+
+    def jit_asm(self, variant: int = 1) -> str:
+        """The compiled program's assembly (variant 1: the main.rs register layout, 0: with
+        init_regs)."""
+        L = _lib.lib()
+        n = ctypes.c_size_t(0)
+        rc = L.ebpf_prog_jit_asm(self._h, variant, None, 0, ctypes.byref(n))
+        if rc:
+            raise _lib.EbpfError(rc, "ebpf_prog_jit_asm")
+        buf = ctypes.create_string_buffer(n.value + 1)
+        L.ebpf_prog_jit_asm(self._h, variant, buf, n.value + 1, ctypes.byref(n))
+        return buf.value.decode()
+
     @property
     def instructions(self):
         return _decoded(self._h)
@@ -84,7 +104,8 @@ class Program:
     def make_batch(self, frames, n: int | None = None, stride: int = 0, offsets=None, lens=None,
                    mem_size: int = _lib.DEFAULT_MEM, r10: int = _lib.DEFAULT_R10,
                    max_steps: int = _lib.DEFAULT_STEPS, init_regs=None,
-                   workspace=None, generic: bool = False, xdp_md: bool = False) -> _lib.Batch:
+                   workspace=None, generic: bool = False, xdp_md: bool = False,
+                   no_jit: bool = False) -> _lib.Batch:
         b = _lib.Batch()
         _lib.lib().ebpf_batch_init(ctypes.byref(b))
         if n is None:
@@ -98,7 +119,8 @@ class Program:
         b.r10 = r10 & ((1 << 64) - 1)
         b.max_steps = max_steps
         b.init_regs = init_regs.data_ptr() if init_regs is not None else None
-        b.flags = (_lib.BATCH_GENERIC if generic else 0) | (_lib.BATCH_XDP_MD if xdp_md else 0)
+        b.flags = ((_lib.BATCH_GENERIC if generic else 0) | (_lib.BATCH_XDP_MD if xdp_md else 0) |
+                   (_lib.BATCH_NO_JIT if no_jit else 0))
         if workspace is not None:
             b.workspace = workspace.data_ptr()
             b.workspace_bytes = workspace.numel() * workspace.element_size()
@@ -122,13 +144,14 @@ class Program:
             max_steps: int = _lib.DEFAULT_STEPS, init_regs=None, verdict: bool = True,
             r0: bool = False, status: bool = False, counters=None, mem: bool = False,
             regs: bool = False, stream=None, generic: bool = False,
-            xdp_md: bool = False) -> BatchResult:
+            xdp_md: bool = False, no_jit: bool = False) -> BatchResult:
         """Run the program over a device-resident batch; returns device tensors.
 
         frames: torch.uint8 CUDA tensor. Layout: packet i at frames[i*stride:] (stride layout,
         len = lens[i] or stride) or at frames[offsets[i]:] (offsets: torch.int32 / uint32 bits,
         lens: torch.int16/uint16 bits). counters: an optional torch.int64 [8] tensor to add to.
         generic: run on the general interpreter even if the forward-jump fast path applies.
+        no_jit: run a compiled program (compile()) on the tile interpreter instead.
         xdp_md: the xdp_md calling convention (EBPF_BATCH_XDP_MD): each image is
         [u32 data = 8][u32 data_end = 8 + len][packet], r1 = 0 the ctx, r2 = 8 + len.
         """
@@ -136,7 +159,7 @@ class Program:
 
         dev = frames.device
         b = self.make_batch(frames, n, stride, offsets, lens, mem_size, r10, max_steps, init_regs,
-                            generic=generic, xdp_md=xdp_md)
+                            generic=generic, xdp_md=xdp_md, no_jit=no_jit)
         n = b.n
         res = BatchResult()
         if verdict:

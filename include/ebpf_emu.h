@@ -38,6 +38,7 @@ typedef struct ihipStream_t* ebpf_stream_t; /* == hipStream_t */
 #define EBPF_ETOOBIG       (-11) /* program beyond the device limit (EBPF_MAX_INSNS) */
 #define EBPF_ERCCL         (-12) /* an RCCL call failed */
 #define EBPF_EPCAP         (-13) /* not a classic pcap capture, or a truncated record */
+#define EBPF_EJIT          (-14) /* the program compiler failed (amd_comgr assembler/linker) */
 
 /* ---- per-packet status (u8) ---- */
 #define EBPF_ST_OK          0  /* exit with empty frame stack or pc past the end (emu.rs:49,277) */
@@ -78,6 +79,9 @@ typedef struct ihipStream_t* ebpf_stream_t; /* == hipStream_t */
  * ctx-prefixed bytes. The library stages the images in the workspace (a device copy of the
  * packets), then runs the batch as usual. Requires mem_size <= 65528. */
 #define EBPF_BATCH_XDP_MD  2u
+/* ebpf_batch.flags: run a compiled program (ebpf_prog_compile) on the tile interpreter instead
+ * (differential testing; results are identical by contract). */
+#define EBPF_BATCH_NO_JIT  4u
 #define EBPF_DEFAULT_MEM    1024   /* main.rs:16 */
 #define EBPF_DEFAULT_R10    512    /* main.rs:31 */
 #define EBPF_DEFAULT_STEPS  (1ull << 22)
@@ -93,7 +97,7 @@ typedef struct ebpf_batch {
                                n * stride bytes (every slot whole, as in a ring of fixed slots) */
   uint64_t n;               /* packets */
   uint32_t mem_size;        /* bytes of the per-packet memory image (multiple of 8, >= 8) */
-  uint32_t flags;           /* 0, or EBPF_BATCH_GENERIC | EBPF_BATCH_XDP_MD */
+  uint32_t flags;           /* 0, or EBPF_BATCH_GENERIC | EBPF_BATCH_XDP_MD | EBPF_BATCH_NO_JIT */
   uint64_t r10;             /* initial r10 (stack top) */
   uint64_t max_steps;       /* per-packet step budget, 1..; faults EBPF_ST_STEPS beyond */
   void* workspace;          /* optional device scratch of ebpf_workspace_bytes() bytes, ZEROED before its
@@ -145,6 +149,19 @@ int ebpf_prog_tier(const ebpf_prog* prog);
  * forward-jump fast path -- for batches with max_steps >= its length and without
  * EBPF_BATCH_GENERIC -- else 0; -1 for NULL. */
 int ebpf_prog_forward_only(const ebpf_prog* prog);
+
+/* Compile the program to gfx950 machine code now, if it is one the tile fast path runs (memory
+ * tier 0, every jump forward, <= 62 micro-ops): straight-line code in pc order with direct
+ * register operands, replacing the interpreter's dispatch for those programs (ebpf_run_batch
+ * then launches it for batches with max_steps >= the program length). Needs no GPU; done
+ * implicitly by the first upload. Returns 1 = compiled, 0 = not such a program (or compilation
+ * disabled by EBPFEMU_NO_JIT=1), EBPF_EJIT on a compiler failure. */
+int ebpf_prog_compile(ebpf_prog* prog);
+
+/* The compiled program's gfx950 assembly (variant 0: batches with init_regs, 1: the main.rs
+ * register layout, whose constant-address loads are resolved), for inspection: copies up to cap
+ * bytes (NUL-terminated) and sets *len to the full length. EBPF_EINVAL if not compiled. */
+int ebpf_prog_jit_asm(ebpf_prog* prog, int variant, char* buf, size_t cap, size_t* len);
 
 /* Device scratch a batch needs (counter shards; tier 1 adds per-wave memory images). */
 uint64_t ebpf_workspace_bytes(const ebpf_prog* prog, const ebpf_batch* batch, int device);

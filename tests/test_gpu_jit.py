@@ -1,0 +1,194 @@
+"""The program compiler (csrc/jit.cpp): forward-only tier-0 programs of <= 62 micro-ops compiled
+to gfx950 code for the tile kernel, instead of interpreted.
+
+CPU (no GPU needed, the compiler and assembler run in process): every such program compiles,
+the assembler accepts it, and its code has no interpreter machinery left (no index mode, no
+dispatch jumps, no micro-op loads).
+
+GPU: the compiled kernels against the oracle and against the tile interpreter on the same batch
+(EBPF_BATCH_NO_JIT) -- every output bit-identical, counters included -- in the fixed-slot layout
+(ebpf_tile_jit_fixed), the offsets + lens layout (ebpf_tile_jit_var) and with init_regs (the
+variant whose constant-address loads stay register-based)."""
+import random
+
+import numpy as np
+import pytest
+
+from fuzzgen import gen_packet, gen_program
+
+STEPS = 20000
+
+
+def _eligible(img):
+    from ebpf_emu import Program
+
+    p = Program(img)
+    try:
+        return p, p.compile()
+    except Exception:
+        p.close()
+        raise
+
+
+def test_workloads_compile():
+    from ebpf_emu import workloads as W
+    from ebpf_emu.asm import assemble
+
+    for name, src in W.PROGRAMS.items():
+        p, ok = _eligible(assemble(src))
+        assert ok == (name != "checksum"), name  # the checksum loops: interpreted (loop mode)
+        if ok:
+            for variant in (0, 1):
+                text = p.jit_asm(variant)
+                body = text[text.index("; compiled eBPF program"):]
+                body = body[:body.index(".Ldone")]
+                for word in ("s_set_gpr_idx", "s_setpc", "s_load_dwordx16", "s_ff1"):
+                    assert word not in body, (name, word)
+        p.close()
+
+
+def test_fuzz_programs_compile():
+    """Random forward-only tier-0 programs: each compiles and assembles (a template or
+    token-expansion bug is an assembler error here, on the CPU)."""
+    rng = random.Random(31337)
+    n = 0
+    for _ in range(300):
+        img = gen_program(rng, allow_loops=False, tier0=True)
+        try:
+            p, ok = _eligible(img)
+        except Exception as e:  # decode errors: not a program
+            assert "ebpf_prog_load" in str(e) or "decode" in str(e).lower(), e
+            continue
+        if ok:
+            n += 1
+            assert p.jit_asm(0) and p.jit_asm(1)
+        p.close()
+    assert n >= 150
+
+
+# ---------------------------------------------------------------------------------------------
+def _run(img, pkts, dev, fixed_stride=None, offsets_layout=False, init_regs=None, no_jit=False,
+         mem_size=1024, r10=512):
+    import torch
+
+    from ebpf_emu import Program
+    from test_gpu_parity import _stage
+
+    prog = Program(img)
+    assert prog.compile()
+    if fixed_stride:  # no lens: every packet is `fixed_stride` bytes (the fixed-slot layout)
+        buf = np.zeros(len(pkts) * fixed_stride, dtype=np.uint8)
+        for i, p in enumerate(pkts):
+            assert len(p) == fixed_stride
+            buf[i * fixed_stride:(i + 1) * fixed_stride] = np.frombuffer(p, dtype=np.uint8)
+        frames = torch.tensor(buf, device=dev)
+        kw = dict(n=len(pkts), stride=fixed_stride)
+    else:
+        frames, kw = _stage(pkts, dev, offsets_layout=offsets_layout)
+    ir = None
+    if init_regs is not None:
+        ir = torch.tensor(np.array(init_regs, dtype=np.uint64).view(np.int64), device=dev)
+    cnt = torch.zeros(8, dtype=torch.int64, device=dev)
+    res = prog.run(frames, mem_size=mem_size, r10=r10, max_steps=STEPS, verdict=True, r0=True,
+                   status=True, regs=True, counters=cnt, init_regs=ir, no_jit=no_jit, **kw)
+    torch.cuda.synchronize()
+    out = dict(status=res.status.cpu().numpy(), r0=res.r0.cpu().numpy().view(np.uint64),
+               verdict=res.verdict.cpu().numpy(), regs=res.regs.cpu().numpy().view(np.uint64),
+               counters=cnt.cpu().numpy().view(np.uint64))
+    prog.close()
+    return out
+
+
+def _vs_oracle(oracle_mod, img, pkts, got, init_regs=None, tag=""):
+    op = oracle_mod.Program(img)
+    cnt = np.zeros(8, dtype=np.uint64)
+    for i, p in enumerate(pkts):
+        if init_regs is None:
+            st, regs, _mem, steps = op.run_full(p, 1024, 512, STEPS)
+        else:
+            st, regs, _mem, steps = op.run_full(p, 1024, 512, STEPS, init_regs=list(init_regs))
+        ctx = f"{tag} pkt {i} prog {img.hex()} pkt {p.hex()}"
+        assert got["status"][i] == st, ctx
+        if st == 0:
+            assert [int(v) for v in got["regs"][i]] == regs, ctx
+            cnt[regs[0] if regs[0] < 5 else 5] += 1
+        else:
+            cnt[6] += 1
+        cnt[7] += steps
+    assert list(got["counters"]) == list(cnt), tag
+
+
+def _same(a, b, ctx):
+    for k in ("status", "r0", "verdict", "regs", "counters"):
+        assert np.array_equal(a[k], b[k]), f"{ctx}: {k} differs"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layout", ["fixed", "offsets", "init_regs"])
+@pytest.mark.parametrize("seed", range(3))
+def test_compiled_vs_interpreter_and_oracle(cuda, oracle_mod, layout, seed):
+    rng = random.Random(5150 + 7 * seed + 1000 * ["fixed", "offsets", "init_regs"].index(layout))
+    n_run = 0
+    for it in range(40):
+        img = gen_program(rng, allow_loops=False, tier0=True)
+        try:
+            oracle_mod.Program(img)
+            p, ok = _eligible(img)
+            p.close()
+        except Exception:
+            continue
+        if not ok:
+            continue
+        kw = {}
+        ir = None
+        if layout == "fixed":
+            stride = rng.choice([64, 128])
+            pkts = [bytes(rng.getrandbits(8) for _ in range(stride))
+                    for _ in range(rng.choice([64, 100, 130]))]
+            kw = dict(fixed_stride=stride)
+        else:
+            pkts = [gen_packet(rng) for _ in range(rng.choice([64, 65, 100, 130]))]
+            kw = dict(offsets_layout=True)
+            if layout == "init_regs":
+                ir = [rng.getrandbits(64) if rng.random() < 0.5 else rng.randrange(0, 200)
+                      for _ in range(11)]
+                ir[1] = 0  # r1 = the image address, so the loads stay mostly in bounds
+                kw["init_regs"] = ir
+        got = _run(img, pkts, cuda, **kw)
+        ref = _run(img, pkts, cuda, no_jit=True, **kw)
+        _same(got, ref, f"{layout} seed {seed} it {it} prog {img.hex()}")
+        _vs_oracle(oracle_mod, img, pkts, got, init_regs=ir, tag=f"{layout} {seed} {it}")
+        n_run += 1
+    assert n_run >= 20
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("config", ["drop", "5tuple"])
+def test_workloads_compiled_vs_interpreter(cuda, oracle_mod, config):
+    """The bench workloads (BASELINE configs 1-4) on 8192 synthetic 64-byte frames, fixed-slot
+    layout: compiled == interpreted == oracle."""
+    from ebpf_emu import workloads as W
+    from ebpf_emu.asm import assemble
+
+    img = assemble(W.PROGRAMS[config])
+    frames = W.frames_fixed(8192, 64)
+    pkts = [bytes(frames[i * 64:(i + 1) * 64]) for i in range(8192)]
+    got = _run(img, pkts, cuda, fixed_stride=64)
+    ref = _run(img, pkts, cuda, fixed_stride=64, no_jit=True)
+    _same(got, ref, config)
+    sub = {k: v[:512] for k, v in got.items() if k != "counters"}
+    sub["counters"] = _cnt(oracle_mod, img, pkts[:512])
+    _vs_oracle(oracle_mod, img, pkts[:512], sub, tag=config)
+
+
+def _cnt(oracle_mod, img, pkts):
+    op = oracle_mod.Program(img)
+    cnt = np.zeros(8, dtype=np.uint64)
+    for p in pkts:
+        st, regs, _mem, steps = op.run_full(p, 1024, 512, STEPS)
+        if st == 0:
+            cnt[regs[0] if regs[0] < 5 else 5] += 1
+        else:
+            cnt[6] += 1
+        cnt[7] += steps
+    return cnt
