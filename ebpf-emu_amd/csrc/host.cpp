@@ -903,7 +903,6 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* bin, const ebpf_batch_out* ou
   a.status = out->status;
   a.counters = out->counters;
   a.shards = (uint64_t*)(ws + kWsShardsOff);
-  a.tickets = (uint32_t*)(ws + kWsTicketsOff);
   a.image_ws = ws + kWsSlotsOff;
   a.n_tiles = n_tiles;
   a.init_regs = b->init_regs;

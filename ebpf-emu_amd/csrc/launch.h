@@ -16,10 +16,9 @@ constexpr int kWinStride = kWin + 4;  // padded per-lane LDS stride: 17 dwords, 
 constexpr int kMaxLdsUops = 4096;     // programs up to this many micro-ops are staged in LDS
 constexpr int kCallDepth = 64;        // EBPF_MAX_CALL_DEPTH
 constexpr int kCounterShards = 64;    // device-atomic counter shards (spread contention)
-// workspace layout: [arrival tickets u32[64 + 1] | length-bin counts u32[16] @384 | bin cursors
+// workspace layout: [(unused) | xdp_md cursor u64 @320 | length-bin counts u32[16] @384 | bin cursors
 // u32[16] @448, 512 B][shards u64[64][8]][tier-1 wave slots, or the length-binned packet order
-// u32[n]]; tickets, bin counts/cursors and shards are zero between batches
-constexpr uint64_t kWsTicketsOff = 0;
+// u32[n]]; bin counts/cursors and shards are zero between batches
 constexpr uint64_t kWsBinCountsOff = 384;
 constexpr uint64_t kWsBinCursorOff = 448;
 constexpr int kBinClasses = 16;  // packets are binned by ceil(len / 128), capped
@@ -51,13 +50,13 @@ struct LaunchArgs {
   uint8_t* status;
   uint64_t* counters;   // optional caller counters [8] (added to)
   uint64_t* shards;     // workspace: [kCounterShards][8] partial counters (left zeroed)
-  uint32_t* tickets;    // workspace: [kCounterShards] per-shard arrivals + [1] shard arrivals
   uint8_t* image_ws;    // tier 1: per-wave-slot images + call stacks
   uint64_t n_tiles;     // ceil(n / 64)
   const uint64_t* init_regs;  // optional [11] initial registers (else main.rs layout)
   uint8_t* mem_out;           // optional [n][mem_size] final images
   uint64_t* regs_out;         // optional [n][11] final registers
-  uint32_t fold_kernel;       // 1: shards are folded by fold_counters after the launch (A/B)
+  uint32_t fold_kernel;       // 1: shards are folded by fold_counters after the launch, 0:
+                              //    in-kernel (counted shard words, flush_counters)
   const uint32_t* perm;       // loop mode: packet index of tile slot i (length-binned), else null
   uint32_t* bin_counts;       // with perm: bin counts + cursors, zeroed again by the tile kernel
   uint32_t tile_prefetch;     // fixed-slot tile kernel: prefetch each wave's next tile (A/B)
