@@ -841,6 +841,39 @@ v_cndmask_b32 {{RH}}, {{t3}}, {{t11}}, vcc
 
 TAILS = {"c": CHAIN, "e": END_N, "j": ""}
 
+def fixed_dma(winb):
+    """FIXED layout: DMA the header windows of tile T0 / 64 (T0 = tile << 6) into the LDS window
+    buffer at `winb` (as dma_window_stride in interp.hip): round r moves packets 16r..16r+15, lane
+    l filling chunk slot (l & 3) of packet 16r + l/4 from logical chunk (l & 3) ^ ((l >> 4) & 3);
+    lanes past the batch read the micro-op table instead. Four global_load_lds_dwordx4 in flight
+    afterwards; t0 (the lane) is kept."""
+    return """v_lshrrev_b32 {t4}, 2, {t0}
+v_mov_b32 {t5}, 0
+v_lshl_add_u64 {T45}, {T45}, 0, {T0}
+v_and_b32 {t6}, 3, {t0}
+v_bfe_u32 {t7}, {t0}, 4, 2
+v_xor_b32 {t6}, {t6}, {t7}
+v_lshlrev_b32 {t6}, 4, {t6}
+v_mov_b32 {t7}, 0
+v_mov_b32 {t10}, {KSTL}
+v_mad_u64_u32 {T89}, {T4}, {t4}, {t10}, {KFR}
+v_mul_lo_u32 {t11}, {t5}, {KSTL}
+v_mul_lo_u32 {t12}, {t4}, {KSTH}
+v_add3_u32 {t9}, {t9}, {t11}, {t12}
+v_lshl_add_u64 {T89}, {T89}, 0, {T67}
+s_lshl_b64 {T1}, {KST}, 4
+v_mov_b32 {t10}, {PROGL}
+v_mov_b32 {t11}, {PROGH}
+""" + "\n".join(f"""v_cmp_gt_u64 vcc, {{KN}}, {{T45}}
+v_cndmask_b32 {{t12}}, {{t10}}, {{t8}}, vcc
+v_cndmask_b32 {{t13}}, {{t11}}, {{t9}}, vcc
+s_add_u32 m0, {winb}, {1024 * r}
+s_nop 0
+global_load_lds_dwordx4 {{T1213}}, off
+v_lshl_add_u64 {{T45}}, {{T45}}, 0, 16
+v_lshl_add_u64 {{T89}}, {{T89}}, 0, {{T1}}""" for r in range(4))
+
+
 # ---- prologue / epilogue ----
 # %[ka]: the kernel-argument segment (LaunchArgs at offset 0; LA_* offsets are "i" operands);
 # %[tile]: the tile index (64-bit SGPR pair); %[winb]: this wave's window region (LDS byte
@@ -869,59 +902,27 @@ ds_read_b32 {t7}, {t5} offset:256
 .endif
 s_waitcnt lgkmcnt(0)
 .if %[fixed]
-; the tile's header windows HBM -> LDS (as dma_window_stride in interp.hip): round r moves
-; packets 16r..16r+15, lane l filling chunk slot (l & 3) of packet 16r + l/4 from logical
-; chunk (l & 3) ^ ((l >> 4) & 3); lanes past the batch read the micro-op table instead
-v_lshrrev_b32 {t4}, 2, {t0}
-v_mov_b32 {t5}, 0
-v_lshl_add_u64 {T45}, {T45}, 0, {T0}
-v_and_b32 {t6}, 3, {t0}
-v_bfe_u32 {t7}, {t0}, 4, 2
-v_xor_b32 {t6}, {t6}, {t7}
-v_lshlrev_b32 {t6}, 4, {t6}
-v_mov_b32 {t7}, 0
-v_mov_b32 {t10}, {KSTL}
-v_mad_u64_u32 {T89}, {T4}, {t4}, {t10}, {KFR}
-v_mul_lo_u32 {t11}, {t5}, {KSTL}
-v_mul_lo_u32 {t12}, {t4}, {KSTH}
-v_add3_u32 {t9}, {t9}, {t11}, {t12}
-v_lshl_add_u64 {T89}, {T89}, 0, {T67}
-s_lshl_b64 {T1}, {KST}, 4
-v_mov_b32 {t10}, {PROGL}
-v_mov_b32 {t11}, {PROGH}
-""" + "\n".join(f"""v_cmp_gt_u64 vcc, {{KN}}, {{T45}}
-v_cndmask_b32 {{t12}}, {{t10}}, {{t8}}, vcc
-v_cndmask_b32 {{t13}}, {{t11}}, {{t9}}, vcc
-s_add_u32 m0, %[winb], {1024 * r}
-s_nop 0
-global_load_lds_dwordx4 {{T1213}}, off
-v_lshl_add_u64 {{T45}}, {{T45}}, 0, 16
-v_lshl_add_u64 {{T89}}, {{T89}}, 0, {{T1}}""" for r in range(4)) + """
-; prefetch the wave's next tile (%[ntile]; %[pf] = 0: none) into L2 / the Infinity Cache while
-; this one is interpreted: one dword of every packet, landing in the 512 B of LDS metadata the
-; FIXED layout does not use; the windows wait for all but this youngest load
+.if %[db]
+; double-buffered windows (the compiled fixed-slot kernel): the wave's next tile (%[ntile], if
+; %[pf]) is DMA'd into the other buffer (%[nwinb]) before this one is processed, so every wave
+; keeps a window in flight; the first tile of the wave is DMA'd here too (%[first])
+s_cmp_eq_u32 %[first], 0
+s_cbranch_scc1 .Lnofirst%=
+""" + fixed_dma("%[winb]") + """
+.Lnofirst%=:
 s_cmp_eq_u32 %[pf], 0
-s_cbranch_scc1 .Lnopf%=
-v_mov_b32 {t4}, {t0}
-v_mov_b32 {t5}, 0
-s_lshl_b64 {T1}, %[ntile], 6
-v_lshl_add_u64 {T45}, {T45}, 0, {T1}
-v_cmp_gt_u64 vcc, {KN}, {T45}
-v_mov_b32 {t12}, {KSTL}
-v_mad_u64_u32 {T89}, {T4}, {t4}, {t12}, {KFR}
-v_mul_lo_u32 {t12}, {t5}, {KSTL}
-v_mul_lo_u32 {t13}, {t4}, {KSTH}
-v_add3_u32 {t9}, {t9}, {t12}, {t13}
-v_cndmask_b32 {t12}, {t10}, {t8}, vcc
-v_cndmask_b32 {t13}, {t11}, {t9}, vcc
-s_mov_b32 m0, %[metab]
-s_nop 0
-global_load_lds_dword {T1213}, off
-s_waitcnt vmcnt(1)
-s_branch .Lpfd%=
-.Lnopf%=:
+s_cbranch_scc1 .Lnonext%=
+s_lshl_b64 {T0}, %[ntile], 6
+""" + fixed_dma("%[nwinb]") + """
+s_waitcnt vmcnt(4)
+s_branch .Ldmad%=
+.Lnonext%=:
 s_waitcnt vmcnt(0)
-.Lpfd%=:
+.Ldmad%=:
+.else
+""" + fixed_dma("%[winb]") + """
+s_waitcnt vmcnt(0)
+.endif
 .endif
 v_cmp_gt_u64 vcc, {KN}, {T23}
 s_and_b64 {VM}, vcc, exec

@@ -1257,7 +1257,8 @@ constexpr uint32_t kTileWaveLds = kWinBytes + kDagMetaBytes;  // window + metada
         : [bkt] "=&v"(bkt), [nst] "=&v"(nst) \
         : [ka] "s"(ka), [tile] "s"(t), [winb] "s"(winb), [metab] "s"(metab), \
           [fixed] "i"(FIXED ? 1 : 0), [loops] "i"(LOOPS ? 1 : 0), [aligned] "s"(rfl(aligned)), \
-          [pf] "s"(rfl(pf)), [ntile] "s"(nt), \
+          [pf] "s"(rfl(pf)), [ntile] "s"(nt), [db] "i"(DB ? 1 : 0), [first] "s"(first), \
+          [nwinb] "s"(nwinb), \
           [o_tprog] "i"(offsetof(LaunchArgs, tprog)), \
           [o_tprog_exact] "i"(offsetof(LaunchArgs, tprog_exact)), \
           [o_maxs] "i"(offsetof(LaunchArgs, max_steps)), [o_perm] "i"(offsetof(LaunchArgs, perm)), \
@@ -1271,7 +1272,11 @@ constexpr uint32_t kTileWaveLds = kWinBytes + kDagMetaBytes;  // window + metada
 
 // JIT: the statement of the compiled-program template kernels (tile_jit.inc; jit.cpp fills in the
 // program's code at load time).
-template <bool FIXED, bool LOOPS, bool JIT>
+// DB (the compiled fixed-slot kernel): two window buffers per wave, the next tile's DMA in flight
+// while the current one runs (kTileWaveLdsDb of LDS per wave).
+constexpr uint32_t kTileWaveLdsDb = 2 * kWinBytes;
+
+template <bool FIXED, bool LOOPS, bool JIT, bool DB = JIT && FIXED && !LOOPS>
 __device__ __forceinline__ void tile_body(LaunchArgs& a) {
   counters_init();
   // the length bins of this batch were consumed by bin_scatter (earlier on the stream): re-zero
@@ -1280,11 +1285,12 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t wv = rfl(threadIdx.x / kWave);  // wave-uniform: keeps LDS addresses scalar
   WaveLds L;
-  L.win = smem + wv * kTileWaveLds;
-  L.meta_off = (uint32_t*)(L.win + kWinBytes);
+  L.win = smem + wv * (DB ? kTileWaveLdsDb : kTileWaveLds);
+  L.meta_off = (uint32_t*)(L.win + kWinBytes);  // (not used in DB mode)
   L.meta_len = L.meta_off + kWave;
-  const uint32_t winb = lds_addr(L.win);
+  const uint32_t win0 = lds_addr(L.win);
   const uint32_t metab = lds_addr(L.meta_off);
+  uint32_t buf = 0, first = 1;
   const uint64_t wave_slot = (uint64_t)blockIdx.x * kWavesPerBlock + wv;
   const uint64_t total_waves = (uint64_t)gridDim.x * kWavesPerBlock;
   const auto ka = __builtin_amdgcn_kernarg_segment_ptr();
@@ -1330,8 +1336,10 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
       __builtin_amdgcn_s_waitcnt(0xc07f);  // the window's LDS writes / metadata reads: done
     }
     const uint64_t t = rfl64(tile);
-    const uint64_t nt = t + total_waves;  // this wave's next tile (prefetched in FIXED mode)
-    const uint32_t pf = a.tile_prefetch && nt < a.n_tiles ? 1u : 0u;
+    const uint64_t nt = t + total_waves;  // this wave's next tile (DMA'd now in DB mode)
+    const uint32_t pf = nt < a.n_tiles ? 1u : 0u;
+    const uint32_t winb = DB ? win0 + buf * kWinBytes : win0;
+    const uint32_t nwinb = DB ? win0 + (buf ^ 1u) * kWinBytes : win0;
     uint32_t bkt, nst;
     if constexpr (JIT) {
       asm volatile(
@@ -1371,6 +1379,8 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
 #pragma unroll
     for (int b = 0; b < 7; b++) cnt[b] += __builtin_popcountll(ballot(bkt == (uint32_t)b));
     retired += nst;
+    buf ^= 1u;
+    first = 0;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // a next-tile prefetch may be in flight
   uint64_t cnt64[7];
@@ -1429,14 +1439,6 @@ static bool g_fixed = [] {
 static bool g_db = [] {  // tier-0 window double-buffering (EBPFEMU_TIER0_DB=0|1 for A/B runs)
   const char* e = getenv("EBPFEMU_TIER0_DB");
   return e ? e[0] == '1' : false;
-}();
-
-// A/B switch: EBPFEMU_TILE_PREFETCH=1 makes the fixed-slot tile kernel prefetch each wave's next
-// tile while it interprets the current one. Off: it doubles the launch's opening HBM burst
-// (5-tuple, 1 Mi packets: 29.9 us with, 28.2 us without).
-static bool g_tile_prefetch = [] {
-  const char* e = getenv("EBPFEMU_TILE_PREFETCH");
-  return e && e[0] == '1';
 }();
 
 // A/B switch: EBPFEMU_NO_TILE=1 runs forward-only programs on dag_kernel instead of tile_kernel.
@@ -1547,11 +1549,41 @@ int interp_grid(int kind, uint32_t n_uops, bool tiny, uint64_t n_tiles, int* gri
   return 0;
 }
 
+// Balanced persistent grid of a compiled kernel (its own occupancy: the DB kernel holds two
+// window buffers per wave).
+static int jit_grid(hipFunction_t f, uint32_t lds, uint64_t n_tiles) {
+  static std::mutex mu;
+  static std::map<std::tuple<int, hipFunction_t, uint32_t>, std::pair<int, int>> cache;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::pair<int, int> occ;  // (CUs, workgroups per CU)
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    auto key = std::make_tuple(dev, f, lds);
+    auto it = cache.find(key);
+    if (it != cache.end()) {
+      occ = it->second;
+    } else {
+      int cus = 256, per_cu = 1;
+      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, kBlock, lds) !=
+              hipSuccess ||
+          per_cu < 1)
+        per_cu = 1;
+      occ = cache[key] = {cus, per_cu};
+    }
+  }
+  const uint64_t resident = (uint64_t)occ.first * occ.second * kWavesPerBlock;
+  const uint64_t tiles = n_tiles ? n_tiles : 1;
+  const uint64_t per_wave = (tiles + resident - 1) / resident;
+  const uint64_t waves = (tiles + per_wave - 1) / per_wave;
+  return (int)((waves + kWavesPerBlock - 1) / kWavesPerBlock);
+}
+
 hipError_t launch_interp(int kind, const LaunchArgs& a, int grid, hipStream_t stream,
                          const JitFns* jit) {
   const uint32_t lds = lds_bytes_for(kind, a.n_uops);
   LaunchArgs b = a;
-  b.tile_prefetch = g_tile_prefetch ? 1u : 0u;
   // a shard word's sum must stay below 2^48: bound it by packets x steps per packet
   const uint64_t steps = kind == kKindDag ? (uint64_t)a.n_uops : a.max_steps;
   const bool fits = a.n < (1ull << 40) && steps < (1ull << 47) / (a.n + 1);
@@ -1559,10 +1591,15 @@ hipError_t launch_interp(int kind, const LaunchArgs& a, int grid, hipStream_t st
   b.fold_kernel = fold_kernel ? 1u : 0u;
   void* bargs[] = {(void*)&b};
   hipError_t e;
-  if (jit && kind == kKindDag && tile_kernel_for(kind, a.n_uops))  // the compiled program
-    e = hipModuleLaunchKernel(fixed_layout(&a) ? jit->fixed : jit->var, grid, 1, 1, kBlock, 1, 1,
-                              lds, stream, bargs, nullptr);
-  else
+  if (jit && kind == kKindDag && tile_kernel_for(kind, a.n_uops)) {  // the compiled program
+    if (fixed_layout(&a)) {  // double-buffered windows: its own LDS size and grid
+      const uint32_t dlds = g_lds_pad + kWavesPerBlock * kTileWaveLdsDb;
+      e = hipModuleLaunchKernel(jit->fixed, jit_grid(jit->fixed, dlds, a.n_tiles), 1, 1, kBlock,
+                                1, 1, dlds, stream, bargs, nullptr);
+    } else {
+      e = hipModuleLaunchKernel(jit->var, grid, 1, 1, kBlock, 1, 1, lds, stream, bargs, nullptr);
+    }
+  } else
     e = hipLaunchKernel(kernel_for(kind, a.n_uops, &a), dim3(grid), dim3(kBlock), bargs, lds,
                         stream);
   if (e != hipSuccess || a.counters == nullptr || !fold_kernel) return e;

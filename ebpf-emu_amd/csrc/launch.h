@@ -59,7 +59,6 @@ struct LaunchArgs {
                               //    in-kernel (counted shard words, flush_counters)
   const uint32_t* perm;       // loop mode: packet index of tile slot i (length-binned), else null
   uint32_t* bin_counts;       // with perm: bin counts + cursors, zeroed again by the tile kernel
-  uint32_t tile_prefetch;     // fixed-slot tile kernel: prefetch each wave's next tile (A/B)
 };
 
 // Bytes of tier-1 scratch per wave slot: lane-interleaved image dwords + call stack.

@@ -1,2 +1,3 @@
 B="python bench.py --cpu-seconds 0 --steps 100"
-bash tools/gpu_session.sh "tests|400|python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread" "b5|120|$B" "b5k|120|EBPFEMU_FOLD=kernel $B" "bd|120|$B --config drop" "bdk|120|EBPFEMU_FOLD=kernel $B --config drop" "bc|200|python bench.py --cpu-seconds 0 --steps 20 --warmup 3 --config checksum" "bck|200|EBPFEMU_FOLD=kernel python bench.py --cpu-seconds 0 --steps 20 --warmup 3 --config checksum" "b5_8m|120|$B --packets 8388608" "bd_8m|120|$B --packets 8388608 --config drop"
+T="python -u -m pytest -x -q --timeout 120 --timeout-method thread"
+bash tools/gpu_session.sh "jit|300|$T tests/test_gpu_jit.py -m gpu" "b5|120|$B" "bd|120|$B --config drop" "b5_8m|120|$B --packets 8388608" "bd_8m|120|$B --packets 8388608 --config drop" "b5n|120|EBPFEMU_NO_JIT=1 $B"
