@@ -67,12 +67,14 @@ M = {
     # prologue / epilogue scratch inside the micro-op registers
     "KFR": u(0, 2), "KST": u(2, 2), "KSTL": u(2), "KSTH": u(3), "KN": u(4, 2),
     "KOFF": u(6, 2), "KLEN": u(8, 2), "KINIT": u(10, 2), "KR10": u(12, 2),
-    "KR10L": u(12), "KR10H": u(13),
+    "KR10L": u(12), "KR10H": u(13), "KFRL": u(0), "KFRH": u(1), "KNL": u(4), "KNH": u(5),
     "EV": u(0, 2), "ER0": u(2, 2), "EST": u(4, 2), "ERG": u(6, 2),
     "KMEM": "s33", "T3": "s34", "CNT": "s34", "M0S": "s35",
     "LIVE": "s[52:53]", "PROG": "s[54:55]", "PROGL": "s54", "PROGH": "s55",
     "SLOTB": "s[56:57]", "SLOTBL": "s56", "SLOTBH": "s57", "VM": "s[58:59]",
     "T0": "s[60:61]", "T1": "s[62:63]", "T4": "s[64:65]", "T5": "s[66:67]", "T7": "s[68:69]",
+    "T0L": "s60", "T0H": "s61", "T1L": "s62", "T1H": "s63", "T5L": "s66", "T5H": "s67",
+    "T7L": "s68", "T7H": "s69",
     "PCOFF": "s70",
     # loop mode: the step budget (max_steps, clamped to 32 bits)
     "MAXS": "s71",
@@ -874,10 +876,65 @@ v_lshl_add_u64 {{T45}}, {{T45}}, 0, 16
 v_lshl_add_u64 {{T89}}, {{T89}}, 0, {{T1}}""" for r in range(4))
 
 
+def fixed_dma_db(winb, tag):
+    """As fixed_dma, for the double-buffered compiled kernel: a whole tile (the scalar check
+    (T0 + 64 <= n), every tile but a batch's last) takes per-lane offsets from %[dmaoff] (lane l:
+    (l/4) * stride + its swizzled chunk * 16, computed once per wave) and a scalar tile base --
+    one VALU per round instead of five; a partial tile takes fixed_dma's per-lane checks."""
+    return f"""s_add_u32 {{T5L}}, {{T0L}}, 64
+s_addc_u32 {{T5H}}, {{T0H}}, 0
+s_sub_u32 {{T5L}}, {{KNL}}, {{T5L}}
+s_subb_u32 {{T5H}}, {{KNH}}, {{T5H}}
+s_cbranch_scc1 .Lpart{tag}%=
+s_mul_i32 {{T7L}}, {{T0L}}, {{KSTL}}
+s_mul_hi_u32 {{T7H}}, {{T0L}}, {{KSTL}}
+s_mul_i32 {{T5L}}, {{T0L}}, {{KSTH}}
+s_add_u32 {{T7H}}, {{T7H}}, {{T5L}}
+s_mul_i32 {{T5L}}, {{T0H}}, {{KSTL}}
+s_add_u32 {{T7H}}, {{T7H}}, {{T5L}}
+s_add_u32 {{T7L}}, {{T7L}}, {{KFRL}}
+s_addc_u32 {{T7H}}, {{T7H}}, {{KFRH}}
+s_lshl_b64 {{T1}}, {{KST}}, 4
+""" + "\n".join(f"""v_lshl_add_u64 {{T1213}}, %[dmaoff], 0, {{T7}}
+s_add_u32 m0, {winb}, {1024 * r}
+s_nop 0
+global_load_lds_dwordx4 {{T1213}}, off ; @DMAPOLICY@
+s_add_u32 {{T7L}}, {{T7L}}, {{T1L}}
+s_addc_u32 {{T7H}}, {{T7H}}, {{T1H}}""" for r in range(4)) + f"""
+s_branch .Ldmaok{tag}%=
+.Lpart{tag}%=:
+""" + fixed_dma(winb) + f"""
+.Ldmaok{tag}%=:"""
+
+
 # ---- prologue / epilogue ----
 # %[ka]: the kernel-argument segment (LaunchArgs at offset 0; LA_* offsets are "i" operands);
 # %[tile]: the tile index (64-bit SGPR pair); %[winb]: this wave's window region (LDS byte
 # address); %[metab]: this wave's metadata region (offsets u32[64], lengths u32[64]).
+FIXED_DMA = """.if %[fixed]
+""" + fixed_dma("%[winb]") + """
+s_waitcnt vmcnt(0)
+.endif
+"""
+FIXED_DMA_DB = """.if %[fixed]
+; double-buffered windows (the compiled fixed-slot kernel): the wave's next tile (%[ntile], if
+; %[pf]) is DMA'd into the other buffer (%[nwinb]) before this one is processed, so every wave
+; keeps a window in flight; the first tile of the wave is DMA'd here too (%[first])
+s_cmp_eq_u32 %[first], 0
+s_cbranch_scc1 .Lnofirst%=
+""" + fixed_dma_db("%[winb]", "c") + """
+.Lnofirst%=:
+s_cmp_eq_u32 %[pf], 0
+s_cbranch_scc1 .Lnonext%=
+s_lshl_b64 {T0}, %[ntile], 6
+""" + fixed_dma_db("%[nwinb]", "n") + """
+s_waitcnt vmcnt(4)
+s_branch .Ldmad%=
+.Lnonext%=:
+s_waitcnt vmcnt(0)
+.Ldmad%=:
+.endif
+"""
 PROLOGUE = """s_mov_b32 {M0S}, m0
 s_mov_b64 {LIVE}, 0
 s_load_dwordx2 {PROG}, %[ka], %[o_tprog]
@@ -901,30 +958,7 @@ ds_read_b32 {t6}, {t5}
 ds_read_b32 {t7}, {t5} offset:256
 .endif
 s_waitcnt lgkmcnt(0)
-.if %[fixed]
-.if %[db]
-; double-buffered windows (the compiled fixed-slot kernel): the wave's next tile (%[ntile], if
-; %[pf]) is DMA'd into the other buffer (%[nwinb]) before this one is processed, so every wave
-; keeps a window in flight; the first tile of the wave is DMA'd here too (%[first])
-s_cmp_eq_u32 %[first], 0
-s_cbranch_scc1 .Lnofirst%=
-""" + fixed_dma("%[winb]") + """
-.Lnofirst%=:
-s_cmp_eq_u32 %[pf], 0
-s_cbranch_scc1 .Lnonext%=
-s_lshl_b64 {T0}, %[ntile], 6
-""" + fixed_dma("%[nwinb]") + """
-s_waitcnt vmcnt(4)
-s_branch .Ldmad%=
-.Lnonext%=:
-s_waitcnt vmcnt(0)
-.Ldmad%=:
-.else
-""" + fixed_dma("%[winb]") + """
-s_waitcnt vmcnt(0)
-.endif
-.endif
-v_cmp_gt_u64 vcc, {KN}, {T23}
+""" + FIXED_DMA + """v_cmp_gt_u64 vcc, {KN}, {T23}
 s_and_b64 {VM}, vcc, exec
 s_cmp_gt_u32 {KSTH}, 0
 s_cselect_b32 {T3}, -1, {KSTL}
@@ -1194,7 +1228,7 @@ def cstr(text):
 
 # The template kernel's statement: the prologue, a marker the compiler fills in at load time, the
 # epilogue. The marker line carries the statement's label number and operand registers.
-JIT_STATEMENT = PROLOGUE + """
+JIT_STATEMENT = PROLOGUE.replace(FIXED_DMA, FIXED_DMA_DB) + """
 ; JIT N=%= fixed=%[fixed] loops=%[loops] aligned=%[aligned]
 ;@@JIT@@
 """ + EPILOGUE

@@ -1253,9 +1253,9 @@ hipError_t launch_xdp_stage(const uint8_t* frames, const uint32_t* offsets, cons
 constexpr uint32_t kTileWaveLds = kWinBytes + kDagMetaBytes;  // window + metadata, 4.5 KiB
 
 
-#define TILE_ASM_OPERANDS \
-        : [bkt] "=&v"(bkt), [nst] "=&v"(nst) \
-        : [ka] "s"(ka), [tile] "s"(t), [winb] "s"(winb), [metab] "s"(metab), \
+#define TILE_ASM_OUT [bkt] "=&v"(bkt), [nst] "=&v"(nst)
+#define TILE_ASM_IN \
+          [ka] "s"(ka), [tile] "s"(t), [winb] "s"(winb), [metab] "s"(metab), \
           [fixed] "i"(FIXED ? 1 : 0), [loops] "i"(LOOPS ? 1 : 0), [aligned] "s"(rfl(aligned)), \
           [pf] "s"(rfl(pf)), [ntile] "s"(nt), [db] "i"(DB ? 1 : 0), [first] "s"(first), \
           [nwinb] "s"(nwinb), \
@@ -1267,8 +1267,10 @@ constexpr uint32_t kTileWaveLds = kWinBytes + kDagMetaBytes;  // window + metada
           [o_offsets] "i"(offsetof(LaunchArgs, offsets)), [o_lens] "i"(offsetof(LaunchArgs, lens)), \
           [o_init] "i"(offsetof(LaunchArgs, init_regs)), [o_r10] "i"(offsetof(LaunchArgs, r10)), \
           [o_verdict] "i"(offsetof(LaunchArgs, verdict)), [o_r0] "i"(offsetof(LaunchArgs, r0)), \
-          [o_status] "i"(offsetof(LaunchArgs, status)), [o_regs] "i"(offsetof(LaunchArgs, regs_out)) \
-        : "s33", "s34", "s35", "s36", "s37", "s38", "s39", "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53", "s54", "s55", "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71", "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15", "v16", "v17", "v18", "v19", "v20", "v21", "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32", "v33", "v34", "v35", "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", "vcc", "scc", "memory"
+          [o_status] "i"(offsetof(LaunchArgs, status)), [o_regs] "i"(offsetof(LaunchArgs, regs_out))
+#define TILE_ASM_CLOBBER "s33", "s34", "s35", "s36", "s37", "s38", "s39", "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53", "s54", "s55", "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71", "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15", "v16", "v17", "v18", "v19", "v20", "v21", "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32", "v33", "v34", "v35", "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", "vcc", "scc", "memory"
+#define TILE_ASM_OPERANDS : TILE_ASM_OUT : TILE_ASM_IN : TILE_ASM_CLOBBER
+
 
 // JIT: the statement of the compiled-program template kernels (tile_jit.inc; jit.cpp fills in the
 // program's code at load time).
@@ -1291,6 +1293,14 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
   const uint32_t win0 = lds_addr(L.win);
   const uint32_t metab = lds_addr(L.meta_off);
   uint32_t buf = 0, first = 1;
+  // DB: lane l's window-DMA source offset within a tile, (l/4) * stride + its swizzled 16-byte
+  // chunk (fixed_dma_db in gen_tile.py); a loop-invariant VGPR pair
+  uint64_t dmaoff = 0;
+  if (DB) {
+    uint32_t lane;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+    dmaoff = (uint64_t)(lane >> 2) * a.stride + (uint64_t)(((lane & 3u) ^ ((lane >> 4) & 3u)) * 16u);
+  }
   const uint64_t wave_slot = (uint64_t)blockIdx.x * kWavesPerBlock + wv;
   const uint64_t total_waves = (uint64_t)gridDim.x * kWavesPerBlock;
   const auto ka = __builtin_amdgcn_kernarg_segment_ptr();
@@ -1344,7 +1354,9 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
     if constexpr (JIT) {
       asm volatile(
 #include "tile_jit.inc"
-          TILE_ASM_OPERANDS);
+          : TILE_ASM_OUT
+          : TILE_ASM_IN, [dmaoff] "v"(dmaoff)
+          : TILE_ASM_CLOBBER);
     } else {
       asm volatile(
 #include "tile.inc"
@@ -1399,7 +1411,8 @@ __global__ __launch_bounds__(kBlock, 8) void tile_kernel(LaunchArgs a) {
 #else
 // The JIT template kernels (build/tile_jit.s, embedded in the library): jit.cpp inserts each
 // program's compiled code at the marker of their statement and assembles the result.
-extern "C" __global__ __launch_bounds__(kBlock, 8) void ebpf_tile_jit_fixed(LaunchArgs a) {
+// (4 workgroups per CU: its two window buffers per wave take the LDS, so 128 VGPRs are free)
+extern "C" __global__ __launch_bounds__(kBlock, 4) void ebpf_tile_jit_fixed(LaunchArgs a) {
   tile_body<true, false, true>(a);
 }
 extern "C" __global__ __launch_bounds__(kBlock, 8) void ebpf_tile_jit_var(LaunchArgs a) {
