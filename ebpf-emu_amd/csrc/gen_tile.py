@@ -911,6 +911,23 @@ s_branch .Ldmaok{tag}%=
 # %[ka]: the kernel-argument segment (LaunchArgs at offset 0; LA_* offsets are "i" operands);
 # %[tile]: the tile index (64-bit SGPR pair); %[winb]: this wave's window region (LDS byte
 # address); %[metab]: this wave's metadata region (offsets u32[64], lengths u32[64]).
+# the main.rs:28-31 register layout (r1 = 0, r2 = len, r10 = the batch's r10, the rest 0)
+DEFAULT_INIT = "\n".join(f"v_mov_b64 v[{i}:{i + 1}], 0" for i in range(0, 20, 2) if i != 4) + """
+v_mov_b32 v4, {LEN}
+v_mov_b32 v5, 0
+v_mov_b32 v20, {KR10L}
+v_mov_b32 v21, {KR10H}
+"""
+# compiled programs: only the registers the program may read before writing them, and r0 (the
+# compiler fills in ;@@JITINIT@@) -- all of them when the batch asks for the final registers
+JIT_INIT = """s_load_dwordx2 {T5}, %[ka], %[o_regs]
+s_waitcnt lgkmcnt(0)
+s_cmp_lg_u64 {T5}, 0
+s_cbranch_scc1 .Lallinit%=
+;@@JITINIT@@
+s_branch .Linitd%=
+.Lallinit%=:
+""" + DEFAULT_INIT
 FIXED_DMA = """.if %[fixed]
 """ + fixed_dma("%[winb]") + """
 s_waitcnt vmcnt(0)
@@ -1014,12 +1031,7 @@ s_load_dwordx2 {KR10}, %[ka], %[o_r10]
 s_waitcnt lgkmcnt(0)
 s_cmp_lg_u64 {KINIT}, 0
 s_cbranch_scc1 .Linitc%=
-""" + "\n".join(f"v_mov_b64 v[{i}:{i + 1}], 0" for i in range(0, 20, 2) if i != 4) + """
-v_mov_b32 v4, {LEN}
-v_mov_b32 v5, 0
-v_mov_b32 v20, {KR10L}
-v_mov_b32 v21, {KR10H}
-s_branch .Linitd%=
+""" + DEFAULT_INIT + """s_branch .Linitd%=
 .Linitc%=:
 s_mov_b64 {T5}, {KINIT}
 s_load_dwordx16 {UOP}, {T5}, 0x0
@@ -1228,7 +1240,7 @@ def cstr(text):
 
 # The template kernel's statement: the prologue, a marker the compiler fills in at load time, the
 # epilogue. The marker line carries the statement's label number and operand registers.
-JIT_STATEMENT = PROLOGUE.replace(FIXED_DMA, FIXED_DMA_DB) + """
+JIT_STATEMENT = PROLOGUE.replace(FIXED_DMA, FIXED_DMA_DB).replace(DEFAULT_INIT, JIT_INIT) + """
 ; JIT N=%= fixed=%[fixed] loops=%[loops] aligned=%[aligned]
 ;@@JIT@@
 """ + EPILOGUE
@@ -1318,7 +1330,20 @@ def main():
     for idx, (name, base, sfx) in enumerate(table):
         main_t, ool_t = jit_template(base)
         out.append(f"// {name}\n{{{cstr(main_t)},\n{cstr(ool_t)}}},")
-    out += ["};", "// clang-format on"]
+    out += ["};"]
+    # per-register initialisation of the main.rs layout (the compiler's ;@@JITINIT@@)
+    inits = []
+    for r in range(11):
+        if r == 2:
+            t = "v_mov_b32 v4, {LEN}\nv_mov_b32 v5, 0"
+        elif r == 10:
+            t = "v_mov_b32 v20, {KR10L}\nv_mov_b32 v21, {KR10H}"
+        else:
+            t = f"v_mov_b64 v[{2 * r}:{2 * r + 1}], 0"
+        inits.append(cstr(F(t)))
+    assert F("\n".join(DEFAULT_INIT.split("\n"))) == F(DEFAULT_INIT)
+    out += ["static const char* const kJitInitReg[11] = {" + ",\n".join(inits) + "};",
+            "// clang-format on"]
     with open(os.path.join(HERE, "jit_tmpl.h"), "w") as f:
         f.write("\n".join(out) + "\n")
 

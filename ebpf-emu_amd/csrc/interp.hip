@@ -1270,6 +1270,9 @@ constexpr uint32_t kTileWaveLds = kWinBytes + kDagMetaBytes;  // window + metada
           [o_status] "i"(offsetof(LaunchArgs, status)), [o_regs] "i"(offsetof(LaunchArgs, regs_out))
 #define TILE_ASM_CLOBBER "s33", "s34", "s35", "s36", "s37", "s38", "s39", "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53", "s54", "s55", "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71", "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15", "v16", "v17", "v18", "v19", "v20", "v21", "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32", "v33", "v34", "v35", "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", "vcc", "scc", "memory"
 #define TILE_ASM_OPERANDS : TILE_ASM_OUT : TILE_ASM_IN : TILE_ASM_CLOBBER
+// the compiled programs' preloaded window dwords (jit.cpp ldxk_fast): v[64:79]
+#define TILE_ASM_CLOBBER_WINDOW "v64", "v65", "v66", "v67", "v68", "v69", "v70", "v71", "v72", \
+    "v73", "v74", "v75", "v76", "v77", "v78", "v79"
 
 
 // JIT: the statement of the compiled-program template kernels (tile_jit.inc; jit.cpp fills in the
@@ -1351,7 +1354,13 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
     const uint32_t winb = DB ? win0 + buf * kWinBytes : win0;
     const uint32_t nwinb = DB ? win0 + (buf ^ 1u) * kWinBytes : win0;
     uint32_t bkt, nst;
-    if constexpr (JIT) {
+    if constexpr (JIT && DB) {
+      asm volatile(
+#include "tile_jit.inc"
+          : TILE_ASM_OUT
+          : TILE_ASM_IN, [dmaoff] "v"(dmaoff)
+          : TILE_ASM_CLOBBER, TILE_ASM_CLOBBER_WINDOW);
+    } else if constexpr (JIT) {
       asm volatile(
 #include "tile_jit.inc"
           : TILE_ASM_OUT

@@ -23,6 +23,7 @@
 
 #include <amd_comgr/amd_comgr.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -43,6 +44,7 @@ constexpr uint32_t kFieldSgpr = 36;  // TUop dword d lives in s[36 + d] (gen_til
 
 struct Marker {
   size_t begin = 0, end = 0;  // the marker line ";@@JIT@@" (replaced)
+  size_t init_begin = 0, init_end = 0;  // ";@@JITINIT@@" of the same statement (replaced)
   std::string n;              // the statement's %= number
   std::string fixed = "0";
   std::string aligned;
@@ -79,6 +81,10 @@ bool find_markers(const std::string& s, std::vector<Marker>& out) {
     m.aligned = field("aligned=");
     const size_t mk = s.find(";@@JIT@@", eol);
     if (mk == std::string::npos || m.n.empty()) return false;
+    const size_t ik = s.rfind(";@@JITINIT@@", pos);
+    if (ik == std::string::npos || (!out.empty() && ik < out.back().end)) return false;
+    m.init_begin = ik;
+    m.init_end = s.find('\n', ik);
     m.begin = mk;
     m.end = s.find('\n', mk);
     out.push_back(m);
@@ -110,6 +116,54 @@ struct Compiler {
       }
     }
     start[n] = 1;
+  }
+
+  // Registers the program may read before writing them (backward liveness over the forward
+  // jumps; conservative: LDX reads its base and, merging, its destination, Q1).
+  uint32_t live_in() const {
+    std::vector<uint32_t> in(n + 1, 0);
+    auto rw = [&](const Uop& u, uint32_t& rd, uint32_t& wr) {
+      const uint32_t d = 1u << u.dst, s = (u.aux & F_SRC) ? 1u << u.src : 0u;
+      rd = wr = 0;
+      if (u.op <= U_ARSH32) {  // ALU64 / ALU32
+        wr = d;
+        rd = s | ((u.op == U_MOV64 || u.op == U_MOV32) ? 0u : d);
+      } else if (u.op <= U_BSWAP64) {  // END
+        rd = wr = d;
+      } else if (u.op >= U_JA && u.op <= U_JLE32) {
+        rd = u.op == U_JA ? 0u : (d | s);
+      } else if (u.op == U_LDIMM) {
+        wr = d;
+      } else if (u.op == U_LDX) {
+        rd = d | (1u << u.src);
+        wr = d;
+      }
+    };
+    for (uint32_t i = n; i-- > 0;) {
+      const Uop& u = uops[i];
+      uint32_t rd, wr;
+      rw(u, rd, wr);
+      uint32_t out = 0;
+      const bool jump = u.op >= U_JA && u.op <= U_JLE32;
+      const bool ends = u.op == U_EXIT || u.op == U_FAULT;
+      if (jump) {
+        if (t[i].x < n) out |= in[t[i].x];
+        if (u.op != U_JA && t[i].npc < n) out |= in[t[i].npc];
+      } else if (!ends && i + 1 < n) {
+        out = in[i + 1];
+      }
+      in[i] = (rd | (out & ~wr)) & 0x7ffu;
+    }
+    return in[0];
+  }
+
+  // ;@@JITINIT@@: r0 and the live-in registers in the main.rs layout
+  std::string init_code() const {
+    const uint32_t live = live_in() | 1u;
+    std::string s = "; registers read before written: " + std::to_string(live) + "\n";
+    for (int r = 0; r < 11; r++)
+      if (live & (1u << r)) s += kJitInitReg[r];
+    return s;
   }
 
   uint32_t next_start(uint32_t i) const {
@@ -254,11 +308,50 @@ struct Compiler {
   }
 
   // The program's code for the statement behind marker m.
-  bool body(const Marker& m, std::string& out) {
-    const std::string P = "J" + m.n + "_";
-    std::string main = "; compiled eBPF program: " + std::to_string(n) + " micro-ops\n"
-                       "s_mov_b64 exec, 0\n";
-    std::string ool;
+  // Constant-address window loads (the LDXK handlers) of the fixed-slot layout.
+  static bool is_ldxk(uint32_t id) {
+    return id == T_LDXK_C || id == T_LDXK_E || id == T_LDXK1_C || id == T_LDXK1_E ||
+           id == T_LDXK2_C || id == T_LDXK2_E;
+  }
+
+  // A window load from the registers the fast copy preloaded: window dword k of the lane is
+  // v[64 + k] (the fixed-slot layout: every packet >= 64 bytes, so no length masking; the caller
+  // checked mem_size against every such load's end). The access's bytes are merged into dst as
+  // the handlers do (Q1): v_perm_b32 picks bytes of the window dword for the low `width` bytes
+  // and keeps dst's other bytes.
+  std::string ldxk_fast(uint32_t i) const {
+    const TUop& u = t[i];
+    const uint32_t a0 = u.a0, width = u.x - u.a0, sh = a0 & 3, d = a0 >> 2;
+    auto W = [](uint32_t k) { return "v" + std::to_string(64 + k); };
+    const std::string D0 = "v" + std::to_string(u.dst2), D1 = "v" + std::to_string(u.dst2 + 1);
+    std::string s;
+    if (width == 8) {
+      if (sh == 0)
+        return "v_mov_b32 " + D0 + ", " + W(d) + "\nv_mov_b32 " + D1 + ", " + W(d + 1) + "\n";
+      return "v_alignbyte_b32 " + D0 + ", " + W(d + 1) + ", " + W(d) + ", " + std::to_string(sh) +
+             "\nv_alignbyte_b32 " + D1 + ", " + W(d + 2) + ", " + W(d + 1) + ", " +
+             std::to_string(sh) + "\n";
+    }
+    std::string src = W(d);
+    uint32_t off = sh;
+    if (sh + width > 4 && width == 4)
+      return "v_alignbyte_b32 " + D0 + ", " + W(d + 1) + ", " + W(d) + ", " + std::to_string(sh) +
+             "\n";
+    if (sh + width > 4) {  // spans two dwords: align into v26 first
+      s += "v_alignbyte_b32 v26, " + W(d + 1) + ", " + W(d) + ", " + std::to_string(sh) + "\n";
+      src = "v26";
+      off = 0;
+    }
+    if (width == 4) return s + "v_mov_b32 " + D0 + ", " + src + "\n";
+    uint32_t sel = 0;
+    for (uint32_t b = 0; b < 4; b++) sel |= (b < width ? 4 + off + b : b) << (8 * b);
+    return s + "s_mov_b32 s36, " + hex32(sel) + "\nv_perm_b32 " + D0 + ", " + src + ", " + D0 +
+           ", s36\n";
+  }
+
+  // One copy of the program. fast: window loads from preloaded registers (ldxk_fast).
+  bool copy(const Marker& m, const std::string& P, bool fast, std::string& main,
+            std::string& ool) {
     for (uint32_t i = 0; i < n; i++) {
       if (start[i]) {
         main += ".L" + P + "b" + std::to_string(i) + ":\n";
@@ -273,6 +366,10 @@ struct Compiler {
         err = "bad handler id";
         return false;
       }
+      if (fast && is_ldxk(id)) {
+        main += ldxk_fast(i);
+        continue;
+      }
       std::set<uint32_t> sg;
       std::string mt, ot;
       if (!expand(kJitTemplates[id][0], i, m, P, sg, mt)) return false;
@@ -284,6 +381,43 @@ struct Compiler {
       ool += ot;
     }
     main += ".L" + P + "b" + std::to_string(n) + ":\n";
+    return true;
+  }
+
+  // The program's code for the statement behind marker m. In the fixed-slot layout, a program
+  // with window loads gets a second, fast copy: the window dwords it loads are read from LDS
+  // once, up front (one ds_read_b128 per 16-byte chunk), and each load becomes one or two VALU
+  // ops. The fast copy runs when mem_size covers every such load's end (so none can fault);
+  // otherwise the handlers' copy, with its per-load bounds checks.
+  bool body(const Marker& m, std::string& out) {
+    const std::string P = "J" + m.n + "_";
+    std::string main = "; compiled eBPF program: " + std::to_string(n) + " micro-ops\n";
+    std::string ool;
+    uint32_t chunks = 0, maxend = 0;
+    if (m.fixed == "1")
+      for (uint32_t i = 0; i < n; i++) {
+        const TUop& u = t[i];
+        if (!is_ldxk(u.hoff / TILE_SLOT)) continue;
+        const uint32_t a0 = u.a0, end = u.x, width = end - a0;
+        const uint32_t last = width == 8 && (a0 & 3) ? (a0 >> 2) + 2 : (end - 1) >> 2;
+        for (uint32_t k = a0 >> 2; k <= last && k < 16; k++) chunks |= 1u << (k >> 2);
+        maxend = std::max(maxend, end);
+      }
+    if (chunks) {
+      const std::string F = "J" + m.n + "f_";
+      main += "s_cmp_gt_u32 " + std::to_string(maxend) + ", s33\ns_cbranch_scc1 .L" + P +
+              "slow\n";
+      for (uint32_t c = 0; c < 4; c++)
+        if (chunks & (1u << c))
+          main += "v_xad_u32 v36, v35, " + std::to_string(16 * c) + ", v34\nds_read_b128 v[" +
+                  std::to_string(64 + 4 * c) + ":" + std::to_string(67 + 4 * c) + "], v36\n";
+      main += "s_waitcnt lgkmcnt(0)\ns_mov_b64 exec, 0\n";
+      if (!copy(m, F, true, main, ool)) return false;
+      main += "s_branch .L" + P + "end\n.L" + P + "slow:\n";
+    }
+    main += "s_mov_b64 exec, 0\n";
+    if (!copy(m, P, false, main, ool)) return false;
+    main += ".L" + P + "end:\n";
     if (!ool.empty()) main += "s_branch .Ldone" + m.n + "\n" + ool;
     out = main;
     return true;
@@ -380,13 +514,16 @@ bool jit_compile(const std::vector<Uop>& uops, const std::vector<TUop>& t,
   Compiler c(uops, t);
   std::string src;
   size_t at = 0;
+  const std::string init = c.init_code();
   for (const Marker& m : marks) {
     std::string b;
     if (!c.body(m, b)) {
       if (err) *err = c.err;
       return false;
     }
-    src += tmpl.substr(at, m.begin - at);
+    src += tmpl.substr(at, m.init_begin - at);
+    src += init;
+    src += tmpl.substr(m.init_end, m.begin - m.init_end);
     src += b;
     at = m.end;
   }

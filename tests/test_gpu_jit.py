@@ -163,6 +163,33 @@ def test_compiled_vs_interpreter_and_oracle(cuda, oracle_mod, layout, seed):
 
 
 @pytest.mark.gpu
+def test_compiled_fixed_small_image(cuda, oracle_mod):
+    """Fixed-slot batches whose image is as small as the slots (mem_size = stride = 64): window
+    loads past the image fault (ST_MEM / ST_MEM_UB), so the compiled kernel takes its checked copy
+    of the program instead of the preloaded-window one. Both against the interpreter and the
+    oracle."""
+    from ebpf_emu.asm import assemble
+
+    srcs = ["ldxdw r0, [r1+60]\nexit", "ldxw r0, [r1+62]\nexit", "ldxb r0, [r1+63]\nexit",
+            "ldxh r3, [r1+12]\nldxdw r0, [r1+58]\nadd r0, r3\nexit",
+            "mov r0, 2\njlt r2, 70, +1\nldxdw r0, [r1+60]\nexit"]
+    rng = random.Random(99)
+    pkts = [bytes(rng.getrandbits(8) for _ in range(64)) for _ in range(130)]
+    for src in srcs:
+        img = assemble(src)
+        for mem in (64, 1024):
+            got = _run(img, pkts, cuda, fixed_stride=64, mem_size=mem)
+            ref = _run(img, pkts, cuda, fixed_stride=64, mem_size=mem, no_jit=True)
+            _same(got, ref, f"{src!r} mem {mem}")
+            op = oracle_mod.Program(img)
+            for i, p in enumerate(pkts[:20]):
+                st, regs, _m, _s = op.run_full(p, mem, 512, STEPS)
+                assert got["status"][i] == st, (src, mem, i)
+                if st == 0:
+                    assert int(got["r0"][i]) == regs[0], (src, mem, i)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("config", ["drop", "5tuple"])
 def test_workloads_compiled_vs_interpreter(cuda, oracle_mod, config):
     """The bench workloads (BASELINE configs 1-4) on 8192 synthetic 64-byte frames, fixed-slot
