@@ -1238,12 +1238,118 @@ def cstr(text):
                      for ln in text.splitlines()) or '""'
 
 
-# The template kernel's statement: the prologue, a marker the compiler fills in at load time, the
-# epilogue. The marker line carries the statement's label number and operand registers.
-JIT_STATEMENT = PROLOGUE.replace(FIXED_DMA, FIXED_DMA_DB).replace(DEFAULT_INIT, JIT_INIT) + """
+# The template kernel's statement (ebpf_tile_jit_var, every layout but the fixed-slot one): the
+# prologue, a marker the compiler fills in at load time, the epilogue. The marker line carries the
+# statement's label number and operand registers.
+JIT_STATEMENT = PROLOGUE.replace(DEFAULT_INIT, JIT_INIT) + """
 ; JIT N=%= fixed=%[fixed] loops=%[loops] aligned=%[aligned]
 ;@@JIT@@
 """ + EPILOGUE
+
+
+# The compiled fixed-slot kernel's statement (ebpf_tile_jit_fixed): the FIXED layout with double-
+# buffered windows (FIXED_DMA_DB), kernel arguments as loop-invariant SGPR operands (%[k_*],
+# loaded once per wave at kernel start instead of per-tile scalar loads and their waits), and the
+# rarely set outputs / init_regs behind %[k_flags] (bit 0 init_regs, 1 r0, 2 status, 3 regs).
+PROLOGUE_DB = """s_mov_b32 {M0S}, m0
+s_mov_b64 {PROG}, %[k_tprog]
+s_mov_b64 {KFR}, %[k_frames]
+s_mov_b64 {KST}, %[k_stride]
+s_mov_b64 {KN}, %[k_n]
+s_mov_b32 {KMEM}, %[k_mem]
+v_mbcnt_lo_u32_b32 {t0}, -1, 0
+v_mbcnt_hi_u32_b32 {t0}, -1, {t0}
+s_lshl_b64 {T0}, %[tile], 6
+v_mov_b32 {t1}, 0
+v_lshl_add_u64 {T23}, {T01}, 0, {T0}
+""" + FIXED_DMA_DB + """v_cmp_gt_u64 vcc, {KN}, {T23}
+s_and_b64 {VM}, vcc, exec
+s_cmp_gt_u32 {KSTH}, 0
+s_cselect_b32 {T3}, -1, {KSTL}
+v_mov_b32 {LEN}, {T3}
+v_mov_b32 {t4}, {KSTL}
+v_mad_u64_u32 {BASE}, {T4}, {t2}, {t4}, {KFR}
+v_mul_lo_u32 {t4}, {t3}, {KSTL}
+v_mul_lo_u32 {t9}, {t2}, {KSTH}
+v_add3_u32 {BASEH}, {BASEH}, {t4}, {t9}
+v_cndmask_b32 {LEN}, 0, {LEN}, vcc
+v_lshlrev_b32 {WIN}, 6, {t0}
+v_add_u32 {WIN}, %[winb], {WIN}
+v_lshrrev_b32 {SWZ}, 2, {t0}
+v_and_b32 {SWZ}, 3, {SWZ}
+v_lshlrev_b32 {SWZ}, 4, {SWZ}
+v_mov_b32 {NST}, 0
+v_mov_b32 {ST}, 0
+v_mov_b32 {LPC}, -1
+v_cmp_lt_u32 {T0}, {KMEM}, {LEN}
+s_and_b64 {T0}, {T0}, {VM}
+s_andn2_b64 {T1}, {VM}, {T0}
+s_mov_b64 exec, {T0}
+v_mov_b32 {ST}, 7
+s_mov_b64 exec, {T1}
+v_mov_b32 {LPC}, 0
+s_mov_b64 exec, {EXEC0}
+s_mov_b64 {KR10}, %[k_r10]
+s_bitcmp1_b32 %[k_flags], 0
+s_cbranch_scc1 .Linitc%=
+s_bitcmp1_b32 %[k_flags], 3
+s_cbranch_scc1 .Lallinit%=
+;@@JITINIT@@
+s_branch .Linitd%=
+.Lallinit%=:
+""" + DEFAULT_INIT + """s_branch .Linitd%=
+.Linitc%=:
+s_load_dwordx2 {T5}, %[ka], %[o_init]
+s_waitcnt lgkmcnt(0)
+s_load_dwordx16 {UOP}, {T5}, 0x0
+s_waitcnt lgkmcnt(0)
+""" + "\n".join(f"v_mov_b32 v{i}, s{UB + i}" for i in range(16)) + """
+s_load_dwordx4 s[36:39], {T5}, 0x40
+s_load_dwordx2 s[40:41], {T5}, 0x50
+s_waitcnt lgkmcnt(0)
+""" + "\n".join(f"v_mov_b32 v{16 + i}, s{UB + i}" for i in range(6)) + """
+.Linitd%=:
+"""
+
+EPILOGUE_DB = """.Ldone%=:
+s_mov_b64 exec, {EXEC0}
+v_cmp_gt_u64 vcc, 5, {RF}
+v_cndmask_b32 %[bkt], 5, {RF0}, vcc
+v_cmp_ne_u32 vcc, 0, {ST}
+v_cndmask_b32_e64 %[bkt], %[bkt], 6, vcc
+v_cndmask_b32_e64 %[bkt], 7, %[bkt], {VM}
+v_cndmask_b32_e64 %[nst], 0, {NST}, {VM}
+s_mov_b64 exec, {VM}
+s_cmp_lg_u64 exec, 0
+s_cbranch_scc0 .Lend%=
+v_mbcnt_lo_u32_b32 {t0}, -1, 0
+v_mbcnt_hi_u32_b32 {t0}, -1, {t0}
+s_lshl_b64 {T0}, %[tile], 6
+v_mov_b32 {t1}, 0
+v_lshl_add_u64 {T23}, {T01}, 0, {T0}
+s_cmp_lg_u64 %[k_verdict], 0
+s_cbranch_scc0 .Lnov%=
+v_cmp_gt_u32 vcc, 5, %[bkt]
+v_mov_b32 {t5}, 0xfe
+v_cndmask_b32 {t4}, {t5}, {RF0}, vcc
+v_cmp_ne_u32 vcc, 6, %[bkt]
+v_mov_b32 {t5}, 0xff
+v_cndmask_b32 {t4}, {t5}, {t4}, vcc
+v_lshl_add_u64 {T67}, {T23}, 0, %[k_verdict]
+global_store_byte {T67}, {t4}, off
+.Lnov%=:
+s_and_b32 {T3}, %[k_flags], 14
+s_cbranch_scc0 .Lend%=
+s_load_dwordx2 {ER0}, %[ka], %[o_r0]
+s_load_dwordx2 {EST}, %[ka], %[o_status]
+s_load_dwordx2 {ERG}, %[ka], %[o_regs]
+s_waitcnt lgkmcnt(0)
+""" + EPILOGUE[EPILOGUE.index("s_cmp_lg_u64 {ER0}, 0"):]
+
+JIT_STATEMENT_DB = PROLOGUE_DB + """
+; JIT N=%= fixed=%[fixed] loops=%[loops] aligned=%[aligned]
+;@@JIT@@
+""" + EPILOGUE_DB
 
 
 def handler_table():
@@ -1318,12 +1424,18 @@ def main():
     ids.append("static const short kTileIdEnd[] = {" + ", ".join(e_map) + "};")
     with open(os.path.join(HERE, "tile_ids.h"), "w") as f:
         f.write("\n".join(ids) + "\n")
-    # JIT: the template kernel's statement and the per-handler templates, indexed by tile id
+    # JIT: the template kernels' statements and the per-handler templates, indexed by tile id
     text = F(JIT_STATEMENT)
     assert "{" not in text
     with open(os.path.join(HERE, "tile_jit.inc"), "w") as f:
         f.write("// GENERATED by gen_tile.py -- do not edit. The JIT template kernel's statement.\n"
                 "// clang-format off\n" + cstr(text) + "\n// clang-format on\n")
+    # the double-buffered fixed-slot kernel's (PROLOGUE_DB / EPILOGUE_DB)
+    text = F(JIT_STATEMENT_DB)
+    assert "{" not in text
+    with open(os.path.join(HERE, "tile_jit_db.inc"), "w") as f:
+        f.write("// GENERATED by gen_tile.py -- do not edit. The double-buffered JIT template "
+                "kernel's statement.\n// clang-format off\n" + cstr(text) + "\n// clang-format on\n")
     out = ["// GENERATED by gen_tile.py -- do not edit. Per-handler JIT templates (jit.cpp), indexed",
            "// by tile id (tile_ids.h): {main text, out-of-line text}.", "#pragma once",
            "// clang-format off", "static const char* const kJitTemplates[T_COUNT][2] = {"]

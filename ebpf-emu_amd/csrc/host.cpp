@@ -242,6 +242,15 @@ struct ebpf_prog {
   JitFns jit_fn[kMaxDevices][2];
 };
 
+// Diagnostics: EBPFEMU_TRACE=1 gives the compiled fixed-slot kernel a per-device stamp buffer
+// (LaunchArgs::trace, kTraceWaves x kTraceSlots u64), zeroed before each launch;
+// ebpf_debug_trace() returns it.
+static const bool g_trace = [] {
+  const char* e = getenv("EBPFEMU_TRACE");
+  return e && e[0] == '1';
+}();
+static uint64_t* g_trace_buf[kMaxDevices] = {};
+
 // EBPFEMU_NO_JIT=1: forward-only programs run on the tile interpreter (A/B runs).
 static const bool g_no_jit = [] {
   const char* e = getenv("EBPFEMU_NO_JIT");
@@ -907,6 +916,13 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* bin, const ebpf_batch_out* ou
   a.n_tiles = n_tiles;
   a.init_regs = b->init_regs;
   a.mem_out = out->mem;
+  if (g_trace) {
+    const size_t tb = kTraceWaves * kTraceSlots * sizeof(uint64_t);
+    if (!g_trace_buf[device] && hipMalloc(&g_trace_buf[device], tb) != hipSuccess)
+      g_trace_buf[device] = nullptr;
+    if (g_trace_buf[device] && hipMemsetAsync(g_trace_buf[device], 0, tb, s) == hipSuccess)
+      a.trace = g_trace_buf[device];
+  }
   a.regs_out = out->regs;
   if (kind == kKindLoop && use_binning(p, b)) {
     a.perm = (const uint32_t*)(ws + kWsSlotsOff);
@@ -1028,6 +1044,13 @@ const char* ebpf_strerror(int err) {
     case EBPF_EPCAP: return "not a classic pcap capture, or a truncated record";
     default: return "unknown error";
   }
+}
+
+int ebpf_debug_trace(int device, void** dev_ptr, size_t* bytes) {
+  if (device < 0 || device >= kMaxDevices || !dev_ptr || !bytes) return EBPF_EINVAL;
+  *dev_ptr = g_trace_buf[device];
+  *bytes = g_trace_buf[device] ? kTraceWaves * kTraceSlots * sizeof(uint64_t) : 0;
+  return EBPF_OK;
 }
 
 const char* ebpf_version(void) { return "ebpfemu 0.1 gfx950"; }

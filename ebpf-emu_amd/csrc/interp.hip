@@ -1296,6 +1296,9 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
   const uint32_t win0 = lds_addr(L.win);
   const uint32_t metab = lds_addr(L.meta_off);
   uint32_t buf = 0, first = 1;
+  // DB: the rarely set inputs / outputs (tile_jit_db.inc %[k_flags])
+  const uint32_t kflags = (a.init_regs ? 1u : 0u) | (a.r0 ? 2u : 0u) | (a.status ? 4u : 0u) |
+                          (a.regs_out ? 8u : 0u);
   // DB: lane l's window-DMA source offset within a tile, (l/4) * stride + its swizzled 16-byte
   // chunk (fixed_dma_db in gen_tile.py); a loop-invariant VGPR pair
   uint64_t dmaoff = 0;
@@ -1310,6 +1313,17 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
 
   uint32_t cnt[7] = {0, 0, 0, 0, 0, 0, 0};  // per wave: < 2^32 packets
   uint32_t retired = 0;                      // per lane: <= 63 steps per tile
+  // diagnostics only (a.trace, EBPFEMU_TRACE=1): s_memrealtime stamps per wave -- entry, after
+  // each tile, before and after the counter flush; no stamp executes otherwise
+  uint64_t* const trace = DB && a.trace && wave_slot < kTraceWaves
+                              ? a.trace + wave_slot * kTraceSlots : nullptr;
+  uint32_t ntr = 0;
+  auto stamp = [&](uint32_t slot) {
+    uint64_t ts;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ts)::"memory");
+    if (__builtin_amdgcn_mbcnt_lo(~0u, 0) == 0) trace[slot] = ts;
+  };
+  if (trace) stamp(0);
 
   for (uint64_t tile = wave_slot; tile < a.n_tiles; tile += total_waves) {
     // the lane index is re-derived inside the loop (volatile: not hoistable), so no per-lane
@@ -1354,18 +1368,18 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
     const uint32_t winb = DB ? win0 + buf * kWinBytes : win0;
     const uint32_t nwinb = DB ? win0 + (buf ^ 1u) * kWinBytes : win0;
     uint32_t bkt, nst;
-    if constexpr (JIT && DB) {
+    if constexpr (JIT && DB) {  // kernel arguments as loop-invariant SGPR operands
       asm volatile(
-#include "tile_jit.inc"
+#include "tile_jit_db.inc"
           : TILE_ASM_OUT
-          : TILE_ASM_IN, [dmaoff] "v"(dmaoff)
+          : TILE_ASM_IN, [dmaoff] "v"(dmaoff), [k_frames] "s"(a.frames), [k_stride] "s"(a.stride),
+            [k_n] "s"(a.n), [k_mem] "s"(a.mem_size), [k_tprog] "s"(a.tprog), [k_r10] "s"(a.r10),
+            [k_verdict] "s"(a.verdict), [k_flags] "s"(rfl(kflags))
           : TILE_ASM_CLOBBER, TILE_ASM_CLOBBER_WINDOW);
     } else if constexpr (JIT) {
       asm volatile(
 #include "tile_jit.inc"
-          : TILE_ASM_OUT
-          : TILE_ASM_IN, [dmaoff] "v"(dmaoff)
-          : TILE_ASM_CLOBBER);
+          TILE_ASM_OPERANDS);
     } else {
       asm volatile(
 #include "tile.inc"
@@ -1402,6 +1416,17 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
     retired += nst;
     buf ^= 1u;
     first = 0;
+    if (trace && ntr < 10) stamp(1 + ntr++);
+  }
+  if (trace) {
+    stamp(12);
+    uint32_t xcc, hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)\n\ts_getreg_b32 %1, hwreg(HW_REG_HW_ID)"
+                 : "=s"(xcc), "=s"(hw));
+    if (__builtin_amdgcn_mbcnt_lo(~0u, 0) == 0) {
+      trace[14] = ((uint64_t)xcc << 32) | hw;
+      trace[15] = ntr;
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // a next-tile prefetch may be in flight
   uint64_t cnt64[7];
@@ -1410,6 +1435,7 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
   uint32_t ln;
   asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
   flush_counters(a, cnt64, retired, smem, ln, wv);
+  if (trace) stamp(13);
 }
 
 #ifndef EBPFEMU_JIT_TEMPLATE

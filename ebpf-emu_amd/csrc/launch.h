@@ -59,7 +59,12 @@ struct LaunchArgs {
                               //    in-kernel (counted shard words, flush_counters)
   const uint32_t* perm;       // loop mode: packet index of tile slot i (length-binned), else null
   uint32_t* bin_counts;       // with perm: bin counts + cursors, zeroed again by the tile kernel
+  uint64_t* trace;            // diagnostics (EBPFEMU_TRACE=1): per-wave s_memrealtime stamps of
+                              // the compiled fixed-slot kernel, kTraceSlots per wave; else null
 };
+
+constexpr int kTraceSlots = 16;
+constexpr uint64_t kTraceWaves = 1 << 16;
 
 // Bytes of tier-1 scratch per wave slot: lane-interleaved image dwords + call stack.
 __host__ __device__ inline uint64_t tier1_slot_bytes(uint32_t mem_size) {

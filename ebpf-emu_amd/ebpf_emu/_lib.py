@@ -30,7 +30,7 @@ MAX_CALL_DEPTH = 64
 
 EXPORTS = ["ebpf_batch_init", "ebpf_prog_load", "ebpf_prog_load_hex", "ebpf_prog_free",
            "ebpf_prog_len", "ebpf_prog_insn", "ebpf_prog_tier", "ebpf_prog_forward_only",
-           "ebpf_workspace_bytes", "ebpf_prog_compile", "ebpf_prog_jit_asm",
+           "ebpf_workspace_bytes", "ebpf_prog_compile", "ebpf_prog_jit_asm", "ebpf_debug_trace",
            "ebpf_prog_upload", "ebpf_run_batch", "ebpf_run_batch_multi", "ebpf_pcap_index",
            "ebpf_strerror", "ebpf_version"]
 
@@ -87,6 +87,7 @@ def lib():
     L.ebpf_prog_tier.argtypes = [vp]
     L.ebpf_prog_forward_only.argtypes = [vp]
     L.ebpf_prog_compile.argtypes = [vp]
+    L.ebpf_debug_trace.argtypes = [ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(sz)]
     L.ebpf_prog_jit_asm.argtypes = [vp, ctypes.c_int, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
     L.ebpf_workspace_bytes.argtypes = [vp, ctypes.POINTER(Batch), ctypes.c_int]
     L.ebpf_workspace_bytes.restype = u64

@@ -101,6 +101,34 @@ __global__ __launch_bounds__(256) void sol_stream(const uint8_t* frames, uint64_
   }
 }
 
+// (f): (c) + a returning agent-scope atomic per workgroup at the end (the counter flush's round trip)
+__global__ __launch_bounds__(256) void sol_lds_atomic(const uint8_t* frames, uint64_t n,
+                                                      uint8_t* verdict, unsigned long long* ctr) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x / 64);
+  const uint64_t tile = (uint64_t)blockIdx.x * 4 + wv;
+  uint8_t* win = smem + wv * 4608;
+  const uint32_t lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)win;
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const uint64_t p = tile * kWave + r * 16 + lane / 4;
+    const uintptr_t src = p < n ? (uintptr_t)(frames + p * 64 + (lane & 3) * 16) : (uintptr_t)frames;
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(src), "s"(lds + r * 1024) : "memory");
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const uint32_t v = *(const uint32_t*)(win + lane * 64 + 12);
+  const uint64_t pkt = tile * kWave + lane;
+  if (pkt < n) verdict[pkt] = (uint8_t)(1 + (v == 0x12345678u));
+  if (wv == 0 && lane < 8) {
+    const unsigned long long old = __hip_atomic_fetch_add(&ctr[(blockIdx.x % 64) * 8 + lane], 1ull,
+                                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == 0xFFFFFFFFFFFFull) ctr[lane] = 0;  // (never: keeps the returned value live)
+  }
+}
+
 template <typename K>
 static float time_it(K launch, int reps = 200) {
   hipEvent_t a, b;
@@ -119,8 +147,8 @@ static float time_it(K launch, int reps = 200) {
 int main() {
   int cus = 256;
   hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
-  for (uint64_t n : {1ull << 20, 1ull << 23}) {
-    const int pool = n == (1ull << 20) ? 8 : 2;  // distinct batches > the 256 MiB Infinity Cache
+  for (uint64_t n : {1ull << 12, 1ull << 16, 1ull << 20, 1ull << 23}) {
+    const int pool = n <= (1ull << 20) ? 8 : 2;  // distinct batches (> the 256 MiB Infinity Cache at 1 Mi)
     std::vector<uint8_t*> fr(pool);
     for (auto& f : fr) {
       hipMalloc(&f, n * 64);
@@ -148,6 +176,13 @@ int main() {
     report("(c) LDS-DMA, 4.5 KiB per wave", time_it([&](int i) {
              sol_lds<512><<<grid, 256, 4 * 4608>>>(fr[i % pool], n, verdict);
            }));
+    unsigned long long* ctr;
+    hipMalloc(&ctr, 64 * 8 * 8);
+    hipMemset(ctr, 0, 64 * 8 * 8);
+    report("(f) as (c) + a returning atomic per WG", time_it([&](int i) {
+             sol_lds_atomic<<<grid, 256, 4 * 4608>>>(fr[i % pool], n, verdict, ctr);
+           }));
+    hipFree(ctr);
     report("(d) LDS-DMA, 4.5 KiB, balanced persistent", time_it([&](int i) {
              sol_lds_persist<<<pgrid, 256, 4 * 4608>>>(fr[i % pool], n, verdict);
            }));
