@@ -153,6 +153,7 @@ def main():
     ev0.record(stream)
     for i in range(args.steps):
         step(i)
+    t_enq = time.perf_counter() - t0  # host time to enqueue the K steps (launch-bound check)
     ev1.record(stream)
     D.reduce_counters(counters)  # the one exchange step: per-verdict counters, RCCL / xGMI
     torch.cuda.synchronize(dev)
@@ -224,6 +225,7 @@ def main():
             "counters": {"drop": cnt[1], "pass": cnt[2], "other": cnt[5], "faults": cnt[6],
                          "insns_retired": cnt[7]},
             "ebpf_insns_per_s": round(cnt[7] / elapsed, 1),
+            "host_enqueue_us_per_step": round(t_enq / args.steps * 1e6, 3),
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

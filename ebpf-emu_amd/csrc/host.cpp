@@ -250,6 +250,7 @@ static const bool g_trace = [] {
   return e && e[0] == '1';
 }();
 static uint64_t* g_trace_buf[kMaxDevices] = {};
+static uint32_t g_trace_launch[kMaxDevices] = {};
 
 // EBPFEMU_NO_JIT=1: forward-only programs run on the tile interpreter (A/B runs).
 static const bool g_no_jit = [] {
@@ -916,12 +917,16 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* bin, const ebpf_batch_out* ou
   a.n_tiles = n_tiles;
   a.init_regs = b->init_regs;
   a.mem_out = out->mem;
-  if (g_trace) {
+  if (g_trace) {  // a ring of kTraceRing launches' stamps
     const size_t tb = kTraceWaves * kTraceSlots * sizeof(uint64_t);
-    if (!g_trace_buf[device] && hipMalloc(&g_trace_buf[device], tb) != hipSuccess)
+    if (!g_trace_buf[device] && (hipMalloc(&g_trace_buf[device], tb * kTraceRing) != hipSuccess ||
+                                 hipMemset(g_trace_buf[device], 0, tb * kTraceRing) != hipSuccess))
       g_trace_buf[device] = nullptr;
-    if (g_trace_buf[device] && hipMemsetAsync(g_trace_buf[device], 0, tb, s) == hipSuccess)
-      a.trace = g_trace_buf[device];
+    // (no per-launch clearing: a memset between launches would sit in the gaps being measured;
+    // every wave rewrites its slots, so only the stamps of tiles it did not run are stale)
+    if (g_trace_buf[device])
+      a.trace = g_trace_buf[device] + (g_trace_launch[device]++ % kTraceRing) *
+                                          (kTraceWaves * kTraceSlots);
   }
   a.regs_out = out->regs;
   if (kind == kKindLoop && use_binning(p, b)) {
@@ -1049,7 +1054,7 @@ const char* ebpf_strerror(int err) {
 int ebpf_debug_trace(int device, void** dev_ptr, size_t* bytes) {
   if (device < 0 || device >= kMaxDevices || !dev_ptr || !bytes) return EBPF_EINVAL;
   *dev_ptr = g_trace_buf[device];
-  *bytes = g_trace_buf[device] ? kTraceWaves * kTraceSlots * sizeof(uint64_t) : 0;
+  *bytes = g_trace_buf[device] ? kTraceRing * kTraceWaves * kTraceSlots * sizeof(uint64_t) : 0;
   return EBPF_OK;
 }
 

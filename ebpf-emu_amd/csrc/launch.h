@@ -65,6 +65,7 @@ struct LaunchArgs {
 
 constexpr int kTraceSlots = 16;
 constexpr uint64_t kTraceWaves = 1 << 16;
+constexpr int kTraceRing = 4;  // launches kept (consecutive launches' gaps)
 
 // Bytes of tier-1 scratch per wave slot: lane-interleaved image dwords + call stack.
 __host__ __device__ inline uint64_t tier1_slot_bytes(uint32_t mem_size) {

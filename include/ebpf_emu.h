@@ -204,9 +204,10 @@ const char* ebpf_strerror(int err);
 
 /* Version string of the library (build configuration). */
 /* Diagnostics: with EBPFEMU_TRACE=1 in the environment, the compiled fixed-slot kernel writes
- * per-wave s_memrealtime stamps (100 MHz) into a device buffer of `device`, zeroed before each
- * launch: wave w's 16 u64 at w * 16 -- [0] entry, [1..10] after each tile, [12] before and [13]
- * after the counter flush, [14] XCC_ID << 32 | HW_ID, [15] tiles. NULL / 0 when off. */
+ * per-wave s_memrealtime stamps (100 MHz) into a device buffer of `device`: a ring of 4 launches
+ * of 65536 waves x 16 u64 (launch k in slot k % 4, zeroed once); wave w's 16 u64 at
+ * w * 16 -- [0] entry, [1..10] after each tile, [12] before and [13] after the counter flush,
+ * [14] XCC_ID << 32 | HW_ID, [15] tiles. NULL / 0 when off. */
 int ebpf_debug_trace(int device, void** dev_ptr, size_t* bytes);
 
 const char* ebpf_version(void);
