@@ -236,8 +236,10 @@ def main():
 def kernel_name(prog):
     """The kernel ebpf_run_batch picks for this program (interp.hip kernel_for; a compiled
     program runs as the JIT template kernel with its code, csrc/jit.cpp)."""
-    if prog.forward_only and prog.compile() and os.environ.get("EBPFEMU_NO_JIT") != "1":
-        return "ebpf_tile_jit_fixed (compiled program)"
+    if prog.tier == 0 and len(prog) <= 62 and prog.compile() and os.environ.get("EBPFEMU_NO_JIT") != "1":
+        if prog.forward_only:
+            return "ebpf_tile_jit_fixed (compiled program)"
+        return "ebpf_tile_jit_loop (compiled loop program)"
     if prog.tier == 0 and len(prog) <= 62:
         return "ebpfemu::tile_kernel<" + ("forward" if prog.forward_only else "loops") + ">"
     if prog.forward_only:

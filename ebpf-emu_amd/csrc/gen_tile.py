@@ -1199,7 +1199,7 @@ s_cmp_ge_u32 {{A0}}, {{KMEM}}
 s_cselect_b32 {{T3}}, {ST_MEM}, {ST_MEM_UB}
 v_mov_b32 {{ST}}, {{T3}}
 v_subrev_u32 {{NST}}, {{REMK}}, {{NST}}
-s_mov_b64 exec, 0
+@EXIT@
 s_branch @NEXT@"""
 
 JIT_TERM = {
@@ -1224,8 +1224,10 @@ def jit_template(base):
         raw = body
     elif kind == "div":
         raw = body + "\n" + divmod("j")
-    elif body == "ldx1":
-        raw = ldx1("j", False)
+    elif body == "ldx1":  # loop programs: the refillable-window forms
+        raw = ".if %[loops]\n" + ldx1("j", True) + "\n.else\n" + ldx1("j", False) + "\n.endif"
+    elif body == "ldx":
+        raw = ".if %[loops]\n" + ldx_loop("j") + "\n.else\n" + ldx("j") + "\n.endif"
     else:
         raw = JIT_OOL[body]("j")
     main = jit_text(F(raw))
@@ -1241,7 +1243,8 @@ def cstr(text):
 # The template kernel's statement (ebpf_tile_jit_var, every layout but the fixed-slot one): the
 # prologue, a marker the compiler fills in at load time, the epilogue. The marker line carries the
 # statement's label number and operand registers.
-JIT_STATEMENT = PROLOGUE.replace(DEFAULT_INIT, JIT_INIT) + """
+# (s70: loop programs' exact-mode flag, set by the compiled code's step-budget restart)
+JIT_STATEMENT = "s_mov_b32 s70, 0\n" + PROLOGUE.replace(DEFAULT_INIT, JIT_INIT) + """
 ; JIT N=%= fixed=%[fixed] loops=%[loops] aligned=%[aligned]
 ;@@JIT@@
 """ + EPILOGUE

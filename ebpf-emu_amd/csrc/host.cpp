@@ -233,13 +233,16 @@ struct ebpf_prog {
   TUop* dev_ltuops[kMaxDevices] = {};
   TUop* dev_ltuopsx[kMaxDevices] = {};
   // the compiled program (jit.cpp), per variant of tuops / tuopsk: code object, and its module on
-  // each device. jit_state: 0 not compiled yet, 1 compiled, 2 not a compiled program, < 0 failed
+  // each device. Variants: 0 tuops (init_regs batches), 1 tuopsk (the main.rs layout), 2 the loop
+  // program (ltuops + ltuopsx). jit_state: 0 not compiled yet, 1 compiled, 2 not a compiled
+  // program, < 0 failed
   int jit_state = 0;
-  std::vector<char> jit_co[2];
-  std::string jit_asm[2];
+  bool jit_has[3] = {};
+  std::vector<char> jit_co[3];
+  std::string jit_asm[3];
   std::string jit_err;
-  hipModule_t jit_mod[kMaxDevices][2] = {};
-  JitFns jit_fn[kMaxDevices][2];
+  hipModule_t jit_mod[kMaxDevices][3] = {};
+  JitFns jit_fn[kMaxDevices][3];
 };
 
 // Diagnostics: EBPFEMU_TRACE=1 gives the compiled fixed-slot kernel a per-device stamp buffer
@@ -261,14 +264,20 @@ static const bool g_no_jit = [] {
 // Compile both table variants (caller holds p->mu). Returns the C ABI code of ebpf_prog_compile.
 static int jit_compile_locked(ebpf_prog* p) {
   if (p->jit_state == 0) {
-    if (g_no_jit || p->tuops.empty() || p->tuopsk.empty()) {
+    p->jit_has[0] = p->jit_has[1] = !p->tuops.empty() && !p->tuopsk.empty();
+    p->jit_has[2] = !p->ltuops.empty() && !p->ltuopsx.empty();
+    if (g_no_jit || (!p->jit_has[0] && !p->jit_has[2])) {
       p->jit_state = 2;
     } else {
       p->jit_state = 1;
-      for (int v = 0; v < 2 && p->jit_state == 1; v++)
-        if (!jit_compile(p->uops, v ? p->tuopsk : p->tuops, p->jit_co[v], &p->jit_err,
-                         &p->jit_asm[v]))
-          p->jit_state = EBPF_EJIT;
+      for (int v = 0; v < 3 && p->jit_state == 1; v++) {
+        if (!p->jit_has[v]) continue;
+        const bool ok = v == 2 ? jit_compile_loop(p->uops, p->ltuops, p->ltuopsx, p->jit_co[v],
+                                                  &p->jit_err, &p->jit_asm[v])
+                               : jit_compile(p->uops, v ? p->tuopsk : p->tuops, p->jit_co[v],
+                                             &p->jit_err, &p->jit_asm[v]);
+        if (!ok) p->jit_state = EBPF_EJIT;
+      }
       if (p->jit_state == EBPF_EJIT && getenv("EBPFEMU_JIT_VERBOSE"))
         fprintf(stderr, "ebpfemu: program compiler: %s\n", p->jit_err.c_str());
     }
@@ -650,7 +659,7 @@ void ebpf_prog_free(ebpf_prog* p) {
       if (p->dev_ltuops[d]) hipFree(p->dev_ltuops[d]);
       if (p->dev_ltuopsx[d]) hipFree(p->dev_ltuopsx[d]);
     }
-    for (int v = 0; v < 2; v++)
+    for (int v = 0; v < 3; v++)
       if (p->jit_mod[d][v]) {
         hipSetDevice(d);
         (void)hipModuleUnload(p->jit_mod[d][v]);
@@ -686,9 +695,9 @@ int ebpf_prog_compile(ebpf_prog* p) {
 }
 
 int ebpf_prog_jit_asm(ebpf_prog* p, int variant, char* buf, size_t cap, size_t* len) {
-  if (!p || variant < 0 || variant > 1) return EBPF_EINVAL;
+  if (!p || variant < 0 || variant > 2) return EBPF_EINVAL;
   std::lock_guard<std::mutex> lk(p->mu);
-  if (jit_compile_locked(p) != 1) return EBPF_EINVAL;
+  if (jit_compile_locked(p) != 1 || !p->jit_has[variant]) return EBPF_EINVAL;
   const std::string& a = p->jit_asm[variant];
   if (len) *len = a.size();
   if (buf && cap) {
@@ -744,8 +753,10 @@ int ebpf_prog_upload(ebpf_prog* p, int device) {
   putt(p->ltuopsx, &tlx);
   // the compiled program's modules on this device (a compiler failure leaves the interpreter)
   if (rc == EBPF_OK && jit_compile_locked(p) == 1) {
-    for (int v = 0; v < 2 && rc == EBPF_OK; v++)
-      if (!jit_load(p->jit_co[v], &p->jit_mod[device][v], &p->jit_fn[device][v])) rc = EBPF_EHIP;
+    for (int v = 0; v < 3 && rc == EBPF_OK; v++)
+      if (p->jit_has[v] &&
+          !jit_load(p->jit_co[v], &p->jit_mod[device][v], &p->jit_fn[device][v]))
+        rc = EBPF_EHIP;
   }
   if (rc == EBPF_OK) {
     p->dev_uops[device] = d;
@@ -941,6 +952,8 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* bin, const ebpf_batch_out* ou
   const JitFns* jit = nullptr;
   if (kind == kKindDag && !(b->flags & EBPF_BATCH_NO_JIT) && p->jit_mod[device][0])
     jit = &p->jit_fn[device][b->init_regs ? 0 : 1];
+  if (kind == kKindLoop && !(b->flags & EBPF_BATCH_NO_JIT) && p->jit_mod[device][2])
+    jit = &p->jit_fn[device][2];
   hipError_t e = launch_interp(kind, a, grid, s, jit);
   if (cur != device) hipSetDevice(cur);
   return e == hipSuccess ? EBPF_OK : EBPF_EHIP;

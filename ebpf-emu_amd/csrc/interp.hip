@@ -1453,6 +1453,11 @@ extern "C" __global__ __launch_bounds__(kBlock, 4) void ebpf_tile_jit_fixed(Laun
 extern "C" __global__ __launch_bounds__(kBlock, 8) void ebpf_tile_jit_var(LaunchArgs a) {
   tile_body<false, false, true>(a);
 }
+// loop programs (back edges, or a step budget that can bind): the exact budget and refillable
+// windows as tile_kernel<false, true>
+extern "C" __global__ __launch_bounds__(kBlock, 8) void ebpf_tile_jit_loop(LaunchArgs a) {
+  tile_body<false, true, true>(a);
+}
 #endif
 
 #ifndef EBPFEMU_JIT_TEMPLATE
@@ -1639,7 +1644,9 @@ hipError_t launch_interp(int kind, const LaunchArgs& a, int grid, hipStream_t st
   b.fold_kernel = fold_kernel ? 1u : 0u;
   void* bargs[] = {(void*)&b};
   hipError_t e;
-  if (jit && kind == kKindDag && tile_kernel_for(kind, a.n_uops)) {  // the compiled program
+  if (jit && jit->loop && kind == kKindLoop) {  // the compiled loop program
+    e = hipModuleLaunchKernel(jit->loop, grid, 1, 1, kBlock, 1, 1, lds, stream, bargs, nullptr);
+  } else if (jit && jit->fixed && kind == kKindDag && tile_kernel_for(kind, a.n_uops)) {
     if (fixed_layout(&a)) {  // double-buffered windows: its own LDS size and grid
       const uint32_t dlds = g_lds_pad + kWavesPerBlock * kTileWaveLdsDb;
       e = hipModuleLaunchKernel(jit->fixed, jit_grid(jit->fixed, dlds, a.n_tiles), 1, 1, kBlock,

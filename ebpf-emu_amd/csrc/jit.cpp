@@ -27,6 +27,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <cctype>
 #include <cstring>
 #include <set>
 #include <string>
@@ -47,6 +48,7 @@ struct Marker {
   size_t init_begin = 0, init_end = 0;  // ";@@JITINIT@@" of the same statement (replaced)
   std::string n;              // the statement's %= number
   std::string fixed = "0";
+  std::string loops = "0";
   std::string aligned;
 };
 
@@ -78,6 +80,7 @@ bool find_markers(const std::string& s, std::vector<Marker>& out) {
     };
     m.n = field("N=");
     m.fixed = field("fixed=");
+    m.loops = field("loops=");
     m.aligned = field("aligned=");
     const size_t mk = s.find(";@@JIT@@", eol);
     if (mk == std::string::npos || m.n.empty()) return false;
@@ -93,29 +96,115 @@ bool find_markers(const std::string& s, std::vector<Marker>& out) {
   return !out.empty();
 }
 
+// Peephole on one micro-op's code: the handlers copy a source register pair into a temporary
+// first (READ_S into v[24:25], READ_A into v[54:55]) because the interpreter indexes it; compiled,
+// the instructions can read the register itself. Done when no instruction of the micro-op writes
+// the source pair or the temporary after the copy (so both hold the same value throughout).
+std::string dest_of(const std::string& line) {
+  const size_t sp = line.find(' ');
+  if (sp == std::string::npos || line.compare(0, 2, "v_") != 0 || line.compare(0, 5, "v_cmp") == 0)
+    return "";
+  const size_t c = line.find(',', sp);
+  return line.substr(sp + 1, (c == std::string::npos ? line.size() : c) - sp - 1);
+}
+
+bool reg_overlap(const std::string& op, uint32_t lo, uint32_t hi) {
+  uint32_t a, b;
+  if (sscanf(op.c_str(), "v[%u:%u]", &a, &b) == 2) return !(b < lo || a > hi);
+  if (sscanf(op.c_str(), "v%u", &a) == 1) return a >= lo && a <= hi;
+  return false;
+}
+
+void replace_token(std::string& s, const std::string& from, const std::string& to) {
+  size_t q = 0;
+  while ((q = s.find(from, q)) != std::string::npos) {
+    const bool left_ok = q == 0 || !(isalnum((unsigned char)s[q - 1]) || s[q - 1] == '_');
+    const size_t e = q + from.size();
+    const bool right_ok = e >= s.size() || !(isalnum((unsigned char)s[e]) || s[e] == '_');
+    if (left_ok && right_ok) {
+      s.replace(q, from.size(), to);
+      q += to.size();
+    } else {
+      q = e;
+    }
+  }
+}
+
+std::string fold_copy(const std::string& text, uint32_t tmp) {
+  std::vector<std::string> lines;
+  size_t p = 0;
+  while (p < text.size()) {
+    size_t e = text.find('\n', p);
+    if (e == std::string::npos) e = text.size();
+    lines.push_back(text.substr(p, e - p));
+    p = e + 1;
+  }
+  const std::string tpair = "v[" + std::to_string(tmp) + ":" + std::to_string(tmp + 1) + "]";
+  const std::string head = "v_mov_b64 " + tpair + ", ";
+  size_t l0 = lines.size();
+  for (size_t i = 0; i < lines.size(); i++)
+    if (lines[i].compare(0, head.size(), head) == 0) {
+      l0 = i;
+      break;
+    }
+  if (l0 == lines.size()) return text;
+  uint32_t a, b;
+  if (sscanf(lines[l0].c_str() + head.size(), "v[%u:%u]", &a, &b) != 2 || b != a + 1) return text;
+  for (size_t i = l0 + 1; i < lines.size(); i++) {
+    const std::string d = dest_of(lines[i]);
+    if (reg_overlap(d, a, b) || reg_overlap(d, tmp, tmp + 1)) return text;
+    if (lines[i].compare(0, 4, "s_se") == 0) return text;  // (no index mode here, but be safe)
+  }
+  std::string out;
+  for (size_t i = 0; i < lines.size(); i++) {
+    if (i == l0) continue;
+    std::string ln = lines[i];
+    if (i > l0) {
+      replace_token(ln, tpair, "v[" + std::to_string(a) + ":" + std::to_string(b) + "]");
+      replace_token(ln, "v" + std::to_string(tmp), "v" + std::to_string(a));
+      replace_token(ln, "v" + std::to_string(tmp + 1), "v" + std::to_string(b));
+    }
+    out += ln + "\n";
+  }
+  return out;
+}
+
 struct Compiler {
   const std::vector<Uop>& uops;
   const std::vector<TUop>& t;
   uint32_t n;
+  // loops: a loop program (ebpf_tile_jit_loop): back edges, the step budget checked at every
+  // block entry; exact: the one-micro-op-per-block copy of the exact step budget
+  bool loops = false, exact = false;
   std::vector<char> start, target;
   std::string err;
 
-  Compiler(const std::vector<Uop>& u, const std::vector<TUop>& tt)
-      : uops(u), t(tt), n((uint32_t)u.size()) {
+  static bool is_jump(const Uop& o) { return o.op >= U_JA && o.op <= U_JLE32; }
+
+  Compiler(const std::vector<Uop>& u, const std::vector<TUop>& tt, bool lp = false, bool ex = false)
+      : uops(u), t(tt), n((uint32_t)u.size()), loops(lp), exact(ex) {
     start.assign(n + 1, 0);
     target.assign(n + 1, 0);
     target[0] = 1;
     for (uint32_t i = 0; i < n; i++) {
       if (t[i].blen) start[i] = 1;
       const Uop& o = uops[i];
-      if (o.op >= U_JA && o.op <= U_JLE32) {
+      if (is_jump(o)) {
         const uint32_t x = t[i].x;  // the canonical taken target (PC_DONE past the end)
         const uint32_t np = t[i].npc;
         if (x < n) target[x] = 1;
         if (np < n && np != i + 1) target[np] = 1;
+        // a back edge parks both successors (the fall-through one at i + 1)
+        if (loops && ((x <= i && x < n) || (np <= i && np < n)) && i + 1 < n) target[i + 1] = 1;
       }
     }
     start[n] = 1;
+  }
+
+  // a jump whose taken or not-taken successor is at or before it
+  bool back_edge(uint32_t i) const {
+    return loops && is_jump(uops[i]) &&
+           ((t[i].x <= i && t[i].x < n) || (uops[i].op != U_JA && t[i].npc <= i && t[i].npc < n));
   }
 
   // Registers the program may read before writing them (backward liveness over the forward
@@ -139,20 +228,26 @@ struct Compiler {
         wr = d;
       }
     };
-    for (uint32_t i = n; i-- > 0;) {
-      const Uop& u = uops[i];
-      uint32_t rd, wr;
-      rw(u, rd, wr);
-      uint32_t out = 0;
-      const bool jump = u.op >= U_JA && u.op <= U_JLE32;
-      const bool ends = u.op == U_EXIT || u.op == U_FAULT;
-      if (jump) {
-        if (t[i].x < n) out |= in[t[i].x];
-        if (u.op != U_JA && t[i].npc < n) out |= in[t[i].npc];
-      } else if (!ends && i + 1 < n) {
-        out = in[i + 1];
+    for (bool changed = true; changed;) {  // one pass without back edges; to a fixpoint with
+      changed = false;                     // them
+      for (uint32_t i = n; i-- > 0;) {
+        const Uop& u = uops[i];
+        uint32_t rd, wr;
+        rw(u, rd, wr);
+        uint32_t out = 0;
+        const bool ends = u.op == U_EXIT || u.op == U_FAULT;
+        if (is_jump(u)) {
+          if (t[i].x < n) out |= in[t[i].x];
+          if (u.op != U_JA && t[i].npc < n) out |= in[t[i].npc];
+        } else if (!ends && i + 1 < n) {
+          out = in[i + 1];
+        }
+        const uint32_t v = (rd | (out & ~wr)) & 0x7ffu;
+        if (v != in[i]) {
+          in[i] = v;
+          changed = true;
+        }
       }
-      in[i] = (rd | (out & ~wr)) & 0x7ffu;
     }
     return in[0];
   }
@@ -174,12 +269,37 @@ struct Compiler {
 
   // park the lanes of `mask` ("vcc" or "exec") at pc x (x >= n: they are done, their last
   // entry's LPC is below every later entry)
-  static std::string park(const std::string& lpc_val, bool done) {
-    return done ? std::string() : "v_mov_b32 v28, " + lpc_val + "\n";
+  std::string park(const std::string& lpc_val, bool done) const {
+    if (done) return loops ? "v_mov_b32 v28, -1\n" : std::string();
+    return "v_mov_b32 v28, " + lpc_val + "\n";
+  }
+
+  std::string entry_label(const std::string& P, uint32_t i) const {
+    return ".L" + P + "b" + std::to_string(i);
+  }
+
+  // Tail of a jump with a successor at or before it (loop programs): both successors' lanes
+  // park (taken: vcc), then the code continues at the lowest backward successor's entry, whose
+  // lanes run first (min-pc order; the other successor's lanes are re-admitted on the way).
+  std::string back_tail(uint32_t i, const std::string& P) const {
+    const uint32_t x = t[i].x, np = t[i].npc;
+    const bool ja = uops[i].op == U_JA;
+    std::string s;
+    if (ja) {
+      s += park(std::to_string(x), x >= n);
+    } else {
+      s += "s_mov_b64 s[64:65], exec\ns_mov_b64 exec, vcc\n" + park(std::to_string(x), x >= n) +
+           "s_andn2_b64 exec, s[64:65], vcc\n" + park(std::to_string(np), np >= n);
+    }
+    uint32_t back = n;
+    if (x <= i && x < n) back = x;
+    if (!ja && np <= i && np < n) back = std::min(back, np);
+    return s + "s_mov_b64 exec, 0\ns_branch " + entry_label(P, back) + "\n";
   }
 
   // Conditional jump tail: vcc = taken among the active lanes.
-  std::string jtail(uint32_t i) const {
+  std::string jtail(uint32_t i, const std::string& P) const {
+    if (back_edge(i)) return back_tail(i, P);
     const uint32_t x = t[i].x, np = t[i].npc;
     const bool x_next = x == i + 1, n_next = np == i + 1;
     const bool x_done = x >= n, n_done = np >= n;
@@ -199,7 +319,8 @@ struct Compiler {
     return s;
   }
 
-  std::string ja(uint32_t i) const {
+  std::string ja(uint32_t i, const std::string& P) const {
+    if (back_edge(i)) return back_tail(i, P);
     const uint32_t x = t[i].x;
     if (x == i + 1) return "";
     return park(std::to_string(x), x >= n) + "s_mov_b64 exec, 0\n";
@@ -242,11 +363,11 @@ struct Compiler {
         } else if (tok == "NEXT") {
           o += next;
         } else if (tok == "JTAIL") {
-          o += jtail(i);
+          o += jtail(i, P);
         } else if (tok == "JA") {
-          o += ja(i);
+          o += ja(i, P);
         } else if (tok == "EXIT") {
-          o += "s_mov_b64 exec, 0\n";
+          o += loops ? "v_mov_b32 v28, -1\ns_mov_b64 exec, 0\n" : "s_mov_b64 exec, 0\n";
         } else if (tok[0] == 'D' || tok[0] == 'S') {
           const uint32_t base = tok[0] == 'D' ? u.dst2 : u.src2;
           if (base > 20) {
@@ -292,7 +413,7 @@ struct Compiler {
       }
       // the statement's own operands
       for (const auto& kv : {std::make_pair(std::string("%[fixed]"), m.fixed),
-                             std::make_pair(std::string("%[loops]"), std::string("0")),
+                             std::make_pair(std::string("%[loops]"), m.loops),
                              std::make_pair(std::string("%[aligned]"), m.aligned)}) {
         size_t q;
         while ((q = o.find(kv.first)) != std::string::npos) o.replace(q, kv.first.size(), kv.second);
@@ -360,6 +481,7 @@ struct Compiler {
                   std::to_string(i) + ", v28\ns_or_b64 exec, s[64:65], vcc\n";
         main += "s_cbranch_execz .L" + P + "b" + std::to_string(next_start(i)) + "\n";
         main += "v_add_u32 v29, " + std::to_string(t[i].blen) + ", v29\n";
+        if (loops) main += budget_check(i, P);
       }
       const uint32_t id = t[i].hoff / TILE_SLOT;
       if (id >= (uint32_t)T_COUNT || id == (uint32_t)T_DONE) {
@@ -377,11 +499,27 @@ struct Compiler {
       const uint32_t* w = (const uint32_t*)&t[i];
       for (uint32_t d : sg)
         main += "s_mov_b32 s" + std::to_string(kFieldSgpr + d) + ", " + hex32(w[d]) + "\n";
+      if (ot.empty()) mt = fold_copy(fold_copy(mt, 24), 54);  // (out-of-line code may read them)
       main += mt;
       ool += ot;
     }
     main += ".L" + P + "b" + std::to_string(n) + ":\n";
+    if (loops) main += "v_mov_b32 v28, -1\n";  // lanes past the end are done
     return true;
+  }
+
+  // The step budget (s71 = max_steps) at a block entry of a loop program, as the interpreter's
+  // dispatcher: the block copy restarts the tile in exact mode when some lane would pass it inside
+  // the block (s70 = 1, windows re-read where refills are possible, tile_kernel's .Lbudget); the
+  // exact copy (one micro-op per block) stops the lanes whose step this would be, ST_STEPS.
+  std::string budget_check(uint32_t i, const std::string& P) const {
+    std::string s = "v_cmp_lt_u32 vcc, s71, v29\n";
+    if (!exact) return s + "s_cbranch_vccnz .L" + P + "budget\n";
+    const std::string ok = ".L" + P + "bok" + std::to_string(i);
+    return s + "s_cbranch_vccz " + ok + "\ns_mov_b64 s[64:65], exec\ns_mov_b64 exec, vcc\n"
+               "v_mov_b32 v30, 5\nv_mov_b32 v28, -1\nv_subrev_u32 v29, 1, v29\n"
+               "s_andn2_b64 exec, s[64:65], vcc\ns_cbranch_scc0 " +
+           entry_label(P, next_start(i)) + "\n" + ok + ":\n";
   }
 
   // The program's code for the statement behind marker m. In the fixed-slot layout, a program
@@ -417,6 +555,30 @@ struct Compiler {
     }
     main += "s_mov_b64 exec, 0\n";
     if (!copy(m, P, false, main, ool)) return false;
+    main += ".L" + P + "end:\n";
+    if (!ool.empty()) main += "s_branch .Ldone" + m.n + "\n" + ool;
+    out = main;
+    return true;
+  }
+
+  // A loop program (this compiler: the block table; xc: the exact table's) for the statement of
+  // ebpf_tile_jit_loop: s70 = 0 runs the block copy, whose budget failure restarts the tile
+  // (.Lreinit of the statement's prologue) with s70 = 1, which runs the exact copy.
+  bool body_loop(const Marker& m, Compiler& xc, std::string& out) {
+    const std::string P = "J" + m.n + "_", PX = "J" + m.n + "x_";
+    std::string main = "; compiled eBPF loop program: " + std::to_string(n) + " micro-ops\n"
+                       "s_cmp_lg_u32 s70, 0\ns_cbranch_scc1 .L" + PX + "start\n"
+                       "s_mov_b64 exec, 0\n";
+    std::string ool;
+    if (!copy(m, P, false, main, ool)) return false;
+    main += "s_branch .L" + P + "end\n.L" + P + "budget:\ns_mov_b32 s70, 1\n"
+            "s_cmp_eq_u32 " + m.aligned + ", 0\ns_cbranch_scc1 .L" + P + "bkeep\n"
+            "v_mov_b32 v22, -64\n.L" + P + "bkeep:\ns_mov_b64 exec, -1\n"
+            "s_branch .Lreinit" + m.n + "\n.L" + PX + "start:\ns_mov_b64 exec, 0\n";
+    if (!xc.copy(m, PX, false, main, ool)) {
+      err = xc.err;
+      return false;
+    }
     main += ".L" + P + "end:\n";
     if (!ool.empty()) main += "s_branch .Ldone" + m.n + "\n" + ool;
     out = main;
@@ -489,12 +651,13 @@ bool assemble(const std::string& src, std::vector<char>& co, std::string* err) {
 
 }  // namespace
 
-bool jit_compile(const std::vector<Uop>& uops, const std::vector<TUop>& t,
-                 std::vector<char>& code_object, std::string* err, std::string* asm_out) {
-  if (uops.empty() || uops.size() > kTileMaxUops || t.size() < uops.size()) {
-    if (err) *err = "not a tile program";
-    return false;
-  }
+namespace {
+
+// Insert the compiled code at every marker of the template assembly (markers of the other kind of
+// kernel -- loop vs forward-only -- get an empty body: never launched for this program), then
+// assemble.
+bool compile_into_template(Compiler& c, Compiler* xc, std::vector<char>& code_object,
+                           std::string* err, std::string* asm_out) {
   std::string tmpl(kJitTemplateAsm);
   // cache policy of the window DMA (the fixed-slot kernel's whole tiles): non-temporal -- every
   // packet byte is read once (MI355X guide, nt-weights: issued -> landed ~18 % shorter). A/B, one
@@ -511,13 +674,18 @@ bool jit_compile(const std::vector<Uop>& uops, const std::vector<TUop>& t,
     if (err) *err = "template markers not found";
     return false;
   }
-  Compiler c(uops, t);
   std::string src;
   size_t at = 0;
   const std::string init = c.init_code();
   for (const Marker& m : marks) {
     std::string b;
-    if (!c.body(m, b)) {
+    const bool loop_marker = m.loops == "1";
+    bool ok = true;
+    if (loop_marker != (xc != nullptr))
+      b = "s_mov_b64 exec, 0  ; (not this program's kernel)\n";
+    else
+      ok = xc ? c.body_loop(m, *xc, b) : c.body(m, b);
+    if (!ok) {
       if (err) *err = c.err;
       return false;
     }
@@ -532,12 +700,37 @@ bool jit_compile(const std::vector<Uop>& uops, const std::vector<TUop>& t,
   return assemble(src, code_object, err);
 }
 
+}  // namespace
+
+bool jit_compile(const std::vector<Uop>& uops, const std::vector<TUop>& t,
+                 std::vector<char>& code_object, std::string* err, std::string* asm_out) {
+  if (uops.empty() || uops.size() > kTileMaxUops || t.size() < uops.size()) {
+    if (err) *err = "not a tile program";
+    return false;
+  }
+  Compiler c(uops, t);
+  return compile_into_template(c, nullptr, code_object, err, asm_out);
+}
+
+bool jit_compile_loop(const std::vector<Uop>& uops, const std::vector<TUop>& t,
+                      const std::vector<TUop>& tx, std::vector<char>& code_object,
+                      std::string* err, std::string* asm_out) {
+  if (uops.empty() || uops.size() > kTileMaxUops || t.size() < uops.size() ||
+      tx.size() < uops.size()) {
+    if (err) *err = "not a tile program";
+    return false;
+  }
+  Compiler c(uops, t, true, false), xc(uops, tx, true, true);
+  return compile_into_template(c, &xc, code_object, err, asm_out);
+}
+
 bool jit_load(const std::vector<char>& co, hipModule_t* mod, JitFns* fns) {
   hipModule_t m = nullptr;
   if (hipModuleLoadData(&m, co.data()) != hipSuccess) return false;
   JitFns f;
   if (hipModuleGetFunction(&f.fixed, m, "ebpf_tile_jit_fixed") != hipSuccess ||
-      hipModuleGetFunction(&f.var, m, "ebpf_tile_jit_var") != hipSuccess) {
+      hipModuleGetFunction(&f.var, m, "ebpf_tile_jit_var") != hipSuccess ||
+      hipModuleGetFunction(&f.loop, m, "ebpf_tile_jit_loop") != hipSuccess) {
     (void)hipModuleUnload(m);
     return false;
   }

@@ -14,6 +14,7 @@ namespace ebpfemu {
 struct JitFns {
   hipFunction_t fixed = nullptr;
   hipFunction_t var = nullptr;
+  hipFunction_t loop = nullptr;  // loop programs (ebpf_tile_jit_loop)
 };
 
 // Compiles a forward-only program of <= kTileMaxUops micro-ops (its tile table `t`, built by
@@ -22,7 +23,13 @@ struct JitFns {
 bool jit_compile(const std::vector<Uop>& uops, const std::vector<TUop>& t,
                  std::vector<char>& code_object, std::string* err, std::string* asm_out = nullptr);
 
-// Loads a code object on the current device.
+// Loop programs (back edges, or budgets that can bind; tile tables of build_tile: `t` the block
+// table, `tx` the exact one-micro-op-per-block table) for ebpf_tile_jit_loop.
+bool jit_compile_loop(const std::vector<Uop>& uops, const std::vector<TUop>& t,
+                      const std::vector<TUop>& tx, std::vector<char>& code_object,
+                      std::string* err, std::string* asm_out = nullptr);
+
+// Loads a code object on the current device (the functions it does not hold stay null).
 bool jit_load(const std::vector<char>& code_object, hipModule_t* mod, JitFns* fns);
 
 }  // namespace ebpfemu

@@ -150,17 +150,19 @@ int ebpf_prog_tier(const ebpf_prog* prog);
  * EBPF_BATCH_GENERIC -- else 0; -1 for NULL. */
 int ebpf_prog_forward_only(const ebpf_prog* prog);
 
-/* Compile the program to gfx950 machine code now, if it is one the tile fast path runs (memory
- * tier 0, every jump forward, <= 62 micro-ops): straight-line code in pc order with direct
- * register operands, replacing the interpreter's dispatch for those programs (ebpf_run_batch
- * then launches it for batches with max_steps >= the program length). Needs no GPU; done
- * implicitly by the first upload. Returns 1 = compiled, 0 = not such a program (or compilation
- * disabled by EBPFEMU_NO_JIT=1), EBPF_EJIT on a compiler failure. */
+/* Compile the program to gfx950 machine code now, if it is one the tile kernels run (memory tier
+ * 0, <= 62 micro-ops): straight-line code in pc order with direct register operands, replacing
+ * the interpreter's dispatch. Forward-only programs get the forward kernels (batches with
+ * max_steps >= the program length); every such program also gets the loop kernel (back edges,
+ * or a step budget that can bind: the exact budget of the reference's step count). Needs no
+ * GPU; done implicitly by the first upload. Returns 1 = compiled, 0 = not such a program (or
+ * compilation disabled by EBPFEMU_NO_JIT=1), EBPF_EJIT on a compiler failure. */
 int ebpf_prog_compile(ebpf_prog* prog);
 
-/* The compiled program's gfx950 assembly (variant 0: batches with init_regs, 1: the main.rs
- * register layout, whose constant-address loads are resolved), for inspection: copies up to cap
- * bytes (NUL-terminated) and sets *len to the full length. EBPF_EINVAL if not compiled. */
+/* The compiled program's gfx950 assembly (variant 0: forward-only, batches with init_regs; 1:
+ * forward-only, the main.rs register layout, whose constant-address loads are resolved; 2: the
+ * loop-program kernel), for inspection: copies up to cap bytes (NUL-terminated) and sets *len to
+ * the full length. EBPF_EINVAL if that variant is not compiled. */
 int ebpf_prog_jit_asm(ebpf_prog* prog, int variant, char* buf, size_t cap, size_t* len);
 
 /* Device scratch a batch needs (counter shards; tier 1 adds per-wave memory images). */

@@ -36,14 +36,20 @@ def test_workloads_compile():
 
     for name, src in W.PROGRAMS.items():
         p, ok = _eligible(assemble(src))
-        assert ok == (name != "checksum"), name  # the checksum loops: interpreted (loop mode)
-        if ok:
-            for variant in (0, 1):
-                text = p.jit_asm(variant)
-                body = text[text.index("; compiled eBPF program"):]
-                body = body[:body.index(".Ldone")]
-                for word in ("s_set_gpr_idx", "s_setpc", "s_load_dwordx16", "s_ff1"):
-                    assert word not in body, (name, word)
+        assert ok, name
+        # forward-only programs: the forward kernels (0, 1) and the loop kernel (2, for budgets
+        # that can bind); the checksum loops: the loop kernel only
+        variants = (2,) if name == "checksum" else (0, 1, 2)
+        for variant in variants:
+            text = p.jit_asm(variant)
+            key = "; compiled eBPF loop program" if variant == 2 else "; compiled eBPF program"
+            body = text[text.index(key):]
+            body = body[:body.index(".Ldone")]
+            for word in ("s_set_gpr_idx", "s_setpc", "s_load_dwordx16", "s_ff1"):
+                assert word not in body, (name, word)
+        if name == "checksum":
+            with pytest.raises(Exception):
+                p.jit_asm(1)
         p.close()
 
 
@@ -61,9 +67,29 @@ def test_fuzz_programs_compile():
             continue
         if ok:
             n += 1
-            assert p.jit_asm(0) and p.jit_asm(1)
+            assert p.jit_asm(2)
+            if p.forward_only:
+                assert p.jit_asm(0) and p.jit_asm(1)
         p.close()
     assert n >= 150
+
+
+def test_fuzz_loop_programs_compile():
+    """Random tier-0 programs with back edges: the loop kernel compiles and assembles."""
+    rng = random.Random(4711)
+    n = 0
+    for _ in range(200):
+        img = gen_program(rng, allow_loops=True, tier0=True)
+        try:
+            p, ok = _eligible(img)
+        except Exception as e:
+            assert "ebpf_prog_load" in str(e) or "decode" in str(e).lower(), e
+            continue
+        if ok:
+            n += 1
+            assert p.jit_asm(2)
+        p.close()
+    assert n >= 100
 
 
 # ---------------------------------------------------------------------------------------------
