@@ -1457,7 +1457,10 @@ def main():
             t = f"v_mov_b64 v[{2 * r}:{2 * r + 1}], 0"
         inits.append(cstr(F(t)))
     assert F("\n".join(DEFAULT_INIT.split("\n"))) == F(DEFAULT_INIT)
-    out += ["static const char* const kJitInitReg[11] = {" + ",\n".join(inits) + "};",
+    out += ["static const char* const kJitInitReg[11] = {" + ",\n".join(inits) + "};"]
+    # loop programs' window refill (refill() above): exec = the lanes whose access needs packet
+    # bytes outside their window (T7), v36 = the address; WB = a & ~15 and 64 bytes from there
+    out += ["static const char* const kJitRefill =\n" + cstr(F(refill("x"))) + ";",
             "// clang-format on"]
     with open(os.path.join(HERE, "jit_tmpl.h"), "w") as f:
         f.write("\n".join(out) + "\n")

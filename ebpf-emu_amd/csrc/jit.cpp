@@ -130,6 +130,47 @@ void replace_token(std::string& s, const std::string& from, const std::string& t
   }
 }
 
+// Resolve the assembler conditionals of an expanded handler (".if 1", ".if 0 == 0", ...; the
+// statement's %[fixed] / %[loops] are known here), so only the live branch is emitted (and the
+// peepholes see straight-line code). Text with any other condition is returned unchanged.
+std::string resolve_ifs(const std::string& text) {
+  std::string out;
+  std::vector<std::pair<bool, bool>> st;  // (this branch active, enclosing active)
+  size_t p = 0;
+  while (p < text.size()) {
+    size_t e = text.find('\n', p);
+    if (e == std::string::npos) e = text.size();
+    const std::string ln = text.substr(p, e - p);
+    p = e + 1;
+    const bool live = st.empty() || (st.back().first && st.back().second);
+    if (ln.compare(0, 4, ".if ") == 0) {
+      long a = 0, b = 0;
+      char op[3] = {0};
+      bool v;
+      if (sscanf(ln.c_str() + 4, "%ld %2s %ld", &a, op, &b) == 3 && std::string(op) == "==")
+        v = a == b;
+      else if (sscanf(ln.c_str() + 4, "%ld", &a) == 1 && ln.find_first_not_of("0123456789 ", 4) == std::string::npos)
+        v = a != 0;
+      else
+        return text;
+      st.push_back({v, live});
+      continue;
+    }
+    if (ln == ".else") {
+      if (st.empty()) return text;
+      st.back().first = !st.back().first;
+      continue;
+    }
+    if (ln == ".endif") {
+      if (st.empty()) return text;
+      st.pop_back();
+      continue;
+    }
+    if (live) out += ln + "\n";
+  }
+  return st.empty() ? out : text;
+}
+
 std::string fold_copy(const std::string& text, uint32_t tmp) {
   std::vector<std::string> lines;
   size_t p = 0;
@@ -196,10 +237,16 @@ struct Compiler {
         if (np < n && np != i + 1) target[np] = 1;
         // a back edge parks both successors (the fall-through one at i + 1)
         if (loops && ((x <= i && x < n) || (np <= i && np < n)) && i + 1 < n) target[i + 1] = 1;
+        if (x <= i && x < n) back_in[x]++;
+        if (o.op != U_JA && np <= i && np < n) back_in[np]++;
       }
     }
     start[n] = 1;
   }
+
+  // back edges into each pc: a loop head with exactly one lets that jump's taken lanes run the
+  // head's block straight away (no lane can be parked there but them)
+  std::vector<uint32_t> back_in = std::vector<uint32_t>(64, 0);
 
   // a jump whose taken or not-taken successor is at or before it
   bool back_edge(uint32_t i) const {
@@ -284,6 +331,20 @@ struct Compiler {
   std::string back_tail(uint32_t i, const std::string& P) const {
     const uint32_t x = t[i].x, np = t[i].npc;
     const bool ja = uops[i].op == U_JA;
+    const bool xb = x <= i && x < n, nb = !ja && np <= i && np < n;
+    // one backward successor whose only back edge this is: its lanes continue into the loop
+    // head's block directly; the others park at their (forward or done) successor
+    if (xb != nb) {
+      const uint32_t L = xb ? x : np, F = xb ? np : x;
+      if (L < back_in.size() && back_in[L] == 1) {
+        if (ja) return "s_branch .L" + P + "body" + std::to_string(L) + "\n";
+        const std::string stay = xb ? "vcc" : "exec", leave_op = xb ? "s_andn2_b64" : "s_and_b64";
+        std::string s = "s_mov_b64 s[64:65], exec\n" + leave_op + " exec, s[64:65], vcc\n" +
+                        park(std::to_string(F), F >= n);
+        s += (xb ? "s_and_b64 exec, s[64:65], vcc\n" : "s_andn2_b64 exec, s[64:65], vcc\n");
+        return s + "s_cbranch_scc1 .L" + P + "body" + std::to_string(L) + "\n";
+      }
+    }
     std::string s;
     if (ja) {
       s += park(std::to_string(x), x >= n);
@@ -470,6 +531,74 @@ struct Compiler {
            ", s36\n";
   }
 
+  // A one-byte register-address load in a loop program (the per-byte loops): the handler's
+  // semantics (ldx1 in gen_tile.py, loop form) with its checks merged -- in bounds is a < mem
+  // as one 64-bit compare against s[52:53] = mem (mem < 2^24, so a nonzero high word fails it),
+  // the byte read with ds_read_u8 at its swizzled window address, and the window refill (or, in
+  // tiles with unaligned packets, the packet dword's load) out of line.
+  std::string ldx1_loop(uint32_t i, const Marker& m, const std::string& P, std::string& ool) const {
+    const TUop& u = t[i];
+    const std::string U = P + "u" + std::to_string(i), next = entry_label(P, next_start(i));
+    const int64_t off = (int64_t)u.imm;
+    std::string s;
+    std::string offs;
+    if (inline_const(off)) {
+      offs = std::to_string(off);
+    } else {
+      s += "s_mov_b32 s48, " + hex32((uint32_t)u.imm) + "\ns_mov_b32 s49, " +
+           hex32((uint32_t)(u.imm >> 32)) + "\n";
+      offs = "s[48:49]";
+    }
+    const std::string D0 = "v" + std::to_string(u.dst2);
+    s += "v_lshl_add_u64 v[36:37], " + vpair(u.src2, 0, 1) + ", 0, " + offs + "\n"
+         "v_cmp_gt_u64 vcc, s[52:53], v[36:37]\n"
+         "s_andn2_b64 s[64:65], exec, vcc\n"
+         "s_cbranch_scc0 .Lok" + U + "\n"
+         "s_mov_b64 s[66:67], exec\ns_mov_b64 exec, s[64:65]\n"
+         "v_mov_b32 v30, 1\nv_mov_b32 v28, -1\n"
+         "v_subrev_u32 v29, " + std::to_string(u.a0) + ", v29\n"
+         "s_andn2_b64 exec, s[66:67], s[64:65]\n"
+         "s_cbranch_execz " + next + "\n"
+         ".Lok" + U + ":\n"
+         "v_sub_u32 v42, v36, v22\n"
+         "v_cmp_le_u32_e64 s[62:63], 64, v42\n"
+         "v_cmp_lt_u32_e64 s[60:61], v36, v31\n"
+         "s_and_b64 s[68:69], s[62:63], s[60:61]\n"
+         "s_and_b64 s[68:69], s[68:69], exec\n"
+         "s_cbranch_scc1 .Lrf" + U + "\n"
+         ".Lrfb" + U + ":\n"
+         "v_min_u32 v42, 63, v42\n"
+         "v_xad_u32 v42, v35, v42, v34\n"
+         "ds_read_u8 v26, v42\n"
+         "s_waitcnt lgkmcnt(0)\n"
+         "v_cmp_lt_u32 vcc, v36, v31\n"
+         "v_cndmask_b32 v26, 0, v26, vcc\n"
+         ".Lfarb" + U + ":\n"
+         "s_mov_b32 s42, 0xff\n"
+         "v_bfi_b32 " + D0 + ", s42, v26, " + D0 + "\n";
+    ool += ".Lrf" + U + ":\n"
+           "s_cmp_eq_u32 " + m.aligned + ", 0\n"
+           "s_cbranch_scc1 .Lfar" + U + "\n" + std::string(kJitRefill) +
+           "v_sub_u32 v42, v36, v22\n"
+           "s_branch .Lrfb" + U + "\n"
+           ".Lfar" + U + ":\n"
+           "v_min_u32 v42, 63, v42\n"
+           "v_xad_u32 v42, v35, v42, v34\n"
+           "ds_read_u8 v26, v42\n"
+           "s_mov_b64 s[66:67], exec\ns_mov_b64 exec, s[68:69]\n"
+           "v_and_b32 v46, -4, v36\nv_mov_b32 v47, 0\n"
+           "v_lshl_add_u64 v[44:45], v[32:33], 0, v[46:47]\n"
+           "global_load_dword v49, v[44:45], off\n"
+           "s_waitcnt vmcnt(0) lgkmcnt(0)\n"
+           "v_and_b32 v48, 3, v36\nv_lshlrev_b32 v48, 3, v48\n"
+           "v_bfe_u32 v26, v49, v48, 8\n"
+           "s_mov_b64 exec, s[66:67]\n"
+           "v_cmp_lt_u32 vcc, v36, v31\n"
+           "v_cndmask_b32 v26, 0, v26, vcc\n"
+           "s_branch .Lfarb" + U + "\n";
+    return s;
+  }
+
   // One copy of the program. fast: window loads from preloaded registers (ldxk_fast).
   bool copy(const Marker& m, const std::string& P, bool fast, std::string& main,
             std::string& ool) {
@@ -480,6 +609,7 @@ struct Compiler {
           main += "s_mov_b64 s[64:65], exec\ns_mov_b64 exec, -1\nv_cmp_eq_u32 vcc, " +
                   std::to_string(i) + ", v28\ns_or_b64 exec, s[64:65], vcc\n";
         main += "s_cbranch_execz .L" + P + "b" + std::to_string(next_start(i)) + "\n";
+        if (loops) main += ".L" + P + "body" + std::to_string(i) + ":\n";
         main += "v_add_u32 v29, " + std::to_string(t[i].blen) + ", v29\n";
         if (loops) main += budget_check(i, P);
       }
@@ -492,6 +622,12 @@ struct Compiler {
         main += ldxk_fast(i);
         continue;
       }
+      if (loops && (id == T_LDX1_C || id == T_LDX1_E)) {
+        std::string ot;
+        main += ldx1_loop(i, m, P, ot);
+        ool += ot;
+        continue;
+      }
       std::set<uint32_t> sg;
       std::string mt, ot;
       if (!expand(kJitTemplates[id][0], i, m, P, sg, mt)) return false;
@@ -499,6 +635,8 @@ struct Compiler {
       const uint32_t* w = (const uint32_t*)&t[i];
       for (uint32_t d : sg)
         main += "s_mov_b32 s" + std::to_string(kFieldSgpr + d) + ", " + hex32(w[d]) + "\n";
+      mt = resolve_ifs(mt);
+      ot = resolve_ifs(ot);
       if (ot.empty()) mt = fold_copy(fold_copy(mt, 24), 54);  // (out-of-line code may read them)
       main += mt;
       ool += ot;
@@ -567,6 +705,7 @@ struct Compiler {
   bool body_loop(const Marker& m, Compiler& xc, std::string& out) {
     const std::string P = "J" + m.n + "_", PX = "J" + m.n + "x_";
     std::string main = "; compiled eBPF loop program: " + std::to_string(n) + " micro-ops\n"
+                       "s_mov_b32 s52, s33\ns_mov_b32 s53, 0\n"
                        "s_cmp_lg_u32 s70, 0\ns_cbranch_scc1 .L" + PX + "start\n"
                        "s_mov_b64 exec, 0\n";
     std::string ool;
