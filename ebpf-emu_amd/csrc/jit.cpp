@@ -599,6 +599,93 @@ struct Compiler {
     return s;
   }
 
+  // A register-address load in the fixed-slot layout (ldx in gen_tile.py, non-loop form; every
+  // packet a multiple of 16 bytes >= 64 long, the window its first 64 bytes): in bounds is
+  // a < mem (64-bit, so a nonzero high word fails) and a + width <= mem; window accesses read the
+  // one to three dwords they span (ds_read_u8 for one byte); accesses past the window read the
+  // packet's dwords from HBM (zeros past its end) out of line.
+  std::string ldx_fixed(uint32_t i, bool one, const std::string& P, std::string& ool) const {
+    const TUop& u = t[i];
+    const uint32_t w = one ? 1u : u.width;
+    const std::string U = P + "u" + std::to_string(i), next = entry_label(P, next_start(i));
+    const int64_t off = (int64_t)u.imm;
+    std::string s, offs;
+    if (inline_const(off)) {
+      offs = std::to_string(off);
+    } else {
+      s += "s_mov_b32 s48, " + hex32((uint32_t)u.imm) + "\ns_mov_b32 s49, " +
+           hex32((uint32_t)(u.imm >> 32)) + "\n";
+      offs = "s[48:49]";
+    }
+    const std::string D0 = "v" + std::to_string(u.dst2);
+    s += "v_lshl_add_u64 v[36:37], " + vpair(u.src2, 0, 1) + ", 0, " + offs + "\n"
+         "v_cmp_gt_u64_e64 s[60:61], s[52:53], v[36:37]\n"
+         "v_add_u32 v38, " + std::to_string(w) + ", v36\n"
+         "v_cmp_ge_u32_e64 s[62:63], s52, v38\n"
+         "s_and_b64 vcc, s[60:61], s[62:63]\n"
+         "s_andn2_b64 s[64:65], exec, vcc\n"
+         "s_cbranch_scc0 .Lok" + U + "\n"
+         "s_mov_b64 s[66:67], exec\ns_mov_b64 exec, s[64:65]\n"
+         "v_cndmask_b32_e64 v30, 1, 2, s[60:61]\n"
+         "v_mov_b32 v28, -1\n"
+         "v_subrev_u32 v29, " + std::to_string(u.a0) + ", v29\n"
+         "s_andn2_b64 exec, s[66:67], s[64:65]\n"
+         "s_cbranch_execz " + next + "\n"
+         ".Lok" + U + ":\n"
+         "v_cmp_lt_u32_e64 s[62:63], 64, v38\n"
+         "s_and_b64 s[68:69], s[62:63], exec\n"
+         "s_cbranch_scc1 .Lfar" + U + "\n";
+    // the window bytes a .. a + w - 1 (all inside [0, 64) here) into v26 (v27)
+    std::string win;
+    if (w == 1) {
+      win = "v_xad_u32 v42, v35, v36, v34\nds_read_u8 v26, v42\ns_waitcnt lgkmcnt(0)\n";
+    } else {
+      win = "v_and_b32 v42, -4, v36\nv_xad_u32 v43, v35, v42, v34\nds_read_b32 v49, v43\n"
+            "v_add_u32 v44, 4, v42\nv_min_u32 v44, 60, v44\nv_xad_u32 v44, v35, v44, v34\n"
+            "ds_read_b32 v50, v44\n";
+      if (w == 8)
+        win += "v_add_u32 v45, 8, v42\nv_min_u32 v45, 60, v45\nv_xad_u32 v45, v35, v45, v34\n"
+               "ds_read_b32 v51, v45\n";
+      win += "s_waitcnt lgkmcnt(0)\nv_alignbyte_b32 v26, v50, v49, v36\n";
+      if (w == 8) win += "v_alignbyte_b32 v27, v51, v50, v36\n";
+    }
+    s += win + ".Lmrg" + U + ":\n";
+    if (w == 1 || w == 2)
+      s += "s_mov_b32 s42, " + std::string(w == 1 ? "0xff" : "0xffff") + "\nv_bfi_b32 " + D0 +
+           ", s42, v26, " + D0 + "\n";
+    else if (w == 4)
+      s += "v_mov_b32 " + D0 + ", v26\n";
+    else
+      s += "v_mov_b64 " + vpair(u.dst2, 0, 1) + ", v[26:27]\n";
+    // out of line: lanes whose access ends past the window (in bounds: their bytes come from
+    // the packet's dwords that hold a packet byte, zeros past its end)
+    std::string far = ".Lfar" + U + ":\n" + win +
+                      "s_mov_b64 s[66:67], exec\ns_mov_b64 exec, s[68:69]\n"
+                      "v_mov_b32 v26, 0\nv_mov_b32 v27, 0\n"
+                      "v_cmp_lt_u32 vcc, v36, v31\ns_and_b64 exec, s[68:69], vcc\n"
+                      "s_cbranch_execz .Lfd" + U + "\n"
+                      "v_and_b32 v46, -4, v36\nv_mov_b32 v47, 0\n"
+                      "v_lshl_add_u64 v[44:45], v[32:33], 0, v[46:47]\n"
+                      "s_mov_b64 s[64:65], exec\n"
+                      "global_load_dword v49, v[44:45], off\n"
+                      "v_mov_b32 v50, 0\nv_mov_b32 v51, 0\n";
+    const int nd = w == 8 ? 3 : (w == 1 ? 1 : 2);
+    for (int k = 1; k < nd; k++)
+      far += "v_add_u32 v48, " + std::to_string(4 * k) + ", v46\nv_cmp_lt_u32 vcc, v48, v31\n"
+             "s_and_b64 exec, s[64:65], vcc\n"
+             "global_load_dword v" + std::to_string(49 + k) + ", v[44:45], off offset:" +
+             std::to_string(4 * k) + "\ns_mov_b64 exec, s[64:65]\n";
+    far += "s_waitcnt vmcnt(0)\n";
+    if (w == 1)
+      far += "v_and_b32 v48, 3, v36\nv_lshlrev_b32 v48, 3, v48\nv_bfe_u32 v26, v49, v48, 8\n";
+    else
+      far += "v_alignbyte_b32 v26, v50, v49, v36\n" +
+             std::string(w == 8 ? "v_alignbyte_b32 v27, v51, v50, v36\n" : "");
+    far += ".Lfd" + U + ":\ns_mov_b64 exec, s[66:67]\ns_branch .Lmrg" + U + "\n";
+    ool += far;
+    return s;
+  }
+
   // One copy of the program. fast: window loads from preloaded registers (ldxk_fast).
   bool copy(const Marker& m, const std::string& P, bool fast, std::string& main,
             std::string& ool) {
@@ -620,6 +707,13 @@ struct Compiler {
       }
       if (fast && is_ldxk(id)) {
         main += ldxk_fast(i);
+        continue;
+      }
+      if (!loops && m.fixed == "1" &&
+          (id == T_LDX_C || id == T_LDX_E || id == T_LDX1_C || id == T_LDX1_E)) {
+        std::string ot;
+        main += ldx_fixed(i, id == T_LDX1_C || id == T_LDX1_E, P, ot);
+        ool += ot;
         continue;
       }
       if (loops && (id == T_LDX1_C || id == T_LDX1_E)) {
@@ -667,7 +761,8 @@ struct Compiler {
   // otherwise the handlers' copy, with its per-load bounds checks.
   bool body(const Marker& m, std::string& out) {
     const std::string P = "J" + m.n + "_";
-    std::string main = "; compiled eBPF program: " + std::to_string(n) + " micro-ops\n";
+    std::string main = "; compiled eBPF program: " + std::to_string(n) + " micro-ops\n"
+                       "s_mov_b32 s52, s33\ns_mov_b32 s53, 0\n";
     std::string ool;
     uint32_t chunks = 0, maxend = 0;
     if (m.fixed == "1")
