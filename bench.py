@@ -42,6 +42,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", choices=sorted(CONFIGS), default="5tuple")
     ap.add_argument("--packets", type=int, default=1 << 20, help="packets per batch per GPU")
+    ap.add_argument("--frame-bytes", type=int, default=64,
+                    help="fixed-slot configs: bytes per frame slot (rounded up to 16; e.g. 1500)")
     ap.add_argument("--total-packets", type=int, default=0,
                     help="strong scaling: one global batch of this many packets (BASELINE config 4"
                          " = 100000000), sharded over the ranks in seeded 1Mi-packet chunks")
@@ -73,6 +75,8 @@ def main():
     torch.cuda.set_device(dev)
 
     cfg_idx, desc = CONFIGS[args.config]
+    if args.frame_bytes != 64 and args.config != "checksum":
+        desc = desc.replace("64B frames", f"{(max(64, args.frame_bytes) + 15) // 16 * 16}B frame slots")
     n = args.packets
     img = W.program(args.config)
     prog = Program(img)
@@ -82,6 +86,7 @@ def main():
     from ebpf_emu import dist as D
 
     mixed = args.config == "checksum"
+    fb = (max(64, args.frame_bytes) + 15) // 16 * 16  # fixed slots: 16-byte aligned, >= 64
     batches = []
     pool_bytes = 0
     if args.total_packets:
@@ -105,15 +110,18 @@ def main():
                                 offsets=torch.from_numpy(offs.view(np.int32)).to(dev),
                                 lens=torch.from_numpy(lens.view(np.int16)).to(dev)))
             algo_bytes = int(lens.astype(np.int64).sum()) + n * (4 + 2 + 1)
-        else:
-            buf = W.frames_fixed(n, 64, cid)
+        elif fb == 64 or k == 0:
+            buf = W.frames_fixed(n, fb, cid)
             batches.append(dict(frames=torch.from_numpy(buf).to(dev)))
-            algo_bytes = n * (64 + 1)
-        pool_bytes += buf.nbytes
+            algo_bytes = n * (64 + 1)  # the bytes a header program touches: its 64-byte window
+        else:  # large slots: copies of the first batch at other addresses (host RNG is slow)
+            batches.append(dict(frames=batches[0]["frames"].clone()))
+        # (the bytes a launch touches decide whether the pool outgrows the Infinity Cache)
+        pool_bytes += buf.nbytes if mixed else n * 64
         k += 1
         if pool_bytes >= args.pool_mib * (1 << 20) or k >= 16:
             break
-    mem_size, r10 = (2048, 2048) if mixed else (1024, 512)
+    mem_size, r10 = (2048, 2048) if mixed or fb > 1024 else (1024, 512)
     verdict = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
     counters = torch.zeros(8, dtype=torch.int64, device=dev)
 
@@ -125,7 +133,7 @@ def main():
             bd = prog.make_batch(b["frames"], n=n, offsets=b["offsets"], lens=b["lens"],
                                  mem_size=mem_size, r10=r10)
         else:
-            bd = prog.make_batch(b["frames"], n=n, stride=64, mem_size=mem_size, r10=r10)
+            bd = prog.make_batch(b["frames"], n=n, stride=fb, mem_size=mem_size, r10=r10)
         descs.append(bd)
     out = _lib.BatchOut()
     out.verdict = verdict.data_ptr()
@@ -203,7 +211,7 @@ def main():
                 "baseline_config": cfg_idx,
                 "packets_per_step_per_gpu": n,
                 "global_batch": args.total_packets or n * world,
-                "frame_bytes": "64/1500 mixed" if mixed else 64,
+                "frame_bytes": "64/1500 mixed" if mixed else fb,
                 "program_insns": len(prog),
                 "mem_size": mem_size,
                 "pool_batches": len(batches),
@@ -272,7 +280,7 @@ def cpu_baseline(args, img, batch0, mixed, n, mem_size, r10):
             op.run_batch(frames, hi - lo, offsets=o, lens=lens[lo:hi], **kw)
             done += hi - lo
         else:
-            op.run_batch(frames, n, stride=64, **kw)
+            op.run_batch(frames, n, stride=(max(64, args.frame_bytes) + 15) // 16 * 16, **kw)
             done += n
     dt = time.perf_counter() - t0
     return {"value": round(done / dt / 1e6, 3), "unit": "Mpkt/s", "cores": threads,
