@@ -321,6 +321,12 @@ struct Compiler {
     return "v_mov_b32 v28, " + lpc_val + "\n";
   }
 
+  // the LPC value of lanes parked at pc x ("" = no write: done lanes of a forward program)
+  std::string lpc_of(uint32_t x, bool done) const {
+    if (done) return loops ? "-1" : std::string();
+    return std::to_string(x);
+  }
+
   std::string entry_label(const std::string& P, uint32_t i) const {
     return ".L" + P + "b" + std::to_string(i);
   }
@@ -349,8 +355,10 @@ struct Compiler {
     if (ja) {
       s += park(std::to_string(x), x >= n);
     } else {
-      s += "s_mov_b64 s[64:65], exec\ns_mov_b64 exec, vcc\n" + park(std::to_string(x), x >= n) +
-           "s_andn2_b64 exec, s[64:65], vcc\n" + park(std::to_string(np), np >= n);
+      const std::string lx = lpc_of(x, x >= n), ln = lpc_of(np, np >= n);
+      if (!lx.empty() || !ln.empty())
+        s += "v_cndmask_b32_e64 v28, " + (ln.empty() ? "v28" : ln) + ", " +
+             (lx.empty() ? "v28" : lx) + ", vcc\n";
     }
     uint32_t back = n;
     if (x <= i && x < n) back = x;
@@ -365,19 +373,20 @@ struct Compiler {
     const bool x_next = x == i + 1, n_next = np == i + 1;
     const bool x_done = x >= n, n_done = np >= n;
     if (x_next && n_next) return "";
-    std::string s = "s_mov_b64 s[64:65], exec\n";
-    if (n_next) {  // taken lanes leave
-      s += "s_mov_b64 exec, vcc\n" + park(std::to_string(x), x_done) +
-           "s_andn2_b64 exec, s[64:65], vcc\n";
-    } else if (x_next) {  // not-taken lanes leave
-      s += "s_andn2_b64 exec, s[64:65], vcc\n" + park(std::to_string(np), n_done) +
-           "s_mov_b64 exec, vcc\n";
-    } else {  // both leave
-      s += "s_mov_b64 exec, vcc\n" + park(std::to_string(x), x_done) +
-           "s_andn2_b64 exec, s[64:65], vcc\n" + park(std::to_string(np), n_done) +
-           "s_mov_b64 exec, 0\n";
-    }
-    return s;
+    // the leaving lanes' LPC by one select on vcc (the pcs are inline constants), then exec
+    const std::string lx = lpc_of(x, x_done), ln = lpc_of(np, n_done);
+    if (n_next)  // taken lanes leave
+      return (lx.empty() ? "" : "v_cndmask_b32_e64 v28, v28, " + lx + ", vcc\n") +
+             "s_andn2_b64 exec, exec, vcc\n";
+    if (x_next)  // not-taken lanes leave
+      return (ln.empty() ? "" : "v_cndmask_b32_e64 v28, " + ln + ", v28, vcc\n") +
+             "s_and_b64 exec, exec, vcc\n";
+    // both leave
+    std::string s;
+    if (!lx.empty() || !ln.empty())
+      s = "v_cndmask_b32_e64 v28, " + (ln.empty() ? "v28" : ln) + ", " +
+          (lx.empty() ? "v28" : lx) + ", vcc\n";
+    return s + "s_mov_b64 exec, 0\n";
   }
 
   std::string ja(uint32_t i, const std::string& P) const {
@@ -693,8 +702,8 @@ struct Compiler {
       if (start[i]) {
         main += ".L" + P + "b" + std::to_string(i) + ":\n";
         if (target[i])
-          main += "s_mov_b64 s[64:65], exec\ns_mov_b64 exec, -1\nv_cmp_eq_u32 vcc, " +
-                  std::to_string(i) + ", v28\ns_or_b64 exec, s[64:65], vcc\n";
+          main += "s_or_saveexec_b64 s[64:65], -1\nv_cmp_eq_u32 vcc, " + std::to_string(i) +
+                  ", v28\ns_or_b64 exec, s[64:65], vcc\n";
         main += "s_cbranch_execz .L" + P + "b" + std::to_string(next_start(i)) + "\n";
         if (loops) main += ".L" + P + "body" + std::to_string(i) + ":\n";
         main += "v_add_u32 v29, " + std::to_string(t[i].blen) + ", v29\n";

@@ -81,6 +81,31 @@ def main():
     out["end_by_xcd"] = {int(x): round(float(us(tr[xcc == x, 13]).max()), 2) for x in sorted(set(xcc))}
     out["mean_end_by_xcd"] = {int(x): round(float(us(tr[xcc == x, 13]).mean()), 2)
                               for x in sorted(set(xcc))}
+    # where the spread of the waves' end times lives: across CUs, or among the waves of a CU /
+    # SIMD (HW_ID: wave [3:0], SIMD [5:4], CU [11:8], SH [12], SE [15:13]; XCC separately)
+    hw = (tr[:, 14] & 0xFFFFFFFF).astype(np.int64)
+    cu = xcc * 1000 + ((hw >> 13) & 7) * 100 + ((hw >> 12) & 1) * 50 + ((hw >> 8) & 15)
+    simd = cu * 10 + ((hw >> 4) & 3)
+    end = us(tr[:, 13])
+    import collections
+    def spread(keys):
+        g = collections.defaultdict(list)
+        for k, e in zip(keys, end):
+            g[k].append(e)
+        within = float(np.mean([max(v) - min(v) for v in g.values() if len(v) > 1]))
+        means = [np.mean(v) for v in g.values()]
+        return round(within, 2), round(float(np.max(means) - np.min(means)), 2), len(g)
+    out["end_spread_within_cu_us, across_cu_means_us, cus"] = spread(cu)
+    out["end_spread_within_simd_us, across_simd_means_us, simds"] = spread(simd)
+    # the waves of a SIMD by launch order (wave slot in the hardware): mean end per rank
+    order = collections.defaultdict(list)
+    for k, slot, e in zip(simd, (hw & 15), end):
+        order[k].append((slot, e))
+    ranks = collections.defaultdict(list)
+    for k, v in order.items():
+        for r, (_, e) in enumerate(sorted(v)):
+            ranks[r].append(e)
+    out["mean_end_by_wave_rank_in_simd"] = {r: round(float(np.mean(v)), 2) for r, v in sorted(ranks.items())}
     out["wave_span_us"] = [round((b - a) / 100.0, 2) for a, b in spans]
     out["gap_to_next_launch_us"] = gaps
     print(json.dumps(out, indent=1))
