@@ -306,6 +306,7 @@ __device__ __forceinline__ void stage_window_lane(uint8_t* pw, uint32_t swz, con
 struct WgCounters {
   uint64_t acc[8];
   uint32_t arrived;
+  uint32_t next;  // the compiled fixed-slot kernel's tile hand-out (tile_body)
 };
 __device__ __forceinline__ WgCounters* wg_counters() {
   __shared__ WgCounters c;
@@ -316,6 +317,7 @@ __device__ __forceinline__ void counters_init() {
   WgCounters* w = wg_counters();
   if (threadIdx.x < 8) w->acc[threadIdx.x] = 0;
   if (threadIdx.x == 0) w->arrived = 0;
+  if (threadIdx.x == 1) w->next = 0;
   __syncthreads();
 }
 
@@ -336,6 +338,7 @@ __device__ __forceinline__ void counters_init() {
 constexpr uint64_t kShardCountShift = 48;
 constexpr uint64_t kShardSumMask = (1ull << kShardCountShift) - 1;
 
+template <uint32_t WPB = kWavesPerBlock>
 __device__ __forceinline__ void flush_counters(const LaunchArgs& a, const uint64_t (&cnt)[7],
                                                uint64_t retired, uint8_t*, uint32_t lane,
                                                uint32_t) {
@@ -350,7 +353,7 @@ __device__ __forceinline__ void flush_counters(const LaunchArgs& a, const uint64
   uint32_t old = 0;
   if (lane == 0) old = atomicAdd(&w->arrived, 1u);
   old = __builtin_amdgcn_readfirstlane(old);
-  if (old != (uint32_t)kWavesPerBlock - 1) return;
+  if (old != WPB - 1) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   // the workgroup's last wave
   const uint32_t g = blockIdx.x % kCounterShards;
@@ -1281,8 +1284,14 @@ constexpr uint32_t kTileWaveLds = kWinBytes + kDagMetaBytes;  // window + metada
 // while the current one runs (kTileWaveLdsDb of LDS per wave).
 constexpr uint32_t kTileWaveLdsDb = 2 * kWinBytes;
 
+// DB also takes the whole CU as one workgroup of kDbWaves waves, whose tiles (b, b + G, b + 2G,
+// ... for workgroup b of G) the waves take in turn from an LDS counter instead of a fixed
+// stride: the waves of a SIMD are served in age order (the youngest used to finish ~3 us after
+// the oldest at 1 Mi packets), so a wave whose windows arrive early takes more tiles. Wave w
+// starts with ordinal w; each iteration takes the next ordinal for the window DMA it issues.
 template <bool FIXED, bool LOOPS, bool JIT, bool DB = JIT && FIXED && !LOOPS>
 __device__ __forceinline__ void tile_body(LaunchArgs& a) {
+  constexpr uint32_t WPB = DB ? (uint32_t)kDbWaves : (uint32_t)kWavesPerBlock;
   counters_init();
   // the length bins of this batch were consumed by bin_scatter (earlier on the stream): re-zero
   if (LOOPS && a.perm && blockIdx.x == 0 && threadIdx.x < 2 * kBinClasses)
@@ -1307,9 +1316,10 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
     asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
     dmaoff = (uint64_t)(lane >> 2) * a.stride + (uint64_t)(((lane & 3u) ^ ((lane >> 4) & 3u)) * 16u);
   }
-  const uint64_t wave_slot = (uint64_t)blockIdx.x * kWavesPerBlock + wv;
-  const uint64_t total_waves = (uint64_t)gridDim.x * kWavesPerBlock;
+  const uint64_t wave_slot = (uint64_t)blockIdx.x * WPB + wv;
+  const uint64_t total_waves = (uint64_t)gridDim.x * WPB;
   const auto ka = __builtin_amdgcn_kernarg_segment_ptr();
+  const uint64_t grid = gridDim.x;  // DB: ordinal k is tile blockIdx + k * G
 
   uint32_t cnt[7] = {0, 0, 0, 0, 0, 0, 0};  // per wave: < 2^32 packets
   uint32_t retired = 0;                      // per lane: <= 63 steps per tile
@@ -1325,7 +1335,20 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
   };
   if (trace) stamp(0);
 
-  for (uint64_t tile = wave_slot; tile < a.n_tiles; tile += total_waves) {
+  for (uint64_t tile = DB ? blockIdx.x + (uint64_t)wv * grid : wave_slot; tile < a.n_tiles;) {
+    uint32_t nk = 0;
+    if (DB) {  // the next ordinal, from the workgroup's counter (one lane's LDS atomic)
+      uint32_t c;
+      uint64_t sv;
+      asm volatile(
+          "s_mov_b64 %[sv], exec\n\ts_mov_b64 exec, 1\n\t"
+          "ds_add_rtn_u32 %[c], %[addr], %[one]\n\ts_waitcnt lgkmcnt(0)\n\t"
+          "s_mov_b64 exec, %[sv]\n\tv_readfirstlane_b32 %[k], %[c]"
+          : [c] "=&v"(c), [sv] "=&s"(sv), [k] "=s"(nk)
+          : [addr] "v"(lds_addr(&wg_counters()->next)), [one] "v"(1u)
+          : "memory");
+      nk += WPB;
+    }
     // the lane index is re-derived inside the loop (volatile: not hoistable), so no per-lane
     // address of the window DMA stays live across the asm statement
     uint32_t aligned = 1;  // every packet base of the tile 16-byte aligned (loop-mode refills)
@@ -1363,7 +1386,11 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
       __builtin_amdgcn_s_waitcnt(0xc07f);  // the window's LDS writes / metadata reads: done
     }
     const uint64_t t = rfl64(tile);
-    const uint64_t nt = t + total_waves;  // this wave's next tile (DMA'd now in DB mode)
+    // this wave's next tile (DMA'd now in DB mode)
+    // (32-bit scalar multiplies: a 64-bit one would be done in VGPRs)
+    const uint64_t nt =
+        DB ? blockIdx.x + ((uint64_t)__umulhi(nk, (uint32_t)grid) << 32 | (uint32_t)(nk * (uint32_t)grid))
+           : t + total_waves;
     const uint32_t pf = nt < a.n_tiles ? 1u : 0u;
     const uint32_t winb = DB ? win0 + buf * kWinBytes : win0;
     const uint32_t nwinb = DB ? win0 + (buf ^ 1u) * kWinBytes : win0;
@@ -1417,6 +1444,7 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
     buf ^= 1u;
     first = 0;
     if (trace && ntr < 10) stamp(1 + ntr++);
+    tile = nt;
   }
   if (trace) {
     stamp(12);
@@ -1434,7 +1462,7 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
   for (int b = 0; b < 7; b++) cnt64[b] = cnt[b];
   uint32_t ln;
   asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
-  flush_counters(a, cnt64, retired, smem, ln, wv);
+  flush_counters<WPB>(a, cnt64, retired, smem, ln, wv);
   if (trace) stamp(13);
 }
 
@@ -1446,8 +1474,9 @@ __global__ __launch_bounds__(kBlock, 8) void tile_kernel(LaunchArgs a) {
 #else
 // The JIT template kernels (build/tile_jit.s, embedded in the library): jit.cpp inserts each
 // program's compiled code at the marker of their statement and assembles the result.
-// (4 workgroups per CU: its two window buffers per wave take the LDS, so 128 VGPRs are free)
-extern "C" __global__ __launch_bounds__(kBlock, 4) void ebpf_tile_jit_fixed(LaunchArgs a) {
+// (one workgroup of 16 waves per CU: its two window buffers per wave take the LDS, so 128 VGPRs
+// are free)
+extern "C" __global__ __launch_bounds__(kDbBlock, 1) void ebpf_tile_jit_fixed(LaunchArgs a) {
   tile_body<true, false, true>(a);
 }
 extern "C" __global__ __launch_bounds__(kBlock, 8) void ebpf_tile_jit_var(LaunchArgs a) {
@@ -1604,7 +1633,8 @@ int interp_grid(int kind, uint32_t n_uops, bool tiny, uint64_t n_tiles, int* gri
 
 // Balanced persistent grid of a compiled kernel (its own occupancy: the DB kernel holds two
 // window buffers per wave).
-static int jit_grid(hipFunction_t f, uint32_t lds, uint64_t n_tiles) {
+static int jit_grid(hipFunction_t f, uint32_t lds, uint64_t n_tiles, int block = kBlock) {
+  const uint64_t wpb = (uint64_t)block / kWave;
   static std::mutex mu;
   static std::map<std::tuple<int, hipFunction_t, uint32_t>, std::pair<int, int>> cache;
   int dev = 0;
@@ -1619,18 +1649,21 @@ static int jit_grid(hipFunction_t f, uint32_t lds, uint64_t n_tiles) {
     } else {
       int cus = 256, per_cu = 1;
       (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-      if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, kBlock, lds) !=
+      if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, block, lds) !=
               hipSuccess ||
           per_cu < 1)
         per_cu = 1;
       occ = cache[key] = {cus, per_cu};
     }
   }
-  const uint64_t resident = (uint64_t)occ.first * occ.second * kWavesPerBlock;
   const uint64_t tiles = n_tiles ? n_tiles : 1;
+  const uint64_t wgs = (uint64_t)occ.first * occ.second;
+  if (wpb == (uint64_t)kDbWaves)  // tiles handed out within the workgroup: >= 1 tile each
+    return (int)(tiles < wgs ? tiles : wgs);
+  const uint64_t resident = wgs * wpb;
   const uint64_t per_wave = (tiles + resident - 1) / resident;
   const uint64_t waves = (tiles + per_wave - 1) / per_wave;
-  return (int)((waves + kWavesPerBlock - 1) / kWavesPerBlock);
+  return (int)((waves + wpb - 1) / wpb);
 }
 
 hipError_t launch_interp(int kind, const LaunchArgs& a, int grid, hipStream_t stream,
@@ -1648,9 +1681,9 @@ hipError_t launch_interp(int kind, const LaunchArgs& a, int grid, hipStream_t st
     e = hipModuleLaunchKernel(jit->loop, grid, 1, 1, kBlock, 1, 1, lds, stream, bargs, nullptr);
   } else if (jit && jit->fixed && kind == kKindDag && tile_kernel_for(kind, a.n_uops)) {
     if (fixed_layout(&a)) {  // double-buffered windows: its own LDS size and grid
-      const uint32_t dlds = g_lds_pad + kWavesPerBlock * kTileWaveLdsDb;
-      e = hipModuleLaunchKernel(jit->fixed, jit_grid(jit->fixed, dlds, a.n_tiles), 1, 1, kBlock,
-                                1, 1, dlds, stream, bargs, nullptr);
+      const uint32_t dlds = g_lds_pad + kDbWaves * kTileWaveLdsDb;
+      e = hipModuleLaunchKernel(jit->fixed, jit_grid(jit->fixed, dlds, a.n_tiles, kDbBlock), 1, 1,
+                                kDbBlock, 1, 1, dlds, stream, bargs, nullptr);
     } else {
       e = hipModuleLaunchKernel(jit->var, grid, 1, 1, kBlock, 1, 1, lds, stream, bargs, nullptr);
     }

@@ -11,6 +11,10 @@ namespace ebpfemu {
 constexpr int kWave = 64;
 constexpr int kBlock = 256;           // 4 waves per workgroup
 constexpr int kWavesPerBlock = kBlock / kWave;
+// the compiled fixed-slot kernel: one workgroup of 16 waves per CU, its tiles handed out to
+// the waves by an LDS counter (interp.hip tile_body)
+constexpr int kDbWaves = 16;
+constexpr int kDbBlock = kDbWaves * kWave;
 constexpr int kWin = 64;              // packet bytes staged in LDS per lane (header window)
 constexpr int kWinStride = kWin + 4;  // padded per-lane LDS stride: 17 dwords, conflict-free b32
 constexpr int kMaxLdsUops = 4096;     // programs up to this many micro-ops are staged in LDS
