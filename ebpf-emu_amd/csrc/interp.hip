@@ -50,6 +50,28 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
   return __builtin_amdgcn_readlane(v, 63);
 }
 
+// Sum over the 64 lanes (all lanes active), 64-bit: the same DPP pattern as wave_min_u32 (row
+// prefix sums, then rows 1/3 take row 0/2's total, rows 2/3 take lanes 0-31's), lane 63's value.
+#define WAVE_SUM_STEP(ctrl, rows)                                                              \
+  do {                                                                                         \
+    const uint32_t lo_ = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, ctrl, rows, \
+                                                               0xf, true);                      \
+    const uint32_t hi_ = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32),    \
+                                                               ctrl, rows, 0xf, true);          \
+    v += (uint64_t)lo_ | ((uint64_t)hi_ << 32);                                                \
+  } while (0)
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
+  WAVE_SUM_STEP(0x111, 0xf);
+  WAVE_SUM_STEP(0x112, 0xf);
+  WAVE_SUM_STEP(0x114, 0xf);
+  WAVE_SUM_STEP(0x118, 0xf);
+  WAVE_SUM_STEP(0x142, 0xa);
+  WAVE_SUM_STEP(0x143, 0xc);
+  return (uint64_t)__builtin_amdgcn_readlane((uint32_t)v, 63) |
+         ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), 63) << 32);
+}
+#undef WAVE_SUM_STEP
+
 // Explicit global (address space 1) accesses: pointers carried in LaunchArgs would otherwise be
 // generic and lower to flat_* instructions (which also count against lgkmcnt).
 typedef __attribute__((address_space(1))) const uint8_t g_u8;
@@ -342,8 +364,8 @@ template <uint32_t WPB = kWavesPerBlock>
 __device__ __forceinline__ void flush_counters(const LaunchArgs& a, const uint64_t (&cnt)[7],
                                                uint64_t retired, uint8_t*, uint32_t lane,
                                                uint32_t) {
-  for (int off = 32; off >= 1; off >>= 1) retired += (uint64_t)__shfl_xor((long long)retired, off);
   if (a.counters == nullptr) return;
+  retired = wave_sum_u64(retired);
   WgCounters* w = wg_counters();
   uint64_t mine = retired;
 #pragma unroll
