@@ -245,3 +245,34 @@ def _cnt(oracle_mod, img, pkts):
             cnt[6] += 1
         cnt[7] += steps
     return cnt
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("config", ["drop", "5tuple"])
+def test_compiled_large_batches(cuda, config):
+    """Batches of several tiles per wave for the compiled fixed-slot kernel (tiles handed out
+    within each workgroup by its LDS counter, interp.hip tile_body) with ragged tails: three
+    launches in a row on one workspace (counted counter shards reused) each equal the tile
+    interpreter, verdicts and counters."""
+    import torch
+
+    from ebpf_emu import Program
+    from ebpf_emu import workloads as W
+    from ebpf_emu.asm import assemble
+
+    prog = Program(assemble(W.PROGRAMS[config]))
+    assert prog.compile()
+    for n in (786432 + 64 * 5 + 7, 2500013):
+        frames = torch.from_numpy(W.frames_fixed(n, 64, n % 7)).to(cuda)
+        ref_cnt = torch.zeros(8, dtype=torch.int64, device=cuda)
+        ref = prog.run(frames, n=n, stride=64, counters=ref_cnt, no_jit=True)
+        torch.cuda.synchronize()
+        ref_v = ref.verdict.cpu().numpy()
+        for rep in range(3):
+            cnt = torch.zeros(8, dtype=torch.int64, device=cuda)
+            got = prog.run(frames, n=n, stride=64, counters=cnt)
+            torch.cuda.synchronize()
+            assert np.array_equal(got.verdict.cpu().numpy(), ref_v), (config, n, rep)
+            assert cnt.cpu().tolist() == ref_cnt.cpu().tolist(), (config, n, rep)
+            assert int(cnt[:7].sum()) == n
+    prog.close()
