@@ -880,12 +880,26 @@ def fixed_dma_db(winb, tag):
     """As fixed_dma, for the double-buffered compiled kernel: a whole tile (the scalar check
     (T0 + 64 <= n), every tile but a batch's last) takes per-lane offsets from %[dmaoff] (lane l:
     (l/4) * stride + its swizzled chunk * 16, computed once per wave) and a scalar tile base --
-    one VALU per round instead of five; a partial tile takes fixed_dma's per-lane checks."""
+    one VALU per round instead of five; a partial tile takes fixed_dma's per-lane checks.
+    64-byte slots: one address and the four 1 KiB rows by the instruction offset, which the
+    LDS-DMA adds to both the global and the LDS address."""
     return f"""s_add_u32 {{T5L}}, {{T0L}}, 64
 s_addc_u32 {{T5H}}, {{T0H}}, 0
 s_sub_u32 {{T5L}}, {{KNL}}, {{T5L}}
 s_subb_u32 {{T5H}}, {{KNH}}, {{T5H}}
 s_cbranch_scc1 .Lpart{tag}%=
+s_cmp_eq_u64 {{KST}}, 64
+s_cbranch_scc0 .Lgen{tag}%=
+s_lshl_b64 {{T7}}, {{T0}}, 6
+s_add_u32 {{T7L}}, {{T7L}}, {{KFRL}}
+s_addc_u32 {{T7H}}, {{T7H}}, {{KFRH}}
+v_lshl_add_u64 {{T1213}}, %[dmaoff], 0, {{T7}}
+s_mov_b32 m0, {winb}
+s_nop 0
+""" + "\n".join(f"global_load_lds_dwordx4 {{T1213}}, off offset:{1024 * r} ; @DMAPOLICY@"
+                for r in range(4)) + f"""
+s_branch .Ldmaok{tag}%=
+.Lgen{tag}%=:
 s_mul_i32 {{T7L}}, {{T0L}}, {{KSTL}}
 s_mul_hi_u32 {{T7H}}, {{T0L}}, {{KSTL}}
 s_mul_i32 {{T5L}}, {{T0L}}, {{KSTH}}
