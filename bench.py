@@ -49,7 +49,10 @@ def parse():
                          " = 100000000), sharded over the ranks in seeded 1Mi-packet chunks")
     ap.add_argument("--pool-mib", type=int, default=512, help="min bytes of distinct batches")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0=skip)")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, affinity)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="0 = every CPU this process may use (affinity, capped by the cgroup quota)")
+    ap.add_argument("--cpu-seconds-1core", type=float, default=4.0,
+                    help="single-thread CPU baseline budget (0 = skip)")
     ap.add_argument("--no-counters", action="store_true", help="A/B: verdicts only")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC traffic summary (profiles/*.json) to report as roofline.traffic")
@@ -151,7 +154,9 @@ def main():
     # ---- timed region: barrier + sync on both sides, K steps, max over ranks ----
     # HIP events on the launch stream: one pair around the K back-to-back batches (a batch =
     # every launch of one ebpf_run_batch), so the per-batch time includes the dispatch gaps
-    # between launches but no event packets between them
+    # between launches but no event packets between them. The host waits for the last event by
+    # polling it (a blocking synchronize sleeps and wakes tens of us late, which at K = 20 steps
+    # of ~15 us was ~9 % of the wall clock); the synchronize after it then returns at once.
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
     if world > 1:
@@ -163,6 +168,8 @@ def main():
         step(i)
     t_enq = time.perf_counter() - t0  # host time to enqueue the K steps (launch-bound check)
     ev1.record(stream)
+    while not ev1.query():
+        pass
     D.reduce_counters(counters)  # the one exchange step: per-verdict counters, RCCL / xGMI
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -180,7 +187,10 @@ def main():
     if not args.no_counters:
         assert sum(cnt[:7]) == total_pkts, (cnt, total_pkts)  # every packet: exactly one verdict
     mpps = total_pkts / elapsed / 1e6
+    # the dominant kernel's rate from its HIP-event time (rocprof's per-kernel average agrees),
+    # and the same bytes over the wall-clock step time that `value` uses
     achieved_gbs = algo_bytes / (kern_avg_ms * 1e-3) / 1e9
+    wall_gbs = algo_bytes * args.steps / elapsed / 1e9
 
     traffic = None
     tj = args.traffic_json or os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
@@ -224,6 +234,9 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved_gbs / HBM_PEAK_GBS, 5),
                 "traffic": traffic,
+                # the wall-clock view of the same launches (value's time base): GB/s and fraction
+                "achieved_wall": round(wall_gbs, 2),
+                "frac_wall": round(wall_gbs / HBM_PEAK_GBS, 5),
                 "algo_bytes_per_launch": algo_bytes,
                 "kernel_avg_us": round(kern_avg_ms * 1e3, 3),
                 # HIP events bracket one whole batch: one interpreter launch (with counters, its
@@ -233,6 +246,8 @@ def main():
             "counters": {"drop": cnt[1], "pass": cnt[2], "other": cnt[5], "faults": cnt[6],
                          "insns_retired": cnt[7]},
             "ebpf_insns_per_s": round(cnt[7] / elapsed, 1),
+            # device-resident rate from the HIP-event time of the K steps (no host launch / sync)
+            "value_device": round((args.total_packets or n * world) / (kern_avg_ms * 1e-3) / 1e6, 2),
             "host_enqueue_us_per_step": round(t_enq / args.steps * 1e6, 3),
             "cpu_baseline": cpu,
         }
@@ -255,38 +270,78 @@ def kernel_name(prog):
     return f"ebpfemu::interp_kernel<{prog.tier}>"
 
 
+def host_cpus():
+    """CPUs this process may use: its affinity set, capped by a cgroup v2 CPU quota (on the GPU
+    box os.cpu_count() / nproc show the whole machine, while the box's share is smaller)."""
+    n = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(period)))
+    except (OSError, ValueError):
+        pass
+    return (min(n, quota) if quota else n), n, quota
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(args, img, batch0, mixed, n, mem_size, r10):
-    """The C oracle ("port" of the reference semantics) on host cores over a bounded sample."""
+    """The C oracle ("port" of the reference semantics) on host cores over a bounded sample:
+    every usable core (static contiguous partitions, std::thread-style pthreads inside
+    or_run_batch), then one core."""
     import numpy as np
 
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
 
-    threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
+    usable, affinity, quota = host_cpus()
+    threads = args.cpu_threads or usable
     op = oracle.Program(img)
     frames = batch0["frames"].cpu().numpy()
-    kw = dict(mem_size=mem_size, r10=r10, threads=threads)
     if mixed:
         offs = batch0["offsets"].cpu().numpy().view(np.uint32)
         lens = batch0["lens"].cpu().numpy().view(np.uint16)
-    chunk = 1 << 16 if mixed else n
-    done = 0
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < args.cpu_seconds:
-        if mixed:
+    stride = (max(64, args.frame_bytes) + 15) // 16 * 16
+
+    def rate(nthreads, seconds):
+        kw = dict(mem_size=mem_size, r10=r10, threads=nthreads)
+        # chunks sized to ~0.2 s of work so the time budget is met closely
+        chunk = max(4096, min(n, int((1 << 14 if mixed else 1 << 20) * nthreads / 8)))
+        done = 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < seconds:
             lo = done % n
             hi = min(n, lo + chunk)
-            o = offs[lo:hi]
-            op.run_batch(frames, hi - lo, offsets=o, lens=lens[lo:hi], **kw)
+            if mixed:
+                op.run_batch(frames, hi - lo, offsets=offs[lo:hi], lens=lens[lo:hi], **kw)
+            else:
+                op.run_batch(frames[lo * stride:hi * stride], hi - lo, stride=stride, **kw)
             done += hi - lo
-        else:
-            op.run_batch(frames, n, stride=(max(64, args.frame_bytes) + 15) // 16 * 16, **kw)
-            done += n
-    dt = time.perf_counter() - t0
-    return {"value": round(done / dt / 1e6, 3), "unit": "Mpkt/s", "cores": threads,
-            "kind": "port",
-            "sample": f"{done} packets of the same workload ({'mixed' if mixed else '64B'} frames), "
-                      f"{dt:.1f} s, C oracle (oracle/ebpf_oracle.c) with {threads} threads"}
+        dt = time.perf_counter() - t0
+        return done / dt / 1e6, done, dt
+
+    v, done, dt = rate(threads, args.cpu_seconds)
+    out = {"value": round(v, 3), "unit": "Mpkt/s", "cores": threads, "kind": "port",
+           "sample": f"{done} packets of the same workload ({'mixed' if mixed else '64B'} frames), "
+                     f"{dt:.1f} s, C oracle (oracle/ebpf_oracle.c) with {threads} threads",
+           "nproc": os.cpu_count(), "affinity_cpus": affinity, "cgroup_cpus": quota,
+           "cpu_model": cpu_model()}
+    if args.cpu_seconds_1core > 0:
+        v1, done1, dt1 = rate(1, args.cpu_seconds_1core)
+        out["value_1core"] = round(v1, 3)
+        out["sample_1core"] = f"{done1} packets, {dt1:.1f} s, one thread"
+    return out
 
 
 if __name__ == "__main__":

@@ -1,6 +1,6 @@
 // emem.cpp — bpf_conformance plugin CLI, byte-for-byte the reference's protocol (src/main.rs):
 //   emem [<memory hex>]            program hex on one stdin line
-//   emem <ignored> <program hex>   when the stdin line is blank (main.rs:65-69)
+//   emem <ignored> <program hex>   when the stdin line is blank (main.rs:33-37)
 // prints r0 as lowercase hex without padding (main.rs:43: "{:x}" of i64 = two's complement).
 // The single execution runs on the GPU through libebpfemu.so (a batch of one packet).
 // Where the reference panics (exit code 101) this CLI prints the reason to stderr and exits 101.

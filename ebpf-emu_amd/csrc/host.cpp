@@ -778,7 +778,7 @@ int ebpf_prog_upload(ebpf_prog* p, int device) {
 // lens).
 static bool use_binning(const ebpf_prog* p, const ebpf_batch* b) {
   const bool ol = (b->offsets && b->lens) || (b->flags & EBPF_BATCH_XDP_MD);
-  if (p->ltuops.empty() || !ol || (b->flags & EBPF_BATCH_GENERIC)) return false;
+  if (p->ltuops.empty() || !ol || (b->flags & EBPF_BATCH_GENERIC) || b->init_fp_len) return false;
   return g_bin >= 0 ? g_bin == 1 : b->n >= kBinMinPackets;
 }
 
@@ -794,16 +794,22 @@ static uint64_t xdp_region_bytes(const ebpf_batch* b) {
   return align16(b->n * 4) + align16(b->n * 2) + xdp_image_bytes(b);
 }
 
+// The memory tier a batch runs at: a caller-set frame stack needs the general interpreter's call
+// stack (an EXIT pops it), whatever the program.
+static int batch_tier(const ebpf_prog* p, const ebpf_batch* b) {
+  return p->tier == 1 || b->init_fp_len ? 1 : 0;
+}
+
 uint64_t ebpf_workspace_bytes(const ebpf_prog* p, const ebpf_batch* b, int device) {
   if (!p || !b) return 0;
   const uint64_t x = (b->flags & EBPF_BATCH_XDP_MD) ? xdp_region_bytes(b) : 0;
   uint64_t bytes = kWsSlotsOff + x;
   if (use_binning(p, b)) bytes += b->n * 4;  // the binned packet order
-  if (p->tier == 1) {
+  if (batch_tier(p, b) == 1) {
     int cur = device_of_current();
     hipSetDevice(device);
     int grid = 0;
-    interp_grid(p->tier, (uint32_t)p->uops.size(), p->tiny, (b->n + 63) / 64, &grid);
+    interp_grid(kKindTier1, (uint32_t)p->uops.size(), p->tiny, (b->n + 63) / 64, &grid);
     hipSetDevice(cur);
     bytes += (uint64_t)grid * kWavesPerBlock * tier1_slot_bytes(b->mem_size);
   }
@@ -812,7 +818,8 @@ uint64_t ebpf_workspace_bytes(const ebpf_prog* p, const ebpf_batch* b, int devic
 
 static int check_batch(const ebpf_batch* b) {
   if (!b) return EBPF_EINVAL;
-  if (b->mem_size < 8 || b->mem_size % 8 || b->mem_size > (1u << 24)) return EBPF_EINVAL;
+  if (b->mem_size > (1u << 24)) return EBPF_EINVAL;
+  if (b->init_fp_len > EBPF_MAX_CALL_DEPTH || (b->init_fp_len && !b->init_fp)) return EBPF_EINVAL;
   if (b->max_steps == 0) return EBPF_EINVAL;
   if (b->n && !b->frames) return EBPF_EINVAL;
   if (!b->offsets && b->stride == 0 && !b->lens) return EBPF_EINVAL;
@@ -846,10 +853,10 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* bin, const ebpf_batch_out* ou
   const uint64_t n_tiles = (b->n + 63) / 64;
   // dag_kernel needs no step budget: a lane of a forward-only program retires <= n_uops steps
   // the tile kernel in loop mode: loops, or a step budget that can bind (exact budget)
-  const bool generic = g_no_dag || (b->flags & EBPF_BATCH_GENERIC);
+  const bool generic = g_no_dag || (b->flags & EBPF_BATCH_GENERIC) || b->init_fp_len;
   const int kind = (p->dev_duops[device] && b->max_steps >= p->uops.size() && !generic) ? kKindDag
                    : (p->dev_ltuops[device] && !generic && !g_no_loop)            ? kKindLoop
-                                                                                   : p->tier;
+                                                                                   : batch_tier(p, b);
   int grid = 0;
   if (interp_grid(kind, (uint32_t)p->uops.size(), p->tiny, n_tiles, &grid) != 0) {
     if (cur != device) hipSetDevice(cur);
@@ -940,6 +947,16 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* bin, const ebpf_batch_out* ou
                                           (kTraceWaves * kTraceSlots);
   }
   a.regs_out = out->regs;
+  a.init_fp = b->init_fp;
+  a.init_fp_len = b->init_fp_len;
+  a.fp_out = out->fp;
+  a.fp_len_out = out->fp_len;
+  // only the tier-1 kernel has a frame stack; every other kernel runs programs without CALL and
+  // with an empty initial stack, whose final stack is empty
+  if (kind != kKindTier1 && out->fp_len && hipMemsetAsync(out->fp_len, 0, b->n, s) != hipSuccess) {
+    if (cur != device) hipSetDevice(cur);
+    return EBPF_EHIP;
+  }
   if (kind == kKindLoop && use_binning(p, b)) {
     a.perm = (const uint32_t*)(ws + kWsSlotsOff);
     a.bin_counts = (uint32_t*)(ws + kWsBinCountsOff);
@@ -963,15 +980,44 @@ int ebpf_run_batch_multi(ebpf_prog* p, int nshards, const int* devices, const eb
                          const ebpf_batch_out* outs, ebpf_stream_t const* streams) {
   if (!p || nshards <= 0 || nshards > kMaxDevices || !devices || !batches || !outs || !streams)
     return EBPF_EINVAL;
-  for (int s = 0; s < nshards; s++)
-    if (!outs[s].counters || !streams[s]) return EBPF_EINVAL;
+  for (int s = 0; s < nshards; s++) {
+    if (!outs[s].counters || !streams[s] || devices[s] < 0 || devices[s] >= kMaxDevices)
+      return EBPF_EINVAL;
+    for (int t = 0; t < s; t++)
+      if (devices[t] == devices[s]) return EBPF_EINVAL;  // one communicator rank per device
+  }
   int cur = device_of_current();
+  // Each shard's counters go to a library-owned per-device scratch u64[8] (zeroed on the shard's
+  // stream), the scratch words are all-reduced, and the global totals are then ADDED to every
+  // outs[s].counters: the caller's counters accumulate, as ebpf_run_batch's do (the header's
+  // contract). A failing shard leaves every caller counter untouched.
+  static std::mutex smu;
+  static std::map<std::pair<int, void*>, uint64_t*> scratch;  // per (device, stream)
+  std::vector<ebpf_batch_out> o(outs, outs + nshards);
+  for (int s = 0; s < nshards; s++) {
+    const int d = devices[s];
+    if (hipSetDevice(d) != hipSuccess) { hipSetDevice(cur); return EBPF_EHIP; }
+    uint64_t* sc = nullptr;
+    {
+      std::lock_guard<std::mutex> lk(smu);
+      uint64_t*& slot = scratch[{d, (void*)streams[s]}];
+      if (!slot && hipMalloc(&slot, EBPF_NCOUNTERS * sizeof(uint64_t)) != hipSuccess) {
+        slot = nullptr;
+        hipSetDevice(cur);
+        return EBPF_ENOMEM;
+      }
+      sc = slot;
+    }
+    o[s].counters = sc;
+    if (hipMemsetAsync(sc, 0, EBPF_NCOUNTERS * sizeof(uint64_t), (hipStream_t)streams[s]) != hipSuccess) {
+      hipSetDevice(cur);
+      return EBPF_EHIP;
+    }
+  }
   // per-shard launches: independent, no data-path exchange
   for (int s = 0; s < nshards; s++) {
-    if (hipSetDevice(devices[s]) != hipSuccess) return EBPF_EHIP;
-    hipMemsetAsync(outs[s].counters, 0, EBPF_NCOUNTERS * sizeof(uint64_t),
-                   (hipStream_t)streams[s]);
-    int rc = ebpf_run_batch(p, &batches[s], &outs[s], streams[s]);
+    hipSetDevice(devices[s]);
+    int rc = ebpf_run_batch(p, &batches[s], &o[s], streams[s]);
     if (rc) { hipSetDevice(cur); return rc; }
   }
   // the one exchange step: sum the counters across GPUs over RCCL / xGMI
@@ -995,14 +1041,20 @@ int ebpf_run_batch_multi(ebpf_prog* p, int nshards, const int* devices, const eb
   if (ncclGroupStart() != ncclSuccess) { hipSetDevice(cur); return EBPF_ERCCL; }
   for (int s = 0; s < nshards; s++) {
     hipSetDevice(devices[s]);
-    if (ncclAllReduce(outs[s].counters, outs[s].counters, EBPF_NCOUNTERS, ncclUint64, ncclSum,
-                      (*cs)[s], (hipStream_t)streams[s]) != ncclSuccess) {
+    if (ncclAllReduce(o[s].counters, o[s].counters, EBPF_NCOUNTERS, ncclUint64, ncclSum, (*cs)[s],
+                      (hipStream_t)streams[s]) != ncclSuccess) {
       ncclGroupEnd();
       hipSetDevice(cur);
       return EBPF_ERCCL;
     }
   }
-  int rc = ncclGroupEnd() == ncclSuccess ? EBPF_OK : EBPF_ERCCL;
+  if (ncclGroupEnd() != ncclSuccess) { hipSetDevice(cur); return EBPF_ERCCL; }
+  int rc = EBPF_OK;
+  for (int s = 0; s < nshards && rc == EBPF_OK; s++) {
+    hipSetDevice(devices[s]);
+    if (launch_counters_add(o[s].counters, outs[s].counters, (hipStream_t)streams[s]) != hipSuccess)
+      rc = EBPF_EHIP;
+  }
   hipSetDevice(cur);
   return rc;
 }

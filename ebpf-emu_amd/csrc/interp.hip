@@ -200,6 +200,17 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
   return rfl((uint32_t)(uintptr_t)(__attribute__((address_space(3))) const void*)p);
 }
 
+// Dword d of a final image (mem_out row of mem_size bytes, any length): one dword store when the
+// row is dword-aligned, else its in-bounds bytes one by one (the reference's Mmu.memory is a Vec<u8>
+// of any length, mmu.rs:2-4).
+__device__ __forceinline__ void put_image(uint8_t* row, uint32_t d, uint32_t v, uint32_t mem_size) {
+  if ((mem_size & 3) == 0) {
+    ((uint32_t*)row)[d] = v;
+    return;
+  }
+  for (uint32_t i = 0; i < 4 && d * 4 + i < mem_size; i++) row[d * 4 + i] = (uint8_t)(v >> (8 * i));
+}
+
 // ---- tier-1 image: lane-interleaved dwords, dword d of this lane at img[d * 64] ----
 __device__ __forceinline__ uint64_t img_read(const uint32_t* img, uint32_t a, uint32_t w) {
   const uint32_t* p = img + (size_t)(a >> 2) * kWave;
@@ -439,7 +450,7 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
   uint32_t* const img = TIER == 1
       ? (uint32_t*)(a.image_ws + wave_slot * tier1_slot_bytes(mem_size)) + lane
       : nullptr;
-  uint32_t* const cstack = TIER == 1 ? img + (size_t)(mem_size / 4) * kWave : nullptr;
+  uint32_t* const cstack = TIER == 1 ? img + (size_t)((mem_size + 3) / 4) * kWave : nullptr;
 
   uint64_t cnt[7] = {0, 0, 0, 0, 0, 0, 0};  // wave-uniform verdict buckets + faults
   uint64_t retired = 0;                     // per lane
@@ -511,10 +522,13 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
       pc = PC_DONE;
     }
     if (TIER == 1) {
-      const uint32_t md = mem_size / 4;
+      const uint32_t md = (mem_size + 3) / 4;
       const uint32_t m = (pc != PC_DONE) ? len : 0u;
       for (uint32_t d = 0; d < md; d++)
         img[(size_t)d * kWave] = (d * 4 < m) ? (uint32_t)pkt_read(base, d * 4, 4, len) : 0u;
+      // the caller's initial frame stack (Emu.fp, emu.rs:26): an EXIT pops it (emu.rs:273-279)
+      csp = a.init_fp_len;
+      for (uint32_t i = 0; i < csp; i++) cstack[(size_t)i * kWave] = a.init_fp[i];
     }
 
     if (TIER == 0) {
@@ -801,16 +815,21 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
     // ---- outputs: r0 (main.rs:43), status, verdict (xdp.rs:3-9), final image ----
     const uint64_t r0v = RF_GET(0);
     if (a.mem_out && valid) {
-      uint32_t* mo = (uint32_t*)(a.mem_out + pkt * (uint64_t)mem_size);
+      uint8_t* mo = a.mem_out + pkt * (uint64_t)mem_size;
       const uint32_t m = min(len, mem_size);
-      for (uint32_t d = 0; d < mem_size / 4; d++) {
+      for (uint32_t d = 0; d < (mem_size + 3) / 4; d++) {
         uint32_t v;
         if (TIER == 1) v = img[(size_t)d * kWave];
         else if (d * 4 >= m) v = 0u;
         else if (d * 4 < (uint32_t)kWin) v = (uint32_t)win_read(my_win, my_swz, d * 4, 4, len);
         else v = (uint32_t)pkt_read(base, d * 4, 4, len);
-        mo[d] = v;
+        put_image(mo, d, v, mem_size);
       }
+    }
+    if (TIER == 1 && valid && a.fp_len_out) {  // the final frame stack (Emu.fp)
+      a.fp_len_out[pkt] = (uint8_t)csp;
+      if (a.fp_out)
+        for (uint32_t i = 0; i < csp; i++) a.fp_out[pkt * kCallDepth + i] = cstack[(size_t)i * kWave];
     }
     if (a.regs_out && valid) {
 #pragma unroll
@@ -1108,14 +1127,14 @@ __global__ __launch_bounds__(kBlock) void dag_kernel(LaunchArgs a) {
     // ---- outputs: r0 (main.rs:43), status, verdict (xdp.rs:3-9), final image/registers ----
     const uint64_t r0v = rget(rl, 0);
     if (a.mem_out && valid) {
-      uint32_t* mo = (uint32_t*)(a.mem_out + pkt * (uint64_t)mem_size);
+      uint8_t* mo = a.mem_out + pkt * (uint64_t)mem_size;
       const uint32_t m = min(len, mem_size);
-      for (uint32_t d = 0; d < mem_size / 4; d++) {
+      for (uint32_t d = 0; d < (mem_size + 3) / 4; d++) {
         uint32_t v;
         if (d * 4 >= m) v = 0u;
         else if (d * 4 < (uint32_t)kWin) v = (uint32_t)win_read(my_win, my_swz, d * 4, 4, len);
         else v = (uint32_t)pkt_read(base, d * 4, 4, len);
-        mo[d] = v;
+        put_image(mo, d, v, mem_size);
       }
     }
     if (a.regs_out && valid) {
@@ -1448,15 +1467,15 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
         const uint32_t len = ml;
         const uint8_t* base = (const uint8_t*)mb;
         const uint32_t mem_size = a.mem_size;
-        uint32_t* mo = (uint32_t*)(a.mem_out + pk * (uint64_t)mem_size);
+        uint8_t* mo = a.mem_out + pk * (uint64_t)mem_size;
         const uint32_t m = min(len, mem_size);
-        for (uint32_t d = 0; d < mem_size / 4; d++) {
+        for (uint32_t d = 0; d < (mem_size + 3) / 4; d++) {
           uint32_t v;
           if (d * 4 >= m) v = 0u;
           else if (!LOOPS && d * 4 < (uint32_t)kWin)  // (loop mode may have moved the window)
             v = (uint32_t)win_read(L.win + ln * kWin, win_swz(ln), d * 4, 4, len);
           else v = (uint32_t)pkt_read(base, d * 4, 4, len);
-          mo[d] = v;
+          put_image(mo, d, v, mem_size);
         }
       }
     }
@@ -1526,6 +1545,18 @@ __global__ __launch_bounds__(kCounterShards * 8) void fold_counters(uint64_t* sh
     for (int i = threadIdx.x; i < kCounterShards * 8; i += 8) t += fold[i];
     if (t) atomicAdd((unsigned long long*)&counters[threadIdx.x], (unsigned long long)t);
   }
+}
+
+// Adds src[0..7] into dst[0..7] (ebpf_run_batch_multi: the all-reduced totals of one call into the
+// caller's counters, which are accumulated, never overwritten).
+__global__ __launch_bounds__(64) void counters_add(const uint64_t* src, uint64_t* dst) {
+  if (threadIdx.x < EBPF_NCOUNTERS && src[threadIdx.x])
+    atomicAdd((unsigned long long*)&dst[threadIdx.x], (unsigned long long)src[threadIdx.x]);
+}
+
+hipError_t launch_counters_add(const uint64_t* src, uint64_t* dst, hipStream_t stream) {
+  hipLaunchKernelGGL(counters_add, dim3(1), dim3(64), 0, stream, src, dst);
+  return hipGetLastError();
 }
 
 // Counter fold: in-kernel with counted shard words (default), or fold_counters after the launch
@@ -1692,9 +1723,13 @@ hipError_t launch_interp(int kind, const LaunchArgs& a, int grid, hipStream_t st
                          const JitFns* jit) {
   const uint32_t lds = lds_bytes_for(kind, a.n_uops);
   LaunchArgs b = a;
-  // a shard word's sum must stay below 2^48: bound it by packets x steps per packet
+  // a shard word's sum must stay below 2^48: bound it by packets x steps per packet; and its
+  // arrival count (16 bits) must reach the shard's workgroups - 1: at most 65535 members (the
+  // compiled fixed-slot kernel's grid is one workgroup per CU, every other grid is `grid`)
   const uint64_t steps = kind == kKindDag ? (uint64_t)a.n_uops : a.max_steps;
-  const bool fits = a.n < (1ull << 40) && steps < (1ull << 47) / (a.n + 1);
+  const uint64_t members = ((uint64_t)grid + kCounterShards - 1) / kCounterShards;
+  const bool fits = a.n < (1ull << 40) && steps < (1ull << 47) / (a.n + 1) &&
+                    members < (1ull << (64 - kShardCountShift));
   const bool fold_kernel = g_fold_mode >= 0 ? (g_fold_mode == 1 || !fits) : !fits;
   b.fold_kernel = fold_kernel ? 1u : 0u;
   void* bargs[] = {(void*)&b};

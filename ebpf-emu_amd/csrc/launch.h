@@ -65,6 +65,10 @@ struct LaunchArgs {
   uint32_t* bin_counts;       // with perm: bin counts + cursors, zeroed again by the tile kernel
   uint64_t* trace;            // diagnostics (EBPFEMU_TRACE=1): per-wave s_memrealtime stamps of
                               // the compiled fixed-slot kernel, kTraceSlots per wave; else null
+  const uint32_t* init_fp;    // tier-1 kernel: initial frame stack (Emu.fp, emu.rs:26), bottom first
+  uint32_t init_fp_len;       //   its depth (<= kCallDepth)
+  uint32_t* fp_out;           // tier-1 kernel: optional [n][kCallDepth] final frame stacks
+  uint8_t* fp_len_out;        //   optional [n] their depths
 };
 
 constexpr int kTraceSlots = 16;
@@ -73,7 +77,7 @@ constexpr int kTraceRing = 4;  // launches kept (consecutive launches' gaps)
 
 // Bytes of tier-1 scratch per wave slot: lane-interleaved image dwords + call stack.
 __host__ __device__ inline uint64_t tier1_slot_bytes(uint32_t mem_size) {
-  return (uint64_t)(mem_size / 4 + kCallDepth) * kWave * 4;
+  return (uint64_t)((mem_size + 3) / 4 + kCallDepth) * kWave * 4;
 }
 
 // Programs this short with no back edge do a fixed, tiny amount of work per tile.
@@ -99,6 +103,9 @@ hipError_t launch_xdp_stage(const uint8_t* frames, const uint32_t* offsets, cons
                             uint64_t stride, uint64_t n, uint32_t mem_size, uint8_t* dst,
                             uint32_t* doffs, uint16_t* dlens, unsigned long long* cursor,
                             hipStream_t stream);
+
+// dst[0..7] += src[0..7] on `stream` (one tiny kernel).
+hipError_t launch_counters_add(const uint64_t* src, uint64_t* dst, hipStream_t stream);
 
 // Enqueue the interpreter on `stream`; with counters, its last workgroup folds the shards into them.
 // jit: the program's compiled kernels, launched instead of the tile interpreter where it would run.

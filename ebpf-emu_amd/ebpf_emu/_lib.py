@@ -41,12 +41,14 @@ class Batch(ctypes.Structure):  # ebpf_batch
                 ("mem_size", ctypes.c_uint32), ("flags", ctypes.c_uint32),
                 ("r10", ctypes.c_uint64), ("max_steps", ctypes.c_uint64),
                 ("workspace", ctypes.c_void_p), ("workspace_bytes", ctypes.c_uint64),
-                ("init_regs", ctypes.c_void_p)]
+                ("init_regs", ctypes.c_void_p), ("init_fp", ctypes.c_void_p),
+                ("init_fp_len", ctypes.c_uint32)]
 
 
 class BatchOut(ctypes.Structure):  # ebpf_batch_out
     _fields_ = [("verdict", ctypes.c_void_p), ("r0", ctypes.c_void_p), ("status", ctypes.c_void_p),
-                ("counters", ctypes.c_void_p), ("mem", ctypes.c_void_p), ("regs", ctypes.c_void_p)]
+                ("counters", ctypes.c_void_p), ("mem", ctypes.c_void_p), ("regs", ctypes.c_void_p),
+                ("fp", ctypes.c_void_p), ("fp_len", ctypes.c_void_p)]
 
 
 class EbpfError(RuntimeError):

@@ -62,26 +62,41 @@ class Emu:  # emu.rs:19-45
         self.device = device
 
     def run(self) -> None:
-        """Emu::run (emu.rs:452-458): one execution on the GPU."""
+        """Emu::run (emu.rs:452-458): one execution on the GPU, on the caller's state -- the
+        memory image of any length (Mmu.memory: Vec<u8>, mmu.rs:2-4), the registers and the frame
+        stack `fp` (emu.rs:26); all three are written back."""
+        import numpy as np
         import torch
 
         from .program import Program
 
         mem = bytes(self.state.mmu.memory)
-        if len(mem) < 8 or len(mem) % 8:
-            raise ValueError("device images are a multiple of 8 bytes (>= 8)")
-        if self.fp:
-            raise ValueError("a non-empty initial frame stack is not supported")
+        if len(self.fp) > _lib.MAX_CALL_DEPTH:
+            raise ValueError(f"frame stack deeper than {_lib.MAX_CALL_DEPTH}")
         prog = Program(encode_instructions(self.instructions))
         dev = torch.device("cuda", self.device)
-        frames = torch.tensor(list(mem), dtype=torch.uint8, device=dev)
+        # the image as one packet of its own length: [0, len) = the image, nothing past it
+        frames = torch.tensor(list(mem) or [0], dtype=torch.uint8, device=dev)
+        if mem:
+            layout = dict(stride=len(mem))
+        else:  # an empty image: one zero-length packet
+            layout = dict(offsets=torch.zeros(1, dtype=torch.int32, device=dev),
+                          lens=torch.zeros(1, dtype=torch.int16, device=dev))
         regs = torch.tensor([_s64(r) for r in self.state.regs], dtype=torch.int64, device=dev)
-        res = prog.run(frames, n=1, stride=len(mem), mem_size=len(mem), init_regs=regs,
-                       max_steps=self.max_steps, verdict=False, status=True, mem=True, regs=True)
+        init_fp = None
+        if self.fp:
+            init_fp = torch.from_numpy(np.array([int(x) & 0xFFFFFFFF for x in self.fp],
+                                                dtype=np.uint32).view(np.int32)).to(dev)
+        res = prog.run(frames, n=1, mem_size=len(mem), init_regs=regs, **layout,
+                       max_steps=self.max_steps, verdict=False, status=True, mem=len(mem) > 0,
+                       regs=True, init_fp=init_fp, fp=True)
         torch.cuda.synchronize(dev)
         st = int(res.status[0].item())
         self.state.regs = [_s64(v) for v in res.regs[0].tolist()]
-        self.state.mmu.memory = bytearray(bytes(res.mem[0].cpu().numpy().tobytes()))
+        if len(mem):
+            self.state.mmu.memory = bytearray(bytes(res.mem[0].cpu().numpy().tobytes()))
+        depth = int(res.fp_len[0].item())
+        self.fp = [int(v) & 0xFFFFFFFF for v in res.fp[0, :depth].tolist()]
         prog.close()
         if st != _lib.ST_OK:
             raise EmuPanic(st)

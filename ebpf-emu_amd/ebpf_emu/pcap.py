@@ -128,6 +128,12 @@ class Capture:
             o.counters = counters.data_ptr()
             outs.append(o)
         s_in, s_k, s_out = (torch.cuda.Stream(dev) for _ in range(3))
+        # the buffers and the counters were allocated / zeroed on the current stream: the side
+        # streams start after that work (the caching allocator may also have handed back memory
+        # that pending current-stream work still uses)
+        cur = torch.cuda.current_stream(dev)
+        for st in (s_in, s_k, s_out):
+            st.wait_stream(cur)
         ev_in = [torch.cuda.Event() for _ in chunks]
         ev_k = [torch.cuda.Event() for _ in chunks]
         ev_out = [torch.cuda.Event() for _ in chunks]

@@ -23,6 +23,8 @@ class BatchResult:
     counters: object = None  # torch.int64 [8] (u64 bits), accumulated
     mem: object = None       # torch.uint8 [n, mem_size]
     regs: object = None      # torch.int64 [n, 11]
+    fp: object = None        # torch.int32 [n, 64] (u32 bits): final frame stacks, bottom first
+    fp_len: object = None    # torch.uint8 [n]: their depths
 
 
 def _ptr(t):
@@ -105,7 +107,7 @@ class Program:
                    mem_size: int = _lib.DEFAULT_MEM, r10: int = _lib.DEFAULT_R10,
                    max_steps: int = _lib.DEFAULT_STEPS, init_regs=None,
                    workspace=None, generic: bool = False, xdp_md: bool = False,
-                   no_jit: bool = False) -> _lib.Batch:
+                   no_jit: bool = False, init_fp=None) -> _lib.Batch:
         b = _lib.Batch()
         _lib.lib().ebpf_batch_init(ctypes.byref(b))
         if n is None:
@@ -119,6 +121,9 @@ class Program:
         b.r10 = r10 & ((1 << 64) - 1)
         b.max_steps = max_steps
         b.init_regs = init_regs.data_ptr() if init_regs is not None else None
+        if init_fp is not None and init_fp.numel():
+            b.init_fp = init_fp.data_ptr()
+            b.init_fp_len = init_fp.numel()
         b.flags = ((_lib.BATCH_GENERIC if generic else 0) | (_lib.BATCH_XDP_MD if xdp_md else 0) |
                    (_lib.BATCH_NO_JIT if no_jit else 0))
         if workspace is not None:
@@ -144,7 +149,8 @@ class Program:
             max_steps: int = _lib.DEFAULT_STEPS, init_regs=None, verdict: bool = True,
             r0: bool = False, status: bool = False, counters=None, mem: bool = False,
             regs: bool = False, stream=None, generic: bool = False,
-            xdp_md: bool = False, no_jit: bool = False) -> BatchResult:
+            xdp_md: bool = False, no_jit: bool = False, init_fp=None,
+            fp: bool = False) -> BatchResult:
         """Run the program over a device-resident batch; returns device tensors.
 
         frames: torch.uint8 CUDA tensor. Layout: packet i at frames[i*stride:] (stride layout,
@@ -152,6 +158,8 @@ class Program:
         lens: torch.int16/uint16 bits). counters: an optional torch.int64 [8] tensor to add to.
         generic: run on the general interpreter even if the forward-jump fast path applies.
         no_jit: run a compiled program (compile()) on the tile interpreter instead.
+        init_fp: an optional device int32 tensor, the initial frame stack (Emu.fp, emu.rs:26) of
+        every packet, bottom first; fp: return the final frame stacks (res.fp, res.fp_len).
         xdp_md: the xdp_md calling convention (EBPF_BATCH_XDP_MD): each image is
         [u32 data = 8][u32 data_end = 8 + len][packet], r1 = 0 the ctx, r2 = 8 + len.
         """
@@ -159,7 +167,7 @@ class Program:
 
         dev = frames.device
         b = self.make_batch(frames, n, stride, offsets, lens, mem_size, r10, max_steps, init_regs,
-                            generic=generic, xdp_md=xdp_md, no_jit=no_jit)
+                            generic=generic, xdp_md=xdp_md, no_jit=no_jit, init_fp=init_fp)
         n = b.n
         res = BatchResult()
         if verdict:
@@ -172,6 +180,9 @@ class Program:
             res.mem = torch.empty((n, mem_size), dtype=torch.uint8, device=dev)
         if regs:
             res.regs = torch.empty((n, 11), dtype=torch.int64, device=dev)
+        if fp:
+            res.fp = torch.zeros((n, _lib.MAX_CALL_DEPTH), dtype=torch.int32, device=dev)
+            res.fp_len = torch.empty(n, dtype=torch.uint8, device=dev)
         res.counters = counters
         out = _lib.BatchOut()
         out.verdict = res.verdict.data_ptr() if verdict else None
@@ -180,6 +191,8 @@ class Program:
         out.counters = counters.data_ptr() if counters is not None else None
         out.mem = res.mem.data_ptr() if mem else None
         out.regs = res.regs.data_ptr() if regs else None
+        out.fp = res.fp.data_ptr() if fp else None
+        out.fp_len = res.fp_len.data_ptr() if fp else None
         with torch.cuda.device(dev):
             self.launch(b, out, stream)
         return res

@@ -96,7 +96,8 @@ typedef struct ebpf_batch {
   uint64_t stride;          /* bytes between packets in the stride layout, where frames must hold
                                n * stride bytes (every slot whole, as in a ring of fixed slots) */
   uint64_t n;               /* packets */
-  uint32_t mem_size;        /* bytes of the per-packet memory image (multiple of 8, >= 8) */
+  uint32_t mem_size;        /* bytes of the per-packet memory image, 0..2^24 (any length: Mmu.memory
+                               is a Vec<u8>, mmu.rs:2-4) */
   uint32_t flags;           /* 0, or EBPF_BATCH_GENERIC | EBPF_BATCH_XDP_MD | EBPF_BATCH_NO_JIT */
   uint64_t r10;             /* initial r10 (stack top) */
   uint64_t max_steps;       /* per-packet step budget, 1..; faults EBPF_ST_STEPS beyond */
@@ -107,6 +108,10 @@ typedef struct ebpf_batch {
   uint64_t workspace_bytes;
   const uint64_t* init_regs; /* optional device u64[11]: initial r0..r10 for every packet, replacing
                                 the main.rs layout (Emu.state.regs set by the caller, emu.rs:14-17) */
+  const uint32_t* init_fp;  /* optional device u32[init_fp_len]: the initial frame stack of every
+                               packet, bottom first (Emu.fp is pub, emu.rs:26; an EXIT pops its top,
+                               emu.rs:273-279). A batch with one runs on the general interpreter */
+  uint32_t init_fp_len;     /* 0..EBPF_MAX_CALL_DEPTH */
 } ebpf_batch;
 
 /* Outputs (device pointers; any may be NULL). */
@@ -117,6 +122,9 @@ typedef struct ebpf_batch_out {
   uint64_t* counters; /* u64[EBPF_NCOUNTERS], ADDED to (not overwritten) */
   uint8_t* mem;       /* u8[n][mem_size]: final memory image per packet (Emu.state.mmu.memory) */
   uint64_t* regs;     /* u64[n][11]: final r0..r10 per packet (Emu.state.regs) */
+  uint32_t* fp;       /* u32[n][EBPF_MAX_CALL_DEPTH]: final frame stack per packet, bottom first
+                         (Emu.fp; non-empty when a program falls off its end inside a call) */
+  uint8_t* fp_len;    /* u8[n]: its depth */
 } ebpf_batch_out;
 
 /* Fill a batch descriptor with the reference harness defaults (mem 1024, r10 512). */
@@ -179,10 +187,13 @@ int ebpf_prog_upload(ebpf_prog* prog, int device);
 int ebpf_run_batch(ebpf_prog* prog, const ebpf_batch* batch, const ebpf_batch_out* out,
                    ebpf_stream_t stream);
 
-/* Multi-GPU: shard s runs on devices[s] / streams[s]; afterwards the per-shard counters are
- * summed with one RCCL all-reduce over xGMI so that every outs[s].counters holds the global
- * totals. Shards are independent (no data-path exchange). Requires counters in every out.
- * Returns after enqueueing (asynchronous on each stream). */
+/* Multi-GPU: shard s runs on devices[s] / streams[s] (distinct devices); the shards' counters are
+ * summed with one RCCL all-reduce over xGMI, and the global totals of this call are ADDED to
+ * every outs[s].counters (accumulated as in ebpf_run_batch, never overwritten; the per-shard sums
+ * go through a library-owned device scratch first). Shards are independent (no data-path
+ * exchange). Requires counters in every out. A failing call leaves every caller counter
+ * untouched. Returns after enqueueing (asynchronous on each stream; the scratch is per (device,
+ * stream), so calls on the same streams are ordered by them). */
 int ebpf_run_batch_multi(ebpf_prog* prog, int nshards, const int* devices,
                          const ebpf_batch* batches, const ebpf_batch_out* outs,
                          ebpf_stream_t const* streams);

@@ -101,12 +101,13 @@ static int mem_addr(const mmu_t* m, int64_t base, int16_t off, int w, size_t* ad
   return OR_ST_OK;
 }
 
-int or_run(const or_insn* prog, size_t n, uint8_t* mem, size_t mem_size, int64_t regs[11],
-           uint64_t max_steps, uint64_t* steps_out) {
+int or_run_fp(const or_insn* prog, size_t n, uint8_t* mem, size_t mem_size, int64_t regs[11],
+              uint32_t fp[OR_MAX_CALL_DEPTH], size_t* fp_len_io, uint64_t max_steps,
+              uint64_t* steps_out) {
   mmu_t m = {mem, mem_size};
   uint32_t pc = 0;                   /* emu.rs:23,33 */
-  uint32_t fp[OR_MAX_CALL_DEPTH];    /* emu.rs:26 (Vec<u32>, bounded here) */
-  size_t fp_len = 0;
+  /* fp: emu.rs:26 (pub Vec<u32>, bounded here), the caller's initial frame stack */
+  size_t fp_len = *fp_len_io > OR_MAX_CALL_DEPTH ? OR_MAX_CALL_DEPTH : *fp_len_io;
   uint64_t steps = 0;
   int st = OR_ST_OK;
   for (;;) {
@@ -318,7 +319,15 @@ int or_run(const or_insn* prog, size_t n, uint8_t* mem, size_t mem_size, int64_t
   }
 done:
   if (steps_out) *steps_out = steps;
+  *fp_len_io = fp_len;
   return st;
+}
+
+int or_run(const or_insn* prog, size_t n, uint8_t* mem, size_t mem_size, int64_t regs[11],
+           uint64_t max_steps, uint64_t* steps_out) {
+  uint32_t fp[OR_MAX_CALL_DEPTH];
+  size_t fp_len = 0;
+  return or_run_fp(prog, n, mem, mem_size, regs, fp, &fp_len, max_steps, steps_out);
 }
 
 int or_run_packet(const or_insn* prog, size_t n, const uint8_t* pkt, size_t len, size_t mem_size,

@@ -15,7 +15,7 @@
  * it cannot be executed here. The oracle is pinned by (a) the reference's own decode unit
  * tests (ins.rs:291-500), (b) the three program KATs embedded in the reference (ins.rs:435,
  * notes.md:27, Makefile:16) and the behaviours its comments quote from bpf_conformance
- * (emu.rs:97,108-111,131,150-155; main.rs:58), and (c) an independently written Python
+ * (emu.rs:97,108-111,131,150-155; main.rs:26-28), and (c) an independently written Python
  * restatement (oracle/pyref.py) cross-checked by differential fuzzing. The 180-vector
  * bpf_conformance suite (notes.md:19) is absent (empty submodule): that part is UNPINNED.
  *
@@ -77,6 +77,12 @@ long or_decode(const uint8_t* code, size_t nbytes, or_insn* out, size_t cap, siz
  * executed (the final exit included, a faulting instruction excluded). Returns OR_ST_*. */
 int or_run(const or_insn* prog, size_t n, uint8_t* mem, size_t mem_size, int64_t regs[11],
            uint64_t max_steps, uint64_t* steps);
+
+/* or_run with the frame stack exposed (Emu.fp is pub, emu.rs:26): fp[0..*fp_len) is the initial
+ * stack (bottom first; an EXIT pops its top, emu.rs:273-279), and on return the final stack. */
+int or_run_fp(const or_insn* prog, size_t n, uint8_t* mem, size_t mem_size, int64_t regs[11],
+              uint32_t fp[OR_MAX_CALL_DEPTH], size_t* fp_len, uint64_t max_steps,
+              uint64_t* steps);
 
 /* One packet with the reference harness layout (main.rs:14-31): zeroed mem_size image,
  * packet copied to [0,len), r1 = 0, r2 = len, r10 = r10_init, other registers 0. */

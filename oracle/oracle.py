@@ -44,6 +44,11 @@ def lib():
         L.or_run.argtypes = [ctypes.POINTER(OrInsn), ctypes.c_size_t, ctypes.c_void_p,
                              ctypes.c_size_t, ctypes.POINTER(ctypes.c_int64), ctypes.c_uint64,
                              ctypes.POINTER(ctypes.c_uint64)]
+        L.or_run_fp.restype = ctypes.c_int
+        L.or_run_fp.argtypes = [ctypes.POINTER(OrInsn), ctypes.c_size_t, ctypes.c_void_p,
+                                ctypes.c_size_t, ctypes.POINTER(ctypes.c_int64),
+                                ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_size_t),
+                                ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]
         L.or_run_batch.restype = ctypes.c_int
         L.or_run_batch.argtypes = [ctypes.POINTER(OrInsn), ctypes.c_size_t, ctypes.c_void_p,
                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
@@ -104,6 +109,24 @@ class Program:
         steps = ctypes.c_uint64(0)
         st = lib().or_run(self.insns, self.n, mem, mem_size, regs, max_steps, ctypes.byref(steps))
         return st, [r & ((1 << 64) - 1) for r in regs], bytes(mem), steps.value
+
+    def run_image(self, image: bytes, regs, fp=(), max_steps: int = 0):
+        """Emu::run on a caller-built state (emu.rs:14-26 pub fields): the memory image of any
+        length, 11 registers, the frame stack fp (bottom first). -> (status, regs u64[11],
+        final memory bytes, final fp list, steps)."""
+        mem = (ctypes.c_uint8 * max(1, len(image)))()
+        ctypes.memmove(mem, bytes(image), len(image))
+        r = (ctypes.c_int64 * 11)()
+        for i, v in enumerate(regs):
+            v &= (1 << 64) - 1
+            r[i] = v - (1 << 64) if v >> 63 else v
+        f = (ctypes.c_uint32 * 64)(*[int(x) & 0xFFFFFFFF for x in fp])
+        fl = ctypes.c_size_t(len(fp))
+        steps = ctypes.c_uint64(0)
+        st = lib().or_run_fp(self.insns, self.n, mem, len(image), r, f, ctypes.byref(fl),
+                             max_steps, ctypes.byref(steps))
+        return (st, [x & ((1 << 64) - 1) for x in r], bytes(mem)[:len(image)],
+                [int(f[i]) for i in range(fl.value)], steps.value)
 
     def run_batch(self, frames: np.ndarray, n: int, stride: int = 0, offsets=None, lens=None,
                   mem_size: int = 1024, r10: int = 512, max_steps: int = 0, threads: int = 1):

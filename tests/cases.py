@@ -58,7 +58,7 @@ CASES = [
          cite="emu.rs:96-98 (div32-by-zero-reg.data)"),
     Case("mod64_by_zero_reg", A("mov r0, 7\nmov r3, 0\nmod r0, r3\nexit"), r0=7,
          cite="emu.rs:130-133 (mod64-by-zero-reg.data)"),
-    Case("mem_len", A("mov r0, r2\nexit"), pkt=bytes(5), r0=5, cite="main.rs:58-60 (mem-len.data)"),
+    Case("mem_len", A("mov r0, r2\nexit"), pkt=bytes(5), r0=5, cite="main.rs:26-28 (mem-len.data)"),
     # ---- Q1 LDX sub-width preserves the upper bytes (emu.rs:341-349,443) ----
     Case("q1_ldxb", A("lddw r0, 0x1122334455667788\nldxb r0, [r1+0]\nexit"), pkt=h("aa"),
          r0=0x11223344556677AA, cite="emu.rs:341-349"),

@@ -5,7 +5,11 @@ fuzz vector is cross-checked against the independent Python restatement before i
   fuzz_vectors.json : 160 random programs x up to 8 packets -> status, r0, regs, CRC32(memory)
   workloads.json    : BASELINE configs 2/3/5 at full size (1,048,576 packets) -> counters,
                       CRC32 of the verdict array, first 256 verdicts
-Usage: python tests/golden/make_golden.py
+  config4.json      : BASELINE config 4, the 5-tuple over a 100,000,000-packet global batch of
+                      seeded 1 Mi-packet chunks (chunk k: workloads.frames_fixed(size, 64,
+                      3 + 100 k), as bench.py --total-packets builds it) -> per-chunk counters and
+                      verdict CRC32s, and the global counters
+Usage: python tests/golden/make_golden.py [config4]
 """
 import json
 import os
@@ -74,7 +78,37 @@ def workloads():
     return res
 
 
+def _config4_chunk(args):
+    k, size = args
+    p = oracle.Program(W.program("5tuple"))
+    buf = W.frames_fixed(size, 64, 3 + 100 * k)
+    r0, st, cnt = p.run_batch(buf, size, stride=64, threads=1)
+    verdict = np.where(st != 0, 0xFF, np.where(r0 < 5, r0, 0xFE)).astype(np.uint8)
+    return [int(c) for c in cnt], zlib.crc32(verdict.tobytes())
+
+
+def config4(total=100_000_000, chunk=1 << 20):
+    from multiprocessing import Pool
+
+    from ebpf_emu import dist as D
+
+    sizes = D.chunk_sizes(total, chunk)
+    with Pool(max(1, min(8, os.cpu_count() or 1) - 1)) as pool:
+        per = pool.map(_config4_chunk, list(enumerate(sizes)))
+    tot = [sum(c[i] for c, _ in per) for i in range(8)]
+    assert sum(tot[:7]) == total
+    return {"program": W.program("5tuple").hex(), "total_packets": total, "chunk": chunk,
+            "seed": "chunk k: workloads.frames_fixed(size, 64, config_id=3 + 100 * k)",
+            "mem_size": 1024, "r10": 512, "chunk_sizes": sizes,
+            "chunk_counters": [c for c, _ in per], "chunk_verdict_crc32": [v for _, v in per],
+            "counters": tot}
+
+
 if __name__ == "__main__":
+    if sys.argv[1:] == ["config4"]:
+        with open(os.path.join(HERE, "config4.json"), "w") as f:
+            json.dump(config4(), f, indent=0)
+        sys.exit(0)
     with open(os.path.join(HERE, "fuzz_vectors.json"), "w") as f:
         json.dump(fuzz_vectors(), f, indent=0)
     with open(os.path.join(HERE, "workloads.json"), "w") as f:

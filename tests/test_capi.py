@@ -110,9 +110,22 @@ def test_invalid_arguments_fail_before_any_device_call(product_lib):
     assert (b.mem_size, b.r10, b.max_steps) == (1024, 512, 1 << 22)
     out = _lib.BatchOut()
     assert product_lib.ebpf_run_batch(h, None, ctypes.byref(out), None) == _lib.EBPF_EINVAL
-    b.mem_size = 12  # not a multiple of 8
+    # no packet layout (stride 0, no offsets / lens)
+    assert product_lib.ebpf_run_batch(h, ctypes.byref(b), ctypes.byref(out), None) == _lib.EBPF_EINVAL
+    b.stride = 64  # (n = 0: a valid batch returns before touching a device)
+    assert product_lib.ebpf_run_batch(h, ctypes.byref(b), ctypes.byref(out), None) == _lib.EBPF_OK
+    b.mem_size = 12  # any image length is valid (Mmu.memory is a Vec<u8>, mmu.rs:2-4)
+    assert product_lib.ebpf_run_batch(h, ctypes.byref(b), ctypes.byref(out), None) == _lib.EBPF_OK
+    b.mem_size = (1 << 24) + 1
     assert product_lib.ebpf_run_batch(h, ctypes.byref(b), ctypes.byref(out), None) == _lib.EBPF_EINVAL
     b.mem_size = 1024
+    b.init_fp_len = 65  # deeper than EBPF_MAX_CALL_DEPTH
+    b.init_fp = 8
+    assert product_lib.ebpf_run_batch(h, ctypes.byref(b), ctypes.byref(out), None) == _lib.EBPF_EINVAL
+    b.init_fp_len = 1
+    b.init_fp = None  # a depth without a stack
+    assert product_lib.ebpf_run_batch(h, ctypes.byref(b), ctypes.byref(out), None) == _lib.EBPF_EINVAL
+    b.init_fp_len = 0
     b.max_steps = 0
     assert product_lib.ebpf_run_batch(h, ctypes.byref(b), ctypes.byref(out), None) == _lib.EBPF_EINVAL
     product_lib.ebpf_prog_free(h)

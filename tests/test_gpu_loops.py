@@ -11,7 +11,9 @@ import random
 
 import pytest
 
-from test_gpu_parity import _check_against_oracle, _run_full, _same_outputs
+from fuzzgen import gen_packet, gen_program
+from test_gpu_parity import (_check_against_oracle, _check_prod_against_oracle, _run_full,
+                             _run_prod, _same_outputs)
 
 pytestmark = pytest.mark.gpu
 
@@ -96,6 +98,30 @@ def test_loop_programs_layouts(cuda, oracle_mod, layout):
         got = _run_full(img, pkts, cuda, **layout)
         _check_against_oracle(oracle_mod, img, pkts, got, tag=f"{layout} {src[:40]}")
         _same_outputs(got, _run_full(img, pkts, cuda, generic=True, **layout), src)
+        prod = _run_prod(img, pkts, cuda, **layout)
+        _check_prod_against_oracle(oracle_mod, img, pkts, prod, tag=f"prod {layout} {src[:40]}")
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_fuzz_loop_programs_production_outputs(cuda, oracle_mod, seed):
+    """Random tier-0 programs with back edges (the compiled loop kernel) with the production
+    outputs only -- no registers, so the liveness-pruned register init runs -- vs the oracle,
+    in the stride and offsets + lens layouts."""
+    rng = random.Random(6060 + seed)
+    n_run = 0
+    for it in range(40):
+        img = gen_program(rng, allow_loops=True, tier0=True)
+        try:
+            oracle_mod.Program(img)
+        except oracle_mod.OracleDecodeError:
+            continue
+        pkts = [gen_packet(rng) for _ in range(rng.choice([64, 65, 100, 130]))]
+        layout = dict(offsets_layout=True, align=16) if it % 2 else dict()
+        prod = _run_prod(img, pkts, cuda, max_steps=2000, **layout)
+        _check_prod_against_oracle(oracle_mod, img, pkts, prod, max_steps=2000,
+                                   tag=f"seed {seed} it {it}")
+        n_run += 1
+    assert n_run >= 25
 
 
 @pytest.mark.parametrize("budget", [1, 2, 3, 5, 6, 7, 8, 13, 50, 101, 997])

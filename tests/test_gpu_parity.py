@@ -70,6 +70,48 @@ def _run_full(prog_img, pkts, dev, mem_size=1024, r10=512, max_steps=STEPS, gene
     return out
 
 
+def _run_prod(prog_img, pkts, dev, mem_size=1024, r10=512, max_steps=STEPS, **layout):
+    """The outputs a production caller asks for (bench.py, pcap.py): no registers, no image, so
+    the kernels take their production paths -- the compiled programs' liveness-pruned register
+    init (jit.cpp live_in, ;@@JITINIT@@) and, for a verdict-only launch, the k_flags = 0 epilogue.
+    Two launches: verdict + counters only, then r0 + status (still without registers)."""
+    from ebpf_emu import Program
+
+    torch = _torch()
+    prog = Program(prog_img)
+    frames, kw = _stage(pkts, dev, **layout)
+    cnt = torch.zeros(8, dtype=torch.int64, device=dev)
+    v = prog.run(frames, mem_size=mem_size, r10=r10, max_steps=max_steps, verdict=True,
+                 counters=cnt, **kw)
+    rs = prog.run(frames, mem_size=mem_size, r10=r10, max_steps=max_steps, verdict=False,
+                  r0=True, status=True, **kw)
+    torch.cuda.synchronize()
+    out = dict(verdict=v.verdict.cpu().numpy(), counters=cnt.cpu().numpy().view(np.uint64),
+               r0=rs.r0.cpu().numpy().view(np.uint64), status=rs.status.cpu().numpy())
+    prog.close()
+    return out
+
+
+def _check_prod_against_oracle(oracle_mod, img, pkts, got, mem_size=1024, r10=512, tag="",
+                               max_steps=STEPS):
+    op = oracle_mod.Program(img)
+    cnt = np.zeros(8, dtype=np.uint64)
+    for i, p in enumerate(pkts):
+        st, r0, steps = op.run_packet(p, mem_size, r10, max_steps)
+        ctx = f"{tag} pkt {i} prog {img.hex()} pkt {p.hex()}"
+        assert got["status"][i] == st, ctx
+        if st == 0:
+            assert int(got["r0"][i]) == r0, ctx
+            v = r0 if r0 < 5 else 0xFE
+            cnt[r0 if r0 < 5 else 5] += 1
+        else:
+            v = 0xFF
+            cnt[6] += 1
+        assert got["verdict"][i] == v, ctx
+        cnt[7] += steps
+    assert list(got["counters"]) == list(cnt), tag
+
+
 def _check_against_oracle(oracle_mod, img, pkts, got, mem_size=1024, r10=512, tag=""):
     op = oracle_mod.Program(img)
     cnt = np.zeros(8, dtype=np.uint64)
@@ -122,6 +164,9 @@ def test_fuzz_wave_divergence(cuda, oracle_mod, seed):
         got = _run_full(img, pkts, cuda)
         tiers.add(got["tier"])
         _check_against_oracle(oracle_mod, img, pkts, got, tag=f"seed {seed} it {it}")
+        # the production outputs (no registers / image): the same program and packets
+        prod = _run_prod(img, pkts, cuda)
+        _check_prod_against_oracle(oracle_mod, img, pkts, prod, tag=f"prod seed {seed} it {it}")
     assert tiers == {0, 1}
 
 
@@ -153,6 +198,8 @@ def test_forward_only_fast_path_fuzz(cuda, oracle_mod, seed):
         ref = _run_full(img, pkts, cuda, generic=True)
         _same_outputs(got, ref, f"seed {seed} it {it} prog {img.hex()}")
         _check_against_oracle(oracle_mod, img, pkts, got, tag=f"seed {seed} it {it}")
+        prod = _run_prod(img, pkts, cuda)
+        _check_prod_against_oracle(oracle_mod, img, pkts, prod, tag=f"prod seed {seed} it {it}")
     assert n_fast >= 35
 
 
@@ -452,3 +499,131 @@ def test_conformance_runner(cuda):
 
     d = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "conformance")
     assert main([d]) == 0
+
+
+@pytest.mark.timeout(600)
+def test_config4_global_batch_golden(cuda):
+    """BASELINE config 4: the 5-tuple over the 100,000,000-packet global batch (seeded 1 Mi-packet
+    chunks, bench.py --total-packets) as ONE batch on one GPU -- the strong-scaling workload every
+    rank count must reproduce. Counters and every chunk's verdict CRC32 equal the committed
+    fixture (tests/golden/make_golden.py config4, from the oracle)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    import torch
+
+    from ebpf_emu import Program
+    from ebpf_emu import workloads as W
+
+    with open(os.path.join(GOLDEN, "config4.json")) as f:
+        g = json.load(f)
+    sizes = g["chunk_sizes"]
+    n = g["total_packets"]
+    assert sum(sizes) == n
+    frames = torch.empty(n * 64, dtype=torch.uint8, device=cuda)
+    starts = np.concatenate([[0], np.cumsum(sizes)])
+
+    def put(k):
+        return k, W.frames_fixed(sizes[k], 64, 3 + 100 * k)
+
+    with ThreadPoolExecutor(8) as ex:  # host generation in threads, copies in order
+        for k, buf in ex.map(put, range(len(sizes))):
+            frames[int(starts[k]) * 64:int(starts[k + 1]) * 64].copy_(torch.from_numpy(buf))
+    prog = Program(bytes.fromhex(g["program"]))
+    cnt = torch.zeros(8, dtype=torch.int64, device=cuda)
+    res = prog.run(frames, n=n, stride=64, counters=cnt)
+    torch.cuda.synchronize()
+    verdict = res.verdict.cpu().numpy()
+    assert [int(x) for x in cnt.cpu().numpy().view(np.uint64)] == g["counters"]
+    for k in range(len(sizes)):
+        v = verdict[int(starts[k]):int(starts[k + 1])]
+        assert zlib.crc32(v.tobytes()) == g["chunk_verdict_crc32"][k], k
+        assert np.bincount(v, minlength=256)[1] == g["chunk_counters"][k][1], k
+    del frames, res
+    prog.close()
+
+
+def test_run_batch_multi_single_shard(cuda):
+    """ebpf_run_batch_multi with one shard on device 0 (the RCCL counter all-reduce over a
+    one-rank communicator) equals ebpf_run_batch: the same verdicts, and the counters ADDED to
+    the caller's (accumulated, as the header promises), twice in a row."""
+    import ctypes
+
+    import torch
+
+    from ebpf_emu import Program, _lib
+    from ebpf_emu import workloads as W
+
+    n = 300_001
+    frames = torch.from_numpy(W.frames_fixed(n, 64, 3)).to(cuda)
+    prog = Program(W.program("5tuple"))
+    ref_cnt = torch.zeros(8, dtype=torch.int64, device=cuda)
+    ref = prog.run(frames, n=n, stride=64, counters=ref_cnt)
+    torch.cuda.synchronize()
+    b = prog.make_batch(frames, n=n, stride=64)
+    verdict = torch.empty(n, dtype=torch.uint8, device=cuda)
+    cnt = torch.full((8,), 7, dtype=torch.int64, device=cuda)  # caller's running totals
+    out = _lib.BatchOut()
+    out.verdict = verdict.data_ptr()
+    out.counters = cnt.data_ptr()
+    stream = torch.cuda.current_stream(cuda)
+    devs = (ctypes.c_int * 1)(0)
+    batches = (_lib.Batch * 1)(b)
+    outs = (_lib.BatchOut * 1)(out)
+    streams = (ctypes.c_void_p * 1)(stream.cuda_stream)
+    L = _lib.lib()
+    for rep in (1, 2):
+        rc = L.ebpf_run_batch_multi(prog._h, 1, devs, batches, outs, streams)
+        assert rc == 0, _lib.strerror(rc)
+        torch.cuda.synchronize()
+        assert torch.equal(verdict, ref.verdict)
+        assert cnt.cpu().tolist() == [7 + rep * int(c) for c in ref_cnt.cpu().tolist()]
+    # a repeated device is rejected before anything runs
+    devs2 = (ctypes.c_int * 2)(0, 0)
+    assert L.ebpf_run_batch_multi(prog._h, 2, devs2, (_lib.Batch * 2)(b, b),
+                                  (_lib.BatchOut * 2)(out, out),
+                                  (ctypes.c_void_p * 2)(stream.cuda_stream, stream.cuda_stream)) \
+        == _lib.EBPF_EINVAL
+    prog.close()
+
+
+def test_emu_any_image_length_and_frame_stack(cuda, oracle_mod):
+    """The Emu surface beyond the main.rs layout: an image of any length (Mmu.memory: Vec<u8>,
+    mmu.rs:2-4) with loads at its last bytes, and the pub frame stack Emu.fp (emu.rs:26) -- an
+    initial stack popped by EXIT (emu.rs:273-279), and a program that falls off its end inside a
+    call leaving a non-empty stack. Every case against the oracle's run_image."""
+    from ebpf_emu import Emu, EmuPanic
+    from ebpf_emu.asm import assemble
+    from ebpf_emu.ins import decode_image
+    from ebpf_emu.mmu import Mmu
+
+    cases = [
+        ("ldxb r0, [r1+12]\nexit", bytes(range(1, 14)), (), [0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0]),
+        ("ldxh r0, [r1+12]\nexit", bytes(range(1, 14)), (), [0] * 11),       # tail past the end
+        ("ldxw r0, [r1+9]\nexit", bytes(range(1, 14)), (), [0] * 11),
+        ("stb [r1+4], 0x77\nldxdw r0, [r1+0]\nexit", bytes(range(1, 10)), (), [0] * 11),
+        ("mov r0, 5\nexit", b"", (), [0] * 11),                              # empty image
+        ("ldxb r0, [r1+0]\nexit", b"", (), [0] * 11),                        # ... faults
+        ("mov r0, 1\nexit\nmov r0, 2\nexit", bytes(3), (2,), [0] * 11),      # EXIT pops fp
+        ("mov r0, 1\nexit\nmov r0, 2\nexit", bytes(3), (2, 3), [0] * 11),    # pops to pc 3
+        ("mov r0, 1\nexit", bytes(5), (1000,), [0] * 11),                    # pops past the end
+        ("call 1\nexit\nmov r0, 9", bytes(7), (), [0] * 11),                 # falls off in a call
+        ("call 1\nexit\nmov r0, 9", bytes(7), (5, 6), [0] * 11),
+        ("add r0, r3\nexit", bytes(11), (), [1, 0, 0, 41, 0, 0, 0, 0, 0, 0, 0]),
+    ]
+    for src, image, fp, regs in cases:
+        img = assemble(src)
+        st, oregs, omem, ofp, _ = oracle_mod.Program(img).run_image(image, regs, fp, 20000)
+        emu = Emu()
+        emu.state.mmu = Mmu(bytearray(image))
+        emu.state.regs = list(regs)
+        emu.fp = list(fp)
+        emu.instructions = decode_image(img)
+        if st == 0:
+            emu.run()
+            assert [r & ((1 << 64) - 1) for r in emu.state.regs] == oregs, src
+            assert bytes(emu.state.mmu.memory) == omem, src
+            assert emu.fp == ofp, (src, fp)
+        else:
+            with pytest.raises(EmuPanic) as e:
+                emu.run()
+            assert e.value.status == st, src
