@@ -154,9 +154,11 @@ def main():
     # ---- timed region: barrier + sync on both sides, K steps, max over ranks ----
     # HIP events on the launch stream: one pair around the K back-to-back batches (a batch =
     # every launch of one ebpf_run_batch), so the per-batch time includes the dispatch gaps
-    # between launches but no event packets between them. The host waits for the last event by
-    # polling it (a blocking synchronize sleeps and wakes tens of us late, which at K = 20 steps
-    # of ~15 us was ~9 % of the wall clock); the synchronize after it then returns at once.
+    # between launches but no event packets between them. The wall clock adds one host -> GPU ->
+    # host round trip (the first launch's latency and the completion signal: ~13 us measured for
+    # an empty stream, tools/timing_probe.py), i.e. ~7 % of K = 20 steps of ~15 us; busy-polling
+    # the end event instead of synchronizing measured worse (35 vs 20 us), a graph of the K
+    # launches no better.
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
     if world > 1:
@@ -168,8 +170,6 @@ def main():
         step(i)
     t_enq = time.perf_counter() - t0  # host time to enqueue the K steps (launch-bound check)
     ev1.record(stream)
-    while not ev1.query():
-        pass
     D.reduce_counters(counters)  # the one exchange step: per-verdict counters, RCCL / xGMI
     torch.cuda.synchronize(dev)
     if world > 1:

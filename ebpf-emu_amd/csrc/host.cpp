@@ -981,7 +981,8 @@ int ebpf_run_batch_multi(ebpf_prog* p, int nshards, const int* devices, const eb
   if (!p || nshards <= 0 || nshards > kMaxDevices || !devices || !batches || !outs || !streams)
     return EBPF_EINVAL;
   for (int s = 0; s < nshards; s++) {
-    if (!outs[s].counters || !streams[s] || devices[s] < 0 || devices[s] >= kMaxDevices)
+    // (a NULL stream is the device's null stream)
+    if (!outs[s].counters || devices[s] < 0 || devices[s] >= kMaxDevices)
       return EBPF_EINVAL;
     for (int t = 0; t < s; t++)
       if (devices[t] == devices[s]) return EBPF_EINVAL;  // one communicator rank per device

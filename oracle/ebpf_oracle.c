@@ -366,6 +366,7 @@ typedef struct {
 
 static void* batch_worker(void* arg) {
   batch_job* j = (batch_job*)arg;
+  uint64_t cnt[8] = {0}; /* thread-local: the jobs share cache lines */
   for (uint64_t i = j->lo; i < j->hi; i++) {
     const uint8_t* p = j->frames + (j->offsets ? (uint64_t)j->offsets[i] : i * j->stride);
     size_t len = j->lens ? j->lens[i] : (size_t)j->stride;
@@ -373,11 +374,12 @@ static void* batch_worker(void* arg) {
     int st = or_run_packet(j->prog, j->n, p, len, j->mem_size, j->r10, j->max_steps, &r0, &steps);
     if (j->r0_out) j->r0_out[i] = r0;
     if (j->status_out) j->status_out[i] = (uint8_t)st;
-    if (st) j->counters[6]++;
-    else if (r0 < 5) j->counters[r0]++;
-    else j->counters[5]++;
-    j->counters[7] += steps;
+    if (st) cnt[6]++;
+    else if (r0 < 5) cnt[r0]++;
+    else cnt[5]++;
+    cnt[7] += steps;
   }
+  memcpy(j->counters, cnt, sizeof cnt);
   return NULL;
 }
 
