@@ -344,10 +344,12 @@ struct Compiler {
       const uint32_t L = xb ? x : np, F = xb ? np : x;
       if (L < back_in.size() && back_in[L] == 1) {
         if (ja) return "s_branch .L" + P + "body" + std::to_string(L) + "\n";
-        const std::string stay = xb ? "vcc" : "exec", leave_op = xb ? "s_andn2_b64" : "s_and_b64";
-        std::string s = "s_mov_b64 s[64:65], exec\n" + leave_op + " exec, s[64:65], vcc\n" +
-                        park(std::to_string(F), F >= n);
-        s += (xb ? "s_and_b64 exec, s[64:65], vcc\n" : "s_andn2_b64 exec, s[64:65], vcc\n");
+        // the leaving lanes' parked pc by one select on vcc (a VOP3 write touches only the active
+        // lanes), then exec keeps the staying lanes; SCC = some lane stays
+        const std::string F_lpc = lpc_of(F, F >= n);  // (loop programs: "-1" for done lanes)
+        std::string s = xb ? "v_cndmask_b32_e64 v28, " + F_lpc + ", v28, vcc\n"
+                           : "v_cndmask_b32_e64 v28, v28, " + F_lpc + ", vcc\n";
+        s += (xb ? "s_and_b64 exec, exec, vcc\n" : "s_andn2_b64 exec, exec, vcc\n");
         return s + "s_cbranch_scc1 .L" + P + "body" + std::to_string(L) + "\n";
       }
     }
@@ -542,9 +544,13 @@ struct Compiler {
 
   // A one-byte register-address load in a loop program (the per-byte loops): the handler's
   // semantics (ldx1 in gen_tile.py, loop form) with its checks merged -- in bounds is a < mem
-  // as one 64-bit compare against s[52:53] = mem (mem < 2^24, so a nonzero high word fails it),
-  // the byte read with ds_read_u8 at its swizzled window address, and the window refill (or, in
-  // tiles with unaligned packets, the packet dword's load) out of line.
+  // as one 64-bit compare against s[52:53] = mem (mem < 2^24, so a nonzero high word fails it);
+  // a < len is computed once into s[60:61] (a VOPC result is 0 for inactive lanes), and the
+  // window offset a - WB is zeroed for lanes at or past len, so one unsigned compare finds the
+  // lanes that need a refill (vcc, branched on directly) and the LDS address needs no clamp; the
+  // byte is read with ds_read_u8 at its swizzled window address, zeroed past len by the same
+  // mask, and merged with the 0xff in s56 (set once per program). The window refill (or, in
+  // tiles with unaligned packets, the packet dword's load) is out of line.
   std::string ldx1_loop(uint32_t i, const Marker& m, const std::string& P, std::string& ool) const {
     const TUop& u = t[i];
     const std::string U = P + "u" + std::to_string(i), next = entry_label(P, next_start(i));
@@ -570,29 +576,27 @@ struct Compiler {
          "s_cbranch_execz " + next + "\n"
          ".Lok" + U + ":\n"
          "v_sub_u32 v42, v36, v22\n"
-         "v_cmp_le_u32_e64 s[62:63], 64, v42\n"
          "v_cmp_lt_u32_e64 s[60:61], v36, v31\n"
-         "s_and_b64 s[68:69], s[62:63], s[60:61]\n"
-         "s_and_b64 s[68:69], s[68:69], exec\n"
-         "s_cbranch_scc1 .Lrf" + U + "\n"
+         "v_cndmask_b32_e64 v43, 0, v42, s[60:61]\n"
+         "v_cmp_le_u32 vcc, 64, v43\n"
+         "s_cbranch_vccnz .Lrf" + U + "\n"
          ".Lrfb" + U + ":\n"
-         "v_min_u32 v42, 63, v42\n"
-         "v_xad_u32 v42, v35, v42, v34\n"
+         "v_xad_u32 v42, v35, v43, v34\n"
          "ds_read_u8 v26, v42\n"
          "s_waitcnt lgkmcnt(0)\n"
-         "v_cmp_lt_u32 vcc, v36, v31\n"
-         "v_cndmask_b32 v26, 0, v26, vcc\n"
+         "v_cndmask_b32_e64 v26, 0, v26, s[60:61]\n"
          ".Lfarb" + U + ":\n"
-         "s_mov_b32 s42, 0xff\n"
-         "v_bfi_b32 " + D0 + ", s42, v26, " + D0 + "\n";
+         "v_bfi_b32 " + D0 + ", s56, v26, " + D0 + "\n";
     ool += ".Lrf" + U + ":\n"
+           "s_mov_b64 s[68:69], vcc\n"
            "s_cmp_eq_u32 " + m.aligned + ", 0\n"
            "s_cbranch_scc1 .Lfar" + U + "\n" + std::string(kJitRefill) +
            "v_sub_u32 v42, v36, v22\n"
+           "v_cndmask_b32_e64 v43, 0, v42, s[60:61]\n"
            "s_branch .Lrfb" + U + "\n"
            ".Lfar" + U + ":\n"
-           "v_min_u32 v42, 63, v42\n"
-           "v_xad_u32 v42, v35, v42, v34\n"
+           "v_min_u32 v43, 63, v43\n"
+           "v_xad_u32 v42, v35, v43, v34\n"
            "ds_read_u8 v26, v42\n"
            "s_mov_b64 s[66:67], exec\ns_mov_b64 exec, s[68:69]\n"
            "v_and_b32 v46, -4, v36\nv_mov_b32 v47, 0\n"
@@ -602,8 +606,7 @@ struct Compiler {
            "v_and_b32 v48, 3, v36\nv_lshlrev_b32 v48, 3, v48\n"
            "v_bfe_u32 v26, v49, v48, 8\n"
            "s_mov_b64 exec, s[66:67]\n"
-           "v_cmp_lt_u32 vcc, v36, v31\n"
-           "v_cndmask_b32 v26, 0, v26, vcc\n"
+           "v_cndmask_b32_e64 v26, 0, v26, s[60:61]\n"
            "s_branch .Lfarb" + U + "\n";
     return s;
   }
@@ -809,7 +812,7 @@ struct Compiler {
   bool body_loop(const Marker& m, Compiler& xc, std::string& out) {
     const std::string P = "J" + m.n + "_", PX = "J" + m.n + "x_";
     std::string main = "; compiled eBPF loop program: " + std::to_string(n) + " micro-ops\n"
-                       "s_mov_b32 s52, s33\ns_mov_b32 s53, 0\n"
+                       "s_mov_b32 s52, s33\ns_mov_b32 s53, 0\ns_movk_i32 s56, 0xff\n"
                        "s_cmp_lg_u32 s70, 0\ns_cbranch_scc1 .L" + PX + "start\n"
                        "s_mov_b64 exec, 0\n";
     std::string ool;

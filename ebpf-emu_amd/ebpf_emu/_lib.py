@@ -10,7 +10,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libebpfemu.so")
+# (EBPFEMU_LIB_PATH: another build of the same library, for A/B runs of two builds on one box)
+LIB_PATH = os.environ.get("EBPFEMU_LIB_PATH") or os.path.join(_HERE, "libebpfemu.so")
 
 # ---- constants mirrored from include/ebpf_emu.h ----
 EBPF_OK = 0
