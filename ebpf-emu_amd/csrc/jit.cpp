@@ -242,7 +242,28 @@ struct Compiler {
       }
     }
     start[n] = 1;
+    // single-block loops (a head with one back edge, the jump at the end of the head's own
+    // block): every lane leaving through that jump parks at the same successor F, so its parked
+    // pc is written once when lanes enter the head (they all stay in exec until they leave)
+    hoist.assign(n + 1, -2);
+    if (loops)
+      for (uint32_t i = 0; i < n; i++) {
+        const Uop& o = uops[i];
+        if (!is_jump(o) || o.op == U_JA) continue;
+        const uint32_t x = t[i].x, np = t[i].npc;
+        const bool xb = x <= i && x < n, nb = np <= i && np < n;
+        if (xb == nb) continue;
+        const uint32_t L = xb ? x : np, F = xb ? np : x;
+        if (L >= back_in.size() || back_in[L] != 1) continue;
+        bool one_block = true;
+        for (uint32_t j = L + 1; j <= i; j++) one_block = one_block && !start[j];
+        if (one_block) hoist[L] = F >= n ? -1 : (int64_t)F;
+      }
   }
+
+  // hoist[L] (loop programs): the parked pc written at the entry of single-block loop head L, or
+  // -2 (none)
+  std::vector<int64_t> hoist;
 
   // back edges into each pc: a loop head with exactly one lets that jump's taken lanes run the
   // head's block straight away (no lane can be parked there but them)
@@ -344,6 +365,9 @@ struct Compiler {
       const uint32_t L = xb ? x : np, F = xb ? np : x;
       if (L < back_in.size() && back_in[L] == 1) {
         if (ja) return "s_branch .L" + P + "body" + std::to_string(L) + "\n";
+        if (hoist[L] != -2)  // the leaving lanes' parked pc was set at the head's entry
+          return std::string(xb ? "s_and_b64 exec, exec, vcc\n" : "s_andn2_b64 exec, exec, vcc\n") +
+                 "s_cbranch_scc1 .L" + P + "body" + std::to_string(L) + "\n";
         // the leaving lanes' parked pc by one select on vcc (a VOP3 write touches only the active
         // lanes), then exec keeps the staying lanes; SCC = some lane stays
         const std::string F_lpc = lpc_of(F, F >= n);  // (loop programs: "-1" for done lanes)
@@ -551,6 +575,13 @@ struct Compiler {
   // byte is read with ds_read_u8 at its swizzled window address, zeroed past len by the same
   // mask, and merged with the 0xff in s56 (set once per program). The window refill (or, in
   // tiles with unaligned packets, the packet dword's load) is out of line.
+  // kJitRefill with the address's low word in register A instead of v36
+  static std::string refill(const std::string& A) {
+    std::string r(kJitRefill);
+    replace_token(r, "v36", A);
+    return r;
+  }
+
   std::string ldx1_loop(uint32_t i, const Marker& m, const std::string& P, std::string& ool) const {
     const TUop& u = t[i];
     const std::string U = P + "u" + std::to_string(i), next = entry_label(P, next_start(i));
@@ -565,8 +596,16 @@ struct Compiler {
       offs = "s[48:49]";
     }
     const std::string D0 = "v" + std::to_string(u.dst2);
-    s += "v_lshl_add_u64 v[36:37], " + vpair(u.src2, 0, 1) + ", 0, " + offs + "\n"
-         "v_cmp_gt_u64 vcc, s[52:53], v[36:37]\n"
+    // the address a = src + off in v[36:37]; with off = 0 the source pair itself (the refill
+    // reads only its low word and uses v37 as a temporary)
+    std::string A = "v36", AP = "v[36:37]";
+    if (off == 0) {
+      A = vreg(u.src2, 0);
+      AP = vpair(u.src2, 0, 1);
+    } else {
+      s += "v_lshl_add_u64 v[36:37], " + vpair(u.src2, 0, 1) + ", 0, " + offs + "\n";
+    }
+    s += "v_cmp_gt_u64 vcc, s[52:53], " + AP + "\n"
          "s_andn2_b64 s[64:65], exec, vcc\n"
          "s_cbranch_scc0 .Lok" + U + "\n"
          "s_mov_b64 s[66:67], exec\ns_mov_b64 exec, s[64:65]\n"
@@ -575,8 +614,8 @@ struct Compiler {
          "s_andn2_b64 exec, s[66:67], s[64:65]\n"
          "s_cbranch_execz " + next + "\n"
          ".Lok" + U + ":\n"
-         "v_sub_u32 v42, v36, v22\n"
-         "v_cmp_lt_u32_e64 s[60:61], v36, v31\n"
+         "v_sub_u32 v42, " + A + ", v22\n"
+         "v_cmp_lt_u32_e64 s[60:61], " + A + ", v31\n"
          "v_cndmask_b32_e64 v43, 0, v42, s[60:61]\n"
          "v_cmp_le_u32 vcc, 64, v43\n"
          "s_cbranch_vccnz .Lrf" + U + "\n"
@@ -590,8 +629,8 @@ struct Compiler {
     ool += ".Lrf" + U + ":\n"
            "s_mov_b64 s[68:69], vcc\n"
            "s_cmp_eq_u32 " + m.aligned + ", 0\n"
-           "s_cbranch_scc1 .Lfar" + U + "\n" + std::string(kJitRefill) +
-           "v_sub_u32 v42, v36, v22\n"
+           "s_cbranch_scc1 .Lfar" + U + "\n" + refill(A) +
+           "v_sub_u32 v42, " + A + ", v22\n"
            "v_cndmask_b32_e64 v43, 0, v42, s[60:61]\n"
            "s_branch .Lrfb" + U + "\n"
            ".Lfar" + U + ":\n"
@@ -599,11 +638,11 @@ struct Compiler {
            "v_xad_u32 v42, v35, v43, v34\n"
            "ds_read_u8 v26, v42\n"
            "s_mov_b64 s[66:67], exec\ns_mov_b64 exec, s[68:69]\n"
-           "v_and_b32 v46, -4, v36\nv_mov_b32 v47, 0\n"
+           "v_and_b32 v46, -4, " + A + "\nv_mov_b32 v47, 0\n"
            "v_lshl_add_u64 v[44:45], v[32:33], 0, v[46:47]\n"
            "global_load_dword v49, v[44:45], off\n"
            "s_waitcnt vmcnt(0) lgkmcnt(0)\n"
-           "v_and_b32 v48, 3, v36\nv_lshlrev_b32 v48, 3, v48\n"
+           "v_and_b32 v48, 3, " + A + "\nv_lshlrev_b32 v48, 3, v48\n"
            "v_bfe_u32 v26, v49, v48, 8\n"
            "s_mov_b64 exec, s[66:67]\n"
            "v_cndmask_b32_e64 v26, 0, v26, s[60:61]\n"
@@ -708,9 +747,13 @@ struct Compiler {
           main += "s_or_saveexec_b64 s[64:65], -1\nv_cmp_eq_u32 vcc, " + std::to_string(i) +
                   ", v28\ns_or_b64 exec, s[64:65], vcc\n";
         main += "s_cbranch_execz .L" + P + "b" + std::to_string(next_start(i)) + "\n";
+        if (loops && hoist[i] != -2) main += "v_mov_b32 v28, " + std::to_string(hoist[i]) + "\n";
         if (loops) main += ".L" + P + "body" + std::to_string(i) + ":\n";
-        main += "v_add_u32 v29, " + std::to_string(t[i].blen) + ", v29\n";
-        if (loops) main += budget_check(i, P);
+        if (loops)  // biased counter: the add's carry-out is the budget test (budget_check)
+          main += "v_add_co_u32_e32 v29, vcc, " + std::to_string(t[i].blen) + ", v29\n" +
+                  budget_check(i, P);
+        else
+          main += "v_add_u32 v29, " + std::to_string(t[i].blen) + ", v29\n";
       }
       const uint32_t id = t[i].hoff / TILE_SLOT;
       if (id >= (uint32_t)T_COUNT || id == (uint32_t)T_DONE) {
@@ -756,8 +799,11 @@ struct Compiler {
   // dispatcher: the block copy restarts the tile in exact mode when some lane would pass it inside
   // the block (s70 = 1, windows re-read where refills are possible, tile_kernel's .Lbudget); the
   // exact copy (one micro-op per block) stops the lanes whose step this would be, ST_STEPS.
+  // Loop programs keep the step counter biased, v29 = steps + (2^32 - 1 - max_steps) (s57 holds
+  // the bias; body_loop sets and removes it), so the block entry's add carries out exactly for
+  // the lanes whose steps pass max_steps (vcc).
   std::string budget_check(uint32_t i, const std::string& P) const {
-    std::string s = "v_cmp_lt_u32 vcc, s71, v29\n";
+    std::string s;
     if (!exact) return s + "s_cbranch_vccnz .L" + P + "budget\n";
     const std::string ok = ".L" + P + "bok" + std::to_string(i);
     return s + "s_cbranch_vccz " + ok + "\ns_mov_b64 s[64:65], exec\ns_mov_b64 exec, vcc\n"
@@ -813,6 +859,7 @@ struct Compiler {
     const std::string P = "J" + m.n + "_", PX = "J" + m.n + "x_";
     std::string main = "; compiled eBPF loop program: " + std::to_string(n) + " micro-ops\n"
                        "s_mov_b32 s52, s33\ns_mov_b32 s53, 0\ns_movk_i32 s56, 0xff\n"
+                       "s_not_b32 s57, s71\ns_mov_b64 exec, -1\nv_add_u32 v29, s57, v29\n"
                        "s_cmp_lg_u32 s70, 0\ns_cbranch_scc1 .L" + PX + "start\n"
                        "s_mov_b64 exec, 0\n";
     std::string ool;
@@ -825,10 +872,42 @@ struct Compiler {
       err = xc.err;
       return false;
     }
-    main += ".L" + P + "end:\n";
+    main += ".L" + P + "end:\ns_mov_b64 exec, -1\nv_subrev_u32 v29, s57, v29\n";
     if (!ool.empty()) main += "s_branch .Ldone" + m.n + "\n" + ool;
-    out = main;
+    out = peephole(main);
     return true;
+  }
+
+  // mov + add of the same 64-bit destination in a row (e.g. `mov r4, r1; add r4, r3`, adjacent
+  // micro-ops with no block entry between them): one add from the moved source.
+  static std::string peephole(const std::string& text) {
+    std::vector<std::string> ln;
+    for (size_t p = 0; p < text.size();) {
+      size_t e = text.find('\n', p);
+      if (e == std::string::npos) e = text.size();
+      ln.push_back(text.substr(p, e - p));
+      p = e + 1;
+    }
+    std::string out;
+    for (size_t i = 0; i < ln.size(); i++) {
+      uint32_t d0, d1, s0, s1;
+      char rest[128];
+      if (i + 1 < ln.size() &&
+          sscanf(ln[i].c_str(), "v_mov_b64 v[%u:%u], v[%u:%u]", &d0, &d1, &s0, &s1) == 4) {
+        const std::string D = "v[" + std::to_string(d0) + ":" + std::to_string(d1) + "]";
+        const std::string head = "v_lshl_add_u64 " + D + ", " + D + ", 0, ";
+        if (ln[i + 1].compare(0, head.size(), head) == 0 &&
+            sscanf(ln[i + 1].c_str() + head.size(), "%127s", rest) == 1 &&
+            ln[i + 1].find(D, head.size()) == std::string::npos) {
+          out += "v_lshl_add_u64 " + D + ", v[" + std::to_string(s0) + ":" + std::to_string(s1) +
+                 "], 0, " + ln[i + 1].substr(head.size()) + "\n";
+          i++;
+          continue;
+        }
+      }
+      out += ln[i] + "\n";
+    }
+    return out;
   }
 };
 
