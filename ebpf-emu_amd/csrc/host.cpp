@@ -225,6 +225,10 @@ struct ebpf_prog {
   Uop* dev_uops[kMaxDevices] = {};
   DUop* dev_duops[kMaxDevices] = {};
   DUop* dev_duopsk[kMaxDevices] = {};
+  // memory tier 0.5 (analyze_stack): the stack window, and the constant-address loads the compiled
+  // code reads from the header window without a run-time window check: (address, width)
+  StackPlan stack;
+  std::vector<std::pair<uint64_t, uint32_t>> kloads;
   std::vector<TUop> tuops, tuopsk;  // tile_kernel's tables (forward-only, <= 62 micro-ops)
   TUop* dev_tuops[kMaxDevices] = {};
   TUop* dev_tuopsk[kMaxDevices] = {};
@@ -266,7 +270,8 @@ static int jit_compile_locked(ebpf_prog* p) {
   if (p->jit_state == 0) {
     p->jit_has[0] = p->jit_has[1] = !p->tuops.empty() && !p->tuopsk.empty();
     p->jit_has[2] = !p->ltuops.empty() && !p->ltuopsx.empty();
-    if (g_no_jit || (!p->jit_has[0] && !p->jit_has[2])) {
+    if (p->stack.k) p->jit_has[1] = true;  // (the main.rs layout's fixed-slot kernel only)
+    if (g_no_jit || (!p->jit_has[0] && !p->jit_has[1] && !p->jit_has[2])) {
       p->jit_state = 2;
     } else {
       p->jit_state = 1;
@@ -275,7 +280,8 @@ static int jit_compile_locked(ebpf_prog* p) {
         const bool ok = v == 2 ? jit_compile_loop(p->uops, p->ltuops, p->ltuopsx, p->jit_co[v],
                                                   &p->jit_err, &p->jit_asm[v])
                                : jit_compile(p->uops, v ? p->tuopsk : p->tuops, p->jit_co[v],
-                                             &p->jit_err, &p->jit_asm[v]);
+                                             &p->jit_err, &p->jit_asm[v],
+                                             p->stack.k ? &p->stack : nullptr);
         if (!ok) p->jit_state = EBPF_EJIT;
       }
       if (p->jit_state == EBPF_EJIT && getenv("EBPFEMU_JIT_VERBOSE"))
@@ -296,6 +302,12 @@ constexpr uint64_t kBinMinPackets = 16384;
 // A/B: EBPFEMU_NO_LOOP=1 runs loop programs on the general interpreter (interp_kernel).
 static const bool g_no_loop = [] {
   const char* e = getenv("EBPFEMU_NO_LOOP");
+  return e && e[0] == '1';
+}();
+
+// EBPFEMU_NO_STACK=1: no memory tier 0.5 (stack-window programs run on interp_kernel tier 1).
+static const bool g_no_stack = [] {
+  const char* e = getenv("EBPFEMU_NO_STACK");
   return e && e[0] == '1';
 }();
 
@@ -428,7 +440,7 @@ static std::vector<DUop> build_dag(const std::vector<Uop>& uops) {
 // runs its successor next on the same lanes without touching the pc set (basic-block chaining).
 // exact: every micro-op its own block (the loop mode's exact-budget table).
 static std::vector<TUop> build_tile(const std::vector<Uop>& uops, const std::vector<DUop>& d,
-                                    bool exact = false) {
+                                    bool exact = false, bool stack = false) {
   const uint32_t n = (uint32_t)uops.size();
   std::vector<TUop> t(kTileUops);
   std::memset(t.data(), 0, t.size() * sizeof(TUop));
@@ -440,7 +452,9 @@ static std::vector<TUop> build_tile(const std::vector<Uop>& uops, const std::vec
     const uint32_t h = d[i].hoff / DAG_SLOT;
     const bool is_jump = uops[i].op >= U_JA && uops[i].op <= U_JLE32;
     if (is_jump && (uint32_t)uops[i].x < n) start[(uint32_t)uops[i].x] = 1;
-    term[i] = exact || is_jump || h == H_EXIT || h == H_FAULT || h == H_SLOW;
+    // (a stack-window program's stores are compiled in line: jit.cpp, not block ends)
+    const bool stack_store = stack && (uops[i].op == U_ST || uops[i].op == U_STX);
+    term[i] = exact || is_jump || h == H_EXIT || h == H_FAULT || (h == H_SLOW && !stack_store);
     if (term[i]) start[i + 1] = 1;
   }
   // rem[i]: micro-ops from i to the end of its block (steps not retired when i faults);
@@ -585,6 +599,116 @@ static std::vector<DUop> fold_const_loads(const std::vector<Uop>& uops, std::vec
   return d;
 }
 
+// Memory tier 0.5 (stack-window programs): a forward-only program of <= kTileMaxUops micro-ops
+// whose only memory writes are ST/STX at r10 + c for a c known at load time (the XDP spill / key
+// pattern: `stxdw [r10-8], r3`, also through a copy such as `mov r2, r10; add r2, -16`), with no
+// ATOMIC or CALL. A load-time dataflow over the main.rs register layout (main.rs:28-31) tracks
+// each register as unknown, a constant, or r10 + c; every store must be r10 + c on all paths, with
+// all its bytes in [r10 - k, r10) for the window size k <= kStackMax (emu.rs:354-372; the
+// reference has no separate stack -- r10 is just a register into the flat image, which is why the
+// launch also checks that the window lies inside the image, past the packet, and away from every
+// constant-address load). Loads whose base is r10 + c and whose bytes lie in the window read it
+// directly; loads partly inside it make the program ineligible; every other load is checked
+// against the window at run time (a store-forwarding overlay).
+struct StackAnalysis {
+  StackPlan plan;  // k = 0: not a stack-window program
+};
+
+static StackAnalysis analyze_stack(const std::vector<Uop>& uops) {
+  StackAnalysis res;
+  const uint32_t n = (uint32_t)uops.size();
+  if (n == 0 || n > kTileMaxUops) return res;
+  bool any_store = false;
+  for (uint32_t i = 0; i < n; i++) {
+    const Uop& u = uops[i];
+    if (u.op == U_ATOMIC || u.op == U_CALL) return res;
+    if (u.op >= U_JA && u.op <= U_JLE32 && (uint32_t)u.x <= i) return res;  // forward only
+    any_store = any_store || u.op == U_ST || u.op == U_STX;
+  }
+  if (!any_store) return res;
+  enum Kind : uint8_t { TOP, CONST, FP };
+  struct Val { Kind k = TOP; int64_t v = 0; };
+  struct Regs { bool reached = false; Val r[11]; };
+  std::vector<Regs> in(n + 1);
+  in[0].reached = true;
+  for (int r = 0; r < 11; r++) in[0].r[r] = Val{CONST, 0};
+  in[0].r[2] = Val{TOP, 0};   // len
+  in[0].r[10] = Val{FP, 0};   // r10 itself
+  auto same = [](const Val& a, const Val& b) { return a.k == b.k && (a.k == TOP || a.v == b.v); };
+  auto flow = [&](uint32_t to, const Regs& st) {
+    if (to >= n) return;
+    Regs& t = in[to];
+    if (!t.reached) { t = st; return; }
+    for (int r = 0; r < 11; r++)
+      if (!same(t.r[r], st.r[r])) t.r[r] = Val{TOP, 0};
+  };
+  std::vector<int32_t> off(n, kNoStack);
+  std::vector<char> dyn(n, 0);  // LDX with an unknown base
+  int64_t lo = 0, hi = INT64_MIN;  // store bytes relative to r10: [lo, hi)
+  for (uint32_t i = 0; i < n; i++) {
+    if (!in[i].reached) continue;
+    const Uop& u = uops[i];
+    Regs st = in[i];
+    const bool src = u.aux & F_SRC;
+    const Val S = st.r[u.src], D = st.r[u.dst];
+    if (u.op == U_ST || u.op == U_STX) {
+      if (D.k != FP) return res;
+      const int64_t d = D.v + (int64_t)u.x;
+      if (d < -(int64_t)kStackMax || d + u.aux > 0) return res;
+      off[i] = (int32_t)d;
+      lo = std::min(lo, d);
+      hi = std::max(hi, d + (int64_t)u.aux);
+    }
+    if (u.op == U_LDX) {
+      if (S.k == FP) off[i] = (int32_t)std::max<int64_t>(INT32_MIN + 1, std::min<int64_t>(INT32_MAX, S.v + u.x));
+      else dyn[i] = 1;
+    }
+    switch (u.op) {
+      case U_JA: case U_JEQ: case U_JGT: case U_JGE: case U_JSET: case U_JNE: case U_JLT:
+      case U_JLE: case U_JEQ32: case U_JGT32: case U_JGE32: case U_JSET32: case U_JNE32:
+      case U_JLT32: case U_JLE32:
+        flow((uint32_t)u.x, st);
+        if (u.op != U_JA) flow(i + 1, st);
+        continue;
+      case U_EXIT: case U_FAULT:
+        continue;
+      case U_ST: case U_STX: case U_NOP:
+        break;  // the destination register keeps its value (emu.rs:443)
+      case U_MOV64: st.r[u.dst] = src ? S : Val{CONST, u.k}; break;
+      case U_LDIMM: st.r[u.dst] = Val{CONST, u.k}; break;
+      case U_ADD64: case U_SUB64: {
+        const Val B = src ? S : Val{CONST, u.k};
+        const bool sub = u.op == U_SUB64;
+        Val r{TOP, 0};
+        if (B.k == CONST && (D.k == CONST || D.k == FP))
+          r = Val{D.k, (int64_t)((uint64_t)D.v + (sub ? 0 - (uint64_t)B.v : (uint64_t)B.v))};
+        else if (!sub && D.k == CONST && B.k == FP)
+          r = Val{FP, (int64_t)((uint64_t)D.v + (uint64_t)B.v)};
+        st.r[u.dst] = r;
+        break;
+      }
+      default: st.r[u.dst] = Val{TOP, 0}; break;
+    }
+    flow(i + 1, st);
+  }
+  const uint32_t k = (uint32_t)((-lo + 3) & ~3);
+  if (hi > 0 || k == 0 || k > kStackMax) return res;
+  for (uint32_t i = 0; i < n; i++) {
+    const Uop& u = uops[i];
+    if (u.op != U_LDX || off[i] == kNoStack) continue;
+    const int64_t d = off[i];
+    if (d >= -(int64_t)k && d + u.aux <= 0) continue;       // inside the window
+    if (d + u.aux <= -(int64_t)k || d >= 0) {                 // disjoint: an ordinary load at a
+      off[i] = kNoStack;                                      // uniform address, checked at run
+      continue;                                               // time like any other
+    }
+    return res;                                               // straddles the window's edge
+  }
+  res.plan.k = k;
+  res.plan.off = std::move(off);
+  return res;
+}
+
 extern "C" {
 
 void ebpf_batch_init(ebpf_batch* b) {
@@ -630,6 +754,16 @@ int ebpf_prog_load(const uint8_t* code, size_t nbytes, ebpf_prog** out, size_t* 
     const std::vector<DUop> d = p->duops.empty() ? build_dag(p->uops) : p->duops;
     p->ltuops = build_tile(p->uops, d);
     p->ltuopsx = build_tile(p->uops, d, true);
+  }
+  if (p->tier == 1 && !g_no_stack) {  // memory tier 0.5: the compiled fixed-slot kernel only
+    StackAnalysis sa = analyze_stack(p->uops);
+    if (sa.plan.k) {
+      const std::vector<DUop> dk = fold_const_loads(p->uops, build_dag(p->uops));
+      for (const DUop& o : dk)
+        if ((o.opaux & 0xff) == U_LDXK) p->kloads.push_back({o.addr, o.opaux >> 8});
+      p->tuopsk = build_tile(p->uops, dk, false, true);
+      p->stack = std::move(sa.plan);
+    }
   }
   *out = p;
   return EBPF_OK;
@@ -687,6 +821,8 @@ int ebpf_prog_insn(const ebpf_prog* p, size_t i, int32_t* imm, int64_t* imm64, i
 int ebpf_prog_tier(const ebpf_prog* p) { return p ? p->tier : -1; }
 
 int ebpf_prog_forward_only(const ebpf_prog* p) { return p ? (p->duops.empty() ? 0 : 1) : -1; }
+
+int ebpf_prog_stack_window(const ebpf_prog* p) { return p ? (int)p->stack.k : -1; }
 
 int ebpf_prog_compile(ebpf_prog* p) {
   if (!p) return EBPF_EINVAL;
@@ -800,6 +936,49 @@ static int batch_tier(const ebpf_prog* p, const ebpf_batch* b) {
   return p->tier == 1 || b->init_fp_len ? 1 : 0;
 }
 
+// Memory tier 0.5 (analyze_stack) on this batch: the compiled fixed-slot kernel with the main.rs
+// register layout, and a window [r10 - k, r10) that lies in the image, past every packet byte (so
+// it starts as zeros) and away from every constant-address load; else the general interpreter.
+static bool stack_launch_ok(const ebpf_prog* p, const ebpf_batch* b, const ebpf_batch_out* out,
+                            int device) {
+  if (!p->stack.k || !p->jit_mod[device][1]) return false;
+  if (b->flags & (EBPF_BATCH_GENERIC | EBPF_BATCH_NO_JIT | EBPF_BATCH_XDP_MD)) return false;
+  if (b->init_regs || b->init_fp_len || out->mem || b->max_steps < p->uops.size()) return false;
+  const uint64_t k = p->stack.k, r10 = b->r10;
+  if (r10 % 4 || r10 < k || r10 > b->mem_size || r10 - k < b->stride) return false;
+  for (const auto& kl : p->kloads)
+    if (kl.first < r10 && kl.first + kl.second > r10 - k) return false;
+  LaunchArgs a{};
+  a.frames = b->frames;
+  a.offsets = b->offsets;
+  a.lens = b->lens;
+  a.stride = b->stride;
+  a.mem_out = out->mem;
+  return launch_fixed_layout(a);
+}
+
+// The kernel kind of a batch (uploaded program): dag_kernel needs no step budget (a lane of a
+// forward-only program retires <= n_uops steps); the tile kernel in loop mode runs loops, or a
+// step budget that can bind (exact budget); a stack-window batch runs the compiled fixed-slot kernel.
+static int batch_kind(const ebpf_prog* p, const ebpf_batch* b, const ebpf_batch_out* out,
+                      int device, bool* stk) {
+  const bool generic = g_no_dag || (b->flags & EBPF_BATCH_GENERIC) || b->init_fp_len;
+  *stk = !generic && stack_launch_ok(p, b, out, device);
+  return *stk ? kKindDag
+         : (p->dev_duops[device] && b->max_steps >= p->uops.size() && !generic) ? kKindDag
+         : (p->dev_ltuops[device] && !generic && !g_no_loop)            ? kKindLoop
+                                                                         : batch_tier(p, b);
+}
+
+// The compiled program, where it applies (tile-kernel programs; same tables, same results).
+static const JitFns* batch_jit(ebpf_prog* p, const ebpf_batch* b, int kind, bool stk, int device) {
+  if (stk) return &p->jit_fn[device][1];
+  if (b->flags & EBPF_BATCH_NO_JIT) return nullptr;
+  if (kind == kKindDag && p->jit_mod[device][0]) return &p->jit_fn[device][b->init_regs ? 0 : 1];
+  if (kind == kKindLoop && p->jit_mod[device][2]) return &p->jit_fn[device][2];
+  return nullptr;
+}
+
 uint64_t ebpf_workspace_bytes(const ebpf_prog* p, const ebpf_batch* b, int device) {
   if (!p || !b) return 0;
   const uint64_t x = (b->flags & EBPF_BATCH_XDP_MD) ? xdp_region_bytes(b) : 0;
@@ -851,12 +1030,8 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* bin, const ebpf_batch_out* ou
   if (cur != device) hipSetDevice(device);
 
   const uint64_t n_tiles = (b->n + 63) / 64;
-  // dag_kernel needs no step budget: a lane of a forward-only program retires <= n_uops steps
-  // the tile kernel in loop mode: loops, or a step budget that can bind (exact budget)
-  const bool generic = g_no_dag || (b->flags & EBPF_BATCH_GENERIC) || b->init_fp_len;
-  const int kind = (p->dev_duops[device] && b->max_steps >= p->uops.size() && !generic) ? kKindDag
-                   : (p->dev_ltuops[device] && !generic && !g_no_loop)            ? kKindLoop
-                                                                                   : batch_tier(p, b);
+  bool stk = false;
+  const int kind = batch_kind(p, b, out, device, &stk);
   int grid = 0;
   if (interp_grid(kind, (uint32_t)p->uops.size(), p->tiny, n_tiles, &grid) != 0) {
     if (cur != device) hipSetDevice(cur);
@@ -965,15 +1140,35 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* bin, const ebpf_batch_out* ou
       return EBPF_EHIP;
     }
   }
-  // the compiled program, where it applies (tile-kernel programs; same tables, same results)
-  const JitFns* jit = nullptr;
-  if (kind == kKindDag && !(b->flags & EBPF_BATCH_NO_JIT) && p->jit_mod[device][0])
-    jit = &p->jit_fn[device][b->init_regs ? 0 : 1];
-  if (kind == kKindLoop && !(b->flags & EBPF_BATCH_NO_JIT) && p->jit_mod[device][2])
-    jit = &p->jit_fn[device][2];
+  const JitFns* jit = batch_jit(p, b, kind, stk, device);
   hipError_t e = launch_interp(kind, a, grid, s, jit);
   if (cur != device) hipSetDevice(cur);
   return e == hipSuccess ? EBPF_OK : EBPF_EHIP;
+}
+
+int ebpf_batch_kernel(ebpf_prog* p, const ebpf_batch* bin, const ebpf_batch_out* out, int device) {
+  if (!p || !out || device < 0 || device >= kMaxDevices) return EBPF_EINVAL;
+  int rc = check_batch(bin);
+  if (rc) return rc;
+  rc = ebpf_prog_upload(p, device);
+  if (rc) return rc;
+  ebpf_batch staged = *bin;  // xdp_md batches run as offsets + lens batches
+  if (bin->flags & EBPF_BATCH_XDP_MD) {
+    staged.offsets = (const uint32_t*)16;
+    staged.lens = (const uint16_t*)16;
+    staged.stride = 0;
+    staged.flags &= ~EBPF_BATCH_XDP_MD;
+  }
+  bool stk = false;
+  const int kind = batch_kind(p, bin, out, device, &stk);
+  LaunchArgs a{};
+  a.n_uops = (uint32_t)p->uops.size();
+  a.frames = staged.frames;
+  a.offsets = staged.offsets;
+  a.lens = staged.lens;
+  a.stride = staged.stride;
+  a.mem_out = out->mem;
+  return launch_kernel_id(kind, a, batch_jit(p, &staged, kind, stk, device), stk);
 }
 
 int ebpf_run_batch_multi(ebpf_prog* p, int nshards, const int* devices, const ebpf_batch* batches,

@@ -1315,8 +1315,10 @@ constexpr uint32_t kTileWaveLds = kWinBytes + kDagMetaBytes;  // window + metada
 #define TILE_ASM_CLOBBER "s33", "s34", "s35", "s36", "s37", "s38", "s39", "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53", "s54", "s55", "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71", "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15", "v16", "v17", "v18", "v19", "v20", "v21", "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32", "v33", "v34", "v35", "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", "vcc", "scc", "memory"
 #define TILE_ASM_OPERANDS : TILE_ASM_OUT : TILE_ASM_IN : TILE_ASM_CLOBBER
 // the compiled programs' preloaded window dwords (jit.cpp ldxk_fast): v[64:79]
+// and the stack window of memory tier 0.5 (jit.h kStackVgpr, kStackMax / 4 dwords): v[80:95]
 #define TILE_ASM_CLOBBER_WINDOW "v64", "v65", "v66", "v67", "v68", "v69", "v70", "v71", "v72", \
-    "v73", "v74", "v75", "v76", "v77", "v78", "v79"
+    "v73", "v74", "v75", "v76", "v77", "v78", "v79", "v80", "v81", "v82", "v83", "v84", "v85", \
+    "v86", "v87", "v88", "v89", "v90", "v91", "v92", "v93", "v94", "v95"
 
 
 // JIT: the statement of the compiled-program template kernels (tile_jit.inc; jit.cpp fills in the
@@ -1620,6 +1622,8 @@ static bool fixed_layout(const LaunchArgs* a) {
          a->stride >= (uint64_t)kWin && (((uintptr_t)a->frames | (uintptr_t)a->stride) & 15) == 0;
 }
 
+bool launch_fixed_layout(const LaunchArgs& a) { return fixed_layout(&a) && !g_no_tile; }
+
 static const void* kernel_for(int kind, uint32_t n_uops, const LaunchArgs* a = nullptr) {
   if (kind == kKindDag) {
     if (tile_kernel_for(kind, n_uops))
@@ -1717,6 +1721,17 @@ static int jit_grid(hipFunction_t f, uint32_t lds, uint64_t n_tiles, int block =
   const uint64_t per_wave = (tiles + resident - 1) / resident;
   const uint64_t waves = (tiles + per_wave - 1) / per_wave;
   return (int)((waves + wpb - 1) / wpb);
+}
+
+int launch_kernel_id(int kind, const LaunchArgs& a, const JitFns* jit, bool stack) {
+  if (jit && jit->loop && kind == kKindLoop) return EBPF_KERNEL_JIT_LOOP;
+  if (jit && jit->fixed && kind == kKindDag && tile_kernel_for(kind, a.n_uops))
+    return fixed_layout(&a) ? (stack ? EBPF_KERNEL_JIT_STACK : EBPF_KERNEL_JIT_FIXED)
+                            : EBPF_KERNEL_JIT_VAR;
+  if (kind == kKindDag)
+    return tile_kernel_for(kind, a.n_uops) ? EBPF_KERNEL_TILE : EBPF_KERNEL_DAG;
+  if (kind == kKindLoop) return EBPF_KERNEL_TILE_LOOP;
+  return kind == kKindTier1 ? EBPF_KERNEL_GENERAL_T1 : EBPF_KERNEL_GENERAL_T0;
 }
 
 hipError_t launch_interp(int kind, const LaunchArgs& a, int grid, hipStream_t stream,

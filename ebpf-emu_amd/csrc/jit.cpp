@@ -222,8 +222,11 @@ struct Compiler {
 
   static bool is_jump(const Uop& o) { return o.op >= U_JA && o.op <= U_JLE32; }
 
-  Compiler(const std::vector<Uop>& u, const std::vector<TUop>& tt, bool lp = false, bool ex = false)
-      : uops(u), t(tt), n((uint32_t)u.size()), loops(lp), exact(ex) {
+  const StackPlan* stk = nullptr;  // a stack-window program (memory tier 0.5)
+
+  Compiler(const std::vector<Uop>& u, const std::vector<TUop>& tt, bool lp = false, bool ex = false,
+           const StackPlan* sp = nullptr)
+      : uops(u), t(tt), n((uint32_t)u.size()), loops(lp), exact(ex), stk(sp) {
     start.assign(n + 1, 0);
     target.assign(n + 1, 0);
     target[0] = 1;
@@ -294,6 +297,8 @@ struct Compiler {
       } else if (u.op == U_LDX) {
         rd = d | (1u << u.src);
         wr = d;
+      } else if (u.op == U_STX) {
+        rd = 1u << u.src;  // (the address r10 + c is resolved at load time)
       }
     };
     for (bool changed = true; changed;) {  // one pass without back edges; to a fixpoint with
@@ -575,6 +580,123 @@ struct Compiler {
   // byte is read with ds_read_u8 at its swizzled window address, zeroed past len by the same
   // mask, and merged with the 0xff in s56 (set once per program). The window refill (or, in
   // tiles with unaligned packets, the packet dword's load) is out of line.
+  // ---- memory tier 0.5: the stack window [r10 - k, r10) in v[kStackVgpr + j] (dword j) ----
+  std::string sv(uint32_t j) const { return "v" + std::to_string(kStackVgpr + j); }
+
+  // LDX from the window at byte p = k + off (static): the bytes merged into dst as the handlers
+  // do (Q1, emu.rs:341-349) -- ldxk_fast's code over the window registers.
+  std::string stack_load(uint32_t i) const {
+    const Uop& o = uops[i];
+    const uint32_t p = (uint32_t)((int32_t)stk->k + stk->off[i]), width = o.aux, sh = p & 3, d = p >> 2;
+    const std::string D0 = "v" + std::to_string(2 * o.dst), D1 = "v" + std::to_string(2 * o.dst + 1);
+    auto W = [&](uint32_t q) { return sv(q); };
+    if (width == 8) {
+      if (sh == 0) return "v_mov_b32 " + D0 + ", " + W(d) + "\nv_mov_b32 " + D1 + ", " + W(d + 1) + "\n";
+      return "v_alignbyte_b32 " + D0 + ", " + W(d + 1) + ", " + W(d) + ", " + std::to_string(sh) +
+             "\nv_alignbyte_b32 " + D1 + ", " + W(d + 2) + ", " + W(d + 1) + ", " +
+             std::to_string(sh) + "\n";
+    }
+    std::string s, src = W(d);
+    uint32_t off = sh;
+    if (sh + width > 4 && width == 4)
+      return "v_alignbyte_b32 " + D0 + ", " + W(d + 1) + ", " + W(d) + ", " + std::to_string(sh) + "\n";
+    if (sh + width > 4) {
+      s += "v_alignbyte_b32 v26, " + W(d + 1) + ", " + W(d) + ", " + std::to_string(sh) + "\n";
+      src = "v26";
+      off = 0;
+    }
+    if (width == 4) return s + "v_mov_b32 " + D0 + ", " + src + "\n";
+    uint32_t sel = 0;
+    for (uint32_t b = 0; b < 4; b++) sel |= (b < width ? 4 + off + b : b) << (8 * b);
+    return s + "s_mov_b32 s36, " + hex32(sel) + "\nv_perm_b32 " + D0 + ", " + src + ", " + D0 + ", s36\n";
+  }
+
+  // ST / STX into the window at byte p = k + off (static): the low `width` bytes of the value
+  // (STX: src register; ST: the zero-extended immediate, Q8) written little-endian
+  // (emu.rs:354-372). Per window dword the bytes it takes, by a move (whole dword) or a v_perm.
+  std::string stack_store(uint32_t i) const {
+    const Uop& o = uops[i];
+    const uint32_t p = (uint32_t)((int32_t)stk->k + stk->off[i]), w = o.aux;
+    const bool imm = o.op == U_ST;
+    const uint64_t kv = (uint64_t)o.k;  // ST: imm64 (zero-extended imm)
+    const std::string V0 = "v" + std::to_string(2 * o.src), V1 = "v" + std::to_string(2 * o.src + 1);
+    std::string s;
+    for (uint32_t j = p >> 2; j <= (p + w - 1) >> 2; j++) {
+      const uint32_t lo = std::max(p, 4 * j), hi = std::min(p + w, 4 * j + 4);
+      const int32_t sft = (int32_t)(4 * j) - (int32_t)p;  // value byte at this dword's byte 0
+      // t: a dword whose byte q is value byte q + sft (where that byte is used)
+      std::string t;
+      uint32_t tc = 0;  // (ST) the constant t
+      if (imm) {
+        for (uint32_t q = 0; q < 4; q++) {
+          const int32_t vb = (int32_t)q + sft;
+          if (vb >= 0 && vb < 8) tc |= (uint32_t)((kv >> (8 * vb)) & 0xff) << (8 * q);
+        }
+      } else if (sft == 0) {
+        t = V0;
+      } else if (sft == 4) {
+        t = V1;
+      } else if (sft > 0 && sft < 4) {
+        s += "v_alignbyte_b32 v42, " + V1 + ", " + V0 + ", " + std::to_string(sft) + "\n";
+        t = "v42";
+      } else if (sft > 4) {
+        s += "v_alignbyte_b32 v42, 0, " + V1 + ", " + std::to_string(sft - 4) + "\n";
+        t = "v42";
+      } else {  // sft < 0: the first dword of a misaligned store
+        s += "v_lshlrev_b32 v42, " + std::to_string(-sft * 8) + ", " + V0 + "\n";
+        t = "v42";
+      }
+      if (lo == 4 * j && hi == 4 * j + 4) {  // the whole dword
+        s += imm ? "v_mov_b32 " + sv(j) + ", " + hex32(tc) + "\n" : "v_mov_b32 " + sv(j) + ", " + t + "\n";
+        continue;
+      }
+      uint32_t sel = 0;
+      for (uint32_t q = 0; q < 4; q++)
+        sel |= (4 * j + q >= lo && 4 * j + q < hi ? 4 + q : q) << (8 * q);
+      if (imm) {
+        s += "v_mov_b32 v42, " + hex32(tc) + "\n";
+        t = "v42";
+      }
+      s += "s_mov_b32 s36, " + hex32(sel) + "\nv_perm_b32 " + sv(j) + ", " + t + ", " + sv(j) +
+           ", s36\n";
+    }
+    return s;
+  }
+
+  // A register-address load of a stack-window program: the lanes whose bytes [a, a + w) overlap
+  // the window (a - S0 < k or a + w - 1 - S0 < k, u32, S0 = r10 - k in s57) take the window's bytes
+  // instead of the image's (store forwarding); the value v[26:27] is patched byte by byte, each
+  // byte's window dword picked by a compare/select chain. Out of line; returns the check.
+  std::string stack_overlay(const std::string& U, uint32_t w, std::string& ool) const {
+    const uint32_t k = stk->k;
+    std::string s = "v_subrev_u32 v44, s57, v36\n"
+                    "v_add_u32 v45, " + std::to_string(w - 1) + ", v44\n"
+                    "v_cmp_gt_u32 vcc, " + std::to_string(k) + ", v44\n"
+                    "v_cmp_gt_u32 s[60:61], " + std::to_string(k) + ", v45\n"
+                    "s_or_b64 vcc, vcc, s[60:61]\n"
+                    "s_cbranch_vccnz .Lovl" + U + "\n"
+                    ".Lovd" + U + ":\n";
+    std::string o = ".Lovl" + U + ":\ns_mov_b64 s[66:67], exec\ns_mov_b64 exec, vcc\n";
+    for (uint32_t j = 0; j < w; j++) {
+      const std::string T = j < 4 ? "v26" : "v27";
+      const uint32_t q = j & 3;
+      o += "v_add_u32 v46, " + std::to_string(j) + ", v44\n"
+           "v_cmp_gt_u32 s[68:69], " + std::to_string(k) + ", v46\n"
+           "v_lshrrev_b32 v47, 2, v46\nv_mov_b32 v48, 0\n";
+      for (uint32_t d = 0; d < k / 4; d++)
+        o += "v_cmp_eq_u32 vcc, " + std::to_string(d) + ", v47\nv_cndmask_b32 v48, v48, " + sv(d) +
+             ", vcc\n";
+      uint32_t sel = 0;
+      for (uint32_t b = 0; b < 4; b++) sel |= (b == q ? 4u : b) << (8 * b);
+      o += "v_and_b32 v49, 3, v46\nv_lshlrev_b32 v49, 3, v49\nv_bfe_u32 v48, v48, v49, 8\n"
+           "s_mov_b32 s36, " + hex32(sel) + "\nv_perm_b32 v49, v48, " + T + ", s36\n"
+           "v_cndmask_b32_e64 " + T + ", " + T + ", v49, s[68:69]\n";
+    }
+    o += "s_mov_b64 exec, s[66:67]\ns_branch .Lovd" + U + "\n";
+    ool += o;
+    return s;
+  }
+
   // kJitRefill with the address's low word in register A instead of v36
   static std::string refill(const std::string& A) {
     std::string r(kJitRefill);
@@ -701,6 +823,7 @@ struct Compiler {
       if (w == 8) win += "v_alignbyte_b32 v27, v51, v50, v36\n";
     }
     s += win + ".Lmrg" + U + ":\n";
+    if (stk) s += stack_overlay(U, w, ool);
     if (w == 1 || w == 2)
       s += "s_mov_b32 s42, " + std::string(w == 1 ? "0xff" : "0xffff") + "\nv_bfi_b32 " + D0 +
            ", s42, v26, " + D0 + "\n";
@@ -759,6 +882,15 @@ struct Compiler {
       if (id >= (uint32_t)T_COUNT || id == (uint32_t)T_DONE) {
         err = "bad handler id";
         return false;
+      }
+      if (stk && (uops[i].op == U_ST || uops[i].op == U_STX)) {
+        // (a store the load-time dataflow never reached has no offset: no lane executes it)
+        main += stk->off[i] == kNoStack ? std::string("; unreachable store\n") : stack_store(i);
+        continue;
+      }
+      if (stk && uops[i].op == U_LDX && stk->off[i] != kNoStack) {
+        main += stack_load(i);
+        continue;
       }
       if (fast && is_ldxk(id)) {
         main += ldxk_fast(i);
@@ -821,6 +953,15 @@ struct Compiler {
     const std::string P = "J" + m.n + "_";
     std::string main = "; compiled eBPF program: " + std::to_string(n) + " micro-ops\n"
                        "s_mov_b32 s52, s33\ns_mov_b32 s53, 0\n";
+    if (stk) {  // the window starts as the image's bytes there: zeros (the launch checked that it
+                // lies past every packet byte); s57 = its image address S0 = r10 - k (s48 = r10)
+      main += "; stack window: " + std::to_string(stk->k) + " bytes\ns_sub_u32 s57, s48, " +
+              std::to_string(stk->k) + "\n";
+      for (uint32_t j = 0; j < stk->k / 4; j += 2)
+        main += j + 1 < stk->k / 4 ? "v_mov_b64 v[" + std::to_string(kStackVgpr + j) + ":" +
+                                         std::to_string(kStackVgpr + j + 1) + "], 0\n"
+                                   : "v_mov_b32 " + sv(j) + ", 0\n";
+    }
     std::string ool;
     uint32_t chunks = 0, maxend = 0;
     if (m.fixed == "1")
@@ -1006,7 +1147,7 @@ bool compile_into_template(Compiler& c, Compiler* xc, std::vector<char>& code_ob
     std::string b;
     const bool loop_marker = m.loops == "1";
     bool ok = true;
-    if (loop_marker != (xc != nullptr))
+    if (loop_marker != (xc != nullptr) || (c.stk && m.fixed != "1"))
       b = "s_mov_b64 exec, 0  ; (not this program's kernel)\n";
     else
       ok = xc ? c.body_loop(m, *xc, b) : c.body(m, b);
@@ -1028,12 +1169,14 @@ bool compile_into_template(Compiler& c, Compiler* xc, std::vector<char>& code_ob
 }  // namespace
 
 bool jit_compile(const std::vector<Uop>& uops, const std::vector<TUop>& t,
-                 std::vector<char>& code_object, std::string* err, std::string* asm_out) {
-  if (uops.empty() || uops.size() > kTileMaxUops || t.size() < uops.size()) {
+                 std::vector<char>& code_object, std::string* err, std::string* asm_out,
+                 const StackPlan* stk) {
+  if (uops.empty() || uops.size() > kTileMaxUops || t.size() < uops.size() ||
+      (stk && (stk->k == 0 || stk->k > kStackMax || stk->k % 4 || stk->off.size() != uops.size()))) {
     if (err) *err = "not a tile program";
     return false;
   }
-  Compiler c(uops, t);
+  Compiler c(uops, t, false, false, stk);
   return compile_into_template(c, nullptr, code_object, err, asm_out);
 }
 

@@ -2,6 +2,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <climits>
+#include <cstdint>
 #include <string>
 #include <vector>
 
@@ -17,11 +19,25 @@ struct JitFns {
   hipFunction_t loop = nullptr;  // loop programs (ebpf_tile_jit_loop)
 };
 
+// Stack-window programs (memory tier 0.5, host.cpp analyze_stack): every store writes the
+// window [r10 - k, r10) at an offset known at load time, so the window lives in VGPRs of the
+// compiled fixed-slot kernel (v[kStackVgpr : kStackVgpr + k/4]).
+constexpr uint32_t kStackMax = 64;    // window bytes
+constexpr uint32_t kStackVgpr = 80;   // first VGPR of the window (ebpf_tile_jit_fixed)
+constexpr int32_t kNoStack = INT32_MIN;
+struct StackPlan {
+  uint32_t k = 0;            // window bytes (multiple of 4, <= kStackMax); 0 = no stack window
+  std::vector<int32_t> off;  // per micro-op: ST/STX, and LDX inside the window: the access's
+                             // offset from r10 (-k <= off, off + width <= 0); else kNoStack
+};
+
 // Compiles a forward-only program of <= kTileMaxUops micro-ops (its tile table `t`, built by
 // build_tile) into the assembly of the two template kernels, then assembles and links it
 // (amd_comgr) into a gfx950 code object. Returns false with a reason in *err on failure.
+// stk: a stack-window program (only the fixed-slot kernel gets its code).
 bool jit_compile(const std::vector<Uop>& uops, const std::vector<TUop>& t,
-                 std::vector<char>& code_object, std::string* err, std::string* asm_out = nullptr);
+                 std::vector<char>& code_object, std::string* err, std::string* asm_out = nullptr,
+                 const StackPlan* stk = nullptr);
 
 // Loop programs (back edges, or budgets that can bind; tile tables of build_tile: `t` the block
 // table, `tx` the exact one-micro-op-per-block table) for ebpf_tile_jit_loop.

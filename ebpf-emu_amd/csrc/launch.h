@@ -104,6 +104,14 @@ hipError_t launch_xdp_stage(const uint8_t* frames, const uint32_t* offsets, cons
                             uint32_t* doffs, uint16_t* dlens, unsigned long long* cursor,
                             hipStream_t stream);
 
+// Whether a launch runs the fixed-slot kernels (stride layout, 16-byte aligned slots of >= 64
+// bytes, no lengths, no image output; EBPFEMU_FIXED=0 disables them).
+bool launch_fixed_layout(const LaunchArgs& a);
+
+// The EBPF_KERNEL_* id of the kernel launch_interp runs for (kind, a, jit); stack: a memory
+// tier 0.5 batch.
+int launch_kernel_id(int kind, const LaunchArgs& a, const JitFns* jit, bool stack);
+
 // dst[0..7] += src[0..7] on `stream` (one tiny kernel).
 hipError_t launch_counters_add(const uint64_t* src, uint64_t* dst, hipStream_t stream);
 

@@ -28,11 +28,21 @@ BATCH_GENERIC = 1  # ebpf_batch.flags: EBPF_BATCH_GENERIC
 BATCH_XDP_MD = 2   # ebpf_batch.flags: EBPF_BATCH_XDP_MD (the xdp_md calling convention)
 BATCH_NO_JIT = 4   # ebpf_batch.flags: EBPF_BATCH_NO_JIT (the tile interpreter, not the compiled program)
 MAX_CALL_DEPTH = 64
+# ebpf_batch_kernel ids (EBPF_KERNEL_*)
+(EBPF_KERNEL_GENERAL_T0, EBPF_KERNEL_GENERAL_T1, EBPF_KERNEL_DAG, EBPF_KERNEL_TILE,
+ EBPF_KERNEL_TILE_LOOP, EBPF_KERNEL_JIT_FIXED, EBPF_KERNEL_JIT_VAR, EBPF_KERNEL_JIT_LOOP,
+ EBPF_KERNEL_JIT_STACK) = range(9)
+KERNEL_NAMES = ["ebpfemu::interp_kernel<0>", "ebpfemu::interp_kernel<1>", "ebpfemu::dag_kernel",
+                "ebpfemu::tile_kernel<forward>", "ebpfemu::tile_kernel<loops>",
+                "ebpf_tile_jit_fixed (compiled program)", "ebpf_tile_jit_var (compiled program)",
+                "ebpf_tile_jit_loop (compiled loop program)",
+                "ebpf_tile_jit_fixed (compiled stack-window program)"]
 
 EXPORTS = ["ebpf_batch_init", "ebpf_prog_load", "ebpf_prog_load_hex", "ebpf_prog_free",
            "ebpf_prog_len", "ebpf_prog_insn", "ebpf_prog_tier", "ebpf_prog_forward_only",
+           "ebpf_prog_stack_window",
            "ebpf_workspace_bytes", "ebpf_prog_compile", "ebpf_prog_jit_asm", "ebpf_debug_trace",
-           "ebpf_prog_upload", "ebpf_run_batch", "ebpf_run_batch_multi", "ebpf_pcap_index",
+           "ebpf_prog_upload", "ebpf_run_batch", "ebpf_run_batch_multi", "ebpf_batch_kernel", "ebpf_pcap_index",
            "ebpf_strerror", "ebpf_version"]
 
 
@@ -89,6 +99,7 @@ def lib():
                                  ctypes.POINTER(ctypes.c_uint8)]
     L.ebpf_prog_tier.argtypes = [vp]
     L.ebpf_prog_forward_only.argtypes = [vp]
+    L.ebpf_prog_stack_window.argtypes = [vp]
     L.ebpf_prog_compile.argtypes = [vp]
     L.ebpf_debug_trace.argtypes = [ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(sz)]
     L.ebpf_prog_jit_asm.argtypes = [vp, ctypes.c_int, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
@@ -96,6 +107,7 @@ def lib():
     L.ebpf_workspace_bytes.restype = u64
     L.ebpf_prog_upload.argtypes = [vp, ctypes.c_int]
     L.ebpf_run_batch.argtypes = [vp, ctypes.POINTER(Batch), ctypes.POINTER(BatchOut), vp]
+    L.ebpf_batch_kernel.argtypes = [vp, ctypes.POINTER(Batch), ctypes.POINTER(BatchOut), ctypes.c_int]
     L.ebpf_run_batch_multi.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
                                        ctypes.POINTER(Batch), ctypes.POINTER(BatchOut),
                                        ctypes.POINTER(vp)]

@@ -63,6 +63,12 @@ class Program:
         """True when batches run on the forward-jump fast path (max_steps >= len(self))."""
         return bool(_lib.lib().ebpf_prog_forward_only(self._h))
 
+    @property
+    def stack_window(self) -> int:
+        """Memory tier 0.5: bytes of the stack window kept in registers (ebpf_prog_stack_window),
+        0 when the program is not a stack-window program."""
+        return _lib.lib().ebpf_prog_stack_window(self._h)
+
     def compile(self) -> bool:
         """Compile to gfx950 code now (ebpf_prog_compile): True if this is a compiled program
         (tier 0, forward jumps only, <= 62 micro-ops), False if it runs interpreted."""
@@ -130,6 +136,16 @@ class Program:
             b.workspace = workspace.data_ptr()
             b.workspace_bytes = workspace.numel() * workspace.element_size()
         return b
+
+    def batch_kernel(self, batch: _lib.Batch, out: _lib.BatchOut | None = None,
+                     device: int = 0) -> int:
+        """The EBPF_KERNEL_* id of the kernel ebpf_run_batch runs for `batch` and `out` on
+        `device` (ebpf_batch_kernel; _lib.KERNEL_NAMES[id] names it)."""
+        o = out if out is not None else _lib.BatchOut()
+        rc = _lib.lib().ebpf_batch_kernel(self._h, ctypes.byref(batch), ctypes.byref(o), device)
+        if rc < 0:
+            raise _lib.EbpfError(rc, "ebpf_batch_kernel")
+        return rc
 
     def workspace_bytes(self, batch: _lib.Batch, device: int) -> int:
         return int(_lib.lib().ebpf_workspace_bytes(self._h, ctypes.byref(batch), device))

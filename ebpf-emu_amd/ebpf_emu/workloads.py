@@ -86,7 +86,56 @@ done:
     exit
 """
 
-PROGRAMS = {"drop": DROP_ALL, "5tuple": FIVE_TUPLE, "checksum": CHECKSUM}
+# the 5-tuple with its flow key spilled to the stack and read back (memory tier 0.5, the XDP
+# pattern of building a map key at r10 - N): saddr, daddr, protocol and destination port stored
+# at r10 - 16 .. r10 - 5, the decisions taken on the reloaded key. Same verdicts as FIVE_TUPLE.
+FIVE_TUPLE_STACK = """
+    mov r0, 2                 # default XDP_PASS
+    jlt r2, 34, out
+    ldxh r3, [r1+12]          # EtherType
+    jne r3, 0x0008, out
+    ldxb r4, [r1+14]
+    and r4, 0x0f
+    lsh r4, 2                 # IHL * 4
+    jlt r4, 20, drop
+    ldxw r6, [r1+26]          # saddr
+    stxw [r10-16], r6         # key.saddr
+    ldxw r7, [r1+30]          # daddr
+    stxw [r10-12], r7         # key.daddr
+    ldxb r5, [r1+23]          # protocol
+    stxb [r10-8], r5          # key.proto
+    stb [r10-7], 0            # key.pad
+    mov r8, r1
+    add r8, r4
+    ldxh r9, [r8+16]          # L4 destination port
+    stxh [r10-6], r9          # key.dport
+    ldxb r5, [r10-8]          # reload the key
+    jeq r5, 1, icmp
+    ldxh r9, [r10-6]
+    be16 r9
+    jeq r5, 17, udp
+    jne r5, 6, out
+    jge r9, 1024, out
+    ldxb r6, [r10-16]         # first octet of key.saddr (upper bytes kept: emu.rs:341-349)
+    and r6, 0xff
+    jeq r6, 10, drop
+    ja out
+udp:
+    jeq r9, 53, drop
+    ja out
+icmp:
+    ldxw r7, [r10-12]
+    and r7, 0xf0
+    jeq r7, 0xe0, drop
+    ja out
+drop:
+    mov r0, 1                 # XDP_DROP
+out:
+    exit
+"""
+
+PROGRAMS = {"drop": DROP_ALL, "5tuple": FIVE_TUPLE, "checksum": CHECKSUM,
+            "5tuple_stack": FIVE_TUPLE_STACK}
 
 
 def program(name: str) -> bytes:

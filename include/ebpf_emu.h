@@ -158,6 +158,14 @@ int ebpf_prog_tier(const ebpf_prog* prog);
  * EBPF_BATCH_GENERIC -- else 0; -1 for NULL. */
 int ebpf_prog_forward_only(const ebpf_prog* prog);
 
+/* Memory tier 0.5: the bytes of the stack window [r10 - k, r10) of a program whose only memory
+ * writes are ST/STX at r10 + c (c known at load time, all in the window; forward jumps only, no
+ * ATOMIC/CALL, <= 62 micro-ops). Such a program keeps the window in registers of the compiled
+ * fixed-slot kernel, for batches in the fixed-slot layout with the main.rs register layout whose
+ * window lies past every packet byte and inside the image (r10 % 4 == 0); other batches run it
+ * on the general interpreter. 0 = not such a program; -1 for NULL. */
+int ebpf_prog_stack_window(const ebpf_prog* prog);
+
 /* Compile the program to gfx950 machine code now, if it is one the tile kernels run (memory tier
  * 0, <= 62 micro-ops): straight-line code in pc order with direct register operands, replacing
  * the interpreter's dispatch. Forward-only programs get the forward kernels (batches with
@@ -186,6 +194,20 @@ int ebpf_prog_upload(ebpf_prog* prog, int device);
  * kernel; with out->counters, its last workgroup folds the per-shard sums into them. */
 int ebpf_run_batch(ebpf_prog* prog, const ebpf_batch* batch, const ebpf_batch_out* out,
                    ebpf_stream_t stream);
+
+/* The kernel ebpf_run_batch would run for this batch and outputs on `device` (uploads the
+ * program there first, so it needs that device): one of EBPF_KERNEL_*, or < 0 = EBPF_E*. */
+#define EBPF_KERNEL_GENERAL_T0 0  /* interp_kernel, memory tier 0 (read-only packet window) */
+#define EBPF_KERNEL_GENERAL_T1 1  /* interp_kernel, memory tier 1 (per-packet images in scratch) */
+#define EBPF_KERNEL_DAG        2  /* dag_kernel: forward-only programs of 63..256 micro-ops */
+#define EBPF_KERNEL_TILE       3  /* tile interpreter, forward-only programs */
+#define EBPF_KERNEL_TILE_LOOP  4  /* tile interpreter, loop mode */
+#define EBPF_KERNEL_JIT_FIXED  5  /* compiled program, fixed-slot layout (ebpf_tile_jit_fixed) */
+#define EBPF_KERNEL_JIT_VAR    6  /* compiled program, other layouts (ebpf_tile_jit_var) */
+#define EBPF_KERNEL_JIT_LOOP   7  /* compiled loop program (ebpf_tile_jit_loop) */
+#define EBPF_KERNEL_JIT_STACK  8  /* compiled stack-window program (memory tier 0.5, fixed slots) */
+int ebpf_batch_kernel(ebpf_prog* prog, const ebpf_batch* batch, const ebpf_batch_out* out,
+                      int device);
 
 /* Multi-GPU: shard s runs on devices[s] / streams[s] (distinct devices); the shards' counters are
  * summed with one RCCL all-reduce over xGMI, and the global totals of this call are ADDED to

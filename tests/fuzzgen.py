@@ -119,3 +119,58 @@ def gen_program(rng: random.Random, n: int | None = None, valid_only: bool = Tru
 def gen_packet(rng: random.Random, max_len: int = 80) -> bytes:
     n = rng.choice([0, 1, 2, 5, 14, 34, 60, 63, 64, 65, rng.randrange(0, max_len + 1)])
     return bytes(rng.getrandbits(8) for _ in range(n))
+
+
+def gen_stack_program(rng: random.Random, n: int | None = None, k: int = 32) -> bytes:
+    """Forward-only programs whose stores all hit the stack window [r10 - k, r10) (memory tier
+    0.5): ST/STX of every width at aligned and misaligned r10 offsets, directly and through a copy
+    of r10 (`mov r9, r10; add r9, -c`), loads of the window at r10 offsets, loads of the packet,
+    and register-address loads aimed just below and into the window through r1 (the store-
+    forwarding overlay, r10 = 512 in the main.rs layout) -- mixed with ALU ops and forward jumps."""
+    n = n or rng.randrange(6, 40)
+    words: list[bytes] = []
+    if rng.random() < 0.5:  # a second pointer into the stack
+        c = rng.randrange(0, 9)
+        words.append(encode(0xBF, 9, 10, 0, 0))         # mov r9, r10
+        words.append(encode(0x07, 9, 0, 0, -c))         # add r9, -c
+    else:
+        c = None
+    sizes = {0x00: 4, 0x08: 2, 0x10: 1, 0x18: 8}
+    while len(words) < n:
+        q = rng.random()
+        dst = rng.randrange(9)
+        src = rng.randrange(10)
+        size = rng.choice(list(sizes))
+        w = sizes[size]
+        if q < 0.25:  # ST / STX into the window
+            d = -rng.randrange(w, k + 1)
+            base, off = (10, d) if c is None or rng.random() < 0.5 else (9, d + c)
+            if rng.random() < 0.4:
+                words.append(encode(0x62 | size, base, 0, off, _imm(rng)))
+            else:
+                words.append(encode(0x63 | size, base, src, off))
+        elif q < 0.42:  # LDX from the window
+            d = -rng.randrange(w, k + 1)
+            base, off = (10, d) if c is None or rng.random() < 0.5 else (9, d + c)
+            words.append(encode(0x61 | size, dst, base, off))
+        elif q < 0.55:  # LDX from the packet
+            words.append(encode(0x61 | size, dst, 1, rng.randrange(-2, 72)))
+        elif q < 0.62:  # register-address LDX around the window (r1 + 512 - k - 8 .. 512 + 8)
+            r = rng.choice([3, 4, 5])
+            words.append(encode(0xB7, r, 0, 0, rng.randrange(512 - k - 8, 520)))
+            words.append(encode(0x0F, r, 1, 0, 0))            # add r, r1
+            words.append(encode(0x61 | size, dst, r, 0))
+        elif q < 0.82:  # ALU (never on r9 / r10)
+            cls = rng.choice([0x04, 0x07])
+            op = rng.choice([0, 1, 2, 4, 5, 6, 7, 10, 11, 12])
+            srcbit = rng.choice([0, 0x08])
+            words.append(encode((op << 4) | srcbit | cls, dst, src, 0, _imm(rng)))
+        elif q < 0.94:  # forward jumps
+            cls = rng.choice([0x05, 0x06])
+            op = rng.choice([0, 1, 2, 3, 4, 5, 6, 7, 10, 11, 12, 13])
+            off = rng.randrange(0, max(1, n - len(words)) + 1)
+            words.append(encode((op << 4) | rng.choice([0, 0x08]) | cls, dst, src, off, _imm(rng)))
+        else:
+            words.append(encode(0x95))
+    words.append(encode(0x95))
+    return b"".join(words)

@@ -1,0 +1,228 @@
+"""Memory tier 0.5 (stack-window programs, host.cpp analyze_stack, jit.cpp stack_*): programs
+whose only memory writes are ST/STX at r10 + c keep the window [r10 - k, r10) in VGPRs of the
+compiled fixed-slot kernel instead of running on the general interpreter with per-packet images.
+
+CPU: the load-time analysis on directed programs (which are stack-window programs and how large
+their window is), and every eligible fuzzed program compiles and assembles.
+GPU: the compiled stack-window kernel against the general interpreter (EBPF_BATCH_GENERIC, tier 1)
+and the oracle on the same batch -- status, r0, every register, verdicts and counters -- and the
+launches that must fall back to the general interpreter (window over the packet, image output,
+other layouts, init_regs), each still equal to the oracle. Reference: emu.rs:354-372 (ST/STX),
+emu.rs:341-349 (LDX), main.rs:28-31 (r10 = 512)."""
+import random
+
+import numpy as np
+import pytest
+
+from fuzzgen import gen_packet, gen_stack_program
+
+STEPS = 20000
+
+DIRECTED = [
+    ("stxdw [r10-8], r1\nexit", 8),
+    ("stb [r10-1], 1\nexit", 4),                                   # rounded up to a dword
+    ("mov r2, r10\nadd r2, -16\nstxw [r2+4], r3\nexit", 12),      # through a copy of r10
+    ("mov r2, r10\nsub r2, 20\nsth [r2+0], 7\nexit", 20),
+    ("stxdw [r10-64], r1\nexit", 64),
+    ("stxdw [r10-72], r1\nexit", 0),                               # past kStackMax
+    ("stxw [r10-2], r1\nexit", 0),                                 # crosses r10
+    ("stxw [r1+0], r2\nexit", 0),                                  # a packet store
+    ("jeq r2, 60, +2\nmov r3, r10\nja +1\nmov r3, r1\nstxb [r3-4], r0\nexit", 0),  # join differs
+    ("jeq r2, 60, +2\nmov r3, r10\nja +1\nmov r3, r10\nstxb [r3-4], r0\nexit", 4),  # join agrees
+    ("stxdw [r10-8], r1\nldxw r0, [r10-10]\nexit", 0),             # a load straddling the edge
+    ("stxdw [r10-8], r1\nldxw r0, [r10-16]\nexit", 8),             # a load below the window
+    ("stxdw [r10-8], r1\nlock add [r10-16], r2\nexit", 0),         # atomics: general image
+    ("stxdw [r10-8], r1\ncall 0\nexit", 0),                        # calls
+    ("mov r0, 0\nstxb [r10-1], r0\nadd r0, 1\njlt r0, 5, -3\nexit", 0),  # a loop
+    ("mov32 r2, r10\nstxb [r2-1], r0\nexit", 0),                   # a truncated pointer
+    ("mov r0, 1\nexit", 0),                                        # no store: tier 0
+]
+
+
+def test_stack_analysis_directed(product_lib):
+    from ebpf_emu import Program
+    from ebpf_emu.asm import assemble
+
+    for src, k in DIRECTED:
+        p = Program(assemble(src))
+        assert p.stack_window == k, (src, p.stack_window)
+        if k:
+            assert p.tier == 1 and p.compile(), src
+        p.close()
+
+
+def test_stack_programs_compile():
+    """Every eligible random stack program compiles and assembles (on the CPU); its code keeps no
+    interpreter machinery and writes the window registers."""
+    from ebpf_emu import Program
+
+    rng = random.Random(2024)
+    n_ok = 0
+    for _ in range(250):
+        img = gen_stack_program(rng)
+        try:
+            p = Program(img)
+        except Exception:
+            continue
+        if p.stack_window:
+            assert p.compile(), img.hex()
+            text = p.jit_asm(1)
+            body = text[text.index("; compiled eBPF program"):]
+            body = body[:body.index(".Ldone")]
+            for word in ("s_set_gpr_idx", "s_setpc", "s_load_dwordx16", "s_ff1"):
+                assert word not in body, word
+            assert "; stack window:" in body
+            n_ok += 1
+        p.close()
+    assert n_ok >= 150
+
+
+# ---------------------------------------------------------------------------------------------
+def _fixed_frames(pkts, stride, dev):
+    import torch
+
+    buf = np.zeros(len(pkts) * stride, dtype=np.uint8)
+    for i, p in enumerate(pkts):
+        buf[i * stride:i * stride + len(p)] = np.frombuffer(p, dtype=np.uint8)
+    return torch.tensor(buf, device=dev)
+
+
+def _run(img, frames, n, dev, kernel=None, generic=False, **kw):
+    import torch
+
+    from ebpf_emu import Program, _lib
+
+    prog = Program(img)
+    cnt = torch.zeros(8, dtype=torch.int64, device=dev)
+    mem = kw.pop("mem", False)
+    b = prog.make_batch(frames, n=n, generic=generic, max_steps=STEPS, **kw)
+    o = _lib.BatchOut()
+    if mem:
+        o.mem = 1
+    got_kernel = prog.batch_kernel(b, o, dev.index or 0)
+    if kernel is not None:
+        assert got_kernel == kernel, (_lib.KERNEL_NAMES[got_kernel], img.hex())
+    res = prog.run(frames, n=n, max_steps=STEPS, verdict=True, r0=True, status=True, regs=True,
+                   counters=cnt, generic=generic, mem=mem, **kw)
+    torch.cuda.synchronize()
+    out = dict(status=res.status.cpu().numpy(), r0=res.r0.cpu().numpy().view(np.uint64),
+               verdict=res.verdict.cpu().numpy(), regs=res.regs.cpu().numpy().view(np.uint64),
+               counters=cnt.cpu().numpy().view(np.uint64), kernel=got_kernel)
+    prog.close()
+    return out
+
+
+def _vs_oracle(oracle_mod, img, pkts, got, mem_size=1024, r10=512, tag=""):
+    op = oracle_mod.Program(img)
+    cnt = np.zeros(8, dtype=np.uint64)
+    for i, p in enumerate(pkts):
+        st, regs, _m, steps = op.run_full(p, mem_size, r10, STEPS)
+        ctx = f"{tag} pkt {i} prog {img.hex()}"
+        assert got["status"][i] == st, ctx
+        if st == 0:
+            assert [int(v) for v in got["regs"][i]] == regs, ctx
+            cnt[regs[0] if regs[0] < 5 else 5] += 1
+        else:
+            cnt[6] += 1
+        cnt[7] += steps
+    assert list(got["counters"]) == list(cnt), tag
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(4))
+def test_stack_window_fuzz(cuda, oracle_mod, seed):
+    """Random stack programs over fixed-slot batches: the compiled stack-window kernel ==
+    the general interpreter (tier 1) == the oracle, every output; production outputs too."""
+    from ebpf_emu import _lib
+
+    rng = random.Random(880 + seed)
+    n_run = 0
+    for it in range(40):
+        img = gen_stack_program(rng)
+        try:
+            oracle_mod.Program(img)
+        except oracle_mod.OracleDecodeError:
+            continue
+        from ebpf_emu import Program
+
+        p = Program(img)
+        k = p.stack_window
+        p.close()
+        if not k:
+            continue
+        stride = rng.choice([64, 128])
+        pkts = [bytes(rng.getrandbits(8) for _ in range(stride)) for _ in range(rng.choice([64, 100, 130]))]
+        frames = _fixed_frames(pkts, stride, cuda)
+        got = _run(img, frames, len(pkts), cuda, kernel=_lib.EBPF_KERNEL_JIT_STACK, stride=stride)
+        ref = _run(img, frames, len(pkts), cuda, generic=True, stride=stride)
+        assert ref["kernel"] == _lib.EBPF_KERNEL_GENERAL_T1
+        for key in ("status", "r0", "verdict", "regs", "counters"):
+            assert np.array_equal(got[key], ref[key]), (key, seed, it, img.hex())
+        _vs_oracle(oracle_mod, img, pkts, got, tag=f"seed {seed} it {it}")
+        n_run += 1
+    assert n_run >= 20
+
+
+@pytest.mark.gpu
+def test_stack_window_fallbacks(cuda, oracle_mod):
+    """Batches the stack-window kernel must not take -- each on the general interpreter, equal
+    to the oracle: the window over packet bytes (r10 = 96 with 128-byte slots), r10 not a multiple
+    of 4, an image output, the offsets + lens layout, a constant-address load into the window."""
+    import torch
+
+    from ebpf_emu import _lib
+    from ebpf_emu.asm import assemble
+
+    rng = random.Random(5)
+    src = "ldxdw r3, [r1+8]\nstxdw [r10-16], r3\nstb [r10-3], 0x5a\nldxw r0, [r10-14]\n" \
+          "ldxb r4, [r10-3]\nadd r0, r4\nexit"
+    img = assemble(src)
+    pkts = [bytes(rng.getrandbits(8) for _ in range(128)) for _ in range(70)]
+    frames = _fixed_frames(pkts, 128, cuda)
+    ok = _run(img, frames, len(pkts), cuda, kernel=_lib.EBPF_KERNEL_JIT_STACK, stride=128)
+    _vs_oracle(oracle_mod, img, pkts, ok, tag="eligible")
+    for kw, r10 in ((dict(r10=96), 96), (dict(r10=510), 510), (dict(mem=True), 512)):
+        got = _run(img, frames, len(pkts), cuda, kernel=_lib.EBPF_KERNEL_GENERAL_T1, stride=128, **kw)
+        _vs_oracle(oracle_mod, img, pkts, got, r10=r10, tag=str(kw))
+    lens = torch.tensor(np.full(len(pkts), 128, dtype=np.int16), device=cuda)
+    offs = torch.tensor(np.arange(len(pkts), dtype=np.int32) * 128, device=cuda)
+    got = _run(img, frames, len(pkts), cuda, kernel=_lib.EBPF_KERNEL_GENERAL_T1, offsets=offs,
+               lens=lens)
+    _vs_oracle(oracle_mod, img, pkts, got, tag="offsets")
+    alias = assemble("stxdw [r10-8], r2\nldxdw r0, [r1+504]\nexit")  # reads the window at r1+504
+    got = _run(alias, frames, len(pkts), cuda, kernel=_lib.EBPF_KERNEL_GENERAL_T1, stride=128)
+    _vs_oracle(oracle_mod, alias, pkts, got, tag="constant alias")
+    # register-address loads into the window (r3 = len + 376 = 504: not a load-time constant),
+    # wholly and partly inside it: the store-forwarding overlay
+    alias2 = assemble("stxdw [r10-8], r2\nmov r3, r2\nadd r3, 376\nldxdw r0, [r3+0]\n"
+                      "ldxdw r4, [r3-4]\nadd r0, r4\nldxh r4, [r3-1]\nadd r0, r4\nexit")
+    got = _run(alias2, frames, len(pkts), cuda, kernel=_lib.EBPF_KERNEL_JIT_STACK, stride=128)
+    _vs_oracle(oracle_mod, alias2, pkts, got, tag="register alias (overlay)")
+
+
+@pytest.mark.gpu
+def test_stack_workload_vs_oracle(cuda, oracle_mod):
+    """The 5-tuple with its key spilled to the stack (workloads.FIVE_TUPLE_STACK) on 64 Ki + 37
+    fixed-slot frames: the stack-window kernel vs the oracle, and the same verdicts as the plain
+    5-tuple."""
+    import torch
+
+    from ebpf_emu import Program, _lib
+    from ebpf_emu import workloads as W
+
+    n = 65536 + 37
+    buf = W.frames_fixed(n, 64, 3)
+    frames = torch.from_numpy(buf).to(cuda)
+    prog = Program(W.program("5tuple_stack"))
+    assert prog.stack_window == 16
+    b = prog.make_batch(frames, n=n, stride=64)
+    assert prog.batch_kernel(b) == _lib.EBPF_KERNEL_JIT_STACK
+    cnt = torch.zeros(8, dtype=torch.int64, device=cuda)
+    res = prog.run(frames, n=n, stride=64, r0=True, status=True, counters=cnt)
+    torch.cuda.synchronize()
+    r0, st, ocnt = oracle_mod.Program(W.program("5tuple_stack")).run_batch(buf, n, stride=64, threads=8)
+    assert np.array_equal(res.status.cpu().numpy(), st)
+    assert np.array_equal(res.r0.cpu().numpy().view(np.uint64), r0)
+    assert np.array_equal(cnt.cpu().numpy().view(np.uint64), ocnt)
+    r0b, _, _ = oracle_mod.Program(W.program("5tuple")).run_batch(buf, n, stride=64, threads=8)
+    assert np.array_equal(r0, r0b)
