@@ -32,7 +32,11 @@ CONFIGS = {
     "5tuple": (2, "IPv4 5-tuple header parse -> PASS/DROP (31 insns) over 1Mi x 64B frames"),
     "drop": (1, "XDP_DROP-all (3 insns) over 1Mi x 64B frames"),
     "checksum": (4, "per-byte checksum loop over 1Mi mixed 64B/1500B frames"),
+    # the 5-tuple with its flow key spilled to the stack and reloaded (memory tier 0.5: the
+    # stack window in registers of the compiled kernel); same frames and verdicts as 5tuple
+    "stack": (2, "IPv4 5-tuple, flow key spilled to r10-16 and reloaded (38 insns) over 1Mi x 64B frames"),
 }
+PROGRAM_OF = {"stack": "5tuple_stack"}
 
 
 def parse():
@@ -54,6 +58,8 @@ def parse():
     ap.add_argument("--cpu-seconds-1core", type=float, default=4.0,
                     help="single-thread CPU baseline budget (0 = skip)")
     ap.add_argument("--no-counters", action="store_true", help="A/B: verdicts only")
+    ap.add_argument("--generic", action="store_true",
+                    help="run on the general interpreter (EBPF_BATCH_GENERIC), for comparison")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC traffic summary (profiles/*.json) to report as roofline.traffic")
     return ap.parse_args()
@@ -81,7 +87,7 @@ def main():
     if args.frame_bytes != 64 and args.config != "checksum":
         desc = desc.replace("64B frames", f"{(max(64, args.frame_bytes) + 15) // 16 * 16}B frame slots")
     n = args.packets
-    img = W.program(args.config)
+    img = W.program(PROGRAM_OF.get(args.config, args.config))
     prog = Program(img)
     prog.upload(local)
 
@@ -134,9 +140,10 @@ def main():
     for b in batches:
         if mixed:
             bd = prog.make_batch(b["frames"], n=n, offsets=b["offsets"], lens=b["lens"],
-                                 mem_size=mem_size, r10=r10)
+                                 mem_size=mem_size, r10=r10, generic=args.generic)
         else:
-            bd = prog.make_batch(b["frames"], n=n, stride=fb, mem_size=mem_size, r10=r10)
+            bd = prog.make_batch(b["frames"], n=n, stride=fb, mem_size=mem_size, r10=r10,
+                                 generic=args.generic)
         descs.append(bd)
     out = _lib.BatchOut()
     out.verdict = verdict.data_ptr()
@@ -241,7 +248,7 @@ def main():
                 "kernel_avg_us": round(kern_avg_ms * 1e3, 3),
                 # HIP events bracket one whole batch: one interpreter launch (with counters, its
                 # last workgroup folds the per-shard sums into them)
-                "kernel": kernel_name(prog),
+                "kernel": _lib.KERNEL_NAMES[prog.batch_kernel(descs[0], out, local)],
             },
             "counters": {"drop": cnt[1], "pass": cnt[2], "other": cnt[5], "faults": cnt[6],
                          "insns_retired": cnt[7]},
@@ -254,20 +261,6 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
-
-
-def kernel_name(prog):
-    """The kernel ebpf_run_batch picks for this program (interp.hip kernel_for; a compiled
-    program runs as the JIT template kernel with its code, csrc/jit.cpp)."""
-    if prog.tier == 0 and len(prog) <= 62 and prog.compile() and os.environ.get("EBPFEMU_NO_JIT") != "1":
-        if prog.forward_only:
-            return "ebpf_tile_jit_fixed (compiled program)"
-        return "ebpf_tile_jit_loop (compiled loop program)"
-    if prog.tier == 0 and len(prog) <= 62:
-        return "ebpfemu::tile_kernel<" + ("forward" if prog.forward_only else "loops") + ">"
-    if prog.forward_only:
-        return "ebpfemu::dag_kernel"
-    return f"ebpfemu::interp_kernel<{prog.tier}>"
 
 
 def host_cpus():

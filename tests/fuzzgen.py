@@ -155,10 +155,15 @@ def gen_stack_program(rng: random.Random, n: int | None = None, k: int = 32) -> 
             words.append(encode(0x61 | size, dst, base, off))
         elif q < 0.55:  # LDX from the packet
             words.append(encode(0x61 | size, dst, 1, rng.randrange(-2, 72)))
-        elif q < 0.62:  # register-address LDX around the window (r1 + 512 - k - 8 .. 512 + 8)
-            r = rng.choice([3, 4, 5])
-            words.append(encode(0xB7, r, 0, 0, rng.randrange(512 - k - 8, 520)))
-            words.append(encode(0x0F, r, 1, 0, 0))            # add r, r1
+        elif q < 0.62:  # LDX around the window (512 - k - 8 .. 512 + 8): mostly through a
+            r = rng.choice([3, 4, 5])                        # register the load-time dataflow
+            if rng.random() < 0.75:                          # cannot resolve (r2 & 0 + c)
+                words.append(encode(0xBF, r, 2, 0, 0))        # mov r, r2
+                words.append(encode(0x57, r, 0, 0, 0))        # and r, 0
+                words.append(encode(0x07, r, 0, 0, rng.randrange(512 - k - 8, 520)))
+            else:                                            # else a constant address (whose
+                words.append(encode(0xB7, r, 0, 0, rng.randrange(512 - k - 8, 520)))
+                words.append(encode(0x0F, r, 1, 0, 0))        # overlap sends the batch to tier 1)
             words.append(encode(0x61 | size, dst, r, 0))
         elif q < 0.82:  # ALU (never on r9 / r10)
             cls = rng.choice([0x04, 0x07])

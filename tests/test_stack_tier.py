@@ -136,7 +136,7 @@ def test_stack_window_fuzz(cuda, oracle_mod, seed):
     from ebpf_emu import _lib
 
     rng = random.Random(880 + seed)
-    n_run = 0
+    n_run = n_stack = 0
     for it in range(40):
         img = gen_stack_program(rng)
         try:
@@ -153,14 +153,17 @@ def test_stack_window_fuzz(cuda, oracle_mod, seed):
         stride = rng.choice([64, 128])
         pkts = [bytes(rng.getrandbits(8) for _ in range(stride)) for _ in range(rng.choice([64, 100, 130]))]
         frames = _fixed_frames(pkts, stride, cuda)
-        got = _run(img, frames, len(pkts), cuda, kernel=_lib.EBPF_KERNEL_JIT_STACK, stride=stride)
+        # (a constant-address load into the window sends the batch to the general interpreter)
+        got = _run(img, frames, len(pkts), cuda, stride=stride)
+        assert got["kernel"] in (_lib.EBPF_KERNEL_JIT_STACK, _lib.EBPF_KERNEL_GENERAL_T1)
+        n_stack += got["kernel"] == _lib.EBPF_KERNEL_JIT_STACK
         ref = _run(img, frames, len(pkts), cuda, generic=True, stride=stride)
         assert ref["kernel"] == _lib.EBPF_KERNEL_GENERAL_T1
         for key in ("status", "r0", "verdict", "regs", "counters"):
             assert np.array_equal(got[key], ref[key]), (key, seed, it, img.hex())
         _vs_oracle(oracle_mod, img, pkts, got, tag=f"seed {seed} it {it}")
         n_run += 1
-    assert n_run >= 20
+    assert n_run >= 20 and n_stack >= 15, (n_run, n_stack)
 
 
 @pytest.mark.gpu
