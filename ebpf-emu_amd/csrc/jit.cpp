@@ -223,6 +223,10 @@ struct Compiler {
   static bool is_jump(const Uop& o) { return o.op >= U_JA && o.op <= U_JLE32; }
 
   const StackPlan* stk = nullptr;  // a stack-window program (memory tier 0.5)
+  // loop programs: one-byte loads through the per-lane byte cache (byte_cache) in v[50:53] / v55,
+  // unless other compiled code uses those registers (cache_conflict: compiled again without)
+  bool cache = false;
+  bool cache_conflict = false;
 
   Compiler(const std::vector<Uop>& u, const std::vector<TUop>& tt, bool lp = false, bool ex = false,
            const StackPlan* sp = nullptr)
@@ -735,8 +739,9 @@ struct Compiler {
          "v_subrev_u32 v29, " + std::to_string(u.a0) + ", v29\n"
          "s_andn2_b64 exec, s[66:67], s[64:65]\n"
          "s_cbranch_execz " + next + "\n"
-         ".Lok" + U + ":\n"
-         "v_sub_u32 v42, " + A + ", v22\n"
+         ".Lok" + U + ":\n";
+    if (cache) return s + byte_cache(U, A, D0, m, ool);
+    s += "v_sub_u32 v42, " + A + ", v22\n"
          "v_cmp_lt_u32_e64 s[60:61], " + A + ", v31\n"
          "v_cndmask_b32_e64 v43, 0, v42, s[60:61]\n"
          "v_cmp_le_u32 vcc, 64, v43\n"
@@ -770,6 +775,100 @@ struct Compiler {
            "v_cndmask_b32_e64 v26, 0, v26, s[60:61]\n"
            "s_branch .Lfarb" + U + "\n";
     return s;
+  }
+
+  // The byte cache of the per-byte loops: each lane keeps 16 packet bytes [TAG, TAG + 16) in
+  // v[50:53] (zeros past its length), TAG in v55 (0x80000000 = empty: no address reaches it). A
+  // one-byte load whose address a is in the cache (a - TAG < 16) extracts its byte with two
+  // selects and a 64-bit shift -- no LDS access, no wait; the other lanes (about one load in 16
+  // of a byte scan) fill the cache out of line from their LDS window with one ds_read_b128 (16
+  // bytes: conflict-free under the window swizzle, where 64 lanes' ds_read_u8 of one offset hit
+  // 16 banks), refilling the window first when the chunk is outside it. Packet bytes never change
+  // (memory tier 0), so the cache stays valid across refills and micro-ops. Tiles with unaligned
+  // packets (no refills) read their byte as before. In bounds (a < mem) on entry; result in v26.
+  std::string byte_cache(const std::string& U, const std::string& A, const std::string& D0,
+                         const Marker& m, std::string& ool) const {
+    std::string s = "v_sub_u32 v42, " + A + ", v55\n"
+                    "v_cmp_gt_u32 vcc, 16, v42\n"
+                    "s_andn2_b64 s[68:69], exec, vcc\n"
+                    "s_cbranch_scc1 .Lcm" + U + "\n"
+                    ".Lch" + U + ":\n"
+                    "v_cmp_gt_u32 vcc, 8, v42\n"
+                    "v_cndmask_b32 v26, v52, v50, vcc\n"
+                    "v_cndmask_b32 v27, v53, v51, vcc\n"
+                    "v_lshlrev_b32 v42, 3, v42\n"
+                    "v_lshrrev_b64 v[26:27], v42, v[26:27]\n"
+                    ".Lcd" + U + ":\n"
+                    "v_bfi_b32 " + D0 + ", s56, v26, " + D0 + "\n";
+    std::string o = ".Lcm" + U + ":\n"
+                    "s_mov_b64 s[64:65], exec\n"
+                    "s_cmp_eq_u32 " + m.aligned + ", 0\n"
+                    "s_cbranch_scc1 .Lcf" + U + "\n"
+                    "s_mov_b64 exec, s[68:69]\n"
+                    "v_and_b32 v43, -16, " + A + "\n"
+                    "v_sub_u32 v42, v43, v22\n"
+                    "v_cmp_lt_u32 vcc, v43, v31\n"
+                    "v_cmp_lt_u32_e64 s[60:61], 48, v42\n"
+                    "s_and_b64 s[68:69], vcc, s[60:61]\n"
+                    "s_cbranch_scc0 .Lcn" + U + "\n" + refill(A) +
+                    ".Lcn" + U + ":\n"
+                    "v_and_b32 v55, -16, " + A + "\n"
+                    "v_sub_u32 v42, v55, v22\n"
+                    "v_min_u32 v42, 48, v42\n"
+                    "v_xad_u32 v42, v35, v42, v34\n"
+                    "ds_read_b128 v[50:53], v42\n"
+                    "v_sub_u32 v43, v31, v55\n"
+                    "s_waitcnt lgkmcnt(0)\n";
+    for (int j = 0; j < 4; j++) {  // bytes at or past len read as zero (the zeroed image)
+      const std::string C = "v" + std::to_string(50 + j);
+      o += "v_subrev_u32 v44, " + std::to_string(4 * j) + ", v43\n"
+           "v_med3_i32 v44, v44, 0, 4\n"
+           "v_lshlrev_b32 v45, 3, v44\n"
+           "v_bfe_u32 v46, " + C + ", 0, v45\n"
+           "v_cmp_eq_u32 vcc, 4, v44\n"
+           "v_cndmask_b32 " + C + ", v46, " + C + ", vcc\n";
+    }
+    o += "s_mov_b64 exec, s[64:65]\n"
+         "v_sub_u32 v42, " + A + ", v55\n"
+         "s_branch .Lch" + U + "\n"
+         // unaligned tile: the window (or the packet in HBM past it), byte by byte
+         ".Lcf" + U + ":\n"
+         "v_sub_u32 v42, " + A + ", v22\n"
+         "v_cmp_lt_u32_e64 s[60:61], " + A + ", v31\n"
+         "v_cndmask_b32_e64 v43, 0, v42, s[60:61]\n"
+         "v_cmp_le_u32_e64 s[68:69], 64, v43\n"
+         "v_min_u32 v43, 63, v43\n"
+         "v_xad_u32 v42, v35, v43, v34\n"
+         "ds_read_u8 v26, v42\n"
+         "s_and_b64 exec, s[64:65], s[68:69]\n"
+         "s_cbranch_execz .Lcg" + U + "\n"
+         "v_and_b32 v46, -4, " + A + "\nv_mov_b32 v47, 0\n"
+         "v_lshl_add_u64 v[44:45], v[32:33], 0, v[46:47]\n"
+         "global_load_dword v49, v[44:45], off\n"
+         "s_waitcnt vmcnt(0) lgkmcnt(0)\n"
+         "v_and_b32 v48, 3, " + A + "\nv_lshlrev_b32 v48, 3, v48\n"
+         "v_bfe_u32 v26, v49, v48, 8\n"
+         ".Lcg" + U + ":\n"
+         "s_mov_b64 exec, s[64:65]\n"
+         "s_waitcnt lgkmcnt(0)\n"
+         "v_cndmask_b32_e64 v26, 0, v26, s[60:61]\n"
+         "s_branch .Lcd" + U + "\n";
+    ool += o;
+    return s;
+  }
+
+  // Whether code text names any of v[lo..hi] (single registers or ranges).
+  static bool touches(const std::string& text, uint32_t lo, uint32_t hi) {
+    for (size_t q = 0; (q = text.find('v', q)) != std::string::npos; q++) {
+      if (q > 0 && (isalnum((unsigned char)text[q - 1]) || text[q - 1] == '_')) continue;
+      uint32_t a, b;
+      if (sscanf(text.c_str() + q, "v[%u:%u]", &a, &b) == 2) {
+        if (!(b < lo || a > hi)) return true;
+      } else if (isdigit((unsigned char)text[q + 1]) && sscanf(text.c_str() + q, "v%u", &a) == 1) {
+        if (a >= lo && a <= hi) return true;
+      }
+    }
+    return false;
   }
 
   // A register-address load in the fixed-slot layout (ldx in gen_tile.py, non-loop form; every
@@ -919,6 +1018,7 @@ struct Compiler {
       mt = resolve_ifs(mt);
       ot = resolve_ifs(ot);
       if (ot.empty()) mt = fold_copy(fold_copy(mt, 24), 54);  // (out-of-line code may read them)
+      if (cache && (touches(mt, 50, 55) || touches(ot, 50, 55))) cache_conflict = true;
       main += mt;
       ool += ot;
     }
@@ -997,10 +1097,25 @@ struct Compiler {
   // ebpf_tile_jit_loop: s70 = 0 runs the block copy, whose budget failure restarts the tile
   // (.Lreinit of the statement's prologue) with s70 = 1, which runs the exact copy.
   bool body_loop(const Marker& m, Compiler& xc, std::string& out) {
+    // opt-in (EBPFEMU_BYTE_CACHE=1): A/B on one MI355X, checksum config, 1 Mi packets: 474 us
+    // with the cache vs 466 without -- the LDS instructions drop 7.5x and the bank-conflict
+    // cycles 14x, but the extra selects and the miss path's SALU turn the waits into issue
+    // stalls (SQ_WAIT_INST_ANY doubled; profiles/r02_pmc_checksum_bytecache.json)
+    const char* bc = getenv("EBPFEMU_BYTE_CACHE");
+    cache = xc.cache = bc && bc[0] == '1';
+    cache_conflict = xc.cache_conflict = false;
+    if (!body_loop_once(m, xc, out)) return false;
+    if (!cache_conflict && !xc.cache_conflict) return true;
+    cache = xc.cache = false;
+    return body_loop_once(m, xc, out);
+  }
+
+  bool body_loop_once(const Marker& m, Compiler& xc, std::string& out) {
     const std::string P = "J" + m.n + "_", PX = "J" + m.n + "x_";
     std::string main = "; compiled eBPF loop program: " + std::to_string(n) + " micro-ops\n"
                        "s_mov_b32 s52, s33\ns_mov_b32 s53, 0\ns_movk_i32 s56, 0xff\n"
                        "s_not_b32 s57, s71\ns_mov_b64 exec, -1\nv_add_u32 v29, s57, v29\n"
+                       "v_mov_b32 v55, 0x80000000\n"
                        "s_cmp_lg_u32 s70, 0\ns_cbranch_scc1 .L" + PX + "start\n"
                        "s_mov_b64 exec, 0\n";
     std::string ool;
