@@ -60,8 +60,10 @@ def parse():
     ap.add_argument("--no-counters", action="store_true", help="A/B: verdicts only")
     ap.add_argument("--generic", action="store_true",
                     help="run on the general interpreter (EBPF_BATCH_GENERIC), for comparison")
-    ap.add_argument("--traffic-json", default=None,
-                    help="PMC traffic summary (profiles/*.json) to report as roofline.traffic")
+    ap.add_argument("--pmc-json", default=None,
+                    help="PMC summary (tools/pmc_summary.py output) of this workload: its HBM bytes"
+                         " per launch (roofline.traffic) and VALU instructions (issue_roofline);"
+                         " default profiles/pmc_<config>[_<slot>B].json")
     return ap.parse_args()
 
 
@@ -199,16 +201,36 @@ def main():
     achieved_gbs = algo_bytes / (kern_avg_ms * 1e-3) / 1e9
     wall_gbs = algo_bytes * args.steps / elapsed / 1e9
 
+    # PMC of the same workload (FETCH_SIZE doubled + WRITE_SIZE, MI355X guide HBM section;
+    # SQ_INSTS_VALU), collected by tools/pmc.sh into the committed summary
     traffic = None
-    tj = args.traffic_json or os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
-    if os.path.exists(tj):
-        with open(tj) as f:
-            traffic = json.load(f).get("hbm_bytes_per_launch")
+    issue = None
+    suffix = "" if mixed or fb == 64 else f"_{fb}B"
+    pj = args.pmc_json or os.path.join(ROOT, "profiles", f"pmc_{args.config}{suffix}.json")
+    if os.path.exists(pj) and not args.total_packets and n == 1 << 20 and not args.generic:
+        with open(pj) as f:
+            pmc = json.load(f)
+        traffic = pmc.get("hbm_bytes_per_launch")
+        valu = pmc.get("avg", {}).get("SQ_INSTS_VALU")
+        if valu:
+            # instruction-issue roofline: wave64 VALU instructions per second of the dominant
+            # kernel vs 256 CUs x 4 SIMDs x one wave64 VALU op per 2 cycles x 2.4 GHz
+            ceil = 256 * 4 * 2.4e9 / 2
+            per_s = valu / (pmc["kernel_avg_us_profiled"] * 1e-6)
+            issue = {"valu_wave_insts_per_launch": int(valu),
+                     "valu_wave_insts_per_s": round(per_s, 1),
+                     "valu_lane_ops_per_s": round(per_s * 64, 1),
+                     "ceiling_wave_insts_per_s": ceil,
+                     "frac": round(per_s / ceil, 4),
+                     "ebpf_lane_insts_per_s": None,
+                     "source": os.path.relpath(pj, ROOT)}
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(args, img, batches[0], mixed, n, mem_size, r10)
 
+    if issue is not None:
+        issue["ebpf_lane_insts_per_s"] = round(cnt[7] / (kern_avg_ms * 1e-3 * args.steps), 1)
     if rank == 0:
         line = {
             "metric": "Mpkt/s device-resident, 64B frames, fixed XDP prog; achieved HBM GB/s vs peak",
@@ -250,6 +272,7 @@ def main():
                 # last workgroup folds the per-shard sums into them)
                 "kernel": _lib.KERNEL_NAMES[prog.batch_kernel(descs[0], out, local)],
             },
+            "issue_roofline": issue,
             "counters": {"drop": cnt[1], "pass": cnt[2], "other": cnt[5], "faults": cnt[6],
                          "insns_retired": cnt[7]},
             "ebpf_insns_per_s": round(cnt[7] / elapsed, 1),
