@@ -227,6 +227,7 @@ struct Compiler {
   // unless other compiled code uses those registers (cache_conflict: compiled again without)
   bool cache = false;
   bool cache_conflict = false;
+  bool zwin = false;  // zero-past-len windows (ldx1_zero_window)
 
   Compiler(const std::vector<Uop>& u, const std::vector<TUop>& tt, bool lp = false, bool ex = false,
            const StackPlan* sp = nullptr)
@@ -741,6 +742,7 @@ struct Compiler {
          "s_cbranch_execz " + next + "\n"
          ".Lok" + U + ":\n";
     if (cache) return s + byte_cache(U, A, D0, m, ool);
+    if (zwin) return s + ldx1_zero_window(U, A, D0, m, ool);
     s += "v_sub_u32 v42, " + A + ", v22\n"
          "v_cmp_lt_u32_e64 s[60:61], " + A + ", v31\n"
          "v_cndmask_b32_e64 v43, 0, v42, s[60:61]\n"
@@ -775,6 +777,104 @@ struct Compiler {
            "v_cndmask_b32_e64 v26, 0, v26, s[60:61]\n"
            "s_branch .Lfarb" + U + "\n";
     return s;
+  }
+
+  // Zero-past-len windows (zwin: loop programs whose register-address loads are all one byte
+  // wide, so this handler is the only reader and refiller of the LDS windows): every window byte
+  // at or past the packet's length is kept zero -- the prologue clears them after the DMA
+  // (window_zero_prologue), each refill before its LDS writes (refill_zero) -- so the load needs
+  // no a < len test: it refills when a - WB >= 64 (u32; a lane past its packet refills a window
+  // of zeros) and reads its byte. 4 VALU per byte fewer than the masked form.
+  std::string ldx1_zero_window(const std::string& U, const std::string& A, const std::string& D0,
+                               const Marker& m, std::string& ool) const {
+    std::string s = "v_sub_u32 v42, " + A + ", v22\n"
+                    "v_cmp_le_u32 vcc, 64, v42\n"
+                    "s_cbranch_vccnz .Lrf" + U + "\n"
+                    ".Lrfb" + U + ":\n"
+                    "v_xad_u32 v42, v35, v42, v34\n"
+                    "ds_read_u8 v26, v42\n"
+                    "s_waitcnt lgkmcnt(0)\n"
+                    ".Lfarb" + U + ":\n"
+                    "v_bfi_b32 " + D0 + ", s56, v26, " + D0 + "\n";
+    ool += ".Lrf" + U + ":\n"
+           "s_mov_b64 s[68:69], vcc\n"
+           "s_cmp_eq_u32 " + m.aligned + ", 0\n"
+           "s_cbranch_scc1 .Lfar" + U + "\n" + refill_zero(A, U) +
+           "v_sub_u32 v42, " + A + ", v22\n"
+           "s_branch .Lrfb" + U + "\n"
+           // unaligned tile: its window [0, 64) was staged with zeros past len and is never
+           // refilled; lanes outside it read the packet's dword from HBM (a < len) or zero
+           ".Lfar" + U + ":\n"
+           "s_mov_b64 s[66:67], exec\n"
+           "v_min_u32 v43, 63, v42\n"
+           "v_xad_u32 v42, v35, v43, v34\n"
+           "ds_read_u8 v26, v42\n"
+           "s_waitcnt lgkmcnt(0)\n"
+           "s_mov_b64 exec, s[68:69]\n"
+           "v_mov_b32 v26, 0\n"
+           "v_cmp_lt_u32 vcc, " + A + ", v31\n"
+           "s_and_b64 exec, exec, vcc\n"
+           "s_cbranch_execz .Lfz" + U + "\n"
+           "v_and_b32 v46, -4, " + A + "\nv_mov_b32 v47, 0\n"
+           "v_lshl_add_u64 v[44:45], v[32:33], 0, v[46:47]\n"
+           "global_load_dword v49, v[44:45], off\n"
+           "s_waitcnt vmcnt(0)\n"
+           "v_and_b32 v48, 3, " + A + "\nv_lshlrev_b32 v48, 3, v48\n"
+           "v_bfe_u32 v26, v49, v48, 8\n"
+           ".Lfz" + U + ":\n"
+           "s_mov_b64 exec, s[66:67]\n"
+           "s_branch .Lfarb" + U + "\n";
+    return s;
+  }
+
+  // zwin: the DMA'd windows of an aligned tile hold whatever follows a packet shorter than 64
+  // bytes; clear those bytes once per tile (lanes with len - WB < 64; skipped when none).
+  std::string window_zero_prologue(const Marker& m, const std::string& P) const {
+    if (!zwin) return "";
+    const std::string L = ".L" + P + "pz";
+    std::string z = "s_cmp_eq_u32 " + m.aligned + ", 0\ns_cbranch_scc1 " + L + "\n"
+                    "v_sub_u32 v37, v31, v22\n"
+                    "v_cmp_gt_i32 vcc, 64, v37\n"
+                    "s_cbranch_vccz " + L + "\n"
+                    "s_mov_b64 exec, vcc\n";
+    for (uint32_t c = 0; c < 4; c++) {
+      z += "v_xad_u32 v43, v35, " + std::to_string(16 * c) + ", v34\n"
+           "ds_read_b128 v[44:47], v43\ns_waitcnt lgkmcnt(0)\n";
+      for (uint32_t d = 0; d < 4; d++) z += zero_dword("v" + std::to_string(44 + d), 16 * c + 4 * d);
+      z += "ds_write_b128 v43, v[44:47]\n";
+    }
+    return z + "s_waitcnt lgkmcnt(0)\ns_mov_b64 exec, -1\n" + L + ":\n";
+  }
+
+  // Zero the bytes at or past the packet's length in dword register R holding window bytes
+  // [o, o + 4) of a window starting at packet offset WB, given v37 = len - WB (signed):
+  // clamp(len - WB - o, 0, 4) bytes stay. Temporaries v26, v27, v42; vcc.
+  static std::string zero_dword(const std::string& R, uint32_t o) {
+    return "v_subrev_u32 v26, " + std::to_string(o) + ", v37\n"
+           "v_med3_i32 v26, v26, 0, 4\n"
+           "v_lshlrev_b32 v27, 3, v26\n"
+           "v_bfe_u32 v42, " + R + ", 0, v27\n"
+           "v_cmp_eq_u32 vcc, 4, v26\n"
+           "v_cndmask_b32 " + R + ", v42, " + R + ", vcc\n";
+  }
+
+  // kJitRefill with the bytes past the packet's length zeroed before the LDS writes (only for
+  // lanes whose new window passes the packet's end: a uniform branch skips it otherwise).
+  std::string refill_zero(const std::string& A, const std::string& U) const {
+    std::string r = refill(A);
+    const size_t w = r.find("v_xad_u32 v37, v35, 0, v34\nds_write_b128");
+    if (w == std::string::npos) return "; (refill layout changed)\ns_trap 2\n";
+    static const char* regs[4][4] = {{"v44", "v45", "v46", "v47"}, {"v48", "v49", "v50", "v51"},
+                                     {"v52", "v53", "v54", "v55"}, {"v38", "v39", "v40", "v41"}};
+    std::string z = "v_sub_u32 v37, v31, v22\n"
+                    "v_cmp_gt_i32 vcc, 64, v37\n"
+                    "s_cbranch_vccz .Lrz" + U + "\n"
+                    "s_mov_b64 s[62:63], exec\ns_mov_b64 exec, vcc\n";
+    for (uint32_t c = 0; c < 4; c++)
+      for (uint32_t d = 0; d < 4; d++) z += zero_dword(regs[c][d], 16 * c + 4 * d);
+    z += "s_mov_b64 exec, s[62:63]\n.Lrz" + U + ":\n";
+    r.insert(w, z);
+    return r;
   }
 
   // The byte cache of the per-byte loops: each lane keeps 16 packet bytes [TAG, TAG + 16) in
@@ -1103,6 +1203,9 @@ struct Compiler {
     // stalls (SQ_WAIT_INST_ANY doubled; profiles/r02_pmc_checksum_bytecache.json)
     const char* bc = getenv("EBPFEMU_BYTE_CACHE");
     cache = xc.cache = bc && bc[0] == '1';
+    bool only_bytes = !getenv("EBPFEMU_NO_ZERO_WINDOW");
+    for (const Uop& o : uops) only_bytes = only_bytes && (o.op != U_LDX || o.aux == 1);
+    zwin = xc.zwin = only_bytes && !cache;
     cache_conflict = xc.cache_conflict = false;
     if (!body_loop_once(m, xc, out)) return false;
     if (!cache_conflict && !xc.cache_conflict) return true;
@@ -1115,7 +1218,7 @@ struct Compiler {
     std::string main = "; compiled eBPF loop program: " + std::to_string(n) + " micro-ops\n"
                        "s_mov_b32 s52, s33\ns_mov_b32 s53, 0\ns_movk_i32 s56, 0xff\n"
                        "s_not_b32 s57, s71\ns_mov_b64 exec, -1\nv_add_u32 v29, s57, v29\n"
-                       "v_mov_b32 v55, 0x80000000\n"
+                       "v_mov_b32 v55, 0x80000000\n" + window_zero_prologue(m, P) +
                        "s_cmp_lg_u32 s70, 0\ns_cbranch_scc1 .L" + PX + "start\n"
                        "s_mov_b64 exec, 0\n";
     std::string ool;
