@@ -228,6 +228,7 @@ struct Compiler {
   bool cache = false;
   bool cache_conflict = false;
   bool zwin = false;  // zero-past-len windows (ldx1_zero_window)
+  bool qcache = false;  // with the 8-byte per-lane cache (ldx1_qword_cache)
 
   Compiler(const std::vector<Uop>& u, const std::vector<TUop>& tt, bool lp = false, bool ex = false,
            const StackPlan* sp = nullptr)
@@ -742,6 +743,7 @@ struct Compiler {
          "s_cbranch_execz " + next + "\n"
          ".Lok" + U + ":\n";
     if (cache) return s + byte_cache(U, A, D0, m, ool);
+    if (zwin && qcache) return s + ldx1_qword_cache(U, A, D0, m, ool);
     if (zwin) return s + ldx1_zero_window(U, A, D0, m, ool);
     s += "v_sub_u32 v42, " + A + ", v22\n"
          "v_cmp_lt_u32_e64 s[60:61], " + A + ", v31\n"
@@ -844,6 +846,68 @@ struct Compiler {
       z += "ds_write_b128 v43, v[44:47]\n";
     }
     return z + "s_waitcnt lgkmcnt(0)\ns_mov_b64 exec, -1\n" + L + ":\n";
+  }
+
+  // zwin + an 8-byte per-lane cache: the lane keeps window bytes [TAG, TAG + 8) (TAG 8-aligned,
+  // in v55; 0x80000000 = empty) in v[52:53], so seven of eight bytes of a scan are one 64-bit
+  // shift with no LDS access; a miss reads the qword with one ds_read_b64 (refilling the window
+  // first if the qword is outside it). Bytes past len read as zero from the zeroed windows. Tiles
+  // with unaligned packets (no refills) take ldx1_zero_window's far path every time.
+  std::string ldx1_qword_cache(const std::string& U, const std::string& A, const std::string& D0,
+                               const Marker& m, std::string& ool) const {
+    std::string s = "v_sub_u32 v42, " + A + ", v55\n"
+                    "v_cmp_gt_u32 vcc, 8, v42\n"
+                    "s_andn2_b64 s[68:69], exec, vcc\n"
+                    "s_cbranch_scc1 .Lqm" + U + "\n"
+                    ".Lqh" + U + ":\n"
+                    "v_lshlrev_b32 v42, 3, v42\n"
+                    "v_lshrrev_b64 v[26:27], v42, v[52:53]\n"
+                    ".Lqd" + U + ":\n"
+                    "v_bfi_b32 " + D0 + ", s56, v26, " + D0 + "\n";
+    ool += ".Lqm" + U + ":\n"
+           "s_mov_b64 s[64:65], exec\n"
+           "s_cmp_eq_u32 " + m.aligned + ", 0\n"
+           "s_cbranch_scc1 .Lqf" + U + "\n"
+           "s_mov_b64 exec, s[68:69]\n"
+           "v_and_b32 v55, -8, " + A + "\n"
+           "v_sub_u32 v42, v55, v22\n"
+           "v_cmp_lt_u32 vcc, 56, v42\n"
+           "s_cbranch_vccz .Lqn" + U + "\n"
+           "s_mov_b64 s[68:69], vcc\n" + refill_zero(A, U) +
+           "v_and_b32 v55, -8, " + A + "\n"
+           "v_sub_u32 v42, v55, v22\n"
+           ".Lqn" + U + ":\n"
+           "v_xad_u32 v42, v35, v42, v34\n"
+           "ds_read_b64 v[52:53], v42\n"
+           "s_waitcnt lgkmcnt(0)\n"
+           "s_mov_b64 exec, s[64:65]\n"
+           "v_sub_u32 v42, " + A + ", v55\n"
+           "s_branch .Lqh" + U + "\n"
+           // unaligned tile: the window [0, 64) or the packet's dword in HBM, byte by byte
+           ".Lqf" + U + ":\n"
+           "v_sub_u32 v42, " + A + ", v22\n"
+           "v_cmp_le_u32 s[68:69], 64, v42\n"
+           "s_mov_b64 s[66:67], exec\n"
+           "v_min_u32 v43, 63, v42\n"
+           "v_xad_u32 v42, v35, v43, v34\n"
+           "ds_read_u8 v26, v42\n"
+           "s_waitcnt lgkmcnt(0)\n"
+           "s_and_b64 exec, exec, s[68:69]\n"
+           "s_cbranch_execz .Lqz" + U + "\n"
+           "v_mov_b32 v26, 0\n"
+           "v_cmp_lt_u32 vcc, " + A + ", v31\n"
+           "s_and_b64 exec, exec, vcc\n"
+           "s_cbranch_execz .Lqz" + U + "\n"
+           "v_and_b32 v46, -4, " + A + "\nv_mov_b32 v47, 0\n"
+           "v_lshl_add_u64 v[44:45], v[32:33], 0, v[46:47]\n"
+           "global_load_dword v49, v[44:45], off\n"
+           "s_waitcnt vmcnt(0)\n"
+           "v_and_b32 v48, 3, " + A + "\nv_lshlrev_b32 v48, 3, v48\n"
+           "v_bfe_u32 v26, v49, v48, 8\n"
+           ".Lqz" + U + ":\n"
+           "s_mov_b64 exec, s[66:67]\n"
+           "s_branch .Lqd" + U + "\n";
+    return s;
   }
 
   // Zero the bytes at or past the packet's length in dword register R holding window bytes
@@ -1118,7 +1182,7 @@ struct Compiler {
       mt = resolve_ifs(mt);
       ot = resolve_ifs(ot);
       if (ot.empty()) mt = fold_copy(fold_copy(mt, 24), 54);  // (out-of-line code may read them)
-      if (cache && (touches(mt, 50, 55) || touches(ot, 50, 55))) cache_conflict = true;
+      if ((cache || qcache) && (touches(mt, 50, 55) || touches(ot, 50, 55))) cache_conflict = true;
       main += mt;
       ool += ot;
     }
@@ -1206,10 +1270,11 @@ struct Compiler {
     bool only_bytes = !getenv("EBPFEMU_NO_ZERO_WINDOW");
     for (const Uop& o : uops) only_bytes = only_bytes && (o.op != U_LDX || o.aux == 1);
     zwin = xc.zwin = only_bytes && !cache;
+    qcache = xc.qcache = zwin && !getenv("EBPFEMU_NO_QCACHE");
     cache_conflict = xc.cache_conflict = false;
     if (!body_loop_once(m, xc, out)) return false;
     if (!cache_conflict && !xc.cache_conflict) return true;
-    cache = xc.cache = false;
+    cache = xc.cache = qcache = xc.qcache = false;
     return body_loop_once(m, xc, out);
   }
 
