@@ -86,6 +86,10 @@ def main():
     torch.cuda.set_device(dev)
 
     cfg_idx, desc = CONFIGS[args.config]
+    if args.total_packets:
+        desc = desc.replace("1Mi x 64B frames", f"a {args.total_packets}-packet global batch of "
+                            "64B frames (seeded 1Mi-packet chunks)")
+        cfg_idx = 3 if args.config == "5tuple" else cfg_idx
     if args.frame_bytes != 64 and args.config != "checksum":
         desc = desc.replace("64B frames", f"{(max(64, args.frame_bytes) + 15) // 16 * 16}B frame slots")
     n = args.packets

@@ -855,16 +855,18 @@ struct Compiler {
   // with unaligned packets (no refills) take ldx1_zero_window's far path every time.
   std::string ldx1_qword_cache(const std::string& U, const std::string& A, const std::string& D0,
                                const Marker& m, std::string& ool) const {
+    // (a VOPC result is 0 for inactive lanes, so vcc is exactly the missing lanes; the byte at
+    // cache offset x = a - TAG < 8 is selector x of v_perm over {v53, v52}; its other selector
+    // bytes are 0, and only the low byte is merged)
     std::string s = "v_sub_u32 v42, " + A + ", v55\n"
-                    "v_cmp_gt_u32 vcc, 8, v42\n"
-                    "s_andn2_b64 s[68:69], exec, vcc\n"
-                    "s_cbranch_scc1 .Lqm" + U + "\n"
+                    "v_cmp_le_u32 vcc, 8, v42\n"
+                    "s_cbranch_vccnz .Lqm" + U + "\n"
                     ".Lqh" + U + ":\n"
-                    "v_lshlrev_b32 v42, 3, v42\n"
-                    "v_lshrrev_b64 v[26:27], v42, v[52:53]\n"
+                    "v_perm_b32 v26, v53, v52, v42\n"
                     ".Lqd" + U + ":\n"
                     "v_bfi_b32 " + D0 + ", s56, v26, " + D0 + "\n";
     ool += ".Lqm" + U + ":\n"
+           "s_mov_b64 s[68:69], vcc\n"
            "s_mov_b64 s[64:65], exec\n"
            "s_cmp_eq_u32 " + m.aligned + ", 0\n"
            "s_cbranch_scc1 .Lqf" + U + "\n"
