@@ -134,8 +134,33 @@ out:
     exit
 """
 
+# memory tier 1 (the general interpreter): an XDP_TX reflector that swaps the Ethernet source
+# and destination MACs in the packet (stores into the packet: emu.rs:354-372), accumulates the
+# length into a stack slot with an atomic add (emu.rs:373-437) and reflects frames of >= 60
+# bytes (XDP_TX), dropping runts.
+MAC_SWAP_TX = """
+    ldxw r3, [r1+0]           # destination MAC
+    ldxh r4, [r1+4]
+    ldxw r5, [r1+6]           # source MAC
+    ldxh r6, [r1+10]
+    stxw [r1+0], r5           # swap them in the packet
+    stxh [r1+4], r6
+    stxw [r1+6], r3
+    stxh [r1+10], r4
+    stdw [r10-8], 0
+    mov r7, r2
+    lock add [r10-8], r7      # length into a stack counter
+    ldxdw r0, [r10-8]
+    jlt r0, 60, drop
+    mov r0, 3                 # XDP_TX
+    exit
+drop:
+    mov r0, 1
+    exit
+"""
+
 PROGRAMS = {"drop": DROP_ALL, "5tuple": FIVE_TUPLE, "checksum": CHECKSUM,
-            "5tuple_stack": FIVE_TUPLE_STACK}
+            "5tuple_stack": FIVE_TUPLE_STACK, "mac_swap_tx": MAC_SWAP_TX}
 
 
 def program(name: str) -> bytes:

@@ -36,6 +36,10 @@ def test_workloads_compile():
 
     for name, src in W.PROGRAMS.items():
         p, ok = _eligible(assemble(src))
+        if name == "mac_swap_tx":  # packet stores + an atomic: the general interpreter's
+            assert not ok and p.tier == 1 and p.stack_window == 0
+            p.close()
+            continue
         assert ok, name
         # forward-only programs: the forward kernels (0, 1) and the loop kernel (2, for budgets
         # that can bind); the checksum loops: the loop kernel only
