@@ -947,25 +947,6 @@ FIXED_DMA = """.if %[fixed]
 s_waitcnt vmcnt(0)
 .endif
 """
-FIXED_DMA_DB = """.if %[fixed]
-; double-buffered windows (the compiled fixed-slot kernel): the wave's next tile (%[ntile], if
-; %[pf]) is DMA'd into the other buffer (%[nwinb]) before this one is processed, so every wave
-; keeps a window in flight; the first tile of the wave is DMA'd here too (%[first])
-s_cmp_eq_u32 %[first], 0
-s_cbranch_scc1 .Lnofirst%=
-""" + fixed_dma_db("%[winb]", "c") + """
-.Lnofirst%=:
-s_cmp_eq_u32 %[pf], 0
-s_cbranch_scc1 .Lnonext%=
-s_lshl_b64 {T0}, %[ntile], 6
-""" + fixed_dma_db("%[nwinb]", "n") + """
-s_waitcnt vmcnt(4)
-s_branch .Ldmad%=
-.Lnonext%=:
-s_waitcnt vmcnt(0)
-.Ldmad%=:
-.endif
-"""
 PROLOGUE = """s_mov_b32 {M0S}, m0
 s_mov_b64 {LIVE}, 0
 s_load_dwordx2 {PROG}, %[ka], %[o_tprog]
@@ -1264,56 +1245,181 @@ JIT_STATEMENT = "s_mov_b32 s70, 0\n" + PROLOGUE.replace(DEFAULT_INIT, JIT_INIT) 
 """ + EPILOGUE
 
 
-# The compiled fixed-slot kernel's statement (ebpf_tile_jit_fixed): the FIXED layout with double-
-# buffered windows (FIXED_DMA_DB), kernel arguments as loop-invariant SGPR operands (%[k_*],
-# loaded once per wave at kernel start instead of per-tile scalar loads and their waits), and the
-# rarely set outputs / init_regs behind %[k_flags] (bit 0 init_regs, 1 r0, 2 status, 3 regs).
-PROLOGUE_DB = """s_mov_b32 {M0S}, m0
-s_mov_b64 {PROG}, %[k_tprog]
-s_mov_b64 {KFR}, %[k_frames]
-s_mov_b64 {KST}, %[k_stride]
-s_mov_b64 {KN}, %[k_n]
+# ---- the compiled fixed-slot kernel's tile loop (ebpf_tile_jit_fixed) ----
+# One statement runs up to %[cdn] (511) of the wave's tiles back to back, so nothing of the
+# C++ around it is paid per tile (PMC: the per-tile statement above cost 241 instructions per
+# tile of 64 packets for a 3-instruction program, 116 of them SALU). Per tile:
+#   * the next ordinal of the workgroup's LDS counter, fetched one tile ahead (%[ordv]), gives
+#     the wave's next tile nt = wg + (ordinal + 16) * grid; its four window DMAs go to the other
+#     buffer (%[nwinb]) before this tile runs;
+#   * this tile's lanes: packet address = tile base + lane * stride, LDS window, registers;
+#   * the compiled program;
+#   * the verdict byte, and the lane's counter bucket as one add to a packed per-lane word
+#     (%[acc]: seven 9-bit fields, bucket b at bit 9b; <= 511 tiles per statement), retired steps
+#     added per lane (%[ret]) -- the C++ after the statement unpacks and sums them per wave.
+# Tiles wholly inside the batch in 64-byte slots take the inline DMA (%[nfast]: the tiles below
+# it); the batch's last partial tile and other slot sizes take fixed_dma_db out of line.
+# Loop state lives in the C++ operands (SGPRs / VGPRs outside the statement's v[0:95] and
+# s[33:71], which the program's code owns).
+def loop_dma(tidx, winb, tag):
+    """DMA tile `tidx` (an SGPR holding the tile index) into the window buffer `winb`. Returns
+    (inline text, out-of-line text)."""
+    main = f"""s_cmp_lt_u32 {tidx}, %[nfast]
+s_cbranch_scc0 .Lx{tag}%=
+s_mul_i32 {{T7L}}, {tidx}, %[tbytes]
+s_mul_hi_u32 {{T7H}}, {tidx}, %[tbytes]
+s_add_u32 {{T7L}}, {{T7L}}, %[fr_lo]
+s_addc_u32 {{T7H}}, {{T7H}}, %[fr_hi]
+v_lshl_add_u64 {{T1213}}, %[dmaoff], 0, {{T7}}
+s_mov_b32 m0, {winb}
+s_nop 0
+""" + "\n".join(f"global_load_lds_dwordx4 {{T1213}}, off offset:{1024 * r} ; @DMAPOLICY@"
+                for r in range(4)) + f"""
+.Ld{tag}%=:
+"""
+    ool = f""".Lx{tag}%=:
+s_mov_b64 {{KFR}}, %[k_frames]
+s_mov_b64 {{KST}}, %[k_stride]
+s_mov_b64 {{KN}}, %[k_n]
+s_mov_b64 {{PROG}}, %[k_tprog]
+s_mov_b32 {{T0L}}, {tidx}
+s_mov_b32 {{T0H}}, 0
+s_lshl_b64 {{T0}}, {{T0}}, 6
+v_mbcnt_lo_u32_b32 {{t0}}, -1, 0
+v_mbcnt_hi_u32_b32 {{t0}}, -1, {{t0}}
+""" + fixed_dma_db(winb, "y" + tag) + f"""
+s_branch .Ld{tag}%=
+"""
+    return main, ool
+
+
+def jit_statement_loop():
+    dma_f, ool_f = loop_dma("{T3}", "%[winb]", "f")
+    dma_n, ool_n = loop_dma("%[ntile]", "%[nwinb]", "n")
+    # the r0 / status / register outputs (%[oflags]): EPILOGUE's stores with T23 = packet index
+    out_tail = EPILOGUE[EPILOGUE.index("s_cmp_lg_u64 {ER0}, 0"):EPILOGUE.index(".Lend%=:")]
+    out_tail = out_tail.replace(".Lend%=", ".Loutd%=") + "s_branch .Loutd%="
+    main = """s_mov_b32 {M0S}, m0
+s_cmp_eq_u32 %[first], 0
+s_cbranch_scc1 .Lent%=
+; the wave's first tile: its windows
+s_mov_b32 {T3}, %[tile]
+""" + dma_f + """.Lent%=:
+s_movk_i32 %[cdn], 511
+.Lloop%=:
+; the next tile: nt = wg + (ordinal + waves) * grid, DMA'd into the other buffer
+s_mov_b64 exec, 1
+ds_add_rtn_u32 %[ordv], %[nxa], %[one]
+s_waitcnt lgkmcnt(0)
+s_mov_b64 exec, -1
+v_readfirstlane_b32 {T3}, %[ordv]
+s_add_u32 {T3}, {T3}, %[wpb]
+s_mul_i32 {T3}, {T3}, %[grid]
+s_add_u32 %[ntile], {T3}, %[wg]
+s_cmp_lt_u32 %[ntile], %[ntiles]
+s_cbranch_scc0 .Lnonext%=
+""" + dma_n + """s_waitcnt vmcnt(4)
+s_branch .Ldmad%=
+.Lnonext%=:
+s_waitcnt vmcnt(0)
+.Ldmad%=:
+; this tile's lanes (fixed slots: every lane of a whole tile is a packet of length %[lenc])
 s_mov_b32 {KMEM}, %[k_mem]
-v_mbcnt_lo_u32_b32 {t0}, -1, 0
-v_mbcnt_hi_u32_b32 {t0}, -1, {t0}
-s_lshl_b64 {T0}, %[tile], 6
-v_mov_b32 {t1}, 0
-v_lshl_add_u64 {T23}, {T01}, 0, {T0}
-""" + FIXED_DMA_DB + """v_cmp_gt_u64 vcc, {KN}, {T23}
-s_and_b64 {VM}, vcc, exec
-s_cmp_gt_u32 {KSTH}, 0
-s_cselect_b32 {T3}, -1, {KSTL}
-v_mov_b32 {LEN}, {T3}
-v_mov_b32 {t4}, {KSTL}
-v_mad_u64_u32 {BASE}, {T4}, {t2}, {t4}, {KFR}
-v_mul_lo_u32 {t4}, {t3}, {KSTL}
-v_mul_lo_u32 {t9}, {t2}, {KSTH}
-v_add3_u32 {BASEH}, {BASEH}, {t4}, {t9}
-v_cndmask_b32 {LEN}, 0, {LEN}, vcc
-v_lshlrev_b32 {WIN}, 6, {t0}
-v_add_u32 {WIN}, %[winb], {WIN}
-v_lshrrev_b32 {SWZ}, 2, {t0}
-v_and_b32 {SWZ}, 3, {SWZ}
-v_lshlrev_b32 {SWZ}, 4, {SWZ}
+s_mov_b64 {KR10}, %[k_r10]
+s_mov_b64 {VM}, -1
+s_mul_i32 {T0L}, %[tile], %[tbytes]
+s_mul_hi_u32 {T0H}, %[tile], %[tbytes]
+s_add_u32 {T0L}, {T0L}, %[fr_lo]
+s_addc_u32 {T0H}, {T0H}, %[fr_hi]
+v_lshl_add_u64 {BASE}, %[laneoff], 0, {T0}
+v_mov_b32 {LEN}, %[lenc]
+v_add_u32 {WIN}, %[winb], %[lane64]
+v_mov_b32 {SWZ}, %[swz]
 v_mov_b32 {NST}, 0
 v_mov_b32 {ST}, 0
-v_mov_b32 {LPC}, -1
-v_cmp_lt_u32 {T0}, {KMEM}, {LEN}
-s_and_b64 {T0}, {T0}, {VM}
-s_andn2_b64 {T1}, {VM}, {T0}
-s_mov_b64 exec, {T0}
-v_mov_b32 {ST}, 7
-s_mov_b64 exec, {T1}
 v_mov_b32 {LPC}, 0
-s_mov_b64 exec, {EXEC0}
-s_mov_b64 {KR10}, %[k_r10]
+s_cmp_lt_u32 %[tile], %[nfull]
+s_cbranch_scc0 .Lvm%=
+.Lvmd%=:
+s_cmp_gt_u32 %[lenc], %[k_mem]
+s_cbranch_scc1 .Lbad%=
+.Lbadd%=:
+s_cmp_lg_u32 %[initx], 0
+s_cbranch_scc1 .Linitx%=
+;@@JITINIT@@
+.Linitd%=:
+
+; JIT N=%= fixed=%[fixed] loops=%[loops] aligned=%[aligned]
+;@@JIT@@
+.Ldone%=:
+; verdict byte, the lane's counter bucket (verdict 0..4, 0xfe -> 5, 0xff -> 6) into %[acc]
+s_mov_b64 exec, {VM}
+v_cmp_gt_u64 vcc, 5, {RF}
+v_mov_b32 {t5}, 0xfe
+v_cndmask_b32 {t4}, {t5}, {RF0}, vcc
+v_cmp_eq_u32 vcc, 0, {ST}
+v_mov_b32 {t5}, 0xff
+v_cndmask_b32 {t4}, {t5}, {t4}, vcc
+v_subrev_u32 {t5}, 0xf9, {t4}
+v_min_u32 {t5}, {t4}, {t5}
+v_mul_u32_u24 {t5}, 9, {t5}
+v_lshlrev_b64 {T67}, {t5}, 1
+v_lshl_add_u64 %[acc], %[acc], 0, {T67}
+v_add_u32 %[ret], %[ret], {NST}
+s_cmp_lg_u64 %[k_verdict], 0
+s_cbranch_scc0 .Lnov%=
+s_lshl_b32 {T0L}, %[tile], 6
+s_lshr_b32 {T0H}, %[tile], 26
+s_add_u32 {T0L}, {T0L}, %[vd_lo]
+s_addc_u32 {T0H}, {T0H}, %[vd_hi]
+v_lshl_add_u64 {T67}, %[lanep], 0, {T0}
+global_store_byte {T67}, {t4}, off
+.Lnov%=:
+s_cmp_lg_u32 %[oflags], 0
+s_cbranch_scc1 .Lout%=
+.Loutd%=:
+s_mov_b64 exec, -1
+s_sub_u32 %[cdn], %[cdn], 1
+s_cmp_lt_u32 %[ntile], %[ntiles]
+s_cbranch_scc0 .Lfin%=
+s_mov_b32 %[tile], %[ntile]
+s_xor_b32 %[winb], %[winb], %[wx]
+s_xor_b32 %[nwinb], %[nwinb], %[wx]
+s_cmp_eq_u32 %[cdn], 0
+s_cbranch_scc0 .Lloop%=
+s_branch .Lexit%=
+.Lfin%=:
+s_mov_b32 %[tile], %[ntiles]
+.Lexit%=:
+s_waitcnt lgkmcnt(0)
+s_mov_b32 m0, {M0S}
+s_branch .Lend%=
+"""
+    # out of line: partial tile lanes, ST_BADPKT, init_regs / every register, the rare outputs
+    ool = ool_f + ool_n + """.Lvm%=:
+v_mbcnt_lo_u32_b32 {t0}, -1, 0
+v_mbcnt_hi_u32_b32 {t0}, -1, {t0}
+s_mov_b32 {T1L}, %[tile]
+s_mov_b32 {T1H}, 0
+s_lshl_b64 {T1}, {T1}, 6
+v_mov_b32 {t1}, 0
+v_lshl_add_u64 {T23}, {T01}, 0, {T1}
+v_cmp_gt_u64 vcc, %[k_n], {T23}
+s_mov_b64 {VM}, vcc
+s_not_b64 exec, vcc
+v_mov_b32 {LPC}, -1
+v_mov_b32 {LEN}, 0
+s_mov_b64 exec, -1
+s_branch .Lvmd%=
+.Lbad%=:
+s_mov_b64 exec, {VM}
+v_mov_b32 {ST}, 7
+v_mov_b32 {LPC}, -1
+s_mov_b64 exec, -1
+s_branch .Lbadd%=
+.Linitx%=:
 s_bitcmp1_b32 %[k_flags], 0
 s_cbranch_scc1 .Linitc%=
-s_bitcmp1_b32 %[k_flags], 3
-s_cbranch_scc1 .Lallinit%=
-;@@JITINIT@@
-s_branch .Linitd%=
-.Lallinit%=:
 """ + DEFAULT_INIT + """s_branch .Linitd%=
 .Linitc%=:
 s_load_dwordx2 {T5}, %[ka], %[o_init]
@@ -1325,48 +1431,20 @@ s_load_dwordx4 s[36:39], {T5}, 0x40
 s_load_dwordx2 s[40:41], {T5}, 0x50
 s_waitcnt lgkmcnt(0)
 """ + "\n".join(f"v_mov_b32 v{16 + i}, s{UB + i}" for i in range(6)) + """
-.Linitd%=:
-"""
-
-EPILOGUE_DB = """.Ldone%=:
-s_mov_b64 exec, {EXEC0}
-v_cmp_gt_u64 vcc, 5, {RF}
-v_cndmask_b32 %[bkt], 5, {RF0}, vcc
-v_cmp_ne_u32 vcc, 0, {ST}
-v_cndmask_b32_e64 %[bkt], %[bkt], 6, vcc
-v_cndmask_b32_e64 %[bkt], 7, %[bkt], {VM}
-v_cndmask_b32_e64 %[nst], 0, {NST}, {VM}
-s_mov_b64 exec, {VM}
-s_cmp_lg_u64 exec, 0
-s_cbranch_scc0 .Lend%=
-v_mbcnt_lo_u32_b32 {t0}, -1, 0
-v_mbcnt_hi_u32_b32 {t0}, -1, {t0}
-s_lshl_b64 {T0}, %[tile], 6
-v_mov_b32 {t1}, 0
-v_lshl_add_u64 {T23}, {T01}, 0, {T0}
-s_cmp_lg_u64 %[k_verdict], 0
-s_cbranch_scc0 .Lnov%=
-v_cmp_gt_u32 vcc, 5, %[bkt]
-v_mov_b32 {t5}, 0xfe
-v_cndmask_b32 {t4}, {t5}, {RF0}, vcc
-v_cmp_ne_u32 vcc, 6, %[bkt]
-v_mov_b32 {t5}, 0xff
-v_cndmask_b32 {t4}, {t5}, {t4}, vcc
-v_lshl_add_u64 {T67}, {T23}, 0, %[k_verdict]
-global_store_byte {T67}, {t4}, off
-.Lnov%=:
-s_and_b32 {T3}, %[k_flags], 14
-s_cbranch_scc0 .Lend%=
+s_branch .Linitd%=
+.Lout%=:
+s_mov_b32 {T1L}, %[tile]
+s_mov_b32 {T1H}, 0
+s_lshl_b64 {T1}, {T1}, 6
+v_lshl_add_u64 {T23}, %[lanep], 0, {T1}
 s_load_dwordx2 {ER0}, %[ka], %[o_r0]
 s_load_dwordx2 {EST}, %[ka], %[o_status]
 s_load_dwordx2 {ERG}, %[ka], %[o_regs]
 s_waitcnt lgkmcnt(0)
-""" + EPILOGUE[EPILOGUE.index("s_cmp_lg_u64 {ER0}, 0"):]
-
-JIT_STATEMENT_DB = PROLOGUE_DB + """
-; JIT N=%= fixed=%[fixed] loops=%[loops] aligned=%[aligned]
-;@@JIT@@
-""" + EPILOGUE_DB
+""" + out_tail + """
+.Lend%=:
+"""
+    return main + ool
 
 
 def handler_table():
@@ -1447,12 +1525,13 @@ def main():
     with open(os.path.join(HERE, "tile_jit.inc"), "w") as f:
         f.write("// GENERATED by gen_tile.py -- do not edit. The JIT template kernel's statement.\n"
                 "// clang-format off\n" + cstr(text) + "\n// clang-format on\n")
-    # the double-buffered fixed-slot kernel's (PROLOGUE_DB / EPILOGUE_DB)
-    text = F(JIT_STATEMENT_DB)
-    assert "{" not in text
-    with open(os.path.join(HERE, "tile_jit_db.inc"), "w") as f:
-        f.write("// GENERATED by gen_tile.py -- do not edit. The double-buffered JIT template "
-                "kernel's statement.\n// clang-format off\n" + cstr(text) + "\n// clang-format on\n")
+    # the compiled fixed-slot kernel's tile loop (jit_statement_loop)
+    text = F(jit_statement_loop())
+    assert "{" not in text, "unsubstituted register name: " + text[text.index("{"):][:40]
+    with open(os.path.join(HERE, "tile_jit_loop.inc"), "w") as f:
+        f.write("// GENERATED by gen_tile.py -- do not edit. The compiled fixed-slot kernel's tile "
+                "loop (one statement, many tiles).\n// clang-format off\n" + cstr(text) +
+                "\n// clang-format on\n")
     out = ["// GENERATED by gen_tile.py -- do not edit. Per-handler JIT templates (jit.cpp), indexed",
            "// by tile id (tile_ids.h): {main text, out-of-line text}.", "#pragma once",
            "// clang-format off", "static const char* const kJitTemplates[T_COUNT][2] = {"]

@@ -72,6 +72,17 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 }
 #undef WAVE_SUM_STEP
 
+// 32-bit: one DPP add per step
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, true);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, true);
+  return __builtin_amdgcn_readlane(v, 63);
+}
+
 // Explicit global (address space 1) accesses: pointers carried in LaunchArgs would otherwise be
 // generic and lower to flat_* instructions (which also count against lgkmcnt).
 typedef __attribute__((address_space(1))) const uint8_t g_u8;
@@ -371,12 +382,13 @@ __device__ __forceinline__ void counters_init() {
 constexpr uint64_t kShardCountShift = 48;
 constexpr uint64_t kShardSumMask = (1ull << kShardCountShift) - 1;
 
-template <uint32_t WPB = kWavesPerBlock>
+// (REDUCED: `retired` is already the wave's total)
+template <uint32_t WPB = kWavesPerBlock, bool REDUCED = false>
 __device__ __forceinline__ void flush_counters(const LaunchArgs& a, const uint64_t (&cnt)[7],
                                                uint64_t retired, uint8_t*, uint32_t lane,
                                                uint32_t) {
   if (a.counters == nullptr) return;
-  retired = wave_sum_u64(retired);
+  if (!REDUCED) retired = wave_sum_u64(retired);
   WgCounters* w = wg_counters();
   uint64_t mine = retired;
 #pragma unroll
@@ -1301,8 +1313,6 @@ constexpr uint32_t kTileWaveLds = kWinBytes + kDagMetaBytes;  // window + metada
 #define TILE_ASM_IN \
           [ka] "s"(ka), [tile] "s"(t), [winb] "s"(winb), [metab] "s"(metab), \
           [fixed] "i"(FIXED ? 1 : 0), [loops] "i"(LOOPS ? 1 : 0), [aligned] "s"(rfl(aligned)), \
-          [pf] "s"(rfl(pf)), [ntile] "s"(nt), [db] "i"(DB ? 1 : 0), [first] "s"(first), \
-          [nwinb] "s"(nwinb), \
           [o_tprog] "i"(offsetof(LaunchArgs, tprog)), \
           [o_tprog_exact] "i"(offsetof(LaunchArgs, tprog_exact)), \
           [o_maxs] "i"(offsetof(LaunchArgs, max_steps)), [o_perm] "i"(offsetof(LaunchArgs, perm)), \
@@ -1322,19 +1332,14 @@ constexpr uint32_t kTileWaveLds = kWinBytes + kDagMetaBytes;  // window + metada
 
 
 // JIT: the statement of the compiled-program template kernels (tile_jit.inc; jit.cpp fills in the
-// program's code at load time).
-// DB (the compiled fixed-slot kernel): two window buffers per wave, the next tile's DMA in flight
-// while the current one runs (kTileWaveLdsDb of LDS per wave).
+// program's code at load time). The compiled fixed-slot kernel (ebpf_tile_jit_fixed, below) has a
+// statement of its own that loops over the wave's tiles, with two window buffers per wave (the
+// next tile's DMA in flight while the current one runs).
 constexpr uint32_t kTileWaveLdsDb = 2 * kWinBytes;
 
-// DB also takes the whole CU as one workgroup of kDbWaves waves, whose tiles (b, b + G, b + 2G,
-// ... for workgroup b of G) the waves take in turn from an LDS counter instead of a fixed
-// stride: the waves of a SIMD are served in age order (the youngest used to finish ~3 us after
-// the oldest at 1 Mi packets), so a wave whose windows arrive early takes more tiles. Wave w
-// starts with ordinal w; each iteration takes the next ordinal for the window DMA it issues.
-template <bool FIXED, bool LOOPS, bool JIT, bool DB = JIT && FIXED && !LOOPS>
+template <bool FIXED, bool LOOPS, bool JIT>
 __device__ __forceinline__ void tile_body(LaunchArgs& a) {
-  constexpr uint32_t WPB = DB ? (uint32_t)kDbWaves : (uint32_t)kWavesPerBlock;
+  constexpr uint32_t WPB = kWavesPerBlock;
   counters_init();
   // the length bins of this batch were consumed by bin_scatter (earlier on the stream): re-zero
   if (LOOPS && a.perm && blockIdx.x == 0 && threadIdx.x < 2 * kBinClasses)
@@ -1342,56 +1347,19 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t wv = rfl(threadIdx.x / kWave);  // wave-uniform: keeps LDS addresses scalar
   WaveLds L;
-  L.win = smem + wv * (DB ? kTileWaveLdsDb : kTileWaveLds);
-  L.meta_off = (uint32_t*)(L.win + kWinBytes);  // (not used in DB mode)
+  L.win = smem + wv * kTileWaveLds;
+  L.meta_off = (uint32_t*)(L.win + kWinBytes);
   L.meta_len = L.meta_off + kWave;
-  const uint32_t win0 = lds_addr(L.win);
+  const uint32_t winb = lds_addr(L.win);
   const uint32_t metab = lds_addr(L.meta_off);
-  uint32_t buf = 0, first = 1;
-  // DB: the rarely set inputs / outputs (tile_jit_db.inc %[k_flags])
-  const uint32_t kflags = (a.init_regs ? 1u : 0u) | (a.r0 ? 2u : 0u) | (a.status ? 4u : 0u) |
-                          (a.regs_out ? 8u : 0u);
-  // DB: lane l's window-DMA source offset within a tile, (l/4) * stride + its swizzled 16-byte
-  // chunk (fixed_dma_db in gen_tile.py); a loop-invariant VGPR pair
-  uint64_t dmaoff = 0;
-  if (DB) {
-    uint32_t lane;
-    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
-    dmaoff = (uint64_t)(lane >> 2) * a.stride + (uint64_t)(((lane & 3u) ^ ((lane >> 4) & 3u)) * 16u);
-  }
   const uint64_t wave_slot = (uint64_t)blockIdx.x * WPB + wv;
   const uint64_t total_waves = (uint64_t)gridDim.x * WPB;
   const auto ka = __builtin_amdgcn_kernarg_segment_ptr();
-  const uint64_t grid = gridDim.x;  // DB: ordinal k is tile blockIdx + k * G
 
   uint32_t cnt[7] = {0, 0, 0, 0, 0, 0, 0};  // per wave: < 2^32 packets
   uint32_t retired = 0;                      // per lane: <= 63 steps per tile
-  // diagnostics only (a.trace, EBPFEMU_TRACE=1): s_memrealtime stamps per wave -- entry, after
-  // each tile, before and after the counter flush; no stamp executes otherwise
-  uint64_t* const trace = DB && a.trace && wave_slot < kTraceWaves
-                              ? a.trace + wave_slot * kTraceSlots : nullptr;
-  uint32_t ntr = 0;
-  auto stamp = [&](uint32_t slot) {
-    uint64_t ts;
-    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ts)::"memory");
-    if (__builtin_amdgcn_mbcnt_lo(~0u, 0) == 0) trace[slot] = ts;
-  };
-  if (trace) stamp(0);
 
-  for (uint64_t tile = DB ? blockIdx.x + (uint64_t)wv * grid : wave_slot; tile < a.n_tiles;) {
-    uint32_t nk = 0;
-    if (DB) {  // the next ordinal, from the workgroup's counter (one lane's LDS atomic)
-      uint32_t c;
-      uint64_t sv;
-      asm volatile(
-          "s_mov_b64 %[sv], exec\n\ts_mov_b64 exec, 1\n\t"
-          "ds_add_rtn_u32 %[c], %[addr], %[one]\n\ts_waitcnt lgkmcnt(0)\n\t"
-          "s_mov_b64 exec, %[sv]\n\tv_readfirstlane_b32 %[k], %[c]"
-          : [c] "=&v"(c), [sv] "=&s"(sv), [k] "=s"(nk)
-          : [addr] "v"(lds_addr(&wg_counters()->next)), [one] "v"(1u)
-          : "memory");
-      nk += WPB;
-    }
+  for (uint64_t tile = wave_slot; tile < a.n_tiles;) {
     // the lane index is re-derived inside the loop (volatile: not hoistable), so no per-lane
     // address of the window DMA stays live across the asm statement
     uint32_t aligned = 1;  // every packet base of the tile 16-byte aligned (loop-mode refills)
@@ -1429,24 +1397,9 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
       __builtin_amdgcn_s_waitcnt(0xc07f);  // the window's LDS writes / metadata reads: done
     }
     const uint64_t t = rfl64(tile);
-    // this wave's next tile (DMA'd now in DB mode)
-    // (32-bit scalar multiplies: a 64-bit one would be done in VGPRs)
-    const uint64_t nt =
-        DB ? blockIdx.x + ((uint64_t)__umulhi(nk, (uint32_t)grid) << 32 | (uint32_t)(nk * (uint32_t)grid))
-           : t + total_waves;
-    const uint32_t pf = nt < a.n_tiles ? 1u : 0u;
-    const uint32_t winb = DB ? win0 + buf * kWinBytes : win0;
-    const uint32_t nwinb = DB ? win0 + (buf ^ 1u) * kWinBytes : win0;
+    const uint64_t nt = t + total_waves;
     uint32_t bkt, nst;
-    if constexpr (JIT && DB) {  // kernel arguments as loop-invariant SGPR operands
-      asm volatile(
-#include "tile_jit_db.inc"
-          : TILE_ASM_OUT
-          : TILE_ASM_IN, [dmaoff] "v"(dmaoff), [k_frames] "s"(a.frames), [k_stride] "s"(a.stride),
-            [k_n] "s"(a.n), [k_mem] "s"(a.mem_size), [k_tprog] "s"(a.tprog), [k_r10] "s"(a.r10),
-            [k_verdict] "s"(a.verdict), [k_flags] "s"(rfl(kflags))
-          : TILE_ASM_CLOBBER, TILE_ASM_CLOBBER_WINDOW);
-    } else if constexpr (JIT) {
+    if constexpr (JIT) {
       asm volatile(
 #include "tile_jit.inc"
           TILE_ASM_OPERANDS);
@@ -1484,29 +1437,14 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
 #pragma unroll
     for (int b = 0; b < 7; b++) cnt[b] += __builtin_popcountll(ballot(bkt == (uint32_t)b));
     retired += nst;
-    buf ^= 1u;
-    first = 0;
-    if (trace && ntr < 10) stamp(1 + ntr++);
     tile = nt;
   }
-  if (trace) {
-    stamp(12);
-    uint32_t xcc, hw;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)\n\ts_getreg_b32 %1, hwreg(HW_REG_HW_ID)"
-                 : "=s"(xcc), "=s"(hw));
-    if (__builtin_amdgcn_mbcnt_lo(~0u, 0) == 0) {
-      trace[14] = ((uint64_t)xcc << 32) | hw;
-      trace[15] = ntr;
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // a next-tile prefetch may be in flight
   uint64_t cnt64[7];
 #pragma unroll
   for (int b = 0; b < 7; b++) cnt64[b] = cnt[b];
   uint32_t ln;
   asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
   flush_counters<WPB>(a, cnt64, retired, smem, ln, wv);
-  if (trace) stamp(13);
 }
 
 #ifndef EBPFEMU_JIT_TEMPLATE
@@ -1519,8 +1457,106 @@ __global__ __launch_bounds__(kBlock, 8) void tile_kernel(LaunchArgs a) {
 // program's compiled code at the marker of their statement and assembles the result.
 // (one workgroup of 16 waves per CU: its two window buffers per wave take the LDS, so 128 VGPRs
 // are free)
+//
+// ebpf_tile_jit_fixed: the wave's whole run of tiles in one asm statement (tile_jit_loop.inc,
+// gen_tile.py jit_statement_loop), re-entered only every 511 tiles to unpack the per-lane packed
+// counter buckets. Launch conditions (jit_fixed_ok): the fixed-slot layout, n_tiles < 2^31 and
+// 64 * stride < 2^32, so tile indices and tile byte offsets are 32-bit scalars.
 extern "C" __global__ __launch_bounds__(kDbBlock, 1) void ebpf_tile_jit_fixed(LaunchArgs a) {
-  tile_body<true, false, true>(a);
+  counters_init();
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint32_t wv = rfl(threadIdx.x / kWave);
+  uint32_t winb = lds_addr(smem + wv * kTileWaveLdsDb), nwinb = winb + kWinBytes;
+  const uint32_t wx = winb ^ nwinb;
+  uint32_t lane;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+  // lane l's window-DMA source offset within a tile (fixed_dma_db in gen_tile.py), its packet's
+  // offset, its LDS window offset and chunk swizzle -- loop-invariant
+  const uint64_t dmaoff =
+      (uint64_t)(lane >> 2) * a.stride + (uint64_t)(((lane & 3u) ^ ((lane >> 4) & 3u)) * 16u);
+  const uint64_t laneoff = (uint64_t)lane * a.stride;
+  const uint32_t lane64 = lane << 6, swz = ((lane >> 2) & 3u) << 4;
+  const uint64_t lanep = lane;
+  const uint32_t nxa = lds_addr(&wg_counters()->next), one = 1;
+  const uint32_t grid = gridDim.x, wg = blockIdx.x;
+  // (scalars computed with selects go through readfirstlane: an "s" operand left in a VGPR by the
+  // compiler would be printed as one)
+  const uint32_t ntiles = rfl((uint32_t)a.n_tiles), nfull = rfl((uint32_t)(a.n / kWave));
+  const uint32_t nfast = rfl(a.stride == (uint64_t)kWin ? nfull : 0u);
+  const uint32_t tbytes = rfl((uint32_t)(a.stride * kWave));
+  const uint32_t lenc = rfl(a.stride >> 32 ? 0xffffffffu : (uint32_t)a.stride);
+  const uint32_t kflags = rfl((a.init_regs ? 1u : 0u) | (a.r0 ? 2u : 0u) | (a.status ? 4u : 0u) |
+                              (a.regs_out ? 8u : 0u));
+  const uint32_t initx = rfl(kflags & 9u), oflags = rfl(kflags & 14u);
+  const uint64_t ka = (uint64_t)__builtin_amdgcn_kernarg_segment_ptr();
+  uint64_t* const trace = a.trace && (uint64_t)wg * kDbWaves + wv < kTraceWaves
+                              ? a.trace + ((uint64_t)wg * kDbWaves + wv) * kTraceSlots : nullptr;
+  auto stamp = [&](uint32_t slot) {
+    uint64_t ts;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ts)::"memory");
+    if (lane == 0) trace[slot] = ts;
+  };
+  if (trace) stamp(0);
+
+  uint32_t cnt[7] = {0, 0, 0, 0, 0, 0, 0};
+  uint32_t ret = 0, ordv = 0, first = 1, tile = wg + wv * grid, rounds = 0;
+  uint64_t retired = 0;
+  while (tile < ntiles) {
+    uint64_t acc = 0;
+    uint32_t cdn, ntile;
+    asm volatile(
+#include "tile_jit_loop.inc"
+        : [tile] "+s"(tile), [winb] "+s"(winb), [nwinb] "+s"(nwinb), [ordv] "+v"(ordv),
+          [acc] "+v"(acc), [ret] "+v"(ret), [cdn] "=&s"(cdn), [ntile] "=&s"(ntile)
+        : [first] "s"(first), [ka] "s"(ka), [k_tprog] "s"(a.tprog), [k_frames] "s"(a.frames),
+          [fr_lo] "s"((uint32_t)(uintptr_t)a.frames), [fr_hi] "s"((uint32_t)((uintptr_t)a.frames >> 32)),
+          [k_stride] "s"(a.stride), [k_n] "s"(a.n), [k_mem] "s"(a.mem_size), [k_r10] "s"(a.r10),
+          [k_verdict] "s"(a.verdict), [vd_lo] "s"((uint32_t)(uintptr_t)a.verdict),
+          [vd_hi] "s"((uint32_t)((uintptr_t)a.verdict >> 32)), [k_flags] "s"(kflags),
+          [initx] "s"(initx), [oflags] "s"(oflags), [grid] "s"(grid), [wg] "s"(wg),
+          [wpb] "i"(kDbWaves), [ntiles] "s"(ntiles), [nfull] "s"(nfull), [nfast] "s"(nfast),
+          [tbytes] "s"(tbytes), [lenc] "s"(lenc), [wx] "s"(wx),
+          [dmaoff] "v"(dmaoff), [laneoff] "v"(laneoff), [lane64] "v"(lane64), [swz] "v"(swz),
+          [lanep] "v"(lanep), [nxa] "v"(nxa), [one] "v"(one), [aligned] "s"(one),
+          [fixed] "i"(1), [loops] "i"(0), [o_init] "i"(offsetof(LaunchArgs, init_regs)),
+          [o_r0] "i"(offsetof(LaunchArgs, r0)), [o_status] "i"(offsetof(LaunchArgs, status)),
+          [o_regs] "i"(offsetof(LaunchArgs, regs_out))
+        : TILE_ASM_CLOBBER, TILE_ASM_CLOBBER_WINDOW);
+    // (an asm statement with VGPR outputs is divergent as a whole to the compiler: the scalar
+    // loop state goes back through readfirstlane, which is free on an SGPR)
+    tile = rfl(tile);
+    winb = rfl(winb);
+    nwinb = rfl(nwinb);
+    first = 0;
+    rounds++;
+    // the packed buckets (seven 9-bit fields per lane) summed over the wave two at a time, as
+    // 16-bit fields (<= 64 x 511), and this round's retired steps (<= 64 x 511 x 62 < 2^32)
+#pragma unroll
+    for (int b = 0; b < 7; b += 2) {
+      const uint32_t q = (uint32_t)(acc >> (9 * b)) & 511u;
+      const uint32_t s =
+          wave_sum_u32(b < 6 ? q | ((uint32_t)(acc >> (9 * b + 9)) & 511u) << 16 : q);
+      cnt[b] += s & 0xffffu;
+      if (b < 6) cnt[b + 1] += s >> 16;
+    }
+    retired += wave_sum_u32(ret);
+    ret = 0;
+  }
+  if (trace) {
+    stamp(12);
+    uint32_t xcc, hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)\n\ts_getreg_b32 %1, hwreg(HW_REG_HW_ID)"
+                 : "=s"(xcc), "=s"(hw));
+    if (lane == 0) {
+      trace[14] = ((uint64_t)xcc << 32) | hw;
+      trace[15] = rounds;
+    }
+  }
+  uint64_t cnt64[7];
+#pragma unroll
+  for (int b = 0; b < 7; b++) cnt64[b] = cnt[b];
+  flush_counters<kDbWaves, true>(a, cnt64, retired, smem, lane, wv);
+  if (trace) stamp(13);
 }
 extern "C" __global__ __launch_bounds__(kBlock, 8) void ebpf_tile_jit_var(LaunchArgs a) {
   tile_body<false, false, true>(a);
@@ -1624,6 +1660,11 @@ static bool fixed_layout(const LaunchArgs* a) {
 
 bool launch_fixed_layout(const LaunchArgs& a) { return fixed_layout(&a) && !g_no_tile; }
 
+// The compiled fixed-slot kernel keeps tile indices and tile byte offsets in 32-bit scalars.
+static bool jit_fixed_layout(const LaunchArgs* a) {
+  return fixed_layout(a) && a->n_tiles < (1ull << 31) && a->stride < (1ull << 26);
+}
+
 static const void* kernel_for(int kind, uint32_t n_uops, const LaunchArgs* a = nullptr) {
   if (kind == kKindDag) {
     if (tile_kernel_for(kind, n_uops))
@@ -1726,7 +1767,7 @@ static int jit_grid(hipFunction_t f, uint32_t lds, uint64_t n_tiles, int block =
 int launch_kernel_id(int kind, const LaunchArgs& a, const JitFns* jit, bool stack) {
   if (jit && jit->loop && kind == kKindLoop) return EBPF_KERNEL_JIT_LOOP;
   if (jit && jit->fixed && kind == kKindDag && tile_kernel_for(kind, a.n_uops))
-    return fixed_layout(&a) ? (stack ? EBPF_KERNEL_JIT_STACK : EBPF_KERNEL_JIT_FIXED)
+    return jit_fixed_layout(&a) ? (stack ? EBPF_KERNEL_JIT_STACK : EBPF_KERNEL_JIT_FIXED)
                             : EBPF_KERNEL_JIT_VAR;
   if (kind == kKindDag)
     return tile_kernel_for(kind, a.n_uops) ? EBPF_KERNEL_TILE : EBPF_KERNEL_DAG;
@@ -1752,7 +1793,7 @@ hipError_t launch_interp(int kind, const LaunchArgs& a, int grid, hipStream_t st
   if (jit && jit->loop && kind == kKindLoop) {  // the compiled loop program
     e = hipModuleLaunchKernel(jit->loop, grid, 1, 1, kBlock, 1, 1, lds, stream, bargs, nullptr);
   } else if (jit && jit->fixed && kind == kKindDag && tile_kernel_for(kind, a.n_uops)) {
-    if (fixed_layout(&a)) {  // double-buffered windows: its own LDS size and grid
+    if (jit_fixed_layout(&a)) {  // double-buffered windows: its own LDS size and grid
       const uint32_t dlds = g_lds_pad + kDbWaves * kTileWaveLdsDb;
       e = hipModuleLaunchKernel(jit->fixed, jit_grid(jit->fixed, dlds, a.n_tiles, kDbBlock), 1, 1,
                                 kDbBlock, 1, 1, dlds, stream, bargs, nullptr);

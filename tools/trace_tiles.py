@@ -71,9 +71,10 @@ def main():
     ntiles = tr[:, 15].astype(int)
     out = {"waves": int(len(tr)), "tiles_per_wave": sorted(set(ntiles.tolist())),
            "entry": pct(us(tr[:, 0]))}
-    for k in range(1, int(ntiles.max()) + 1):
-        sel = ntiles >= k
-        out[f"tile{k}_done"] = pct(us(tr[sel, k]))
+    for k in range(1, min(10, int(ntiles.max())) + 1):
+        sel = (ntiles >= k) & (tr[:, k] != 0)  # (the tile-loop kernel stamps no tiles)
+        if sel.any():
+            out[f"tile{k}_done"] = pct(us(tr[sel, k]))
     out["flush_start"] = pct(us(tr[:, 12]))
     out["flush_end"] = pct(us(tr[:, 13]))
     out["flush_len"] = pct((tr[:, 13].astype(np.int64) - tr[:, 12].astype(np.int64)) / 100.0)
