@@ -1239,10 +1239,13 @@ def cstr(text):
 # prologue, a marker the compiler fills in at load time, the epilogue. The marker line carries the
 # statement's label number and operand registers.
 # (s70: loop programs' exact-mode flag, set by the compiled code's step-budget restart)
-JIT_STATEMENT = "s_mov_b32 s70, 0\n" + PROLOGUE.replace(DEFAULT_INIT, JIT_INIT) + """
+# s70 bit 1: the registers are not the main.rs layout (init_regs) or are outputs (regs) -- the
+# compiled loop programs' proven copy (jit.cpp prove_loads) assumes the layout and dead registers
+JIT_STATEMENT = ("s_mov_b32 s70, 0\n" + PROLOGUE.replace(DEFAULT_INIT, JIT_INIT) + """
 ; JIT N=%= fixed=%[fixed] loops=%[loops] aligned=%[aligned]
 ;@@JIT@@
-""" + EPILOGUE
+""" + EPILOGUE).replace(".Lallinit%=:\n", ".Lallinit%=:\ns_or_b32 s70, s70, 2\n").replace(
+    ".Linitc%=:\n", ".Linitc%=:\ns_or_b32 s70, s70, 2\n")
 
 
 # ---- the compiled fixed-slot kernel's tile loop (ebpf_tile_jit_fixed) ----

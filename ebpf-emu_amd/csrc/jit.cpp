@@ -24,6 +24,7 @@
 #include <amd_comgr/amd_comgr.h>
 
 #include <algorithm>
+#include <array>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -273,6 +274,246 @@ struct Compiler {
   // hoist[L] (loop programs): the parked pc written at the entry of single-block loop head L, or
   // -2 (none)
   std::vector<int64_t> hoist;
+
+  // ---- load-time value ranges: one-byte loads proven in bounds (loop programs) ----
+  // The abstract value of a register in the main.rs layout (main.rs:28-31): an unsigned interval
+  // [lo, hi]; slack d >= 0 when 0 <= r and r + d <= LEN, the packet's length (LEN <= mem_size for
+  // every lane that runs, main.rs:20-21, and <= 2^24), else -1; is_len: r == LEN. Jumps compare
+  // signed (emu.rs:230-290, Q2), so a bound is taken from a compare only for a value known
+  // non-negative. A one-byte load [r + off] with off + 1 <= slack(r) reads a packet byte: it can
+  // neither fault (mmu.rs:16) nor read past the packet, whatever mem_size is.
+  struct AbsVal {
+    uint64_t lo = 0, hi = ~0ull;
+    int64_t slack = -1;
+    bool is_len = false;
+  };
+  using AbsRegs = std::array<AbsVal, 11>;
+  static constexpr uint64_t kLenMax = 1ull << 24;  // mem_size bound (include/ebpf_emu.h)
+  std::vector<char> inb;   // inb[i]: the one-byte LDX i is proven in bounds
+  bool proven = false;     // emitting the proven copy (ldx1_loop drops inb[i] loads' checks)
+
+  static AbsVal av_const(uint64_t c) {
+    AbsVal v;
+    v.lo = v.hi = c;
+    v.slack = c == 0 ? 0 : -1;
+    return v;
+  }
+  static void av_norm(AbsVal& v) {
+    if (v.slack >= 0) v.hi = std::min(v.hi, kLenMax), v.lo = std::min(v.lo, v.hi);
+  }
+  static AbsVal av_meet(const AbsVal& a, const AbsVal& b) {
+    AbsVal v;
+    v.lo = std::min(a.lo, b.lo);
+    v.hi = std::max(a.hi, b.hi);
+    v.slack = (a.slack < 0 || b.slack < 0) ? -1 : std::min(a.slack, b.slack);
+    v.is_len = a.is_len && b.is_len;
+    return v;
+  }
+  static bool av_eq(const AbsVal& a, const AbsVal& b) {
+    return a.lo == b.lo && a.hi == b.hi && a.slack == b.slack && a.is_len == b.is_len;
+  }
+  // r + c (c as a two's complement 64-bit constant)
+  static AbsVal av_add_const(const AbsVal& r, uint64_t c) {
+    AbsVal v;  // (full range unless proven free of wrap-around)
+    const int64_t sc = (int64_t)c;
+    if (sc >= 0 && sc < (1ll << 40) && r.hi < (1ull << 62)) {
+      v.lo = r.lo + c, v.hi = r.hi + c;
+      if (r.slack >= sc) v.slack = r.slack - sc;
+    } else if (sc < 0 && sc > -(1ll << 40) && r.lo >= (uint64_t)-sc) {
+      v.lo = r.lo + c, v.hi = r.hi + c;
+      if (r.slack >= 0) v.slack = r.slack - sc;
+    }
+    av_norm(v);
+    return v;
+  }
+
+  // Transfer of micro-op u over s; jumps also give the taken successor's state (tk).
+  static void av_step(const Uop& u, const AbsRegs& s, AbsRegs& nt, AbsRegs& tk) {
+    nt = s;
+    tk = s;
+    const bool reg = (u.aux & F_SRC) != 0;
+    const AbsVal b = reg ? s[u.src] : av_const((uint64_t)u.k);
+    const bool bconst = b.lo == b.hi;
+    AbsVal& d = nt[u.dst];
+    const AbsVal a = s[u.dst];
+    auto full32 = [] { AbsVal v; v.hi = 0xffffffffull; return v; };
+    switch (u.op) {
+      case U_MOV64: d = b; return;
+      case U_ADD64: {  // (both facts hold when both operands are constants: keep the stronger)
+        AbsVal x, y;
+        if (bconst) x = av_add_const(a, b.lo);
+        if (a.lo == a.hi) y = av_add_const(b, a.lo);
+        d.lo = std::max(x.lo, y.lo), d.hi = std::min(x.hi, y.hi);
+        d.slack = std::max(x.slack, y.slack);
+        d.is_len = (a.is_len && bconst && b.lo == 0) || (b.is_len && a.lo == 0 && a.hi == 0);
+        return;
+      }
+      case U_SUB64:
+        d = bconst ? av_add_const(a, 0 - b.lo) : AbsVal();
+        d.is_len = a.is_len && bconst && b.lo == 0;
+        return;
+      case U_AND64:
+        d = AbsVal();
+        if (b.hi < (1ull << 63)) d.hi = b.hi;
+        if (a.hi < (1ull << 63)) d.hi = std::min(d.hi, a.hi), d.slack = a.slack;  // r & c <= r
+        if (a.lo == a.hi && bconst) d = av_const(a.lo & b.lo);
+        return;
+      case U_RSH64:
+        if (bconst && b.lo < 64) {
+          d = AbsVal();
+          d.lo = a.lo >> b.lo, d.hi = a.hi >> b.lo, d.slack = a.slack;  // r >> c <= r
+          return;
+        }
+        d = AbsVal();
+        return;
+      case U_LSH64:
+        d = AbsVal();
+        if (bconst && b.lo < 63 && a.hi < (1ull << (62 - b.lo))) d.lo = a.lo << b.lo, d.hi = a.hi << b.lo;
+        return;
+      case U_MOV32:
+        d = bconst ? av_const(b.lo & 0xffffffffull) : full32();
+        return;
+      case U_AND32:
+        d = full32();
+        if (bconst) d.hi = b.lo & 0xffffffffull;
+        return;
+      case U_ZX16: case U_BSWAP16: d = AbsVal(); d.hi = 0xffff; return;
+      case U_ZX32: case U_BSWAP32: d = full32(); return;
+      case U_BSWAP64: d = AbsVal(); return;
+      case U_NOP: return;
+      case U_LDIMM: d = av_const((uint64_t)u.k); return;
+      case U_LDX: {  // the loaded bytes replace the low aux bytes; the rest of dst stays (Q1)
+        d = AbsVal();
+        if (u.aux < 8 && a.hi < (1ull << (8 * u.aux))) d.hi = (1ull << (8 * u.aux)) - 1;
+        return;
+      }
+      default: break;
+    }
+    if (u.op <= U_ARSH32) {  // the other ALU operations
+      d = u.op >= U_ADD32 ? full32() : AbsVal();
+      return;
+    }
+    if (u.op < U_JEQ || u.op > U_JLE) return;  // JA, 32-bit jumps, EXIT, ...: no refinement
+    // signed compares of dst with b (Q2); refinements only for a non-negative dst
+    AbsVal& dt = tk[u.dst];
+    AbsVal& dn = nt[u.dst];
+    const bool nn = a.hi < (1ull << 63);
+    const int64_t K = (int64_t)b.lo;
+    auto below = [&](AbsVal& v, int64_t lim) {  // v < lim
+      if (nn && lim >= 1) v.hi = std::min(v.hi, (uint64_t)lim - 1), v.lo = std::min(v.lo, v.hi);
+    };
+    auto atleast = [&](AbsVal& v, int64_t lim) {  // v >= lim
+      if (nn && lim >= 0 && (uint64_t)lim <= v.hi) v.lo = std::max(v.lo, (uint64_t)lim);
+    };
+    auto lt_len = [&](AbsVal& v, int64_t sl) {  // 0 <= v and v + sl <= LEN
+      if (v.hi < (1ull << 63)) v.slack = std::max(v.slack, sl), av_norm(v);
+    };
+    if (bconst && !b.is_len) {
+      switch (u.op) {
+        case U_JEQ:
+          if (nn && b.lo <= a.hi && b.lo >= a.lo) dt = av_const(b.lo), dt.slack = std::max(dt.slack, a.slack);
+          break;
+        case U_JNE:
+          if (nn && b.lo <= a.hi && b.lo >= a.lo) dn = av_const(b.lo), dn.slack = std::max(dn.slack, a.slack);
+          break;
+        case U_JGT: atleast(dt, K + 1); below(dn, K + 1); break;
+        case U_JGE: atleast(dt, K); below(dn, K); break;
+        case U_JLT: below(dt, K); atleast(dn, K); break;
+        case U_JLE: below(dt, K + 1); atleast(dn, K + 1); break;
+        default: break;
+      }
+    }
+    if (!reg) return;
+    AbsVal& st = tk[u.src];
+    AbsVal& sn = nt[u.src];
+    if (b.is_len) {  // dst ? LEN
+      switch (u.op) {
+        case U_JLT: lt_len(dt, 1); break;
+        case U_JGE: lt_len(dn, 1); break;
+        case U_JLE: lt_len(dt, 0); break;
+        case U_JGT: lt_len(dn, 0); break;
+        default: break;
+      }
+    } else if (a.is_len) {  // LEN ? src
+      switch (u.op) {
+        case U_JGT: lt_len(st, 1); break;
+        case U_JLE: lt_len(sn, 1); break;
+        case U_JGE: lt_len(st, 0); break;
+        case U_JLT: lt_len(sn, 0); break;
+        default: break;
+      }
+    }
+  }
+
+  // Forward dataflow to a fixpoint over the micro-ops (meet at joins, bounds widened after a few
+  // changes at a loop head); fills inb[]. Programs with stores, atomics or calls prove nothing.
+  void prove_loads() {
+    inb.assign(n, 0);
+    for (const Uop& u : uops)
+      if (u.op == U_ST || u.op == U_STX || u.op == U_ATOMIC || u.op == U_CALL) return;
+    std::vector<AbsRegs> in(n);
+    std::vector<char> seen(n, 0);
+    std::vector<uint32_t> changes(n, 0);
+    AbsRegs init;
+    for (int r = 0; r < 11; r++) init[r] = av_const(0);
+    init[2] = AbsVal();
+    init[2].hi = kLenMax, init[2].slack = 0, init[2].is_len = true;  // r2 = LEN (main.rs:29)
+    init[10] = AbsVal();                                              // r10: a launch value
+    std::vector<char> head(n, 0);  // targets of back edges
+    for (uint32_t i = 0; i < n; i++)
+      if (is_jump(uops[i]) && (uint32_t)uops[i].x <= i) head[(uint32_t)uops[i].x] = 1;
+    std::vector<uint32_t> work{0};
+    in[0] = init;
+    seen[0] = 1;
+    auto flow = [&](uint32_t to, const AbsRegs& s) {
+      if (to >= n) return;
+      if (!seen[to]) {
+        in[to] = s, seen[to] = 1, work.push_back(to);
+        return;
+      }
+      AbsRegs m;
+      bool ch = false;
+      for (int r = 0; r < 11; r++) {
+        m[r] = av_meet(in[to][r], s[r]);
+        if (head[to] && changes[to] > 4) {  // widen at loop heads
+          if (m[r].hi != in[to][r].hi) m[r].hi = m[r].slack >= 0 ? kLenMax : ~0ull;
+          if (m[r].lo != in[to][r].lo) m[r].lo = 0;
+        }
+        ch = ch || !av_eq(m[r], in[to][r]);
+      }
+      if (ch) in[to] = m, changes[to]++, work.push_back(to);
+    };
+    for (size_t steps = 0; !work.empty() && steps < 100000; steps++) {
+      const uint32_t i = work.back();
+      work.pop_back();
+      const Uop& u = uops[i];
+      AbsRegs nt, tk;
+      av_step(u, in[i], nt, tk);
+      if (u.op == U_EXIT || u.op == U_FAULT) continue;
+      if (u.op == U_JA) {
+        flow((uint32_t)u.x, tk);
+        continue;
+      }
+      if (is_jump(u)) flow((uint32_t)u.x, tk);
+      flow(i + 1, nt);
+    }
+    if (!work.empty()) return;  // (no fixpoint within the bound: prove nothing)
+    if (getenv("EBPFEMU_RANGES"))  // diagnostics: the state at every micro-op
+      for (uint32_t i = 0; i < n; i++) {
+        fprintf(stderr, "%2u op %2u d%u s%u:", i, uops[i].op, uops[i].dst, uops[i].src);
+        for (int r = 0; r < 11 && seen[i]; r++)
+          fprintf(stderr, " r%d[%llx,%llx]%s%lld", r, (unsigned long long)in[i][r].lo,
+                  (unsigned long long)in[i][r].hi, in[i][r].is_len ? "L" : "", (long long)in[i][r].slack);
+        fprintf(stderr, "\n");
+      }
+    for (uint32_t i = 0; i < n; i++) {
+      const Uop& u = uops[i];
+      if (!seen[i] || u.op != U_LDX || u.aux != 1) continue;
+      const int64_t off = (int64_t)(int32_t)u.x;
+      const AbsVal& b = in[i][u.src];
+      inb[i] = b.slack >= 0 && off >= 0 && off + 1 <= b.slack;
+    }
+  }
 
   // back edges into each pc: a loop head with exactly one lets that jump's taken lanes run the
   // head's block straight away (no lane can be parked there but them)
@@ -733,15 +974,16 @@ struct Compiler {
     } else {
       s += "v_lshl_add_u64 v[36:37], " + vpair(u.src2, 0, 1) + ", 0, " + offs + "\n";
     }
-    s += "v_cmp_gt_u64 vcc, s[52:53], " + AP + "\n"
-         "s_andn2_b64 s[64:65], exec, vcc\n"
-         "s_cbranch_scc0 .Lok" + U + "\n"
-         "s_mov_b64 s[66:67], exec\ns_mov_b64 exec, s[64:65]\n"
-         "v_mov_b32 v30, 1\nv_mov_b32 v28, -1\n"
-         "v_subrev_u32 v29, " + std::to_string(u.a0) + ", v29\n"
-         "s_andn2_b64 exec, s[66:67], s[64:65]\n"
-         "s_cbranch_execz " + next + "\n"
-         ".Lok" + U + ":\n";
+    if (!(proven && inb[i]))  // (a load proven to read a packet byte cannot fault)
+      s += "v_cmp_gt_u64 vcc, s[52:53], " + AP + "\n"
+           "s_andn2_b64 s[64:65], exec, vcc\n"
+           "s_cbranch_scc0 .Lok" + U + "\n"
+           "s_mov_b64 s[66:67], exec\ns_mov_b64 exec, s[64:65]\n"
+           "v_mov_b32 v30, 1\nv_mov_b32 v28, -1\n"
+           "v_subrev_u32 v29, " + std::to_string(u.a0) + ", v29\n"
+           "s_andn2_b64 exec, s[66:67], s[64:65]\n"
+           "s_cbranch_execz " + next + "\n"
+           ".Lok" + U + ":\n";
     if (cache) return s + byte_cache(U, A, D0, m, ool);
     if (zwin && qcache) return s + ldx1_qword_cache(U, A, D0, m, ool);
     if (zwin) return s + ldx1_zero_window(U, A, D0, m, ool);
@@ -1280,17 +1522,33 @@ struct Compiler {
     return body_loop_once(m, xc, out);
   }
 
+  // s70 (set by the statement's prologue, tile_jit.inc): bit 0 = exact mode (the step-budget
+  // restart), bit 1 = registers not in the main.rs layout (init_regs) or requested as outputs.
+  // With bit 1 clear, a program with loads proven in bounds (prove_loads) runs its proven copy.
   bool body_loop_once(const Marker& m, Compiler& xc, std::string& out) {
-    const std::string P = "J" + m.n + "_", PX = "J" + m.n + "x_";
+    const std::string P = "J" + m.n + "_", PX = "J" + m.n + "x_", PC = "J" + m.n + "c_";
     std::string main = "; compiled eBPF loop program: " + std::to_string(n) + " micro-ops\n"
                        "s_mov_b32 s52, s33\ns_mov_b32 s53, 0\ns_movk_i32 s56, 0xff\n"
                        "s_not_b32 s57, s71\ns_mov_b64 exec, -1\nv_add_u32 v29, s57, v29\n"
                        "v_mov_b32 v55, 0x80000000\n" + window_zero_prologue(m, P) +
-                       "s_cmp_lg_u32 s70, 0\ns_cbranch_scc1 .L" + PX + "start\n"
-                       "s_mov_b64 exec, 0\n";
+                       "s_bitcmp1_b32 s70, 0\ns_cbranch_scc1 .L" + PX + "start\n";
     std::string ool;
-    if (!copy(m, P, false, main, ool)) return false;
-    main += "s_branch .L" + P + "end\n.L" + P + "budget:\ns_mov_b32 s70, 1\n"
+    prove_loads();
+    const bool any = std::find(inb.begin(), inb.end(), 1) != inb.end();
+    if (any) {
+      main += "; one-byte loads proven in bounds: the proven copy unless s70 bit 1\n"
+              "s_bitcmp1_b32 s70, 1\ns_cbranch_scc1 .L" + PC + "go\ns_mov_b64 exec, 0\n";
+      proven = true;
+      const bool ok = copy(m, P, false, main, ool);
+      proven = false;
+      if (!ok) return false;
+      main += "s_branch .L" + P + "end\n.L" + PC + "go:\n";
+    }
+    main += "s_mov_b64 exec, 0\n";
+    const std::string PB = any ? PC : P;  // the checked block copy
+    if (!copy(m, PB, false, main, ool)) return false;
+    main += "s_branch .L" + P + "end\n" + (any ? ".L" + PC + "budget:\n" : std::string()) +
+            ".L" + P + "budget:\ns_or_b32 s70, s70, 1\n"
             "s_cmp_eq_u32 " + m.aligned + ", 0\ns_cbranch_scc1 .L" + P + "bkeep\n"
             "v_mov_b32 v22, -64\n.L" + P + "bkeep:\ns_mov_b64 exec, -1\n"
             "s_branch .Lreinit" + m.n + "\n.L" + PX + "start:\ns_mov_b64 exec, 0\n";

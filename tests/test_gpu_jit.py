@@ -97,6 +97,32 @@ def test_fuzz_loop_programs_compile():
     assert n >= 100
 
 
+def test_loop_range_proofs_compile():
+    """The loop compiler's range analysis (jit.cpp prove_loads) proves exactly the byte scans whose
+    index is non-negative and below r2 on every path (test_gpu_loops.RANGE_PROGRAMS); the proven
+    copy has no bounds check on those loads. Random scans compile either way."""
+    import random as _r
+
+    from ebpf_emu import Program
+    from ebpf_emu.asm import assemble
+    from test_gpu_loops import RANGE_PROGRAMS, gen_scan_program
+
+    for name, src in RANGE_PROGRAMS.items():
+        p = Program(assemble(src))
+        assert p.compile()
+        text = p.jit_asm(2)
+        assert ("one-byte loads proven in bounds" in text) == name.startswith("proven"), name
+        p.close()
+    rng = _r.Random(3)
+    proven = 0
+    for _ in range(60):
+        p = Program(assemble(gen_scan_program(rng)))
+        assert p.compile()
+        proven += "one-byte loads proven in bounds" in p.jit_asm(2)
+        p.close()
+    assert 6 <= proven <= 54, proven
+
+
 # ---------------------------------------------------------------------------------------------
 def _run(img, pkts, dev, fixed_stride=None, offsets_layout=False, init_regs=None, no_jit=False,
          mem_size=1024, r10=512, prod=False):

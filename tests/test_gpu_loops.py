@@ -185,3 +185,107 @@ def _oracle_batch(pkts):
         pos += len(p)
     return (np.frombuffer(buf, dtype=np.uint8), len(pkts)), dict(
         offsets=np.array(offs, dtype=np.uint32), lens=np.array([len(p) for p in pkts], dtype=np.uint16))
+
+
+# Loop programs whose one-byte loads the compiler proves in bounds (jit.cpp prove_loads: the
+# index is non-negative and below r2 = the packet length on every path) or must not prove: the
+# proven copy drops their bounds checks, so these pin the analysis's edges -- an offset past the
+# proof, a `jle` bound (index == len), a negative start (signed compares, Q2), r2 changed in the
+# loop, the `jgt r2, r3` form, a 32-bit compare -- on packets as long as the image (mem_size), so
+# that every unproven load that overruns faults exactly where the oracle does.
+RANGE_PROGRAMS = {
+    "proven": FORWARD_SUM,
+    "proven_jgt_len": """
+    mov r0, 0
+    mov r3, 0
+    jge r3, r2, done
+loop:
+    mov r4, r1
+    add r4, r3
+    ldxb r5, [r4+0]
+    add r0, r5
+    add r3, 1
+    jgt r2, r3, loop
+done:
+    exit
+""",
+    "off_past_proof": FORWARD_SUM.replace("[r4+0]", "[r4+1]"),
+    "jle_bound": FORWARD_SUM.replace("jlt r3, r2, loop", "jle r3, r2, loop"),
+    "negative_start": FORWARD_SUM.replace("mov r3, 0", "mov r3, -3"),
+    "len_changed": FORWARD_SUM.replace("add r3, 1", "add r3, 1\n    add r2, 1"),
+    "jlt32": FORWARD_SUM.replace("jlt r3, r2, loop", "jlt32 r3, r2, loop"),
+    "proven_stride2": FORWARD_SUM.replace("add r3, 1", "add r3, 2"),
+}
+
+
+def gen_scan_program(rng):
+    """A random byte scan: r3 from a start value, step, guard and back-edge compare drawn from
+    forms the range analysis proves or must refuse (offsets past the proof, <= bounds, negative
+    starts, constant bounds, r2 rewritten), loads [r1 + r3 + off]."""
+    ok = rng.random() < 0.5  # half from the provable forms only
+    start = rng.choice([0, 1, 3] + ([] if ok else [-1, -5]))
+    step = rng.choice([1, 1, 2, 3])
+    off = rng.choice([0] if ok else [0, 1, 2, -1])
+    guard = rng.choice(["jge r3, r2, done", "jle r2, r3, done"] +
+                       ([] if ok else ["jge r3, 40, done", ""]))
+    back = rng.choice(["jlt r3, r2, loop", "jgt r2, r3, loop"] +
+                      ([] if ok else ["jle r3, r2, loop", "jge r2, r3, loop", "jne r3, r2, loop",
+                                      "jlt r3, 40, loop", "jlt32 r3, r2, loop"]))
+    extra = rng.choice(["", "and r3, 0x3f"] + ([] if ok else ["add r2, 1", "mov r2, 200"]))
+    return f"""
+    mov r0, 0
+    mov r3, {start}
+    {guard}
+loop:
+    mov r4, r1
+    add r4, r3
+    ldxb r5, [r4{off:+d}]
+    add r0, r5
+    {extra}
+    add r3, {step}
+    {back}
+done:
+    exit
+"""
+
+
+@pytest.mark.parametrize("seed", range(2))
+def test_fuzz_range_proofs(cuda, oracle_mod, seed):
+    """Random byte scans (gen_scan_program), proven or not, on packets as long as the image:
+    the production outputs (the proven copy) and the full outputs (the checked copy) against the
+    oracle, status of every packet included."""
+    from ebpf_emu.asm import assemble
+
+    rng = random.Random(8080 + seed)
+    for it in range(24):
+        img = assemble(gen_scan_program(rng))
+        mem = rng.choice([64, 96])
+        pkts = [bytes(rng.getrandbits(8) for _ in range(rng.choice([0, 5, mem - 2, mem, mem])))
+                for _ in range(130)]
+        prod = _run_prod(img, pkts, cuda, mem_size=mem, max_steps=3000)
+        _check_prod_against_oracle(oracle_mod, img, pkts, prod, mem_size=mem, max_steps=3000,
+                                   tag=f"seed {seed} it {it}")
+
+
+@pytest.mark.parametrize("name", sorted(RANGE_PROGRAMS))
+def test_loop_range_proofs(cuda, oracle_mod, name):
+    from ebpf_emu import Program
+    from ebpf_emu.asm import assemble
+
+    img = assemble(RANGE_PROGRAMS[name])
+    p = Program(img)
+    assert p.compile()
+    proven = "one-byte loads proven in bounds" in p.jit_asm(2)
+    p.close()
+    assert proven == name.startswith("proven"), name
+    rng = random.Random(hash(name) & 0xffff)
+    for mem in (64, 128):
+        pkts = [bytes(rng.getrandbits(8) for _ in range(rng.choice([0, 1, 17, mem - 1, mem, mem])))
+                for _ in range(200)]
+        for layout in (dict(), dict(offsets_layout=True, align=16)):
+            prod = _run_prod(img, pkts, cuda, mem_size=mem, **layout)
+            _check_prod_against_oracle(oracle_mod, img, pkts, prod, mem_size=mem,
+                                       tag=f"{name} mem {mem} {layout}")
+            got = _run_full(img, pkts, cuda, mem_size=mem, **layout)
+            _check_against_oracle(oracle_mod, img, pkts, got, mem_size=mem,
+                                  tag=f"full {name} mem {mem} {layout}")
