@@ -35,8 +35,9 @@ CONFIGS = {
     # the 5-tuple with its flow key spilled to the stack and reloaded (memory tier 0.5: the
     # stack window in registers of the compiled kernel); same frames and verdicts as 5tuple
     "stack": (2, "IPv4 5-tuple, flow key spilled to r10-16 and reloaded (38 insns) over 1Mi x 64B frames"),
-    # memory tier 1 (stores into the packet, an atomic): the general interpreter's throughput
-    "tier1": (2, "XDP_TX MAC-swap reflector with packet stores and a stack atomic (17 insns, general interpreter) over 1Mi x 64B frames"),
+    # stores into the packet's header window and an atomic on the stack (memory tier 0.5 with
+    # packet-window stores; --generic: the general interpreter's tier 1)
+    "tier1": (2, "XDP_TX MAC-swap reflector with packet stores and a stack atomic (17 insns) over 1Mi x 64B frames"),
 }
 PROGRAM_OF = {"stack": "5tuple_stack", "tier1": "mac_swap_tx"}
 

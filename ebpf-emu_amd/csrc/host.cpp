@@ -452,8 +452,9 @@ static std::vector<TUop> build_tile(const std::vector<Uop>& uops, const std::vec
     const uint32_t h = d[i].hoff / DAG_SLOT;
     const bool is_jump = uops[i].op >= U_JA && uops[i].op <= U_JLE32;
     if (is_jump && (uint32_t)uops[i].x < n) start[(uint32_t)uops[i].x] = 1;
-    // (a stack-window program's stores are compiled in line: jit.cpp, not block ends)
-    const bool stack_store = stack && (uops[i].op == U_ST || uops[i].op == U_STX);
+    // (a stack-window program's stores and atomics are compiled in line: jit.cpp, not block ends)
+    const bool stack_store =
+        stack && (uops[i].op == U_ST || uops[i].op == U_STX || uops[i].op == U_ATOMIC);
     term[i] = exact || is_jump || h == H_EXIT || h == H_FAULT || (h == H_SLOW && !stack_store);
     if (term[i]) start[i + 1] = 1;
   }
@@ -478,7 +479,8 @@ static std::vector<TUop> build_tile(const std::vector<Uop>& uops, const std::vec
     u.imm = o.imm;
     u.width = o.width;
     u.blen = start[i] ? rem[i] : 0;
-    if (h == H_LDX || h == H_ARSH64_IMM || h == H_ARSH64_REG) u.a0 = rem[i];  // REMX
+    if (h == H_LDX || h == H_ARSH64_IMM || h == H_ARSH64_REG || (stack && uops[i].op == U_ATOMIC))
+      u.a0 = rem[i];  // REMX
     if (h == H_LDX && o.width == 1) id = chained ? T_LDX1_C : T_LDX1_E;  // one byte: one dword
     if (h == H_LDXK || h == H_LDXK_FAR) {
       const uint32_t a0 = o.a0, w = o.end - o.a0;
@@ -590,6 +592,11 @@ static std::vector<DUop> fold_const_loads(const std::vector<Uop>& uops, std::vec
         break;
       case U_NOP:
         break;
+      case U_ST: case U_STX:  // registers unchanged (the dst write-back of emu.rs:443)
+        break;
+      case U_ATOMIC:  // (a stack-window program's) fetch writes src, CMPXCHG r0 (emu.rs:409-436)
+        s.known[u.src] = s.known[0] = s.known[u.dst] = false;
+        break;
       default:  // every other micro-op of tier 0 writes dst with a value not tracked here
         s.known[u.dst] = false;
         break;
@@ -621,9 +628,13 @@ static StackAnalysis analyze_stack(const std::vector<Uop>& uops) {
   bool any_store = false;
   for (uint32_t i = 0; i < n; i++) {
     const Uop& u = uops[i];
-    if (u.op == U_ATOMIC || u.op == U_CALL) return res;
+    if (u.op == U_CALL) return res;
     if (u.op >= U_JA && u.op <= U_JLE32 && (uint32_t)u.x <= i) return res;  // forward only
-    any_store = any_store || u.op == U_ST || u.op == U_STX;
+    // atomics: the operations emu.rs:391-419 implements (others panic: the general interpreter)
+    if (u.op == U_ATOMIC && !(u.k == 0x00 || u.k == 0x40 || u.k == 0x50 || u.k == 0xa0 ||
+                              u.k == 0xe0 || u.k == 0xf0))
+      return res;
+    any_store = any_store || u.op == U_ST || u.op == U_STX || u.op == U_ATOMIC;
   }
   if (!any_store) return res;
   enum Kind : uint8_t { TOP, CONST, FP };
@@ -642,8 +653,9 @@ static StackAnalysis analyze_stack(const std::vector<Uop>& uops) {
     for (int r = 0; r < 11; r++)
       if (!same(t.r[r], st.r[r])) t.r[r] = Val{TOP, 0};
   };
-  std::vector<int32_t> off(n, kNoStack);
+  std::vector<int32_t> off(n, kNoStack), pw(n, kNoStack);
   std::vector<char> dyn(n, 0);  // LDX with an unknown base
+  bool any_pw = false;
   int64_t lo = 0, hi = INT64_MIN;  // store bytes relative to r10: [lo, hi)
   for (uint32_t i = 0; i < n; i++) {
     if (!in[i].reached) continue;
@@ -651,17 +663,26 @@ static StackAnalysis analyze_stack(const std::vector<Uop>& uops) {
     Regs st = in[i];
     const bool src = u.aux & F_SRC;
     const Val S = st.r[u.src], D = st.r[u.dst];
-    if (u.op == U_ST || u.op == U_STX) {
-      if (D.k != FP) return res;
-      const int64_t d = D.v + (int64_t)u.x;
-      if (d < -(int64_t)kStackMax || d + u.aux > 0) return res;
-      off[i] = (int32_t)d;
-      lo = std::min(lo, d);
-      hi = std::max(hi, d + (int64_t)u.aux);
+    if (u.op == U_ST || u.op == U_STX || u.op == U_ATOMIC) {
+      const int64_t w = u.op == U_ATOMIC ? 8 : u.aux;  // (an atomic reads and writes 8 bytes)
+      if (D.k == CONST && u.op != U_ATOMIC) {  // into the packet's header window (r1 = 0)
+        const int64_t c = D.v + (int64_t)u.x;
+        if (c < 0 || c + w > (int64_t)kWin) return res;
+        pw[i] = (int32_t)c;
+        any_pw = true;
+      } else {
+        if (D.k != FP) return res;
+        const int64_t d = D.v + (int64_t)u.x;
+        if (d < -(int64_t)kStackMax || d + w > 0) return res;
+        if (u.op == U_ATOMIC && (d & 3)) return res;
+        off[i] = (int32_t)d;
+        lo = std::min(lo, d);
+        hi = std::max(hi, d + w);
+      }
     }
     if (u.op == U_LDX) {
       if (S.k == FP) off[i] = (int32_t)std::max<int64_t>(INT32_MIN + 1, std::min<int64_t>(INT32_MAX, S.v + u.x));
-      else dyn[i] = 1;
+      else if (S.k != CONST) dyn[i] = 1;
     }
     switch (u.op) {
       case U_JA: case U_JEQ: case U_JGT: case U_JGE: case U_JSET: case U_JNE: case U_JLT:
@@ -674,6 +695,11 @@ static StackAnalysis analyze_stack(const std::vector<Uop>& uops) {
         continue;
       case U_ST: case U_STX: case U_NOP:
         break;  // the destination register keeps its value (emu.rs:443)
+      case U_ATOMIC:  // fetch: src = the old value; CMPXCHG: r0 = it; dst restored (Q14)
+        if (u.aux & F_FETCH) st.r[u.src] = Val{TOP, 0};
+        if (u.k == 0xf0) st.r[0] = Val{TOP, 0};
+        st.r[u.dst] = D;
+        break;
       case U_MOV64: st.r[u.dst] = src ? S : Val{CONST, u.k}; break;
       case U_LDIMM: st.r[u.dst] = Val{CONST, u.k}; break;
       case U_ADD64: case U_SUB64: {
@@ -691,7 +717,19 @@ static StackAnalysis analyze_stack(const std::vector<Uop>& uops) {
     }
     flow(i + 1, st);
   }
-  const uint32_t k = (uint32_t)((-lo + 3) & ~3);
+  // packet-window stores: every load must be a constant-address one (fold_const_loads reads the
+  // stored bytes from the window registers) or a stack-window one, none straddling the window's
+  // end (its bytes below kWin would come from HBM)
+  if (any_pw)
+    for (uint32_t i = 0; i < n; i++) {
+      const Uop& u = uops[i];
+      if (u.op != U_LDX || !in[i].reached || off[i] != kNoStack) continue;
+      const Val S = in[i].r[u.src];
+      const int64_t a = S.v + (int64_t)u.x;
+      if (dyn[i] || S.k != CONST || (a < (int64_t)kWin && a + u.aux > (int64_t)kWin)) return res;
+    }
+  // (a plan with packet-window stores only keeps a 4-byte stack window)
+  const uint32_t k = std::max<uint32_t>((uint32_t)((-lo + 3) & ~3), any_pw ? 4u : 0u);
   if (hi > 0 || k == 0 || k > kStackMax) return res;
   for (uint32_t i = 0; i < n; i++) {
     const Uop& u = uops[i];
@@ -699,13 +737,16 @@ static StackAnalysis analyze_stack(const std::vector<Uop>& uops) {
     const int64_t d = off[i];
     if (d >= -(int64_t)k && d + u.aux <= 0) continue;       // inside the window
     if (d + u.aux <= -(int64_t)k || d >= 0) {                 // disjoint: an ordinary load at a
-      off[i] = kNoStack;                                      // uniform address, checked at run
-      continue;                                               // time like any other
+      if (any_pw) return res;                                 // uniform address, checked at run
+      off[i] = kNoStack;                                      // time like any other (not with
+      continue;                                               // packet stores: LDS is stale)
     }
     return res;                                               // straddles the window's edge
   }
   res.plan.k = k;
   res.plan.off = std::move(off);
+  res.plan.pw = std::move(pw);
+  res.plan.any_pw = any_pw;
   return res;
 }
 
@@ -757,8 +798,14 @@ int ebpf_prog_load(const uint8_t* code, size_t nbytes, ebpf_prog** out, size_t* 
   }
   if (p->tier == 1 && !g_no_stack) {  // memory tier 0.5: the compiled fixed-slot kernel only
     StackAnalysis sa = analyze_stack(p->uops);
+    const std::vector<DUop> dk =
+        sa.plan.k ? fold_const_loads(p->uops, build_dag(p->uops)) : std::vector<DUop>();
+    // packet-window stores: every load outside the stack window must be a constant-address one
+    // (read from the window registers the stores update)
+    for (size_t i = 0; sa.plan.k && sa.plan.any_pw && i < p->uops.size(); i++)
+      if (p->uops[i].op == U_LDX && sa.plan.off[i] == kNoStack && (dk[i].opaux & 0xff) != U_LDXK)
+        sa.plan.k = 0;
     if (sa.plan.k) {
-      const std::vector<DUop> dk = fold_const_loads(p->uops, build_dag(p->uops));
       for (const DUop& o : dk)
         if ((o.opaux & 0xff) == U_LDXK) p->kloads.push_back({o.addr, o.opaux >> 8});
       p->tuopsk = build_tile(p->uops, dk, false, true);
@@ -946,8 +993,14 @@ static bool stack_launch_ok(const ebpf_prog* p, const ebpf_batch* b, const ebpf_
   if (b->init_regs || b->init_fp_len || out->mem || b->max_steps < p->uops.size()) return false;
   const uint64_t k = p->stack.k, r10 = b->r10;
   if (r10 % 4 || r10 < k || r10 > b->mem_size || r10 - k < b->stride) return false;
-  for (const auto& kl : p->kloads)
+  for (const auto& kl : p->kloads) {
     if (kl.first < r10 && kl.first + kl.second > r10 - k) return false;
+    // packet-window stores: the compiled code has only the copy whose window loads read the
+    // preloaded (and stored-to) registers, which runs when mem_size covers every such load
+    if (p->stack.any_pw && kl.first + kl.second <= (uint64_t)kWin &&
+        kl.first + kl.second > b->mem_size)
+      return false;
+  }
   LaunchArgs a{};
   a.frames = b->frames;
   a.offsets = b->offsets;

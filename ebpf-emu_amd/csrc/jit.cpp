@@ -862,8 +862,19 @@ struct Compiler {
   // (STX: src register; ST: the zero-extended immediate, Q8) written little-endian
   // (emu.rs:354-372). Per window dword the bytes it takes, by a move (whole dword) or a v_perm.
   std::string stack_store(uint32_t i) const {
+    return store_bytes(i, (uint32_t)((int32_t)stk->k + stk->off[i]), kStackVgpr);
+  }
+
+  // ST / STX into the packet's header window at the constant image address pw[i]: the window
+  // dwords the fast copy preloaded into v[64 + j] (every later load of those bytes is a
+  // constant-address one reading them, host.cpp analyze_stack)
+  std::string pw_store(uint32_t i) const { return store_bytes(i, (uint32_t)stk->pw[i], 64); }
+
+  // The store of micro-op i at byte p of a window held in v[base + j] (dword j).
+  std::string store_bytes(uint32_t i, uint32_t p, uint32_t base) const {
     const Uop& o = uops[i];
-    const uint32_t p = (uint32_t)((int32_t)stk->k + stk->off[i]), w = o.aux;
+    const uint32_t w = o.aux;
+    auto sv = [&](uint32_t j) { return "v" + std::to_string(base + j); };
     const bool imm = o.op == U_ST;
     const uint64_t kv = (uint64_t)o.k;  // ST: imm64 (zero-extended imm)
     const std::string V0 = "v" + std::to_string(2 * o.src), V1 = "v" + std::to_string(2 * o.src + 1);
@@ -908,6 +919,69 @@ struct Compiler {
            ", s36\n";
     }
     return s;
+  }
+
+  // ATOMIC on the stack window at byte p = k + off (static, 4-aligned; 8 bytes read and written,
+  // emu.rs:373-437 as oracle/ebpf_oracle.c restates it): orig = the window qword; the 32-bit form
+  // works on its low word, the operand's and r0's low words, and adds the high word back after
+  // the operation (a 32-bit ADD's carry leaks into it, Q13); ADD and the recombination fault
+  // ST_ARITH on signed overflow (the debug build's checks, Q21); XCHG and CMPXCHG as the
+  // reference (CMPXCHG: r0 = the fetched value, 0 without fetch); fetch writes the old value to
+  // src; dst is written back from its snapshot last (Q14). Faulting lanes stop with the steps of
+  // this micro-op and the rest of its block not retired.
+  std::string stack_atomic(uint32_t i, const std::string& P) const {
+    const Uop& o = uops[i];
+    const uint32_t p = (uint32_t)((int32_t)stk->k + stk->off[i]), j = p >> 2;
+    const bool w32 = o.aux & F_ATOMIC32, fetch = o.aux & F_FETCH;
+    const uint32_t op = (uint32_t)o.k;
+    const std::string W0 = sv(j), W1 = sv(j + 1);
+    const std::string S0 = "v" + std::to_string(2 * o.src), S1 = "v" + std::to_string(2 * o.src + 1);
+    const std::string D = vpair(2 * o.dst, 0, 1), S = vpair(2 * o.src, 0, 1);
+    const std::string U = P + "u" + std::to_string(i), next = entry_label(P, next_start(i));
+    // v[36:37] orig, v[38:39] operand, v[40:41] fetched, v[42:43] result, v[44:45] dst snapshot
+    std::string s = "v_mov_b64 v[44:45], " + D + "\nv_mov_b32 v36, " + W0 + "\n" +
+                    (w32 ? "v_mov_b32 v37, 0\n" : "v_mov_b32 v37, " + W1 + "\n") +
+                    "v_mov_b32 v38, " + S0 + "\n" +
+                    (w32 ? "v_mov_b32 v39, 0\n" : "v_mov_b32 v39, " + S1 + "\n") +
+                    (fetch ? "v_mov_b64 v[40:41], v[36:37]\n" : "v_mov_b64 v[40:41], 0\n");
+    std::string ovf;  // lanes that overflow (vcc), from the operation and the recombination
+    switch (op) {
+      case 0x00:  // ADD
+        s += "v_lshl_add_u64 v[42:43], v[36:37], 0, v[38:39]\n";
+        if (!w32)  // signed overflow: both operands' signs differ from the sum's
+          s += "v_xor_b32 v46, v37, v43\nv_xor_b32 v47, v39, v43\nv_and_b32 v46, v46, v47\n"
+               "v_cmp_gt_i32 vcc, 0, v46\n";
+        break;
+      case 0x40: s += "v_or_b32 v42, v36, v38\nv_or_b32 v43, v37, v39\n"; break;
+      case 0x50: s += "v_and_b32 v42, v36, v38\nv_and_b32 v43, v37, v39\n"; break;
+      case 0xa0: s += "v_xor_b32 v42, v36, v38\nv_xor_b32 v43, v37, v39\n"; break;
+      case 0xe0: s += "v_mov_b64 v[42:43], v[38:39]\nv_mov_b64 v[40:41], v[36:37]\n"; break;
+      default:  // 0xf0 CMPXCHG: compare with r0 (its low word in the 32-bit form)
+        s += std::string("v_mov_b32 v46, v0\n") + (w32 ? "v_mov_b32 v47, 0\n" : "v_mov_b32 v47, v1\n") +
+             "v_cmp_eq_u64 vcc, v[36:37], v[46:47]\n"
+             "v_cndmask_b32 v42, v36, v38, vcc\nv_cndmask_b32 v43, v37, v39, vcc\n";
+        break;
+    }
+    const bool add_ovf = op == 0x00 && !w32;
+    if (w32) {  // + (high << 32): overflows when the high word is non-negative and the sum is not
+      s += "v_add_u32 v43, v43, " + W1 + "\nv_not_b32 v46, " + W1 + "\nv_and_b32 v46, v46, v43\n"
+           "v_cmp_gt_i32 vcc, 0, v46\n";
+      ovf = "vcc";
+    } else if (add_ovf) {
+      ovf = "vcc";
+    }
+    if (!ovf.empty())
+      s += "s_cbranch_vccz .Lnf" + U + "\n"
+           "s_mov_b64 s[66:67], exec\ns_mov_b64 exec, vcc\n"
+           "v_mov_b32 v30, 4\nv_mov_b32 v28, -1\n"
+           "v_subrev_u32 v29, " + std::to_string(t[i].a0) + ", v29\n"
+           "s_andn2_b64 exec, s[66:67], vcc\n"
+           "s_cbranch_execz " + next + "\n"
+           ".Lnf" + U + ":\n";
+    s += "v_mov_b32 " + W0 + ", v42\nv_mov_b32 " + W1 + ", v43\n";
+    if (op == 0xf0) s += "v_mov_b64 v[0:1], v[40:41]\n";
+    if (fetch) s += "v_mov_b64 " + S + ", v[40:41]\n";
+    return s + "v_mov_b64 " + D + ", v[44:45]\n";
   }
 
   // A register-address load of a stack-window program: the lanes whose bytes [a, a + w) overlap
@@ -1392,7 +1466,13 @@ struct Compiler {
       }
       if (stk && (uops[i].op == U_ST || uops[i].op == U_STX)) {
         // (a store the load-time dataflow never reached has no offset: no lane executes it)
-        main += stk->off[i] == kNoStack ? std::string("; unreachable store\n") : stack_store(i);
+        main += stk->pw[i] != kNoStack    ? pw_store(i)
+                : stk->off[i] == kNoStack ? std::string("; unreachable store\n")
+                                          : stack_store(i);
+        continue;
+      }
+      if (stk && uops[i].op == U_ATOMIC) {
+        main += stk->off[i] == kNoStack ? std::string("; unreachable atomic\n") : stack_atomic(i, P);
         continue;
       }
       if (stk && uops[i].op == U_LDX && stk->off[i] != kNoStack) {
@@ -1481,20 +1561,30 @@ struct Compiler {
         for (uint32_t k = a0 >> 2; k <= last && k < 16; k++) chunks |= 1u << (k >> 2);
         maxend = std::max(maxend, end);
       }
+    // packet-window stores merge into the preloaded dwords; such programs have only the fast
+    // copy (the launch checks mem_size >= every window load's end, host.cpp stack_launch_ok)
+    const bool pw = stk && stk->any_pw && m.fixed == "1";
+    for (uint32_t i = 0; pw && i < n; i++)
+      if (stk->pw[i] != kNoStack)
+        for (uint32_t b = (uint32_t)stk->pw[i]; b < (uint32_t)stk->pw[i] + uops[i].aux; b++)
+          chunks |= 1u << (b >> 4);
     if (chunks) {
       const std::string F = "J" + m.n + "f_";
-      main += "s_cmp_gt_u32 " + std::to_string(maxend) + ", s33\ns_cbranch_scc1 .L" + P +
-              "slow\n";
+      if (!pw)
+        main += "s_cmp_gt_u32 " + std::to_string(maxend) + ", s33\ns_cbranch_scc1 .L" + P +
+                "slow\n";
       for (uint32_t c = 0; c < 4; c++)
         if (chunks & (1u << c))
           main += "v_xad_u32 v36, v35, " + std::to_string(16 * c) + ", v34\nds_read_b128 v[" +
                   std::to_string(64 + 4 * c) + ":" + std::to_string(67 + 4 * c) + "], v36\n";
       main += "s_waitcnt lgkmcnt(0)\ns_mov_b64 exec, 0\n";
       if (!copy(m, F, true, main, ool)) return false;
-      main += "s_branch .L" + P + "end\n.L" + P + "slow:\n";
+      main += "s_branch .L" + P + "end\n" + (pw ? "" : ".L" + P + "slow:\n");
     }
-    main += "s_mov_b64 exec, 0\n";
-    if (!copy(m, P, false, main, ool)) return false;
+    if (!pw) {
+      main += "s_mov_b64 exec, 0\n";
+      if (!copy(m, P, false, main, ool)) return false;
+    }
     main += ".L" + P + "end:\n";
     if (!ool.empty()) main += "s_branch .Ldone" + m.n + "\n" + ool;
     out = main;
@@ -1715,7 +1805,8 @@ bool jit_compile(const std::vector<Uop>& uops, const std::vector<TUop>& t,
                  std::vector<char>& code_object, std::string* err, std::string* asm_out,
                  const StackPlan* stk) {
   if (uops.empty() || uops.size() > kTileMaxUops || t.size() < uops.size() ||
-      (stk && (stk->k == 0 || stk->k > kStackMax || stk->k % 4 || stk->off.size() != uops.size()))) {
+      (stk && (stk->k == 0 || stk->k > kStackMax || stk->k % 4 || stk->off.size() != uops.size() ||
+               stk->pw.size() != uops.size()))) {
     if (err) *err = "not a tile program";
     return false;
   }

@@ -19,16 +19,21 @@ struct JitFns {
   hipFunction_t loop = nullptr;  // loop programs (ebpf_tile_jit_loop)
 };
 
-// Stack-window programs (memory tier 0.5, host.cpp analyze_stack): every store writes the
-// window [r10 - k, r10) at an offset known at load time, so the window lives in VGPRs of the
-// compiled fixed-slot kernel (v[kStackVgpr : kStackVgpr + k/4]).
+// Stack-window programs (memory tier 0.5, host.cpp analyze_stack): every store or atomic writes
+// the window [r10 - k, r10) at an offset known at load time, so the window lives in VGPRs of the
+// compiled fixed-slot kernel (v[kStackVgpr : kStackVgpr + k/4]); stores may also write the
+// packet's header window at constant addresses (the preloaded window dwords v[64 : 79]).
 constexpr uint32_t kStackMax = 64;    // window bytes
 constexpr uint32_t kStackVgpr = 80;   // first VGPR of the window (ebpf_tile_jit_fixed)
 constexpr int32_t kNoStack = INT32_MIN;
 struct StackPlan {
-  uint32_t k = 0;            // window bytes (multiple of 4, <= kStackMax); 0 = no stack window
-  std::vector<int32_t> off;  // per micro-op: ST/STX, and LDX inside the window: the access's
-                             // offset from r10 (-k <= off, off + width <= 0); else kNoStack
+  uint32_t k = 0;            // window bytes (multiple of 4, <= kStackMax); 0 = no plan
+  std::vector<int32_t> off;  // per micro-op: ST/STX, ATOMIC (8 bytes, 4-aligned) and LDX inside
+                             // the window: the access's offset from r10 (-k <= off,
+                             // off + width <= 0); else kNoStack
+  std::vector<int32_t> pw;   // per micro-op: ST/STX into the packet's header window at a constant
+                             // image address [0, kWin - width] (r1 = 0, main.rs:28); else kNoStack
+  bool any_pw = false;
 };
 
 // Compiles a forward-only program of <= kTileMaxUops micro-ops (its tile table `t`, built by

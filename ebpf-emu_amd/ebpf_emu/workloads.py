@@ -134,10 +134,10 @@ out:
     exit
 """
 
-# memory tier 1 (the general interpreter): an XDP_TX reflector that swaps the Ethernet source
-# and destination MACs in the packet (stores into the packet: emu.rs:354-372), accumulates the
-# length into a stack slot with an atomic add (emu.rs:373-437) and reflects frames of >= 60
-# bytes (XDP_TX), dropping runts.
+# an XDP_TX reflector that swaps the Ethernet source and destination MACs in the packet (stores
+# into the packet: emu.rs:354-372), accumulates the length into a stack slot with an atomic add
+# (emu.rs:373-437) and reflects frames of >= 60 bytes (XDP_TX), dropping runts. Memory tier 0.5
+# with packet-window stores on fixed slots (the compiled kernel), tier 1 elsewhere.
 MAC_SWAP_TX = """
     ldxw r3, [r1+0]           # destination MAC
     ldxh r4, [r1+4]

@@ -121,12 +121,15 @@ def gen_packet(rng: random.Random, max_len: int = 80) -> bytes:
     return bytes(rng.getrandbits(8) for _ in range(n))
 
 
-def gen_stack_program(rng: random.Random, n: int | None = None, k: int = 32) -> bytes:
+def gen_stack_program(rng: random.Random, n: int | None = None, k: int = 32,
+                      pw_atomics: bool = False) -> bytes:
     """Forward-only programs whose stores all hit the stack window [r10 - k, r10) (memory tier
     0.5): ST/STX of every width at aligned and misaligned r10 offsets, directly and through a copy
     of r10 (`mov r9, r10; add r9, -c`), loads of the window at r10 offsets, loads of the packet,
     and register-address loads aimed just below and into the window through r1 (the store-
-    forwarding overlay, r10 = 512 in the main.rs layout) -- mixed with ALU ops and forward jumps."""
+    forwarding overlay, r10 = 512 in the main.rs layout) -- mixed with ALU ops and forward jumps.
+    pw_atomics: also stack atomics (every operation, 32/64-bit, with and without fetch, at aligned
+    r10 offsets) and ST/STX into the packet's first 64 bytes, without register-address loads."""
     n = n or rng.randrange(6, 40)
     words: list[bytes] = []
     if rng.random() < 0.5:  # a second pointer into the stack
@@ -142,6 +145,21 @@ def gen_stack_program(rng: random.Random, n: int | None = None, k: int = 32) -> 
         src = rng.randrange(10)
         size = rng.choice(list(sizes))
         w = sizes[size]
+        if pw_atomics and q < 0.12:  # an atomic on the window, or a packet-window store
+            if rng.random() < 0.5:
+                d = -4 * rng.randrange(2, k // 4 + 1)
+                base, off = (10, d) if c is None or rng.random() < 0.5 else (9, d + c)
+                aop = rng.choice([0x00, 0x40, 0x50, 0xA0, 0xE0, 0xF0]) | rng.choice([0, 1])
+                words.append(encode(0xC3 | rng.choice([0x00, 0x18]), base, src, off, aop))
+            else:
+                off = rng.randrange(0, 64 - w + 1)
+                if rng.random() < 0.4:
+                    words.append(encode(0x62 | size, 1, 0, off, _imm(rng)))
+                else:
+                    words.append(encode(0x63 | size, 1, src, off))
+            continue
+        if pw_atomics and 0.55 <= q < 0.62:
+            q = 0.5  # (no register-address loads)
         if q < 0.25:  # ST / STX into the window
             d = -rng.randrange(w, k + 1)
             base, off = (10, d) if c is None or rng.random() < 0.5 else (9, d + c)

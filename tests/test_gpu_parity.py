@@ -414,8 +414,9 @@ def test_workload_sample_vs_oracle(cuda, oracle_mod):
 
 def test_tier1_workload_vs_oracle(cuda, oracle_mod):
     """The tier-1 bench workload (workloads.MAC_SWAP_TX: packet stores, a stack atomic) on 64 Ki
-    + 5 fixed-slot frames on the general interpreter: status, r0 and counters equal the oracle's,
-    and the final images of a sample show the swapped MACs."""
+    + 5 fixed-slot frames -- on the compiled kernel (memory tier 0.5 with packet-window stores)
+    and on the general interpreter (tier 1): status, r0 and counters equal the oracle's, and the
+    final images of a sample (an image output: the general interpreter) show the swapped MACs."""
     import torch
 
     from ebpf_emu import Program, _lib
@@ -426,15 +427,16 @@ def test_tier1_workload_vs_oracle(cuda, oracle_mod):
     frames = torch.from_numpy(buf).to(cuda)
     img = W.program("mac_swap_tx")
     prog = Program(img)
-    assert prog.batch_kernel(prog.make_batch(frames, n=n, stride=64)) == _lib.EBPF_KERNEL_GENERAL_T1
-    cnt = torch.zeros(8, dtype=torch.int64, device=cuda)
-    res = prog.run(frames, n=n, stride=64, r0=True, status=True, counters=cnt)
-    torch.cuda.synchronize()
     r0, st, ocnt = oracle_mod.Program(img).run_batch(buf, n, stride=64, threads=8)
-    assert np.array_equal(res.status.cpu().numpy(), st)
-    assert np.array_equal(res.r0.cpu().numpy().view(np.uint64), r0)
-    assert np.array_equal(cnt.cpu().numpy().view(np.uint64), ocnt)
     assert int(ocnt[3]) == n  # every 64-byte frame reflected
+    for generic, kernel in ((False, _lib.EBPF_KERNEL_JIT_STACK), (True, _lib.EBPF_KERNEL_GENERAL_T1)):
+        assert prog.batch_kernel(prog.make_batch(frames, n=n, stride=64, generic=generic)) == kernel
+        cnt = torch.zeros(8, dtype=torch.int64, device=cuda)
+        res = prog.run(frames, n=n, stride=64, r0=True, status=True, counters=cnt, generic=generic)
+        torch.cuda.synchronize()
+        assert np.array_equal(res.status.cpu().numpy(), st), generic
+        assert np.array_equal(res.r0.cpu().numpy().view(np.uint64), r0), generic
+        assert np.array_equal(cnt.cpu().numpy().view(np.uint64), ocnt), generic
     pk = [bytes(buf[i * 64:(i + 1) * 64]) for i in range(64)]
     got = _run_full(img, pk, cuda, stride=64)
     _check_against_oracle(oracle_mod, img, pk, got, tag="mac swap")

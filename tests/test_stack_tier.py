@@ -1,6 +1,8 @@
-"""Memory tier 0.5 (stack-window programs, host.cpp analyze_stack, jit.cpp stack_*): programs
-whose only memory writes are ST/STX at r10 + c keep the window [r10 - k, r10) in VGPRs of the
-compiled fixed-slot kernel instead of running on the general interpreter with per-packet images.
+"""Memory tier 0.5 (stack-window programs, host.cpp analyze_stack, jit.cpp stack_* / pw_store):
+programs whose memory writes are ST/STX/ATOMIC at r10 + c, or ST/STX into the packet's header
+window at constant addresses, keep the stack window [r10 - k, r10) in VGPRs of the compiled
+fixed-slot kernel (and the stored window bytes in its preloaded window registers) instead of
+running on the general interpreter with per-packet images.
 
 CPU: the load-time analysis on directed programs (which are stack-window programs and how large
 their window is), and every eligible fuzzed program compiles and assembles.
@@ -26,12 +28,21 @@ DIRECTED = [
     ("stxdw [r10-64], r1\nexit", 64),
     ("stxdw [r10-72], r1\nexit", 0),                               # past kStackMax
     ("stxw [r10-2], r1\nexit", 0),                                 # crosses r10
-    ("stxw [r1+0], r2\nexit", 0),                                  # a packet store
+    ("stxw [r1+0], r2\nexit", 4),                                  # a packet-window store
+    ("stxw [r1+60], r2\nldxw r0, [r1+60]\nexit", 4),              # stored, then read back
+    ("stxw [r1+62], r2\nexit", 0),                                 # crosses the window's end
+    ("stxw [r1+8], r2\nmov r3, r2\nldxb r0, [r3+0]\nexit", 0),    # + a register-address load
+    ("stxw [r1+8], r2\nldxw r0, [r1+62]\nexit", 0),               # + a load across byte 64
+    ("stxw [r1+8], r2\nldxw r0, [r10-8]\nexit", 0),               # + a load outside the window
+    ("mov r3, r2\nstxw [r3+0], r2\nexit", 0),                     # through an unknown pointer
     ("jeq r2, 60, +2\nmov r3, r10\nja +1\nmov r3, r1\nstxb [r3-4], r0\nexit", 0),  # join differs
     ("jeq r2, 60, +2\nmov r3, r10\nja +1\nmov r3, r10\nstxb [r3-4], r0\nexit", 4),  # join agrees
     ("stxdw [r10-8], r1\nldxw r0, [r10-10]\nexit", 0),             # a load straddling the edge
     ("stxdw [r10-8], r1\nldxw r0, [r10-16]\nexit", 8),             # a load below the window
-    ("stxdw [r10-8], r1\nlock add [r10-16], r2\nexit", 0),         # atomics: general image
+    ("stxdw [r10-8], r1\nlock add [r10-16], r2\nexit", 16),        # a stack atomic (8 bytes)
+    ("lock fetch add32 [r10-8], r2\nexit", 8),
+    ("lock add [r10-6], r2\nexit", 0),                             # misaligned atomic
+    ("lock add [r1+8], r2\nexit", 0),                              # an atomic on the packet
     ("stxdw [r10-8], r1\ncall 0\nexit", 0),                        # calls
     ("mov r0, 0\nstxb [r10-1], r0\nadd r0, 1\njlt r0, 5, -3\nexit", 0),  # a loop
     ("mov32 r2, r10\nstxb [r2-1], r0\nexit", 0),                   # a truncated pointer
@@ -58,8 +69,8 @@ def test_stack_programs_compile():
 
     rng = random.Random(2024)
     n_ok = 0
-    for _ in range(250):
-        img = gen_stack_program(rng)
+    for it in range(350):
+        img = gen_stack_program(rng, pw_atomics=it >= 250)
         try:
             p = Program(img)
         except Exception:
@@ -229,3 +240,95 @@ def test_stack_workload_vs_oracle(cuda, oracle_mod):
     assert np.array_equal(cnt.cpu().numpy().view(np.uint64), ocnt)
     r0b, _, _ = oracle_mod.Program(W.program("5tuple")).run_batch(buf, n, stride=64, threads=8)
     assert np.array_equal(r0, r0b)
+
+
+# Atomics on the stack window and packet-window stores, directed at the reference's corner cases
+# (emu.rs:373-437, oracle/ebpf_oracle.c): 64-bit ADD overflow (ST_ARITH, the debug build), the
+# 32-bit form's carry into the high word and the recombination's overflow, fetch, XCHG, CMPXCHG
+# (equal and not, 32-bit, without fetch: r0 = 0), src == dst and dst == r0 (the dst write-back,
+# Q14), and packet stores of every width read back through constant loads.
+ATOMIC_PROGRAMS = [
+    "lddw r5, 0x7fffffffffffffc0\nstxdw [r10-8], r5\nmov r6, r2\nlock add [r10-8], r6\n"
+    "ldxdw r0, [r10-8]\nexit",
+    "lddw r5, 0x7fffffffffffffff\nstxdw [r10-8], r5\nmov r6, 1\nlock add32 [r10-8], r6\n"
+    "ldxdw r0, [r10-8]\nexit",
+    "lddw r5, 0x7ffffffeffffffff\nstxdw [r10-16], r5\nmov r6, 1\nlock fetch add32 [r10-16], r6\n"
+    "ldxdw r0, [r10-16]\nadd r0, r6\nexit",
+    "ldxdw r3, [r1+8]\nstxdw [r10-8], r3\nldxdw r4, [r1+16]\nlock fetch or [r10-8], r4\n"
+    "lock and [r10-8], r3\nlock fetch xor32 [r10-8], r2\nldxdw r0, [r10-8]\nxor r0, r4\nexit",
+    "ldxdw r3, [r1+24]\nstxdw [r10-24], r3\nmov r4, r2\nlock xchg [r10-24], r4\n"
+    "ldxdw r0, [r10-24]\nadd r0, r4\nexit",
+    "ldxdw r0, [r1+0]\nstxdw [r10-8], r0\nmov r4, r2\nlock cmpxchg [r10-8], r4\n"
+    "ldxdw r5, [r10-8]\nadd r0, r5\nexit",
+    "mov r0, 7\nldxdw r3, [r1+0]\nstxdw [r10-8], r3\nmov r4, r2\nlock cmpxchg [r10-8], r4\n"
+    "ldxdw r5, [r10-8]\nadd r0, r5\nexit",
+    "ldxw r0, [r1+4]\nstxdw [r10-8], r0\nmov r4, r2\nlock cmpxchg32 [r10-8], r4\n"
+    "ldxdw r5, [r10-8]\nadd r0, r5\nexit",
+    "ldxdw r3, [r1+0]\nstxdw [r10-8], r3\nlock cmpxchg [r10-8], r2\nexit",
+    "mov r3, r10\nstxdw [r3-8], r2\nlock fetch add [r3-8], r3\nldxdw r0, [r10-8]\nadd r0, r3\nexit",
+    "mov r0, r10\nstdw [r10-8], 5\nmov r4, 9\nlock cmpxchg [r0-8], r4\nldxdw r5, [r10-8]\n"
+    "mov r0, r5\nexit",
+    "ldxw r3, [r1+0]\nldxh r4, [r1+4]\nldxw r5, [r1+6]\nldxh r6, [r1+10]\nstxw [r1+0], r5\n"
+    "stxh [r1+4], r6\nstxw [r1+6], r3\nstxh [r1+10], r4\nldxdw r0, [r1+0]\nldxw r7, [r1+8]\n"
+    "add r0, r7\nexit",
+    "stb [r1+63], 0x5a\nsth [r1+13], 0x1234\nstdw [r1+40], 7\nstxdw [r1+21], r2\n"
+    "ldxdw r0, [r1+56]\nldxdw r3, [r1+40]\nadd r0, r3\nldxdw r3, [r1+12]\nadd r0, r3\n"
+    "ldxdw r3, [r1+20]\nadd r0, r3\nexit",
+]
+
+
+@pytest.mark.gpu
+def test_stack_atomics_and_packet_stores(cuda, oracle_mod):
+    """ATOMIC_PROGRAMS on fixed-slot frames: the compiled stack-window kernel == the general
+    interpreter == the oracle, every output (faults included), on 64- and 128-byte slots; and the
+    MAC-swap workload (workloads.MAC_SWAP_TX) the same way."""
+    from ebpf_emu import Program, _lib
+    from ebpf_emu import workloads as W
+    from ebpf_emu.asm import assemble
+
+    rng = random.Random(17)
+    for src in ATOMIC_PROGRAMS + [W.MAC_SWAP_TX]:
+        img = assemble(src)
+        p = Program(img)
+        assert p.stack_window, src
+        p.close()
+        for stride in (64, 128):
+            pkts = [bytes(rng.getrandbits(8) for _ in range(stride)) for _ in range(100)]
+            frames = _fixed_frames(pkts, stride, cuda)
+            got = _run(img, frames, len(pkts), cuda, kernel=_lib.EBPF_KERNEL_JIT_STACK, stride=stride)
+            ref = _run(img, frames, len(pkts), cuda, generic=True, stride=stride)
+            for key in ("status", "r0", "verdict", "regs", "counters"):
+                assert np.array_equal(got[key], ref[key]), (key, stride, src)
+            _vs_oracle(oracle_mod, img, pkts, got, tag=f"{stride} {src!r}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(3))
+def test_stack_atomics_fuzz(cuda, oracle_mod, seed):
+    """Random stack programs with stack atomics and packet-window stores (gen_stack_program
+    pw_atomics): compiled == general interpreter == oracle."""
+    from ebpf_emu import Program, _lib
+
+    rng = random.Random(990 + seed)
+    n_stack = 0
+    for it in range(40):
+        img = gen_stack_program(rng, pw_atomics=True)
+        try:
+            oracle_mod.Program(img)
+        except oracle_mod.OracleDecodeError:
+            continue
+        p = Program(img)
+        k = p.stack_window
+        p.close()
+        if not k:
+            continue
+        stride = rng.choice([64, 128])
+        pkts = [bytes(rng.getrandbits(8) for _ in range(stride)) for _ in range(rng.choice([64, 100]))]
+        frames = _fixed_frames(pkts, stride, cuda)
+        got = _run(img, frames, len(pkts), cuda, stride=stride)
+        n_stack += got["kernel"] == _lib.EBPF_KERNEL_JIT_STACK
+        ref = _run(img, frames, len(pkts), cuda, generic=True, stride=stride)
+        for key in ("status", "r0", "verdict", "regs", "counters"):
+            assert np.array_equal(got[key], ref[key]), (key, seed, it, img.hex())
+        _vs_oracle(oracle_mod, img, pkts, got, tag=f"seed {seed} it {it}")
+    assert n_stack >= 12, n_stack
