@@ -158,12 +158,15 @@ int ebpf_prog_tier(const ebpf_prog* prog);
  * EBPF_BATCH_GENERIC -- else 0; -1 for NULL. */
 int ebpf_prog_forward_only(const ebpf_prog* prog);
 
-/* Memory tier 0.5: the bytes of the stack window [r10 - k, r10) of a program whose only memory
- * writes are ST/STX at r10 + c (c known at load time, all in the window; forward jumps only, no
- * ATOMIC/CALL, <= 62 micro-ops). Such a program keeps the window in registers of the compiled
+/* Memory tier 0.5: the bytes of the stack window [r10 - k, r10) of a program whose memory writes
+ * are ST/STX/ATOMIC at r10 + c (c known at load time, all in the window; atomics 4-aligned), or
+ * ST/STX into the packet's first 64 bytes at load-time constant addresses (then every other load
+ * must be a constant-address or stack-window one); forward jumps only, no CALL, <= 62 micro-ops.
+ * Such a program keeps the window (and the stored packet bytes) in registers of the compiled
  * fixed-slot kernel, for batches in the fixed-slot layout with the main.rs register layout whose
  * window lies past every packet byte and inside the image (r10 % 4 == 0); other batches run it
- * on the general interpreter. 0 = not such a program; -1 for NULL. */
+ * on the general interpreter. A program with packet stores only reports a 4-byte window.
+ * 0 = not such a program; -1 for NULL. */
 int ebpf_prog_stack_window(const ebpf_prog* prog);
 
 /* Compile the program to gfx950 machine code now, if it is one the tile kernels run (memory tier
