@@ -290,6 +290,7 @@ struct Compiler {
   using AbsRegs = std::array<AbsVal, 11>;
   static constexpr uint64_t kLenMax = 1ull << 24;  // mem_size bound (include/ebpf_emu.h)
   std::vector<char> inb;   // inb[i]: the one-byte LDX i is proven in bounds
+  std::vector<AbsRegs> ranges;  // the registers' abstract values at each reached micro-op
   bool proven = false;     // emitting the proven copy (ldx1_loop drops inb[i] loads' checks)
 
   static AbsVal av_const(uint64_t c) {
@@ -498,6 +499,9 @@ struct Compiler {
       flow(i + 1, nt);
     }
     if (!work.empty()) return;  // (no fixpoint within the bound: prove nothing)
+    ranges.assign(n, AbsRegs());
+    for (uint32_t i = 0; i < n; i++)
+      if (seen[i]) ranges[i] = in[i];
     if (getenv("EBPFEMU_RANGES"))  // diagnostics: the state at every micro-op
       for (uint32_t i = 0; i < n; i++) {
         fprintf(stderr, "%2u op %2u d%u s%u:", i, uops[i].op, uops[i].dst, uops[i].src);
@@ -1452,6 +1456,7 @@ struct Compiler {
                   ", v28\ns_or_b64 exec, s[64:65], vcc\n";
         main += "s_cbranch_execz .L" + P + "b" + std::to_string(next_start(i)) + "\n";
         if (loops && hoist[i] != -2) main += "v_mov_b32 v28, " + std::to_string(hoist[i]) + "\n";
+        if (loops && proven && !counted_entry(m, i, P, main, ool)) return false;
         if (loops) main += ".L" + P + "body" + std::to_string(i) + ":\n";
         if (loops)  // biased counter: the add's carry-out is the budget test (budget_check)
           main += "v_add_co_u32_e32 v29, vcc, " + std::to_string(t[i].blen) + ", v29\n" +
@@ -1459,59 +1464,122 @@ struct Compiler {
         else
           main += "v_add_u32 v29, " + std::to_string(t[i].blen) + ", v29\n";
       }
-      const uint32_t id = t[i].hoff / TILE_SLOT;
-      if (id >= (uint32_t)T_COUNT || id == (uint32_t)T_DONE) {
-        err = "bad handler id";
-        return false;
-      }
-      if (stk && (uops[i].op == U_ST || uops[i].op == U_STX)) {
-        // (a store the load-time dataflow never reached has no offset: no lane executes it)
-        main += stk->pw[i] != kNoStack    ? pw_store(i)
-                : stk->off[i] == kNoStack ? std::string("; unreachable store\n")
-                                          : stack_store(i);
-        continue;
-      }
-      if (stk && uops[i].op == U_ATOMIC) {
-        main += stk->off[i] == kNoStack ? std::string("; unreachable atomic\n") : stack_atomic(i, P);
-        continue;
-      }
-      if (stk && uops[i].op == U_LDX && stk->off[i] != kNoStack) {
-        main += stack_load(i);
-        continue;
-      }
-      if (fast && is_ldxk(id)) {
-        main += ldxk_fast(i);
-        continue;
-      }
-      if (!loops && m.fixed == "1" &&
-          (id == T_LDX_C || id == T_LDX_E || id == T_LDX1_C || id == T_LDX1_E)) {
-        std::string ot;
-        main += ldx_fixed(i, id == T_LDX1_C || id == T_LDX1_E, P, ot);
-        ool += ot;
-        continue;
-      }
-      if (loops && (id == T_LDX1_C || id == T_LDX1_E)) {
-        std::string ot;
-        main += ldx1_loop(i, m, P, ot);
-        ool += ot;
-        continue;
-      }
-      std::set<uint32_t> sg;
-      std::string mt, ot;
-      if (!expand(kJitTemplates[id][0], i, m, P, sg, mt)) return false;
-      if (!expand(kJitTemplates[id][1], i, m, P, sg, ot)) return false;
-      const uint32_t* w = (const uint32_t*)&t[i];
-      for (uint32_t d : sg)
-        main += "s_mov_b32 s" + std::to_string(kFieldSgpr + d) + ", " + hex32(w[d]) + "\n";
-      mt = resolve_ifs(mt);
-      ot = resolve_ifs(ot);
-      if (ot.empty()) mt = fold_copy(fold_copy(mt, 24), 54);  // (out-of-line code may read them)
-      if ((cache || qcache) && (touches(mt, 50, 55) || touches(ot, 50, 55))) cache_conflict = true;
-      main += mt;
-      ool += ot;
+      if (!emit_uop(m, i, P, fast, main, ool)) return false;
     }
     main += ".L" + P + "b" + std::to_string(n) + ":\n";
     if (loops) main += "v_mov_b32 v28, -1\n";  // lanes past the end are done
+    return true;
+  }
+
+  // ---- counted single-block loops (the proven copy) ----
+  // A loop whose block L..J runs `add rI, 1` once, leaves only through its back edge
+  // `jlt rI, rN` (or `jgt rN, rI`; both signed, Q2) with rN unchanged in the block, and holds no
+  // micro-op that can fault, runs max(1, rN - rI) times from its entry when rI and rN are in
+  // [0, 2^24] there (the range analysis): the steps its lanes will retire are known at the entry.
+  // If no lane's total passes the budget, they are added once and the block runs as a copy
+  // without the per-iteration step count and budget check (out of line, prefix PU); otherwise
+  // the ordinary block runs. Returns false only on a compiler error.
+  bool counted_entry(const Marker& m, uint32_t L, const std::string& P, std::string& main,
+                     std::string& ool) {
+    if (!loops || exact || hoist[L] == -2 || ranges.empty()) return true;
+    uint32_t J = L;
+    while (J + 1 < n && !start[J + 1]) J++;
+    const Uop& jb = uops[J];
+    uint32_t rI, rN;
+    if (jb.op == U_JLT && (jb.aux & F_SRC) && (uint32_t)jb.x == L) {
+      rI = jb.dst, rN = jb.src;
+    } else if (jb.op == U_JGT && (jb.aux & F_SRC) && (uint32_t)jb.x == L) {
+      rI = jb.src, rN = jb.dst;
+    } else {
+      return true;
+    }
+    if (rI == rN || rI > 10 || rN > 10) return true;
+    uint32_t incs = 0;
+    for (uint32_t i = L; i < J; i++) {
+      const Uop& u = uops[i];
+      const bool alu = u.op <= U_ARSH32 && u.op != U_DIV64 && u.op != U_MOD64 && u.op != U_DIV32 &&
+                       u.op != U_MOD32 && u.op != U_ARSH64 && u.op != U_ARSH32;
+      const bool ok = alu || (u.op >= U_ZX16 && u.op <= U_BSWAP64) || u.op == U_LDIMM ||
+                      (u.op == U_LDX && u.aux == 1 && inb[i]);
+      if (!ok || u.dst == rN) return true;  // (not a counted loop)
+      if (u.dst == rI) {
+        if (u.op != U_ADD64 || (u.aux & F_SRC) || u.k != 1) return true;
+        incs++;
+      }
+    }
+    if (incs != 1) return true;
+    const AbsVal &vi = ranges[L][rI], &vn = ranges[L][rN];
+    if (vi.hi > kLenMax || vn.hi > kLenMax) return true;
+    const std::string PU = P + "n" + std::to_string(L) + "_", Ls = std::to_string(L);
+    main += "; counted loop: max(1, r" + std::to_string(rN) + " - r" + std::to_string(rI) +
+            ") runs of " + std::to_string(t[L].blen) + " steps\n"
+            "v_sub_u32 v46, v" + std::to_string(2 * rN) + ", v" + std::to_string(2 * rI) + "\n"
+            "v_max_i32 v46, 1, v46\n"
+            "v_mul_u32_u24 v46, " + std::to_string(t[L].blen) + ", v46\n"
+            "v_add_co_u32_e32 v46, vcc, v46, v29\n"
+            "s_cbranch_vccnz .L" + P + "body" + Ls + "\n"
+            "v_mov_b32 v29, v46\n"
+            "s_branch .L" + PU + "body" + Ls + "\n";
+    std::string c = ".L" + PU + "body" + Ls + ":\n";
+    for (uint32_t i = L; i <= J; i++)
+      if (!emit_uop(m, i, PU, false, c, ool)) return false;
+    ool += c + "s_branch .L" + P + "b" + std::to_string(J + 1) + "\n";
+    return true;
+  }
+
+  // The code of micro-op i (no block entry) in copy P.
+  bool emit_uop(const Marker& m, uint32_t i, const std::string& P, bool fast, std::string& main,
+                std::string& ool) {
+    const uint32_t id = t[i].hoff / TILE_SLOT;
+    if (id >= (uint32_t)T_COUNT || id == (uint32_t)T_DONE) {
+      err = "bad handler id";
+      return false;
+    }
+    if (stk && (uops[i].op == U_ST || uops[i].op == U_STX)) {
+      // (a store the load-time dataflow never reached has no offset: no lane executes it)
+      main += stk->pw[i] != kNoStack    ? pw_store(i)
+              : stk->off[i] == kNoStack ? std::string("; unreachable store\n")
+                                        : stack_store(i);
+      return true;
+    }
+    if (stk && uops[i].op == U_ATOMIC) {
+      main += stk->off[i] == kNoStack ? std::string("; unreachable atomic\n") : stack_atomic(i, P);
+      return true;
+    }
+    if (stk && uops[i].op == U_LDX && stk->off[i] != kNoStack) {
+      main += stack_load(i);
+      return true;
+    }
+    if (fast && is_ldxk(id)) {
+      main += ldxk_fast(i);
+      return true;
+    }
+    if (!loops && m.fixed == "1" &&
+        (id == T_LDX_C || id == T_LDX_E || id == T_LDX1_C || id == T_LDX1_E)) {
+      std::string ot;
+      main += ldx_fixed(i, id == T_LDX1_C || id == T_LDX1_E, P, ot);
+      ool += ot;
+      return true;
+    }
+    if (loops && (id == T_LDX1_C || id == T_LDX1_E)) {
+      std::string ot;
+      main += ldx1_loop(i, m, P, ot);
+      ool += ot;
+      return true;
+    }
+    std::set<uint32_t> sg;
+    std::string mt, ot;
+    if (!expand(kJitTemplates[id][0], i, m, P, sg, mt)) return false;
+    if (!expand(kJitTemplates[id][1], i, m, P, sg, ot)) return false;
+    const uint32_t* w = (const uint32_t*)&t[i];
+    for (uint32_t d : sg)
+      main += "s_mov_b32 s" + std::to_string(kFieldSgpr + d) + ", " + hex32(w[d]) + "\n";
+    mt = resolve_ifs(mt);
+    ot = resolve_ifs(ot);
+    if (ot.empty()) mt = fold_copy(fold_copy(mt, 24), 54);  // (out-of-line code may read them)
+    if ((cache || qcache) && (touches(mt, 50, 55) || touches(ot, 50, 55))) cache_conflict = true;
+    main += mt;
+    ool += ot;
     return true;
   }
 

@@ -124,7 +124,7 @@ def test_fuzz_loop_programs_production_outputs(cuda, oracle_mod, seed):
     assert n_run >= 25
 
 
-@pytest.mark.parametrize("budget", [1, 2, 3, 5, 6, 7, 8, 13, 50, 101, 997])
+@pytest.mark.parametrize("budget", [1, 2, 3, 5, 6, 7, 8, 13, 50, 101, 389, 997])
 def test_loop_step_budget_exact(cuda, oracle_mod, budget):
     """Budgets that bind at every position of the loop body, for lanes of different lengths in
     one tile: ST_STEPS exactly where the oracle stops (and faults before the budget win)."""
@@ -147,6 +147,11 @@ def test_loop_step_budget_exact(cuda, oracle_mod, budget):
         gen = _run_full(img, pkts, cuda, max_steps=budget, offsets_layout=True, align=16,
                         generic=True)
         _same_outputs(got, gen, f"budget {budget}")
+        # the production outputs: the proven copy, whose counted loops (jit.cpp counted_entry)
+        # check the budget once per loop entry from the trip count
+        prod = _run_prod(img, pkts, cuda, max_steps=budget, offsets_layout=True, align=16)
+        _check_prod_against_oracle(oracle_mod, img, pkts, prod, max_steps=budget,
+                                   tag=f"prod budget {budget} {src[:40]}")
 
 
 @pytest.mark.parametrize("layout", [dict(offsets_layout=True, align=64),
