@@ -1756,8 +1756,14 @@ static int jit_grid(hipFunction_t f, uint32_t lds, uint64_t n_tiles, int block =
   }
   const uint64_t tiles = n_tiles ? n_tiles : 1;
   const uint64_t wgs = (uint64_t)occ.first * occ.second;
-  if (wpb == (uint64_t)kDbWaves)  // tiles handed out within the workgroup: >= 1 tile each
-    return (int)(tiles < wgs ? tiles : wgs);
+  if (wpb == (uint64_t)kDbWaves) {  // tiles handed out within the workgroup: >= 1 tile each
+    // (tests: EBPFEMU_FIXED_WGS caps the workgroups, so a moderate batch gives each wave more
+    // than the 511 tiles one entry of the tile-loop statement runs)
+    const char* cap = getenv("EBPFEMU_FIXED_WGS");
+    const uint64_t lim = cap && atoi(cap) > 0 ? (uint64_t)atoi(cap) : wgs;
+    const uint64_t g = wgs < lim ? wgs : lim;
+    return (int)(tiles < g ? tiles : g);
+  }
   const uint64_t resident = wgs * wpb;
   const uint64_t per_wave = (tiles + resident - 1) / resident;
   const uint64_t waves = (tiles + per_wave - 1) / per_wave;

@@ -291,6 +291,8 @@ struct Compiler {
   static constexpr uint64_t kLenMax = 1ull << 24;  // mem_size bound (include/ebpf_emu.h)
   std::vector<char> inb;   // inb[i]: the one-byte LDX i is proven in bounds
   std::vector<AbsRegs> ranges;  // the registers' abstract values at each reached micro-op
+  // counted loops: a one-byte load's base read from this register instead (-1: its own)
+  std::vector<int> addr_src = std::vector<int>(64, -1);
   bool proven = false;     // emitting the proven copy (ldx1_loop drops inb[i] loads' checks)
 
   static AbsVal av_const(uint64_t c) {
@@ -531,7 +533,10 @@ struct Compiler {
 
   // Registers the program may read before writing them (backward liveness over the forward
   // jumps; conservative: LDX reads its base and, merging, its destination, Q1).
-  uint32_t live_in() const {
+  uint32_t live_in() const { return live()[0]; }
+
+  // Registers live at each micro-op's entry (bit r), for live_in and the counted loops.
+  std::vector<uint32_t> live() const {
     std::vector<uint32_t> in(n + 1, 0);
     auto rw = [&](const Uop& u, uint32_t& rd, uint32_t& wr) {
       const uint32_t d = 1u << u.dst, s = (u.aux & F_SRC) ? 1u << u.src : 0u;
@@ -573,7 +578,7 @@ struct Compiler {
         }
       }
     }
-    return in[0];
+    return in;
   }
 
   // ;@@JITINIT@@: r0 and the live-in registers in the main.rs layout
@@ -1044,13 +1049,15 @@ struct Compiler {
     }
     const std::string D0 = "v" + std::to_string(u.dst2);
     // the address a = src + off in v[36:37]; with off = 0 the source pair itself (the refill
-    // reads only its low word and uses v37 as a temporary)
+    // reads only its low word and uses v37 as a temporary). A counted loop may name another
+    // register holding the same value (addr_src, counted_entry).
+    const uint32_t src2 = addr_src[i] >= 0 ? 2 * (uint32_t)addr_src[i] : u.src2;
     std::string A = "v36", AP = "v[36:37]";
     if (off == 0) {
-      A = vreg(u.src2, 0);
-      AP = vpair(u.src2, 0, 1);
+      A = vreg(src2, 0);
+      AP = vpair(src2, 0, 1);
     } else {
-      s += "v_lshl_add_u64 v[36:37], " + vpair(u.src2, 0, 1) + ", 0, " + offs + "\n";
+      s += "v_lshl_add_u64 v[36:37], " + vpair(src2, 0, 1) + ", 0, " + offs + "\n";
     }
     if (!(proven && inb[i]))  // (a load proven to read a packet byte cannot fault)
       s += "v_cmp_gt_u64 vcc, s[52:53], " + AP + "\n"
@@ -1510,6 +1517,36 @@ struct Compiler {
     if (incs != 1) return true;
     const AbsVal &vi = ranges[L][rI], &vn = ranges[L][rN];
     if (vi.hi > kLenMax || vn.hi > kLenMax) return true;
+    // an address copy `mov rA, rZ; add rA, rC` with rZ = 0 whose value only the block's one-byte
+    // loads read (rA dead at both successors, rC unchanged until those loads): the loads take
+    // rC as their base and the copy is not emitted
+    std::vector<char> skip(n, 0);
+    const std::vector<uint32_t> lv = live();
+    for (uint32_t i = L; i + 1 < J; i++) {
+      const Uop &a = uops[i], &b = uops[i + 1];
+      if (a.op != U_MOV64 || !(a.aux & F_SRC) || ranges[i][a.src].hi != 0 || b.op != U_ADD64 ||
+          !(b.aux & F_SRC) || b.dst != a.dst || b.src == a.dst)
+        continue;
+      const uint32_t rA = a.dst, rC = b.src;
+      if ((lv[L] >> rA) & 1 || (J + 1 < n && (lv[J + 1] >> rA) & 1)) continue;
+      bool ok = true;
+      std::vector<uint32_t> loads;
+      for (uint32_t k = i + 2; k <= J && ok; k++) {
+        const Uop& u = uops[k];
+        const bool reads_a = (u.dst == rA && u.op != U_MOV64 && u.op != U_MOV32 && u.op != U_LDIMM) ||
+                             ((u.aux & F_SRC) && u.src == rA && u.op != U_LDX) || u.dst == rA;
+        if (u.op == U_LDX && u.src == rA && u.dst != rA) loads.push_back(k);
+        else if (reads_a) ok = false;
+        if (u.dst == rC && u.op != U_LDX) {  // rC written: later loads would see another value
+          for (uint32_t q = k + 1; q <= J && ok; q++) ok = !(uops[q].op == U_LDX && uops[q].src == rA);
+          break;
+        }
+      }
+      if (!ok || loads.empty()) continue;
+      skip[i] = skip[i + 1] = 1;
+      for (uint32_t k : loads) addr_src[k] = (int)rC;
+      i++;
+    }
     const std::string PU = P + "n" + std::to_string(L) + "_", Ls = std::to_string(L);
     main += "; counted loop: max(1, r" + std::to_string(rN) + " - r" + std::to_string(rI) +
             ") runs of " + std::to_string(t[L].blen) + " steps\n"
@@ -1521,8 +1558,11 @@ struct Compiler {
             "v_mov_b32 v29, v46\n"
             "s_branch .L" + PU + "body" + Ls + "\n";
     std::string c = ".L" + PU + "body" + Ls + ":\n";
-    for (uint32_t i = L; i <= J; i++)
-      if (!emit_uop(m, i, PU, false, c, ool)) return false;
+    bool ok = true;
+    for (uint32_t i = L; i <= J && ok; i++)
+      if (!skip[i]) ok = emit_uop(m, i, PU, false, c, ool);
+    for (uint32_t i = L; i <= J; i++) addr_src[i] = -1;
+    if (!ok) return false;
     ool += c + "s_branch .L" + P + "b" + std::to_string(J + 1) + "\n";
     return true;
   }

@@ -323,3 +323,33 @@ def test_compiled_large_batches(cuda, config):
             assert cnt.cpu().tolist() == ref_cnt.cpu().tolist(), (config, n, rep)
             assert int(cnt[:7].sum()) == n
     prog.close()
+
+
+@pytest.mark.gpu
+def test_tile_loop_reentry(cuda, monkeypatch):
+    """The compiled fixed-slot kernel's statement runs at most 511 tiles per entry before the
+    C++ unpacks the packed counter buckets (interp.hip ebpf_tile_jit_fixed): with the grid capped
+    to one workgroup (EBPFEMU_FIXED_WGS=1, read per launch: 16 waves), 600 Ki packets give each
+    wave ~600 tiles. Verdicts and counters equal the tile interpreter's."""
+    import torch
+
+    from ebpf_emu import Program
+    from ebpf_emu import workloads as W
+    from ebpf_emu.asm import assemble
+
+    n = 600 * 1024 + 13
+    frames = torch.from_numpy(W.frames_fixed(n, 64, 9)).to(cuda)
+    for name in ("5tuple", "drop"):
+        prog = Program(assemble(W.PROGRAMS[name]))
+        assert prog.compile()
+        rc = torch.zeros(8, dtype=torch.int64, device=cuda)
+        ref = prog.run(frames, n=n, stride=64, counters=rc, no_jit=True)
+        monkeypatch.setenv("EBPFEMU_FIXED_WGS", "1")
+        gc = torch.zeros(8, dtype=torch.int64, device=cuda)
+        got = prog.run(frames, n=n, stride=64, counters=gc)
+        torch.cuda.synchronize()
+        monkeypatch.delenv("EBPFEMU_FIXED_WGS")
+        assert np.array_equal(got.verdict.cpu().numpy(), ref.verdict.cpu().numpy()), name
+        assert gc.cpu().tolist() == rc.cpu().tolist(), name
+        assert int(gc[:7].sum()) == n
+        prog.close()
