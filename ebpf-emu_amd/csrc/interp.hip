@@ -1175,7 +1175,8 @@ __global__ __launch_bounds__(kBlock) void dag_kernel(LaunchArgs a) {
 // longest packet is done, so a tile mixing 64- and 1500-byte frames idles half its lanes in a
 // per-byte loop. A counting sort by class ceil(len / 128) (capped) groups similar lengths:
 // bin_hist counts the classes (per-workgroup LDS histogram, one device atomic per class per
-// workgroup), bin_scatter reserves each workgroup's range per class and writes the indices.
+// workgroup), bin_scatter reserves each workgroup's range per class and writes the indices,
+// longest class first.
 // The order within a class is arbitrary; every output stays indexed by the original packet.
 // ============================================================================================
 constexpr int kBinBlock = 1024;
@@ -1185,6 +1186,28 @@ __device__ __forceinline__ uint32_t bin_class(uint32_t len) {
   return c < (uint32_t)kBinClasses ? c : (uint32_t)kBinClasses - 1;
 }
 
+// The lanes of a wave that hold class c add their count with one LDS atomic (its lowest lane);
+// returns this lane's slot: the class's count before the wave's add plus the lane's rank among
+// the wave's lanes of its class. A mixed 64/1500-byte batch has two classes per wave, so two
+// atomics instead of 64 serialized on two LDS words.
+__device__ __forceinline__ uint32_t wave_class_slot(uint32_t c, uint32_t* h) {
+  const uint32_t lane = __lane_id();
+  const uint64_t below = (1ull << lane) - 1;
+  uint64_t todo = __ballot(1);
+  uint32_t slot = 0;
+  while (todo) {
+    const int lead = __ffsll((unsigned long long)todo) - 1;
+    const uint32_t cc = __shfl(c, lead);
+    const uint64_t m = __ballot(c == cc) & todo;
+    uint32_t b = 0;
+    if ((int)lane == lead) b = atomicAdd(&h[cc], (uint32_t)__popcll(m));
+    b = __shfl(b, lead);
+    if (c == cc) slot = b + (uint32_t)__popcll(m & below);
+    todo &= ~m;
+  }
+  return slot;
+}
+
 __global__ __launch_bounds__(kBinBlock) void bin_hist(const uint16_t* lens, uint64_t n,
                                                       uint32_t* bins) {
   __shared__ uint32_t h[kBinClasses];
@@ -1192,7 +1215,7 @@ __global__ __launch_bounds__(kBinBlock) void bin_hist(const uint16_t* lens, uint
   __syncthreads();
   for (uint64_t i = (uint64_t)blockIdx.x * kBinBlock + threadIdx.x; i < n;
        i += (uint64_t)gridDim.x * kBinBlock)
-    atomicAdd(&h[bin_class(lens[i])], 1u);
+    (void)wave_class_slot(bin_class(lens[i]), h);
   __syncthreads();
   if (threadIdx.x < kBinClasses && h[threadIdx.x]) atomicAdd(&bins[threadIdx.x], h[threadIdx.x]);
 }
@@ -1204,18 +1227,20 @@ __global__ __launch_bounds__(kBinBlock) void bin_scatter(const uint16_t* lens, u
   if (t < kBinClasses) h[t] = 0;
   __syncthreads();
   for (uint64_t i = (uint64_t)blockIdx.x * kBinBlock + t; i < n; i += (uint64_t)gridDim.x * kBinBlock)
-    atomicAdd(&h[bin_class(lens[i])], 1u);
+    (void)wave_class_slot(bin_class(lens[i]), h);
   __syncthreads();
   if (t < kBinClasses) {
-    uint32_t start = 0;  // exclusive prefix of the global class counts
-    for (int c = 0; c < (int)t; c++) start += bins[c];
+    // classes in descending order (longest packets first): the hardware dispatches tiles in
+    // order, so the long tiles start first and the short ones fill the launch's tail
+    uint32_t start = 0;
+    for (int c = (int)t + 1; c < kBinClasses; c++) start += bins[c];
     base[t] = start + (h[t] ? atomicAdd(&bins[kBinClasses + t], h[t]) : 0u);
     h[t] = 0;
   }
   __syncthreads();
   for (uint64_t i = (uint64_t)blockIdx.x * kBinBlock + t; i < n; i += (uint64_t)gridDim.x * kBinBlock) {
     const uint32_t c = bin_class(lens[i]);
-    perm[base[c] + atomicAdd(&h[c], 1u)] = (uint32_t)i;
+    perm[base[c] + wave_class_slot(c, h)] = (uint32_t)i;
   }
 }
 

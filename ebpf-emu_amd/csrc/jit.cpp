@@ -1548,23 +1548,166 @@ struct Compiler {
       i++;
     }
     const std::string PU = P + "n" + std::to_string(L) + "_", Ls = std::to_string(L);
+    std::string grp;
+    const int g = counted_group(m, L, J, rI, rN, skip, P, PU, grp);
+    if (g < 0) return false;
     main += "; counted loop: max(1, r" + std::to_string(rN) + " - r" + std::to_string(rI) +
-            ") runs of " + std::to_string(t[L].blen) + " steps\n"
+            ") runs of " + std::to_string(t[L].blen) + " steps" +
+            (g ? ", 8 per pass from one qword while 8 are left" : "") + "\n"
             "v_sub_u32 v46, v" + std::to_string(2 * rN) + ", v" + std::to_string(2 * rI) + "\n"
             "v_max_i32 v46, 1, v46\n"
             "v_mul_u32_u24 v46, " + std::to_string(t[L].blen) + ", v46\n"
             "v_add_co_u32_e32 v46, vcc, v46, v29\n"
             "s_cbranch_vccnz .L" + P + "body" + Ls + "\n"
             "v_mov_b32 v29, v46\n"
-            "s_branch .L" + PU + "body" + Ls + "\n";
+            "s_branch .L" + PU + (g ? "gent" : "body" + Ls) + "\n";
     std::string c = ".L" + PU + "body" + Ls + ":\n";
     bool ok = true;
     for (uint32_t i = L; i <= J && ok; i++)
       if (!skip[i]) ok = emit_uop(m, i, PU, false, c, ool);
     for (uint32_t i = L; i <= J; i++) addr_src[i] = -1;
     if (!ok) return false;
-    ool += c + "s_branch .L" + P + "b" + std::to_string(J + 1) + "\n";
+    ool += c + "s_branch .L" + P + "b" + std::to_string(J + 1) + "\n" + grp;
     return true;
+  }
+
+  // Whether text names an SGPR in [lo, hi] (sN or s[a:b]).
+  static bool names_sgpr(const std::string& text, uint32_t lo, uint32_t hi) {
+    for (size_t p = 0; p + 1 < text.size(); p++) {
+      if (text[p] != 's' || (p && (isalnum((unsigned char)text[p - 1]) || text[p - 1] == '_' ||
+                                   text[p - 1] == '.')))
+        continue;
+      size_t q = p + 1;
+      const bool range = text[q] == '[';
+      if (range) q++;
+      if (q >= text.size() || !isdigit((unsigned char)text[q])) continue;
+      const uint32_t a = (uint32_t)strtoul(text.c_str() + q, nullptr, 10);
+      uint32_t b = a;
+      if (range) {
+        const size_t colon = text.find(':', q);
+        if (colon == std::string::npos) continue;
+        b = (uint32_t)strtoul(text.c_str() + colon + 1, nullptr, 10);
+      } else {
+        while (q < text.size() && isdigit((unsigned char)text[q])) q++;
+        if (q < text.size() && (isalpha((unsigned char)text[q]) || text[q] == '_')) continue;
+      }
+      if (a <= hi && b >= lo) return true;
+    }
+    return false;
+  }
+
+  // ---- counted loops in passes of 8 iterations (the proven copy, zero windows + qword cache) ----
+  // A counted loop (counted_entry) whose only load is the one-byte `ldxb rD, [rI + d]` (d fixed,
+  // rI read as the iteration starts; the base may be an address copy's source, addr_src) reads
+  // bytes a0 .. a0 + 7 in its next 8 iterations. A lane with rN - rI >= 8 left runs those 8
+  // iterations without any exit test -- the back edge is the loop's only way out and is taken 7
+  // times in a row -- so a pass replicates the block 8 times (the jump dropped, rI's increments
+  // summed into one add when nothing else reads rI) and takes the loads from one ds_read_b64 of
+  // the lane's window: byte k is merged into rD's low byte as the one-byte load merges (Q1), one
+  // v_perm (or v_bfi) per byte. A pass needs a0 8-aligned and [a0, a0 + 8) inside the window (zero past len):
+  // lanes outside it are refilled first in an aligned tile; misaligned lanes (or, in an unaligned
+  // tile, lanes past its window) run one ordinary iteration instead and retry. Lanes with fewer
+  // than 8 left run the ordinary counted copy; lanes that finished in passes skip it. The steps
+  // were already added at the entry. s[41:47] (micro-op field SGPRs none of the block's code names;
+  // checked) hold the byte selectors, the loop's lanes and the lanes that ran a pass. Returns 1 with the code (out of
+  // line, entered at .L<PU>gent) in out, 0 when the loop does not qualify, -1 on a compiler error.
+  int counted_group(const Marker& m, uint32_t L, uint32_t J, uint32_t rI, uint32_t rN,
+                    const std::vector<char>& skip, const std::string& P, const std::string& PU,
+                    std::string& out) {
+    if (!zwin || !qcache || cache || getenv("EBPFEMU_NO_GROUP")) return 0;
+    int ld = -1, inc = -1;
+    bool others_read_i = false;
+    for (uint32_t i = L; i < J; i++) {
+      if (skip[i]) continue;
+      const Uop& u = uops[i];
+      if (u.op == U_LDX) {
+        if (ld >= 0) return 0;
+        ld = (int)i;
+      } else if (u.dst == rI) {
+        inc = (int)i;  // (counted_entry: the one write of rI is `add rI, 1`)
+      } else if ((u.aux & F_SRC) && u.src == rI) {
+        others_read_i = true;
+      }
+    }
+    if (ld < 0 || inc < 0) return 0;
+    const uint32_t base = addr_src[ld] >= 0 ? (uint32_t)addr_src[ld] : uops[ld].src;
+    const int64_t d = (int64_t)t[ld].imm + (inc < ld ? 1 : 0);
+    if (base != rI || uops[ld].dst == rI || d < -(1 << 20) || d > (1 << 20)) return 0;
+    const std::string G = ".L" + PU + "g", vI = "v" + std::to_string(2 * rI),
+                      vN = "v" + std::to_string(2 * rN), D0 = "v" + std::to_string(uops[ld].dst * 2);
+    std::string A = vI, uc, uo;  // uc / uo: the micro-ops' code (checked for s[44:47])
+    std::string c = G + "ent:\ns_mov_b64 s[44:45], exec\ns_mov_b64 s[46:47], 0\n"
+                    "s_mov_b32 s41, 0x07060501\ns_mov_b32 s42, 0x07060502\n"
+                    "s_mov_b32 s43, 0x07060503\n" + G + "top:\n"
+                    "s_mov_b64 exec, s[44:45]\n"
+                    "v_sub_u32 v46, " + vN + ", " + vI + "\n"
+                    "v_cmp_le_i32 vcc, 8, v46\n"
+                    "s_and_b64 exec, exec, vcc\n"
+                    "s_cbranch_execz " + G + "rem\n"
+                    "s_or_b64 s[46:47], s[46:47], exec\n";
+    if (d != 0) {
+      c += "v_add_u32 v36, " + std::to_string(d) + ", " + vI + "\n";
+      A = "v36";
+    }
+    c += "v_sub_u32 v42, " + A + ", v22\n"
+         "v_and_b32 v43, 0xffffffc7, v42\n"
+         "v_cmp_ne_u32 vcc, 0, v43\n"
+         "s_cbranch_vccnz " + G + "chk\n" + G + "rd:\n"
+         "v_xad_u32 v43, v35, v42, v34\n"
+         "ds_read_b64 v[52:53], v43\n"
+         "v_mov_b32 v55, " + A + "\n"
+         "s_waitcnt lgkmcnt(0)\n";
+    const bool fold = !others_read_i;
+    for (uint32_t k = 0; k < 8; k++) {
+      const std::string Pk = PU + "g" + std::to_string(k) + "_";
+      for (uint32_t i = L; i < J; i++) {
+        if (skip[i] || (fold && (int)i == inc)) continue;
+        if ((int)i == ld) {
+          const std::string Q = k < 4 ? "v52" : "v53";
+          if (k == 0 || k == 4)
+            c += "v_bfi_b32 " + D0 + ", s56, " + Q + ", " + D0 + "\n";
+          else  // byte k & 3 of Q into byte 0, bytes 1-3 kept (selector 0x070605XX in s41..s43)
+            c += "v_perm_b32 " + D0 + ", " + D0 + ", " + Q + ", s" + std::to_string(40 + (k & 3)) +
+                 "\n";
+          continue;
+        }
+        std::string mc;
+        if (!emit_uop(m, i, Pk, false, mc, uo)) return -1;
+        uc += mc;
+        c += mc;
+      }
+    }
+    if (fold) c += "v_lshl_add_u64 " + vpair(2 * rI, 0, 1) + ", " + vpair(2 * rI, 0, 1) + ", 0, 8\n";
+    c += "s_branch " + G + "top\n" +
+         // lanes failing the pass's test (vcc): misaligned ones run one ordinary iteration; aligned
+         // ones past the window are refilled, or run one iteration in an unaligned tile
+         G + "chk:\n"
+         "v_and_b32 v43, 7, v42\n"
+         "v_cmp_ne_u32 vcc, 0, v43\n"
+         "s_cbranch_vccnz " + G + "one\n"
+         "v_cmp_le_u32 vcc, 64, v42\n"
+         "s_cmp_eq_u32 " + m.aligned + ", 0\n"
+         "s_cbranch_scc1 " + G + "one\n"
+         "s_mov_b64 s[68:69], vcc\n" + refill_zero(A, PU + "g") +
+         "v_sub_u32 v42, " + A + ", v22\n"
+         "s_branch " + G + "rd\n" + G + "one:\ns_mov_b64 exec, vcc\n";
+    for (uint32_t i = L; i < J; i++) {
+      if (skip[i]) continue;
+      std::string mc;
+      if (!emit_uop(m, i, PU + "g1x_", false, mc, uo)) return -1;
+      uc += mc;
+      c += mc;
+    }
+    c += "s_branch " + G + "top\n" + G + "rem:\n"
+         "s_mov_b64 exec, s[44:45]\n"
+         "v_cmp_ne_u32 vcc, " + vN + ", " + vI + "\n"
+         "s_andn2_b64 s[46:47], s[46:47], vcc\n"
+         "s_andn2_b64 exec, exec, s[46:47]\n"
+         "s_cbranch_execz .L" + P + "b" + std::to_string(J + 1) + "\n"
+         "s_branch .L" + PU + "body" + std::to_string(L) + "\n";
+    if (names_sgpr(uc + uo, 41, 47)) return 0;
+    out = c + uo;
+    return 1;
   }
 
   // The code of micro-op i (no block entry) in copy P.

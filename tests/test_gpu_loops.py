@@ -294,3 +294,60 @@ def test_loop_range_proofs(cuda, oracle_mod, name):
             got = _run_full(img, pkts, cuda, mem_size=mem, **layout)
             _check_against_oracle(oracle_mod, img, pkts, got, mem_size=mem,
                                   tag=f"full {name} mem {mem} {layout}")
+
+
+def gen_group_program(rng):
+    """A counted byte scan of the grouped form (jit.cpp counted_group: one `ldxb` from r3, r3
+    stepped by one, back edge `jlt r3, r2`): starts that differ per lane (misaligned passes), a
+    body that reads r3 itself (no folded increment) or not, and a tail that folds the final r3
+    and r5 into r0 so the production outputs see them."""
+    start = rng.choice(["mov r3, 0", "mov r3, 3", "mov r3, 8",
+                        "ldxb r3, [r1+0]\n    and r3, 7", "ldxb r3, [r1+1]\n    and r3, 15"])
+    base = rng.choice(["mov r4, r1\n    add r4, r3\n    ldxb r5, [r4+0]", "ldxb r5, [r3+0]"])
+    mix = rng.choice(["add r0, r5", "xor r0, r5\n    lsh r0, 1", "add r0, r5\n    xor r0, r3",
+                      "mov r6, r5\n    lsh r6, 3\n    sub r0, r6", "add32 r0, r5"])
+    pre = rng.choice(["", "mov r5, -1", "mov r5, 0x1234"])
+    return f"""
+    mov r0, 0
+    {pre}
+    {start}
+    jge r3, r2, done
+loop:
+    {base}
+    {mix}
+    add r3, 1
+    jlt r3, r2, loop
+done:
+    mov r6, r5
+    lsh r6, 8
+    xor r0, r6
+    xor r0, r3
+    exit
+"""
+
+
+@pytest.mark.parametrize("seed", range(2))
+def test_counted_loop_passes(cuda, oracle_mod, seed):
+    """Counted loops run 8 iterations per pass from one qword of the window (counted_group):
+    packets of every length up to 700 bytes (passes, refills, remainders of 0..7, packets shorter
+    than one pass), per-lane starts that differ mod 8, 16-byte aligned and unaligned packet bases
+    (no refills: the far path); production outputs and step counters against the oracle."""
+    from ebpf_emu import Program
+    from ebpf_emu.asm import assemble
+
+    rng = random.Random(4242 + seed)
+    for it in range(10):
+        src = gen_group_program(rng)
+        img = assemble(src)
+        p = Program(img)
+        assert p.compile()
+        assert "8 per pass" in p.jit_asm(2), src
+        p.close()
+        pkts = [bytes(rng.getrandbits(8) for _ in range(rng.choice([0, 3, 8, 9, 63, 64, 65, 71,
+                                                                    rng.randrange(700)])))
+                for _ in range(300)]
+        for layout in (dict(), dict(offsets_layout=True, align=16),
+                       dict(offsets_layout=True, align=1, misalign=3)):
+            prod = _run_prod(img, pkts, cuda, mem_size=1024, max_steps=100000, **layout)
+            _check_prod_against_oracle(oracle_mod, img, pkts, prod, mem_size=1024,
+                                       max_steps=100000, tag=f"seed {seed} it {it} {layout}")
