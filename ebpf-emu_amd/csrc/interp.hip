@@ -1351,6 +1351,10 @@ constexpr uint32_t kTileWaveLds = kWinBytes + kDagMetaBytes;  // window + metada
 #define TILE_ASM_OPERANDS : TILE_ASM_OUT : TILE_ASM_IN : TILE_ASM_CLOBBER
 // the compiled programs' preloaded window dwords (jit.cpp ldxk_fast): v[64:79]
 // and the stack window of memory tier 0.5 (jit.h kStackVgpr, kStackMax / 4 dwords): v[80:95]
+// compiled loop programs: the next 64 bytes of each lane's packet, prefetched by every window
+// refill (jit.cpp refill_prefetch), in v[56:71]
+#define TILE_ASM_CLOBBER_PREFETCH "v56", "v57", "v58", "v59", "v60", "v61", "v62", "v63", "v64", \
+    "v65", "v66", "v67", "v68", "v69", "v70", "v71"
 #define TILE_ASM_CLOBBER_WINDOW "v64", "v65", "v66", "v67", "v68", "v69", "v70", "v71", "v72", \
     "v73", "v74", "v75", "v76", "v77", "v78", "v79", "v80", "v81", "v82", "v83", "v84", "v85", \
     "v86", "v87", "v88", "v89", "v90", "v91", "v92", "v93", "v94", "v95"
@@ -1424,7 +1428,11 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
     const uint64_t t = rfl64(tile);
     const uint64_t nt = t + total_waves;
     uint32_t bkt, nst;
-    if constexpr (JIT) {
+    if constexpr (JIT && LOOPS) {  // + the refill prefetch registers of compiled loop programs
+      asm volatile(
+#include "tile_jit.inc"
+          TILE_ASM_OPERANDS, TILE_ASM_CLOBBER_PREFETCH);
+    } else if constexpr (JIT) {
       asm volatile(
 #include "tile_jit.inc"
           TILE_ASM_OPERANDS);
@@ -1588,7 +1596,8 @@ extern "C" __global__ __launch_bounds__(kBlock, 8) void ebpf_tile_jit_var(Launch
 }
 // loop programs (back edges, or a step budget that can bind): the exact budget and refillable
 // windows as tile_kernel<false, true>
-extern "C" __global__ __launch_bounds__(kBlock, 8) void ebpf_tile_jit_loop(LaunchArgs a) {
+// (6 waves per SIMD: the prefetch registers take the kernel past 64 VGPRs)
+extern "C" __global__ __launch_bounds__(kBlock, 6) void ebpf_tile_jit_loop(LaunchArgs a) {
   tile_body<false, true, true>(a);
 }
 #endif
