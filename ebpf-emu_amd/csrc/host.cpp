@@ -1036,7 +1036,8 @@ uint64_t ebpf_workspace_bytes(const ebpf_prog* p, const ebpf_batch* b, int devic
   if (!p || !b) return 0;
   const uint64_t x = (b->flags & EBPF_BATCH_XDP_MD) ? xdp_region_bytes(b) : 0;
   uint64_t bytes = kWsSlotsOff + x;
-  if (use_binning(p, b)) bytes += b->n * 4;  // the binned packet order
+  if (use_binning(p, b))  // the binned packet order, then the per-workgroup class counts
+    bytes += b->n * 4 + 4ull * kBinMaxWgs * kBinClasses;
   if (batch_tier(p, b) == 1) {
     int cur = device_of_current();
     hipSetDevice(device);
@@ -1188,7 +1189,8 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* bin, const ebpf_batch_out* ou
   if (kind == kKindLoop && use_binning(p, b)) {
     a.perm = (const uint32_t*)(ws + kWsSlotsOff);
     a.bin_counts = (uint32_t*)(ws + kWsBinCountsOff);
-    if (launch_binning(b->lens, b->n, a.bin_counts, (uint32_t*)a.perm, s) != hipSuccess) {
+    if (launch_binning(b->lens, b->n, (uint32_t*)a.perm + b->n, (uint32_t*)a.perm, s) !=
+        hipSuccess) {
       if (cur != device) hipSetDevice(cur);
       return EBPF_EHIP;
     }

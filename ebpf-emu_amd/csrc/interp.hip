@@ -1174,9 +1174,9 @@ __global__ __launch_bounds__(kBlock) void dag_kernel(LaunchArgs a) {
 // Length-binned lane packing (loop mode, offsets + lens layouts). Lanes of a tile run until its
 // longest packet is done, so a tile mixing 64- and 1500-byte frames idles half its lanes in a
 // per-byte loop. A counting sort by class ceil(len / 128) (capped) groups similar lengths:
-// bin_hist counts the classes (per-workgroup LDS histogram, one device atomic per class per
-// workgroup), bin_scatter reserves each workgroup's range per class and writes the indices,
-// longest class first.
+// bin_hist counts the classes per workgroup (LDS histogram, wave-aggregated), bin_scatter
+// derives each workgroup's range per class from those counts and writes the indices, longest
+// class first.
 // The order within a class is arbitrary; every output stays indexed by the original packet.
 // ============================================================================================
 constexpr int kBinBlock = 1024;
@@ -1208,8 +1208,10 @@ __device__ __forceinline__ uint32_t wave_class_slot(uint32_t c, uint32_t* h) {
   return slot;
 }
 
+// Per-workgroup class counts (wgc[block][class], plain stores: no device atomics, which on two
+// class words serialized 256 workgroups' adds in each kernel).
 __global__ __launch_bounds__(kBinBlock) void bin_hist(const uint16_t* lens, uint64_t n,
-                                                      uint32_t* bins) {
+                                                      uint32_t* wgc) {
   __shared__ uint32_t h[kBinClasses];
   if (threadIdx.x < kBinClasses) h[threadIdx.x] = 0;
   __syncthreads();
@@ -1217,25 +1219,34 @@ __global__ __launch_bounds__(kBinBlock) void bin_hist(const uint16_t* lens, uint
        i += (uint64_t)gridDim.x * kBinBlock)
     (void)wave_class_slot(bin_class(lens[i]), h);
   __syncthreads();
-  if (threadIdx.x < kBinClasses && h[threadIdx.x]) atomicAdd(&bins[threadIdx.x], h[threadIdx.x]);
+  if (threadIdx.x < kBinClasses) wgc[blockIdx.x * kBinClasses + threadIdx.x] = h[threadIdx.x];
 }
 
+// Each workgroup sums the class totals and the counts of the workgroups before it (thread t
+// reads class t % 16 of every 64th workgroup), then writes its packets' indices from
+// base(class) = packets of longer classes + earlier workgroups' packets of the class.
 __global__ __launch_bounds__(kBinBlock) void bin_scatter(const uint16_t* lens, uint64_t n,
-                                                         uint32_t* bins, uint32_t* perm) {
-  __shared__ uint32_t h[kBinClasses], base[kBinClasses];
+                                                         const uint32_t* wgc, uint32_t* perm) {
+  static_assert(kBinBlock % kBinClasses == 0, "class of a thread fixed across the sum");
+  __shared__ uint32_t h[kBinClasses], tot[kBinClasses], pre[kBinClasses], base[kBinClasses];
   const uint32_t t = threadIdx.x;
-  if (t < kBinClasses) h[t] = 0;
+  if (t < kBinClasses) h[t] = tot[t] = pre[t] = 0;
   __syncthreads();
-  for (uint64_t i = (uint64_t)blockIdx.x * kBinBlock + t; i < n; i += (uint64_t)gridDim.x * kBinBlock)
-    (void)wave_class_slot(bin_class(lens[i]), h);
+  uint32_t my_tot = 0, my_pre = 0;
+  for (uint32_t j = t; j < gridDim.x * kBinClasses; j += kBinBlock) {
+    const uint32_t v = wgc[j];
+    my_tot += v;
+    if (j / kBinClasses < blockIdx.x) my_pre += v;
+  }
+  if (my_tot) atomicAdd(&tot[t % kBinClasses], my_tot);
+  if (my_pre) atomicAdd(&pre[t % kBinClasses], my_pre);
   __syncthreads();
   if (t < kBinClasses) {
     // classes in descending order (longest packets first): the hardware dispatches tiles in
     // order, so the long tiles start first and the short ones fill the launch's tail
-    uint32_t start = 0;
-    for (int c = (int)t + 1; c < kBinClasses; c++) start += bins[c];
-    base[t] = start + (h[t] ? atomicAdd(&bins[kBinClasses + t], h[t]) : 0u);
-    h[t] = 0;
+    uint32_t start = pre[t];
+    for (int c = (int)t + 1; c < kBinClasses; c++) start += tot[c];
+    base[t] = start;
   }
   __syncthreads();
   for (uint64_t i = (uint64_t)blockIdx.x * kBinBlock + t; i < n; i += (uint64_t)gridDim.x * kBinBlock) {
@@ -1244,12 +1255,12 @@ __global__ __launch_bounds__(kBinBlock) void bin_scatter(const uint16_t* lens, u
   }
 }
 
-hipError_t launch_binning(const uint16_t* lens, uint64_t n, uint32_t* bins, uint32_t* perm,
+hipError_t launch_binning(const uint16_t* lens, uint64_t n, uint32_t* wgc, uint32_t* perm,
                           hipStream_t stream) {
   uint64_t g = (n + 4ull * kBinBlock - 1) / (4ull * kBinBlock);  // ~4 packets per thread
-  const int grid = (int)(g < 1 ? 1 : g > 1024 ? 1024 : g);
-  hipLaunchKernelGGL(bin_hist, dim3(grid), dim3(kBinBlock), 0, stream, lens, n, bins);
-  hipLaunchKernelGGL(bin_scatter, dim3(grid), dim3(kBinBlock), 0, stream, lens, n, bins, perm);
+  const int grid = (int)(g < 1 ? 1 : g > kBinMaxWgs ? kBinMaxWgs : g);
+  hipLaunchKernelGGL(bin_hist, dim3(grid), dim3(kBinBlock), 0, stream, lens, n, wgc);
+  hipLaunchKernelGGL(bin_scatter, dim3(grid), dim3(kBinBlock), 0, stream, lens, n, wgc, perm);
   return hipGetLastError();
 }
 

@@ -26,6 +26,7 @@ constexpr int kCounterShards = 64;    // device-atomic counter shards (spread co
 constexpr uint64_t kWsBinCountsOff = 384;
 constexpr uint64_t kWsBinCursorOff = 448;
 constexpr int kBinClasses = 16;  // packets are binned by ceil(len / 128), capped
+constexpr int kBinMaxWgs = 1024;  // binning grid cap; per-workgroup class counts follow the order
 constexpr uint64_t kWsXdpCursorOff = 320;  // u64: bytes staged by xdp_stage (reset per batch)
 constexpr uint64_t kWsShardsOff = 512;
 constexpr uint64_t kWsSlotsOff = kWsShardsOff + kCounterShards * 8 * 8;
@@ -92,7 +93,7 @@ int interp_grid(int kind, uint32_t n_uops, bool tiny, uint64_t n_tiles, int* gri
 // Length-binned lane packing for the loop-mode tile kernel (offsets + lens layouts): fills
 // perm[n] with the packet indices grouped by ceil(len / 128), so a tile's lanes run loops of
 // similar trip counts. Two kernels on `stream` (histogram, scatter); bins start zeroed.
-hipError_t launch_binning(const uint16_t* lens, uint64_t n, uint32_t* bins, uint32_t* perm,
+hipError_t launch_binning(const uint16_t* lens, uint64_t n, uint32_t* wgc, uint32_t* perm,
                           hipStream_t stream);
 
 // xdp_md calling convention: stage image i = [xdp_md {8, 8 + len}][packet][...] for every packet
