@@ -1347,7 +1347,8 @@ struct Compiler {
            "v_or_b32 v44, 0x40000000, v44\n"
            "v_or_b32 v44, v44, v37\n"
            // (v22 is -64 after a budget restart: sign-extended)
-           "v_mov_b32 v46, v22\nv_ashrrev_i32 v47, 31, v22\n"
+           "v_mov_b32 v46, v22\n"
+           "v_ashrrev_i32 v47, 31, v46\n"
            "v_lshl_add_u64 v[46:47], v[32:33], 0, v[46:47]\n";
   }
 
@@ -1697,8 +1698,12 @@ struct Compiler {
 
   // Whether text names an SGPR in [lo, hi] (sN or s[a:b]).
   static bool names_sgpr(const std::string& text, uint32_t lo, uint32_t hi) {
+    return names_reg(text, 's', lo, hi);
+  }
+  // Whether text names register kind k ('s' or 'v') in [lo, hi] (kN or k[a:b]).
+  static bool names_reg(const std::string& text, char k, uint32_t lo, uint32_t hi) {
     for (size_t p = 0; p + 1 < text.size(); p++) {
-      if (text[p] != 's' || (p && (isalnum((unsigned char)text[p - 1]) || text[p - 1] == '_' ||
+      if (text[p] != k || (p && (isalnum((unsigned char)text[p - 1]) || text[p - 1] == '_' ||
                                    text[p - 1] == '.')))
         continue;
       size_t q = p + 1;
@@ -1737,8 +1742,9 @@ struct Compiler {
   // line, entered at .L<PU>gent) in out, 0 when the loop does not qualify, -1 on a compiler error.
   int counted_group(const Marker& m, uint32_t L, uint32_t J, uint32_t rI, uint32_t rN,
                     const std::vector<char>& skip, const std::string& P, const std::string& PU,
-                    std::string& out) {
+                    std::string& out, bool p16 = true) {
     if (!zwin || !qcache || cache || getenv("EBPFEMU_NO_GROUP")) return 0;
+    if (getenv("EBPFEMU_NO_PASS16")) p16 = false;
     int ld = -1, inc = -1;
     bool others_read_i = false;
     for (uint32_t i = L; i < J; i++) {
@@ -1759,7 +1765,39 @@ struct Compiler {
     if (base != rI || uops[ld].dst == rI || d < -(1 << 20) || d > (1 << 20)) return 0;
     const std::string G = ".L" + PU + "g", vI = "v" + std::to_string(2 * rI),
                       vN = "v" + std::to_string(2 * rN), D0 = "v" + std::to_string(uops[ld].dst * 2);
-    std::string A = vI, uc, uo;  // uc / uo: the micro-ops' code (checked for s[44:47])
+    std::string A = vI, uc, uo;  // uc / uo: the micro-ops' code (checked for s[41:47])
+    std::string body16;          // the 16-byte pass's micro-op code (checked for v[48:51])
+    const bool fold = !others_read_i;
+    // nb copies of the block, the load of copy k taking byte k & 3 of dword src[k / 4]
+    auto pass = [&](uint32_t nb, const std::vector<std::string>& src, const std::string& tag,
+                    std::string& c) {
+      for (uint32_t k = 0; k < nb; k++) {
+        const std::string Pk = PU + tag + std::to_string(k) + "_";
+        for (uint32_t i = L; i < J; i++) {
+          if (skip[i] || (fold && (int)i == inc)) continue;
+          if ((int)i == ld) {
+            const std::string& Q = src[k / 4];
+            if ((k & 3) == 0)
+              c += "v_bfi_b32 " + D0 + ", s56, " + Q + ", " + D0 + "\n";
+            else  // byte k & 3 of Q into byte 0, bytes 1-3 kept (selector 0x070605XX in s41..s43)
+              c += "v_perm_b32 " + D0 + ", " + D0 + ", " + Q + ", s" + std::to_string(40 + (k & 3)) +
+                   "\n";
+            continue;
+          }
+          std::string mc, mo;
+          if (!emit_uop(m, i, Pk, false, mc, mo)) return false;
+          uc += mc;
+          uo += mo;
+          if (nb == 16) body16 += mc + mo;
+          c += mc;
+        }
+      }
+      if (fold)
+        c += "v_lshl_add_u64 " + vpair(2 * rI, 0, 1) + ", " + vpair(2 * rI, 0, 1) + ", 0, " +
+             std::to_string(nb) + "\n";
+      c += "s_branch " + G + "top\n";
+      return true;
+    };
     std::string c = G + "ent:\ns_mov_b64 s[44:45], exec\ns_mov_b64 s[46:47], 0\n"
                     "s_mov_b32 s41, 0x07060501\ns_mov_b32 s42, 0x07060502\n"
                     "s_mov_b32 s43, 0x07060503\n" + G + "top:\n"
@@ -1773,39 +1811,43 @@ struct Compiler {
       c += "v_add_u32 v36, " + std::to_string(d) + ", " + vI + "\n";
       A = "v36";
     }
-    c += "v_sub_u32 v42, " + A + ", v22\n"
-         "v_and_b32 v43, 0xffffffc7, v42\n"
+    c += "v_sub_u32 v42, " + A + ", v22\n";
+    if (p16) {
+      // passes of 16 while every lane has 16 left and a0 16-aligned inside the window (one
+      // ds_read_b128; its second qword becomes the qword cache)
+      c += "v_cmp_gt_i32 vcc, 16, v46\n"
+           "s_cbranch_vccnz " + G + "p8\n"
+           "v_and_b32 v43, 0xffffffcf, v42\n"
+           "v_cmp_ne_u32 vcc, 0, v43\n"
+           "s_cbranch_vccnz " + G + "c16\n" + G + "r16:\n"
+           "v_xad_u32 v43, v35, v42, v34\n"
+           "ds_read_b128 v[48:51], v43\n"
+           "v_add_u32 v55, 8, " + A + "\n"
+           "s_waitcnt lgkmcnt(0)\n"
+           "v_mov_b32 v52, v50\nv_mov_b32 v53, v51\n";
+      if (!pass(16, {"v48", "v49", "v50", "v51"}, "h", c)) return -1;
+      c += G + "c16:\n"
+           "v_and_b32 v43, 15, v42\n"
+           "v_cmp_ne_u32 vcc, 0, v43\n"
+           "s_cbranch_vccnz " + G + "p8\n"
+           "s_cmp_eq_u32 " + m.aligned + ", 0\n"
+           "s_cbranch_scc1 " + G + "p8\n"
+           "v_cmp_le_u32 vcc, 64, v42\n"
+           "s_mov_b64 s[68:69], vcc\n" + refill_zero(A, PU + "h") +
+           "v_sub_u32 v42, " + A + ", v22\n"
+           "s_branch " + G + "r16\n" + G + "p8:\n";
+    }
+    c += "v_and_b32 v43, 0xffffffc7, v42\n"
          "v_cmp_ne_u32 vcc, 0, v43\n"
          "s_cbranch_vccnz " + G + "chk\n" + G + "rd:\n"
          "v_xad_u32 v43, v35, v42, v34\n"
          "ds_read_b64 v[52:53], v43\n"
          "v_mov_b32 v55, " + A + "\n"
          "s_waitcnt lgkmcnt(0)\n";
-    const bool fold = !others_read_i;
-    for (uint32_t k = 0; k < 8; k++) {
-      const std::string Pk = PU + "g" + std::to_string(k) + "_";
-      for (uint32_t i = L; i < J; i++) {
-        if (skip[i] || (fold && (int)i == inc)) continue;
-        if ((int)i == ld) {
-          const std::string Q = k < 4 ? "v52" : "v53";
-          if (k == 0 || k == 4)
-            c += "v_bfi_b32 " + D0 + ", s56, " + Q + ", " + D0 + "\n";
-          else  // byte k & 3 of Q into byte 0, bytes 1-3 kept (selector 0x070605XX in s41..s43)
-            c += "v_perm_b32 " + D0 + ", " + D0 + ", " + Q + ", s" + std::to_string(40 + (k & 3)) +
-                 "\n";
-          continue;
-        }
-        std::string mc;
-        if (!emit_uop(m, i, Pk, false, mc, uo)) return -1;
-        uc += mc;
-        c += mc;
-      }
-    }
-    if (fold) c += "v_lshl_add_u64 " + vpair(2 * rI, 0, 1) + ", " + vpair(2 * rI, 0, 1) + ", 0, 8\n";
-    c += "s_branch " + G + "top\n" +
-         // lanes failing the pass's test (vcc): misaligned ones run one ordinary iteration; aligned
-         // ones past the window are refilled, or run one iteration in an unaligned tile
-         G + "chk:\n"
+    if (!pass(8, {"v52", "v53"}, "g", c)) return -1;
+    // lanes failing the pass's test (vcc): misaligned ones run one ordinary iteration; aligned
+    // ones past the window are refilled, or run one iteration in an unaligned tile
+    c += G + "chk:\n"
          "v_and_b32 v43, 7, v42\n"
          "v_cmp_ne_u32 vcc, 0, v43\n"
          "s_cbranch_vccnz " + G + "one\n"
@@ -1830,6 +1872,8 @@ struct Compiler {
          "s_cbranch_execz .L" + P + "b" + std::to_string(J + 1) + "\n"
          "s_branch .L" + PU + "body" + std::to_string(L) + "\n";
     if (names_sgpr(uc + uo, 41, 47)) return 0;
+    if (p16 && names_reg(body16, 'v', 48, 51))  // the block's code uses the 16-byte pass's registers
+      return counted_group(m, L, J, rI, rN, skip, P, PU, out, false);
     out = c + uo;
     return 1;
   }
