@@ -78,7 +78,74 @@ done:
     exit
 """
 
-LOOP_PROGRAMS = [FORWARD_SUM, BACKWARD_WORDS, STRIDED]
+# byte-only loads (zero windows: the transposed, prefetched refills of jit.cpp refill_prefetch):
+# a backward scan (every refill misses the prefetch, which is the window above), a forward scan
+# that re-reads byte 0 every 48 bytes (window [0, 64) reloaded, then the forward windows again:
+# hits and misses alternate), and strided bytes with reads past len and past the image end
+BACKWARD_BYTES = """
+    mov r0, 0
+    mov r3, r2
+loop:
+    jle r3, 0, done
+    sub r3, 1
+    mov r4, r1
+    add r4, r3
+    ldxb r5, [r4+0]
+    xor r0, r5
+    lsh r0, 1
+    ja loop
+done:
+    exit
+"""
+
+REREAD_BYTES = """
+    mov r0, 0
+    mov r3, 0
+    mov r6, 0
+loop:
+    jge r3, r2, done
+    mov r4, r1
+    add r4, r3
+    ldxb r5, [r4+0]
+    add r0, r5
+    add r3, 1
+    add r6, 1
+    jlt r6, 48, loop
+    mov r6, 0
+    ldxb r5, [r1+0]
+    xor r0, r5
+    ja loop
+done:
+    exit
+"""
+
+STRIDED_BYTES = """
+    mov r0, 0
+    mov r3, 0
+    mov r6, 0
+loop:
+    jge r6, 40, done
+    add r6, 1
+    add r3, 37
+    mov r7, r3
+    mod r7, r2
+    mov r4, r1
+    add r4, r7
+    ldxb r5, [r4+0]
+    add r0, r5
+    ldxb r5, [r4+70]
+    xor r0, r5
+    jset r5, 0x4, far
+    ja loop
+far:
+    ldxb r5, [r4+1000]
+    add r0, r5
+    ja loop
+done:
+    exit
+"""
+
+LOOP_PROGRAMS = [FORWARD_SUM, BACKWARD_WORDS, STRIDED, BACKWARD_BYTES, REREAD_BYTES, STRIDED_BYTES]
 
 
 def _packets(rng, n):
