@@ -1375,10 +1375,12 @@ struct Compiler {
                     "s_cbranch_scc1 .Lpfh" + U + "\n" + transposed_loads(0, true) +
                     "s_waitcnt vmcnt(0)\n"
                     ".Lpfh" + U + ":\n";
-    // bytes at or past len zeroed, then the window slots written
+    // per slot: bytes at or past len zeroed, the window slot written, and the packet's next 64
+    // bytes loaded into the same registers (a DS write reads its data VGPRs at issue)
     for (uint32_t k = 0; k < 4; k++) {
-      const std::string K = std::to_string(k), R0 = std::to_string(56 + 4 * k);
-      r += slot_of(k, false) +
+      const std::string K = std::to_string(k), R0 = std::to_string(56 + 4 * k),
+                        R3 = std::to_string(59 + 4 * k);
+      r += slot_of(k, true) +
            "v_sub_u32 v37, v49, v54\n"   // bytes left past this chunk's start
            "s_mov_b64 exec, s[62:63]\n"
            "v_cmp_gt_i32 vcc, 16, v37\n"
@@ -1387,12 +1389,15 @@ struct Compiler {
       for (uint32_t d = 0; d < 4; d++) r += zero_dword("v" + std::to_string(56 + 4 * k + d), 4 * d);
       r += "s_mov_b64 exec, s[62:63]\n"
            ".Lnz" + K + U + ":\n"
-           "ds_write_b128 v41, v[" + R0 + ":" + std::to_string(59 + 4 * k) + "] offset:" +
-           std::to_string(1024 * k) + "\n"
+           "ds_write_b128 v41, v[" + R0 + ":" + R3 + "] offset:" + std::to_string(1024 * k) + "\n"
+           "v_add_u32 v37, 64, v54\n"
+           "v_cmp_lt_u32 vcc, v37, v49\n"
+           "s_and_b64 exec, exec, vcc\n"
+           "v_add_co_u32 v42, vcc, v50, v40\nv_addc_co_u32 v43, vcc, 0, v51, vcc\n"
+           "global_load_dwordx4 v[" + R0 + ":" + R3 + "], v[42:43], off offset:64\n"
            "s_mov_b64 exec, -1\n";
     }
-    // the next 64 bytes of every refilled packet (the bpermutes' waits also retire the writes)
-    return r + transposed_loads(64, false) + "s_mov_b64 exec, s[66:67]\n";
+    return r + "s_mov_b64 exec, s[66:67]\n";
   }
 
   // The byte cache of the per-byte loops: each lane keeps 16 packet bytes [TAG, TAG + 16) in
