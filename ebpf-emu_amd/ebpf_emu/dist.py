@@ -26,6 +26,6 @@ def reduce_counters(counters, group=None):
     """Sum the per-rank counters (int64 tensor [8], u64 bit patterns) across ranks in place."""
     import torch.distributed as dist
 
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+    if dist.is_available() and dist.is_initialized():
         dist.all_reduce(counters, op=dist.ReduceOp.SUM, group=group)
     return counters
