@@ -1286,11 +1286,12 @@ struct Compiler {
   //  * prefetched: each refill also loads every refilled packet's next 64 bytes [WB + 64,
   //    WB + 128) into v[56:71] (held transposed); the next refill waits for them (they have had
   //    the whole window's scan to arrive) and uses them where the new window is that one (a
-  //    forward scan); lanes whose window moved elsewhere load theirs first. The tile prologue
-  //    issues the first prefetch, the statement's end waits for loads still in flight.
+  //    forward scan: v23 = the prefetched window's offset); lanes whose window moved elsewhere
+  //    load theirs first, as does each lane's first refill. The statement's end waits for loads
+  //    still in flight.
   // Chunks wholly past the packet are not loaded; bytes at or past len are zeroed before the
-  // window writes (zwin). Clobbers v22 (the new WB of the refilled lanes), v26, v27, v37-v51,
-  // v54, v[56:71], s[60:63], s[66:67], vcc; exec restored (s[68:69]: the refilled lanes).
+  // window writes (zwin). Clobbers v22 (the new WB of the refilled lanes), v23, v26, v27,
+  // v37-v51, v54, v[56:71], s[60:63], s[66:67], vcc; exec restored (s[68:69]: the refilled lanes).
   static constexpr uint32_t kRemBias = 1u << 25;  // bytes left (signed, |.| < 2^24) + bias
 
   // Lane constants (exec = all lanes): v38 = L, v39 = 4 (L / 4) (bpermute index of packet q for
@@ -1352,12 +1353,11 @@ struct Compiler {
            "v_lshl_add_u64 v[46:47], v[32:33], 0, v[46:47]\n";
   }
 
-  std::string prefetch_prologue(const Marker& m, const std::string& P) const {
-    if (!prefetch) return "";
-    // every lane's next window [v22 + 64, v22 + 128) (v22 = 0, or -64 on a budget restart)
-    return "s_cmp_eq_u32 " + m.aligned + ", 0\ns_cbranch_scc1 .L" + P + "npf\n"
-           "s_mov_b64 exec, -1\n" + transpose_consts() + pack_lane(false) +
-           transposed_loads(64, false) + ".L" + P + "npf:\n";
+  // No window prefetched yet (v23, the packet offset of the window held in v[56:71], is a value
+  // no window base takes): the first refill of each lane loads its window and starts the
+  // prefetching, so a loop program that never leaves its first window reads nothing more.
+  std::string prefetch_prologue(const Marker&, const std::string&) const {
+    return prefetch ? "v_mov_b32 v23, 0x80000001\n" : "";
   }
 
   // refill_zero's replacement (transposed, prefetched); lanes s[68:69], address A.
@@ -1365,10 +1365,10 @@ struct Compiler {
     std::string r = "s_mov_b64 s[66:67], exec\ns_mov_b64 exec, -1\n" + transpose_consts() +
                     "v_mov_b32 v44, 0\n"
                     "s_mov_b64 exec, s[68:69]\n"
-                    "v_add_u32 v37, 64, v22\n"
                     "v_and_b32 v22, -16, " + A + "\n"
-                    "v_cmp_eq_u32 vcc, v22, v37\n"
+                    "v_cmp_eq_u32 vcc, v22, v23\n"
                     "s_andn2_b64 s[60:61], s[68:69], vcc\n" + pack_lane(true) +
+                    "v_add_u32 v23, 64, v22\n"  // the window this refill prefetches
                     "s_mov_b64 exec, -1\n"
                     "s_waitcnt vmcnt(0)\n"
                     "s_cmp_eq_u64 s[60:61], 0\n"
