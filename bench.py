@@ -38,6 +38,9 @@ CONFIGS = {
     # stores into the packet's header window and an atomic on the stack (memory tier 0.5 with
     # packet-window stores; --generic: the general interpreter's tier 1)
     "tier1": (2, "XDP_TX MAC-swap reflector with packet stores and a stack atomic (17 insns) over 1Mi x 64B frames"),
+    # a ~100-instruction firewall (past the tile interpreter's 62 micro-ops: the forward-program
+    # compiler; EBPFEMU_NO_JIT=1: dag_kernel), same frames as 5tuple
+    "acl": (2, "IPv4/IPv6 ACL firewall (97 insns) over 1Mi x 64B frames"),
 }
 PROGRAM_OF = {"stack": "5tuple_stack", "tier1": "mac_swap_tx"}
 

@@ -442,7 +442,8 @@ static std::vector<DUop> build_dag(const std::vector<Uop>& uops) {
 static std::vector<TUop> build_tile(const std::vector<Uop>& uops, const std::vector<DUop>& d,
                                     bool exact = false, bool stack = false) {
   const uint32_t n = (uint32_t)uops.size();
-  std::vector<TUop> t(kTileUops);
+  // (programs above kTileMaxUops: a table for the compiler only; tile_kernel never runs them)
+  std::vector<TUop> t(std::max<size_t>(kTileUops, n + 2));
   std::memset(t.data(), 0, t.size() * sizeof(TUop));
   // block starts: 0, jump targets, successors of block-ending micro-ops
   std::vector<char> start(n + 1, 0);
@@ -501,8 +502,8 @@ static std::vector<TUop> build_tile(const std::vector<Uop>& uops, const std::vec
     }
     u.hoff = id * TILE_SLOT;
   }
-  t[kTileUops - 1].hoff = T_DONE * TILE_SLOT;
-  t[kTileUops - 2].hoff = T_DONE * TILE_SLOT;  // exact-mode marker bit (loop mode)
+  t[t.size() - 1].hoff = T_DONE * TILE_SLOT;
+  t[t.size() - 2].hoff = T_DONE * TILE_SLOT;  // exact-mode marker bit (loop mode)
   return t;
 }
 
@@ -786,7 +787,7 @@ int ebpf_prog_load(const uint8_t* code, size_t nbytes, ebpf_prog** out, size_t* 
   if (forward && p->tier == 0 && !p->uops.empty() && p->uops.size() <= kMaxDagUops) {
     p->duops = build_dag(p->uops);
     p->duopsk = fold_const_loads(p->uops, p->duops);
-    if (p->uops.size() <= kTileMaxUops) {
+    if (p->uops.size() <= kJitMaxUops) {  // tile_kernel's (<= 62) and the compiler's tables
       p->tuops = build_tile(p->uops, p->duops);
       p->tuopsk = build_tile(p->uops, p->duopsk);
     }

@@ -1815,9 +1815,15 @@ static int jit_grid(hipFunction_t f, uint32_t lds, uint64_t n_tiles, int block =
   return (int)((waves + wpb - 1) / wpb);
 }
 
+// The compiled forward-only program runs where tile_kernel would, and instead of dag_kernel for
+// programs of 63..kJitMaxUops micro-ops.
+static bool jit_forward_for(int kind, uint32_t n_uops) {
+  return kind == kKindDag && (n_uops > kTileMaxUops || tile_kernel_for(kind, n_uops));
+}
+
 int launch_kernel_id(int kind, const LaunchArgs& a, const JitFns* jit, bool stack) {
   if (jit && jit->loop && kind == kKindLoop) return EBPF_KERNEL_JIT_LOOP;
-  if (jit && jit->fixed && kind == kKindDag && tile_kernel_for(kind, a.n_uops))
+  if (jit && jit->fixed && jit_forward_for(kind, a.n_uops))
     return jit_fixed_layout(&a) ? (stack ? EBPF_KERNEL_JIT_STACK : EBPF_KERNEL_JIT_FIXED)
                             : EBPF_KERNEL_JIT_VAR;
   if (kind == kKindDag)
@@ -1843,13 +1849,14 @@ hipError_t launch_interp(int kind, const LaunchArgs& a, int grid, hipStream_t st
   hipError_t e;
   if (jit && jit->loop && kind == kKindLoop) {  // the compiled loop program
     e = hipModuleLaunchKernel(jit->loop, grid, 1, 1, kBlock, 1, 1, lds, stream, bargs, nullptr);
-  } else if (jit && jit->fixed && kind == kKindDag && tile_kernel_for(kind, a.n_uops)) {
+  } else if (jit && jit->fixed && jit_forward_for(kind, a.n_uops)) {
     if (jit_fixed_layout(&a)) {  // double-buffered windows: its own LDS size and grid
       const uint32_t dlds = g_lds_pad + kDbWaves * kTileWaveLdsDb;
       e = hipModuleLaunchKernel(jit->fixed, jit_grid(jit->fixed, dlds, a.n_tiles, kDbBlock), 1, 1,
                                 kDbBlock, 1, 1, dlds, stream, bargs, nullptr);
-    } else {
-      e = hipModuleLaunchKernel(jit->var, grid, 1, 1, kBlock, 1, 1, lds, stream, bargs, nullptr);
+    } else {  // (the tile kernel's window LDS, also for programs past kTileMaxUops)
+      const uint32_t vlds = g_lds_pad + kWavesPerBlock * kTileWaveLds;
+      e = hipModuleLaunchKernel(jit->var, grid, 1, 1, kBlock, 1, 1, vlds, stream, bargs, nullptr);
     }
   } else
     e = hipLaunchKernel(kernel_for(kind, a.n_uops, &a), dim3(grid), dim3(kBlock), bargs, lds,

@@ -235,6 +235,8 @@ struct Compiler {
   Compiler(const std::vector<Uop>& u, const std::vector<TUop>& tt, bool lp = false, bool ex = false,
            const StackPlan* sp = nullptr)
       : uops(u), t(tt), n((uint32_t)u.size()), loops(lp), exact(ex), stk(sp) {
+    back_in.assign(n + 1, 0);
+    addr_src.assign(n + 1, -1);
     start.assign(n + 1, 0);
     target.assign(n + 1, 0);
     target[0] = 1;
@@ -654,6 +656,15 @@ struct Compiler {
     return s + "s_mov_b64 exec, 0\ns_branch " + entry_label(P, back) + "\n";
   }
 
+  // A VOP3 operand for an LPC value: an inline constant, or (programs above 64 micro-ops) a
+  // VGPR loaded in `pre` (v37 / v38: temporaries free at a jump's tail; an SGPR beside vcc would
+  // be a second constant-bus read).
+  static std::string vop3_lpc(const std::string& v, const char* vreg_, std::string& pre) {
+    if (v.empty() || v == "-1" || std::stoul(v) <= 64) return v;
+    pre += std::string("v_mov_b32 ") + vreg_ + ", " + v + "\n";
+    return vreg_;
+  }
+
   // Conditional jump tail: vcc = taken among the active lanes.
   std::string jtail(uint32_t i, const std::string& P) const {
     if (back_edge(i)) return back_tail(i, P);
@@ -661,19 +672,22 @@ struct Compiler {
     const bool x_next = x == i + 1, n_next = np == i + 1;
     const bool x_done = x >= n, n_done = np >= n;
     if (x_next && n_next) return "";
-    // the leaving lanes' LPC by one select on vcc (the pcs are inline constants), then exec
-    const std::string lx = lpc_of(x, x_done), ln = lpc_of(np, n_done);
+    // the leaving lanes' LPC by one select on vcc (the pcs are inline constants, or VGPRs above
+    // 64), then exec
+    std::string pre;
+    const std::string lx = vop3_lpc(lpc_of(x, x_done), "v37", pre),
+                      ln = vop3_lpc(lpc_of(np, n_done), "v38", pre);
     if (n_next)  // taken lanes leave
-      return (lx.empty() ? "" : "v_cndmask_b32_e64 v28, v28, " + lx + ", vcc\n") +
+      return pre + (lx.empty() ? "" : "v_cndmask_b32_e64 v28, v28, " + lx + ", vcc\n") +
              "s_andn2_b64 exec, exec, vcc\n";
     if (x_next)  // not-taken lanes leave
-      return (ln.empty() ? "" : "v_cndmask_b32_e64 v28, " + ln + ", v28, vcc\n") +
+      return pre + (ln.empty() ? "" : "v_cndmask_b32_e64 v28, " + ln + ", v28, vcc\n") +
              "s_and_b64 exec, exec, vcc\n";
     // both leave
-    std::string s;
+    std::string s = pre;
     if (!lx.empty() || !ln.empty())
-      s = "v_cndmask_b32_e64 v28, " + (ln.empty() ? "v28" : ln) + ", " +
-          (lx.empty() ? "v28" : lx) + ", vcc\n";
+      s += "v_cndmask_b32_e64 v28, " + (ln.empty() ? "v28" : ln) + ", " +
+           (lx.empty() ? "v28" : lx) + ", vcc\n";
     return s + "s_mov_b64 exec, 0\n";
   }
 
@@ -2231,7 +2245,8 @@ bool compile_into_template(Compiler& c, Compiler* xc, std::vector<char>& code_ob
 bool jit_compile(const std::vector<Uop>& uops, const std::vector<TUop>& t,
                  std::vector<char>& code_object, std::string* err, std::string* asm_out,
                  const StackPlan* stk) {
-  if (uops.empty() || uops.size() > kTileMaxUops || t.size() < uops.size() ||
+  if (uops.empty() || uops.size() > kJitMaxUops || t.size() < uops.size() ||
+      (stk && uops.size() > kTileMaxUops) ||
       (stk && (stk->k == 0 || stk->k > kStackMax || stk->k % 4 || stk->off.size() != uops.size() ||
                stk->pw.size() != uops.size()))) {
     if (err) *err = "not a tile program";

@@ -83,6 +83,13 @@ def lib():
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"{LIB_PATH} is missing: build it with `make -C ebpf-emu_amd` "
                           "(there is no CPU fallback)")
+    # PyTorch ships its own HIP runtime (torch/lib/libamdhip64.so). Load it first, so this
+    # library's libamdhip64 dependency resolves to that same runtime by soname; loaded the other
+    # way round, torch would bind to /opt/rocm's runtime and find no GPU.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
     vp, sz, u64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64
     L.ebpf_batch_init.argtypes = [ctypes.POINTER(Batch)]

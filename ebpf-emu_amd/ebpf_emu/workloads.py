@@ -159,8 +159,124 @@ drop:
     exit
 """
 
+# a firewall of ~100 instructions (past the tile interpreter's 62 micro-ops: compiled by the
+# forward-program compiler instead of interpreted by dag_kernel): 802.1Q, IPv4 sanity (version,
+# IHL, TTL, fragments), source and destination address rules, TCP flag and port rules, UDP
+# service rules, ICMP types, IPv6 next header / hop limit, ARP opcodes. Loads are little-endian
+# (emu.rs:341-349): big-endian fields are compared byte-swapped or converted with be16.
+ACL = """
+    mov r0, 2                 # XDP_PASS
+    jlt r2, 34, out
+    ldxh r3, [r1+12]          # EtherType
+    mov r8, 14                # L3 offset
+    jne r3, 0x0081, novlan    # 802.1Q (0x8100)
+    ldxh r3, [r1+16]
+    mov r8, 18
+novlan:
+    jeq r3, 0xdd86, ipv6      # 0x86DD
+    jeq r3, 0x0608, arp       # 0x0806
+    jne r3, 0x0008, out       # 0x0800
+    mov r4, r1
+    add r4, r8                # IPv4 header
+    ldxb r5, [r4+0]           # version / IHL
+    mov r6, r5
+    rsh r6, 4
+    jne r6, 4, drop
+    and r5, 0x0f
+    jlt r5, 5, drop
+    lsh r5, 2                 # IHL * 4
+    ldxb r6, [r4+8]           # TTL
+    jlt r6, 2, drop
+    ldxh r6, [r4+6]           # flags / fragment offset
+    be16 r6
+    and r6, 0x1fff
+    jne r6, 0, drop           # fragments
+    ldxb r7, [r4+9]           # protocol
+    ldxw r9, [r4+12]          # saddr (first octet in the low byte)
+    mov r6, r9
+    and r6, 0xff
+    jeq r6, 127, drop         # loopback source
+    jeq r6, 0, drop           # 0.0.0.0/8 source
+    mov r6, r9
+    and r6, 0xffff
+    jeq r6, 0xfea9, drop      # 169.254.0.0/16 source
+    ldxw r3, [r4+16]          # daddr
+    mov r6, r3
+    and r6, 0xf0
+    jeq r6, 0xe0, mcast       # 224.0.0.0/4
+    jeq r6, 0xf0, drop        # 240.0.0.0/4
+    add r4, r5                # L4 header
+    jeq r7, 6, tcp
+    jeq r7, 17, udp
+    jeq r7, 1, icmp
+    jeq r7, 47, drop          # GRE
+    ja out
+mcast:
+    jne r7, 17, drop          # multicast: UDP only
+    ja out
+tcp:
+    ldxh r6, [r4+2]           # destination port
+    be16 r6
+    ldxb r3, [r4+13]          # flags
+    mov r5, r3
+    and r5, 0x03
+    jeq r5, 3, drop           # SYN + FIN
+    jeq r3, 0, drop           # null scan
+    jeq r6, 23, drop          # telnet
+    jeq r6, 3389, drop        # RDP
+    jeq r6, 445, drop         # SMB
+    jge r6, 1024, out
+    mov r5, r9
+    and r5, 0xff
+    jeq r5, 10, drop          # 10.0.0.0/8 to a well-known port
+    ja out
+udp:
+    ldxh r6, [r4+2]
+    be16 r6
+    jeq r6, 53, dns
+    jeq r6, 1900, drop        # SSDP
+    jeq r6, 19, drop          # chargen
+    jeq r6, 123, ntp
+    ja out
+dns:
+    mov r5, r9
+    and r5, 0xffff
+    jeq r5, 0xa8c0, out       # resolvers in 192.168.0.0/16
+    ja drop
+ntp:
+    ldxh r5, [r4+4]           # UDP length
+    be16 r5
+    jgt r5, 100, drop         # amplification-sized
+    ja out
+icmp:
+    ldxb r5, [r4+0]           # type
+    jeq r5, 8, out            # echo request
+    jeq r5, 0, out            # echo reply
+    jeq r5, 3, out            # unreachable
+    jeq r5, 11, out           # time exceeded
+    ja drop
+ipv6:
+    mov r4, r1
+    add r4, r8
+    ldxb r5, [r4+6]           # next header
+    ldxb r6, [r4+7]           # hop limit
+    jlt r6, 2, drop
+    jeq r5, 58, out           # ICMPv6
+    jeq r5, 0, drop           # hop-by-hop options
+    ja out
+arp:
+    ldxh r5, [r1+20]          # opcode
+    be16 r5
+    jgt r5, 2, drop
+    ja out
+drop:
+    mov r0, 1                 # XDP_DROP
+out:
+    exit
+"""
+
 PROGRAMS = {"drop": DROP_ALL, "5tuple": FIVE_TUPLE, "checksum": CHECKSUM,
-            "5tuple_stack": FIVE_TUPLE_STACK, "mac_swap_tx": MAC_SWAP_TX}
+            "5tuple_stack": FIVE_TUPLE_STACK, "mac_swap_tx": MAC_SWAP_TX, "acl": ACL}
 
 
 def program(name: str) -> bytes:

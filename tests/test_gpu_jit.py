@@ -1,5 +1,6 @@
-"""The program compiler (csrc/jit.cpp): forward-only tier-0 programs of <= 62 micro-ops compiled
-to gfx950 code for the tile kernel, instead of interpreted.
+"""The program compiler (csrc/jit.cpp): forward-only tier-0 programs of <= 256 micro-ops compiled
+to gfx950 code for the tile kernel, instead of interpreted (tile_kernel up to 62, dag_kernel
+beyond).
 
 CPU (no GPU needed, the compiler and assembler run in process): every such program compiles,
 the assembler accepts it, and its code has no interpreter machinery left (no index mode, no
@@ -41,9 +42,10 @@ def test_workloads_compile():
         assert ok, name
         # forward-only programs: the forward kernels (0, 1) and the loop kernel (2, for budgets
         # that can bind); the checksum loops: the loop kernel only
-        # (the stack-window programs: the main.rs layout's fixed-slot kernel only)
+        # (the stack-window programs: the main.rs layout's fixed-slot kernel only; the ACL, past
+        # 62 micro-ops: the forward kernels only, budgets that bind run dag_kernel / interp_kernel)
         variants = ((2,) if name == "checksum" else (1,) if name in ("5tuple_stack", "mac_swap_tx")
-                    else (0, 1, 2))
+                    else (0, 1) if name == "acl" else (0, 1, 2))
         for variant in variants:
             text = p.jit_asm(variant)
             key = "; compiled eBPF loop program" if variant == 2 else "; compiled eBPF program"
@@ -192,14 +194,37 @@ def _same(a, b, ctx, keys=("status", "r0", "verdict", "regs", "counters")):
         assert np.array_equal(a[k], b[k]), f"{ctx}: {k} differs"
 
 
+def test_fuzz_large_programs_compile():
+    """Forward-only tier-0 programs of 63-256 micro-ops (past the tile interpreter's 62) compile
+    too, with parked pcs above the inline-constant range staged through SGPRs."""
+    rng = random.Random(4711)
+    n = 0
+    for _ in range(60):
+        img = gen_program(rng, n=rng.randrange(70, 250), allow_loops=False, tier0=True)
+        try:
+            p, ok = _eligible(img)
+        except Exception as e:
+            assert "ebpf_prog_load" in str(e) or "decode" in str(e).lower(), e
+            continue
+        if p.forward_only and ok:
+            n += 1
+            assert p.jit_asm(0) and p.jit_asm(1)
+        p.close()
+    assert n >= 20
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("layout", ["fixed", "offsets", "init_regs"])
 @pytest.mark.parametrize("seed", range(3))
-def test_compiled_vs_interpreter_and_oracle(cuda, oracle_mod, layout, seed):
-    rng = random.Random(5150 + 7 * seed + 1000 * ["fixed", "offsets", "init_regs"].index(layout))
+@pytest.mark.parametrize("size", ["small", "large"])
+def test_compiled_vs_interpreter_and_oracle(cuda, oracle_mod, layout, seed, size):
+    """size large: 63-256 micro-ops, compiled instead of dag_kernel (the no-JIT reference)."""
+    rng = random.Random(5150 + 7 * seed + 1000 * ["fixed", "offsets", "init_regs"].index(layout) +
+                        (0 if size == "small" else 99991))
     n_run = 0
-    for it in range(40):
-        img = gen_program(rng, allow_loops=False, tier0=True)
+    for it in range(40 if size == "small" else 16):
+        img = gen_program(rng, allow_loops=False, tier0=True,
+                          n=None if size == "small" else rng.randrange(70, 250))
         try:
             oracle_mod.Program(img)
             p, ok = _eligible(img)
@@ -232,7 +257,7 @@ def test_compiled_vs_interpreter_and_oracle(cuda, oracle_mod, layout, seed):
         _same(prod, got, f"prod {layout} seed {seed} it {it} prog {img.hex()}",
               keys=("status", "r0", "verdict", "counters"))
         n_run += 1
-    assert n_run >= 20
+    assert n_run >= (20 if size == "small" else 6)
 
 
 @pytest.mark.gpu

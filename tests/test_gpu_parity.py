@@ -392,7 +392,7 @@ def test_workload_sample_vs_oracle(cuda, oracle_mod):
     n = 65536 + 37  # ragged tail
     buf = W.frames_fixed(n, 64, 3)
     frames = torch.from_numpy(buf).to(cuda)
-    for name in ("drop", "5tuple"):
+    for name in ("drop", "5tuple", "acl"):
         prog = Program(W.program(name))
         res = prog.run(frames, n=n, stride=64, r0=True, status=True)
         torch.cuda.synchronize()
