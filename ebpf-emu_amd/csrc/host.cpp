@@ -792,7 +792,8 @@ int ebpf_prog_load(const uint8_t* code, size_t nbytes, ebpf_prog** out, size_t* 
       p->tuopsk = build_tile(p->uops, p->duopsk);
     }
   }
-  if (p->tier == 0 && !p->uops.empty() && p->uops.size() <= kTileMaxUops) {
+  // (past kTileMaxUops: tables for the compiled loop program only, batch_kind)
+  if (p->tier == 0 && !p->uops.empty() && p->uops.size() <= kJitMaxUops) {
     const std::vector<DUop> d = p->duops.empty() ? build_dag(p->uops) : p->duops;
     p->ltuops = build_tile(p->uops, d);
     p->ltuopsx = build_tile(p->uops, d, true);
@@ -1020,7 +1021,9 @@ static int batch_kind(const ebpf_prog* p, const ebpf_batch* b, const ebpf_batch_
   *stk = !generic && stack_launch_ok(p, b, out, device);
   return *stk ? kKindDag
          : (p->dev_duops[device] && b->max_steps >= p->uops.size() && !generic) ? kKindDag
-         : (p->dev_ltuops[device] && !generic && !g_no_loop)            ? kKindLoop
+         : (p->dev_ltuops[device] && !generic && !g_no_loop &&
+            (p->uops.size() <= kTileMaxUops ||  // tile_kernel's loop mode, or compiled only
+             (p->jit_mod[device][2] && !(b->flags & EBPF_BATCH_NO_JIT))))          ? kKindLoop
                                                                          : batch_tier(p, b);
 }
 

@@ -634,9 +634,10 @@ struct Compiler {
                  "s_cbranch_scc1 .L" + P + "body" + std::to_string(L) + "\n";
         // the leaving lanes' parked pc by one select on vcc (a VOP3 write touches only the active
         // lanes), then exec keeps the staying lanes; SCC = some lane stays
-        const std::string F_lpc = lpc_of(F, F >= n);  // (loop programs: "-1" for done lanes)
-        std::string s = xb ? "v_cndmask_b32_e64 v28, " + F_lpc + ", v28, vcc\n"
-                           : "v_cndmask_b32_e64 v28, v28, " + F_lpc + ", vcc\n";
+        std::string s;  // (loop programs: "-1" for done lanes; pcs above 64 from a VGPR)
+        const std::string F_lpc = vop3_lpc(lpc_of(F, F >= n), "v37", s);
+        s += xb ? "v_cndmask_b32_e64 v28, " + F_lpc + ", v28, vcc\n"
+                : "v_cndmask_b32_e64 v28, v28, " + F_lpc + ", vcc\n";
         s += (xb ? "s_and_b64 exec, exec, vcc\n" : "s_andn2_b64 exec, exec, vcc\n");
         return s + "s_cbranch_scc1 .L" + P + "body" + std::to_string(L) + "\n";
       }
@@ -645,7 +646,8 @@ struct Compiler {
     if (ja) {
       s += park(std::to_string(x), x >= n);
     } else {
-      const std::string lx = lpc_of(x, x >= n), ln = lpc_of(np, np >= n);
+      const std::string lx = vop3_lpc(lpc_of(x, x >= n), "v37", s),
+                        ln = vop3_lpc(lpc_of(np, np >= n), "v38", s);
       if (!lx.empty() || !ln.empty())
         s += "v_cndmask_b32_e64 v28, " + (ln.empty() ? "v28" : ln) + ", " +
              (lx.empty() ? "v28" : lx) + ", vcc\n";
@@ -2259,7 +2261,7 @@ bool jit_compile(const std::vector<Uop>& uops, const std::vector<TUop>& t,
 bool jit_compile_loop(const std::vector<Uop>& uops, const std::vector<TUop>& t,
                       const std::vector<TUop>& tx, std::vector<char>& code_object,
                       std::string* err, std::string* asm_out) {
-  if (uops.empty() || uops.size() > kTileMaxUops || t.size() < uops.size() ||
+  if (uops.empty() || uops.size() > kJitMaxUops || t.size() < uops.size() ||
       tx.size() < uops.size()) {
     if (err) *err = "not a tile program";
     return false;

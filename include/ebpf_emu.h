@@ -171,9 +171,9 @@ int ebpf_prog_stack_window(const ebpf_prog* prog);
 
 /* Compile the program to gfx950 machine code now, if it is one the tile kernels run (memory tier
  * 0): straight-line code in pc order with direct register operands, replacing the interpreter's
- * dispatch. Forward-only programs of <= 256 micro-ops get the forward kernels (batches with
- * max_steps >= the program length); programs of <= 62 micro-ops also get the loop kernel (back
- * edges, or a step budget that can bind: the exact budget of the reference's step count). Needs no
+ * dispatch, for programs of <= 256 micro-ops. Forward-only programs get the forward kernels
+ * (batches with max_steps >= the program length); every such program also gets the loop kernel
+ * (back edges, or a step budget that can bind: the exact budget of the reference's step count). Needs no
  * GPU; done implicitly by the first upload. Returns 1 = compiled, 0 = not such a program (or
  * compilation disabled by EBPFEMU_NO_JIT=1), EBPF_EJIT on a compiler failure. */
 int ebpf_prog_compile(ebpf_prog* prog);

@@ -213,6 +213,26 @@ def test_fuzz_large_programs_compile():
     assert n >= 20
 
 
+def test_fuzz_large_loop_programs_compile():
+    """Tier-0 programs with back edges of 63-256 micro-ops: the loop program compiler takes them
+    (both copies and the exact-budget copy), with back-edge selects of pcs above 64."""
+    rng = random.Random(4712)
+    n = 0
+    for _ in range(60):
+        img = gen_program(rng, n=rng.randrange(70, 250), allow_loops=True, tier0=True)
+        try:
+            p, ok = _eligible(img)
+        except Exception as e:
+            assert "ebpf_prog_load" in str(e) or "decode" in str(e).lower(), e
+            continue
+        if p.tier == 0:
+            assert ok
+            assert p.jit_asm(2)
+            n += 1
+        p.close()
+    assert n >= 20
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("layout", ["fixed", "offsets", "init_regs"])
 @pytest.mark.parametrize("seed", range(3))
@@ -233,6 +253,16 @@ def test_compiled_vs_interpreter_and_oracle(cuda, oracle_mod, layout, seed, size
             continue
         if not ok:
             continue
+        if size == "large":  # compiled, not dag_kernel
+            import torch
+
+            from ebpf_emu import Program, _lib
+            q = Program(img)
+            q.compile()
+            fr = torch.zeros(64 * 64, dtype=torch.uint8, device=cuda)
+            k = q.batch_kernel(q.make_batch(fr, n=64, stride=64, max_steps=STEPS))
+            q.close()
+            assert k == _lib.EBPF_KERNEL_JIT_FIXED, _lib.KERNEL_NAMES[k]
         kw = {}
         ir = None
         if layout == "fixed":

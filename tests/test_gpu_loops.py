@@ -191,6 +191,48 @@ def test_fuzz_loop_programs_production_outputs(cuda, oracle_mod, seed):
     assert n_run >= 25
 
 
+@pytest.mark.parametrize("seed", range(2))
+def test_fuzz_large_loop_programs(cuda, oracle_mod, seed):
+    """Random tier-0 programs of 63-256 micro-ops with back edges: the compiled loop kernel
+    (tile_kernel's tables stop at 62) against the oracle (production outputs) and against the
+    general interpreter (every output), binding budgets included."""
+    from ebpf_emu import Program
+
+    rng = random.Random(7070 + seed)
+    n_run = 0
+    for it in range(14):
+        img = gen_program(rng, n=rng.randrange(70, 250), allow_loops=True, tier0=True)
+        try:
+            oracle_mod.Program(img)
+            p = Program(img)
+        except Exception:
+            continue
+        compiled = p.tier == 0 and p.compile()
+        if not compiled:
+            p.close()
+            continue
+        pkts = [gen_packet(rng) for _ in range(rng.choice([64, 65, 100, 130]))]
+        layout = dict(offsets_layout=True, align=16) if it % 2 else dict()
+        steps = rng.choice([2000, 150])
+        # the route: the compiled loop kernel, unless the program is forward-only with a budget
+        # that cannot bind (then the compiled forward kernels)
+        import torch
+        from ebpf_emu import _lib
+        frames = torch.zeros(len(pkts) * 256, dtype=torch.uint8, device=cuda)
+        k = p.batch_kernel(p.make_batch(frames, n=len(pkts), stride=256, max_steps=steps))
+        assert k in (_lib.EBPF_KERNEL_JIT_LOOP, _lib.EBPF_KERNEL_JIT_FIXED,
+                     _lib.EBPF_KERNEL_JIT_VAR), _lib.KERNEL_NAMES[k]
+        p.close()
+        prod = _run_prod(img, pkts, cuda, max_steps=steps, **layout)
+        _check_prod_against_oracle(oracle_mod, img, pkts, prod, max_steps=steps,
+                                   tag=f"seed {seed} it {it}")
+        full = _run_full(img, pkts, cuda, max_steps=steps, **layout)
+        _same_outputs(full, _run_full(img, pkts, cuda, max_steps=steps, generic=True, **layout),
+                      f"seed {seed} it {it} {img.hex()}")
+        n_run += 1
+    assert n_run >= 6
+
+
 @pytest.mark.parametrize("budget", [1, 2, 3, 5, 6, 7, 8, 13, 50, 101, 389, 997])
 def test_loop_step_budget_exact(cuda, oracle_mod, budget):
     """Budgets that bind at every position of the loop body, for lanes of different lengths in
