@@ -1789,9 +1789,44 @@ struct Compiler {
     std::string A = vI, uc, uo;  // uc / uo: the micro-ops' code (checked for s[41:47])
     std::string body16;          // the 16-byte pass's micro-op code (checked for v[48:51])
     const bool fold = !others_read_i;
+    // The byte-sum idiom: a block of exactly `ldxb rD, [rI + d]; add rS, rD` (+ the increment,
+    // folded) adds rD = (rD & ~0xff) | b_k for each byte b_k, so a pass of nb bytes adds
+    // nb * (rD & ~0xff) + the bytes' sum (v_sad_u8 against zero: four bytes per instruction;
+    // exact mod 2^64) and leaves rD's low byte at the last byte -- a few VALU instead of a
+    // dependent select + 64-bit add per byte.
+    int sum_add = -1;
+    if (fold && !getenv("EBPFEMU_NO_SUM_IDIOM")) {
+      int others = 0;
+      for (uint32_t i = L; i < J; i++) {
+        if (skip[i] || (int)i == inc || (int)i == ld) continue;
+        const Uop& u = uops[i];
+        others++;
+        if (u.op == U_ADD64 && (u.aux & F_SRC) && u.src == uops[ld].dst && u.dst != uops[ld].dst &&
+            u.dst != rI && u.dst != rN)
+          sum_add = (int)i;
+      }
+      if (others != 1) sum_add = -1;
+    }
+    const std::string D1 = "v" + std::to_string(uops[ld].dst * 2 + 1);
     // nb copies of the block, the load of copy k taking byte k & 3 of dword src[k / 4]
     auto pass = [&](uint32_t nb, const std::vector<std::string>& src, const std::string& tag,
                     std::string& c) {
+      if (sum_add >= 0) {
+        const std::string S = vpair(2 * uops[sum_add].dst, 0, 1);
+        c += "v_sad_u8 v26, " + src[0] + ", 0, 0\n";
+        for (size_t q = 1; q < src.size(); q++) c += "v_sad_u8 v26, " + src[q] + ", 0, v26\n";
+        c += "v_mov_b32 v27, 0\n"
+             "v_and_b32 v42, 0xffffff00, " + D0 + "\n"
+             "v_mov_b32 v43, " + D1 + "\n"
+             "v_lshlrev_b64 v[42:43], " + std::string(nb == 16 ? "4" : "3") + ", v[42:43]\n"
+             "v_lshl_add_u64 v[42:43], v[26:27], 0, v[42:43]\n"
+             "v_lshl_add_u64 " + S + ", v[42:43], 0, " + S + "\n"
+             "v_perm_b32 " + D0 + ", " + D0 + ", " + src.back() + ", s43\n"
+             "v_lshl_add_u64 " + vpair(2 * rI, 0, 1) + ", " + vpair(2 * rI, 0, 1) + ", 0, " +
+             std::to_string(nb) + "\n"
+             "s_branch " + G + "top\n";
+        return true;
+      }
       for (uint32_t k = 0; k < nb; k++) {
         const std::string Pk = PU + tag + std::to_string(k) + "_";
         for (uint32_t i = L; i < J; i++) {
