@@ -1310,7 +1310,6 @@ struct Compiler {
   // v37-v51, v54, v[56:71], s[60:63], s[66:67], vcc; exec restored (s[68:69]: the refilled lanes).
   static constexpr uint32_t kRemBias = 1u << 25;  // bytes left (signed, |.| < 2^24) + bias
 
-
   // Lane constants (exec = all lanes): v38 = L, v39 = 4 (L / 4) (bpermute index of packet q for
   // k = 0), v40 = the chunk offset 16 ((L ^ L/16) & 3), v54 = v40 + kRemBias, v41 = WIN - 48 L.
   static std::string transpose_consts() {
