@@ -1801,8 +1801,8 @@ struct Compiler {
         if (skip[i] || (int)i == inc || (int)i == ld) continue;
         const Uop& u = uops[i];
         others++;
-        if (u.op == U_ADD64 && (u.aux & F_SRC) && u.src == uops[ld].dst && u.dst != uops[ld].dst &&
-            u.dst != rI && u.dst != rN)
+        if ((int)i > ld && u.op == U_ADD64 && (u.aux & F_SRC) && u.src == uops[ld].dst &&
+            u.dst != uops[ld].dst && u.dst != rI && u.dst != rN)  // (the add after the load)
           sum_add = (int)i;
       }
       if (others != 1) sum_add = -1;

@@ -414,16 +414,18 @@ def gen_group_program(rng):
                         "ldxb r3, [r1+0]\n    and r3, 7", "ldxb r3, [r1+1]\n    and r3, 15"])
     base = rng.choice(["mov r4, r1\n    add r4, r3\n    ldxb r5, [r4+0]", "ldxb r5, [r3+0]"])
     mix = rng.choice(["add r0, r5", "xor r0, r5\n    lsh r0, 1", "add r0, r5\n    xor r0, r3",
-                      "mov r6, r5\n    lsh r6, 3\n    sub r0, r6", "add32 r0, r5"])
+                      "mov r6, r5\n    lsh r6, 3\n    sub r0, r6", "add32 r0, r5", "add r0, r5"])
     pre = rng.choice(["", "mov r5, -1", "mov r5, 0x1234"])
+    # the block's other micro-ops after the load, or before it (then they see the previous
+    # iteration's byte: not the byte-sum idiom)
+    body = f"{base}\n    {mix}" if rng.random() < 0.7 else f"{mix}\n    {base}"
     return f"""
     mov r0, 0
     {pre}
     {start}
     jge r3, r2, done
 loop:
-    {base}
-    {mix}
+    {body}
     add r3, 1
     jlt r3, r2, loop
 done:
