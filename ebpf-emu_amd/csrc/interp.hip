@@ -1608,7 +1608,7 @@ extern "C" __global__ __launch_bounds__(kBlock, 8) void ebpf_tile_jit_var(Launch
 // loop programs (back edges, or a step budget that can bind): the exact budget and refillable
 // windows as tile_kernel<false, true>
 // (6 waves per SIMD: the prefetch registers take the kernel past 64 VGPRs)
-extern "C" __global__ __launch_bounds__(kBlock, 6) void ebpf_tile_jit_loop(LaunchArgs a) {
+extern "C" __global__ __launch_bounds__(kBlock, 5) void ebpf_tile_jit_loop(LaunchArgs a) {
   tile_body<false, true, true>(a);
 }
 #endif
