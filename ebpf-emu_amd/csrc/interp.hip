@@ -1602,7 +1602,7 @@ extern "C" __global__ __launch_bounds__(kDbBlock, 1) void ebpf_tile_jit_fixed(La
   flush_counters<kDbWaves, true>(a, cnt64, retired, smem, lane, wv);
   if (trace) stamp(13);
 }
-extern "C" __global__ __launch_bounds__(kBlock, 8) void ebpf_tile_jit_var(LaunchArgs a) {
+extern "C" __global__ __launch_bounds__(kBlock, 7) void ebpf_tile_jit_var(LaunchArgs a) {
   tile_body<false, false, true>(a);
 }
 // loop programs (back edges, or a step budget that can bind): the exact budget and refillable
