@@ -116,10 +116,11 @@ def main():
     if args.total_packets:
         # strong scaling: this rank's contiguous shard of a global batch of seeded chunks
         assert not mixed, "--total-packets is defined for the 64-byte-frame configs"
-        sizes = D.chunk_sizes(args.total_packets, 1 << 20)
+        sizes = D.chunk_sizes(args.total_packets, D.CHUNK)
         mine = D.shard_chunks(len(sizes), world, rank)
         n = sum(sizes[k] for k in mine)
-        buf = np.concatenate([W.frames_fixed(sizes[k], 64, cfg_idx + 1 + 100 * k) for k in mine])
+        # (the chunks tests/golden/config4.json pins: dist.chunk_frames, one seed formula)
+        buf = np.concatenate([D.chunk_frames(k, sizes[k]) for k in mine])
         batches.append(dict(frames=torch.from_numpy(buf).to(dev)))
         algo_bytes = n * (64 + 1)
         pool_bytes = buf.nbytes
@@ -208,6 +209,19 @@ def main():
     total_pkts = (args.total_packets or n * world) * args.steps
     if not args.no_counters:
         assert sum(cnt[:7]) == total_pkts, (cnt, total_pkts)  # every packet: exactly one verdict
+    pinned = None
+    if args.total_packets and args.config == "5tuple" and not args.no_counters:
+        # parity of the benched workload: the global counters of the K steps equal K times the
+        # oracle's counters of the same chunks (tests/golden/config4.json), checked after timing
+        gp = os.path.join(ROOT, "tests", "golden", "config4.json")
+        if os.path.exists(gp):
+            with open(gp) as f:
+                g4 = json.load(f)
+            if g4["total_packets"] == args.total_packets and g4["chunk"] == D.CHUNK:
+                want = [(c * args.steps) & ((1 << 64) - 1) for c in g4["counters"]]
+                assert cnt == want, ("config-4 counters differ from tests/golden/config4.json",
+                                     cnt, want)
+                pinned = "tests/golden/config4.json: counters == steps x fixture"
     mpps = total_pkts / elapsed / 1e6
     # the dominant kernel's rate from its HIP-event time (rocprof's per-kernel average agrees),
     # and the same bytes over the wall-clock step time that `value` uses
@@ -220,9 +234,17 @@ def main():
     issue = None
     suffix = "" if mixed or fb == 64 else f"_{fb}B"
     pj = args.pmc_json or os.path.join(ROOT, "profiles", f"pmc_{args.config}{suffix}.json")
+    pmc_note = None
     if os.path.exists(pj) and not args.total_packets and n == 1 << 20 and not args.generic:
         with open(pj) as f:
             pmc = json.load(f)
+        # a summary profiled on another build of the kernel does not describe this run: refuse
+        # it when its kernel time differs from this run's by more than 10 %
+        prof_us = pmc.get("kernel_avg_us_profiled")
+        if not prof_us or abs(prof_us - kern_avg_ms * 1e3) > 0.10 * kern_avg_ms * 1e3:
+            pmc_note = (f"{os.path.relpath(pj, ROOT)} not attached: profiled at {prof_us} us vs "
+                        f"{kern_avg_ms * 1e3:.2f} us in this run")
+            pmc = {}
         traffic = pmc.get("hbm_bytes_per_launch")
         valu = pmc.get("avg", {}).get("SQ_INSTS_VALU")
         if valu:
@@ -292,6 +314,11 @@ def main():
             # device-resident rate from the HIP-event time of the K steps (no host launch / sync)
             "value_device": round((args.total_packets or n * world) / (kern_avg_ms * 1e-3) / 1e6, 2),
             "host_enqueue_us_per_step": round(t_enq / args.steps * 1e6, 3),
+            # the wall clock's fixed part: one host -> GPU -> host round trip around the K steps
+            # (first launch's latency + completion signal), which value spreads over K steps
+            "wall_fixed_us": round((elapsed - kern_avg_ms * 1e-3 * args.steps) * 1e6, 2),
+            "pmc_note": pmc_note,
+            "parity_pinned": pinned,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -1053,6 +1053,35 @@ uint64_t ebpf_workspace_bytes(const ebpf_prog* p, const ebpf_batch* b, int devic
   return bytes;  // (the xdp_md region, when present, is the last x bytes)
 }
 
+// The batch's workspace of `need` bytes on `device` (current): the caller's, or the library-owned
+// one of (device, stream), grown as needed (its first kWsSlotsOff bytes zeroed on allocation).
+static int batch_workspace(const ebpf_batch* b, uint64_t need, int device, hipStream_t s,
+                           uint8_t** out) {
+  if (b->workspace) {
+    if (b->workspace_bytes < need) return EBPF_EINVAL;
+    *out = (uint8_t*)b->workspace;
+    return EBPF_OK;
+  }
+  std::lock_guard<std::mutex> lk(g_ws_mu);
+  DevWorkspace& w = g_ws[{device, (void*)s}];
+  if (w.bytes < need) {
+    if (w.ptr) {
+      hipStreamSynchronize(s);
+      hipFree(w.ptr);
+      w.ptr = nullptr;
+      w.bytes = 0;
+    }
+    if (hipMalloc(&w.ptr, need) != hipSuccess) {
+      w.ptr = nullptr;
+      return EBPF_ENOMEM;
+    }
+    if (hipMemset(w.ptr, 0, kWsSlotsOff) != hipSuccess) return EBPF_EHIP;  // shards start at zero
+    w.bytes = need;
+  }
+  *out = (uint8_t*)w.ptr;
+  return EBPF_OK;
+}
+
 static int check_batch(const ebpf_batch* b) {
   if (!b) return EBPF_EINVAL;
   if (b->mem_size > (1u << 24)) return EBPF_EINVAL;
@@ -1096,33 +1125,12 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* bin, const ebpf_batch_out* ou
     return EBPF_EHIP;
   }
   // scratch: caller-provided or library-owned per (device, stream)
-  uint64_t need = ebpf_workspace_bytes(p, bin, device);
-  uint8_t* ws = (uint8_t*)b->workspace;
-  if (ws && b->workspace_bytes < need) {
+  const uint64_t need = ebpf_workspace_bytes(p, bin, device);
+  uint8_t* ws = nullptr;
+  rc = batch_workspace(bin, need, device, s, &ws);
+  if (rc) {
     if (cur != device) hipSetDevice(cur);
-    return EBPF_EINVAL;
-  }
-  if (!ws) {
-    std::lock_guard<std::mutex> lk(g_ws_mu);
-    DevWorkspace& w = g_ws[{device, (void*)s}];
-    if (w.bytes < need) {
-      if (w.ptr) {
-        hipStreamSynchronize(s);
-        hipFree(w.ptr);
-        w.ptr = nullptr;
-        w.bytes = 0;
-      }
-      if (hipMalloc(&w.ptr, need) != hipSuccess) {
-        if (cur != device) hipSetDevice(cur);
-        return EBPF_ENOMEM;
-      }
-      if (hipMemset(w.ptr, 0, kWsSlotsOff) != hipSuccess) {  // counter shards start at zero
-        if (cur != device) hipSetDevice(cur);
-        return EBPF_EHIP;
-      }
-      w.bytes = need;
-    }
-    ws = (uint8_t*)w.ptr;
+    return rc;
   }
   if (bin->flags & EBPF_BATCH_XDP_MD) {
     uint8_t* x = ws + need - xdp_region_bytes(bin);
@@ -1242,27 +1250,22 @@ int ebpf_run_batch_multi(ebpf_prog* p, int nshards, const int* devices, const eb
       if (devices[t] == devices[s]) return EBPF_EINVAL;  // one communicator rank per device
   }
   int cur = device_of_current();
-  // Each shard's counters go to a library-owned per-device scratch u64[8] (zeroed on the shard's
-  // stream), the scratch words are all-reduced, and the global totals are then ADDED to every
+  // Each shard's counters go to a u64[8] in its batch's workspace (kWsMultiOff, zeroed on the
+  // shard's stream), those words are all-reduced, and the global totals are then ADDED to every
   // outs[s].counters: the caller's counters accumulate, as ebpf_run_batch's do (the header's
   // contract). A failing shard leaves every caller counter untouched.
-  static std::mutex smu;
-  static std::map<std::pair<int, void*>, uint64_t*> scratch;  // per (device, stream)
   std::vector<ebpf_batch_out> o(outs, outs + nshards);
   for (int s = 0; s < nshards; s++) {
     const int d = devices[s];
     if (hipSetDevice(d) != hipSuccess) { hipSetDevice(cur); return EBPF_EHIP; }
-    uint64_t* sc = nullptr;
-    {
-      std::lock_guard<std::mutex> lk(smu);
-      uint64_t*& slot = scratch[{d, (void*)streams[s]}];
-      if (!slot && hipMalloc(&slot, EBPF_NCOUNTERS * sizeof(uint64_t)) != hipSuccess) {
-        slot = nullptr;
-        hipSetDevice(cur);
-        return EBPF_ENOMEM;
-      }
-      sc = slot;
-    }
+    int rc = check_batch(&batches[s]);
+    if (!rc) rc = ebpf_prog_upload(p, d);
+    uint8_t* ws = nullptr;
+    if (!rc)
+      rc = batch_workspace(&batches[s], ebpf_workspace_bytes(p, &batches[s], d), d,
+                           (hipStream_t)streams[s], &ws);
+    if (rc) { hipSetDevice(cur); return rc; }
+    uint64_t* sc = (uint64_t*)(ws + kWsMultiOff);
     o[s].counters = sc;
     if (hipMemsetAsync(sc, 0, EBPF_NCOUNTERS * sizeof(uint64_t), (hipStream_t)streams[s]) != hipSuccess) {
       hipSetDevice(cur);

@@ -838,8 +838,8 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
         put_image(mo, d, v, mem_size);
       }
     }
-    if (TIER == 1 && valid && a.fp_len_out) {  // the final frame stack (Emu.fp)
-      a.fp_len_out[pkt] = (uint8_t)csp;
+    if (TIER == 1 && valid && (a.fp_len_out || a.fp_out)) {  // the final frame stack (Emu.fp);
+      if (a.fp_len_out) a.fp_len_out[pkt] = (uint8_t)csp;     // either output may come alone
       if (a.fp_out)
         for (uint32_t i = 0; i < csp; i++) a.fp_out[pkt * kCallDepth + i] = cstack[(size_t)i * kWave];
     }

@@ -468,6 +468,16 @@ struct Compiler {
     std::vector<char> head(n, 0);  // targets of back edges
     for (uint32_t i = 0; i < n; i++)
       if (is_jump(uops[i]) && (uint32_t)uops[i].x <= i) head[(uint32_t)uops[i].x] = 1;
+    // widening thresholds: a bound that grows at a loop head jumps to the next of these (the
+    // program's non-negative constants and their neighbours, LEN's bound, then no bound), so a
+    // counter compared against a constant keeps that bound; a finite ladder, so it terminates
+    std::vector<uint64_t> ladder{kLenMax, ~0ull};
+    for (const Uop& u : uops)
+      if (!(u.aux & F_SRC) && u.k >= 0 && (uint64_t)u.k < (1ull << 62))
+        for (int64_t d = -1; d <= 1; d++)
+          if ((int64_t)u.k + d >= 0) ladder.push_back((uint64_t)(u.k + d));
+    std::sort(ladder.begin(), ladder.end());
+    auto widen_hi = [&](uint64_t h) { return *std::lower_bound(ladder.begin(), ladder.end(), h); };
     std::vector<uint32_t> work{0};
     in[0] = init;
     seen[0] = 1;
@@ -482,7 +492,8 @@ struct Compiler {
       for (int r = 0; r < 11; r++) {
         m[r] = av_meet(in[to][r], s[r]);
         if (head[to] && changes[to] > 4) {  // widen at loop heads
-          if (m[r].hi != in[to][r].hi) m[r].hi = m[r].slack >= 0 ? kLenMax : ~0ull;
+          if (m[r].hi != in[to][r].hi)
+            m[r].hi = m[r].slack >= 0 ? std::min(widen_hi(m[r].hi), kLenMax) : widen_hi(m[r].hi);
           if (m[r].lo != in[to][r].lo) m[r].lo = 0;
         }
         ch = ch || !av_eq(m[r], in[to][r]);
@@ -540,7 +551,10 @@ struct Compiler {
 
   // Registers live at each micro-op's entry (bit r), for live_in and the counted loops.
   std::vector<uint32_t> live() const {
+    // r0 is always an output (the return value and the verdict): live past the end, at EXIT and
+    // at a fault
     std::vector<uint32_t> in(n + 1, 0);
+    in[n] = 1u;
     auto rw = [&](const Uop& u, uint32_t& rd, uint32_t& wr) {
       const uint32_t d = 1u << u.dst, s = (u.aux & F_SRC) ? 1u << u.src : 0u;
       rd = wr = 0;
@@ -569,10 +583,10 @@ struct Compiler {
         uint32_t out = 0;
         const bool ends = u.op == U_EXIT || u.op == U_FAULT;
         if (is_jump(u)) {
-          if (t[i].x < n) out |= in[t[i].x];
-          if (u.op != U_JA && t[i].npc < n) out |= in[t[i].npc];
-        } else if (!ends && i + 1 < n) {
-          out = in[i + 1];
+          out |= in[std::min<uint32_t>(t[i].x, n)];
+          if (u.op != U_JA) out |= in[std::min<uint32_t>(t[i].npc, n)];
+        } else {
+          out = ends ? 1u : in[i + 1];
         }
         const uint32_t v = (rd | (out & ~wr)) & 0x7ffu;
         if (v != in[i]) {
@@ -1663,6 +1677,8 @@ struct Compiler {
     if (incs != 1) return true;
     const AbsVal &vi = ranges[L][rI], &vn = ranges[L][rN];
     if (vi.hi > kLenMax || vn.hi > kLenMax) return true;
+    // the entry's step total blen * max(1, rN - rI) <= blen * 2^24 must fit the 32-bit counter
+    if ((uint64_t)t[L].blen * kLenMax >= (1ull << 32)) return true;
     // an address copy `mov rA, rZ; add rA, rC` with rZ = 0 whose value only the block's one-byte
     // loads read (rA dead at both successors, rC unchanged until those loads): the loads take
     // rC as their base and the copy is not emitted
@@ -1674,7 +1690,7 @@ struct Compiler {
           !(b.aux & F_SRC) || b.dst != a.dst || b.src == a.dst)
         continue;
       const uint32_t rA = a.dst, rC = b.src;
-      if ((lv[L] >> rA) & 1 || (J + 1 < n && (lv[J + 1] >> rA) & 1)) continue;
+      if ((lv[L] >> rA) & 1 || (lv[J + 1] >> rA) & 1) continue;  // (lv[n]: r0)
       bool ok = true;
       std::vector<uint32_t> loads;
       for (uint32_t k = i + 2; k <= J && ok; k++) {
@@ -1683,7 +1699,8 @@ struct Compiler {
                              ((u.aux & F_SRC) && u.src == rA && u.op != U_LDX) || u.dst == rA;
         if (u.op == U_LDX && u.src == rA && u.dst != rA) loads.push_back(k);
         else if (reads_a) ok = false;
-        if (u.dst == rC && u.op != U_LDX) {  // rC written: later loads would see another value
+        if (u.dst == rC) {  // rC written (an LDX into rC included, which itself still reads the
+                            // old value): later loads would see another value
           for (uint32_t q = k + 1; q <= J && ok; q++) ok = !(uops[q].op == U_LDX && uops[q].src == rA);
           break;
         }
@@ -1702,7 +1719,11 @@ struct Compiler {
             (g ? ", 8 per pass from one qword while 8 are left" : "") + "\n"
             "v_sub_u32 v46, v" + std::to_string(2 * rN) + ", v" + std::to_string(2 * rI) + "\n"
             "v_max_i32 v46, 1, v46\n"
+            // the trip count may be 2^24 itself (r2 = LEN = mem_size = 2^24), past the 24-bit
+            // multiplier: blen * (trip - 1) + blen
+            "v_add_u32 v46, -1, v46\n"
             "v_mul_u32_u24 v46, " + std::to_string(t[L].blen) + ", v46\n"
+            "v_add_u32 v46, " + std::to_string(t[L].blen) + ", v46\n"
             "v_add_co_u32_e32 v46, vcc, v46, v29\n"
             "s_cbranch_vccnz .L" + P + "body" + Ls + "\n"
             "v_mov_b32 v29, v46\n"

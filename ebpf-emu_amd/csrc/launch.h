@@ -20,7 +20,7 @@ constexpr int kWinStride = kWin + 4;  // padded per-lane LDS stride: 17 dwords, 
 constexpr int kMaxLdsUops = 4096;     // programs up to this many micro-ops are staged in LDS
 constexpr int kCallDepth = 64;        // EBPF_MAX_CALL_DEPTH
 constexpr int kCounterShards = 64;    // device-atomic counter shards (spread contention)
-// workspace layout: [(unused) | xdp_md cursor u64 @320 | length-bin counts u32[16] @384 | bin cursors
+// workspace layout: [(unused) | multi-GPU counter sums u64[8] @256 | xdp_md cursor u64 @320 | length-bin counts u32[16] @384 | bin cursors
 // u32[16] @448, 512 B][shards u64[64][8]][tier-1 wave slots, or the length-binned packet order
 // u32[n]]; bin counts/cursors and shards are zero between batches
 constexpr uint64_t kWsBinCountsOff = 384;
@@ -28,6 +28,7 @@ constexpr uint64_t kWsBinCursorOff = 448;
 constexpr int kBinClasses = 16;  // packets are binned by ceil(len / 128), capped
 constexpr int kBinMaxWgs = 1024;  // binning grid cap; per-workgroup class counts follow the order
 constexpr uint64_t kWsXdpCursorOff = 320;  // u64: bytes staged by xdp_stage (reset per batch)
+constexpr uint64_t kWsMultiOff = 256;  // u64[8]: ebpf_run_batch_multi's per-shard counter sums
 constexpr uint64_t kWsShardsOff = 512;
 constexpr uint64_t kWsSlotsOff = kWsShardsOff + kCounterShards * 8 * 8;
 

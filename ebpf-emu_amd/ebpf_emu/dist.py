@@ -22,6 +22,22 @@ def chunk_sizes(total_packets: int, chunk: int) -> list[int]:
     return [chunk] * full + ([rest] if rest else [])
 
 
+CHUNK = 1 << 20  # packets per seeded chunk of a global batch (BASELINE config 4)
+
+
+def chunk_seed(k: int) -> int:
+    """config_id of chunk k of the config-4 global batch: the one formula bench.py
+    --total-packets, tests/golden/make_golden.py (config4.json) and the tests all use."""
+    return 3 + 100 * k
+
+
+def chunk_frames(k: int, size: int):
+    """Chunk k of the global batch: `size` seeded 64-byte frames (workloads.frames_fixed)."""
+    from . import workloads as W
+
+    return W.frames_fixed(size, 64, config_id=chunk_seed(k))
+
+
 def reduce_counters(counters, group=None):
     """Sum the per-rank counters (int64 tensor [8], u64 bit patterns) across ranks in place."""
     import torch.distributed as dist

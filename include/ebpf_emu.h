@@ -215,10 +215,10 @@ int ebpf_batch_kernel(ebpf_prog* prog, const ebpf_batch* batch, const ebpf_batch
 /* Multi-GPU: shard s runs on devices[s] / streams[s] (distinct devices); the shards' counters are
  * summed with one RCCL all-reduce over xGMI, and the global totals of this call are ADDED to
  * every outs[s].counters (accumulated as in ebpf_run_batch, never overwritten; the per-shard sums
- * go through a library-owned device scratch first). Shards are independent (no data-path
- * exchange). Requires counters in every out. A failing call leaves every caller counter
- * untouched. Returns after enqueueing (asynchronous on each stream; the scratch is per (device,
- * stream), so calls on the same streams are ordered by them). */
+ * go through 64 bytes of the shard's workspace first -- batches[s].workspace, or the
+ * library-owned one of (device, stream)). Shards are independent (no data-path exchange).
+ * Requires counters in every out. A failing call leaves every caller counter untouched. Returns
+ * after enqueueing (asynchronous on each stream, so calls on the same streams are ordered). */
 int ebpf_run_batch_multi(ebpf_prog* prog, int nshards, const int* devices,
                          const ebpf_batch* batches, const ebpf_batch_out* outs,
                          ebpf_stream_t const* streams);

@@ -6,9 +6,9 @@ fuzz vector is cross-checked against the independent Python restatement before i
   workloads.json    : BASELINE configs 2/3/5 at full size (1,048,576 packets) -> counters,
                       CRC32 of the verdict array, first 256 verdicts
   config4.json      : BASELINE config 4, the 5-tuple over a 100,000,000-packet global batch of
-                      seeded 1 Mi-packet chunks (chunk k: workloads.frames_fixed(size, 64,
-                      3 + 100 k), as bench.py --total-packets builds it) -> per-chunk counters and
-                      verdict CRC32s, and the global counters
+                      seeded 1 Mi-packet chunks (chunk k: ebpf_emu.dist.chunk_frames(k, size), the
+                      one definition bench.py --total-packets also builds its shards with) ->
+                      per-chunk counters and verdict CRC32s, and the global counters
 Usage: python tests/golden/make_golden.py [config4]
 """
 import json
@@ -79,26 +79,30 @@ def workloads():
 
 
 def _config4_chunk(args):
+    from ebpf_emu import dist as D
+
     k, size = args
     p = oracle.Program(W.program("5tuple"))
-    buf = W.frames_fixed(size, 64, 3 + 100 * k)
+    buf = D.chunk_frames(k, size)
     r0, st, cnt = p.run_batch(buf, size, stride=64, threads=1)
     verdict = np.where(st != 0, 0xFF, np.where(r0 < 5, r0, 0xFE)).astype(np.uint8)
     return [int(c) for c in cnt], zlib.crc32(verdict.tobytes())
 
 
-def config4(total=100_000_000, chunk=1 << 20):
+def config4(total=100_000_000):
     from multiprocessing import Pool
 
     from ebpf_emu import dist as D
 
+    chunk = D.CHUNK
     sizes = D.chunk_sizes(total, chunk)
     with Pool(max(1, min(8, os.cpu_count() or 1) - 1)) as pool:
         per = pool.map(_config4_chunk, list(enumerate(sizes)))
     tot = [sum(c[i] for c, _ in per) for i in range(8)]
     assert sum(tot[:7]) == total
     return {"program": W.program("5tuple").hex(), "total_packets": total, "chunk": chunk,
-            "seed": "chunk k: workloads.frames_fixed(size, 64, config_id=3 + 100 * k)",
+            "seed": "chunk k: ebpf_emu.dist.chunk_frames(k, size) = workloads.frames_fixed(size, "
+                    "64, config_id=dist.chunk_seed(k) = 3 + 100 * k)",
             "mem_size": 1024, "r10": 512, "chunk_sizes": sizes,
             "chunk_counters": [c for c, _ in per], "chunk_verdict_crc32": [v for _, v in per],
             "counters": tot}

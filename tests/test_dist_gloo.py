@@ -38,7 +38,7 @@ def _rank_main(rank, world, port, out_dir):
     counters = torch.zeros(8, dtype=torch.int64)
     verdicts = []
     for k in D.shard_chunks(len(sizes), world, rank):
-        buf = W.frames_fixed(sizes[k], 64, config_id=3 + 100 * k)
+        buf = D.chunk_frames(k, sizes[k])
         r0, st, cnt = prog.run_batch(buf, sizes[k], stride=64, threads=2)
         counters += torch.from_numpy(cnt.view(np.int64))
         verdicts.append(np.where(st != 0, 0xFF, np.where(r0 < 5, r0, 0xFE)).astype(np.uint8))
@@ -63,7 +63,7 @@ def test_sharded_counters_match_single_process(tmp_path, oracle_mod, world):
     total = np.zeros(8, np.uint64)
     ref_v = []
     for k, sz in enumerate(D.chunk_sizes(TOTAL, CHUNK)):
-        buf = W.frames_fixed(sz, 64, config_id=3 + 100 * k)
+        buf = D.chunk_frames(k, sz)
         r0, st, cnt = prog.run_batch(buf, sz, stride=64, threads=2)
         total += cnt
         ref_v.append(np.where(st != 0, 0xFF, np.where(r0 < 5, r0, 0xFE)).astype(np.uint8))

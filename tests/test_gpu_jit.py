@@ -114,6 +114,13 @@ def test_loop_range_proofs_compile():
         text = p.jit_asm(2)
         assert ("one-byte loads proven in bounds" in text) == name.startswith("proven"), name
         p.close()
+    from test_gpu_loops import COUNTED_EDGE_PROGRAMS
+
+    for name, src in COUNTED_EDGE_PROGRAMS.items():  # (their GPU runs: test_counted_loop_edges)
+        p = Program(assemble(src))
+        assert p.compile()
+        assert "counted loop" in p.jit_asm(2), name
+        p.close()
     rng = _r.Random(3)
     proven = 0
     for _ in range(60):

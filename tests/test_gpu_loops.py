@@ -332,6 +332,90 @@ done:
 }
 
 
+# Counted-loop edges (jit.cpp counted_entry), each a program the compiler takes as a counted loop:
+# a trip count of exactly 2^24 (past the 24-bit multiplier that prices the entry's steps); an
+# address copy whose register is r0 (an output: the copy must not be dropped); an address copy
+# whose source register is rewritten by the block's own load (a later load through the copy must
+# not be rebased onto the rewritten register).
+COUNTED_EDGE_PROGRAMS = {
+    "trip_2p24": """
+    mov r3, 0
+    mov r6, 0x1000000
+    jge r3, r2, loop
+    ldxb r5, [r3+0]
+loop:
+    add r3, 1
+    jlt r3, r6, loop
+    mov r0, r3
+    exit
+""",
+    "addr_copy_r0": """
+    mov r0, 0
+    mov r6, 0
+    mov r3, 0
+    jge r3, r2, done
+loop:
+    mov r0, r1
+    add r0, r3
+    ldxb r5, [r0+0]
+    add r6, r5
+    add r3, 1
+    jlt r3, r2, loop
+done:
+    lsh r6, 32
+    add r0, r6
+    exit
+""",
+    "addr_src_loaded": """
+    mov r0, 0
+    mov r3, 0
+    jge r3, r2, done
+loop:
+    mov r6, r3
+    mov r4, r1
+    add r4, r6
+    ldxb r6, [r4+0]
+    ldxb r5, [r4+0]
+    add r0, r5
+    lsh r0, 1
+    add r0, r6
+    add r3, 1
+    jlt r3, r2, loop
+done:
+    exit
+""",
+}
+
+
+@pytest.mark.parametrize("name", sorted(COUNTED_EDGE_PROGRAMS))
+def test_counted_loop_edges(cuda, oracle_mod, name):
+    """The counted-loop edges against the oracle, production outputs (the proven copy), at the
+    default budget and at budgets around the 2^24-trip loop's exact step count."""
+    from ebpf_emu import Program
+    from ebpf_emu.asm import assemble
+
+    img = assemble(COUNTED_EDGE_PROGRAMS[name])
+    p = Program(img)
+    assert p.compile()
+    assert "counted loop" in p.jit_asm(2), name
+    p.close()
+    rng = random.Random(len(name))
+    if name == "trip_2p24":  # (the oracle runs 2^25 steps per packet: a few packets)
+        pkts = [bytes(rng.getrandbits(8) for _ in range(n)) for n in (0, 14, 64)]
+        steps = 6 + 2 * (1 << 24)  # the whole run of a non-empty packet (5 + ... when empty)
+        for budget in (1 << 22, steps - 1, steps):
+            prod = _run_prod(img, pkts, cuda, max_steps=budget)
+            _check_prod_against_oracle(oracle_mod, img, pkts, prod, max_steps=budget,
+                                       tag=f"{name} budget {budget}")
+        assert (prod["status"] == 0).all() and (prod["r0"] == 1 << 24).all()
+        return
+    pkts = [bytes(rng.getrandbits(8) for _ in range(rng.choice([0, 1, 9, 63, 64, 65, 300, 700])))
+            for _ in range(200)]
+    for layout in (dict(), dict(offsets_layout=True, align=16)):
+        prod = _run_prod(img, pkts, cuda, **layout)
+        _check_prod_against_oracle(oracle_mod, img, pkts, prod, tag=f"{name} {layout}")
+
+
 def gen_scan_program(rng):
     """A random byte scan: r3 from a start value, step, guard and back-edge compare drawn from
     forms the range analysis proves or must refuse (offsets past the proof, <= bounds, negative

@@ -543,7 +543,7 @@ def test_config4_global_batch_golden(cuda):
     import torch
 
     from ebpf_emu import Program
-    from ebpf_emu import workloads as W
+    from ebpf_emu import dist as D
 
     with open(os.path.join(GOLDEN, "config4.json")) as f:
         g = json.load(f)
@@ -554,7 +554,7 @@ def test_config4_global_batch_golden(cuda):
     starts = np.concatenate([[0], np.cumsum(sizes)])
 
     def put(k):
-        return k, W.frames_fixed(sizes[k], 64, 3 + 100 * k)
+        return k, D.chunk_frames(k, sizes[k])
 
     with ThreadPoolExecutor(8) as ex:  # host generation in threads, copies in order
         for k, buf in ex.map(put, range(len(sizes))):
