@@ -41,8 +41,12 @@ CONFIGS = {
     # a ~100-instruction firewall (past the tile interpreter's 62 micro-ops: the forward-program
     # compiler; EBPFEMU_NO_JIT=1: dag_kernel), same frames as 5tuple
     "acl": (2, "IPv4/IPv6 ACL firewall (97 insns) over 1Mi x 64B frames"),
+    # the 5-tuple as a standard XDP program under the xdp_md calling convention (xdp.rs:16-20:
+    # r1 = ctx, data / data_end read from it), same frames as 5tuple; the ctx is synthesised in
+    # the kernel's window (no staging copy)
+    "xdp": (2, "IPv4 5-tuple as a standard XDP program, xdp_md ctx (37 insns) over 1Mi x 64B frames"),
 }
-PROGRAM_OF = {"stack": "5tuple_stack", "tier1": "mac_swap_tx"}
+PROGRAM_OF = {"stack": "5tuple_stack", "tier1": "mac_swap_tx", "xdp": "5tuple_xdp"}
 
 
 def parse():
@@ -159,7 +163,7 @@ def main():
                                  mem_size=mem_size, r10=r10, generic=args.generic)
         else:
             bd = prog.make_batch(b["frames"], n=n, stride=fb, mem_size=mem_size, r10=r10,
-                                 generic=args.generic)
+                                 generic=args.generic, xdp_md=args.config == "xdp")
         descs.append(bd)
     out = _lib.BatchOut()
     out.verdict = verdict.data_ptr()
@@ -371,7 +375,7 @@ def cpu_baseline(args, img, batch0, mixed, n, mem_size, r10):
     stride = (max(64, args.frame_bytes) + 15) // 16 * 16
 
     def rate(nthreads, seconds):
-        kw = dict(mem_size=mem_size, r10=r10, threads=nthreads)
+        kw = dict(mem_size=mem_size, r10=r10, threads=nthreads, xdp_md=args.config == "xdp")
         # chunks sized to ~0.2 s of work so the time budget is met closely
         chunk = max(4096, min(n, int((1 << 14 if mixed else 1 << 20) * nthreads / 8)))
         done = 0

@@ -957,6 +957,7 @@ s_load_dword {KMEM}, %[ka], %[o_mem]
 .if %[fixed] == 0
 s_load_dwordx2 {KOFF}, %[ka], %[o_offsets]
 s_load_dwordx2 {KLEN}, %[ka], %[o_lens]
+s_load_dword {T5L}, %[ka], %[o_xdp]
 .endif
 v_mbcnt_lo_u32_b32 {t0}, -1, 0
 v_mbcnt_hi_u32_b32 {t0}, -1, {t0}
@@ -991,6 +992,12 @@ s_cmp_lg_u64 {KLEN}, 0
 s_cbranch_scc0 .Lnolen%=
 v_and_b32 {LEN}, 0xffff, {t7}
 .Lnolen%=:
+s_cmp_lg_u32 {T5L}, 0
+s_cbranch_scc0 .Lnoxdp%=
+v_min_u32 {LEN}, 0xffff, {LEN}
+v_add_u32 {LEN}, 8, {LEN}
+v_lshl_add_u64 {BASE}, {BASE}, 0, -8
+.Lnoxdp%=:
 .endif
 v_cndmask_b32 {LEN}, 0, {LEN}, vcc
 v_lshlrev_b32 {WIN}, 6, {t0}
@@ -1352,7 +1359,7 @@ s_cbranch_scc1 .Linitx%=
 ;@@JITINIT@@
 .Linitd%=:
 
-; JIT N=%= fixed=%[fixed] loops=%[loops] aligned=%[aligned]
+; JIT N=%= fixed=%[fixed] loops=%[loops] aligned=%[aligned] xdp=%[xdpf]
 ;@@JIT@@
 .Ldone%=:
 ; verdict byte, the lane's counter bucket (verdict 0..4, 0xfe -> 5, 0xff -> 6) into %[acc]

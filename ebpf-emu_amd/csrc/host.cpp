@@ -12,6 +12,7 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -216,8 +217,13 @@ int device_of_current() {
 
 struct ebpf_prog {
   std::vector<RefInsn> insns;
-  std::vector<Uop> uops;
+  std::vector<Uop> uops;  // one per decoded instruction: the general interpreter's (interp_kernel)
   int tier = 0;
+  // the micro-ops every other kernel runs: uops, or for a program with CALL the copies of
+  // flatten_calls (no CALL, no EXIT with a frame stack); xtier: their memory tier
+  std::vector<Uop> xuops;
+  int xtier = 0;
+  bool flattened = false;  // xuops are flatten_calls' copies
   bool tiny = false;  // straight-line and <= kTinyUops: persistent grid (see interp_grid)
   std::vector<DUop> duops;   // tier 0, forward jumps only, <= kMaxDagUops: dag_kernel's table
   std::vector<DUop> duopsk;  // the same with constant-address loads resolved (no init_regs)
@@ -277,9 +283,9 @@ static int jit_compile_locked(ebpf_prog* p) {
       p->jit_state = 1;
       for (int v = 0; v < 3 && p->jit_state == 1; v++) {
         if (!p->jit_has[v]) continue;
-        const bool ok = v == 2 ? jit_compile_loop(p->uops, p->ltuops, p->ltuopsx, p->jit_co[v],
+        const bool ok = v == 2 ? jit_compile_loop(p->xuops, p->ltuops, p->ltuopsx, p->jit_co[v],
                                                   &p->jit_err, &p->jit_asm[v])
-                               : jit_compile(p->uops, v ? p->tuopsk : p->tuops, p->jit_co[v],
+                               : jit_compile(p->xuops, v ? p->tuopsk : p->tuops, p->jit_co[v],
                                              &p->jit_err, &p->jit_asm[v],
                                              p->stack.k ? &p->stack : nullptr);
         if (!ok) p->jit_state = EBPF_EJIT;
@@ -308,6 +314,12 @@ static const bool g_no_loop = [] {
 // EBPFEMU_NO_STACK=1: no memory tier 0.5 (stack-window programs run on interp_kernel tier 1).
 static const bool g_no_stack = [] {
   const char* e = getenv("EBPFEMU_NO_STACK");
+  return e && e[0] == '1';
+}();
+
+// EBPFEMU_NO_FLATTEN=1: programs with CALL keep the general interpreter's frame stack.
+static const bool g_no_flatten = [] {
+  const char* e = getenv("EBPFEMU_NO_FLATTEN");
   return e && e[0] == '1';
 }();
 
@@ -607,6 +619,174 @@ static std::vector<DUop> fold_const_loads(const std::vector<Uop>& uops, std::vec
   return d;
 }
 
+// CALL / EXIT without a frame stack (emu.rs:265-279, Q12). A CALL at pc p jumps to t = p + 1 + off
+// and pushes t + 1; an EXIT pops the pc, or stops the program on an empty stack. The pushed
+// return address is a load-time constant of the call site, so a program that does not recurse
+// reaches a finite set of frame stacks, and the pair (pc, frame stack) is all the control state
+// there is (no registers are saved, emu.rs:265-272). The reachable pairs become the micro-ops of
+// a program without CALL: a CALL a jump to (t, stack + [t + 1]), an EXIT with a non-empty stack a
+// jump to (popped pc, the rest), a push past EBPF_MAX_CALL_DEPTH a ST_CALLDEPTH fault, a jump or
+// return past the end a jump past the program (a normal stop, Q11). Every instruction is still one
+// micro-op, so steps, faults and the step budget are the reference's. Layout: the pairs in chains
+// of fall-through successors (same stack, pc + 1), the chains in topological order of their jumps
+// where there is one (then the program is forward-only again), the chain that falls off the end
+// last. Fails (the general interpreter's frame stack runs the program) on recursion, more than
+// kJitMaxUops pairs, or two chains falling off the end.
+static bool flatten_calls(const std::vector<Uop>& u, std::vector<Uop>& out) {
+  const uint32_t n = (uint32_t)u.size();
+  if (n == 0) return false;
+  std::map<std::vector<uint32_t>, uint32_t> id;
+  std::vector<std::vector<uint32_t>> ctx;
+  auto ctx_of = [&](const std::vector<uint32_t>& st) -> uint32_t {
+    auto it = id.find(st);
+    if (it != id.end()) return it->second;
+    id.emplace(st, (uint32_t)ctx.size());
+    ctx.push_back(st);
+    return (uint32_t)ctx.size() - 1;
+  };
+  // explore the reachable (stack, pc) pairs; succ: the jump-like successor of each (or none)
+  std::map<std::pair<uint32_t, uint32_t>, int64_t> state;  // -> the pair's index in `order`
+  std::vector<std::pair<uint32_t, uint32_t>> order, work;
+  auto visit = [&](uint32_t c, uint32_t pc) -> bool {
+    if (pc >= n || state.count({c, pc})) return true;
+    if (state.size() >= kJitMaxUops) return false;
+    state[{c, pc}] = (int64_t)order.size();
+    order.push_back({c, pc});
+    work.push_back({c, pc});
+    return true;
+  };
+  // the jump-like successor of a pair: (context, pc), pc >= n for a stop; kind 0 none
+  auto jump_of = [&](uint32_t c, uint32_t pc, std::pair<uint32_t, uint32_t>& to) -> bool {
+    const Uop& o = u[pc];
+    if (o.op == U_CALL) {
+      if (ctx[c].size() >= EBPF_MAX_CALL_DEPTH) return false;  // (a ST_CALLDEPTH fault)
+      std::vector<uint32_t> st = ctx[c];
+      st.push_back((uint32_t)o.x + 1);
+      to = {ctx_of(st), (uint32_t)o.x};
+      return true;
+    }
+    if (o.op == U_EXIT) {
+      if (ctx[c].empty()) return false;
+      std::vector<uint32_t> st = ctx[c];
+      const uint32_t r = st.back();
+      st.pop_back();
+      to = {ctx_of(st), r};
+      return true;
+    }
+    if (o.op >= U_JA && o.op <= U_JLE32) {
+      to = {c, (uint32_t)o.x};
+      return true;
+    }
+    return false;
+  };
+  auto falls = [&](uint32_t pc) {  // the pair continues at pc + 1 (taken or not)
+    const uint8_t op = u[pc].op;
+    return op != U_JA && op != U_EXIT && op != U_FAULT && op != U_CALL;
+  };
+  ctx_of({});
+  visit(0, 0);
+  while (!work.empty()) {
+    const auto w = work.back();
+    work.pop_back();
+    std::pair<uint32_t, uint32_t> to;
+    if (jump_of(w.first, w.second, to) && !visit(to.first, to.second)) return false;
+    if (falls(w.second) && !visit(w.first, w.second + 1)) return false;
+  }
+  // chains of fall-through successors
+  const size_t S = order.size();
+  std::vector<int64_t> chain_of(S, -1);
+  std::vector<std::vector<uint32_t>> chains;
+  for (size_t i = 0; i < S; i++) {
+    const auto [c, pc] = order[i];
+    if (pc > 0 && falls(pc - 1) && state.count({c, pc - 1})) continue;  // inside another chain
+    std::vector<uint32_t> ch;
+    for (uint32_t q = pc;; q++) {
+      const int64_t k = state.at({c, q});
+      chain_of[k] = (int64_t)chains.size();
+      ch.push_back((uint32_t)k);
+      if (!falls(q) || q + 1 >= n) break;
+    }
+    chains.push_back(std::move(ch));
+  }
+  const size_t C = chains.size();
+  int64_t tail = -1;  // the chain whose last pair falls off the end
+  for (size_t k = 0; k < C; k++) {
+    const uint32_t last = order[chains[k].back()].second;
+    if (falls(last) && last + 1 >= n) {
+      if (tail >= 0) return false;
+      tail = (int64_t)k;
+    }
+  }
+  // topological order of the chains by their jumps (Kahn), the falling-off chain last; with a
+  // cycle (a loop, or a return to an earlier pair), discovery order: a loop program
+  std::vector<std::set<uint32_t>> to_ch(C);
+  std::vector<uint32_t> indeg(C, 0);
+  bool cyclic = false;
+  for (size_t k = 0; k < C; k++)
+    for (size_t j = 0; j < chains[k].size(); j++) {
+      const auto [c, pc] = order[chains[k][j]];
+      std::pair<uint32_t, uint32_t> to;
+      if (!jump_of(c, pc, to) || to.second >= n) continue;
+      const int64_t t = state.at(to), tc = chain_of[t];
+      if (tc == (int64_t)k) {
+        const size_t pos = std::find(chains[k].begin(), chains[k].end(), (uint32_t)t) -
+                           chains[k].begin();
+        cyclic = cyclic || pos <= j;
+      } else if (to_ch[k].insert((uint32_t)tc).second) {
+        indeg[tc]++;
+      }
+    }
+  std::vector<uint32_t> seq;
+  if (!cyclic) {
+    std::vector<uint32_t> ready;
+    for (size_t k = C; k-- > 0;)
+      if (!indeg[k] && (int64_t)k != tail) ready.push_back((uint32_t)k);
+    while (!ready.empty()) {
+      const uint32_t k = ready.back();
+      ready.pop_back();
+      seq.push_back(k);
+      for (uint32_t t : to_ch[k])
+        if (--indeg[t] == 0 && (int64_t)t != tail) ready.push_back(t);
+    }
+    if (tail >= 0 && indeg[tail] == 0) seq.push_back((uint32_t)tail);
+  }
+  if (seq.size() != C) {
+    seq.clear();
+    for (size_t k = 0; k < C; k++)
+      if ((int64_t)k != tail) seq.push_back((uint32_t)k);
+    if (tail >= 0) seq.push_back((uint32_t)tail);
+  }
+  std::vector<uint32_t> at(S);
+  uint32_t N = 0;
+  for (uint32_t k : seq)
+    for (uint32_t s2 : chains[k]) at[s2] = N++;
+  const uint32_t kPast = 0xFFFFFFFEu;  // a jump target past the program: a normal stop
+  out.assign(N, Uop{});
+  for (size_t i = 0; i < S; i++) {
+    const auto [c, pc] = order[i];
+    Uop o = u[pc];
+    std::pair<uint32_t, uint32_t> to;
+    const bool j = jump_of(c, pc, to);
+    const uint32_t x = j && to.second < n ? at[state.at(to)] : kPast;
+    if (o.op == U_CALL) {
+      if (!j) {
+        o = fault_uop(EBPF_ST_CALLDEPTH);
+      } else {
+        o.op = U_JA;
+        o.x = (int32_t)x;
+      }
+    } else if (o.op == U_EXIT && j) {
+      o.op = U_JA;
+      o.x = (int32_t)x;
+      o.dst = 0;  // (JA reads dst, emu.rs:220: r0 is always valid)
+    } else if (o.op >= U_JA && o.op <= U_JLE32) {
+      o.x = (int32_t)x;
+    }
+    out[at[i]] = o;
+  }
+  return true;
+}
+
 // Memory tier 0.5 (stack-window programs): a forward-only program of <= kTileMaxUops micro-ops
 // whose only memory writes are ST/STX at r10 + c for a c known at load time (the XDP spill / key
 // pattern: `stxdw [r10-8], r3`, also through a copy such as `mov r2, r10; add r2, -16`), with no
@@ -778,39 +958,53 @@ int ebpf_prog_load(const uint8_t* code, size_t nbytes, ebpf_prog** out, size_t* 
     if (u.op == U_ST || u.op == U_STX || u.op == U_ATOMIC || u.op == U_CALL) p->tier = 1;
     p->uops.push_back(u);
   }
+  // CALL / EXIT: the frame stacks as program copies (flatten_calls) for every kernel but the
+  // general interpreter, unless EBPFEMU_NO_FLATTEN=1 or the program does not flatten
+  p->xuops = p->uops;
+  if (std::any_of(p->uops.begin(), p->uops.end(), [](const Uop& u) { return u.op == U_CALL; }) &&
+      !g_no_flatten) {
+    std::vector<Uop> f;
+    if (flatten_calls(p->uops, f)) {
+      p->xuops = std::move(f);
+      p->flattened = true;
+    }
+  }
+  const std::vector<Uop>& xu = p->xuops;
+  for (const Uop& u : xu)
+    if (u.op == U_ST || u.op == U_STX || u.op == U_ATOMIC || u.op == U_CALL) p->xtier = 1;
   bool forward = true;  // no back edge: every lane's pc only grows (a DAG)
-  for (size_t i = 0; i < p->uops.size(); i++) {
-    const Uop& u = p->uops[i];
+  for (size_t i = 0; i < xu.size(); i++) {
+    const Uop& u = xu[i];
     if (u.op >= U_JA && u.op <= U_CALL && (uint32_t)u.x <= (uint32_t)i) forward = false;
   }
-  p->tiny = forward && p->uops.size() <= kTinyUops;
-  if (forward && p->tier == 0 && !p->uops.empty() && p->uops.size() <= kMaxDagUops) {
-    p->duops = build_dag(p->uops);
-    p->duopsk = fold_const_loads(p->uops, p->duops);
-    if (p->uops.size() <= kJitMaxUops) {  // tile_kernel's (<= 62) and the compiler's tables
-      p->tuops = build_tile(p->uops, p->duops);
-      p->tuopsk = build_tile(p->uops, p->duopsk);
+  p->tiny = forward && xu.size() <= kTinyUops;
+  if (forward && p->xtier == 0 && !xu.empty() && xu.size() <= kMaxDagUops) {
+    p->duops = build_dag(xu);
+    p->duopsk = fold_const_loads(xu, p->duops);
+    if (xu.size() <= kJitMaxUops) {  // tile_kernel's (<= 62) and the compiler's tables
+      p->tuops = build_tile(xu, p->duops);
+      p->tuopsk = build_tile(xu, p->duopsk);
     }
   }
   // (past kTileMaxUops: tables for the compiled loop program only, batch_kind)
-  if (p->tier == 0 && !p->uops.empty() && p->uops.size() <= kJitMaxUops) {
-    const std::vector<DUop> d = p->duops.empty() ? build_dag(p->uops) : p->duops;
-    p->ltuops = build_tile(p->uops, d);
-    p->ltuopsx = build_tile(p->uops, d, true);
+  if (p->xtier == 0 && !xu.empty() && xu.size() <= kJitMaxUops) {
+    const std::vector<DUop> d = p->duops.empty() ? build_dag(xu) : p->duops;
+    p->ltuops = build_tile(xu, d);
+    p->ltuopsx = build_tile(xu, d, true);
   }
-  if (p->tier == 1 && !g_no_stack) {  // memory tier 0.5: the compiled fixed-slot kernel only
-    StackAnalysis sa = analyze_stack(p->uops);
+  if (p->xtier == 1 && !g_no_stack) {  // memory tier 0.5: the compiled fixed-slot kernel only
+    StackAnalysis sa = analyze_stack(xu);
     const std::vector<DUop> dk =
-        sa.plan.k ? fold_const_loads(p->uops, build_dag(p->uops)) : std::vector<DUop>();
+        sa.plan.k ? fold_const_loads(xu, build_dag(xu)) : std::vector<DUop>();
     // packet-window stores: every load outside the stack window must be a constant-address one
     // (read from the window registers the stores update)
-    for (size_t i = 0; sa.plan.k && sa.plan.any_pw && i < p->uops.size(); i++)
-      if (p->uops[i].op == U_LDX && sa.plan.off[i] == kNoStack && (dk[i].opaux & 0xff) != U_LDXK)
+    for (size_t i = 0; sa.plan.k && sa.plan.any_pw && i < xu.size(); i++)
+      if (xu[i].op == U_LDX && sa.plan.off[i] == kNoStack && (dk[i].opaux & 0xff) != U_LDXK)
         sa.plan.k = 0;
     if (sa.plan.k) {
       for (const DUop& o : dk)
         if ((o.opaux & 0xff) == U_LDXK) p->kloads.push_back({o.addr, o.opaux >> 8});
-      p->tuopsk = build_tile(p->uops, dk, false, true);
+      p->tuopsk = build_tile(xu, dk, false, true);
       p->stack = std::move(sa.plan);
     }
   }
@@ -992,7 +1186,7 @@ static bool stack_launch_ok(const ebpf_prog* p, const ebpf_batch* b, const ebpf_
                             int device) {
   if (!p->stack.k || !p->jit_mod[device][1]) return false;
   if (b->flags & (EBPF_BATCH_GENERIC | EBPF_BATCH_NO_JIT | EBPF_BATCH_XDP_MD)) return false;
-  if (b->init_regs || b->init_fp_len || out->mem || b->max_steps < p->uops.size()) return false;
+  if (b->init_regs || b->init_fp_len || out->mem || b->max_steps < p->xuops.size()) return false;
   const uint64_t k = p->stack.k, r10 = b->r10;
   if (r10 % 4 || r10 < k || r10 > b->mem_size || r10 - k < b->stride) return false;
   for (const auto& kl : p->kloads) {
@@ -1017,12 +1211,15 @@ static bool stack_launch_ok(const ebpf_prog* p, const ebpf_batch* b, const ebpf_
 // step budget that can bind (exact budget); a stack-window batch runs the compiled fixed-slot kernel.
 static int batch_kind(const ebpf_prog* p, const ebpf_batch* b, const ebpf_batch_out* out,
                       int device, bool* stk) {
-  const bool generic = g_no_dag || (b->flags & EBPF_BATCH_GENERIC) || b->init_fp_len;
+  // (the final frame stacks of a flattened program are its copies' stacks: the general
+  // interpreter's frame stack writes them)
+  const bool generic = g_no_dag || (b->flags & EBPF_BATCH_GENERIC) || b->init_fp_len ||
+                       (p->flattened && (out->fp || out->fp_len));
   *stk = !generic && stack_launch_ok(p, b, out, device);
   return *stk ? kKindDag
-         : (p->dev_duops[device] && b->max_steps >= p->uops.size() && !generic) ? kKindDag
+         : (p->dev_duops[device] && b->max_steps >= p->xuops.size() && !generic) ? kKindDag
          : (p->dev_ltuops[device] && !generic && !g_no_loop &&
-            (p->uops.size() <= kTileMaxUops ||  // tile_kernel's loop mode, or compiled only
+            (p->xuops.size() <= kTileMaxUops ||  // tile_kernel's loop mode, or compiled only
              (p->jit_mod[device][2] && !(b->flags & EBPF_BATCH_NO_JIT))))          ? kKindLoop
                                                                          : batch_tier(p, b);
 }
@@ -1034,6 +1231,37 @@ static const JitFns* batch_jit(ebpf_prog* p, const ebpf_batch* b, int kind, bool
   if (kind == kKindDag && p->jit_mod[device][0]) return &p->jit_fn[device][b->init_regs ? 0 : 1];
   if (kind == kKindLoop && p->jit_mod[device][2]) return &p->jit_fn[device][2];
   return nullptr;
+}
+
+// The micro-ops a kernel kind runs: the general interpreter the decoded program's, every other
+// kernel the flattened copies (flatten_calls; the same micro-ops for a program without CALL).
+static uint32_t kind_uops(const ebpf_prog* p, int kind) {
+  return (uint32_t)(kind == kKindTier0 || kind == kKindTier1 ? p->uops.size() : p->xuops.size());
+}
+
+// The xdp_md convention in place (no staging copy): the compiled forward kernels and the tile
+// interpreter on the general layouts synthesise each packet's ctx in its window (interp.hip
+// xdp_window, jit.cpp xdp_shift) and read the packet 8 bytes further on; every other kernel runs
+// the images xdp_stage writes into the workspace. EBPFEMU_XDP_STAGE=1 stages always (A/B runs).
+static const bool g_xdp_stage = [] {
+  const char* e = getenv("EBPFEMU_XDP_STAGE");
+  return e && e[0] == '1';
+}();
+
+static bool xdp_in_place(ebpf_prog* p, const ebpf_batch* b, bool mem_out, int device, int kind,
+                         bool stk) {
+  if (!(b->flags & EBPF_BATCH_XDP_MD) || g_xdp_stage || stk || kind != kKindDag) return false;
+  LaunchArgs a{};
+  a.n_uops = kind_uops(p, kind);
+  a.frames = b->frames;
+  a.offsets = b->offsets;
+  a.lens = b->lens;
+  a.stride = b->stride;
+  a.n_tiles = (b->n + 63) / 64;
+  a.mem_out = mem_out ? (uint8_t*)16 : nullptr;
+  const int id = launch_kernel_id(kind, a, batch_jit(p, b, kind, stk, device), false);
+  return id == EBPF_KERNEL_JIT_FIXED || id == EBPF_KERNEL_JIT_VAR ||
+         (id == EBPF_KERNEL_TILE && !launch_fixed_layout(a));
 }
 
 uint64_t ebpf_workspace_bytes(const ebpf_prog* p, const ebpf_batch* b, int device) {
@@ -1120,7 +1348,7 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* bin, const ebpf_batch_out* ou
   bool stk = false;
   const int kind = batch_kind(p, b, out, device, &stk);
   int grid = 0;
-  if (interp_grid(kind, (uint32_t)p->uops.size(), p->tiny, n_tiles, &grid) != 0) {
+  if (interp_grid(kind, kind_uops(p, kind), p->tiny, n_tiles, &grid) != 0) {
     if (cur != device) hipSetDevice(cur);
     return EBPF_EHIP;
   }
@@ -1132,7 +1360,8 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* bin, const ebpf_batch_out* ou
     if (cur != device) hipSetDevice(cur);
     return rc;
   }
-  if (bin->flags & EBPF_BATCH_XDP_MD) {
+  const bool xdp_direct = xdp_in_place(p, bin, out->mem != nullptr, device, kind, stk);
+  if ((bin->flags & EBPF_BATCH_XDP_MD) && !xdp_direct) {
     uint8_t* x = ws + need - xdp_region_bytes(bin);
     uint32_t* doffs = (uint32_t*)x;
     uint16_t* dlens = (uint16_t*)(x + align16(bin->n * 4));
@@ -1158,7 +1387,7 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* bin, const ebpf_batch_out* ou
   a.tprog = kind == kKindLoop ? p->dev_ltuops[device]
            : b->init_regs      ? p->dev_tuops[device] : p->dev_tuopsk[device];
   a.tprog_exact = p->dev_ltuopsx[device];
-  a.n_uops = (uint32_t)p->uops.size();
+  a.n_uops = kind_uops(p, kind);
   a.mem_size = b->mem_size;
   a.frames = b->frames;
   a.offsets = b->offsets;
@@ -1188,6 +1417,7 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* bin, const ebpf_batch_out* ou
                                           (kTraceWaves * kTraceSlots);
   }
   a.regs_out = out->regs;
+  a.xdp = xdp_direct ? 1u : 0u;
   a.init_fp = b->init_fp;
   a.init_fp_len = b->init_fp_len;
   a.fp_out = out->fp;
@@ -1219,17 +1449,18 @@ int ebpf_batch_kernel(ebpf_prog* p, const ebpf_batch* bin, const ebpf_batch_out*
   if (rc) return rc;
   rc = ebpf_prog_upload(p, device);
   if (rc) return rc;
-  ebpf_batch staged = *bin;  // xdp_md batches run as offsets + lens batches
-  if (bin->flags & EBPF_BATCH_XDP_MD) {
+  bool stk = false;
+  const int kind = batch_kind(p, bin, out, device, &stk);
+  ebpf_batch staged = *bin;  // xdp_md batches not run in place run as offsets + lens batches
+  if ((bin->flags & EBPF_BATCH_XDP_MD) &&
+      !xdp_in_place(p, bin, out->mem != nullptr, device, kind, stk)) {
     staged.offsets = (const uint32_t*)16;
     staged.lens = (const uint16_t*)16;
     staged.stride = 0;
     staged.flags &= ~EBPF_BATCH_XDP_MD;
   }
-  bool stk = false;
-  const int kind = batch_kind(p, bin, out, device, &stk);
   LaunchArgs a{};
-  a.n_uops = (uint32_t)p->uops.size();
+  a.n_uops = kind_uops(p, kind);
   a.frames = staged.frames;
   a.offsets = staged.offsets;
   a.lens = staged.lens;

@@ -335,6 +335,48 @@ __device__ __forceinline__ void dma_window_stride(const LaunchArgs& a, uint8_t* 
   }
 }
 
+// The xdp_md convention in place (xdp.rs:16-20, main.rs:14-31 handed [ctx][packet]): the lane's
+// window holds packet bytes [0, 64); make it image bytes [0, 64) = {u32 data = 8, u32 data_end =
+// 8 + len} + packet bytes [0, 56). The statement then sees the image exactly as if the packet
+// had been staged behind its ctx (its BASE is the packet - 8, its LEN 8 + len).
+// (8-byte halves, from the top down in two groups: every half is read before it is overwritten;
+// LDS operations of one wave complete in order)
+__device__ __forceinline__ void xdp_window(uint8_t* pw, uint32_t swz, uint32_t len) {
+  // (the lane's own window: no readfirstlane, unlike lds_addr)
+  const uint32_t win = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const void*)pw;
+  const uint32_t swz16 = swz << 4;
+  const uint64_t ctx = 8ull | ((uint64_t)(min(len, 0xffffu) + 8u) << 32);
+  uint32_t a0, a1, a2, a3;
+  uint64_t q0, q1, q2, q3;
+  asm volatile(
+      "v_xad_u32 %[a0], %[swz], 0, %[win]\n\t"
+      "v_xad_u32 %[a1], %[swz], 16, %[win]\n\t"
+      "v_xad_u32 %[a2], %[swz], 32, %[win]\n\t"
+      "v_xad_u32 %[a3], %[swz], 48, %[win]\n\t"
+      "ds_read_b64 %[q0], %[a3]\n\t"
+      "ds_read_b64 %[q1], %[a2] offset:8\n\t"
+      "ds_read_b64 %[q2], %[a2]\n\t"
+      "ds_read_b64 %[q3], %[a1] offset:8\n\t"
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "ds_write_b64 %[a3], %[q0] offset:8\n\t"
+      "ds_write_b64 %[a3], %[q1]\n\t"
+      "ds_write_b64 %[a2], %[q2] offset:8\n\t"
+      "ds_write_b64 %[a2], %[q3]\n\t"
+      "ds_read_b64 %[q0], %[a1]\n\t"
+      "ds_read_b64 %[q1], %[a0] offset:8\n\t"
+      "ds_read_b64 %[q2], %[a0]\n\t"
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "ds_write_b64 %[a1], %[q0] offset:8\n\t"
+      "ds_write_b64 %[a1], %[q1]\n\t"
+      "ds_write_b64 %[a0], %[q2] offset:8\n\t"
+      "ds_write_b64 %[a0], %[ctx]\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : [a0] "=&v"(a0), [a1] "=&v"(a1), [a2] "=&v"(a2), [a3] "=&v"(a3), [q0] "=&v"(q0),
+        [q1] "=&v"(q1), [q2] "=&v"(q2), [q3] "=&v"(q3)
+      : [win] "v"(win), [swz] "v"(swz16), [ctx] "v"(ctx)
+      : "memory");
+}
+
 // Synchronous per-lane staging for tiles whose packet bases are not all 16-byte aligned.
 __device__ __forceinline__ void stage_window_lane(uint8_t* pw, uint32_t swz, const uint8_t* base,
                                                   uint32_t len, bool valid) {
@@ -1349,6 +1391,7 @@ constexpr uint32_t kTileWaveLds = kWinBytes + kDagMetaBytes;  // window + metada
 #define TILE_ASM_IN \
           [ka] "s"(ka), [tile] "s"(t), [winb] "s"(winb), [metab] "s"(metab), \
           [fixed] "i"(FIXED ? 1 : 0), [loops] "i"(LOOPS ? 1 : 0), [aligned] "s"(rfl(aligned)), \
+          [o_xdp] "i"(offsetof(LaunchArgs, xdp)), \
           [o_tprog] "i"(offsetof(LaunchArgs, tprog)), \
           [o_tprog_exact] "i"(offsetof(LaunchArgs, tprog_exact)), \
           [o_maxs] "i"(offsetof(LaunchArgs, max_steps)), [o_perm] "i"(offsetof(LaunchArgs, perm)), \
@@ -1434,6 +1477,7 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
         stage_window_lane(L.win + lane * kWin, win_swz(lane), (const uint8_t*)mb,
                           valid ? ml : 0u, valid);
       }
+      if (!LOOPS && a.xdp) xdp_window(L.win + lane * kWin, win_swz(lane), ml);
       __builtin_amdgcn_s_waitcnt(0xc07f);  // the window's LDS writes / metadata reads: done
     }
     const uint64_t t = rfl64(tile);
@@ -1463,8 +1507,9 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
         uintptr_t mb;
         uint32_t ml;
         meta_of(a, L, 0, tile, ln, mb, ml);
-        const uint32_t len = ml;
-        const uint8_t* base = (const uint8_t*)mb;
+        // (xdp_md in place: the image is the packet 8 bytes further on, behind its ctx)
+        const uint32_t len = a.xdp ? min(ml, 0xffffu) + 8u : ml;
+        const uint8_t* base = (const uint8_t*)mb - (a.xdp ? 8 : 0);
         const uint32_t mem_size = a.mem_size;
         uint8_t* mo = a.mem_out + pk * (uint64_t)mem_size;
         const uint32_t m = min(len, mem_size);
@@ -1518,7 +1563,9 @@ extern "C" __global__ __launch_bounds__(kDbBlock, 1) void ebpf_tile_jit_fixed(La
   // offset, its LDS window offset and chunk swizzle -- loop-invariant
   const uint64_t dmaoff =
       (uint64_t)(lane >> 2) * a.stride + (uint64_t)(((lane & 3u) ^ ((lane >> 4) & 3u)) * 16u);
-  const uint64_t laneoff = (uint64_t)lane * a.stride;
+  // (xdp_md in place: BASE = the packet - 8, LEN = 8 + len, the ctx synthesised by the program's
+  // code, jit.cpp xdp_shift)
+  const uint64_t laneoff = (uint64_t)lane * a.stride - (a.xdp ? 8u : 0u);
   const uint32_t lane64 = lane << 6, swz = ((lane >> 2) & 3u) << 4;
   const uint64_t lanep = lane;
   const uint32_t nxa = lds_addr(&wg_counters()->next), one = 1;
@@ -1528,7 +1575,9 @@ extern "C" __global__ __launch_bounds__(kDbBlock, 1) void ebpf_tile_jit_fixed(La
   const uint32_t ntiles = rfl((uint32_t)a.n_tiles), nfull = rfl((uint32_t)(a.n / kWave));
   const uint32_t nfast = rfl(a.stride == (uint64_t)kWin ? nfull : 0u);
   const uint32_t tbytes = rfl((uint32_t)(a.stride * kWave));
-  const uint32_t lenc = rfl(a.stride >> 32 ? 0xffffffffu : (uint32_t)a.stride);
+  const uint32_t lenc = rfl(a.xdp ? (uint32_t)min(a.stride, (uint64_t)0xffff) + 8u
+                                 : a.stride >> 32 ? 0xffffffffu : (uint32_t)a.stride);
+  const uint32_t xdpf = rfl(a.xdp);
   const uint32_t kflags = rfl((a.init_regs ? 1u : 0u) | (a.r0 ? 2u : 0u) | (a.status ? 4u : 0u) |
                               (a.regs_out ? 8u : 0u));
   const uint32_t initx = rfl(kflags & 9u), oflags = rfl(kflags & 14u);
@@ -1562,7 +1611,8 @@ extern "C" __global__ __launch_bounds__(kDbBlock, 1) void ebpf_tile_jit_fixed(La
           [tbytes] "s"(tbytes), [lenc] "s"(lenc), [wx] "s"(wx),
           [dmaoff] "v"(dmaoff), [laneoff] "v"(laneoff), [lane64] "v"(lane64), [swz] "v"(swz),
           [lanep] "v"(lanep), [nxa] "v"(nxa), [one] "v"(one), [aligned] "s"(one),
-          [fixed] "i"(1), [loops] "i"(0), [o_init] "i"(offsetof(LaunchArgs, init_regs)),
+          [fixed] "i"(1), [loops] "i"(0), [xdpf] "s"(xdpf),
+          [o_init] "i"(offsetof(LaunchArgs, init_regs)),
           [o_r0] "i"(offsetof(LaunchArgs, r0)), [o_status] "i"(offsetof(LaunchArgs, status)),
           [o_regs] "i"(offsetof(LaunchArgs, regs_out))
         : TILE_ASM_CLOBBER, TILE_ASM_CLOBBER_WINDOW);

@@ -51,6 +51,7 @@ struct Marker {
   std::string fixed = "0";
   std::string loops = "0";
   std::string aligned;
+  std::string xdp;  // the SGPR holding LaunchArgs::xdp (the xdp_md convention in place)
 };
 
 bool inline_const(int64_t v) { return v >= -16 && v <= 64; }
@@ -83,6 +84,7 @@ bool find_markers(const std::string& s, std::vector<Marker>& out) {
     m.fixed = field("fixed=");
     m.loops = field("loops=");
     m.aligned = field("aligned=");
+    m.xdp = field("xdp=");
     const size_t mk = s.find(";@@JIT@@", eol);
     if (mk == std::string::npos || m.n.empty()) return false;
     const size_t ik = s.rfind(";@@JITINIT@@", pos);
@@ -2028,6 +2030,20 @@ struct Compiler {
            entry_label(P, next_start(i)) + "\n" + ok + ":\n";
   }
 
+  // The window shift of the xdp_md convention (see body): packet dwords 0..13 into v[66:79],
+  // the ctx into v[64:65] (data = 8, data_end = LEN = 8 + len), all 16 written back in place.
+  static std::string xdp_shift() {
+    std::string s;
+    for (uint32_t c = 0; c < 4; c++)
+      s += "v_xad_u32 v" + std::to_string(36 + c) + ", v35, " + std::to_string(16 * c) + ", v34\n";
+    s += "ds_read_b128 v[66:69], v36\nds_read_b128 v[70:73], v37\nds_read_b128 v[74:77], v38\n"
+         "ds_read_b64 v[78:79], v39\nv_mov_b32 v64, 8\nv_mov_b32 v65, v31\ns_waitcnt lgkmcnt(0)\n";
+    for (uint32_t c = 0; c < 4; c++)
+      s += "ds_write_b128 v" + std::to_string(36 + c) + ", v[" + std::to_string(64 + 4 * c) + ":" +
+           std::to_string(67 + 4 * c) + "]\n";
+    return s;
+  }
+
   // The program's code for the statement behind marker m. In the fixed-slot layout, a program
   // with window loads gets a second, fast copy: the window dwords it loads are read from LDS
   // once, up front (one ds_read_b128 per 16-byte chunk), and each load becomes one or two VALU
@@ -2046,6 +2062,15 @@ struct Compiler {
                                          std::to_string(kStackVgpr + j + 1) + "], 0\n"
                                    : "v_mov_b32 " + sv(j) + ", 0\n";
     }
+    // xdp_md in place (fixed-slot kernel; the other kernels shift in C++, interp.hip xdp_window):
+    // the lane's window holds packet bytes [0, 64), the program reads image bytes [0, 64) =
+    // {u32 data = 8, u32 data_end = LEN} + packet bytes [0, 56) (xdp.rs:16-20): shifted once in
+    // LDS, before any window read (LDS operations of a wave complete in order)
+    bool reads_window = false;
+    for (const Uop& o : uops) reads_window = reads_window || o.op == U_LDX;
+    if (m.fixed == "1" && reads_window && !m.xdp.empty())
+      main += "s_cmp_lg_u32 " + m.xdp + ", 0\ns_cbranch_scc0 .L" + P + "noxdp\n" + xdp_shift() +
+              ".L" + P + "noxdp:\n";
     std::string ool;
     uint32_t chunks = 0, maxend = 0;
     if (m.fixed == "1")

@@ -20,9 +20,10 @@ constexpr int kWinStride = kWin + 4;  // padded per-lane LDS stride: 17 dwords, 
 constexpr int kMaxLdsUops = 4096;     // programs up to this many micro-ops are staged in LDS
 constexpr int kCallDepth = 64;        // EBPF_MAX_CALL_DEPTH
 constexpr int kCounterShards = 64;    // device-atomic counter shards (spread contention)
-// workspace layout: [(unused) | multi-GPU counter sums u64[8] @256 | xdp_md cursor u64 @320 | length-bin counts u32[16] @384 | bin cursors
-// u32[16] @448, 512 B][shards u64[64][8]][tier-1 wave slots, or the length-binned packet order
-// u32[n]]; bin counts/cursors and shards are zero between batches
+// workspace layout: [(unused) | multi-GPU counter sums u64[8] @256 | xdp_md cursor u64 @320 |
+// length-bin counts u32[16] @384 | bin cursors u32[16] @448, 512 B][shards u64[64][8]][tier-1
+// wave slots, or the length-binned packet order u32[n]]; bin counts/cursors and shards are zero
+// between batches
 constexpr uint64_t kWsBinCountsOff = 384;
 constexpr uint64_t kWsBinCursorOff = 448;
 constexpr int kBinClasses = 16;  // packets are binned by ceil(len / 128), capped
@@ -71,6 +72,10 @@ struct LaunchArgs {
   uint32_t init_fp_len;       //   its depth (<= kCallDepth)
   uint32_t* fp_out;           // tier-1 kernel: optional [n][kCallDepth] final frame stacks
   uint8_t* fp_len_out;        //   optional [n] their depths
+  uint32_t xdp;               // 1: the xdp_md convention run in place (xdp.rs:16-20): image =
+                              //   [u32 data = 8][u32 data_end = 8 + len][packet]; the window is
+                              //   shifted by 8 bytes in LDS and the ctx synthesised per lane, BASE
+                              //   = packet - 8 and LEN = 8 + len (no staging copy)
 };
 
 constexpr int kTraceSlots = 16;

@@ -275,8 +275,58 @@ out:
     exit
 """
 
+# the 5-tuple classifier as a standard XDP program (the xdp_md calling convention, xdp.rs:16-20:
+# r1 = the ctx, packet bytes between ctx->data and ctx->data_end), with the verifier-style bounds
+# checks before the header and port reads. Same verdicts as FIVE_TUPLE on the synthetic frames
+# (their L4 ports lie inside every frame).
+FIVE_TUPLE_XDP = """
+    ldxw r2, [r1+0]           # ctx->data
+    ldxw r1, [r1+4]           # ctx->data_end
+    mov r0, 2                 # default XDP_PASS
+    mov r3, r2
+    add r3, 34
+    jgt r3, r1, out           # no Ethernet + IPv4 header
+    ldxh r3, [r2+12]          # EtherType
+    jne r3, 0x0008, out
+    ldxb r4, [r2+14]          # version / IHL
+    and r4, 0x0f
+    lsh r4, 2                 # IHL * 4
+    jlt r4, 20, drop
+    ldxb r5, [r2+23]          # protocol
+    ldxw r6, [r2+26]          # saddr
+    ldxw r7, [r2+30]          # daddr
+    mov r8, r2
+    add r8, r4                # r8 + 14 = L4 header
+    jeq r5, 1, icmp
+    mov r9, r8
+    add r9, 18
+    jgt r9, r1, out           # no L4 ports
+    jeq r5, 17, udp
+    jne r5, 6, out
+    ldxh r9, [r8+16]          # TCP dport
+    be16 r9
+    jge r9, 1024, out
+    and r6, 0xff
+    jeq r6, 10, drop
+    ja out
+udp:
+    ldxh r9, [r8+16]          # UDP dport
+    be16 r9
+    jeq r9, 53, drop
+    ja out
+icmp:
+    and r7, 0xf0
+    jeq r7, 0xe0, drop
+    ja out
+drop:
+    mov r0, 1                 # XDP_DROP
+out:
+    exit
+"""
+
 PROGRAMS = {"drop": DROP_ALL, "5tuple": FIVE_TUPLE, "checksum": CHECKSUM,
-            "5tuple_stack": FIVE_TUPLE_STACK, "mac_swap_tx": MAC_SWAP_TX, "acl": ACL}
+            "5tuple_stack": FIVE_TUPLE_STACK, "mac_swap_tx": MAC_SWAP_TX, "acl": ACL,
+            "5tuple_xdp": FIVE_TUPLE_XDP}
 
 
 def program(name: str) -> bytes:

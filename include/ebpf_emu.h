@@ -76,8 +76,11 @@ typedef struct ihipStream_t* ebpf_stream_t; /* == hipStream_t */
  * data_end = 8 + len at image offsets 0 and 4, the packet at offset 8, so r1 (= 0) is the ctx
  * pointer, standard XDP programs run unchanged, and r2 = 8 + len (main.rs:18-29 gives r2 the
  * image length). This is exactly the image the reference executes when main.rs is handed the
- * ctx-prefixed bytes. The library stages the images in the workspace (a device copy of the
- * packets), then runs the batch as usual. Requires mem_size <= 65528. */
+ * ctx-prefixed bytes. The compiled forward kernels (and the tile interpreter on offsets / lens
+ * layouts) run such a batch in place: the ctx is synthesised in each packet's LDS window and the
+ * packet read 8 bytes further on, with no extra pass over the frames. Other kernels (loop
+ * programs, the general interpreter) run images the library stages in the workspace first.
+ * Requires mem_size <= 65528. */
 #define EBPF_BATCH_XDP_MD  2u
 /* ebpf_batch.flags: run a compiled program (ebpf_prog_compile) on the tile interpreter instead
  * (differential testing; results are identical by contract). */

@@ -362,14 +362,25 @@ typedef struct {
   uint64_t* r0_out;
   uint8_t* status_out;
   uint64_t counters[8];
+  int xdp; /* the xdp_md convention: image = [u32 8][u32 8 + len][packet] (xdp.rs:16-20) */
 } batch_job;
 
 static void* batch_worker(void* arg) {
   batch_job* j = (batch_job*)arg;
   uint64_t cnt[8] = {0}; /* thread-local: the jobs share cache lines */
+  uint8_t* img = j->xdp ? (uint8_t*)malloc(8 + 0xFFFF) : NULL;
   for (uint64_t i = j->lo; i < j->hi; i++) {
     const uint8_t* p = j->frames + (j->offsets ? (uint64_t)j->offsets[i] : i * j->stride);
     size_t len = j->lens ? j->lens[i] : (size_t)j->stride;
+    if (img) { /* the bytes main.rs is handed for an XDP program: ctx, then the packet */
+      if (len > 0xFFFF) len = 0xFFFF;
+      const uint32_t data = 8, data_end = (uint32_t)(8 + len);
+      memcpy(img, &data, 4);
+      memcpy(img + 4, &data_end, 4);
+      if (len + 8 <= j->mem_size) memcpy(img + 8, p, len); /* (else ST_BADPKT from the length) */
+      p = img;
+      len += 8;
+    }
     uint64_t r0 = 0, steps = 0;
     int st = or_run_packet(j->prog, j->n, p, len, j->mem_size, j->r10, j->max_steps, &r0, &steps);
     if (j->r0_out) j->r0_out[i] = r0;
@@ -380,6 +391,7 @@ static void* batch_worker(void* arg) {
     cnt[7] += steps;
   }
   memcpy(j->counters, cnt, sizeof cnt);
+  free(img);
   return NULL;
 }
 
@@ -387,6 +399,14 @@ int or_run_batch(const or_insn* prog, size_t n, const uint8_t* frames, const uin
                  const uint16_t* lens, uint64_t stride, uint64_t npkts, size_t mem_size,
                  uint64_t r10_init, uint64_t max_steps, uint64_t* r0_out, uint8_t* status_out,
                  uint64_t counters[8], int threads) {
+  return or_run_batch_xdp(prog, n, frames, offsets, lens, stride, npkts, mem_size, r10_init,
+                          max_steps, r0_out, status_out, counters, threads, 0);
+}
+
+int or_run_batch_xdp(const or_insn* prog, size_t n, const uint8_t* frames,
+                     const uint32_t* offsets, const uint16_t* lens, uint64_t stride, uint64_t npkts,
+                     size_t mem_size, uint64_t r10_init, uint64_t max_steps, uint64_t* r0_out,
+                     uint8_t* status_out, uint64_t counters[8], int threads, int xdp) {
   if (threads < 1) threads = 1;
   if (threads > 256) threads = 256;
   batch_job jobs[256];
@@ -396,7 +416,7 @@ int or_run_batch(const or_insn* prog, size_t n, const uint8_t* frames, const uin
     memset(j, 0, sizeof *j);
     j->prog = prog; j->n = n; j->frames = frames; j->offsets = offsets; j->lens = lens;
     j->stride = stride; j->mem_size = mem_size; j->r10 = r10_init; j->max_steps = max_steps;
-    j->r0_out = r0_out; j->status_out = status_out;
+    j->r0_out = r0_out; j->status_out = status_out; j->xdp = xdp;
     j->lo = npkts * (uint64_t)t / (uint64_t)threads;
     j->hi = npkts * (uint64_t)(t + 1) / (uint64_t)threads;
   }

@@ -97,6 +97,12 @@ int or_run_batch(const or_insn* prog, size_t n, const uint8_t* frames, const uin
                  const uint16_t* lens, uint64_t stride, uint64_t npkts, size_t mem_size,
                  uint64_t r10_init, uint64_t max_steps, uint64_t* r0_out, uint8_t* status_out,
                  uint64_t counters[8], int threads);
+/* The same with xdp != 0: each packet runs as the xdp_md image [u32 data = 8][u32 data_end =
+ * 8 + len][packet] (xdp.rs:16-20) handed to main.rs (r2 = 8 + len, main.rs:18-29). */
+int or_run_batch_xdp(const or_insn* prog, size_t n, const uint8_t* frames,
+                     const uint32_t* offsets, const uint16_t* lens, uint64_t stride, uint64_t npkts,
+                     size_t mem_size, uint64_t r10_init, uint64_t max_steps, uint64_t* r0_out,
+                     uint8_t* status_out, uint64_t counters[8], int threads, int xdp);
 
 #ifdef __cplusplus
 }

@@ -55,6 +55,8 @@ def lib():
                                    ctypes.c_uint64, ctypes.c_size_t, ctypes.c_uint64,
                                    ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
                                    ctypes.c_void_p, ctypes.c_int]
+        L.or_run_batch_xdp.restype = ctypes.c_int
+        L.or_run_batch_xdp.argtypes = L.or_run_batch.argtypes + [ctypes.c_int]
     return _LIB
 
 
@@ -129,8 +131,10 @@ class Program:
                 [int(f[i]) for i in range(fl.value)], steps.value)
 
     def run_batch(self, frames: np.ndarray, n: int, stride: int = 0, offsets=None, lens=None,
-                  mem_size: int = 1024, r10: int = 512, max_steps: int = 0, threads: int = 1):
-        """-> (r0 u64[n], status u8[n], counters u64[8])"""
+                  mem_size: int = 1024, r10: int = 512, max_steps: int = 0, threads: int = 1,
+                  xdp_md: bool = False):
+        """-> (r0 u64[n], status u8[n], counters u64[8]). xdp_md: each packet runs as the
+        image [u32 8][u32 8 + len][packet] (the xdp_md calling convention, xdp.rs:16-20)."""
         frames = np.ascontiguousarray(frames, dtype=np.uint8)
         r0 = np.zeros(n, dtype=np.uint64)
         status = np.zeros(n, dtype=np.uint8)
@@ -143,7 +147,7 @@ class Program:
         if lens is not None:
             lens = np.ascontiguousarray(lens, dtype=np.uint16)
             len_p = lens.ctypes.data
-        lib().or_run_batch(self.insns, self.n, frames.ctypes.data, off_p, len_p, stride, n,
-                           mem_size, r10, max_steps, r0.ctypes.data, status.ctypes.data,
-                           counters.ctypes.data, threads)
+        lib().or_run_batch_xdp(self.insns, self.n, frames.ctypes.data, off_p, len_p, stride, n,
+                               mem_size, r10, max_steps, r0.ctypes.data, status.ctypes.data,
+                               counters.ctypes.data, threads, 1 if xdp_md else 0)
         return r0, status, counters

@@ -197,3 +197,39 @@ def gen_stack_program(rng: random.Random, n: int | None = None, k: int = 32,
             words.append(encode(0x95))
     words.append(encode(0x95))
     return b"".join(words)
+
+
+def gen_call_program(rng: random.Random, n: int | None = None, loops: bool = False) -> bytes:
+    """Tier-0 programs with local calls (emu.rs:265-279: CALL jumps to t = pc + 1 + off and
+    pushes t + 1, EXIT pops or stops): calls forward and backward, EXITs along the way, forward
+    jumps (and with loops=True a few backward ones), packet loads and ALU ops. Some recurse (the
+    frame stack grows until ST_CALLDEPTH or the budget), most reach a few frame stacks."""
+    n = n or rng.randrange(6, 30)
+    words: list[bytes] = []
+    while len(words) < n:
+        k = rng.random()
+        pos = len(words)
+        dst, src = rng.randrange(10), rng.randrange(10)
+        if k < 0.16:  # CALL, mostly to a later instruction
+            lo = -pos - 1 if rng.random() < 0.25 else 0
+            words.append(encode(0x85, 0, 0, rng.randrange(lo, max(1, n - pos))))
+        elif k < 0.27:
+            words.append(encode(0x95))
+        elif k < 0.55:
+            cls = rng.choice([0x04, 0x07])
+            op = rng.choice([0, 1, 2, 4, 5, 6, 7, 10, 11, 12])
+            words.append(encode((op << 4) | rng.choice([0, 0x08]) | cls, dst, src, 0, _imm(rng)))
+        elif k < 0.70:
+            cls = rng.choice([0x05, 0x06])
+            op = rng.choice([1, 2, 3, 4, 5, 6, 7, 10, 11, 12, 13])
+            off = rng.randrange(0, max(1, n - pos) + 1)
+            if loops and rng.random() < 0.15:
+                off = -rng.randrange(1, 4)
+            words.append(encode((op << 4) | rng.choice([0, 0x08]) | cls, dst, src, off, _imm(rng)))
+        elif k < 0.85:
+            size = rng.choice([0x00, 0x08, 0x10, 0x18])
+            words.append(encode(0x61 | size, dst, 1, rng.randrange(0, 70)))
+        else:
+            words.append(encode(0xB7 | rng.choice([0, 0x08]), dst, src, 0, _imm(rng)))
+    words.append(encode(0x95))
+    return b"".join(words)

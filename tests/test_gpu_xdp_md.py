@@ -143,3 +143,135 @@ def test_xdp_md_production_outputs(cuda, oracle_mod, layout, src):
     assert list(cnt.cpu().numpy().view(np.uint64)) == list(want)
     assert (status == 7).sum() == sum(len(p) + 8 > 1024 for p in pkts)  # ST_BADPKT
     prog.close()
+
+
+# ctx and packet bytes mixed in one access, reads past the 64-byte window and across its end, a
+# register address from r2 (= data_end in the main.rs layout of an xdp_md image)
+XDP_CTX_MIX = """
+    ldxdw r3, [r1+0]          # data | data_end << 32
+    ldxdw r4, [r1+4]          # data_end | packet bytes 0..3 << 32
+    ldxw r5, [r1+6]           # ctx and packet bytes in one word
+    mov r0, r3
+    xor r0, r4
+    add r0, r5
+    ldxb r6, [r1+70]          # packet byte 62: past the window
+    add r0, r6
+    ldxw r7, [r1+60]          # across the window's end
+    xor r0, r7
+    mov r8, r1
+    add r8, r2
+    ldxb r9, [r8-1]           # the last packet byte, register address
+    lsh r9, 8
+    add r0, r9
+    ldxh r9, [r3+4]           # packet bytes 4..5 through r3 = data (its low word)
+    xor r0, r9
+    exit
+"""
+
+
+def _route(prog, frames, kw, **extra):
+    return prog.batch_kernel(prog.make_batch(frames, xdp_md=True, **kw, **extra))
+
+
+@pytest.mark.parametrize("stride,mem", [(64, 1024), (96, 1024), (64, 72), (64, 71), (128, 100)])
+def test_xdp_md_fixed_slots_in_place(cuda, oracle_mod, stride, mem):
+    """Fixed slots (no lengths: every packet `stride` bytes): the compiled fixed-slot kernel runs
+    the xdp_md batch in place (the ctx synthesised in its LDS window, no staging kernel); every
+    output against the oracle on the ctx-prefixed images, and against the staged general
+    interpreter. Images of exactly mem_size bytes, and one byte past it (ST_BADPKT)."""
+    import torch
+
+    from ebpf_emu import Program, _lib
+    from ebpf_emu import workloads as W
+    from ebpf_emu.asm import assemble
+
+    n = 777
+    buf = W.frames_fixed(n, stride, 3)
+    frames = torch.from_numpy(buf).to(cuda)
+    pkts = [bytes(buf[i * stride:(i + 1) * stride]) for i in range(n)]
+    for src in (XDP_PARSE, W.FIVE_TUPLE_XDP, XDP_CTX_MIX):
+        img = assemble(src)
+        prog = Program(img)
+        assert prog.compile()
+        assert _route(prog, frames, dict(n=n, stride=stride), mem_size=mem) == \
+            _lib.EBPF_KERNEL_JIT_FIXED
+        cnt = torch.zeros(8, dtype=torch.int64, device=cuda)
+        v = prog.run(frames, n=n, stride=stride, mem_size=mem, counters=cnt, xdp_md=True)
+        rs = prog.run(frames, n=n, stride=stride, mem_size=mem, verdict=False, r0=True,
+                      status=True, xdp_md=True)
+        full = prog.run(frames, n=n, stride=stride, mem_size=mem, r0=True, status=True,
+                        regs=True, xdp_md=True)
+        gen = prog.run(frames, n=n, stride=stride, mem_size=mem, r0=True, status=True,
+                       regs=True, xdp_md=True, generic=True)
+        torch.cuda.synchronize()
+        r0, st, ocnt = oracle_mod.Program(img).run_batch(buf, n, stride=stride, mem_size=mem,
+                                                         xdp_md=True, threads=4)
+        assert np.array_equal(rs.status.cpu().numpy(), st), src[:30]
+        ok = st == 0
+        assert np.array_equal(rs.r0.cpu().numpy().view(np.uint64)[ok], r0[ok])
+        want_v = np.where(st != 0, 0xFF, np.where(r0 < 5, r0, 0xFE)).astype(np.uint8)
+        assert np.array_equal(v.verdict.cpu().numpy(), want_v)
+        assert list(cnt.cpu().numpy().view(np.uint64)) == list(ocnt)
+        for k in ("r0", "status", "regs"):
+            assert torch.equal(getattr(full, k), getattr(gen, k)), (k, src[:30])
+        for i in range(0, n, 97):  # every register of a sample against the oracle
+            ost, oregs, _, _ = oracle_mod.Program(img).run_full(
+                struct.pack("<II", 8, 8 + stride) + pkts[i], mem, 512, 1 << 22)
+            assert ost == st[i]
+            if ost == 0:
+                assert [int(x) for x in full.regs[i].cpu().numpy().view(np.uint64)] == oregs
+        prog.close()
+
+
+@pytest.mark.parametrize("layout", [dict(), dict(offsets_layout=True, align=16),
+                                    dict(offsets_layout=True, misalign=3)])
+def test_xdp_md_var_in_place(cuda, oracle_mod, layout):
+    """Offsets + lens and stride + lens layouts: the compiled var kernel runs the batch in place
+    (window shifted in LDS by the C++ prologue), the final images included; against the oracle
+    and the staged general interpreter."""
+    import torch
+
+    from ebpf_emu import Program, _lib
+    from ebpf_emu.asm import assemble
+
+    rng = random.Random(23)
+    pkts = _xdp_packets(rng, 260)
+    for src in (XDP_PARSE, XDP_CTX_MIX):
+        img = assemble(src)
+        prog = Program(img)
+        frames, kw = _stage(pkts, cuda, **layout)
+        assert _route(prog, frames, kw) == _lib.EBPF_KERNEL_JIT_VAR
+        full = prog.run(frames, r0=True, status=True, regs=True, mem=True, xdp_md=True, **kw)
+        gen = prog.run(frames, r0=True, status=True, regs=True, mem=True, xdp_md=True,
+                       generic=True, **kw)
+        torch.cuda.synchronize()
+        for k in ("r0", "status", "regs"):
+            assert torch.equal(getattr(full, k), getattr(gen, k)), (k, src[:30], layout)
+        # (the final image of a packet too long for it, ST_BADPKT, is not defined: the reference
+        # panics before it has one, main.rs:20-21)
+        ok = full.status == 0
+        assert torch.equal(full.mem[ok], gen.mem[ok]), (src[:30], layout)
+        op = oracle_mod.Program(img)
+        status = full.status.cpu().numpy()
+        for i, im in enumerate(_images(pkts)):
+            st, oregs, omem, _ = op.run_full(im, 1024, 512, 1 << 22)
+            assert status[i] == st, i
+            if st == 0:
+                assert [int(x) for x in full.regs[i].cpu().numpy().view(np.uint64)] == oregs
+                assert bytes(full.mem[i].cpu().numpy()) == omem
+        prog.close()
+
+
+def test_xdp_md_loop_programs_staged(cuda):
+    """Loop programs still run the staged images (their window refills read packet bytes by
+    image address): the route is the compiled loop kernel."""
+    import torch
+
+    from ebpf_emu import Program, _lib
+    from ebpf_emu.asm import assemble
+
+    prog = Program(assemble(XDP_SUM))
+    frames, kw = _stage([bytes(100)] * 70, cuda)
+    assert _route(prog, frames, kw) == _lib.EBPF_KERNEL_JIT_LOOP
+    prog.close()
+    del torch

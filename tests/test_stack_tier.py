@@ -43,7 +43,7 @@ DIRECTED = [
     ("lock fetch add32 [r10-8], r2\nexit", 8),
     ("lock add [r10-6], r2\nexit", 0),                             # misaligned atomic
     ("lock add [r1+8], r2\nexit", 0),                              # an atomic on the packet
-    ("stxdw [r10-8], r1\ncall 0\nexit", 0),                        # calls
+    ("stxdw [r10-8], r1\ncall 0\nexit", 8),                        # calls (flatten_calls)
     ("mov r0, 0\nstxb [r10-1], r0\nadd r0, 1\njlt r0, 5, -3\nexit", 0),  # a loop
     ("mov32 r2, r10\nstxb [r2-1], r0\nexit", 0),                   # a truncated pointer
     ("mov r0, 1\nexit", 0),                                        # no store: tier 0
