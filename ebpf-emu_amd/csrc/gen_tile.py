@@ -1535,6 +1535,13 @@ def main():
     with open(os.path.join(HERE, "tile_jit.inc"), "w") as f:
         f.write("// GENERATED by gen_tile.py -- do not edit. The JIT template kernel's statement.\n"
                 "// clang-format off\n" + cstr(text) + "\n// clang-format on\n")
+    # the var kernel's statement for stack-window programs (memory tier 0.5 on offsets / lens and
+    # xdp_md layouts: ebpf_tile_jit_var_stack, whose statement also owns v[64:95])
+    text = F(JIT_STATEMENT).replace("aligned=%[aligned]\n", "aligned=%[aligned] stack=1\n")
+    assert "stack=1" in text
+    with open(os.path.join(HERE, "tile_jit_stack.inc"), "w") as f:
+        f.write("// GENERATED by gen_tile.py -- do not edit. The JIT template kernel's statement for "
+                "stack-window programs.\n// clang-format off\n" + cstr(text) + "\n// clang-format on\n")
     # the compiled fixed-slot kernel's tile loop (jit_statement_loop)
     text = F(jit_statement_loop())
     assert "{" not in text, "unsubstituted register name: " + text[text.index("{"):][:40]

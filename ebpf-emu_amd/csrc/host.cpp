@@ -1185,10 +1185,22 @@ static int batch_tier(const ebpf_prog* p, const ebpf_batch* b) {
 static bool stack_launch_ok(const ebpf_prog* p, const ebpf_batch* b, const ebpf_batch_out* out,
                             int device) {
   if (!p->stack.k || !p->jit_mod[device][1]) return false;
-  if (b->flags & (EBPF_BATCH_GENERIC | EBPF_BATCH_NO_JIT | EBPF_BATCH_XDP_MD)) return false;
+  if (b->flags & (EBPF_BATCH_GENERIC | EBPF_BATCH_NO_JIT)) return false;
   if (b->init_regs || b->init_fp_len || out->mem || b->max_steps < p->xuops.size()) return false;
   const uint64_t k = p->stack.k, r10 = b->r10;
-  if (r10 % 4 || r10 < k || r10 > b->mem_size || r10 - k < b->stride) return false;
+  if (r10 % 4 || r10 < k || r10 > b->mem_size) return false;
+  LaunchArgs la{};
+  la.frames = b->frames;
+  la.offsets = b->offsets;
+  la.lens = b->lens;
+  la.stride = b->stride;
+  la.mem_out = out->mem;
+  const bool fixed = launch_fixed_layout(la);
+  // fixed slots: the window lies past every packet byte (it starts as zeros); other layouts
+  // (ebpf_tile_jit_var_stack): lanes whose packet reaches into it load those bytes at the start,
+  // which needs the window past the header window (and the xdp_md ctx)
+  const uint64_t img_len = b->stride + ((b->flags & EBPF_BATCH_XDP_MD) ? 8 : 0);
+  if (fixed ? r10 - k < img_len : r10 - k < (uint64_t)kWin) return false;
   for (const auto& kl : p->kloads) {
     if (kl.first < r10 && kl.first + kl.second > r10 - k) return false;
     // packet-window stores: the compiled code has only the copy whose window loads read the
@@ -1197,13 +1209,7 @@ static bool stack_launch_ok(const ebpf_prog* p, const ebpf_batch* b, const ebpf_
         kl.first + kl.second > b->mem_size)
       return false;
   }
-  LaunchArgs a{};
-  a.frames = b->frames;
-  a.offsets = b->offsets;
-  a.lens = b->lens;
-  a.stride = b->stride;
-  a.mem_out = out->mem;
-  return launch_fixed_layout(a);
+  return true;
 }
 
 // The kernel kind of a batch (uploaded program): dag_kernel needs no step budget (a lane of a
@@ -1250,7 +1256,7 @@ static const bool g_xdp_stage = [] {
 
 static bool xdp_in_place(ebpf_prog* p, const ebpf_batch* b, bool mem_out, int device, int kind,
                          bool stk) {
-  if (!(b->flags & EBPF_BATCH_XDP_MD) || g_xdp_stage || stk || kind != kKindDag) return false;
+  if (!(b->flags & EBPF_BATCH_XDP_MD) || g_xdp_stage || kind != kKindDag) return false;
   LaunchArgs a{};
   a.n_uops = kind_uops(p, kind);
   a.frames = b->frames;
@@ -1259,8 +1265,9 @@ static bool xdp_in_place(ebpf_prog* p, const ebpf_batch* b, bool mem_out, int de
   a.stride = b->stride;
   a.n_tiles = (b->n + 63) / 64;
   a.mem_out = mem_out ? (uint8_t*)16 : nullptr;
-  const int id = launch_kernel_id(kind, a, batch_jit(p, b, kind, stk, device), false);
+  const int id = launch_kernel_id(kind, a, batch_jit(p, b, kind, stk, device), stk);
   return id == EBPF_KERNEL_JIT_FIXED || id == EBPF_KERNEL_JIT_VAR ||
+         id == EBPF_KERNEL_JIT_STACK || id == EBPF_KERNEL_JIT_VAR_STACK ||
          (id == EBPF_KERNEL_TILE && !launch_fixed_layout(a));
 }
 
@@ -1438,7 +1445,7 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* bin, const ebpf_batch_out* ou
     }
   }
   const JitFns* jit = batch_jit(p, b, kind, stk, device);
-  hipError_t e = launch_interp(kind, a, grid, s, jit);
+  hipError_t e = launch_interp(kind, a, grid, s, jit, stk);
   if (cur != device) hipSetDevice(cur);
   return e == hipSuccess ? EBPF_OK : EBPF_EHIP;
 }

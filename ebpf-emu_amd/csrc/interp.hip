@@ -1420,7 +1420,9 @@ constexpr uint32_t kTileWaveLds = kWinBytes + kDagMetaBytes;  // window + metada
 // next tile's DMA in flight while the current one runs).
 constexpr uint32_t kTileWaveLdsDb = 2 * kWinBytes;
 
-template <bool FIXED, bool LOOPS, bool JIT>
+// STACK (with JIT, !FIXED, !LOOPS): the statement of stack-window programs, which also owns
+// v[64:95] (the preloaded header window and the stack window, jit.cpp body)
+template <bool FIXED, bool LOOPS, bool JIT, bool STACK = false>
 __device__ __forceinline__ void tile_body(LaunchArgs& a) {
   constexpr uint32_t WPB = kWavesPerBlock;
   counters_init();
@@ -1487,6 +1489,10 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
       asm volatile(
 #include "tile_jit.inc"
           TILE_ASM_OPERANDS, TILE_ASM_CLOBBER_PREFETCH);
+    } else if constexpr (JIT && STACK) {
+      asm volatile(
+#include "tile_jit_stack.inc"
+          TILE_ASM_OPERANDS, TILE_ASM_CLOBBER_WINDOW);
     } else if constexpr (JIT) {
       asm volatile(
 #include "tile_jit.inc"
@@ -1654,6 +1660,11 @@ extern "C" __global__ __launch_bounds__(kDbBlock, 1) void ebpf_tile_jit_fixed(La
 }
 extern "C" __global__ __launch_bounds__(kBlock, 7) void ebpf_tile_jit_var(LaunchArgs a) {
   tile_body<false, false, true>(a);
+}
+// stack-window programs (memory tier 0.5) on offsets + lens, stride + lens and xdp_md batches:
+// the var kernel with the preloaded header window and the stack window in v[64:95]
+extern "C" __global__ __launch_bounds__(kBlock, 4) void ebpf_tile_jit_var_stack(LaunchArgs a) {
+  tile_body<false, false, true, true>(a);
 }
 // loop programs (back edges, or a step budget that can bind): the exact budget and refillable
 // windows as tile_kernel<false, true>
@@ -1875,7 +1886,7 @@ int launch_kernel_id(int kind, const LaunchArgs& a, const JitFns* jit, bool stac
   if (jit && jit->loop && kind == kKindLoop) return EBPF_KERNEL_JIT_LOOP;
   if (jit && jit->fixed && jit_forward_for(kind, a.n_uops))
     return jit_fixed_layout(&a) ? (stack ? EBPF_KERNEL_JIT_STACK : EBPF_KERNEL_JIT_FIXED)
-                            : EBPF_KERNEL_JIT_VAR;
+                                : (stack ? EBPF_KERNEL_JIT_VAR_STACK : EBPF_KERNEL_JIT_VAR);
   if (kind == kKindDag)
     return tile_kernel_for(kind, a.n_uops) ? EBPF_KERNEL_TILE : EBPF_KERNEL_DAG;
   if (kind == kKindLoop) return EBPF_KERNEL_TILE_LOOP;
@@ -1883,7 +1894,7 @@ int launch_kernel_id(int kind, const LaunchArgs& a, const JitFns* jit, bool stac
 }
 
 hipError_t launch_interp(int kind, const LaunchArgs& a, int grid, hipStream_t stream,
-                         const JitFns* jit) {
+                         const JitFns* jit, bool stack) {
   const uint32_t lds = lds_bytes_for(kind, a.n_uops);
   LaunchArgs b = a;
   // a shard word's sum must stay below 2^48: bound it by packets x steps per packet; and its
@@ -1906,7 +1917,8 @@ hipError_t launch_interp(int kind, const LaunchArgs& a, int grid, hipStream_t st
                                 kDbBlock, 1, 1, dlds, stream, bargs, nullptr);
     } else {  // (the tile kernel's window LDS, also for programs past kTileMaxUops)
       const uint32_t vlds = g_lds_pad + kWavesPerBlock * kTileWaveLds;
-      e = hipModuleLaunchKernel(jit->var, grid, 1, 1, kBlock, 1, 1, vlds, stream, bargs, nullptr);
+      e = hipModuleLaunchKernel(stack ? jit->var_stack : jit->var, grid, 1, 1, kBlock, 1, 1, vlds,
+                                stream, bargs, nullptr);
     }
   } else
     e = hipLaunchKernel(kernel_for(kind, a.n_uops, &a), dim3(grid), dim3(kBlock), bargs, lds,

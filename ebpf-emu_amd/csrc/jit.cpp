@@ -52,6 +52,7 @@ struct Marker {
   std::string loops = "0";
   std::string aligned;
   std::string xdp;  // the SGPR holding LaunchArgs::xdp (the xdp_md convention in place)
+  bool stack = false;  // the var kernel's statement for stack-window programs
 };
 
 bool inline_const(int64_t v) { return v >= -16 && v <= 64; }
@@ -85,6 +86,7 @@ bool find_markers(const std::string& s, std::vector<Marker>& out) {
     m.loops = field("loops=");
     m.aligned = field("aligned=");
     m.xdp = field("xdp=");
+    m.stack = field("stack=") == "1";
     const size_t mk = s.find(";@@JIT@@", eol);
     if (mk == std::string::npos || m.n.empty()) return false;
     const size_t ik = s.rfind(";@@JITINIT@@", pos);
@@ -1531,7 +1533,10 @@ struct Compiler {
   // a < mem (64-bit, so a nonzero high word fails) and a + width <= mem; window accesses read the
   // one to three dwords they span (ds_read_u8 for one byte); accesses past the window read the
   // packet's dwords from HBM (zeros past its end) out of line.
-  std::string ldx_fixed(uint32_t i, bool one, const std::string& P, std::string& ool) const {
+  // var (the var kernel's stack statement): packets of any length, so the bytes at or past LEN
+  // read as zero (main.rs:16) -- masked after either path, before the stack overlay.
+  std::string ldx_fixed(uint32_t i, bool one, const std::string& P, std::string& ool,
+                        bool var = false) const {
     const TUop& u = t[i];
     const uint32_t w = one ? 1u : u.width;
     const std::string U = P + "u" + std::to_string(i), next = entry_label(P, next_start(i));
@@ -1577,6 +1582,11 @@ struct Compiler {
       if (w == 8) win += "v_alignbyte_b32 v27, v51, v50, v36\n";
     }
     s += win + ".Lmrg" + U + ":\n";
+    if (var)  // the valid bytes: min(8, LEN - a) (0 when a >= LEN), the rest shifted out
+      s += std::string(w <= 4 ? "v_mov_b32 v27, 0\n" : "") +
+           "v_sub_u32 v46, v31, v36\nv_cmp_lt_u32 vcc, v36, v31\nv_cndmask_b32 v46, 0, v46, vcc\n"
+           "v_min_u32 v46, 8, v46\nv_lshlrev_b32 v46, 3, v46\nv_sub_u32 v46, 64, v46\n"
+           "v_lshlrev_b64 v[26:27], v46, v[26:27]\nv_lshrrev_b64 v[26:27], v46, v[26:27]\n";
     if (stk) s += stack_overlay(U, w, ool);
     if (w == 1 || w == 2)
       s += "s_mov_b32 s42, " + std::string(w == 1 ? "0xff" : "0xffff") + "\nv_bfi_b32 " + D0 +
@@ -1984,10 +1994,10 @@ struct Compiler {
       main += ldxk_fast(i);
       return true;
     }
-    if (!loops && m.fixed == "1" &&
+    if (!loops && (m.fixed == "1" || m.stack) &&
         (id == T_LDX_C || id == T_LDX_E || id == T_LDX1_C || id == T_LDX1_E)) {
       std::string ot;
-      main += ldx_fixed(i, id == T_LDX1_C || id == T_LDX1_E, P, ot);
+      main += ldx_fixed(i, id == T_LDX1_C || id == T_LDX1_E, P, ot, m.stack);
       ool += ot;
       return true;
     }
@@ -2072,8 +2082,24 @@ struct Compiler {
       main += "s_cmp_lg_u32 " + m.xdp + ", 0\ns_cbranch_scc0 .L" + P + "noxdp\n" + xdp_shift() +
               ".L" + P + "noxdp:\n";
     std::string ool;
+    if (stk && m.stack) {  // (var layouts: lanes whose packet reaches into the window take its
+                           // bytes there, byte by byte, out of line; the launch checked S0 >= 64)
+      main += "v_cmp_lt_u32 vcc, s57, v31\ns_cbranch_vccnz .L" + P + "skinit\n.L" + P +
+              "skdone:\n";
+      ool += ".L" + P + "skinit:\ns_mov_b64 s[66:67], exec\ns_mov_b64 s[68:69], vcc\n";
+      for (uint32_t b = 0; b < stk->k; b++) {
+        const std::string L = ".L" + P + "sk" + std::to_string(b);
+        ool += "s_mov_b64 exec, s[68:69]\nv_add_u32_e64 v36, s57, " + std::to_string(b) +
+               "\nv_cmp_gt_u32 vcc, v31, v36\ns_and_b64 exec, exec, vcc\ns_cbranch_execz " + L +
+               "\nv_mov_b32 v37, 0\nv_lshl_add_u64 v[38:39], v[32:33], 0, v[36:37]\n"
+               "global_load_ubyte v40, v[38:39], off\ns_waitcnt vmcnt(0)\n"
+               "v_lshl_or_b32 " + sv(b / 4) + ", v40, " + std::to_string(8 * (b % 4)) + ", " +
+               sv(b / 4) + "\n" + L + ":\n";
+      }
+      ool += "s_mov_b64 exec, s[66:67]\ns_branch .L" + P + "skdone\n";
+    }
     uint32_t chunks = 0, maxend = 0;
-    if (m.fixed == "1")
+    if (m.fixed == "1" || m.stack)
       for (uint32_t i = 0; i < n; i++) {
         const TUop& u = t[i];
         if (!is_ldxk(u.hoff / TILE_SLOT)) continue;
@@ -2084,7 +2110,7 @@ struct Compiler {
       }
     // packet-window stores merge into the preloaded dwords; such programs have only the fast
     // copy (the launch checks mem_size >= every window load's end, host.cpp stack_launch_ok)
-    const bool pw = stk && stk->any_pw && m.fixed == "1";
+    const bool pw = stk && stk->any_pw && (m.fixed == "1" || m.stack);
     for (uint32_t i = 0; pw && i < n; i++)
       if (stk->pw[i] != kNoStack)
         for (uint32_t b = (uint32_t)stk->pw[i]; b < (uint32_t)stk->pw[i] + uops[i].aux; b++)
@@ -2098,7 +2124,21 @@ struct Compiler {
         if (chunks & (1u << c))
           main += "v_xad_u32 v36, v35, " + std::to_string(16 * c) + ", v34\nds_read_b128 v[" +
                   std::to_string(64 + 4 * c) + ":" + std::to_string(67 + 4 * c) + "], v36\n";
-      main += "s_waitcnt lgkmcnt(0)\ns_mov_b64 exec, 0\n";
+      main += "s_waitcnt lgkmcnt(0)\n";
+      if (m.stack) {  // var layouts: the preloaded bytes at or past LEN are zeros (main.rs:16),
+                      // skipped when every lane's packet covers the window
+        const std::string D = ".L" + F + "pmd";
+        main += "v_cmp_gt_u32 vcc, 64, v31\ns_cbranch_vccz " + D + "\n";
+        for (uint32_t j = 0; j < 16; j++)
+          if (chunks & (1u << (j >> 2)))
+            main += "v_subrev_u32 v36, " + std::to_string(4 * j) + ", v31\n"
+                    "v_med3_i32 v36, v36, 0, 4\nv_lshlrev_b32 v36, 3, v36\n"
+                    "v_lshlrev_b64 v[36:37], v36, 1\nv_add_u32 v36, -1, v36\n"
+                    "v_and_b32 v" + std::to_string(64 + j) + ", v36, v" + std::to_string(64 + j) +
+                    "\n";
+        main += D + ":\n";
+      }
+      main += "s_mov_b64 exec, 0\n";
       if (!copy(m, F, true, main, ool)) return false;
       main += "s_branch .L" + P + "end\n" + (pw ? "" : ".L" + P + "slow:\n");
     }
@@ -2304,7 +2344,9 @@ bool compile_into_template(Compiler& c, Compiler* xc, std::vector<char>& code_ob
     std::string b;
     const bool loop_marker = m.loops == "1";
     bool ok = true;
-    if (loop_marker != (xc != nullptr) || (c.stk && m.fixed != "1"))
+    // (stack-window programs: the fixed-slot kernel and the var kernel's stack statement; other
+    // programs: every statement but that one)
+    if (loop_marker != (xc != nullptr) || (c.stk ? !(m.fixed == "1" || m.stack) : m.stack))
       b = "s_mov_b64 exec, 0  ; (not this program's kernel)\n";
     else
       ok = xc ? c.body_loop(m, *xc, b) : c.body(m, b);
@@ -2357,7 +2399,8 @@ bool jit_load(const std::vector<char>& co, hipModule_t* mod, JitFns* fns) {
   JitFns f;
   if (hipModuleGetFunction(&f.fixed, m, "ebpf_tile_jit_fixed") != hipSuccess ||
       hipModuleGetFunction(&f.var, m, "ebpf_tile_jit_var") != hipSuccess ||
-      hipModuleGetFunction(&f.loop, m, "ebpf_tile_jit_loop") != hipSuccess) {
+      hipModuleGetFunction(&f.loop, m, "ebpf_tile_jit_loop") != hipSuccess ||
+      hipModuleGetFunction(&f.var_stack, m, "ebpf_tile_jit_var_stack") != hipSuccess) {
     (void)hipModuleUnload(m);
     return false;
   }

@@ -17,6 +17,7 @@ struct JitFns {
   hipFunction_t fixed = nullptr;
   hipFunction_t var = nullptr;
   hipFunction_t loop = nullptr;  // loop programs (ebpf_tile_jit_loop)
+  hipFunction_t var_stack = nullptr;  // stack-window programs, other layouts (ebpf_tile_jit_var_stack)
 };
 
 // Stack-window programs (memory tier 0.5, host.cpp analyze_stack): every store or atomic writes
@@ -39,7 +40,8 @@ struct StackPlan {
 // Compiles a forward-only program of <= kTileMaxUops micro-ops (its tile table `t`, built by
 // build_tile) into the assembly of the two template kernels, then assembles and links it
 // (amd_comgr) into a gfx950 code object. Returns false with a reason in *err on failure.
-// stk: a stack-window program (only the fixed-slot kernel gets its code).
+// stk: a stack-window program (only the fixed-slot kernel and the var kernel's stack variant
+// get its code).
 bool jit_compile(const std::vector<Uop>& uops, const std::vector<TUop>& t,
                  std::vector<char>& code_object, std::string* err, std::string* asm_out = nullptr,
                  const StackPlan* stk = nullptr);

@@ -125,6 +125,6 @@ hipError_t launch_counters_add(const uint64_t* src, uint64_t* dst, hipStream_t s
 // Enqueue the interpreter on `stream`; with counters, its last workgroup folds the shards into them.
 // jit: the program's compiled kernels, launched instead of the tile interpreter where it would run.
 hipError_t launch_interp(int kind, const LaunchArgs& a, int grid, hipStream_t stream,
-                         const JitFns* jit = nullptr);
+                         const JitFns* jit = nullptr, bool stack = false);
 
 }  // namespace ebpfemu

@@ -200,9 +200,12 @@ def test_stack_window_fallbacks(cuda, oracle_mod):
         _vs_oracle(oracle_mod, img, pkts, got, r10=r10, tag=str(kw))
     lens = torch.tensor(np.full(len(pkts), 128, dtype=np.int16), device=cuda)
     offs = torch.tensor(np.arange(len(pkts), dtype=np.int32) * 128, device=cuda)
-    got = _run(img, frames, len(pkts), cuda, kernel=_lib.EBPF_KERNEL_GENERAL_T1, offsets=offs,
+    got = _run(img, frames, len(pkts), cuda, kernel=_lib.EBPF_KERNEL_JIT_VAR_STACK, offsets=offs,
                lens=lens)
     _vs_oracle(oracle_mod, img, pkts, got, tag="offsets")
+    got = _run(img, frames, len(pkts), cuda, kernel=_lib.EBPF_KERNEL_GENERAL_T1, offsets=offs,
+               lens=lens, r10=120)  # (other layouts: the window must lie past byte 64)
+    _vs_oracle(oracle_mod, img, pkts, got, r10=120, tag="offsets r10 120")
     alias = assemble("stxdw [r10-8], r2\nldxdw r0, [r1+504]\nexit")  # reads the window at r1+504
     got = _run(alias, frames, len(pkts), cuda, kernel=_lib.EBPF_KERNEL_GENERAL_T1, stride=128)
     _vs_oracle(oracle_mod, alias, pkts, got, tag="constant alias")
@@ -332,3 +335,110 @@ def test_stack_atomics_fuzz(cuda, oracle_mod, seed):
             assert np.array_equal(got[key], ref[key]), (key, seed, it, img.hex())
         _vs_oracle(oracle_mod, img, pkts, got, tag=f"seed {seed} it {it}")
     assert n_stack >= 12, n_stack
+
+
+# ---------------------------------------------------------------------------------------------
+# Memory tier 0.5 on the other layouts (ebpf_tile_jit_var_stack): offsets + lens (a pcap capture),
+# stride + lens, and xdp_md batches in place, packets of any length -- short ones (the preloaded
+# window's bytes past the packet are zeros) and ones reaching into the stack window (its bytes
+# loaded from the packet at the start)
+VAR_LAYOUTS = {
+    "offsets16": dict(offsets_layout=True, align=16),
+    "offsets_mis3": dict(offsets_layout=True, misalign=3),
+    "stride_lens": dict(),
+    "xdp_offsets": dict(offsets_layout=True, align=16, xdp=True),
+    "xdp_stride_lens": dict(xdp=True),
+}
+
+
+def _var_packets(rng, n):
+    lens = [0, 1, 5, 13, 14, 34, 60, 63, 64, 65, 100, 200, 470, 490, 500, 505, 511, 600, 1000]
+    return [bytes(rng.getrandbits(8) for _ in range(rng.choice(lens))) for _ in range(n)]
+
+
+def _run_var(img, pkts, dev, layout, generic=False):
+    import torch
+
+    from ebpf_emu import Program
+    from test_gpu_parity import _stage
+
+    layout = dict(layout)
+    xdp = layout.pop("xdp", False)
+    frames, kw = _stage(pkts, dev, **layout)
+    prog = Program(img)
+    b = prog.make_batch(frames, max_steps=STEPS, generic=generic, xdp_md=xdp, **kw)
+    kernel = prog.batch_kernel(b, None, dev.index or 0)
+    cnt = torch.zeros(8, dtype=torch.int64, device=dev)
+    res = prog.run(frames, max_steps=STEPS, r0=True, status=True, regs=True, counters=cnt,
+                   generic=generic, xdp_md=xdp, **kw)
+    v = prog.run(frames, max_steps=STEPS, xdp_md=xdp, generic=generic, **kw)  # production
+    torch.cuda.synchronize()
+    out = dict(status=res.status.cpu().numpy(), r0=res.r0.cpu().numpy().view(np.uint64),
+               verdict=res.verdict.cpu().numpy(), regs=res.regs.cpu().numpy().view(np.uint64),
+               counters=cnt.cpu().numpy().view(np.uint64), kernel=kernel,
+               prod_verdict=v.verdict.cpu().numpy())
+    prog.close()
+    return out, xdp
+
+
+def _images_of(pkts, xdp):
+    import struct
+
+    return [struct.pack("<II", 8, 8 + len(p)) + p for p in pkts] if xdp else pkts
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layout", sorted(VAR_LAYOUTS))
+def test_stack_window_fuzz_var(cuda, oracle_mod, layout):
+    """Random stack programs (with and without stack atomics and packet-window stores) on the
+    other layouts: the var kernel's stack statement == the general interpreter == the oracle on
+    the same images, every output, the production verdicts too."""
+    from ebpf_emu import Program, _lib
+
+    rng = random.Random(hash(layout) & 0xffff)
+    n_stack = 0
+    for it in range(30):
+        img = gen_stack_program(rng, pw_atomics=it % 2 == 1)
+        try:
+            oracle_mod.Program(img)
+        except oracle_mod.OracleDecodeError:
+            continue
+        p = Program(img)
+        k = p.stack_window
+        p.close()
+        if not k:
+            continue
+        pkts = _var_packets(rng, rng.choice([64, 100, 130]))
+        got, xdp = _run_var(img, pkts, cuda, VAR_LAYOUTS[layout])
+        assert got["kernel"] in (_lib.EBPF_KERNEL_JIT_VAR_STACK, _lib.EBPF_KERNEL_GENERAL_T1)
+        n_stack += got["kernel"] == _lib.EBPF_KERNEL_JIT_VAR_STACK
+        ref, _ = _run_var(img, pkts, cuda, VAR_LAYOUTS[layout], generic=True)
+        assert ref["kernel"] == _lib.EBPF_KERNEL_GENERAL_T1
+        ok = got["status"] != 7  # (ST_BADPKT lanes have no registers: main.rs:20-21 panics)
+        for key in ("status", "verdict", "counters", "prod_verdict"):
+            assert np.array_equal(got[key], ref[key]), (key, layout, it, img.hex())
+        for key in ("r0", "regs"):
+            assert np.array_equal(got[key][ok], ref[key][ok]), (key, layout, it, img.hex())
+        _vs_oracle(oracle_mod, img, _images_of(pkts, xdp), got, tag=f"{layout} it {it}")
+    assert n_stack >= 8, n_stack
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layout", ["offsets_mis3", "xdp_offsets"])
+def test_stack_workloads_var(cuda, oracle_mod, layout):
+    """ATOMIC_PROGRAMS, the key-spilling 5-tuple and the MAC-swap reflector on the other layouts,
+    against the oracle and the general interpreter."""
+    from ebpf_emu import _lib
+    from ebpf_emu import workloads as W
+    from ebpf_emu.asm import assemble
+
+    rng = random.Random(31)
+    for src in ATOMIC_PROGRAMS + [W.MAC_SWAP_TX, W.FIVE_TUPLE_STACK]:
+        img = assemble(src)
+        pkts = _var_packets(rng, 150)
+        got, xdp = _run_var(img, pkts, cuda, VAR_LAYOUTS[layout])
+        assert got["kernel"] == _lib.EBPF_KERNEL_JIT_VAR_STACK, src
+        ref, _ = _run_var(img, pkts, cuda, VAR_LAYOUTS[layout], generic=True)
+        for key in ("status", "verdict", "counters"):
+            assert np.array_equal(got[key], ref[key]), (key, layout, src)
+        _vs_oracle(oracle_mod, img, _images_of(pkts, xdp), got, tag=f"{layout} {src!r}")
