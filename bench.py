@@ -45,6 +45,9 @@ CONFIGS = {
     # r1 = ctx, data / data_end read from it), same frames as 5tuple; the ctx is synthesised in
     # the kernel's window (no staging copy)
     "xdp": (2, "IPv4 5-tuple as a standard XDP program, xdp_md ctx (37 insns) over 1Mi x 64B frames"),
+    # config 5 with the running sum in a stack slot (memory tier 0.5 with a loop: the loop kernel's
+    # stack variant; --generic: the general interpreter's tier 1)
+    "checksum_stack": (4, "per-byte checksum loop, sum kept at r10-8, over 1Mi mixed 64B/1500B frames"),
 }
 PROGRAM_OF = {"stack": "5tuple_stack", "tier1": "mac_swap_tx", "xdp": "5tuple_xdp"}
 
@@ -113,7 +116,7 @@ def main():
     # ---- synthetic device-resident batches ----
     from ebpf_emu import dist as D
 
-    mixed = args.config == "checksum"
+    mixed = args.config in ("checksum", "checksum_stack")
     fb = (max(64, args.frame_bytes) + 15) // 16 * 16  # fixed slots: 16-byte aligned, >= 64
     batches = []
     pool_bytes = 0

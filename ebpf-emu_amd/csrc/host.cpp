@@ -276,7 +276,7 @@ static int jit_compile_locked(ebpf_prog* p) {
   if (p->jit_state == 0) {
     p->jit_has[0] = p->jit_has[1] = !p->tuops.empty() && !p->tuopsk.empty();
     p->jit_has[2] = !p->ltuops.empty() && !p->ltuopsx.empty();
-    if (p->stack.k) p->jit_has[1] = true;  // (the main.rs layout's fixed-slot kernel only)
+    if (p->stack.k) p->jit_has[1] = !p->tuopsk.empty();  // (the main.rs layout only)
     if (g_no_jit || (!p->jit_has[0] && !p->jit_has[1] && !p->jit_has[2])) {
       p->jit_state = 2;
     } else {
@@ -284,12 +284,25 @@ static int jit_compile_locked(ebpf_prog* p) {
       for (int v = 0; v < 3 && p->jit_state == 1; v++) {
         if (!p->jit_has[v]) continue;
         const bool ok = v == 2 ? jit_compile_loop(p->xuops, p->ltuops, p->ltuopsx, p->jit_co[v],
-                                                  &p->jit_err, &p->jit_asm[v])
+                                                  &p->jit_err, &p->jit_asm[v],
+                                                  p->stack.k ? &p->stack : nullptr)
                                : jit_compile(p->xuops, v ? p->tuopsk : p->tuops, p->jit_co[v],
                                              &p->jit_err, &p->jit_asm[v],
                                              p->stack.k ? &p->stack : nullptr);
+        if (!ok && v >= 1 && p->stack.k && !p->jit_has[0]) {
+          // a stack-window program whose code does not assemble (e.g. branches past the
+          // assembler's reach in a huge program): it stays on the general interpreter
+          p->stack = StackPlan();
+          p->kloads.clear();
+          p->jit_has[1] = p->jit_has[2] = false;
+          p->jit_co[1].clear();
+          p->jit_co[2].clear();
+          break;
+        }
         if (!ok) p->jit_state = EBPF_EJIT;
       }
+      if (p->jit_state == 1 && !p->jit_has[0] && !p->jit_has[1] && !p->jit_has[2])
+        p->jit_state = 2;
       if (p->jit_state == EBPF_EJIT && getenv("EBPFEMU_JIT_VERBOSE"))
         fprintf(stderr, "ebpfemu: program compiler: %s\n", p->jit_err.c_str());
     }
@@ -787,8 +800,9 @@ static bool flatten_calls(const std::vector<Uop>& u, std::vector<Uop>& out) {
   return true;
 }
 
-// Memory tier 0.5 (stack-window programs): a forward-only program of <= kTileMaxUops micro-ops
-// whose only memory writes are ST/STX at r10 + c for a c known at load time (the XDP spill / key
+// Memory tier 0.5 (stack-window programs): a program of <= kJitMaxUops micro-ops (loops included:
+// the compiled loop kernel's stack variant) whose only memory writes are ST/STX at r10 + c for a
+// c known at load time (the XDP spill / key
 // pattern: `stxdw [r10-8], r3`, also through a copy such as `mov r2, r10; add r2, -16`), with no
 // ATOMIC or CALL. A load-time dataflow over the main.rs register layout (main.rs:28-31) tracks
 // each register as unknown, a constant, or r10 + c; every store must be r10 + c on all paths, with
@@ -805,12 +819,12 @@ struct StackAnalysis {
 static StackAnalysis analyze_stack(const std::vector<Uop>& uops) {
   StackAnalysis res;
   const uint32_t n = (uint32_t)uops.size();
-  if (n == 0 || n > kTileMaxUops) return res;
-  bool any_store = false;
+  if (n == 0 || n > kJitMaxUops) return res;
+  bool any_store = false, loops = false;
   for (uint32_t i = 0; i < n; i++) {
     const Uop& u = uops[i];
     if (u.op == U_CALL) return res;
-    if (u.op >= U_JA && u.op <= U_JLE32 && (uint32_t)u.x <= i) return res;  // forward only
+    loops = loops || (u.op >= U_JA && u.op <= U_JLE32 && (uint32_t)u.x <= i);  // back edges
     // atomics: the operations emu.rs:391-419 implements (others panic: the general interpreter)
     if (u.op == U_ATOMIC && !(u.k == 0x00 || u.k == 0x40 || u.k == 0x50 || u.k == 0xa0 ||
                               u.k == 0xe0 || u.k == 0xf0))
@@ -827,17 +841,27 @@ static StackAnalysis analyze_stack(const std::vector<Uop>& uops) {
   in[0].r[2] = Val{TOP, 0};   // len
   in[0].r[10] = Val{FP, 0};   // r10 itself
   auto same = [](const Val& a, const Val& b) { return a.k == b.k && (a.k == TOP || a.v == b.v); };
+  bool changed = false;
   auto flow = [&](uint32_t to, const Regs& st) {
     if (to >= n) return;
     Regs& t = in[to];
-    if (!t.reached) { t = st; return; }
+    if (!t.reached) { t = st; changed = true; return; }
     for (int r = 0; r < 11; r++)
-      if (!same(t.r[r], st.r[r])) t.r[r] = Val{TOP, 0};
+      if (!same(t.r[r], st.r[r]) && t.r[r].k != TOP) t.r[r] = Val{TOP, 0}, changed = true;
   };
   std::vector<int32_t> off(n, kNoStack), pw(n, kNoStack);
   std::vector<char> dyn(n, 0);  // LDX with an unknown base
   bool any_pw = false;
   int64_t lo = 0, hi = INT64_MIN;  // store bytes relative to r10: [lo, hi)
+  // passes in pc order until the states stop changing (one pass without back edges; with them
+  // each join only moves a register towards unknown, so this ends), the last one collecting
+  for (int pass = 0;; pass++) {
+  changed = false;
+  std::fill(off.begin(), off.end(), kNoStack);
+  std::fill(pw.begin(), pw.end(), kNoStack);
+  std::fill(dyn.begin(), dyn.end(), 0);
+  any_pw = false;
+  lo = 0, hi = INT64_MIN;
   for (uint32_t i = 0; i < n; i++) {
     if (!in[i].reached) continue;
     const Uop& u = uops[i];
@@ -898,6 +922,12 @@ static StackAnalysis analyze_stack(const std::vector<Uop>& uops) {
     }
     flow(i + 1, st);
   }
+  if (!changed || !loops) break;
+  if (pass > 4 * (int)n + 16) return res;
+  }
+  // (loop programs run on the loop kernel, whose loads are not constant-folded: no packet-window
+  // stores there)
+  if (loops && any_pw) return res;
   // packet-window stores: every load must be a constant-address one (fold_const_loads reads the
   // stored bytes from the window registers) or a stack-window one, none straddling the window's
   // end (its bytes below kWin would come from HBM)
@@ -995,16 +1025,25 @@ int ebpf_prog_load(const uint8_t* code, size_t nbytes, ebpf_prog** out, size_t* 
   if (p->xtier == 1 && !g_no_stack) {  // memory tier 0.5: the compiled fixed-slot kernel only
     StackAnalysis sa = analyze_stack(xu);
     const std::vector<DUop> dk =
-        sa.plan.k ? fold_const_loads(xu, build_dag(xu)) : std::vector<DUop>();
+        sa.plan.k && forward ? fold_const_loads(xu, build_dag(xu)) : std::vector<DUop>();
     // packet-window stores: every load outside the stack window must be a constant-address one
     // (read from the window registers the stores update)
-    for (size_t i = 0; sa.plan.k && sa.plan.any_pw && i < xu.size(); i++)
+    for (size_t i = 0; sa.plan.k && sa.plan.any_pw && forward && i < xu.size(); i++)
       if (xu[i].op == U_LDX && sa.plan.off[i] == kNoStack && (dk[i].opaux & 0xff) != U_LDXK)
         sa.plan.k = 0;
     if (sa.plan.k) {
-      for (const DUop& o : dk)
-        if ((o.opaux & 0xff) == U_LDXK) p->kloads.push_back({o.addr, o.opaux >> 8});
-      p->tuopsk = build_tile(xu, dk, false, true);
+      if (forward) {  // the forward kernels' table, constant-address loads resolved
+        for (const DUop& o : dk)
+          if ((o.opaux & 0xff) == U_LDXK) p->kloads.push_back({o.addr, o.opaux >> 8});
+        p->tuopsk = build_tile(xu, dk, false, true);
+      }
+      // the loop kernel's stack variant (back edges, or a step budget that can bind; not with
+      // packet-window stores, which need the forward kernels' preloaded window)
+      if (!sa.plan.any_pw) {
+        const std::vector<DUop> d = build_dag(xu);
+        p->ltuops = build_tile(xu, d, false, true);
+        p->ltuopsx = build_tile(xu, d, true, true);
+      }
       p->stack = std::move(sa.plan);
     }
   }
@@ -1182,13 +1221,28 @@ static int batch_tier(const ebpf_prog* p, const ebpf_batch* b) {
 // Memory tier 0.5 (analyze_stack) on this batch: the compiled fixed-slot kernel with the main.rs
 // register layout, and a window [r10 - k, r10) that lies in the image, past every packet byte (so
 // it starts as zeros) and away from every constant-address load; else the general interpreter.
+static bool stack_common_ok(const ebpf_prog* p, const ebpf_batch* b, const ebpf_batch_out* out) {
+  if (!p->stack.k) return false;
+  if (b->flags & (EBPF_BATCH_GENERIC | EBPF_BATCH_NO_JIT)) return false;
+  if (b->init_regs || b->init_fp_len || out->mem) return false;
+  const uint64_t k = p->stack.k, r10 = b->r10;
+  return r10 % 4 == 0 && r10 >= k && r10 <= b->mem_size;
+}
+
+// The stack window on the other layouts (ebpf_tile_jit_var_stack, ebpf_tile_jit_loop_stack):
+// lanes whose packet reaches into it load those bytes at the start, which needs the window past
+// the header window (and the xdp_md ctx).
+static bool stack_var_ok(const ebpf_prog* p, const ebpf_batch* b) {
+  return b->r10 - p->stack.k >= (uint64_t)kWin;
+}
+
+// Forward stack-window programs on the compiled forward kernels (fixed slots: the window must lie
+// past every packet byte, so it starts as zeros; other layouts: stack_var_ok).
 static bool stack_launch_ok(const ebpf_prog* p, const ebpf_batch* b, const ebpf_batch_out* out,
                             int device) {
-  if (!p->stack.k || !p->jit_mod[device][1]) return false;
-  if (b->flags & (EBPF_BATCH_GENERIC | EBPF_BATCH_NO_JIT)) return false;
-  if (b->init_regs || b->init_fp_len || out->mem || b->max_steps < p->xuops.size()) return false;
+  if (!stack_common_ok(p, b, out) || !p->jit_mod[device][1] || b->max_steps < p->xuops.size())
+    return false;
   const uint64_t k = p->stack.k, r10 = b->r10;
-  if (r10 % 4 || r10 < k || r10 > b->mem_size) return false;
   LaunchArgs la{};
   la.frames = b->frames;
   la.offsets = b->offsets;
@@ -1196,11 +1250,8 @@ static bool stack_launch_ok(const ebpf_prog* p, const ebpf_batch* b, const ebpf_
   la.stride = b->stride;
   la.mem_out = out->mem;
   const bool fixed = launch_fixed_layout(la);
-  // fixed slots: the window lies past every packet byte (it starts as zeros); other layouts
-  // (ebpf_tile_jit_var_stack): lanes whose packet reaches into it load those bytes at the start,
-  // which needs the window past the header window (and the xdp_md ctx)
   const uint64_t img_len = b->stride + ((b->flags & EBPF_BATCH_XDP_MD) ? 8 : 0);
-  if (fixed ? r10 - k < img_len : r10 - k < (uint64_t)kWin) return false;
+  if (fixed ? r10 - k < img_len : !stack_var_ok(p, b)) return false;
   for (const auto& kl : p->kloads) {
     if (kl.first < r10 && kl.first + kl.second > r10 - k) return false;
     // packet-window stores: the compiled code has only the copy whose window loads read the
@@ -1212,19 +1263,31 @@ static bool stack_launch_ok(const ebpf_prog* p, const ebpf_batch* b, const ebpf_
   return true;
 }
 
+// Stack-window programs with back edges (or a binding step budget) on the loop kernel's stack
+// variant.
+static bool stack_loop_ok(const ebpf_prog* p, const ebpf_batch* b, const ebpf_batch_out* out,
+                          int device) {
+  return stack_common_ok(p, b, out) && p->jit_mod[device][2] && !g_no_loop && stack_var_ok(p, b);
+}
+
 // The kernel kind of a batch (uploaded program): dag_kernel needs no step budget (a lane of a
 // forward-only program retires <= n_uops steps); the tile kernel in loop mode runs loops, or a
-// step budget that can bind (exact budget); a stack-window batch runs the compiled fixed-slot kernel.
+// step budget that can bind (exact budget); a stack-window batch runs the compiled stack kernels
+// (forward, or the loop kernel's) or the general interpreter.
 static int batch_kind(const ebpf_prog* p, const ebpf_batch* b, const ebpf_batch_out* out,
                       int device, bool* stk) {
   // (the final frame stacks of a flattened program are its copies' stacks: the general
   // interpreter's frame stack writes them)
   const bool generic = g_no_dag || (b->flags & EBPF_BATCH_GENERIC) || b->init_fp_len ||
                        (p->flattened && (out->fp || out->fp_len));
-  *stk = !generic && stack_launch_ok(p, b, out, device);
-  return *stk ? kKindDag
-         : (p->dev_duops[device] && b->max_steps >= p->xuops.size() && !generic) ? kKindDag
-         : (p->dev_ltuops[device] && !generic && !g_no_loop &&
+  *stk = false;
+  if (p->stack.k && !generic) {
+    if (stack_launch_ok(p, b, out, device)) return *stk = true, kKindDag;
+    if (stack_loop_ok(p, b, out, device)) return *stk = true, kKindLoop;
+    return batch_tier(p, b);
+  }
+  return (p->dev_duops[device] && b->max_steps >= p->xuops.size() && !generic) ? kKindDag
+         : (p->dev_ltuops[device] && !generic && !g_no_loop && !p->stack.k &&
             (p->xuops.size() <= kTileMaxUops ||  // tile_kernel's loop mode, or compiled only
              (p->jit_mod[device][2] && !(b->flags & EBPF_BATCH_NO_JIT))))          ? kKindLoop
                                                                          : batch_tier(p, b);
@@ -1232,7 +1295,7 @@ static int batch_kind(const ebpf_prog* p, const ebpf_batch* b, const ebpf_batch_
 
 // The compiled program, where it applies (tile-kernel programs; same tables, same results).
 static const JitFns* batch_jit(ebpf_prog* p, const ebpf_batch* b, int kind, bool stk, int device) {
-  if (stk) return &p->jit_fn[device][1];
+  if (stk) return &p->jit_fn[device][kind == kKindLoop ? 2 : 1];
   if (b->flags & EBPF_BATCH_NO_JIT) return nullptr;
   if (kind == kKindDag && p->jit_mod[device][0]) return &p->jit_fn[device][b->init_regs ? 0 : 1];
   if (kind == kKindLoop && p->jit_mod[device][2]) return &p->jit_fn[device][2];

@@ -1409,6 +1409,9 @@ constexpr uint32_t kTileWaveLds = kWinBytes + kDagMetaBytes;  // window + metada
 // refill (jit.cpp refill_prefetch), in v[56:71]
 #define TILE_ASM_CLOBBER_PREFETCH "v56", "v57", "v58", "v59", "v60", "v61", "v62", "v63", "v64", \
     "v65", "v66", "v67", "v68", "v69", "v70", "v71"
+#define TILE_ASM_CLOBBER_WINDOW_HI "v72", "v73", "v74", "v75", "v76", "v77", "v78", "v79", "v80", \
+    "v81", "v82", "v83", "v84", "v85", "v86", "v87", "v88", "v89", "v90", "v91", "v92", "v93", "v94", \
+    "v95"
 #define TILE_ASM_CLOBBER_WINDOW "v64", "v65", "v66", "v67", "v68", "v69", "v70", "v71", "v72", \
     "v73", "v74", "v75", "v76", "v77", "v78", "v79", "v80", "v81", "v82", "v83", "v84", "v85", \
     "v86", "v87", "v88", "v89", "v90", "v91", "v92", "v93", "v94", "v95"
@@ -1485,7 +1488,11 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
     const uint64_t t = rfl64(tile);
     const uint64_t nt = t + total_waves;
     uint32_t bkt, nst;
-    if constexpr (JIT && LOOPS) {  // + the refill prefetch registers of compiled loop programs
+    if constexpr (JIT && LOOPS && STACK) {  // stack-window loop programs: v[56:95] too
+      asm volatile(
+#include "tile_jit_stack.inc"
+          TILE_ASM_OPERANDS, TILE_ASM_CLOBBER_PREFETCH, TILE_ASM_CLOBBER_WINDOW_HI);
+    } else if constexpr (JIT && LOOPS) {  // + the refill prefetch registers of compiled loop programs
       asm volatile(
 #include "tile_jit.inc"
           TILE_ASM_OPERANDS, TILE_ASM_CLOBBER_PREFETCH);
@@ -1671,6 +1678,11 @@ extern "C" __global__ __launch_bounds__(kBlock, 4) void ebpf_tile_jit_var_stack(
 // (6 waves per SIMD: the prefetch registers take the kernel past 64 VGPRs)
 extern "C" __global__ __launch_bounds__(kBlock, 5) void ebpf_tile_jit_loop(LaunchArgs a) {
   tile_body<false, true, true>(a);
+}
+// stack-window loop programs (memory tier 0.5 with back edges or a binding budget): the stack
+// window in v[80:95]
+extern "C" __global__ __launch_bounds__(kBlock, 4) void ebpf_tile_jit_loop_stack(LaunchArgs a) {
+  tile_body<false, true, true, true>(a);
 }
 #endif
 
@@ -1883,7 +1895,8 @@ static bool jit_forward_for(int kind, uint32_t n_uops) {
 }
 
 int launch_kernel_id(int kind, const LaunchArgs& a, const JitFns* jit, bool stack) {
-  if (jit && jit->loop && kind == kKindLoop) return EBPF_KERNEL_JIT_LOOP;
+  if (jit && jit->loop && kind == kKindLoop)
+    return stack ? EBPF_KERNEL_JIT_LOOP_STACK : EBPF_KERNEL_JIT_LOOP;
   if (jit && jit->fixed && jit_forward_for(kind, a.n_uops))
     return jit_fixed_layout(&a) ? (stack ? EBPF_KERNEL_JIT_STACK : EBPF_KERNEL_JIT_FIXED)
                                 : (stack ? EBPF_KERNEL_JIT_VAR_STACK : EBPF_KERNEL_JIT_VAR);
@@ -1909,7 +1922,8 @@ hipError_t launch_interp(int kind, const LaunchArgs& a, int grid, hipStream_t st
   void* bargs[] = {(void*)&b};
   hipError_t e;
   if (jit && jit->loop && kind == kKindLoop) {  // the compiled loop program
-    e = hipModuleLaunchKernel(jit->loop, grid, 1, 1, kBlock, 1, 1, lds, stream, bargs, nullptr);
+    e = hipModuleLaunchKernel(stack ? jit->loop_stack : jit->loop, grid, 1, 1, kBlock, 1, 1, lds,
+                              stream, bargs, nullptr);
   } else if (jit && jit->fixed && jit_forward_for(kind, a.n_uops)) {
     if (jit_fixed_layout(&a)) {  // double-buffered windows: its own LDS size and grid
       const uint32_t dlds = g_lds_pad + kDbWaves * kTileWaveLdsDb;

@@ -576,7 +576,9 @@ struct Compiler {
         wr = d;
       } else if (u.op == U_STX) {
         rd = 1u << u.src;  // (the address r10 + c is resolved at load time)
-      }
+      } else if (u.op == U_ATOMIC) {  // (stack atomics, emu.rs:373-437) the operand, the dst
+        rd = (1u << u.src) | d | (u.k == 0xf0 ? 1u : 0u);  // snapshot written back, CMPXCHG's r0;
+      }                                                     // its writes kill nothing here
     };
     for (bool changed = true; changed;) {  // one pass without back edges; to a fixpoint with
       changed = false;                     // them
@@ -1031,35 +1033,53 @@ struct Compiler {
   // A register-address load of a stack-window program: the lanes whose bytes [a, a + w) overlap
   // the window (a - S0 < k or a + w - 1 - S0 < k, u32, S0 = r10 - k in s57) take the window's bytes
   // instead of the image's (store forwarding); the value v[26:27] is patched byte by byte, each
-  // byte's window dword picked by a compare/select chain. Out of line; returns the check.
-  std::string stack_overlay(const std::string& U, uint32_t w, std::string& ool) const {
+  // byte's window dword picked by a compare/select chain. The patch is one shared subroutine per
+  // access width (overlay_routines, called with s_swappc: return address in s[62:63]), out of
+  // line; returns the check and the call.
+  mutable uint32_t overlay_widths = 0;  // bit w: the width-w routine is needed
+  std::string stack_overlay(const std::string& U, uint32_t w, std::string&) const {
     const uint32_t k = stk->k;
-    std::string s = "v_subrev_u32 v44, s57, v36\n"
-                    "v_add_u32 v45, " + std::to_string(w - 1) + ", v44\n"
-                    "v_cmp_gt_u32 vcc, " + std::to_string(k) + ", v44\n"
-                    "v_cmp_gt_u32 s[60:61], " + std::to_string(k) + ", v45\n"
-                    "s_or_b64 vcc, vcc, s[60:61]\n"
-                    "s_cbranch_vccnz .Lovl" + U + "\n"
-                    ".Lovd" + U + ":\n";
-    std::string o = ".Lovl" + U + ":\ns_mov_b64 s[66:67], exec\ns_mov_b64 exec, vcc\n";
-    for (uint32_t j = 0; j < w; j++) {
-      const std::string T = j < 4 ? "v26" : "v27";
-      const uint32_t q = j & 3;
-      o += "v_add_u32 v46, " + std::to_string(j) + ", v44\n"
-           "v_cmp_gt_u32 s[68:69], " + std::to_string(k) + ", v46\n"
-           "v_lshrrev_b32 v47, 2, v46\nv_mov_b32 v48, 0\n";
-      for (uint32_t d = 0; d < k / 4; d++)
-        o += "v_cmp_eq_u32 vcc, " + std::to_string(d) + ", v47\nv_cndmask_b32 v48, v48, " + sv(d) +
-             ", vcc\n";
-      uint32_t sel = 0;
-      for (uint32_t b = 0; b < 4; b++) sel |= (b == q ? 4u : b) << (8 * b);
-      o += "v_and_b32 v49, 3, v46\nv_lshlrev_b32 v49, 3, v49\nv_bfe_u32 v48, v48, v49, 8\n"
-           "s_mov_b32 s36, " + hex32(sel) + "\nv_perm_b32 v49, v48, " + T + ", s36\n"
-           "v_cndmask_b32_e64 " + T + ", " + T + ", v49, s[68:69]\n";
+    overlay_widths |= 1u << w;
+    return "v_subrev_u32 v44, s57, v36\n"
+           "v_add_u32 v45, " + std::to_string(w - 1) + ", v44\n"
+           "v_cmp_gt_u32 vcc, " + std::to_string(k) + ", v44\n"
+           "v_cmp_gt_u32 s[60:61], " + std::to_string(k) + ", v45\n"
+           "s_or_b64 vcc, vcc, s[60:61]\n"
+           "s_cbranch_vccz .Lovd" + U + "\n"
+           "s_getpc_b64 s[60:61]\n.Lovp" + U + ":\n"
+           "s_add_u32 s60, s60, " + overlay_label(w) + "-.Lovp" + U + "\n"
+           "s_addc_u32 s61, s61, 0\n"
+           "s_swappc_b64 s[62:63], s[60:61]\n"
+           ".Lovd" + U + ":\n";
+  }
+  std::string overlay_label(uint32_t w) const { return ".Lovr" + ovl_tag + "_" + std::to_string(w); }
+  std::string ovl_tag;  // unique per statement (set by body)
+
+  // The overlay routines the statement's loads call (vcc = the lanes to patch).
+  std::string overlay_routines() const {
+    const uint32_t k = stk ? stk->k : 0;
+    std::string o;
+    for (uint32_t w = 1; w <= 8; w++) {
+      if (!(overlay_widths & (1u << w))) continue;
+      o += overlay_label(w) + ":\ns_mov_b64 s[66:67], exec\ns_mov_b64 exec, vcc\n";
+      for (uint32_t j = 0; j < w; j++) {
+        const std::string T = j < 4 ? "v26" : "v27";
+        const uint32_t q = j & 3;
+        o += "v_add_u32 v46, " + std::to_string(j) + ", v44\n"
+             "v_cmp_gt_u32 s[68:69], " + std::to_string(k) + ", v46\n"
+             "v_lshrrev_b32 v47, 2, v46\nv_mov_b32 v48, 0\n";
+        for (uint32_t d = 0; d < k / 4; d++)
+          o += "v_cmp_eq_u32 vcc, " + std::to_string(d) + ", v47\nv_cndmask_b32 v48, v48, " + sv(d) +
+               ", vcc\n";
+        uint32_t sel = 0;
+        for (uint32_t b = 0; b < 4; b++) sel |= (b == q ? 4u : b) << (8 * b);
+        o += "v_and_b32 v49, 3, v46\nv_lshlrev_b32 v49, 3, v49\nv_bfe_u32 v48, v48, v49, 8\n"
+             "s_mov_b32 s36, " + hex32(sel) + "\nv_perm_b32 v49, v48, " + T + ", s36\n"
+             "v_cndmask_b32_e64 " + T + ", " + T + ", v49, s[68:69]\n";
+      }
+      o += "s_mov_b64 exec, s[66:67]\ns_setpc_b64 s[62:63]\n";
     }
-    o += "s_mov_b64 exec, s[66:67]\ns_branch .Lovd" + U + "\n";
-    ool += o;
-    return s;
+    return o;
   }
 
   // kJitRefill with the address's low word in register A instead of v36
@@ -1117,8 +1137,11 @@ struct Compiler {
          "ds_read_u8 v26, v42\n"
          "s_waitcnt lgkmcnt(0)\n"
          "v_cndmask_b32_e64 v26, 0, v26, s[60:61]\n"
-         ".Lfarb" + U + ":\n"
-         "v_bfi_b32 " + D0 + ", s56, v26, " + D0 + "\n";
+         ".Lfarb" + U + ":\n";
+    if (stk)  // store forwarding from the stack window
+      s += (A == "v36" ? std::string() : "v_mov_b32 v36, " + A + "\n") + "v_mov_b32 v27, 0\n" +
+           stack_overlay(U, 1, ool);
+    s += "v_bfi_b32 " + D0 + ", s56, v26, " + D0 + "\n";
     ool += ".Lrf" + U + ":\n"
            "s_mov_b64 s[68:69], vcc\n"
            "s_cmp_eq_u32 " + m.aligned + ", 0\n"
@@ -1535,8 +1558,10 @@ struct Compiler {
   // packet's dwords from HBM (zeros past its end) out of line.
   // var (the var kernel's stack statement): packets of any length, so the bytes at or past LEN
   // read as zero (main.rs:16) -- masked after either path, before the stack overlay.
+  // loop (the loop kernel's stack statement): the window holds packet bytes [WB, WB + 64) (v22,
+  // moved by the one-byte loads' refills); this load reads it at a - WB and never refills.
   std::string ldx_fixed(uint32_t i, bool one, const std::string& P, std::string& ool,
-                        bool var = false) const {
+                        bool var = false, bool loop = false) const {
     const TUop& u = t[i];
     const uint32_t w = one ? 1u : u.width;
     const std::string U = P + "u" + std::to_string(i), next = entry_label(P, next_start(i));
@@ -1563,16 +1588,19 @@ struct Compiler {
          "v_subrev_u32 v29, " + std::to_string(u.a0) + ", v29\n"
          "s_andn2_b64 exec, s[66:67], s[64:65]\n"
          "s_cbranch_execz " + next + "\n"
-         ".Lok" + U + ":\n"
-         "v_cmp_lt_u32_e64 s[62:63], 64, v38\n"
+         ".Lok" + U + ":\n" +
+         (loop ? "v_sub_u32 v41, v36, v22\nv_cmp_lt_u32_e64 s[62:63], " + std::to_string(64 - w) +
+                     ", v41\n"
+               : std::string("v_cmp_lt_u32_e64 s[62:63], 64, v38\n")) +
          "s_and_b64 s[68:69], s[62:63], exec\n"
          "s_cbranch_scc1 .Lfar" + U + "\n";
-    // the window bytes a .. a + w - 1 (all inside [0, 64) here) into v26 (v27)
+    // the window bytes a .. a + w - 1 (at window offset O: inside [0, 64) here) into v26 (v27)
+    const std::string O = loop ? "v41" : "v36";
     std::string win;
     if (w == 1) {
-      win = "v_xad_u32 v42, v35, v36, v34\nds_read_u8 v26, v42\ns_waitcnt lgkmcnt(0)\n";
+      win = "v_xad_u32 v42, v35, " + O + ", v34\nds_read_u8 v26, v42\ns_waitcnt lgkmcnt(0)\n";
     } else {
-      win = "v_and_b32 v42, -4, v36\nv_xad_u32 v43, v35, v42, v34\nds_read_b32 v49, v43\n"
+      win = "v_and_b32 v42, -4, " + O + "\nv_xad_u32 v43, v35, v42, v34\nds_read_b32 v49, v43\n"
             "v_add_u32 v44, 4, v42\nv_min_u32 v44, 60, v44\nv_xad_u32 v44, v35, v44, v34\n"
             "ds_read_b32 v50, v44\n";
       if (w == 8)
@@ -1597,7 +1625,7 @@ struct Compiler {
       s += "v_mov_b64 " + vpair(u.dst2, 0, 1) + ", v[26:27]\n";
     // out of line: lanes whose access ends past the window (in bounds: their bytes come from
     // the packet's dwords that hold a packet byte, zeros past its end)
-    std::string far = ".Lfar" + U + ":\n" + win +
+    std::string far = ".Lfar" + U + ":\n" + (loop ? "v_min_u32 v41, 63, v41\n" : "") + win +
                       "s_mov_b64 s[66:67], exec\ns_mov_b64 exec, s[68:69]\n"
                       "v_mov_b32 v26, 0\nv_mov_b32 v27, 0\n"
                       "v_cmp_lt_u32 vcc, v36, v31\ns_and_b64 exec, s[68:69], vcc\n"
@@ -2001,6 +2029,12 @@ struct Compiler {
       ool += ot;
       return true;
     }
+    if (loops && stk && (id == T_LDX_C || id == T_LDX_E)) {  // (the overlay needs the value)
+      std::string ot;
+      main += ldx_fixed(i, false, P, ot, true, true);
+      ool += ot;
+      return true;
+    }
     if (loops && (id == T_LDX1_C || id == T_LDX1_E)) {
       std::string ot;
       main += ldx1_loop(i, m, P, ot);
@@ -2040,6 +2074,35 @@ struct Compiler {
            entry_label(P, next_start(i)) + "\n" + ok + ":\n";
   }
 
+  // The stack window starts as the image's bytes there: zeros (fixed slots: the launch checked
+  // that it lies past every packet byte); s57 = its image address S0 = r10 - k (s48 = r10).
+  std::string stack_zero() const {
+    std::string s = "; stack window: " + std::to_string(stk->k) + " bytes\ns_sub_u32 s57, s48, " +
+                    std::to_string(stk->k) + "\n";
+    for (uint32_t j = 0; j < stk->k / 4; j += 2)
+      s += j + 1 < stk->k / 4 ? "v_mov_b64 v[" + std::to_string(kStackVgpr + j) + ":" +
+                                    std::to_string(kStackVgpr + j + 1) + "], 0\n"
+                              : "v_mov_b32 " + sv(j) + ", 0\n";
+    return s;
+  }
+
+  // Other layouts: lanes whose packet reaches into the window take its bytes there, byte by
+  // byte, out of line (the launch checked S0 >= 64, so they are never header-window bytes).
+  std::string stack_init(const std::string& P, std::string& ool) const {
+    ool += ".L" + P + "skinit:\ns_mov_b64 s[66:67], exec\ns_mov_b64 s[68:69], vcc\n";
+    for (uint32_t b = 0; b < stk->k; b++) {
+      const std::string L = ".L" + P + "sk" + std::to_string(b);
+      ool += "s_mov_b64 exec, s[68:69]\nv_add_u32_e64 v36, s57, " + std::to_string(b) +
+             "\nv_cmp_gt_u32 vcc, v31, v36\ns_and_b64 exec, exec, vcc\ns_cbranch_execz " + L +
+             "\nv_mov_b32 v37, 0\nv_lshl_add_u64 v[38:39], v[32:33], 0, v[36:37]\n"
+             "global_load_ubyte v40, v[38:39], off\ns_waitcnt vmcnt(0)\n"
+             "v_lshl_or_b32 " + sv(b / 4) + ", v40, " + std::to_string(8 * (b % 4)) + ", " +
+             sv(b / 4) + "\n" + L + ":\n";
+    }
+    ool += "s_mov_b64 exec, s[66:67]\ns_branch .L" + P + "skdone\n";
+    return "v_cmp_lt_u32 vcc, s57, v31\ns_cbranch_vccnz .L" + P + "skinit\n.L" + P + "skdone:\n";
+  }
+
   // The window shift of the xdp_md convention (see body): packet dwords 0..13 into v[66:79],
   // the ctx into v[64:65] (data = 8, data_end = LEN = 8 + len), all 16 written back in place.
   static std::string xdp_shift() {
@@ -2061,17 +2124,11 @@ struct Compiler {
   // otherwise the handlers' copy, with its per-load bounds checks.
   bool body(const Marker& m, std::string& out) {
     const std::string P = "J" + m.n + "_";
+    ovl_tag = m.n;
+    overlay_widths = 0;
     std::string main = "; compiled eBPF program: " + std::to_string(n) + " micro-ops\n"
                        "s_mov_b32 s52, s33\ns_mov_b32 s53, 0\n";
-    if (stk) {  // the window starts as the image's bytes there: zeros (the launch checked that it
-                // lies past every packet byte); s57 = its image address S0 = r10 - k (s48 = r10)
-      main += "; stack window: " + std::to_string(stk->k) + " bytes\ns_sub_u32 s57, s48, " +
-              std::to_string(stk->k) + "\n";
-      for (uint32_t j = 0; j < stk->k / 4; j += 2)
-        main += j + 1 < stk->k / 4 ? "v_mov_b64 v[" + std::to_string(kStackVgpr + j) + ":" +
-                                         std::to_string(kStackVgpr + j + 1) + "], 0\n"
-                                   : "v_mov_b32 " + sv(j) + ", 0\n";
-    }
+    if (stk) main += stack_zero();
     // xdp_md in place (fixed-slot kernel; the other kernels shift in C++, interp.hip xdp_window):
     // the lane's window holds packet bytes [0, 64), the program reads image bytes [0, 64) =
     // {u32 data = 8, u32 data_end = LEN} + packet bytes [0, 56) (xdp.rs:16-20): shifted once in
@@ -2082,22 +2139,7 @@ struct Compiler {
       main += "s_cmp_lg_u32 " + m.xdp + ", 0\ns_cbranch_scc0 .L" + P + "noxdp\n" + xdp_shift() +
               ".L" + P + "noxdp:\n";
     std::string ool;
-    if (stk && m.stack) {  // (var layouts: lanes whose packet reaches into the window take its
-                           // bytes there, byte by byte, out of line; the launch checked S0 >= 64)
-      main += "v_cmp_lt_u32 vcc, s57, v31\ns_cbranch_vccnz .L" + P + "skinit\n.L" + P +
-              "skdone:\n";
-      ool += ".L" + P + "skinit:\ns_mov_b64 s[66:67], exec\ns_mov_b64 s[68:69], vcc\n";
-      for (uint32_t b = 0; b < stk->k; b++) {
-        const std::string L = ".L" + P + "sk" + std::to_string(b);
-        ool += "s_mov_b64 exec, s[68:69]\nv_add_u32_e64 v36, s57, " + std::to_string(b) +
-               "\nv_cmp_gt_u32 vcc, v31, v36\ns_and_b64 exec, exec, vcc\ns_cbranch_execz " + L +
-               "\nv_mov_b32 v37, 0\nv_lshl_add_u64 v[38:39], v[32:33], 0, v[36:37]\n"
-               "global_load_ubyte v40, v[38:39], off\ns_waitcnt vmcnt(0)\n"
-               "v_lshl_or_b32 " + sv(b / 4) + ", v40, " + std::to_string(8 * (b % 4)) + ", " +
-               sv(b / 4) + "\n" + L + ":\n";
-      }
-      ool += "s_mov_b64 exec, s[66:67]\ns_branch .L" + P + "skdone\n";
-    }
+    if (stk && m.stack) main += stack_init(P, ool);
     uint32_t chunks = 0, maxend = 0;
     if (m.fixed == "1" || m.stack)
       for (uint32_t i = 0; i < n; i++) {
@@ -2147,6 +2189,7 @@ struct Compiler {
       if (!copy(m, P, false, main, ool)) return false;
     }
     main += ".L" + P + "end:\n";
+    ool += overlay_routines();
     if (!ool.empty()) main += "s_branch .Ldone" + m.n + "\n" + ool;
     out = main;
     return true;
@@ -2162,7 +2205,9 @@ struct Compiler {
     // stalls (SQ_WAIT_INST_ANY doubled; profiles/r02_pmc_checksum_bytecache.json)
     const char* bc = getenv("EBPFEMU_BYTE_CACHE");
     cache = xc.cache = bc && bc[0] == '1';
-    bool only_bytes = !getenv("EBPFEMU_NO_ZERO_WINDOW");
+    // (stack-window programs: the plain refillable windows, the loads' store-forwarding overlay)
+    bool only_bytes = !getenv("EBPFEMU_NO_ZERO_WINDOW") && !stk;
+    if (stk) cache = xc.cache = false;
     for (const Uop& o : uops) only_bytes = only_bytes && (o.op != U_LDX || o.aux == 1);
     zwin = xc.zwin = only_bytes && !cache;
     qcache = xc.qcache = zwin && !getenv("EBPFEMU_NO_QCACHE");
@@ -2179,13 +2224,21 @@ struct Compiler {
   // With bit 1 clear, a program with loads proven in bounds (prove_loads) runs its proven copy.
   bool body_loop_once(const Marker& m, Compiler& xc, std::string& out) {
     const std::string P = "J" + m.n + "_", PX = "J" + m.n + "x_", PC = "J" + m.n + "c_";
+    ovl_tag = m.n;
+    xc.ovl_tag = m.n + "x";
+    overlay_widths = xc.overlay_widths = 0;
+    std::string ool;
+    // (stack-window programs keep the budget's bias in s54 -- the statement's table pointer, which
+    // compiled code never reads -- s57 being the window's address)
+    const std::string B = stk ? "s54" : "s57";
     std::string main = "; compiled eBPF loop program: " + std::to_string(n) + " micro-ops\n"
                        "s_mov_b32 s52, s33\ns_mov_b32 s53, 0\ns_movk_i32 s56, 0xff\n"
-                       "s_not_b32 s57, s71\ns_mov_b64 exec, -1\nv_add_u32 v29, s57, v29\n"
+                       "s_not_b32 " + B + ", s71\ns_mov_b64 exec, -1\nv_add_u32 v29, " + B +
+                       ", v29\n"
                        "v_mov_b32 v55, 0x80000000\n" + window_zero_prologue(m, P) +
                        prefetch_prologue(m, P) +
+                       (stk ? stack_zero() + stack_init(P, ool) : std::string()) +
                        "s_bitcmp1_b32 s70, 0\ns_cbranch_scc1 .L" + PX + "start\n";
-    std::string ool;
     prove_loads();
     const bool any = std::find(inb.begin(), inb.end(), 1) != inb.end();
     if (any) {
@@ -2209,8 +2262,9 @@ struct Compiler {
       err = xc.err;
       return false;
     }
-    main += ".L" + P + "end:\ns_mov_b64 exec, -1\nv_subrev_u32 v29, s57, v29\n" +
+    main += ".L" + P + "end:\ns_mov_b64 exec, -1\nv_subrev_u32 v29, " + B + ", v29\n" +
             std::string(prefetch ? "s_waitcnt vmcnt(0)\n" : "");
+    ool += overlay_routines() + xc.overlay_routines();
     if (!ool.empty()) main += "s_branch .Ldone" + m.n + "\n" + ool;
     out = peephole(main);
     return true;
@@ -2346,7 +2400,8 @@ bool compile_into_template(Compiler& c, Compiler* xc, std::vector<char>& code_ob
     bool ok = true;
     // (stack-window programs: the fixed-slot kernel and the var kernel's stack statement; other
     // programs: every statement but that one)
-    if (loop_marker != (xc != nullptr) || (c.stk ? !(m.fixed == "1" || m.stack) : m.stack))
+    if (loop_marker != (xc != nullptr) ||
+        (c.stk ? !(m.stack || (!loop_marker && m.fixed == "1")) : m.stack))
       b = "s_mov_b64 exec, 0  ; (not this program's kernel)\n";
     else
       ok = xc ? c.body_loop(m, *xc, b) : c.body(m, b);
@@ -2371,7 +2426,6 @@ bool jit_compile(const std::vector<Uop>& uops, const std::vector<TUop>& t,
                  std::vector<char>& code_object, std::string* err, std::string* asm_out,
                  const StackPlan* stk) {
   if (uops.empty() || uops.size() > kJitMaxUops || t.size() < uops.size() ||
-      (stk && uops.size() > kTileMaxUops) ||
       (stk && (stk->k == 0 || stk->k > kStackMax || stk->k % 4 || stk->off.size() != uops.size() ||
                stk->pw.size() != uops.size()))) {
     if (err) *err = "not a tile program";
@@ -2383,13 +2437,15 @@ bool jit_compile(const std::vector<Uop>& uops, const std::vector<TUop>& t,
 
 bool jit_compile_loop(const std::vector<Uop>& uops, const std::vector<TUop>& t,
                       const std::vector<TUop>& tx, std::vector<char>& code_object,
-                      std::string* err, std::string* asm_out) {
+                      std::string* err, std::string* asm_out, const StackPlan* stk) {
   if (uops.empty() || uops.size() > kJitMaxUops || t.size() < uops.size() ||
-      tx.size() < uops.size()) {
+      tx.size() < uops.size() ||
+      (stk && (stk->k == 0 || stk->k > kStackMax || stk->k % 4 || stk->off.size() != uops.size() ||
+               stk->any_pw))) {
     if (err) *err = "not a tile program";
     return false;
   }
-  Compiler c(uops, t, true, false), xc(uops, tx, true, true);
+  Compiler c(uops, t, true, false, stk), xc(uops, tx, true, true, stk);
   return compile_into_template(c, &xc, code_object, err, asm_out);
 }
 
@@ -2400,7 +2456,8 @@ bool jit_load(const std::vector<char>& co, hipModule_t* mod, JitFns* fns) {
   if (hipModuleGetFunction(&f.fixed, m, "ebpf_tile_jit_fixed") != hipSuccess ||
       hipModuleGetFunction(&f.var, m, "ebpf_tile_jit_var") != hipSuccess ||
       hipModuleGetFunction(&f.loop, m, "ebpf_tile_jit_loop") != hipSuccess ||
-      hipModuleGetFunction(&f.var_stack, m, "ebpf_tile_jit_var_stack") != hipSuccess) {
+      hipModuleGetFunction(&f.var_stack, m, "ebpf_tile_jit_var_stack") != hipSuccess ||
+      hipModuleGetFunction(&f.loop_stack, m, "ebpf_tile_jit_loop_stack") != hipSuccess) {
     (void)hipModuleUnload(m);
     return false;
   }

@@ -18,6 +18,7 @@ struct JitFns {
   hipFunction_t var = nullptr;
   hipFunction_t loop = nullptr;  // loop programs (ebpf_tile_jit_loop)
   hipFunction_t var_stack = nullptr;  // stack-window programs, other layouts (ebpf_tile_jit_var_stack)
+  hipFunction_t loop_stack = nullptr;  // stack-window loop programs (ebpf_tile_jit_loop_stack)
 };
 
 // Stack-window programs (memory tier 0.5, host.cpp analyze_stack): every store or atomic writes
@@ -50,7 +51,8 @@ bool jit_compile(const std::vector<Uop>& uops, const std::vector<TUop>& t,
 // table, `tx` the exact one-micro-op-per-block table) for ebpf_tile_jit_loop.
 bool jit_compile_loop(const std::vector<Uop>& uops, const std::vector<TUop>& t,
                       const std::vector<TUop>& tx, std::vector<char>& code_object,
-                      std::string* err, std::string* asm_out = nullptr);
+                      std::string* err, std::string* asm_out = nullptr,
+                      const StackPlan* stk = nullptr);
 
 // Loads a code object on the current device (the functions it does not hold stay null).
 bool jit_load(const std::vector<char>& code_object, hipModule_t* mod, JitFns* fns);

@@ -86,6 +86,32 @@ done:
     exit
 """
 
+# config 5 with its running sum kept in a stack slot (r10 - 8) instead of a register, the way
+# compiled C keeps a spilled accumulator: memory tier 0.5 with a loop (the loop kernel's stack
+# variant). Same verdicts as CHECKSUM.
+CHECKSUM_STACK = """
+    stdw [r10-8], 0
+    mov r3, 0
+    jge r3, r2, done
+loop:
+    mov r4, r1
+    add r4, r3
+    ldxb r5, [r4+0]
+    ldxdw r0, [r10-8]
+    add r0, r5
+    stxdw [r10-8], r0
+    add r3, 1
+    jlt r3, r2, loop
+done:
+    ldxdw r0, [r10-8]
+    mov r6, r0
+    rsh r6, 8
+    xor r0, r6
+    and r0, 1
+    add r0, 1                 # DROP (1) or PASS (2) by parity
+    exit
+"""
+
 # the 5-tuple with its flow key spilled to the stack and read back (memory tier 0.5, the XDP
 # pattern of building a map key at r10 - N): saddr, daddr, protocol and destination port stored
 # at r10 - 16 .. r10 - 5, the decisions taken on the reloaded key. Same verdicts as FIVE_TUPLE.
@@ -326,7 +352,7 @@ out:
 
 PROGRAMS = {"drop": DROP_ALL, "5tuple": FIVE_TUPLE, "checksum": CHECKSUM,
             "5tuple_stack": FIVE_TUPLE_STACK, "mac_swap_tx": MAC_SWAP_TX, "acl": ACL,
-            "5tuple_xdp": FIVE_TUPLE_XDP}
+            "5tuple_xdp": FIVE_TUPLE_XDP, "checksum_stack": CHECKSUM_STACK}
 
 
 def program(name: str) -> bytes:

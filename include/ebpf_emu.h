@@ -214,6 +214,8 @@ int ebpf_run_batch(ebpf_prog* prog, const ebpf_batch* batch, const ebpf_batch_ou
 #define EBPF_KERNEL_JIT_STACK  8  /* compiled stack-window program (memory tier 0.5, fixed slots) */
 #define EBPF_KERNEL_JIT_VAR_STACK 9  /* compiled stack-window program, other layouts
                                         (ebpf_tile_jit_var_stack) */
+#define EBPF_KERNEL_JIT_LOOP_STACK 10 /* compiled stack-window loop program
+                                         (ebpf_tile_jit_loop_stack) */
 int ebpf_batch_kernel(ebpf_prog* prog, const ebpf_batch* batch, const ebpf_batch_out* out,
                       int device);
 

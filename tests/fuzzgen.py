@@ -233,3 +233,76 @@ def gen_call_program(rng: random.Random, n: int | None = None, loops: bool = Fal
             words.append(encode(0xB7 | rng.choice([0, 0x08]), dst, src, 0, _imm(rng)))
     words.append(encode(0x95))
     return b"".join(words)
+
+
+def gen_stack_loop_program(rng: random.Random, k: int = 32) -> bytes:
+    """Stack-window programs with a loop (memory tier 0.5 on the loop kernel): before the loop, r9
+    may point into the stack; the loop runs r7 = 0 .. N - 1 (N a constant or the packet length r2)
+    over a body of stack stores / loads / atomics at r10 offsets, byte and word loads of the
+    packet at r1 + r7 (+ c, some past the 64-byte window, some through registers aimed at the
+    stack window: the store-forwarding overlay), and ALU ops; a forward exit from the body; a
+    tail that folds stack bytes into r0."""
+    sizes = {0x00: 4, 0x08: 2, 0x10: 1, 0x18: 8}
+    words: list[bytes] = []
+    words.append(encode(0xB7, 7, 0, 0, 0))                    # mov r7, 0
+    words.append(encode(0x7A, 10, 0, -8, rng.choice([0, 1, 0x55])))  # stdw [r10-8], c
+    c9 = rng.randrange(0, 9)
+    words.append(encode(0xBF, 9, 10, 0, 0))                   # mov r9, r10
+    words.append(encode(0x07, 9, 0, 0, -c9))                  # add r9, -c9
+    body: list[bytes] = []
+    nb = rng.randrange(3, 12)
+    while len(body) < nb:
+        q = rng.random()
+        size = rng.choice(list(sizes))
+        w = sizes[size]
+        dst = rng.choice([0, 3, 4, 5, 6])
+        src = rng.choice([0, 3, 4, 5, 6, 7])
+        if q < 0.2:  # ST / STX into the window (r10 or r9)
+            d = -rng.randrange(w, k + 1)
+            base, off = (10, d) if rng.random() < 0.6 else (9, d + c9)
+            if rng.random() < 0.3:
+                body.append(encode(0x62 | size, base, 0, off, _imm(rng)))
+            else:
+                body.append(encode(0x63 | size, base, src, off))
+        elif q < 0.35:  # LDX from the window
+            d = -rng.randrange(w, k + 1)
+            body.append(encode(0x61 | size, dst, 10, d))
+        elif q < 0.55:  # packet bytes at r1 + r7 + c
+            body.append(encode(0xBF, 4, 1, 0, 0))               # mov r4, r1
+            body.append(encode(0x0F, 4, 7, 0, 0))               # add r4, r7
+            body.append(encode(0x61 | size, dst if dst != 4 else 5, 4, rng.choice([0, 1, 3, 50, 61, 70, 200])))
+        elif q < 0.62:  # a load aimed at the stack window through a register (overlay)
+            body.append(encode(0xBF, 3, 7, 0, 0))               # mov r3, r7
+            body.append(encode(0x57, 3, 0, 0, 7))               # and r3, 7
+            body.append(encode(0x07, 3, 0, 0, 512 - k + rng.randrange(0, k)))
+            body.append(encode(0x61 | size, dst if dst != 3 else 5, 3, 0))
+        elif q < 0.70:  # a stack atomic
+            d = -4 * rng.randrange(2, k // 4 + 1)
+            aop = rng.choice([0x00, 0x40, 0x50, 0xA0, 0xE0, 0xF0]) | rng.choice([0, 1])
+            body.append(encode(0xC3 | rng.choice([0x00, 0x18]), 10, rng.choice([3, 5, 6]), d, aop))
+        elif q < 0.75:  # leave the loop early
+            body.append(encode(0x55 | rng.choice([0, 0x08]), dst, src, 1 << 10, rng.randrange(0, 300)))
+        else:  # ALU (never r7 / r9 / r10)
+            op = rng.choice([0, 1, 2, 4, 5, 6, 7, 10, 11, 12])
+            body.append(encode((op << 4) | rng.choice([0, 0x08]) | rng.choice([0x04, 0x07]), dst,
+                               src, 0, _imm(rng)))
+    # resolve the early exits (off placeholder 1 << 10) to the loop's end
+    fixed = []
+    for i, wd in enumerate(body):
+        if wd[0] & 0x07 in (0x05, 0x06) and int.from_bytes(wd[2:4], "little") == 1 << 10:
+            wd = wd[:2] + (len(body) - i - 1 + 2).to_bytes(2, "little") + wd[4:]
+        fixed.append(wd)
+    body = fixed
+    words += body
+    words.append(encode(0x07, 7, 0, 0, 1))                    # add r7, 1
+    n = len(body) + 1
+    if rng.random() < 0.5:
+        words.append(encode(0xA5, 7, 0, -(n + 1), rng.randrange(1, 24)))  # jlt r7, N, loop
+    else:
+        words.append(encode(0xAD, 7, 2, -(n + 1)))             # jlt r7, r2, loop
+    words.append(encode(0x79, 3, 10, -8))                      # ldxdw r3, [r10-8]
+    words.append(encode(0x0F, 0, 3, 0, 0))                     # add r0, r3
+    words.append(encode(0x71, 3, 10, -k))                      # ldxb r3, [r10-k]
+    words.append(encode(0xAF, 0, 3, 0, 0))                     # xor r0, r3
+    words.append(encode(0x95))
+    return b"".join(words)

@@ -12,6 +12,7 @@ launches that must fall back to the general interpreter (window over the packet,
 other layouts, init_regs), each still equal to the oracle. Reference: emu.rs:354-372 (ST/STX),
 emu.rs:341-349 (LDX), main.rs:28-31 (r10 = 512)."""
 import random
+import zlib
 
 import numpy as np
 import pytest
@@ -44,7 +45,8 @@ DIRECTED = [
     ("lock add [r10-6], r2\nexit", 0),                             # misaligned atomic
     ("lock add [r1+8], r2\nexit", 0),                              # an atomic on the packet
     ("stxdw [r10-8], r1\ncall 0\nexit", 8),                        # calls (flatten_calls)
-    ("mov r0, 0\nstxb [r10-1], r0\nadd r0, 1\njlt r0, 5, -3\nexit", 0),  # a loop
+    ("mov r0, 0\nstxb [r10-1], r0\nadd r0, 1\njlt r0, 5, -3\nexit", 4),  # a loop (loop kernel)
+    ("mov r0, 0\nstxb [r1+3], r0\nadd r0, 1\njlt r0, 5, -3\nexit", 0),  # + packet store
     ("mov32 r2, r10\nstxb [r2-1], r0\nexit", 0),                   # a truncated pointer
     ("mov r0, 1\nexit", 0),                                        # no store: tier 0
 ]
@@ -115,19 +117,22 @@ def _run(img, frames, n, dev, kernel=None, generic=False, **kw):
         assert got_kernel == kernel, (_lib.KERNEL_NAMES[got_kernel], img.hex())
     res = prog.run(frames, n=n, max_steps=STEPS, verdict=True, r0=True, status=True, regs=True,
                    counters=cnt, generic=generic, mem=mem, **kw)
+    # the production launch (verdict only: the liveness-pruned register init)
+    v = prog.run(frames, n=n, max_steps=STEPS, generic=generic, **kw)
     torch.cuda.synchronize()
     out = dict(status=res.status.cpu().numpy(), r0=res.r0.cpu().numpy().view(np.uint64),
                verdict=res.verdict.cpu().numpy(), regs=res.regs.cpu().numpy().view(np.uint64),
-               counters=cnt.cpu().numpy().view(np.uint64), kernel=got_kernel)
+               counters=cnt.cpu().numpy().view(np.uint64), kernel=got_kernel,
+               prod_verdict=v.verdict.cpu().numpy())
     prog.close()
     return out
 
 
-def _vs_oracle(oracle_mod, img, pkts, got, mem_size=1024, r10=512, tag=""):
+def _vs_oracle(oracle_mod, img, pkts, got, mem_size=1024, r10=512, tag="", max_steps=STEPS):
     op = oracle_mod.Program(img)
     cnt = np.zeros(8, dtype=np.uint64)
     for i, p in enumerate(pkts):
-        st, regs, _m, steps = op.run_full(p, mem_size, r10, STEPS)
+        st, regs, _m, steps = op.run_full(p, mem_size, r10, max_steps)
         ctx = f"{tag} pkt {i} prog {img.hex()}"
         assert got["status"][i] == st, ctx
         if st == 0:
@@ -170,7 +175,7 @@ def test_stack_window_fuzz(cuda, oracle_mod, seed):
         n_stack += got["kernel"] == _lib.EBPF_KERNEL_JIT_STACK
         ref = _run(img, frames, len(pkts), cuda, generic=True, stride=stride)
         assert ref["kernel"] == _lib.EBPF_KERNEL_GENERAL_T1
-        for key in ("status", "r0", "verdict", "regs", "counters"):
+        for key in ("status", "r0", "verdict", "regs", "counters", "prod_verdict"):
             assert np.array_equal(got[key], ref[key]), (key, seed, it, img.hex())
         _vs_oracle(oracle_mod, img, pkts, got, tag=f"seed {seed} it {it}")
         n_run += 1
@@ -204,8 +209,8 @@ def test_stack_window_fallbacks(cuda, oracle_mod):
                lens=lens)
     _vs_oracle(oracle_mod, img, pkts, got, tag="offsets")
     got = _run(img, frames, len(pkts), cuda, kernel=_lib.EBPF_KERNEL_GENERAL_T1, offsets=offs,
-               lens=lens, r10=120)  # (other layouts: the window must lie past byte 64)
-    _vs_oracle(oracle_mod, img, pkts, got, r10=120, tag="offsets r10 120")
+               lens=lens, r10=72)  # (other layouts: the window must lie past byte 64)
+    _vs_oracle(oracle_mod, img, pkts, got, r10=72, tag="offsets r10 72")
     alias = assemble("stxdw [r10-8], r2\nldxdw r0, [r1+504]\nexit")  # reads the window at r1+504
     got = _run(alias, frames, len(pkts), cuda, kernel=_lib.EBPF_KERNEL_GENERAL_T1, stride=128)
     _vs_oracle(oracle_mod, alias, pkts, got, tag="constant alias")
@@ -300,7 +305,7 @@ def test_stack_atomics_and_packet_stores(cuda, oracle_mod):
             frames = _fixed_frames(pkts, stride, cuda)
             got = _run(img, frames, len(pkts), cuda, kernel=_lib.EBPF_KERNEL_JIT_STACK, stride=stride)
             ref = _run(img, frames, len(pkts), cuda, generic=True, stride=stride)
-            for key in ("status", "r0", "verdict", "regs", "counters"):
+            for key in ("status", "r0", "verdict", "regs", "counters", "prod_verdict"):
                 assert np.array_equal(got[key], ref[key]), (key, stride, src)
             _vs_oracle(oracle_mod, img, pkts, got, tag=f"{stride} {src!r}")
 
@@ -331,7 +336,7 @@ def test_stack_atomics_fuzz(cuda, oracle_mod, seed):
         got = _run(img, frames, len(pkts), cuda, stride=stride)
         n_stack += got["kernel"] == _lib.EBPF_KERNEL_JIT_STACK
         ref = _run(img, frames, len(pkts), cuda, generic=True, stride=stride)
-        for key in ("status", "r0", "verdict", "regs", "counters"):
+        for key in ("status", "r0", "verdict", "regs", "counters", "prod_verdict"):
             assert np.array_equal(got[key], ref[key]), (key, seed, it, img.hex())
         _vs_oracle(oracle_mod, img, pkts, got, tag=f"seed {seed} it {it}")
     assert n_stack >= 12, n_stack
@@ -356,7 +361,7 @@ def _var_packets(rng, n):
     return [bytes(rng.getrandbits(8) for _ in range(rng.choice(lens))) for _ in range(n)]
 
 
-def _run_var(img, pkts, dev, layout, generic=False):
+def _run_var(img, pkts, dev, layout, generic=False, max_steps=STEPS):
     import torch
 
     from ebpf_emu import Program
@@ -366,12 +371,12 @@ def _run_var(img, pkts, dev, layout, generic=False):
     xdp = layout.pop("xdp", False)
     frames, kw = _stage(pkts, dev, **layout)
     prog = Program(img)
-    b = prog.make_batch(frames, max_steps=STEPS, generic=generic, xdp_md=xdp, **kw)
+    b = prog.make_batch(frames, max_steps=max_steps, generic=generic, xdp_md=xdp, **kw)
     kernel = prog.batch_kernel(b, None, dev.index or 0)
     cnt = torch.zeros(8, dtype=torch.int64, device=dev)
-    res = prog.run(frames, max_steps=STEPS, r0=True, status=True, regs=True, counters=cnt,
+    res = prog.run(frames, max_steps=max_steps, r0=True, status=True, regs=True, counters=cnt,
                    generic=generic, xdp_md=xdp, **kw)
-    v = prog.run(frames, max_steps=STEPS, xdp_md=xdp, generic=generic, **kw)  # production
+    v = prog.run(frames, max_steps=max_steps, xdp_md=xdp, generic=generic, **kw)  # production
     torch.cuda.synchronize()
     out = dict(status=res.status.cpu().numpy(), r0=res.r0.cpu().numpy().view(np.uint64),
                verdict=res.verdict.cpu().numpy(), regs=res.regs.cpu().numpy().view(np.uint64),
@@ -395,7 +400,7 @@ def test_stack_window_fuzz_var(cuda, oracle_mod, layout):
     the same images, every output, the production verdicts too."""
     from ebpf_emu import Program, _lib
 
-    rng = random.Random(hash(layout) & 0xffff)
+    rng = random.Random(zlib.crc32(layout.encode()))
     n_stack = 0
     for it in range(30):
         img = gen_stack_program(rng, pw_atomics=it % 2 == 1)
@@ -442,3 +447,123 @@ def test_stack_workloads_var(cuda, oracle_mod, layout):
         for key in ("status", "verdict", "counters"):
             assert np.array_equal(got[key], ref[key]), (key, layout, src)
         _vs_oracle(oracle_mod, img, _images_of(pkts, xdp), got, tag=f"{layout} {src!r}")
+
+
+def test_large_stack_programs_compile():
+    """Stack-window programs of 63-256 micro-ops (past the tile interpreter's tables) are memory
+    tier 0.5 too: compiled (the compiler-only tables), with the window in registers."""
+    from ebpf_emu import Program
+
+    rng = random.Random(4048)
+    n_ok = 0
+    for it in range(40):
+        img = gen_stack_program(rng, n=rng.randrange(70, 200), pw_atomics=it % 2 == 1)
+        p = Program(img)
+        if p.stack_window:
+            assert len(p.instructions) > 62
+            assert p.compile(), img.hex()
+            assert "; stack window:" in p.jit_asm(1)
+            n_ok += 1
+        p.close()
+    assert n_ok >= 10, n_ok
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layout", ["fixed", "offsets_mis3", "xdp_offsets"])
+def test_large_stack_programs(cuda, oracle_mod, layout):
+    """Stack-window programs of 63-256 micro-ops on the compiled stack kernels == the general
+    interpreter == the oracle."""
+    from ebpf_emu import Program, _lib
+
+    rng = random.Random(zlib.crc32(b"large" + layout.encode()))
+    n_stack = 0
+    for it in range(12):
+        img = gen_stack_program(rng, n=rng.randrange(70, 200), pw_atomics=it % 2 == 1)
+        p = Program(img)
+        k = p.stack_window
+        p.close()
+        if not k:
+            continue
+        if layout == "fixed":
+            pkts = [bytes(rng.getrandbits(8) for _ in range(128)) for _ in range(100)]
+            frames = _fixed_frames(pkts, 128, cuda)
+            got = _run(img, frames, len(pkts), cuda, stride=128)
+            ref = _run(img, frames, len(pkts), cuda, generic=True, stride=128)
+            want = _lib.EBPF_KERNEL_JIT_STACK
+            xdp = False
+        else:
+            pkts = _var_packets(rng, 100)
+            got, xdp = _run_var(img, pkts, cuda, VAR_LAYOUTS[layout])
+            ref, _ = _run_var(img, pkts, cuda, VAR_LAYOUTS[layout], generic=True)
+            want = _lib.EBPF_KERNEL_JIT_VAR_STACK
+        n_stack += got["kernel"] == want
+        ok = got["status"] != 7
+        for key in ("status", "verdict", "counters", "prod_verdict"):
+            assert np.array_equal(got[key], ref[key]), (key, layout, it, img.hex())
+        for key in ("r0", "regs"):
+            assert np.array_equal(got[key][ok], ref[key][ok]), (key, layout, it, img.hex())
+        _vs_oracle(oracle_mod, img, _images_of(pkts, xdp), got, tag=f"{layout} it {it}")
+    assert n_stack >= 4, n_stack
+
+
+# ---------------------------------------------------------------------------------------------
+# Stack-window programs with loops (or a binding step budget): the loop kernel's stack variant
+# (ebpf_tile_jit_loop_stack). STACK_SUM keeps its running sum at r10 - 8 (workloads.CHECKSUM_STACK
+# is the checksum written that way).
+STACK_SUM = """
+    mov r0, 0
+    stdw [r10-8], 0
+    mov r3, 0
+    jge r3, r2, done
+loop:
+    mov r4, r1
+    add r4, r3
+    ldxb r5, [r4+0]
+    ldxdw r6, [r10-8]
+    add r6, r5
+    stxdw [r10-8], r6
+    add r3, 1
+    jlt r3, r2, loop
+done:
+    ldxdw r0, [r10-8]
+    exit
+"""
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layout", ["offsets16", "offsets_mis3", "stride_lens", "xdp_offsets"])
+def test_stack_loop_programs(cuda, oracle_mod, layout):
+    """Random stack-window loop programs (gen_stack_loop_program) and STACK_SUM: the loop
+    kernel's stack variant == the general interpreter == the oracle, every output, budgets that
+    bind included; the forward 5-tuple-with-key under a binding budget too."""
+    from ebpf_emu import Program, _lib
+    from ebpf_emu import workloads as W
+    from ebpf_emu.asm import assemble
+
+    rng = random.Random(zlib.crc32(b"loops" + layout.encode()))
+    progs = [assemble(STACK_SUM), W.program("checksum_stack"), W.program("5tuple_stack")]
+    progs += [gen_stack_loop_program(rng) for _ in range(16)]
+    n_stack = 0
+    for it, img in enumerate(progs):
+        p = Program(img)
+        k = p.stack_window
+        p.close()
+        if not k:
+            continue
+        for steps in ((3000, 37) if it % 2 == 0 else (3000,)):
+            pkts = _var_packets(rng, rng.choice([64, 100]))
+            got, xdp = _run_var(img, pkts, cuda, VAR_LAYOUTS[layout], max_steps=steps)
+            if it == 2 and steps == 3000:  # (forward, budget that cannot bind: forward kernels)
+                assert got["kernel"] in (_lib.EBPF_KERNEL_JIT_VAR_STACK,), layout
+            else:
+                assert got["kernel"] == _lib.EBPF_KERNEL_JIT_LOOP_STACK, (layout, it, img.hex())
+                n_stack += 1
+            ref, _ = _run_var(img, pkts, cuda, VAR_LAYOUTS[layout], generic=True, max_steps=steps)
+            ok = got["status"] != 7
+            for key in ("status", "verdict", "counters", "prod_verdict"):
+                assert np.array_equal(got[key], ref[key]), (key, layout, it, steps, img.hex())
+            for key in ("r0", "regs"):
+                assert np.array_equal(got[key][ok], ref[key][ok]), (key, layout, it, steps, img.hex())
+            _vs_oracle(oracle_mod, img, _images_of(pkts, xdp), got, tag=f"{layout} it {it}",
+                       max_steps=steps)
+    assert n_stack >= 12, n_stack
