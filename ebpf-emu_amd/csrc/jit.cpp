@@ -1614,7 +1614,9 @@ struct Compiler {
       s += std::string(w <= 4 ? "v_mov_b32 v27, 0\n" : "") +
            "v_sub_u32 v46, v31, v36\nv_cmp_lt_u32 vcc, v36, v31\nv_cndmask_b32 v46, 0, v46, vcc\n"
            "v_min_u32 v46, 8, v46\nv_lshlrev_b32 v46, 3, v46\nv_sub_u32 v46, 64, v46\n"
-           "v_lshlrev_b64 v[26:27], v46, v[26:27]\nv_lshrrev_b64 v[26:27], v46, v[26:27]\n";
+           "v_lshlrev_b64 v[26:27], v46, v[26:27]\nv_lshrrev_b64 v[26:27], v46, v[26:27]\n"
+           // (a shift by 64 is one by 0: an access at or past LEN is zeroed by the select)
+           "v_cndmask_b32 v26, 0, v26, vcc\nv_cndmask_b32 v27, 0, v27, vcc\n";
     if (stk) s += stack_overlay(U, w, ool);
     if (w == 1 || w == 2)
       s += "s_mov_b32 s42, " + std::string(w == 1 ? "0xff" : "0xffff") + "\nv_bfi_b32 " + D0 +

@@ -17,7 +17,7 @@ import zlib
 import numpy as np
 import pytest
 
-from fuzzgen import gen_packet, gen_stack_program
+from fuzzgen import gen_packet, gen_stack_loop_program, gen_stack_program
 
 STEPS = 20000
 
@@ -171,7 +171,10 @@ def test_stack_window_fuzz(cuda, oracle_mod, seed):
         frames = _fixed_frames(pkts, stride, cuda)
         # (a constant-address load into the window sends the batch to the general interpreter)
         got = _run(img, frames, len(pkts), cuda, stride=stride)
-        assert got["kernel"] in (_lib.EBPF_KERNEL_JIT_STACK, _lib.EBPF_KERNEL_GENERAL_T1)
+        # (a constant-address load into the window: the loop kernel's stack variant, whose loads
+        # all take the store-forwarding overlay)
+        assert got["kernel"] in (_lib.EBPF_KERNEL_JIT_STACK, _lib.EBPF_KERNEL_JIT_LOOP_STACK,
+                                 _lib.EBPF_KERNEL_GENERAL_T1)
         n_stack += got["kernel"] == _lib.EBPF_KERNEL_JIT_STACK
         ref = _run(img, frames, len(pkts), cuda, generic=True, stride=stride)
         assert ref["kernel"] == _lib.EBPF_KERNEL_GENERAL_T1
@@ -200,7 +203,11 @@ def test_stack_window_fallbacks(cuda, oracle_mod):
     frames = _fixed_frames(pkts, 128, cuda)
     ok = _run(img, frames, len(pkts), cuda, kernel=_lib.EBPF_KERNEL_JIT_STACK, stride=128)
     _vs_oracle(oracle_mod, img, pkts, ok, tag="eligible")
-    for kw, r10 in ((dict(r10=96), 96), (dict(r10=510), 510), (dict(mem=True), 512)):
+    # (the window over packet bytes: the loop kernel's stack variant, which loads them at the start)
+    got = _run(img, frames, len(pkts), cuda, kernel=_lib.EBPF_KERNEL_JIT_LOOP_STACK, stride=128,
+               r10=96)
+    _vs_oracle(oracle_mod, img, pkts, got, r10=96, tag="r10 96")
+    for kw, r10 in ((dict(r10=510), 510), (dict(mem=True), 512)):
         got = _run(img, frames, len(pkts), cuda, kernel=_lib.EBPF_KERNEL_GENERAL_T1, stride=128, **kw)
         _vs_oracle(oracle_mod, img, pkts, got, r10=r10, tag=str(kw))
     lens = torch.tensor(np.full(len(pkts), 128, dtype=np.int16), device=cuda)
@@ -212,7 +219,7 @@ def test_stack_window_fallbacks(cuda, oracle_mod):
                lens=lens, r10=72)  # (other layouts: the window must lie past byte 64)
     _vs_oracle(oracle_mod, img, pkts, got, r10=72, tag="offsets r10 72")
     alias = assemble("stxdw [r10-8], r2\nldxdw r0, [r1+504]\nexit")  # reads the window at r1+504
-    got = _run(alias, frames, len(pkts), cuda, kernel=_lib.EBPF_KERNEL_GENERAL_T1, stride=128)
+    got = _run(alias, frames, len(pkts), cuda, kernel=_lib.EBPF_KERNEL_JIT_LOOP_STACK, stride=128)
     _vs_oracle(oracle_mod, alias, pkts, got, tag="constant alias")
     # register-address loads into the window (r3 = len + 376 = 504: not a load-time constant),
     # wholly and partly inside it: the store-forwarding overlay
@@ -415,7 +422,8 @@ def test_stack_window_fuzz_var(cuda, oracle_mod, layout):
             continue
         pkts = _var_packets(rng, rng.choice([64, 100, 130]))
         got, xdp = _run_var(img, pkts, cuda, VAR_LAYOUTS[layout])
-        assert got["kernel"] in (_lib.EBPF_KERNEL_JIT_VAR_STACK, _lib.EBPF_KERNEL_GENERAL_T1)
+        assert got["kernel"] in (_lib.EBPF_KERNEL_JIT_VAR_STACK, _lib.EBPF_KERNEL_JIT_LOOP_STACK,
+                                 _lib.EBPF_KERNEL_GENERAL_T1)
         n_stack += got["kernel"] == _lib.EBPF_KERNEL_JIT_VAR_STACK
         ref, _ = _run_var(img, pkts, cuda, VAR_LAYOUTS[layout], generic=True)
         assert ref["kernel"] == _lib.EBPF_KERNEL_GENERAL_T1
