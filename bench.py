@@ -59,6 +59,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", choices=sorted(CONFIGS), default="5tuple")
     ap.add_argument("--packets", type=int, default=1 << 20, help="packets per batch per GPU")
+    ap.add_argument("--layout", choices=["fixed", "offsets"], default="fixed",
+                    help="64-byte-frame configs: fixed slots (a NIC ring), or the same frames as an "
+                         "offsets + lens batch (a pcap capture's layout: the var kernels)")
     ap.add_argument("--frame-bytes", type=int, default=64,
                     help="fixed-slot configs: bytes per frame slot (rounded up to 16; e.g. 1500)")
     ap.add_argument("--total-packets", type=int, default=0,
@@ -108,6 +111,9 @@ def main():
         cfg_idx = 3 if args.config == "5tuple" else cfg_idx
     if args.frame_bytes != 64 and args.config != "checksum":
         desc = desc.replace("64B frames", f"{(max(64, args.frame_bytes) + 15) // 16 * 16}B frame slots")
+    if args.layout == "offsets":
+        desc += " (offsets + lens batch)"
+        assert not args.total_packets and args.config not in ("checksum", "checksum_stack")
     n = args.packets
     img = W.program(PROGRAM_OF.get(args.config, args.config))
     prog = Program(img)
@@ -145,7 +151,12 @@ def main():
         elif fb == 64 or k == 0:
             buf = W.frames_fixed(n, fb, cid)
             batches.append(dict(frames=torch.from_numpy(buf).to(dev)))
-            algo_bytes = n * (64 + 1)  # the bytes a header program touches: its 64-byte window
+            if args.layout == "offsets":  # the same frames through u32 offsets + u16 lengths
+                batches[-1]["offsets"] = torch.from_numpy(
+                    (np.arange(n, dtype=np.int64) * fb).astype(np.uint32).view(np.int32)).to(dev)
+                batches[-1]["lens"] = torch.from_numpy(np.full(n, fb, dtype=np.int16)).to(dev)
+            # the bytes a header program touches: its 64-byte window (+ offset and length)
+            algo_bytes = n * (64 + 1 + (6 if args.layout == "offsets" else 0))
         else:  # large slots: copies of the first batch at other addresses (host RNG is slow)
             batches.append(dict(frames=batches[0]["frames"].clone()))
         # (the bytes a launch touches decide whether the pool outgrows the Infinity Cache)
@@ -165,7 +176,8 @@ def main():
             bd = prog.make_batch(b["frames"], n=n, offsets=b["offsets"], lens=b["lens"],
                                  mem_size=mem_size, r10=r10, generic=args.generic)
         else:
-            bd = prog.make_batch(b["frames"], n=n, stride=fb, mem_size=mem_size, r10=r10,
+            bd = prog.make_batch(b["frames"], n=n, stride=fb, offsets=b.get("offsets"),
+                                 lens=b.get("lens"), mem_size=mem_size, r10=r10,
                                  generic=args.generic, xdp_md=args.config == "xdp")
         descs.append(bd)
     out = _lib.BatchOut()
@@ -239,7 +251,7 @@ def main():
     # SQ_INSTS_VALU), collected by tools/pmc.sh into the committed summary
     traffic = None
     issue = None
-    suffix = "" if mixed or fb == 64 else f"_{fb}B"
+    suffix = ("" if mixed or fb == 64 else f"_{fb}B") + ("_offsets" if args.layout == "offsets" else "")
     pj = args.pmc_json or os.path.join(ROOT, "profiles", f"pmc_{args.config}{suffix}.json")
     pmc_note = None
     if os.path.exists(pj) and not args.total_packets and n == 1 << 20 and not args.generic:

@@ -247,12 +247,17 @@ struct ebpf_prog {
   // program (ltuops + ltuopsx). jit_state: 0 not compiled yet, 1 compiled, 2 not a compiled
   // program, < 0 failed
   int jit_state = 0;
-  bool jit_has[3] = {};
-  std::vector<char> jit_co[3];
-  std::string jit_asm[3];
+  bool jit_has[kJitVariants] = {};
+  std::vector<char> jit_co[kJitVariants];
+  std::string jit_asm[kJitVariants];
   std::string jit_err;
-  hipModule_t jit_mod[kMaxDevices][3] = {};
-  JitFns jit_fn[kMaxDevices][3];
+  hipModule_t jit_mod[kMaxDevices][kJitVariants] = {};
+  JitFns jit_fn[kMaxDevices][kJitVariants];
+  // xdp_md batches: the forward table with the ctx's data field (8) known at load time, so a
+  // standard XDP program's `ldxw rD, [r1 + 0]` (ctx->data) is the constant 8 and its packet
+  // loads through rD are constant-address loads (fold_const_loads xdp); variant 3 when it
+  // differs from tuopsk
+  std::vector<TUop> tuopsk_xdp;
 };
 
 // Diagnostics: EBPFEMU_TRACE=1 gives the compiled fixed-slot kernel a per-device stamp buffer
@@ -276,17 +281,20 @@ static int jit_compile_locked(ebpf_prog* p) {
   if (p->jit_state == 0) {
     p->jit_has[0] = p->jit_has[1] = !p->tuops.empty() && !p->tuopsk.empty();
     p->jit_has[2] = !p->ltuops.empty() && !p->ltuopsx.empty();
+    p->jit_has[3] = !p->tuopsk_xdp.empty() && !p->stack.k;
     if (p->stack.k) p->jit_has[1] = !p->tuopsk.empty();  // (the main.rs layout only)
     if (g_no_jit || (!p->jit_has[0] && !p->jit_has[1] && !p->jit_has[2])) {
       p->jit_state = 2;
     } else {
       p->jit_state = 1;
-      for (int v = 0; v < 3 && p->jit_state == 1; v++) {
+      for (int v = 0; v < kJitVariants && p->jit_state == 1; v++) {
         if (!p->jit_has[v]) continue;
         const bool ok = v == 2 ? jit_compile_loop(p->xuops, p->ltuops, p->ltuopsx, p->jit_co[v],
                                                   &p->jit_err, &p->jit_asm[v],
                                                   p->stack.k ? &p->stack : nullptr)
-                               : jit_compile(p->xuops, v ? p->tuopsk : p->tuops, p->jit_co[v],
+                               : jit_compile(p->xuops,
+                                             v == 3 ? p->tuopsk_xdp : v ? p->tuopsk : p->tuops,
+                                             p->jit_co[v],
                                              &p->jit_err, &p->jit_asm[v],
                                              p->stack.k ? &p->stack : nullptr);
         if (!ok && v >= 1 && p->stack.k && !p->jit_has[0]) {
@@ -537,16 +545,21 @@ static std::vector<TUop> build_tile(const std::vector<Uop>& uops, const std::vec
 // per-batch). Every LDX whose base register holds one known constant on all paths into it
 // becomes U_LDXK with its address resolved, so the kernel neither reads that register nor
 // waits on it before reading the packet window. Only used for batches without init_regs.
-static std::vector<DUop> fold_const_loads(const std::vector<Uop>& uops, std::vector<DUop> d) {
+// xdp: the image starts with the xdp_md ctx (xdp.rs:16-20), whose data field is 8 on every lane:
+// a 4-byte load of image address 0 into a register whose upper half is known zero (the loaded
+// bytes replace only the low four, Q1) leaves the constant 8 -- r2 = 8 + len starts below 2^32.
+static std::vector<DUop> fold_const_loads(const std::vector<Uop>& uops, std::vector<DUop> d,
+                                          bool xdp = false) {
   const uint32_t n = (uint32_t)uops.size();
   struct Regs {
     bool reached = false;
     bool known[11] = {};
+    bool hz[11] = {};  // the upper 32 bits are known to be zero
     uint64_t v[11] = {};
   };
   std::vector<Regs> in(n + 1);
   in[0].reached = true;
-  for (int r = 0; r < 11; r++) in[0].known[r] = (r != 2 && r != 10);
+  for (int r = 0; r < 11; r++) in[0].known[r] = (r != 2 && r != 10), in[0].hz[r] = r != 10;
   auto flow = [&](uint32_t to, const Regs& s) {
     if (to >= n) return;
     Regs& t = in[to];
@@ -554,14 +567,19 @@ static std::vector<DUop> fold_const_loads(const std::vector<Uop>& uops, std::vec
       t = s;
       return;
     }
-    for (int r = 0; r < 11; r++)
+    for (int r = 0; r < 11; r++) {
       if (t.known[r] && !(s.known[r] && s.v[r] == t.v[r])) t.known[r] = false;
+      t.hz[r] = t.hz[r] && s.hz[r];
+    }
   };
   for (uint32_t i = 0; i < n; i++) {
     if (!in[i].reached) continue;
     const Uop& u = uops[i];
     Regs s = in[i];
     const bool src = u.aux & F_SRC;
+    const bool ctx_data = xdp && u.op == U_LDX && u.aux == 4 && s.known[u.src] &&
+                          s.v[u.src] + (uint64_t)(int64_t)u.x == 0 && s.hz[u.dst];
+    const bool dst_hz = s.hz[u.dst];
     if (u.op == U_LDX && s.known[u.src]) {
       int64_t a;
       DUop& o = d[i];
@@ -627,6 +645,23 @@ static std::vector<DUop> fold_const_loads(const std::vector<Uop>& uops, std::vec
         s.known[u.dst] = false;
         break;
     }
+    // the upper halves: constants; 32-bit results (zero-extended, emu.rs:214-216); loads of at
+    // most 4 bytes into a register whose upper half was zero
+    if (u.op == U_LDX) {
+      s.hz[u.dst] = dst_hz && u.aux <= 4;
+      if (ctx_data) s.known[u.dst] = true, s.v[u.dst] = 8;
+    } else if (u.op == U_MOV64) {
+      s.hz[u.dst] = src ? s.hz[u.src] : (uint64_t)u.k >> 32 == 0;
+    } else if ((u.op >= U_ADD32 && u.op <= U_ARSH32) || u.op == U_ZX16 || u.op == U_ZX32 ||
+               u.op == U_BSWAP16 || u.op == U_BSWAP32) {
+      s.hz[u.dst] = true;
+    } else if (u.op == U_ATOMIC) {
+      s.hz[u.src] = s.hz[0] = false;
+    } else if (u.op != U_NOP && u.op != U_ST && u.op != U_STX) {
+      s.hz[u.dst] = false;
+    }
+    for (int r = 0; r < 11; r++)
+      if (s.known[r]) s.hz[r] = s.v[r] >> 32 == 0;
     flow(i + 1, s);
   }
   return d;
@@ -1014,6 +1049,10 @@ int ebpf_prog_load(const uint8_t* code, size_t nbytes, ebpf_prog** out, size_t* 
     if (xu.size() <= kJitMaxUops) {  // tile_kernel's (<= 62) and the compiler's tables
       p->tuops = build_tile(xu, p->duops);
       p->tuopsk = build_tile(xu, p->duopsk);
+      std::vector<TUop> tx = build_tile(xu, fold_const_loads(xu, p->duops, true));
+      if (tx.size() != p->tuopsk.size() ||
+          std::memcmp(tx.data(), p->tuopsk.data(), tx.size() * sizeof(TUop)) != 0)
+        p->tuopsk_xdp = std::move(tx);
     }
   }
   // (past kTileMaxUops: tables for the compiled loop program only, batch_kind)
@@ -1075,7 +1114,7 @@ void ebpf_prog_free(ebpf_prog* p) {
       if (p->dev_ltuops[d]) hipFree(p->dev_ltuops[d]);
       if (p->dev_ltuopsx[d]) hipFree(p->dev_ltuopsx[d]);
     }
-    for (int v = 0; v < 3; v++)
+    for (int v = 0; v < kJitVariants; v++)
       if (p->jit_mod[d][v]) {
         hipSetDevice(d);
         (void)hipModuleUnload(p->jit_mod[d][v]);
@@ -1113,7 +1152,7 @@ int ebpf_prog_compile(ebpf_prog* p) {
 }
 
 int ebpf_prog_jit_asm(ebpf_prog* p, int variant, char* buf, size_t cap, size_t* len) {
-  if (!p || variant < 0 || variant > 2) return EBPF_EINVAL;
+  if (!p || variant < 0 || variant >= kJitVariants) return EBPF_EINVAL;
   std::lock_guard<std::mutex> lk(p->mu);
   if (jit_compile_locked(p) != 1 || !p->jit_has[variant]) return EBPF_EINVAL;
   const std::string& a = p->jit_asm[variant];
@@ -1171,7 +1210,7 @@ int ebpf_prog_upload(ebpf_prog* p, int device) {
   putt(p->ltuopsx, &tlx);
   // the compiled program's modules on this device (a compiler failure leaves the interpreter)
   if (rc == EBPF_OK && jit_compile_locked(p) == 1) {
-    for (int v = 0; v < 3 && rc == EBPF_OK; v++)
+    for (int v = 0; v < kJitVariants && rc == EBPF_OK; v++)
       if (p->jit_has[v] &&
           !jit_load(p->jit_co[v], &p->jit_mod[device][v], &p->jit_fn[device][v]))
         rc = EBPF_EHIP;
@@ -1297,7 +1336,9 @@ static int batch_kind(const ebpf_prog* p, const ebpf_batch* b, const ebpf_batch_
 static const JitFns* batch_jit(ebpf_prog* p, const ebpf_batch* b, int kind, bool stk, int device) {
   if (stk) return &p->jit_fn[device][kind == kKindLoop ? 2 : 1];
   if (b->flags & EBPF_BATCH_NO_JIT) return nullptr;
-  if (kind == kKindDag && p->jit_mod[device][0]) return &p->jit_fn[device][b->init_regs ? 0 : 1];
+  if (kind == kKindDag && p->jit_mod[device][0])
+    return &p->jit_fn[device][b->init_regs ? 0
+                              : (b->flags & EBPF_BATCH_XDP_MD) && p->jit_mod[device][3] ? 3 : 1];
   if (kind == kKindLoop && p->jit_mod[device][2]) return &p->jit_fn[device][2];
   return nullptr;
 }

@@ -25,6 +25,10 @@ struct JitFns {
 // the window [r10 - k, r10) at an offset known at load time, so the window lives in VGPRs of the
 // compiled fixed-slot kernel (v[kStackVgpr : kStackVgpr + k/4]); stores may also write the
 // packet's header window at constant addresses (the preloaded window dwords v[64 : 79]).
+// compiled variants of a program: 0 init_regs batches, 1 the main.rs layout (constant-address
+// loads resolved), 2 the loop kernel, 3 xdp_md batches (the ctx's data field known, host.cpp
+// fold_const_loads)
+constexpr int kJitVariants = 4;
 constexpr uint32_t kStackMax = 64;    // window bytes
 constexpr uint32_t kStackVgpr = 80;   // first VGPR of the window (ebpf_tile_jit_fixed)
 constexpr int32_t kNoStack = INT32_MIN;

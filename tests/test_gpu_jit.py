@@ -133,6 +133,33 @@ def test_loop_range_proofs_compile():
     assert 6 <= proven <= 54, proven
 
 
+def test_xdp_ctx_data_folded():
+    """xdp_md batches get a compiled variant of their own (host.cpp fold_const_loads xdp) where a
+    standard XDP program's ctx->data load is the constant 8 and the packet loads through it are
+    constant-address loads; programs that gain nothing from it get none."""
+    from ebpf_emu import Program
+    from ebpf_emu import workloads as W
+    from ebpf_emu.asm import assemble
+    from test_gpu_xdp_md import XDP_CTX_MIX, XDP_PARSE
+
+    def body(text):
+        b = text[text.index("; JIT N=0"):]
+        b = b[b.index("; compiled eBPF program"):]
+        return b[:b.index(".Ldone")].count("\n")
+
+    for img in (W.program("5tuple_xdp"), assemble(XDP_PARSE)):
+        p = Program(img)
+        assert p.compile()
+        assert body(p.jit_asm(3)) < body(p.jit_asm(1))
+        p.close()
+    for img in (W.program("5tuple"), assemble(XDP_CTX_MIX)):
+        p = Program(img)
+        assert p.compile()
+        with pytest.raises(Exception):
+            p.jit_asm(3)
+        p.close()
+
+
 # ---------------------------------------------------------------------------------------------
 def _run(img, pkts, dev, fixed_stride=None, offsets_layout=False, init_regs=None, no_jit=False,
          mem_size=1024, r10=512, prod=False):

@@ -275,3 +275,4 @@ def test_xdp_md_loop_programs_staged(cuda):
     assert _route(prog, frames, kw) == _lib.EBPF_KERNEL_JIT_LOOP
     prog.close()
     del torch
+
