@@ -48,8 +48,12 @@ CONFIGS = {
     # config 5 with the running sum in a stack slot (memory tier 0.5 with a loop: the loop kernel's
     # stack variant; --generic: the general interpreter's tier 1)
     "checksum_stack": (4, "per-byte checksum loop, sum kept at r10-8, over 1Mi mixed 64B/1500B frames"),
+    # the 5-tuple with its L4 decision in a local function (CALL / EXIT flattened at load time onto
+    # the compiled kernel; --generic: the general interpreter's frame stack), same verdicts
+    "call": (2, "IPv4 5-tuple with the L4 decision as a local call (35 insns) over 1Mi x 64B frames"),
 }
-PROGRAM_OF = {"stack": "5tuple_stack", "tier1": "mac_swap_tx", "xdp": "5tuple_xdp"}
+PROGRAM_OF = {"stack": "5tuple_stack", "tier1": "mac_swap_tx", "xdp": "5tuple_xdp",
+              "call": "5tuple_call"}
 
 
 def parse():

@@ -350,9 +350,60 @@ out:
     exit
 """
 
+# the 5-tuple with its L4 decision as a local function (CALL, emu.rs:265-279), the pattern of a
+# bpf-to-bpf call. The reference pushes the callee's entry + 1 as the return address (Q12), so
+# l4's EXIT returns into l4 itself: its body after the first instruction runs a second time and
+# that EXIT, with the frame stack empty, ends the program. The body is idempotent, so the verdicts
+# are FIVE_TUPLE's. On the compiled kernels the calls are flattened at load time (flatten_calls).
+FIVE_TUPLE_CALL = """
+    mov r0, 2                 # default XDP_PASS
+    jlt r2, 34, out
+    ldxh r3, [r1+12]          # EtherType
+    jne r3, 0x0008, out
+    ldxb r4, [r1+14]
+    and r4, 0x0f
+    lsh r4, 2                 # IHL * 4
+    jlt r4, 20, drop
+    ldxb r5, [r1+23]          # protocol
+    ldxw r6, [r1+26]          # saddr
+    ldxw r7, [r1+30]          # daddr
+    call l4
+drop:
+    mov r0, 1                 # XDP_DROP
+out:
+    exit
+l4:
+    mov r0, 2                 # skipped by the return pass (entry + 1)
+    mov r8, r1
+    add r8, r4                # r8 + 14 = L4 header
+    jeq r5, 1, icmp
+    jeq r5, 17, udp
+    jne r5, 6, l4_out
+    ldxh r9, [r8+16]          # TCP dport
+    be16 r9
+    jge r9, 1024, l4_out
+    and r6, 0xff
+    jeq r6, 10, l4_drop
+    ja l4_out
+udp:
+    ldxh r9, [r8+16]          # UDP dport
+    be16 r9
+    jeq r9, 53, l4_drop
+    ja l4_out
+icmp:
+    and r7, 0xf0
+    jeq r7, 0xe0, l4_drop
+    ja l4_out
+l4_drop:
+    mov r0, 1
+l4_out:
+    exit
+"""
+
 PROGRAMS = {"drop": DROP_ALL, "5tuple": FIVE_TUPLE, "checksum": CHECKSUM,
             "5tuple_stack": FIVE_TUPLE_STACK, "mac_swap_tx": MAC_SWAP_TX, "acl": ACL,
-            "5tuple_xdp": FIVE_TUPLE_XDP, "checksum_stack": CHECKSUM_STACK}
+            "5tuple_xdp": FIVE_TUPLE_XDP, "checksum_stack": CHECKSUM_STACK,
+            "5tuple_call": FIVE_TUPLE_CALL}
 
 
 def program(name: str) -> bytes:

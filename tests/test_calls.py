@@ -132,3 +132,51 @@ def test_fuzz_call_programs(cuda, oracle_mod, seed):
         _same_outputs(full, gen, f"seed {seed} it {it} {img.hex()}")
     compiled = sum(v for k, v in routes.items() if "general" not in k.lower())
     assert compiled >= 10, routes
+
+
+def test_call_workload_verdicts_cpu(oracle_mod):
+    """workloads.FIVE_TUPLE_CALL (the L4 decision as a local function) returns the 5-tuple's
+    verdicts in the oracle (its callee body is idempotent under the reference's entry + 1 return
+    address), and flattens onto the compiled kernels."""
+    from ebpf_emu import Program
+    from ebpf_emu import workloads as W
+
+    frames = W.frames_fixed(2048, 64)
+    pkts = [bytes(frames[i * 64:(i + 1) * 64]) for i in range(2048)]
+    a = oracle_mod.Program(W.program("5tuple_call"))
+    b = oracle_mod.Program(W.program("5tuple"))
+    for p in pkts:
+        sa, ra, _m, _s = a.run_full(p, 1024, 512, 10000)
+        sb, rb, _m, _s = b.run_full(p, 1024, 512, 10000)
+        assert (sa, ra[0]) == (sb, rb[0])
+    p = Program(W.program("5tuple_call"))
+    assert p.forward_only and p.compile()
+    p.close()
+
+
+@pytest.mark.gpu
+def test_call_workload(cuda, oracle_mod):
+    """The bench's call workload on 8192 frames: routed to the compiled fixed-slot kernel,
+    compiled == general interpreter (frame stack) == oracle."""
+    import torch
+
+    from ebpf_emu import Program, _lib
+    from ebpf_emu import workloads as W
+    from test_gpu_jit import _run, _same, _vs_oracle, _cnt
+
+    img = W.program("5tuple_call")
+    frames = W.frames_fixed(8192, 64)
+    pkts = [bytes(frames[i * 64:(i + 1) * 64]) for i in range(8192)]
+    p = Program(img)
+    dev = torch.zeros(64 * 64, dtype=torch.uint8, device=cuda)
+    assert p.batch_kernel(p.make_batch(dev, n=64, stride=64)) == _lib.EBPF_KERNEL_JIT_FIXED
+    p.close()
+    got = _run(img, pkts, cuda, fixed_stride=64)
+    gen = _run_full(img, pkts[:1024], cuda, generic=True)
+    assert (got["status"][:1024] == gen["status"]).all()
+    assert (got["r0"][:1024] == gen["regs"][:, 0]).all()
+    sub = {k: v[:512] for k, v in got.items() if k != "counters"}
+    sub["counters"] = _cnt(oracle_mod, img, pkts[:512])
+    _vs_oracle(oracle_mod, img, pkts[:512], sub, tag="5tuple_call")
+    prod = _run(img, pkts, cuda, fixed_stride=64, prod=True)  # the bench's outputs
+    _same(prod, got, "5tuple_call prod", keys=("status", "r0", "verdict", "counters"))

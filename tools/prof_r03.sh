@@ -7,6 +7,7 @@ R=$PWD
 B="$R/bench.py --cpu-seconds 0"
 P="rocprofv3 --kernel-trace --stats --output-format csv"
 bash tools/gpu_session.sh \
+  "tcall|300|python -u -m pytest tests/test_calls.py tests/test_gpu_xdp_md.py -x -v -m gpu --timeout 120 --timeout-method thread" \
   "pxdp|180|cd /tmp && $P -d $R/gpurun_out/pxdp -o run -- python3 $B --steps 100 --config xdp" \
   "pstko|180|cd /tmp && $P -d $R/gpurun_out/pstko -o run -- python3 $B --steps 100 --config stack --layout offsets" \
   "pcs|240|cd /tmp && $P -d $R/gpurun_out/pcs -o run -- python3 $B --steps 20 --warmup 3 --config checksum_stack" \
@@ -14,4 +15,9 @@ bash tools/gpu_session.sh \
   "bxdp|200|python bench.py --config xdp" \
   "bstko|200|python bench.py --config stack --layout offsets" \
   "bstkog|200|python bench.py --config stack --layout offsets --generic --steps 20 --warmup 3 --cpu-seconds 0" \
-  "b5o|200|python bench.py --layout offsets --cpu-seconds 0"
+  "b5o|200|python bench.py --layout offsets --cpu-seconds 0" \
+  "pcall|180|cd /tmp && $P -d $R/gpurun_out/pcall -o run -- python3 $B --steps 100 --config call" \
+  "bcall|200|python bench.py --config call" \
+  "bcallg|200|python bench.py --config call --generic --steps 20 --warmup 3 --cpu-seconds 0" \
+  "b5|200|python bench.py --cpu-seconds 0" \
+  "b5spin|200|EBPFEMU_BENCH_SPIN=1 python bench.py --cpu-seconds 0"
