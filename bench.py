@@ -44,7 +44,7 @@ CONFIGS = {
     # the 5-tuple as a standard XDP program under the xdp_md calling convention (xdp.rs:16-20:
     # r1 = ctx, data / data_end read from it), same frames as 5tuple; the ctx is synthesised in
     # the kernel's window (no staging copy)
-    "xdp": (2, "IPv4 5-tuple as a standard XDP program, xdp_md ctx (37 insns) over 1Mi x 64B frames"),
+    "xdp": (2, "IPv4 5-tuple as a standard XDP program, xdp_md ctx (38 insns) over 1Mi x 64B frames"),
     # config 5 with the running sum in a stack slot (memory tier 0.5 with a loop: the loop kernel's
     # stack variant; --generic: the general interpreter's tier 1)
     "checksum_stack": (4, "per-byte checksum loop, sum kept at r10-8, over 1Mi mixed 64B/1500B frames"),

@@ -1542,6 +1542,14 @@ def main():
     with open(os.path.join(HERE, "tile_jit_stack.inc"), "w") as f:
         f.write("// GENERATED by gen_tile.py -- do not edit. The JIT template kernel's statement for "
                 "stack-window programs.\n// clang-format off\n" + cstr(text) + "\n// clang-format on\n")
+    # the loop kernel's statement with a deeper refill prefetch (ebpf_tile_jit_loop_deep, whose
+    # statement also owns the prefetch stages v[72:103] and their tags v104, v105)
+    text = F(JIT_STATEMENT).replace("aligned=%[aligned]\n", "aligned=%[aligned] deep=1\n")
+    assert "deep=1" in text
+    with open(os.path.join(HERE, "tile_jit_deep.inc"), "w") as f:
+        f.write("// GENERATED by gen_tile.py -- do not edit. The JIT template kernel's statement for "
+                "loop programs with a deep refill prefetch.\n// clang-format off\n" + cstr(text) +
+                "\n// clang-format on\n")
     # the compiled fixed-slot kernel's tile loop (jit_statement_loop)
     text = F(jit_statement_loop())
     assert "{" not in text, "unsubstituted register name: " + text[text.index("{"):][:40]

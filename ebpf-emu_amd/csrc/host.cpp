@@ -249,6 +249,7 @@ struct ebpf_prog {
   int jit_state = 0;
   bool jit_has[kJitVariants] = {};
   std::vector<char> jit_co[kJitVariants];
+  bool jit_deep = false;  // variant 2 compiled into ebpf_tile_jit_loop_deep
   std::string jit_asm[kJitVariants];
   std::string jit_err;
   hipModule_t jit_mod[kMaxDevices][kJitVariants] = {};
@@ -291,7 +292,7 @@ static int jit_compile_locked(ebpf_prog* p) {
         if (!p->jit_has[v]) continue;
         const bool ok = v == 2 ? jit_compile_loop(p->xuops, p->ltuops, p->ltuopsx, p->jit_co[v],
                                                   &p->jit_err, &p->jit_asm[v],
-                                                  p->stack.k ? &p->stack : nullptr)
+                                                  p->stack.k ? &p->stack : nullptr, &p->jit_deep)
                                : jit_compile(p->xuops,
                                              v == 3 ? p->tuopsk_xdp : v ? p->tuopsk : p->tuops,
                                              p->jit_co[v],
@@ -1211,9 +1212,12 @@ int ebpf_prog_upload(ebpf_prog* p, int device) {
   // the compiled program's modules on this device (a compiler failure leaves the interpreter)
   if (rc == EBPF_OK && jit_compile_locked(p) == 1) {
     for (int v = 0; v < kJitVariants && rc == EBPF_OK; v++)
-      if (p->jit_has[v] &&
-          !jit_load(p->jit_co[v], &p->jit_mod[device][v], &p->jit_fn[device][v]))
-        rc = EBPF_EHIP;
+      if (p->jit_has[v]) {
+        if (!jit_load(p->jit_co[v], &p->jit_mod[device][v], &p->jit_fn[device][v]))
+          rc = EBPF_EHIP;
+        else if (v == 2 && p->jit_deep)  // (the code is in the deep-prefetch loop kernel)
+          p->jit_fn[device][v].loop = p->jit_fn[device][v].loop_deep;
+      }
   }
   if (rc == EBPF_OK) {
     p->dev_uops[device] = d;

@@ -1412,6 +1412,11 @@ constexpr uint32_t kTileWaveLds = kWinBytes + kDagMetaBytes;  // window + metada
 #define TILE_ASM_CLOBBER_WINDOW_HI "v72", "v73", "v74", "v75", "v76", "v77", "v78", "v79", "v80", \
     "v81", "v82", "v83", "v84", "v85", "v86", "v87", "v88", "v89", "v90", "v91", "v92", "v93", "v94", \
     "v95"
+// the deep-prefetch loop kernel (jit.cpp refill_prefetch, pf_depth > 1): prefetch stages 1 and 2
+// in v[72:87] and v[88:103], their window tags in v104, v105
+#define TILE_ASM_CLOBBER_DEEP "v72", "v73", "v74", "v75", "v76", "v77", "v78", "v79", "v80", "v81", \
+    "v82", "v83", "v84", "v85", "v86", "v87", "v88", "v89", "v90", "v91", "v92", "v93", "v94", \
+    "v95", "v96", "v97", "v98", "v99", "v100", "v101", "v102", "v103", "v104", "v105"
 #define TILE_ASM_CLOBBER_WINDOW "v64", "v65", "v66", "v67", "v68", "v69", "v70", "v71", "v72", \
     "v73", "v74", "v75", "v76", "v77", "v78", "v79", "v80", "v81", "v82", "v83", "v84", "v85", \
     "v86", "v87", "v88", "v89", "v90", "v91", "v92", "v93", "v94", "v95"
@@ -1425,7 +1430,8 @@ constexpr uint32_t kTileWaveLdsDb = 2 * kWinBytes;
 
 // STACK (with JIT, !FIXED, !LOOPS): the statement of stack-window programs, which also owns
 // v[64:95] (the preloaded header window and the stack window, jit.cpp body)
-template <bool FIXED, bool LOOPS, bool JIT, bool STACK = false>
+// DEEP (with JIT, LOOPS): the loop statement whose refills prefetch two or three windows ahead
+template <bool FIXED, bool LOOPS, bool JIT, bool STACK = false, bool DEEP = false>
 __device__ __forceinline__ void tile_body(LaunchArgs& a) {
   constexpr uint32_t WPB = kWavesPerBlock;
   counters_init();
@@ -1492,6 +1498,10 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
       asm volatile(
 #include "tile_jit_stack.inc"
           TILE_ASM_OPERANDS, TILE_ASM_CLOBBER_PREFETCH, TILE_ASM_CLOBBER_WINDOW_HI);
+    } else if constexpr (JIT && LOOPS && DEEP) {  // + the deeper prefetch's stages
+      asm volatile(
+#include "tile_jit_deep.inc"
+          TILE_ASM_OPERANDS, TILE_ASM_CLOBBER_PREFETCH, TILE_ASM_CLOBBER_DEEP);
     } else if constexpr (JIT && LOOPS) {  // + the refill prefetch registers of compiled loop programs
       asm volatile(
 #include "tile_jit.inc"
@@ -1678,6 +1688,11 @@ extern "C" __global__ __launch_bounds__(kBlock, 4) void ebpf_tile_jit_var_stack(
 // (6 waves per SIMD: the prefetch registers take the kernel past 64 VGPRs)
 extern "C" __global__ __launch_bounds__(kBlock, 5) void ebpf_tile_jit_loop(LaunchArgs a) {
   tile_body<false, true, true>(a);
+}
+// loop programs whose refills prefetch two or three windows ahead (jit.cpp refill_prefetch,
+// EBPFEMU_PF_DEPTH): 32 more prefetch VGPRs, 4 waves per SIMD
+extern "C" __global__ __launch_bounds__(kBlock, 4) void ebpf_tile_jit_loop_deep(LaunchArgs a) {
+  tile_body<false, true, true, false, true>(a);
 }
 // stack-window loop programs (memory tier 0.5 with back edges or a binding budget): the stack
 // window in v[80:95]

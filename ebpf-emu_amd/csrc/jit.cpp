@@ -53,6 +53,7 @@ struct Marker {
   std::string aligned;
   std::string xdp;  // the SGPR holding LaunchArgs::xdp (the xdp_md convention in place)
   bool stack = false;  // the var kernel's statement for stack-window programs
+  bool deep = false;   // the deep-prefetch loop kernel's statement
 };
 
 bool inline_const(int64_t v) { return v >= -16 && v <= 64; }
@@ -87,6 +88,7 @@ bool find_markers(const std::string& s, std::vector<Marker>& out) {
     m.aligned = field("aligned=");
     m.xdp = field("xdp=");
     m.stack = field("stack=") == "1";
+    m.deep = field("deep=") == "1";
     const size_t mk = s.find(";@@JIT@@", eol);
     if (mk == std::string::npos || m.n.empty()) return false;
     const size_t ik = s.rfind(";@@JITINIT@@", pos);
@@ -235,6 +237,7 @@ struct Compiler {
   bool zwin = false;  // zero-past-len windows (ldx1_zero_window)
   bool qcache = false;  // with the 8-byte per-lane cache (ldx1_qword_cache)
   bool prefetch = false;  // zwin refills take the prefetched next window (refill_prefetch)
+  int pf = 1;  // windows prefetched ahead (ebpf_tile_jit_loop_deep for 2, 3)
 
   Compiler(const std::vector<Uop>& u, const std::vector<TUop>& tt, bool lp = false, bool ex = false,
            const StackPlan* sp = nullptr)
@@ -1378,7 +1381,7 @@ struct Compiler {
   // Transposed loads of every slot (packet refilling, chunk start + extra < bytes left; with
   // miss_only, only packets that missed the prefetch) into v[56+4k : 59+4k], from q's window
   // address + chunk offset + extra. exec = all lanes, and again after.
-  static std::string transposed_loads(uint32_t extra, bool miss_only) {
+  static std::string transposed_loads(uint32_t extra, bool miss_only, uint32_t base = 56) {
     std::string r;
     for (uint32_t k = 0; k < 4; k++) {
       r += slot_of(k, true);
@@ -1388,8 +1391,9 @@ struct Compiler {
                   : std::string("v_cmp_lt_u32 vcc, v54, v49\n")) +
            "s_and_b64 exec, vcc, s[62:63]\n"
            "v_add_co_u32 v42, vcc, v50, v40\nv_addc_co_u32 v43, vcc, 0, v51, vcc\n"
-           "global_load_dwordx4 v[" + std::to_string(56 + 4 * k) + ":" + std::to_string(59 + 4 * k) +
-           "], v[42:43], off" + (extra ? " offset:" + std::to_string(extra) : std::string()) + "\n"
+           "global_load_dwordx4 v[" + std::to_string(base + 4 * k) + ":" +
+           std::to_string(base + 3 + 4 * k) + "], v[42:43], off" +
+           (extra ? " offset:" + std::to_string(extra) : std::string()) + "\n"
            "s_mov_b64 exec, -1\n";
     }
     return r;
@@ -1414,11 +1418,161 @@ struct Compiler {
   // no window base takes): the first refill of each lane loads its window and starts the
   // prefetching, so a loop program that never leaves its first window reads nothing more.
   std::string prefetch_prologue(const Marker&, const std::string&) const {
-    return prefetch ? "v_mov_b32 v23, 0x80000001\n" : "";
+    if (!prefetch) return "";
+    std::string r;
+    for (int s = 0; s < (pf < 0 ? -pf : pf); s++) r += "v_mov_b32 " + pf_tag(s) + ", 0x80000001\n";
+    return r;
+  }
+
+  // ---- the deep prefetch (pf = 2, 3 stages; ebpf_tile_jit_loop_deep) ----
+  // Stage s holds, per lane, the transposed 64 bytes of one window (v[56:71], v[72:87],
+  // v[88:103]) and its packet offset as a tag (v23, v104, v105). A forward scan's window W goes
+  // to stage (W / 64) mod pf. A refill picks the stage of its first lane's new window (uniform:
+  // lockstep lanes refill the same window), takes a lane's window from it where the tag matches
+  // and the lane's previous window was W - 64, and reloads that stage with W + 64 pf; other lanes
+  // (the first refill of a packet, a jump, a lane out of step) load W and fill the other stages
+  // with W + 64 .. W + 64 (pf - 1). Every refill issues its loads in the order the windows are
+  // needed, the four prefetch loads last, so a sequential lane's window always has at least
+  // 4 (pf - 1) loads younger than its own: the refill waits with vmcnt(4 (pf - 1)), and the loads
+  // of the next pf - 1 windows stay in flight.
+  static std::string pf_tag(int s) { return s == 0 ? "v23" : s == 1 ? "v104" : "v105"; }
+  static uint32_t pf_base(int s) { return s == 0 ? 56u : s == 1 ? 72u : 88u; }
+
+  std::string refill_deep(const std::string& A, const std::string& U) const {
+    const int D = pf;
+    const std::string W = "s_waitcnt vmcnt(" + std::to_string(4 * (D - 1)) + ")\n";
+    std::string r = "s_mov_b64 s[66:67], exec\ns_mov_b64 exec, -1\n" + transpose_consts() +
+                    "v_mov_b32 v44, 0\n"
+                    "s_mov_b64 exec, s[68:69]\n"
+                    "v_and_b32 v37, -16, " + A + "\n"
+                    "v_sub_u32 v27, v37, v22\n"  // the step from the lane's previous window
+                    "v_mov_b32 v22, v37\n"
+                    "v_readfirstlane_b32 s60, v22\n"
+                    "s_lshr_b32 s60, s60, 6\n";
+    if (D == 2)
+      r += "s_and_b32 s60, s60, 1\n";
+    else  // s60 mod 3
+      r += "s_mul_hi_u32 s61, s60, 0xaaaaaaab\ns_lshr_b32 s61, s61, 1\n"
+           "s_mul_i32 s61, s61, 3\ns_sub_u32 s60, s60, s61\n";
+    for (int st = 1; st < D; st++)
+      r += "s_cmp_eq_u32 s60, " + std::to_string(st) + "\ns_cbranch_scc1 .Lpg" +
+           std::to_string(st) + U + "\n";
+    for (int st = 0; st < D; st++) {
+      const std::string S = std::to_string(st), T = pf_tag(st);
+      const uint32_t base = pf_base(st);
+      if (st) r += ".Lpg" + S + U + ":\n";
+      r += "v_cmp_eq_u32 vcc, 64, v27\n"
+           "v_cmp_eq_u32 s[60:61], v22, " + T + "\n"
+           "s_and_b64 vcc, vcc, s[60:61]\n"              // hit: in sequence, tag matches
+           "s_andn2_b64 s[60:61], s[68:69], vcc\n" +   // misses
+           pack_lane(true) +
+           "v_add_u32 " + T + ", " + std::to_string(64 * D) + ", v22\n"
+           "s_mov_b64 exec, s[60:61]\n";
+      for (int i = 1; i < D; i++)
+        r += "v_add_u32 " + pf_tag((st + i) % D) + ", " + std::to_string(64 * i) + ", v22\n";
+      r += "s_mov_b64 exec, -1\n" + W +
+           "s_cmp_eq_u64 s[60:61], 0\n"
+           "s_cbranch_scc1 .Lph" + S + U + "\n" + transposed_loads(0, true, base);
+      for (int i = 1; i < D; i++)
+        r += transposed_loads(64 * i, true, pf_base((st + i) % D));
+      r += W + ".Lph" + S + U + ":\n";
+      for (uint32_t k = 0; k < 4; k++) {
+        const std::string K = std::to_string(k), R0 = std::to_string(base + 4 * k),
+                          R3 = std::to_string(base + 3 + 4 * k);
+        r += slot_of(k, true) +
+             "v_sub_u32 v37, v49, v54\n"
+             "s_mov_b64 exec, s[62:63]\n"
+             "v_cmp_gt_i32 vcc, 16, v37\n"
+             "s_cbranch_vccz .Lnz" + K + "s" + S + U + "\n"
+             "s_mov_b64 exec, vcc\n";
+        for (uint32_t d = 0; d < 4; d++)
+          r += zero_dword("v" + std::to_string(base + 4 * k + d), 4 * d);
+        r += "s_mov_b64 exec, s[62:63]\n"
+             ".Lnz" + K + "s" + S + U + ":\n"
+             "ds_write_b128 v41, v[" + R0 + ":" + R3 + "] offset:" + std::to_string(1024 * k) + "\n"
+             "v_add_u32 v37, " + std::to_string(64 * D) + ", v54\n"
+             "v_cmp_lt_u32 vcc, v37, v49\n"
+             "s_and_b64 exec, exec, vcc\n"
+             "v_add_co_u32 v42, vcc, v50, v40\nv_addc_co_u32 v43, vcc, 0, v51, vcc\n"
+             "global_load_dwordx4 v[" + R0 + ":" + R3 + "], v[42:43], off offset:" +
+             std::to_string(64 * D) + "\n"
+             "s_mov_b64 exec, -1\n";
+      }
+      r += "s_branch .Lpe" + U + "\n";
+    }
+    return r + ".Lpe" + U + ":\ns_mov_b64 exec, s[66:67]\n";
   }
 
   // refill_zero's replacement (transposed, prefetched); lanes s[68:69], address A.
+  // Pairs (pf = -2, EBPFEMU_PF_DEPTH=pair): the two stages hold an even window (stage 0) and the
+  // odd one after it (stage 1). An odd refill loads the next two windows back to back -- one
+  // 128-byte line of each packet requested at once, W + 64 into stage 0 and W + 128 into stage 1,
+  // per slot -- and an even refill loads nothing. Waits: vmcnt(1) at an even refill (its window is
+  // the second-youngest load of the pair's last slot), vmcnt(0) at an odd one.
+  std::string refill_pair(const std::string& A, const std::string& U) const {
+    std::string r = "s_mov_b64 s[66:67], exec\ns_mov_b64 exec, -1\n" + transpose_consts() +
+                    "v_mov_b32 v44, 0\n"
+                    "s_mov_b64 exec, s[68:69]\n"
+                    "v_and_b32 v37, -16, " + A + "\n"
+                    "v_sub_u32 v27, v37, v22\n"
+                    "v_mov_b32 v22, v37\n"
+                    "v_readfirstlane_b32 s60, v22\n"
+                    "s_bitcmp1_b32 s60, 6\n"
+                    "s_cbranch_scc1 .Lpg1" + U + "\n";
+    for (int st = 0; st < 2; st++) {
+      const std::string S = std::to_string(st), T = pf_tag(st);
+      const uint32_t base = pf_base(st);
+      if (st) r += ".Lpg1" + U + ":\n";
+      r += "v_cmp_eq_u32 vcc, 64, v27\n"
+           "v_cmp_eq_u32 s[60:61], v22, " + T + "\n"
+           "s_and_b64 vcc, vcc, s[60:61]\n"
+           "s_andn2_b64 s[60:61], s[68:69], vcc\n" + pack_lane(true);
+      if (st == 0)  // an even window's misses also load the odd one after it
+        r += "s_mov_b64 exec, s[60:61]\nv_add_u32 " + pf_tag(1) + ", 64, v22\n";
+      else  // the pair this odd refill loads
+        r += "v_add_u32 v23, 64, v22\nv_add_u32 v104, 0x80, v22\n";
+      r += "s_mov_b64 exec, -1\n" + std::string(st ? "s_waitcnt vmcnt(0)\n" : "s_waitcnt vmcnt(1)\n") +
+           "s_cmp_eq_u64 s[60:61], 0\n"
+           "s_cbranch_scc1 .Lph" + S + U + "\n" + transposed_loads(0, true, base);
+      if (st == 0) r += transposed_loads(64, true, pf_base(1)) + "s_waitcnt vmcnt(4)\n";
+      else r += "s_waitcnt vmcnt(0)\n";
+      r += ".Lph" + S + U + ":\n";
+      for (uint32_t k = 0; k < 4; k++) {
+        const std::string K = std::to_string(k), R0 = std::to_string(base + 4 * k),
+                          R3 = std::to_string(base + 3 + 4 * k);
+        r += slot_of(k, true) +
+             "v_sub_u32 v37, v49, v54\n"
+             "s_mov_b64 exec, s[62:63]\n"
+             "v_cmp_gt_i32 vcc, 16, v37\n"
+             "s_cbranch_vccz .Lnz" + K + "s" + S + U + "\n"
+             "s_mov_b64 exec, vcc\n";
+        for (uint32_t d = 0; d < 4; d++)
+          r += zero_dword("v" + std::to_string(base + 4 * k + d), 4 * d);
+        r += "s_mov_b64 exec, s[62:63]\n"
+             ".Lnz" + K + "s" + S + U + ":\n"
+             "ds_write_b128 v41, v[" + R0 + ":" + R3 + "] offset:" + std::to_string(1024 * k) + "\n";
+        if (st == 1) {
+          for (int i = 0; i < 2; i++) {
+            const uint32_t b2 = pf_base(i) + 4 * k;
+            r += "s_mov_b64 exec, s[62:63]\n"
+                 "v_add_u32 v37, " + std::to_string(64 * (i + 1)) + ", v54\n"
+                 "v_cmp_lt_u32 vcc, v37, v49\n"
+                 "s_and_b64 exec, exec, vcc\n"
+                 "v_add_co_u32 v42, vcc, v50, v40\nv_addc_co_u32 v43, vcc, 0, v51, vcc\n"
+                 "global_load_dwordx4 v[" + std::to_string(b2) + ":" + std::to_string(b2 + 3) +
+                 "], v[42:43], off offset:" + std::to_string(64 * (i + 1)) + "\n";
+          }
+        }
+        r += "s_mov_b64 exec, -1\n";
+      }
+      r += "s_branch .Lpe" + U + "\n";
+    }
+    return r + ".Lpe" + U + ":\ns_mov_b64 exec, s[66:67]\n";
+  }
+
   std::string refill_prefetch(const std::string& A, const std::string& U) const {
+    if (pf == -2) return refill_pair(A, U);
+    if (pf > 1) return refill_deep(A, U);
     std::string r = "s_mov_b64 s[66:67], exec\ns_mov_b64 exec, -1\n" + transpose_consts() +
                     "v_mov_b32 v44, 0\n"
                     "s_mov_b64 exec, s[68:69]\n"
@@ -2221,6 +2375,17 @@ struct Compiler {
     return body_loop_once(m, xc, out);
   }
 
+  // Whether body_loop will give this program prefetching refills (zero-past-len windows: every
+  // register load one byte wide, no byte cache).
+  bool prefetches() const {
+    const char* bc = getenv("EBPFEMU_BYTE_CACHE");
+    if (stk || (bc && bc[0] == '1') || getenv("EBPFEMU_NO_ZERO_WINDOW") || getenv("EBPFEMU_NO_PREFETCH"))
+      return false;
+    for (const Uop& o : uops)
+      if (o.op == U_LDX && o.aux != 1) return false;
+    return true;
+  }
+
   // s70 (set by the statement's prologue, tile_jit.inc): bit 0 = exact mode (the step-budget
   // restart), bit 1 = registers not in the main.rs layout (init_regs) or requested as outputs.
   // With bit 1 clear, a program with loads proven in bounds (prove_loads) runs its proven copy.
@@ -2376,7 +2541,7 @@ namespace {
 // kernel -- loop vs forward-only -- get an empty body: never launched for this program), then
 // assemble.
 bool compile_into_template(Compiler& c, Compiler* xc, std::vector<char>& code_object,
-                           std::string* err, std::string* asm_out) {
+                           std::string* err, std::string* asm_out, bool* deep_out = nullptr) {
   std::string tmpl(kJitTemplateAsm);
   // cache policy of the window DMA (the fixed-slot kernel's whole tiles): non-temporal -- every
   // packet byte is read once (MI355X guide, nt-weights: issued -> landed ~18 % shorter). A/B, one
@@ -2396,13 +2561,17 @@ bool compile_into_template(Compiler& c, Compiler* xc, std::vector<char>& code_ob
   std::string src;
   size_t at = 0;
   const std::string init = c.init_code();
+  // (loop programs whose refills prefetch go to the deep-prefetch loop kernel when pf_depth() > 1)
+  // (EBPFEMU_LOOP_DEEP=1: the deep kernel, 4 waves per SIMD, with any depth: A/B of occupancy)
+  const bool deep = xc && !c.stk && c.prefetches() && (pf_depth() != 1 || getenv("EBPFEMU_LOOP_DEEP"));
+  if (deep) c.pf = xc->pf = pf_depth();  // (1 with EBPFEMU_LOOP_DEEP: refill_prefetch's own code)
   for (const Marker& m : marks) {
     std::string b;
     const bool loop_marker = m.loops == "1";
     bool ok = true;
     // (stack-window programs: the fixed-slot kernel and the var kernel's stack statement; other
     // programs: every statement but that one)
-    if (loop_marker != (xc != nullptr) ||
+    if (loop_marker != (xc != nullptr) || (loop_marker && m.deep != deep) ||
         (c.stk ? !(m.stack || (!loop_marker && m.fixed == "1")) : m.stack))
       b = "s_mov_b64 exec, 0  ; (not this program's kernel)\n";
     else
@@ -2419,6 +2588,7 @@ bool compile_into_template(Compiler& c, Compiler* xc, std::vector<char>& code_ob
   }
   src += tmpl.substr(at);
   if (asm_out) *asm_out = src;
+  if (deep_out) *deep_out = deep;
   return assemble(src, code_object, err);
 }
 
@@ -2439,7 +2609,8 @@ bool jit_compile(const std::vector<Uop>& uops, const std::vector<TUop>& t,
 
 bool jit_compile_loop(const std::vector<Uop>& uops, const std::vector<TUop>& t,
                       const std::vector<TUop>& tx, std::vector<char>& code_object,
-                      std::string* err, std::string* asm_out, const StackPlan* stk) {
+                      std::string* err, std::string* asm_out, const StackPlan* stk,
+                      bool* deep) {
   if (uops.empty() || uops.size() > kJitMaxUops || t.size() < uops.size() ||
       tx.size() < uops.size() ||
       (stk && (stk->k == 0 || stk->k > kStackMax || stk->k % 4 || stk->off.size() != uops.size() ||
@@ -2448,7 +2619,14 @@ bool jit_compile_loop(const std::vector<Uop>& uops, const std::vector<TUop>& t,
     return false;
   }
   Compiler c(uops, t, true, false, stk), xc(uops, tx, true, true, stk);
-  return compile_into_template(c, &xc, code_object, err, asm_out);
+  return compile_into_template(c, &xc, code_object, err, asm_out, deep);
+}
+
+int pf_depth() {
+  const char* e = getenv("EBPFEMU_PF_DEPTH");
+  if (e && strcmp(e, "pair") == 0) return -2;
+  const int d = e ? atoi(e) : 1;
+  return d < 1 ? 1 : d > 3 ? 3 : d;
 }
 
 bool jit_load(const std::vector<char>& co, hipModule_t* mod, JitFns* fns) {
@@ -2459,7 +2637,8 @@ bool jit_load(const std::vector<char>& co, hipModule_t* mod, JitFns* fns) {
       hipModuleGetFunction(&f.var, m, "ebpf_tile_jit_var") != hipSuccess ||
       hipModuleGetFunction(&f.loop, m, "ebpf_tile_jit_loop") != hipSuccess ||
       hipModuleGetFunction(&f.var_stack, m, "ebpf_tile_jit_var_stack") != hipSuccess ||
-      hipModuleGetFunction(&f.loop_stack, m, "ebpf_tile_jit_loop_stack") != hipSuccess) {
+      hipModuleGetFunction(&f.loop_stack, m, "ebpf_tile_jit_loop_stack") != hipSuccess ||
+      hipModuleGetFunction(&f.loop_deep, m, "ebpf_tile_jit_loop_deep") != hipSuccess) {
     (void)hipModuleUnload(m);
     return false;
   }

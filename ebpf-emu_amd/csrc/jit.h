@@ -19,6 +19,7 @@ struct JitFns {
   hipFunction_t loop = nullptr;  // loop programs (ebpf_tile_jit_loop)
   hipFunction_t var_stack = nullptr;  // stack-window programs, other layouts (ebpf_tile_jit_var_stack)
   hipFunction_t loop_stack = nullptr;  // stack-window loop programs (ebpf_tile_jit_loop_stack)
+  hipFunction_t loop_deep = nullptr;  // loop programs with the deep refill prefetch
 };
 
 // Stack-window programs (memory tier 0.5, host.cpp analyze_stack): every store or atomic writes
@@ -52,11 +53,16 @@ bool jit_compile(const std::vector<Uop>& uops, const std::vector<TUop>& t,
                  const StackPlan* stk = nullptr);
 
 // Loop programs (back edges, or budgets that can bind; tile tables of build_tile: `t` the block
-// table, `tx` the exact one-micro-op-per-block table) for ebpf_tile_jit_loop.
+// table, `tx` the exact one-micro-op-per-block table) for ebpf_tile_jit_loop. *deep (if given):
+// the code went into ebpf_tile_jit_loop_deep instead (refills prefetching pf_depth() windows).
 bool jit_compile_loop(const std::vector<Uop>& uops, const std::vector<TUop>& t,
                       const std::vector<TUop>& tx, std::vector<char>& code_object,
                       std::string* err, std::string* asm_out = nullptr,
-                      const StackPlan* stk = nullptr);
+                      const StackPlan* stk = nullptr, bool* deep = nullptr);
+
+// Windows the refills of byte-scanning loop programs prefetch ahead: 1 (ebpf_tile_jit_loop, 5
+// waves per SIMD) or 2-3 (ebpf_tile_jit_loop_deep, 4 waves); EBPFEMU_PF_DEPTH overrides.
+int pf_depth();
 
 // Loads a code object on the current device (the functions it does not hold stay null).
 bool jit_load(const std::vector<char>& code_object, hipModule_t* mod, JitFns* fns);

@@ -547,3 +547,63 @@ def test_counted_loop_passes(cuda, oracle_mod, seed):
             prod = _run_prod(img, pkts, cuda, mem_size=1024, max_steps=100000, **layout)
             _check_prod_against_oracle(oracle_mod, img, pkts, prod, mem_size=1024,
                                        max_steps=100000, tag=f"seed {seed} it {it} {layout}")
+
+
+# Byte scans for the deep refill prefetch (jit.cpp refill_deep): sequential windows (lockstep
+# lanes hit their prefetched stage), strides that skip windows (every refill a miss: the window
+# loaded directly, the stages refilled), a backward scan, and lengths that differ per lane.
+DEEP_SCANS = [FORWARD_SUM] + [FORWARD_SUM.replace("add r3, 1", f"add r3, {s}") for s in (5, 64, 100, 130)] + [
+    """
+    mov r0, 0
+    mov r3, r2
+    jeq r3, 0, done
+loop:
+    sub r3, 1
+    mov r4, r1
+    add r4, r3
+    ldxb r5, [r4+0]
+    add r0, r5
+    lsh r0, 1
+    jgt r3, 0, loop
+done:
+    exit
+"""]
+
+
+@pytest.mark.parametrize("depth", [2, 3, "pair"])
+def test_deep_prefetch(cuda, oracle_mod, monkeypatch, depth):
+    """The loop kernel whose refills prefetch 2 or 3 windows ahead (EBPFEMU_PF_DEPTH,
+    ebpf_tile_jit_loop_deep): the checksum and byte scans with window-skipping strides, a backward
+    scan and per-lane lengths, binned and unbinned batches, fixed and offsets layouts --
+    compiled == general interpreter == oracle."""
+    import numpy as np
+
+    from ebpf_emu import Program
+    from ebpf_emu import workloads as W
+    from ebpf_emu.asm import assemble
+
+    monkeypatch.setenv("EBPFEMU_PF_DEPTH", str(depth))
+    rng = random.Random(zlib.crc32(str(depth).encode()))
+    for i, src in enumerate([W.CHECKSUM] + DEEP_SCANS):
+        img = assemble(src)
+        p = Program(img)
+        assert p.compile()
+        assert "global_load_dwordx4 v[72:75]" in p.jit_asm(2), src
+        p.close()
+        n = 17000 if i < 2 else 700  # (>= 16384: length-binned order)
+        lens = [rng.choice([0, 14, 64, 65, 200, 600, 1500, 1500, 1500, rng.randrange(1501)])
+                for _ in range(n)]
+        pkts = [bytes(rng.getrandbits(8) for _ in range(ln)) for ln in lens]
+        for layout in (dict(offsets_layout=True, align=16), dict(offsets_layout=True, align=64)):
+            got = _run_full(img, pkts, cuda, mem_size=2048, r10=2048, **layout)
+            gen = _run_full(img, pkts, cuda, mem_size=2048, r10=2048, generic=True, **layout)
+            _same_outputs(got, gen, f"depth {depth} {layout} {src[:40]}")
+            (frames, nn), kw = _oracle_batch(pkts)
+            r0, st, cnt = oracle_mod.Program(img).run_batch(frames, nn, mem_size=2048, r10=2048,
+                                                            threads=8, **kw)
+            assert np.array_equal(got["status"], st)
+            assert np.array_equal(got["r0"], np.asarray(r0, dtype=np.uint64))
+            assert list(got["counters"]) == [int(c) for c in cnt]
+            prod = _run_prod(img, pkts, cuda, mem_size=2048, r10=2048, **layout)
+            assert np.array_equal(prod["r0"], got["r0"]) and np.array_equal(prod["status"], st)
+            assert list(prod["counters"]) == list(got["counters"])
