@@ -2071,7 +2071,10 @@ struct Compiler {
       c += "s_branch " + G + "top\n";
       return true;
     };
-    std::string c = G + "ent:\ns_mov_b64 s[44:45], exec\ns_mov_b64 s[46:47], 0\n"
+    std::string coop;
+    if (sum_add >= 0 && !getenv("EBPFEMU_NO_COOP_SUM")) coop = coop_sum(L, J, rI, rN, d, ld, sum_add, G, P);
+    std::string c = (coop.empty() ? G + "ent:\n" : coop + G + "ent2:\n") +
+                    "s_mov_b64 s[44:45], exec\ns_mov_b64 s[46:47], 0\n"
                     "s_mov_b32 s41, 0x07060501\ns_mov_b32 s42, 0x07060502\n"
                     "s_mov_b32 s43, 0x07060503\n" + G + "top:\n"
                     "s_mov_b64 exec, s[44:45]\n"
@@ -2149,6 +2152,164 @@ struct Compiler {
       return counted_group(m, L, J, rI, rN, skip, P, PU, out, false);
     out = c + uo;
     return 1;
+  }
+
+  // ---- the byte-sum idiom over a whole range, transposed (counted_group's entry) ----
+  // A counted byte-sum loop adds, over its n = rN - rI iterations, n * (rD & ~0xff) + the sum of
+  // the bytes [a0, a0 + n) (a0 = rI + d, every one proven a packet byte: prove_loads), leaves rD's
+  // low byte at the last byte and rI at rI + n. Lanes with at least kCoopMin bytes to go get that
+  // result without scanning their windows: the wave sums all their ranges together straight from
+  // HBM, transposed as the refills are -- in load k, lane L reads 16 bytes of packet q = 16k + L/4
+  // (four lanes per packet, 16 packets per instruction), 64 bytes of each of its 64 packets per
+  // round -- with v_sad_u8 into a per-lane sum for each k, bytes outside a range masked in its first
+  // and last chunk; then the four lanes of each packet are summed (DPP) and the sum moved to the
+  // packet's lane (ds_bpermute). No LDS window, no per-lane loop: per 64 bytes of 64 packets four
+  // loads and about 20 VALU. Uses v[36:71] (the refill prefetch registers, drained and invalidated
+  // first; the qword cache and the prefetch tags are invalidated after) and s[60:67] (s64: the
+  // round's byte offset W). The finished
+  // lanes leave exec (their parked pc is the loop's exit, hoisted at the head); the others continue
+  // at the group's entry.
+  static constexpr uint32_t kCoopMin = 128;
+  std::string coop_sum(uint32_t L, uint32_t J, uint32_t rI, uint32_t rN, int64_t d, int ld,
+                       int sum_add, const std::string& G, const std::string& P) const {
+    const std::string vI = "v" + std::to_string(2 * rI), vN = "v" + std::to_string(2 * rN),
+                      D0 = "v" + std::to_string(uops[ld].dst * 2),
+                      D1 = "v" + std::to_string(uops[ld].dst * 2 + 1),
+                      S = vpair(2 * uops[sum_add].dst, 0, 1), I2 = vpair(2 * rI, 0, 1),
+                      C = G + "c";
+    auto v = [](uint32_t r) { return "v" + std::to_string(r); };
+    auto vp = [](uint32_t r) { return "v[" + std::to_string(r) + ":" + std::to_string(r + 1) + "]"; };
+    std::string r = G + "ent:\n"
+                    "; the byte sum of whole ranges, transposed (coop_sum)\n"
+                    "v_sub_u32 v46, " + vN + ", " + vI + "\n"
+                    "v_cmp_le_i32 vcc, " + std::to_string(kCoopMin) + ", v46\n"
+                    "s_and_b64 s[60:61], exec, vcc\n"
+                    "s_cbranch_scc0 " + G + "ent2\n"
+                    "s_mov_b64 s[62:63], exec\n"
+                    "s_mov_b64 exec, -1\n"
+                    "s_waitcnt vmcnt(0)\n"  // (v[56:71] may have refill prefetches in flight)
+                    // per lane: [v24:25] = (BASE + a0) & ~15, v26 = (BASE + a0) & 15, v27 = the end
+                    // (v26 + n on the cooperating lanes, 0 elsewhere: nothing is read for them)
+                    "v_sub_u32 v27, " + vN + ", " + vI + "\n" +
+                    (d ? "v_add_u32 v24, " + std::to_string(d) + ", " + vI + "\n"
+                       : "v_mov_b32 v24, " + vI + "\n") +
+                    "v_mov_b32 v25, 0\n"
+                    "v_lshl_add_u64 v[24:25], v[32:33], 0, v[24:25]\n"
+                    "v_and_b32 v26, 15, v24\n"
+                    "v_and_b32 v24, -16, v24\n"
+                    "v_add_u32 v27, v26, v27\n"
+                    "v_cndmask_b32_e64 v27, 0, v27, s[60:61]\n"
+                    "v_mbcnt_lo_u32_b32 v23, -1, 0\nv_mbcnt_hi_u32_b32 v23, -1, v23\n"
+                    "v_and_b32 v23, -4, v23\n";
+    // slot k (packet q = 16k + L/4): v[36+2k:37+2k] address, v44+k lo, v48+k hi (relative to
+    // this lane's chunk), v52+k sum
+    for (uint32_t k = 0; k < 4; k++) {
+      const std::string o = " offset:" + std::to_string(64 * k) + "\n";
+      r += "ds_bpermute_b32 " + v(36 + 2 * k) + ", v23, v24" + o + "ds_bpermute_b32 " +
+           v(37 + 2 * k) + ", v23, v25" + o + "ds_bpermute_b32 " + v(44 + k) + ", v23, v26" + o +
+           "ds_bpermute_b32 " + v(48 + k) + ", v23, v27" + o;
+    }
+    r += "v_mbcnt_lo_u32_b32 v23, -1, 0\nv_mbcnt_hi_u32_b32 v23, -1, v23\n"
+         "v_and_b32 v23, 3, v23\nv_lshlrev_b32 v23, 4, v23\n"
+         "s_waitcnt lgkmcnt(0)\n";
+    for (uint32_t k = 0; k < 4; k++)
+      r += "v_add_co_u32 " + v(36 + 2 * k) + ", vcc, " + v(36 + 2 * k) + ", v23\n"
+           "v_addc_co_u32 " + v(37 + 2 * k) + ", vcc, 0, " + v(37 + 2 * k) + ", vcc\n"
+           "v_sub_u32 " + v(44 + k) + ", " + v(44 + k) + ", v23\n"
+           "v_sub_u32 " + v(48 + k) + ", " + v(48 + k) + ", v23\n"
+           "v_mov_b32 " + v(52 + k) + ", 0\n";
+    r += "s_mov_b32 s64, 0\n" + C + "w:\n";
+    for (uint32_t k = 0; k < 4; k++)
+      r += "v_cmp_lt_i32 vcc, s64, " + v(48 + k) + "\n"
+           "s_mov_b64 exec, vcc\n"
+           "global_load_dwordx4 v[" + std::to_string(56 + 4 * k) + ":" + std::to_string(59 + 4 * k) +
+           "], " + vp(36 + 2 * k) + ", off\n"
+           "s_mov_b64 exec, -1\n";
+    r += "s_waitcnt vmcnt(0)\n";
+    for (uint32_t k = 0; k < 4; k++) {
+      const std::string K = std::to_string(k), A = v(52 + k);
+      // whole chunks (lo <= W, W + 16 <= hi), then the partial ones
+      r += "v_cmp_ge_i32 vcc, s64, " + v(44 + k) + "\n"
+           "v_subrev_u32 v24, 16, " + v(48 + k) + "\n"
+           "v_cmp_le_i32_e64 s[66:67], s64, v24\n"
+           "s_and_b64 s[66:67], s[66:67], vcc\n"
+           "v_cmp_lt_i32 vcc, s64, " + v(48 + k) + "\n"
+           "s_andn2_b64 vcc, vcc, s[66:67]\n"
+           "s_mov_b64 exec, s[66:67]\n";
+      for (uint32_t dw = 0; dw < 4; dw++)
+        r += "v_sad_u8 " + A + ", " + v(56 + 4 * k + dw) + ", 0, " + A + "\n";
+      r += "s_mov_b64 exec, vcc\n"
+           "s_cbranch_execz " + C + "s" + K + "\n"
+           "v_subrev_u32 v24, s64, " + v(44 + k) + "\n"
+           "v_subrev_u32 v25, s64, " + v(48 + k) + "\n";
+      for (uint32_t dw = 0; dw < 4; dw++) {
+        // bytes [clamp(lo - W - 4dw, 0, 4), clamp(hi - W - 4dw, 0, 4)) of dword dw
+        const std::string Dw = v(56 + 4 * k + dw), o4 = std::to_string(4 * dw);
+        r += "v_subrev_u32 v26, " + o4 + ", v24\nv_med3_i32 v26, v26, 0, 4\n"
+             "v_subrev_u32 v27, " + o4 + ", v25\nv_med3_i32 v27, v27, 0, 4\n"
+             "v_sub_u32 v27, v27, v26\nv_max_i32 v27, 0, v27\n"
+             "v_lshlrev_b32 v27, 3, v27\nv_lshlrev_b32 v26, 3, v26\n"
+             "v_bfm_b32 v23, v27, v26\n"
+             "v_cmp_eq_u32 s[66:67], 32, v27\n"  // (a 32-bit field: v_bfm's width is 5 bits)
+             "v_cndmask_b32_e64 v23, v23, -1, s[66:67]\n"
+             "v_and_b32 " + Dw + ", " + Dw + ", v23\n"
+             "v_sad_u8 " + A + ", " + Dw + ", 0, " + A + "\n";
+      }
+      r += C + "s" + K + ":\ns_mov_b64 exec, -1\n";
+    }
+    for (uint32_t k = 0; k < 4; k++)
+      r += "v_lshl_add_u64 " + vp(36 + 2 * k) + ", " + vp(36 + 2 * k) + ", 0, 64\n";
+    r += "s_add_u32 s64, s64, 64\n"
+         "v_max3_i32 v24, v48, v49, v50\nv_max_i32 v24, v24, v51\n"
+         "v_cmp_lt_i32 vcc, s64, v24\n"
+         "s_cbranch_vccnz " + C + "w\n";
+    // each packet's four partial sums (a quad) added, then moved to the packet's lane:
+    // packet L's sum is in slot L / 16, lane 4 (L % 16)
+    for (uint32_t k = 0; k < 4; k++)
+      r += "s_nop 1\n"
+           "v_add_u32_dpp " + v(52 + k) + ", " + v(52 + k) + ", " + v(52 + k) +
+           " quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+           "s_nop 1\n"
+           "v_add_u32_dpp " + v(52 + k) + ", " + v(52 + k) + ", " + v(52 + k) +
+           " quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n";
+    r += "v_mbcnt_lo_u32_b32 v23, -1, 0\nv_mbcnt_hi_u32_b32 v23, -1, v23\n"
+         "v_and_b32 v23, 15, v23\nv_lshlrev_b32 v23, 4, v23\n";
+    for (uint32_t k = 0; k < 4; k++) r += "ds_bpermute_b32 " + v(24 + k) + ", v23, " + v(52 + k) + "\n";
+    r += "s_waitcnt lgkmcnt(0)\n"
+         "s_mov_b32 exec_lo, 0xffff0000\ns_mov_b32 exec_hi, 0\nv_mov_b32 v24, v25\n"
+         "s_mov_b32 exec_lo, 0\ns_mov_b32 exec_hi, 0xffff\nv_mov_b32 v24, v26\n"
+         "s_mov_b32 exec_hi, 0xffff0000\nv_mov_b32 v24, v27\n"
+         // the cooperating lanes: v24 = the bytes' sum, v25 = n, v26 = the last byte
+         "s_mov_b64 exec, s[60:61]\n"
+         "v_sub_u32 v25, " + vN + ", " + vI + "\n"
+         "v_add_u32 v26, " + vI + ", v25\n" +
+         (d - 1 ? "v_add_u32 v26, " + std::to_string(d - 1) + ", v26\n" : std::string()) +
+         "v_mov_b32 v27, 0\n"
+         "v_lshl_add_u64 v[26:27], v[32:33], 0, v[26:27]\n"
+         "global_load_ubyte v26, v[26:27], off\n"
+         "v_and_b32 v27, 0xffffff00, " + D0 + "\n"
+         "v_mad_u64_u32 v[42:43], s[66:67], v27, v25, 0\n"
+         "v_mul_lo_u32 v27, " + D1 + ", v25\n"
+         "v_add_u32 v43, v43, v27\n"
+         "v_add_co_u32 v42, vcc, v42, v24\nv_addc_co_u32 v43, vcc, 0, v43, vcc\n"
+         "v_lshl_add_u64 " + S + ", v[42:43], 0, " + S + "\n"
+         "v_mov_b32 v24, v25\nv_mov_b32 v25, 0\n"
+         "v_lshl_add_u64 " + I2 + ", " + I2 + ", 0, v[24:25]\n"
+         "s_waitcnt vmcnt(0)\n"
+         "v_bfi_b32 " + D0 + ", s56, v26, " + D0 + "\n"
+         // every lane: the qword cache and the refill prefetches are gone
+         "s_mov_b64 exec, -1\n"
+         "v_mov_b32 v55, 0x80000000\n" + invalidate_prefetch() +
+         "s_andn2_b64 exec, s[62:63], s[60:61]\n"
+         "s_cbranch_execz .L" + P + "b" + std::to_string(J + 1) + "\n";
+    (void)L;
+    return r;
+  }
+
+  std::string invalidate_prefetch() const {
+    std::string r;
+    for (int s = 0; s < (pf < 0 ? -pf : pf); s++) r += "v_mov_b32 " + pf_tag(s) + ", 0x80000001\n";
+    return r;
   }
 
   // The code of micro-op i (no block entry) in copy P.

@@ -607,3 +607,88 @@ def test_deep_prefetch(cuda, oracle_mod, monkeypatch, depth):
             prod = _run_prod(img, pkts, cuda, mem_size=2048, r10=2048, **layout)
             assert np.array_equal(prod["r0"], got["r0"]) and np.array_equal(prod["status"], st)
             assert list(prod["counters"]) == list(got["counters"])
+
+
+W_CHECKSUM_BODY = """
+    mov r0, 0
+    {pre}
+    {start}
+    jge r3, r2, done
+loop:
+    {load}
+    add r0, r5
+    add r3, 1
+    jlt r3, r2, loop
+done:
+    mov r6, r5
+    lsh r6, 8
+    xor r0, r6
+    xor r0, r3
+    exit
+"""
+
+
+# Byte-sum loops for coop_sum (jit.cpp: the sum of a whole range, transposed, from HBM): starts
+# that are not 16-aligned, a load offset (d != 0), rD with its upper bytes set (n * (rD & ~0xff)),
+# a 32-bit sum register... and lengths around kCoopMin (128) and up to 1500.
+COOP_PROGRAMS = {
+    "sum": W_CHECKSUM_BODY.format(pre="", start="mov r3, 0", load="ldxb r5, [r3+0]"),
+    "start5_upper": W_CHECKSUM_BODY.format(pre="lddw r5, 0x123456789abcde00", start="mov r3, 5",
+                                           load="ldxb r5, [r3+0]"),
+    "addr_copy": W_CHECKSUM_BODY.format(pre="mov r5, -1", start="ldxb r3, [r1+0]\n    and r3, 31",
+                                        load="mov r4, r1\n    add r4, r3\n    ldxb r5, [r4+0]"),
+    "offset": """
+    mov r0, 7
+    mov r3, 0
+    mov r6, r2
+    sub r6, 3
+    jsge r3, r6, done
+loop:
+    ldxb r5, [r3+2]
+    add r0, r5
+    add r3, 1
+    jlt r3, r6, loop
+done:
+    xor r0, r5
+    lsh r5, 9
+    xor r0, r5
+    xor r0, r3
+    exit
+""",
+}
+
+
+@pytest.mark.parametrize("name", sorted(COOP_PROGRAMS))
+def test_coop_byte_sum(cuda, oracle_mod, name):
+    """Counted byte-sum loops whose long ranges are summed cooperatively (coop_sum): production
+    and full outputs against the oracle on packets of 0-1500 bytes (lengths around the 128-byte
+    threshold included), aligned and misaligned packet bases, binned and unbinned batches."""
+    import numpy as np
+
+    from ebpf_emu import Program
+    from ebpf_emu.asm import assemble
+
+    img = assemble(COOP_PROGRAMS[name])
+    p = Program(img)
+    assert p.compile()
+    coop = "coop_sum" in p.jit_asm(2)
+    p.close()
+    if name != "offset":
+        assert coop, name
+    rng = random.Random(zlib.crc32(name.encode()))
+    for n in (700, 17000):
+        lens = [rng.choice([0, 1, 127, 128, 129, 130, 143, 144, 200, 1500, 1500, rng.randrange(1501)])
+                for _ in range(n)]
+        pkts = [bytes(rng.getrandbits(8) for _ in range(ln)) for ln in lens]
+        for layout in (dict(offsets_layout=True, align=16), dict(offsets_layout=True, misalign=5)):
+            prod = _run_prod(img, pkts, cuda, mem_size=2048, r10=2048, **layout)
+            (frames, nn), kw = _oracle_batch(pkts)
+            r0, st, cnt = oracle_mod.Program(img).run_batch(frames, nn, mem_size=2048, r10=2048,
+                                                            threads=8, **kw)
+            assert np.array_equal(prod["status"], st), (name, n, layout)
+            assert np.array_equal(prod["r0"], np.asarray(r0, dtype=np.uint64)), (name, n, layout)
+            assert list(prod["counters"]) == [int(c) for c in cnt], (name, n, layout)
+            if n == 700:
+                full = _run_full(img, pkts, cuda, mem_size=2048, r10=2048, **layout)
+                gen = _run_full(img, pkts, cuda, mem_size=2048, r10=2048, generic=True, **layout)
+                _same_outputs(full, gen, f"{name} {layout}")

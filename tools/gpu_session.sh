@@ -1,7 +1,7 @@
 #!/bin/bash
-# Runs GPU steps in order on the gpurun box. Each step has its own time limit. A test failure
-# (exit 1) does not stop the session; a crash-type exit (timeout 124/137, abort 134, segfault
-# 139, or anything >= 128) ends it immediately and nothing further touches the GPU.
+# Runs GPU steps in order on the gpurun box. Each step has its own time limit. Any failing step
+# ends the session (a failed test may be a GPU fault: nothing further touches the GPU); so does a
+# log that reports a GPU fault even where the step's exit status is 0.
 #   usage: tools/gpu_session.sh "name|seconds|command" ...
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 mkdir -p gpurun_out
@@ -15,10 +15,9 @@ for spec in "$@"; do
   rc=$?
   echo "=== [$name] exit $rc after $(( $(date +%s) - start ))s" | tee -a gpurun_out/session.log
   tail -n 25 "gpurun_out/$name.log"
-  if [ $rc -ge 124 ] && [ $rc -ne 0 ]; then
-    echo "=== stopping: crash-type exit $rc" | tee -a gpurun_out/session.log
-    exit $rc
+  if [ $rc -ne 0 ] || grep -qi "illegal memory access\|memory access fault\|hipErrorIllegalAddress" "gpurun_out/$name.log"; then
+    echo "=== stopping after [$name]: exit $rc" | tee -a gpurun_out/session.log
+    exit $(( rc ? rc : 1 ))
   fi
-  [ $rc -ne 0 ] && rc_all=$rc
 done
-exit $rc_all
+exit 0
