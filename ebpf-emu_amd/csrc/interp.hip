@@ -1452,6 +1452,17 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
 
   uint32_t cnt[7] = {0, 0, 0, 0, 0, 0, 0};  // per wave: < 2^32 packets
   uint32_t retired = 0;                      // per lane: <= 63 steps per tile
+  // diagnostics (EBPFEMU_TRACE=1, tools/trace_loop.py; JIT kernels only): s_memrealtime stamps of
+  // the wave's first tile -- entry, window ready, statement done, counters flushed -- its lane 0's
+  // packet length and the hardware ids
+  uint64_t* const trace =
+      JIT && a.trace && wave_slot < kTraceWaves ? a.trace + wave_slot * kTraceSlots : nullptr;
+  auto stamp = [&](uint32_t slot) {
+    uint64_t ts;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ts)::"memory");
+    if (threadIdx.x % kWave == 0) trace[slot] = ts;
+  };
+  if (trace) stamp(0);
 
   for (uint64_t tile = wave_slot; tile < a.n_tiles;) {
     // the lane index is re-derived inside the loop (volatile: not hoistable), so no per-lane
@@ -1494,6 +1505,15 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
     const uint64_t t = rfl64(tile);
     const uint64_t nt = t + total_waves;
     uint32_t bkt, nst;
+    if (trace && t == wave_slot) {
+      stamp(1);
+      if (!FIXED && threadIdx.x % kWave == 0) {
+        uintptr_t mb;
+        uint32_t ml;
+        meta_of(a, L, 0, tile, 0, mb, ml);
+        trace[4] = ml;
+      }
+    }
     if constexpr (JIT && LOOPS && STACK) {  // stack-window loop programs: v[56:95] too
       asm volatile(
 #include "tile_jit_stack.inc"
@@ -1549,6 +1569,7 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
 #pragma unroll
     for (int b = 0; b < 7; b++) cnt[b] += __builtin_popcountll(ballot(bkt == (uint32_t)b));
     retired += nst;
+    if (trace && t == wave_slot) stamp(2);
     tile = nt;
   }
   uint64_t cnt64[7];
@@ -1556,7 +1577,15 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
   for (int b = 0; b < 7; b++) cnt64[b] = cnt[b];
   uint32_t ln;
   asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+  if (trace) {
+    stamp(12);
+    uint32_t xcc, hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)\n\ts_getreg_b32 %1, hwreg(HW_REG_HW_ID)"
+                 : "=s"(xcc), "=s"(hw));
+    if (ln == 0) trace[14] = ((uint64_t)xcc << 32) | hw;
+  }
   flush_counters<WPB>(a, cnt64, retired, smem, ln, wv);
+  if (trace) stamp(13);
 }
 
 #ifndef EBPFEMU_JIT_TEMPLATE
@@ -1921,9 +1950,19 @@ int launch_kernel_id(int kind, const LaunchArgs& a, const JitFns* jit, bool stac
   return kind == kKindTier1 ? EBPF_KERNEL_GENERAL_T1 : EBPF_KERNEL_GENERAL_T0;
 }
 
+// The compiled loop kernel's grid (A/B): EBPFEMU_LOOP_GRID=persist -- balanced persistent waves
+// at the kernel's own occupancy (each wave a run of tiles, one counter flush per wave) instead of
+// one tile per wave.
+static int g_loop_grid = [] {
+  const char* e = getenv("EBPFEMU_LOOP_GRID");
+  return e ? (e[0] == 'p' ? 1 : 0) : -1;
+}();
+
 hipError_t launch_interp(int kind, const LaunchArgs& a, int grid, hipStream_t stream,
                          const JitFns* jit, bool stack) {
   const uint32_t lds = lds_bytes_for(kind, a.n_uops);
+  if (jit && jit->loop && kind == kKindLoop && g_loop_grid == 1)
+    grid = jit_grid(stack ? jit->loop_stack : jit->loop, lds, a.n_tiles);
   LaunchArgs b = a;
   // a shard word's sum must stay below 2^48: bound it by packets x steps per packet; and its
   // arrival count (16 bits) must reach the shard's workgroups - 1: at most 65535 members (the

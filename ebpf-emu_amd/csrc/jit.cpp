@@ -238,6 +238,7 @@ struct Compiler {
   bool qcache = false;  // with the 8-byte per-lane cache (ldx1_qword_cache)
   bool prefetch = false;  // zwin refills take the prefetched next window (refill_prefetch)
   int pf = 1;  // windows prefetched ahead (ebpf_tile_jit_loop_deep for 2, 3)
+  bool deep_regs = false;  // compiled for ebpf_tile_jit_loop_deep: v[72:105] are the program's
 
   Compiler(const std::vector<Uop>& u, const std::vector<TUop>& tt, bool lp = false, bool ex = false,
            const StackPlan* sp = nullptr)
@@ -2218,51 +2219,75 @@ struct Compiler {
            "v_sub_u32 " + v(44 + k) + ", " + v(44 + k) + ", v23\n"
            "v_sub_u32 " + v(48 + k) + ", " + v(48 + k) + ", v23\n"
            "v_mov_b32 " + v(52 + k) + ", 0\n";
-    r += "s_mov_b32 s64, 0\n" + C + "w:\n";
-    for (uint32_t k = 0; k < 4; k++)
-      r += "v_cmp_lt_i32 vcc, s64, " + v(48 + k) + "\n"
-           "s_mov_b64 exec, vcc\n"
-           "global_load_dwordx4 v[" + std::to_string(56 + 4 * k) + ":" + std::to_string(59 + 4 * k) +
-           "], " + vp(36 + 2 * k) + ", off\n"
-           "s_mov_b64 exec, -1\n";
-    r += "s_waitcnt vmcnt(0)\n";
-    for (uint32_t k = 0; k < 4; k++) {
-      const std::string K = std::to_string(k), A = v(52 + k);
-      // whole chunks (lo <= W, W + 16 <= hi), then the partial ones
-      r += "v_cmp_ge_i32 vcc, s64, " + v(44 + k) + "\n"
-           "v_subrev_u32 v24, 16, " + v(48 + k) + "\n"
-           "v_cmp_le_i32_e64 s[66:67], s64, v24\n"
-           "s_and_b64 s[66:67], s[66:67], vcc\n"
-           "v_cmp_lt_i32 vcc, s64, " + v(48 + k) + "\n"
-           "s_andn2_b64 vcc, vcc, s[66:67]\n"
-           "s_mov_b64 exec, s[66:67]\n";
-      for (uint32_t dw = 0; dw < 4; dw++)
-        r += "v_sad_u8 " + A + ", " + v(56 + 4 * k + dw) + ", 0, " + A + "\n";
-      r += "s_mov_b64 exec, vcc\n"
-           "s_cbranch_execz " + C + "s" + K + "\n"
-           "v_subrev_u32 v24, s64, " + v(44 + k) + "\n"
-           "v_subrev_u32 v25, s64, " + v(48 + k) + "\n";
-      for (uint32_t dw = 0; dw < 4; dw++) {
-        // bytes [clamp(lo - W - 4dw, 0, 4), clamp(hi - W - 4dw, 0, 4)) of dword dw
-        const std::string Dw = v(56 + 4 * k + dw), o4 = std::to_string(4 * dw);
-        r += "v_subrev_u32 v26, " + o4 + ", v24\nv_med3_i32 v26, v26, 0, 4\n"
-             "v_subrev_u32 v27, " + o4 + ", v25\nv_med3_i32 v27, v27, 0, 4\n"
-             "v_sub_u32 v27, v27, v26\nv_max_i32 v27, 0, v27\n"
-             "v_lshlrev_b32 v27, 3, v27\nv_lshlrev_b32 v26, 3, v26\n"
-             "v_bfm_b32 v23, v27, v26\n"
-             "v_cmp_eq_u32 s[66:67], 32, v27\n"  // (a 32-bit field: v_bfm's width is 5 bits)
-             "v_cndmask_b32_e64 v23, v23, -1, s[66:67]\n"
-             "v_and_b32 " + Dw + ", " + Dw + ", v23\n"
-             "v_sad_u8 " + A + ", " + Dw + ", 0, " + A + "\n";
+    // one round: the loads of round W (s64) into buffer `base`; its sums (buffer `base`)
+    auto loads = [&](uint32_t base, const std::string& W) {
+      std::string q;
+      for (uint32_t k = 0; k < 4; k++)
+        q += "v_cmp_lt_i32 vcc, " + W + ", " + v(48 + k) + "\n"
+             "s_mov_b64 exec, vcc\n"
+             "global_load_dwordx4 v[" + std::to_string(base + 4 * k) + ":" +
+             std::to_string(base + 3 + 4 * k) + "], " + vp(36 + 2 * k) + ", off" +
+             (W == "s64" ? std::string() : " offset:64") + "\n"
+             "s_mov_b64 exec, -1\n";
+      return q;
+    };
+    auto sums = [&](uint32_t base, const std::string& tag) {
+      std::string q;
+      for (uint32_t k = 0; k < 4; k++) {
+        const std::string K = tag + std::to_string(k), A = v(52 + k);
+        // whole chunks (lo <= W, W + 16 <= hi), then the partial ones
+        q += "v_cmp_ge_i32 vcc, s64, " + v(44 + k) + "\n"
+             "v_subrev_u32 v24, 16, " + v(48 + k) + "\n"
+             "v_cmp_le_i32_e64 s[66:67], s64, v24\n"
+             "s_and_b64 s[66:67], s[66:67], vcc\n"
+             "v_cmp_lt_i32 vcc, s64, " + v(48 + k) + "\n"
+             "s_andn2_b64 vcc, vcc, s[66:67]\n"
+             "s_mov_b64 exec, s[66:67]\n";
+        for (uint32_t dw = 0; dw < 4; dw++)
+          q += "v_sad_u8 " + A + ", " + v(base + 4 * k + dw) + ", 0, " + A + "\n";
+        q += "s_mov_b64 exec, vcc\n"
+             "s_cbranch_execz " + C + "s" + K + "\n"
+             "v_subrev_u32 v24, s64, " + v(44 + k) + "\n"
+             "v_subrev_u32 v25, s64, " + v(48 + k) + "\n";
+        for (uint32_t dw = 0; dw < 4; dw++) {
+          // bytes [clamp(lo - W - 4dw, 0, 4), clamp(hi - W - 4dw, 0, 4)) of dword dw
+          const std::string Dw = v(base + 4 * k + dw), o4 = std::to_string(4 * dw);
+          q += "v_subrev_u32 v26, " + o4 + ", v24\nv_med3_i32 v26, v26, 0, 4\n"
+               "v_subrev_u32 v27, " + o4 + ", v25\nv_med3_i32 v27, v27, 0, 4\n"
+               "v_sub_u32 v27, v27, v26\nv_max_i32 v27, 0, v27\n"
+               "v_lshlrev_b32 v27, 3, v27\nv_lshlrev_b32 v26, 3, v26\n"
+               "v_bfm_b32 v23, v27, v26\n"
+               "v_cmp_eq_u32 s[66:67], 32, v27\n"  // (a 32-bit field: v_bfm's width is 5 bits)
+               "v_cndmask_b32_e64 v23, v23, -1, s[66:67]\n"
+               "v_and_b32 " + Dw + ", " + Dw + ", v23\n"
+               "v_sad_u8 " + A + ", " + Dw + ", 0, " + A + "\n";
+        }
+        q += C + "s" + K + ":\ns_mov_b64 exec, -1\n";
       }
-      r += C + "s" + K + ":\ns_mov_b64 exec, -1\n";
+      return q;
+    };
+    // the next round: addresses + 64, W + 64; vcc = some lane has bytes at W
+    const std::string next =
+        "v_lshl_add_u64 " + vp(36) + ", " + vp(36) + ", 0, 64\n"
+        "v_lshl_add_u64 " + vp(38) + ", " + vp(38) + ", 0, 64\n"
+        "v_lshl_add_u64 " + vp(40) + ", " + vp(40) + ", 0, 64\n"
+        "v_lshl_add_u64 " + vp(42) + ", " + vp(42) + ", 0, 64\n"
+        "s_add_u32 s64, s64, 64\n"
+        "v_max3_i32 v24, v48, v49, v50\nv_max_i32 v24, v24, v51\n"
+        "v_cmp_lt_i32 vcc, s64, v24\n";
+    r += "s_mov_b32 s64, 0\n";
+    if (!deep_regs) {
+      r += C + "w:\n" + loads(56, "s64") + "s_waitcnt vmcnt(0)\n" + sums(56, "a") + next +
+           "s_cbranch_vccnz " + C + "w\n";
+    } else {
+      // (the deep kernel: two buffers, v[56:71] and v[72:87] -- the next round's loads are in
+      // flight while a round is summed; s65 = W + 64 for the early loads)
+      r += loads(56, "s64") + C + "w:\n"
+           "s_add_u32 s65, s64, 64\n" + loads(72, "s65") + "s_waitcnt vmcnt(4)\n" + sums(56, "a") +
+           next + "s_cbranch_vccz " + C + "x\n"
+           "s_add_u32 s65, s64, 64\n" + loads(56, "s65") + "s_waitcnt vmcnt(4)\n" + sums(72, "b") +
+           next + "s_cbranch_vccnz " + C + "w\n" + C + "x:\ns_waitcnt vmcnt(0)\n";
     }
-    for (uint32_t k = 0; k < 4; k++)
-      r += "v_lshl_add_u64 " + vp(36 + 2 * k) + ", " + vp(36 + 2 * k) + ", 0, 64\n";
-    r += "s_add_u32 s64, s64, 64\n"
-         "v_max3_i32 v24, v48, v49, v50\nv_max_i32 v24, v24, v51\n"
-         "v_cmp_lt_i32 vcc, s64, v24\n"
-         "s_cbranch_vccnz " + C + "w\n";
     // each packet's four partial sums (a quad) added, then moved to the packet's lane:
     // packet L's sum is in slot L / 16, lane 4 (L % 16)
     for (uint32_t k = 0; k < 4; k++)
@@ -2726,6 +2751,7 @@ bool compile_into_template(Compiler& c, Compiler* xc, std::vector<char>& code_ob
   // (EBPFEMU_LOOP_DEEP=1: the deep kernel, 4 waves per SIMD, with any depth: A/B of occupancy)
   const bool deep = xc && !c.stk && c.prefetches() && (pf_depth() != 1 || getenv("EBPFEMU_LOOP_DEEP"));
   if (deep) c.pf = xc->pf = pf_depth();  // (1 with EBPFEMU_LOOP_DEEP: refill_prefetch's own code)
+  c.deep_regs = xc ? (xc->deep_regs = deep) : false;
   for (const Marker& m : marks) {
     std::string b;
     const bool loop_marker = m.loops == "1";

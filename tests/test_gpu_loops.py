@@ -658,15 +658,20 @@ done:
 }
 
 
+@pytest.mark.parametrize("kernel", ["loop", "deep"])
 @pytest.mark.parametrize("name", sorted(COOP_PROGRAMS))
-def test_coop_byte_sum(cuda, oracle_mod, name):
+def test_coop_byte_sum(cuda, oracle_mod, monkeypatch, name, kernel):
     """Counted byte-sum loops whose long ranges are summed cooperatively (coop_sum): production
     and full outputs against the oracle on packets of 0-1500 bytes (lengths around the 128-byte
-    threshold included), aligned and misaligned packet bases, binned and unbinned batches."""
+    threshold included), aligned and misaligned packet bases, binned and unbinned batches; on the
+    loop kernel and on the deep kernel (two rounds of loads in flight)."""
     import numpy as np
 
     from ebpf_emu import Program
     from ebpf_emu.asm import assemble
+
+    if kernel == "deep":
+        monkeypatch.setenv("EBPFEMU_LOOP_DEEP", "1")
 
     img = assemble(COOP_PROGRAMS[name])
     p = Program(img)

@@ -113,6 +113,41 @@ __global__ __launch_bounds__(256) void scan_mixed(const uint8_t* frames, const u
   out[tile * 64 + lane] = acc;
 }
 
+// scan_mixed behind the loop kernel's tile prologue: the binned order's index (perm), the
+// offset through it, the first 64-byte window of every packet (four transposed loads), each level
+// waiting for the one before -- three dependent HBM round trips before the scan starts.
+__global__ __launch_bounds__(256) void scan_mixed_prologue(const uint8_t* frames, const uint64_t* offs,
+                                                           const uint32_t* perm, uint64_t n,
+                                                           uint32_t* out) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t tile = (uint64_t)blockIdx.x * 4 + threadIdx.x / 64;
+  if (tile * 64 >= n) return;
+  const uint32_t src = perm[tile * 64 + lane];
+  const uint64_t my = offs[src];
+  const uint32_t sub = lane % 4, pk = lane / 4;
+  uint32_t acc = 0;
+  const uint8_t* base[4];
+#pragma unroll
+  for (uint32_t r = 0; r < 4; r++)
+    base[r] = frames + __shfl(my, (int)(r * 16 + pk)) + sub * 16;
+  {
+    uint4 w[4];
+#pragma unroll
+    for (uint32_t r = 0; r < 4; r++) w[r] = *(const uint4*)base[r];
+#pragma unroll
+    for (uint32_t r = 0; r < 4; r++) acc = sad4(w[r], acc) & 1;
+  }
+  for (uint32_t s = 0; s < (kLen + 63) / 64; s++) {
+    uint4 c[4];
+    const uint32_t o = s * 64 + sub * 16;
+#pragma unroll
+    for (uint32_t r = 0; r < 4; r++) c[r] = o < kLen ? *(const uint4*)(base[r] + s * 64) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (uint32_t r = 0; r < 4; r++) acc = sad4(c[r], acc);
+  }
+  out[tile * 64 + lane] = acc;
+}
+
 template <typename K>
 static float time_it(K kernel, const uint8_t* f, uint64_t n, uint32_t* o, uint32_t lds = 0) {
   const int grid = (int)((n / 64 + 3) / 4);
@@ -173,6 +208,27 @@ int main() {
     (void)hipMemset(mf, 1, pos);
     (void)hipMemcpy(mo, off_long.data(), nl * 8, hipMemcpyHostToDevice);
     const int grid = (int)((nl / 64 + 3) / 4);
+    std::vector<uint32_t> idp(nl);
+    for (uint64_t i = 0; i < nl; i++) idp[i] = (uint32_t)i;
+    uint32_t* pm;
+    if (hipMalloc(&pm, nl * 4) != hipSuccess) return 1;
+    (void)hipMemcpy(pm, idp.data(), nl * 4, hipMemcpyHostToDevice);
+    for (uint32_t lds : {0u, 31u * 1024}) {
+      hipEvent_t a, b;
+      (void)hipEventCreate(&a);
+      (void)hipEventCreate(&b);
+      for (int i = 0; i < 3; i++)
+        hipLaunchKernelGGL(scan_mixed_prologue, dim3(grid), dim3(256), lds, 0, mf, mo, pm, nl, o);
+      (void)hipEventRecord(a);
+      for (int i = 0; i < 20; i++)
+        hipLaunchKernelGGL(scan_mixed_prologue, dim3(grid), dim3(256), lds, 0, mf, mo, pm, nl, o);
+      (void)hipEventRecord(b);
+      (void)hipEventSynchronize(b);
+      float ms = 0;
+      (void)hipEventElapsedTime(&ms, a, b);
+      const float us = ms * 1000.f / 20.f;
+      printf("mixed layout + tile prologue, %s %9.1f us\n", lds ? "5 waves/SIMD" : "full occupancy", us);
+    }
     for (uint32_t lds : {0u, 31u * 1024}) {
       hipEvent_t a, b;
       (void)hipEventCreate(&a);
