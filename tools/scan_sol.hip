@@ -148,6 +148,155 @@ __global__ __launch_bounds__(256) void scan_mixed_prologue(const uint8_t* frames
   out[tile * 64 + lane] = acc;
 }
 
+// Config 5 whole, unbinned: every wave takes 64 consecutive packets of the 50/50 mix (no length
+// order). Short packets (< 128 B): each lane reads its own 64 bytes (four dwordx4). Long ones: the
+// whole wave walks them one packet at a time, 64 lanes x 16 B per load instruction (1 KiB
+// contiguous, two loads for 1500 B), with D packets' loads in flight; the per-packet sum is reduced
+// across the wave and lands in the packet's lane.
+template <uint32_t D>
+__global__ __launch_bounds__(256) void scan_unbinned(const uint8_t* frames, const uint32_t* offs,
+                                                     const uint16_t* lens, uint64_t n, uint32_t* out) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t tile = (uint64_t)blockIdx.x * 4 + threadIdx.x / 64;
+  if (tile * 64 >= n) return;
+  const uint64_t me = tile * 64 + lane;
+  const uint32_t my_off = me < n ? offs[me] : 0, my_len = me < n ? lens[me] : 0;
+  uint32_t mine = 0;
+  const bool lng = my_len >= 128;
+  if (!lng && my_len) {
+    const uint4* p = (const uint4*)(frames + my_off);
+    for (uint32_t c = 0; c < 4; c++) {
+      uint4 v = p[c];
+      mine = sad4(v, mine);
+    }
+  }
+  uint64_t mask = __ballot(lng);
+  // ring of D packets in flight: lane reads 16 B at +16*lane and +1024+16*lane
+  uint4 b0[D], b1[D];
+  uint32_t who[D];
+  auto issue = [&](uint32_t s) {
+    if (mask) {
+      const uint32_t l = __builtin_ctzll(mask);
+      mask &= mask - 1;
+      who[s] = l;
+      const uint32_t o = __shfl(my_off, (int)l), ln = __shfl(my_len, (int)l);
+      const uint8_t* p = frames + o + lane * 16;
+      b0[s] = lane * 16 < ln ? *(const uint4*)p : make_uint4(0, 0, 0, 0);
+      b1[s] = 1024 + lane * 16 < ln ? *(const uint4*)(p + 1024) : make_uint4(0, 0, 0, 0);
+    } else {
+      who[s] = 64;
+    }
+  };
+#pragma unroll
+  for (uint32_t s = 0; s < D; s++) issue(s);
+  for (;;) {
+    bool any = false;
+#pragma unroll
+    for (uint32_t s = 0; s < D; s++) {
+      if (who[s] == 64) continue;
+      any = true;
+      uint32_t v = sad4(b1[s], sad4(b0[s], 0));
+      for (int m = 32; m; m >>= 1) v += __shfl_xor(v, m);
+      if (lane == who[s]) mine = v;
+      issue(s);
+    }
+    if (!any) break;
+  }
+  if (me < n) out[me] = mine;
+}
+
+// Config 5 whole, unbinned, the long packets compacted: lanes whose packet has >= 128 bytes get
+// ranks 0..C-1; groups of 32 of them are walked 128 bytes per packet per round (8 lanes x 16 B
+// per packet, 8 packets per load instruction, four instructions per round, full 128-byte lines),
+// with the next round's loads in flight (PF). Short packets: each lane reads its 64 bytes.
+template <bool PF>
+__global__ __launch_bounds__(256) void scan_unbinned_c128(const uint8_t* frames, const uint32_t* offs,
+                                                          const uint16_t* lens, uint64_t n,
+                                                          uint32_t* out) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t tile = (uint64_t)blockIdx.x * 4 + threadIdx.x / 64;
+  if (tile * 64 >= n) return;
+  const uint64_t me = tile * 64 + lane;
+  const uint32_t my_off = me < n ? offs[me] : 0, my_len = me < n ? lens[me] : 0;
+  uint32_t mine = 0;
+  const bool lng = my_len >= 128;
+  if (!lng && my_len) {
+    const uint4* p = (const uint4*)(frames + my_off);
+    for (uint32_t c = 0; c < 4; c++) {
+      uint4 v = p[c];
+      mine = sad4(v, mine);
+    }
+  }
+  const uint64_t mask = __ballot(lng);
+  const uint32_t C = __popcll(mask);
+  const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
+  // srcl[r] = the lane of rank r (a full permutation: the short lanes take ranks C..63)
+  const uint32_t srank = lng ? rank : C + (lane - rank);
+  const int srcl = __builtin_amdgcn_ds_permute((int)(srank * 4), (int)lane);
+  const uint32_t sub = (lane & 7) * 16;
+  for (uint32_t g = 0; g * 32 < C; g++) {
+    uint32_t o[4], hi[4], acc[4];
+    uint32_t mx = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) {
+      const uint32_t r = 32 * g + 8 * k + lane / 8;
+      const int s = __builtin_amdgcn_ds_bpermute((int)(r * 4), srcl);
+      o[k] = (uint32_t)__builtin_amdgcn_ds_bpermute(s * 4, (int)my_off) + sub;
+      hi[k] = r < C ? (uint32_t)__builtin_amdgcn_ds_bpermute(s * 4, (int)my_len) : 0u;
+      acc[k] = 0;
+      mx = max(mx, hi[k]);
+    }
+    for (int m = 32; m; m >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, m));
+    uint4 cur[4], nxt[4];
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++)
+      cur[k] = sub < hi[k] ? *(const uint4*)(frames + o[k]) : make_uint4(0, 0, 0, 0);
+    for (uint32_t W = 0; W < mx; W += 128) {
+      if (PF) {
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++)
+          nxt[k] = W + 128 + sub < hi[k] ? *(const uint4*)(frames + o[k] + W + 128)
+                                         : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (uint32_t k = 0; k < 4; k++) {
+        if (W + sub + 16 <= hi[k]) acc[k] = sad4(cur[k], acc[k]);
+        else if (W + sub < hi[k]) {  // a partial last chunk
+          const uint32_t b = hi[k] - W - sub;
+          uint32_t w[4] = {cur[k].x, cur[k].y, cur[k].z, cur[k].w};
+          for (uint32_t d = 0; d < 4; d++) {
+            const int keep = (int)b - (int)(4 * d);
+            const uint32_t m = keep >= 4 ? 0xffffffffu : keep <= 0 ? 0u : (1u << (8 * keep)) - 1;
+            acc[k] = __builtin_amdgcn_sad_u8(w[d] & m, 0, acc[k]);
+          }
+        }
+      }
+      if (PF) {
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++) cur[k] = nxt[k];
+      } else {
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++)
+          cur[k] = W + 128 + sub < hi[k] ? *(const uint4*)(frames + o[k] + W + 128)
+                                         : make_uint4(0, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) {
+      acc[k] += __shfl_xor((int)acc[k], 1);
+      acc[k] += __shfl_xor((int)acc[k], 2);
+      acc[k] += __shfl_xor((int)acc[k], 4);
+    }
+    // the lane of rank r (group g) takes slot k = (r % 32) / 8, lane 8 * (r % 8)
+    const uint32_t kk = (rank % 32) / 8, from = 8 * (rank % 8);
+    const uint32_t v0 = (uint32_t)__shfl((int)acc[0], (int)from), v1 = (uint32_t)__shfl((int)acc[1], (int)from),
+                   v2 = (uint32_t)__shfl((int)acc[2], (int)from), v3 = (uint32_t)__shfl((int)acc[3], (int)from);
+    if (lng && rank / 32 == g) mine = kk == 0 ? v0 : kk == 1 ? v1 : kk == 2 ? v2 : v3;
+  }
+  if (me < n) out[me] = mine;
+}
+
 template <typename K>
 static float time_it(K kernel, const uint8_t* f, uint64_t n, uint32_t* o, uint32_t lds = 0) {
   const int grid = (int)((n / 64 + 3) / 4);
@@ -228,6 +377,56 @@ int main() {
       (void)hipEventElapsedTime(&ms, a, b);
       const float us = ms * 1000.f / 20.f;
       printf("mixed layout + tile prologue, %s %9.1f us\n", lds ? "5 waves/SIMD" : "full occupancy", us);
+    }
+    {  // the whole mixed batch, unbinned, packet per instruction, D packets in flight
+      std::vector<uint32_t> offs(np);
+      std::vector<uint16_t> lens(np);
+      uint64_t p2 = 0, y = 0x5EED0005ull, tot = 0;
+      for (uint64_t i = 0; i < np; i++) {
+        y = y * 6364136223846793005ull + 1442695040888963407ull;
+        const bool lng = (y >> 33) & 1;
+        offs[i] = (uint32_t)p2;
+        lens[i] = lng ? 1500 : 64;
+        tot += lens[i];
+        p2 += lng ? 1536 : 64;
+      }
+      uint32_t *d_off, *o2;
+      uint16_t* d_len;
+      if (hipMalloc(&d_off, np * 4) != hipSuccess || hipMalloc(&d_len, np * 2) != hipSuccess ||
+          hipMalloc(&o2, np * 4) != hipSuccess)
+        return 1;
+      (void)hipMemcpy(d_off, offs.data(), np * 4, hipMemcpyHostToDevice);
+      (void)hipMemcpy(d_len, lens.data(), np * 2, hipMemcpyHostToDevice);
+      const int g2 = (int)((np / 64 + 3) / 4);
+      auto run = [&](auto kern, const char* name, uint32_t lds) {
+        hipEvent_t a, b;
+        (void)hipEventCreate(&a);
+        (void)hipEventCreate(&b);
+        for (int i = 0; i < 3; i++)
+          hipLaunchKernelGGL(kern, dim3(g2), dim3(256), lds, 0, mf, d_off, d_len, np, o2);
+        (void)hipEventRecord(a);
+        for (int i = 0; i < 20; i++)
+          hipLaunchKernelGGL(kern, dim3(g2), dim3(256), lds, 0, mf, d_off, d_len, np, o2);
+        (void)hipEventRecord(b);
+        (void)hipEventSynchronize(b);
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, a, b);
+        const float us = ms * 1000.f / 20.f;
+        printf("unbinned mixed 1 Mi, packet/instr, %-22s lds %6u %9.1f us  %7.0f GB/s\n", name, lds,
+               us, (double)(tot + np * 7) / (us * 1e3));
+      };
+      for (uint32_t lds : {0u, 31u * 1024, 39u * 1024}) {
+        run(scan_unbinned<1>, "D=1", lds);
+        run(scan_unbinned<2>, "D=2", lds);
+        run(scan_unbinned<4>, "D=4", lds);
+        run(scan_unbinned_c128<true>, "c128 prefetch", lds);
+        run(scan_unbinned_c128<false>, "c128 no prefetch", lds);
+        std::vector<uint32_t> got(np);
+        (void)hipMemcpy(got.data(), o2, np * 4, hipMemcpyDeviceToHost);
+        uint64_t bad = 0;
+        for (uint64_t i = 0; i < np; i++) bad += got[i] != lens[i];  // (every byte is 1)
+        printf("c128 sums wrong: %llu of %llu\n", (unsigned long long)bad, (unsigned long long)np);
+      }
     }
     for (uint32_t lds : {0u, 31u * 1024}) {
       hipEvent_t a, b;
