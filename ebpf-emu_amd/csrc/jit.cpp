@@ -239,6 +239,8 @@ struct Compiler {
   bool prefetch = false;  // zwin refills take the prefetched next window (refill_prefetch)
   int pf = 1;  // windows prefetched ahead (ebpf_tile_jit_loop_deep for 2, 3)
   bool deep_regs = false;  // compiled for ebpf_tile_jit_loop_deep: v[72:105] are the program's
+  mutable bool coop_emitted = false;  // a coop_sum entry was emitted (compile_into_template:
+                                      // such programs go to the deep kernel, unbinned)
 
   Compiler(const std::vector<Uop>& u, const std::vector<TUop>& tt, bool lp = false, bool ex = false,
            const StackPlan* sp = nullptr)
@@ -2073,7 +2075,10 @@ struct Compiler {
       return true;
     };
     std::string coop;
-    if (sum_add >= 0 && !getenv("EBPFEMU_NO_COOP_SUM")) coop = coop_sum(L, J, rI, rN, d, ld, sum_add, G, P);
+    if (sum_add >= 0 && !getenv("EBPFEMU_NO_COOP_SUM"))
+      coop = deep_regs && !getenv("EBPFEMU_COOP_STRIDED")
+                 ? coop_sum_compact(J, rI, rN, d, ld, sum_add, G, P)
+                 : coop_sum(L, J, rI, rN, d, ld, sum_add, G, P);
     std::string c = (coop.empty() ? G + "ent:\n" : coop + G + "ent2:\n") +
                     "s_mov_b64 s[44:45], exec\ns_mov_b64 s[46:47], 0\n"
                     "s_mov_b32 s41, 0x07060501\ns_mov_b32 s42, 0x07060502\n"
@@ -2328,6 +2333,204 @@ struct Compiler {
          "s_andn2_b64 exec, s[62:63], s[60:61]\n"
          "s_cbranch_execz .L" + P + "b" + std::to_string(J + 1) + "\n";
     (void)L;
+    coop_emitted = true;
+    return r;
+  }
+
+  // ---- coop_sum on the deep kernel: the cooperating lanes compacted ----
+  // The same result as coop_sum, but only the C cooperating lanes' packets are walked: lane ranks
+  // 0..C-1 (mbcnt over the cooperating mask; the other lanes take C..63, so ds_permute_b32 makes a
+  // full permutation srcl[rank] = lane), and LPP lanes read one packet, 16 bytes each, with LPP
+  // chosen from C so that four load instructions cover every packet: C <= 16 -> 16 lanes (256
+  // bytes per packet per round), C <= 32 -> 8 lanes (one 128-byte line), else 4 lanes (64 bytes).
+  // So a tile of 32 long packets among 32 short ones fills every lane of every load instead of
+  // half. Two buffers (v[56:71], v[72:87]): the next round's loads are in flight while a round is
+  // summed. After the rounds, each packet's LPP partial sums are added (DPP within a row) and
+  // moved to the packet's lane by ds_bpermute. Uses (deep kernel only) v[88:100] for the
+  // per-lane range, ranks and results and s41 for C, besides coop_sum's v[23:71] and s[60:67].
+  std::string coop_sum_compact(uint32_t J, uint32_t rI, uint32_t rN, int64_t d, int ld,
+                               int sum_add, const std::string& G, const std::string& P) const {
+    const std::string vI = "v" + std::to_string(2 * rI), vN = "v" + std::to_string(2 * rN),
+                      D0 = "v" + std::to_string(uops[ld].dst * 2),
+                      D1 = "v" + std::to_string(uops[ld].dst * 2 + 1),
+                      S = vpair(2 * uops[sum_add].dst, 0, 1), I2 = vpair(2 * rI, 0, 1),
+                      C = G + "k";
+    auto v = [](uint32_t r) { return "v" + std::to_string(r); };
+    auto vp = [](uint32_t r) { return "v[" + std::to_string(r) + ":" + std::to_string(r + 1) + "]"; };
+    auto num = [](int64_t x) { return std::to_string(x); };
+    std::string r = G + "ent:\n"
+                    "; the byte sum of whole ranges, compacted (coop_sum_compact)\n"
+                    "v_sub_u32 v46, " + vN + ", " + vI + "\n"
+                    "v_cmp_le_i32 vcc, " + num(kCoopMin) + ", v46\n"
+                    "s_and_b64 s[60:61], exec, vcc\n"
+                    "s_cbranch_scc0 " + G + "ent2\n"
+                    "s_mov_b64 s[62:63], exec\n"
+                    "s_mov_b64 exec, -1\n"
+                    "s_waitcnt vmcnt(0)\n"  // (refill prefetches may be in flight)
+                    // per lane: v[88:89] = (BASE + a0) & ~15, v90 = (BASE + a0) & 15, v91 = v90 + n
+                    // on the cooperating lanes (0 elsewhere: nothing is read for them)
+                    "v_sub_u32 v91, " + vN + ", " + vI + "\n" +
+                    (d ? "v_add_u32 v88, " + num(d) + ", " + vI + "\n" : "v_mov_b32 v88, " + vI + "\n") +
+                    "v_mov_b32 v89, 0\n"
+                    "v_lshl_add_u64 v[88:89], v[32:33], 0, v[88:89]\n"
+                    "v_and_b32 v90, 15, v88\n"
+                    "v_and_b32 v88, -16, v88\n"
+                    "v_add_u32 v91, v90, v91\n"
+                    "v_cndmask_b32_e64 v91, 0, v91, s[60:61]\n"
+                    // ranks: v93 = cooperating lanes below this one; srcl (v92) by forward permute
+                    "v_mbcnt_lo_u32_b32 v95, -1, 0\nv_mbcnt_hi_u32_b32 v95, -1, v95\n"
+                    "v_mbcnt_lo_u32_b32 v93, s60, 0\nv_mbcnt_hi_u32_b32 v93, s61, v93\n"
+                    "s_bcnt1_i32_b64 s41, s[60:61]\n"
+                    "v_sub_u32 v24, v95, v93\n"
+                    "v_add_u32 v24, s41, v24\n"
+                    "v_cndmask_b32_e64 v24, v24, v93, s[60:61]\n"
+                    "v_lshlrev_b32 v24, 2, v24\n"
+                    "ds_permute_b32 v92, v24, v95\n"
+                    "s_waitcnt lgkmcnt(0)\n"
+                    "s_cmp_gt_u32 s41, 32\n"
+                    "s_cbranch_scc1 " + C + "4\n"
+                    "s_cmp_gt_u32 s41, 16\n"
+                    "s_cbranch_scc1 " + C + "8\n";
+    // one variant per LPP (lanes per packet): PPI = 64 / LPP packets per load instruction
+    for (uint32_t lpp : {16u, 8u, 4u}) {
+      const uint32_t ppi = 64 / lpp, T = 16 * lpp, lg = lpp == 16 ? 4 : lpp == 8 ? 3 : 2,
+                     lgp = lpp == 16 ? 2 : lpp == 8 ? 3 : 4;
+      const std::string K = C + std::to_string(lpp);
+      r += K + ":\n"
+           "v_lshrrev_b32 v24, " + num(lg) + ", v95\n"
+           "v_lshlrev_b32 v24, 2, v24\n";
+      // slot k's packet: rank k * PPI + lane / LPP
+      const char* sr[4] = {"v25", "v26", "v27", "v23"};
+      for (uint32_t k = 0; k < 4; k++)
+        r += std::string("ds_bpermute_b32 ") + sr[k] + ", v24, v92" +
+             (k ? " offset:" + num(4 * ppi * k) : std::string()) + "\n";
+      r += "s_waitcnt lgkmcnt(0)\n";
+      for (uint32_t k = 0; k < 4; k++) r += std::string("v_lshlrev_b32 ") + sr[k] + ", 2, " + sr[k] + "\n";
+      for (uint32_t k = 0; k < 4; k++)
+        r += std::string("ds_bpermute_b32 ") + v(36 + 2 * k) + ", " + sr[k] + ", v88\n" +
+             "ds_bpermute_b32 " + v(37 + 2 * k) + ", " + sr[k] + ", v89\n" +
+             "ds_bpermute_b32 " + v(44 + k) + ", " + sr[k] + ", v90\n" +
+             "ds_bpermute_b32 " + v(48 + k) + ", " + sr[k] + ", v91\n";
+      r += "v_and_b32 v96, " + num(lpp - 1) + ", v95\n"
+           "v_lshlrev_b32 v96, 4, v96\n"
+           "s_waitcnt lgkmcnt(0)\n";
+      for (uint32_t k = 0; k < 4; k++)
+        r += "v_add_co_u32 " + v(36 + 2 * k) + ", vcc, " + v(36 + 2 * k) + ", v96\n"
+             "v_addc_co_u32 " + v(37 + 2 * k) + ", vcc, 0, " + v(37 + 2 * k) + ", vcc\n"
+             "v_sub_u32 " + v(44 + k) + ", " + v(44 + k) + ", v96\n"
+             "v_sub_u32 " + v(48 + k) + ", " + v(48 + k) + ", v96\n"
+             "v_mov_b32 " + v(52 + k) + ", 0\n";
+      auto loads = [&](uint32_t base, bool early) {
+        std::string q;
+        for (uint32_t k = 0; k < 4; k++)
+          q += "v_cmp_lt_i32 vcc, " + std::string(early ? "s65" : "s64") + ", " + v(48 + k) + "\n"
+               "s_mov_b64 exec, vcc\n"
+               "global_load_dwordx4 v[" + num(base + 4 * k) + ":" + num(base + 3 + 4 * k) + "], " +
+               vp(36 + 2 * k) + ", off" + (early ? " offset:" + num(T) : std::string()) + "\n"
+               "s_mov_b64 exec, -1\n";
+        return q;
+      };
+      auto sums = [&](uint32_t base, const std::string& tag) {
+        std::string q;
+        for (uint32_t k = 0; k < 4; k++) {
+          const std::string Kk = K + tag + std::to_string(k), A = v(52 + k);
+          q += "v_cmp_ge_i32 vcc, s64, " + v(44 + k) + "\n"
+               "v_subrev_u32 v24, 16, " + v(48 + k) + "\n"
+               "v_cmp_le_i32_e64 s[66:67], s64, v24\n"
+               "s_and_b64 s[66:67], s[66:67], vcc\n"
+               "v_cmp_lt_i32 vcc, s64, " + v(48 + k) + "\n"
+               "s_andn2_b64 vcc, vcc, s[66:67]\n"
+               "s_mov_b64 exec, s[66:67]\n";
+          for (uint32_t dw = 0; dw < 4; dw++)
+            q += "v_sad_u8 " + A + ", " + v(base + 4 * k + dw) + ", 0, " + A + "\n";
+          q += "s_mov_b64 exec, vcc\n"
+               "s_cbranch_execz " + Kk + "s\n"
+               "v_subrev_u32 v24, s64, " + v(44 + k) + "\n"
+               "v_subrev_u32 v25, s64, " + v(48 + k) + "\n";
+          for (uint32_t dw = 0; dw < 4; dw++) {
+            const std::string Dw = v(base + 4 * k + dw), o4 = num(4 * dw);
+            q += "v_subrev_u32 v26, " + o4 + ", v24\nv_med3_i32 v26, v26, 0, 4\n"
+                 "v_subrev_u32 v27, " + o4 + ", v25\nv_med3_i32 v27, v27, 0, 4\n"
+                 "v_sub_u32 v27, v27, v26\nv_max_i32 v27, 0, v27\n"
+                 "v_lshlrev_b32 v27, 3, v27\nv_lshlrev_b32 v26, 3, v26\n"
+                 "v_bfm_b32 v23, v27, v26\n"
+                 "v_cmp_eq_u32 s[66:67], 32, v27\n"
+                 "v_cndmask_b32_e64 v23, v23, -1, s[66:67]\n"
+                 "v_and_b32 " + Dw + ", " + Dw + ", v23\n"
+                 "v_sad_u8 " + A + ", " + Dw + ", 0, " + A + "\n";
+          }
+          q += Kk + "s:\ns_mov_b64 exec, -1\n";
+        }
+        return q;
+      };
+      // (s[46:47] = T: VOP3 takes no literal on gfx950)
+      const std::string next =
+          "v_lshl_add_u64 " + vp(36) + ", " + vp(36) + ", 0, s[46:47]\n"
+          "v_lshl_add_u64 " + vp(38) + ", " + vp(38) + ", 0, s[46:47]\n"
+          "v_lshl_add_u64 " + vp(40) + ", " + vp(40) + ", 0, s[46:47]\n"
+          "v_lshl_add_u64 " + vp(42) + ", " + vp(42) + ", 0, s[46:47]\n"
+          "s_add_u32 s64, s64, " + num(T) + "\n"
+          "v_max3_i32 v24, v48, v49, v50\nv_max_i32 v24, v24, v51\n"
+          "v_cmp_lt_i32 vcc, s64, v24\n";
+      r += "s_mov_b32 s64, 0\ns_mov_b32 s46, " + num(T) + "\ns_mov_b32 s47, 0\n" + loads(56, false) +
+           K + "w:\n"
+           "s_add_u32 s65, s64, " + num(T) + "\n" + loads(72, true) + "s_waitcnt vmcnt(4)\n" +
+           sums(56, "a") + next + "s_cbranch_vccz " + K + "x\n"
+           "s_add_u32 s65, s64, " + num(T) + "\n" + loads(56, true) + "s_waitcnt vmcnt(4)\n" +
+           sums(72, "b") + next + "s_cbranch_vccnz " + K + "w\n" + K + "x:\ns_waitcnt vmcnt(0)\n";
+      // each packet's LPP partial sums: quads, then rows (lane LPP * j + src of packet j)
+      for (uint32_t k = 0; k < 4; k++) {
+        const std::string A = v(52 + k);
+        r += "s_nop 1\nv_add_u32_dpp " + A + ", " + A + ", " + A +
+             " quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+             "s_nop 1\nv_add_u32_dpp " + A + ", " + A + ", " + A +
+             " quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n";
+        if (lpp >= 8)
+          r += "s_nop 1\nv_add_u32_dpp " + A + ", " + A + ", " + A +
+               " row_shr:4 row_mask:0xf bank_mask:0xf\n";
+        if (lpp == 16)
+          r += "s_nop 1\nv_add_u32_dpp " + A + ", " + A + ", " + A +
+               " row_shr:8 row_mask:0xf bank_mask:0xf\n";
+      }
+      const uint32_t src_off = lpp == 16 ? 12 : lpp == 8 ? 4 : 0;
+      // the cooperating lane of rank q: slot q / PPI, lane LPP * (q % PPI) + src_off
+      r += "v_and_b32 v24, " + num(ppi - 1) + ", v93\n"
+           "v_lshlrev_b32 v24, " + num(lg + 2) + ", v24\n" +
+           (src_off ? "v_add_u32 v24, " + num(4 * src_off) + ", v24\n" : std::string());
+      for (uint32_t k = 0; k < 4; k++)
+        r += "ds_bpermute_b32 " + v(97 + k) + ", v24, " + v(52 + k) + "\n";
+      r += "v_lshrrev_b32 v25, " + num(lgp) + ", v93\n"
+           "s_waitcnt lgkmcnt(0)\n";
+      for (uint32_t k = 1; k < 4; k++)
+        r += "v_cmp_eq_u32 vcc, " + num(k) + ", v25\n"
+             "v_cndmask_b32 v97, v97, " + v(97 + k) + ", vcc\n";
+      r += "s_branch " + C + "fin\n";
+    }
+    r += C + "fin:\n"
+         // the cooperating lanes: v24 = the bytes' sum, v25 = n, v26 = the last byte
+         "s_mov_b64 exec, s[60:61]\n"
+         "v_mov_b32 v24, v97\n"
+         "v_sub_u32 v25, " + vN + ", " + vI + "\n"
+         "v_add_u32 v26, " + vI + ", v25\n" +
+         (d - 1 ? "v_add_u32 v26, " + num(d - 1) + ", v26\n" : std::string()) +
+         "v_mov_b32 v27, 0\n"
+         "v_lshl_add_u64 v[26:27], v[32:33], 0, v[26:27]\n"
+         "global_load_ubyte v26, v[26:27], off\n"
+         "v_and_b32 v27, 0xffffff00, " + D0 + "\n"
+         "v_mad_u64_u32 v[42:43], s[66:67], v27, v25, 0\n"
+         "v_mul_lo_u32 v27, " + D1 + ", v25\n"
+         "v_add_u32 v43, v43, v27\n"
+         "v_add_co_u32 v42, vcc, v42, v24\nv_addc_co_u32 v43, vcc, 0, v43, vcc\n"
+         "v_lshl_add_u64 " + S + ", v[42:43], 0, " + S + "\n"
+         "v_mov_b32 v24, v25\nv_mov_b32 v25, 0\n"
+         "v_lshl_add_u64 " + I2 + ", " + I2 + ", 0, v[24:25]\n"
+         "s_waitcnt vmcnt(0)\n"
+         "v_bfi_b32 " + D0 + ", s56, v26, " + D0 + "\n"
+         "s_mov_b64 exec, -1\n"
+         "v_mov_b32 v55, 0x80000000\n" + invalidate_prefetch() +
+         "s_andn2_b64 exec, s[62:63], s[60:61]\n"
+         "s_cbranch_execz .L" + P + "b" + std::to_string(J + 1) + "\n";
+    coop_emitted = true;
     return r;
   }
 
@@ -2749,7 +2952,20 @@ bool compile_into_template(Compiler& c, Compiler* xc, std::vector<char>& code_ob
   const std::string init = c.init_code();
   // (loop programs whose refills prefetch go to the deep-prefetch loop kernel when pf_depth() > 1)
   // (EBPFEMU_LOOP_DEEP=1: the deep kernel, 4 waves per SIMD, with any depth: A/B of occupancy)
-  const bool deep = xc && !c.stk && c.prefetches() && (pf_depth() != 1 || getenv("EBPFEMU_LOOP_DEEP"));
+  bool deep = xc && !c.stk && c.prefetches() && (pf_depth() != 1 || getenv("EBPFEMU_LOOP_DEEP"));
+  // A loop program with a cooperative byte sum (coop_sum) goes to the deep kernel too, where the sum
+  // runs compacted (coop_sum_compact): found by a dry run of the loop kernel's body.
+  // EBPFEMU_NO_COOP_DEEP=1 keeps such programs on ebpf_tile_jit_loop (A/B).
+  if (!deep && xc && !c.stk && c.prefetches() && !getenv("EBPFEMU_NO_COOP_DEEP")) {
+    for (const Marker& m : marks)
+      if (m.loops == "1" && !m.deep && !m.stack) {
+        std::string dry;
+        c.coop_emitted = xc->coop_emitted = false;
+        deep = c.body_loop(m, *xc, dry) && (c.coop_emitted || xc->coop_emitted);
+        break;
+      }
+    c.coop_emitted = xc->coop_emitted = false;
+  }
   if (deep) c.pf = xc->pf = pf_depth();  // (1 with EBPFEMU_LOOP_DEEP: refill_prefetch's own code)
   c.deep_regs = xc ? (xc->deep_regs = deep) : false;
   for (const Marker& m : marks) {

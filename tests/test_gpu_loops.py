@@ -658,28 +658,34 @@ done:
 }
 
 
-@pytest.mark.parametrize("kernel", ["loop", "deep"])
+@pytest.mark.parametrize("kernel", ["loop", "deep_strided", "deep"])
 @pytest.mark.parametrize("name", sorted(COOP_PROGRAMS))
 def test_coop_byte_sum(cuda, oracle_mod, monkeypatch, name, kernel):
     """Counted byte-sum loops whose long ranges are summed cooperatively (coop_sum): production
     and full outputs against the oracle on packets of 0-1500 bytes (lengths around the 128-byte
     threshold included), aligned and misaligned packet bases, binned and unbinned batches; on the
-    loop kernel and on the deep kernel (two rounds of loads in flight)."""
+    loop kernel (EBPFEMU_NO_COOP_DEEP), on the deep kernel with the strided sum (two rounds of
+    loads in flight) and with the compacted one (the default: coop_sum_compact)."""
     import numpy as np
 
     from ebpf_emu import Program
     from ebpf_emu.asm import assemble
 
-    if kernel == "deep":
+    if kernel == "loop":
+        monkeypatch.setenv("EBPFEMU_NO_COOP_DEEP", "1")
+    elif kernel == "deep_strided":
         monkeypatch.setenv("EBPFEMU_LOOP_DEEP", "1")
+        monkeypatch.setenv("EBPFEMU_COOP_STRIDED", "1")
 
     img = assemble(COOP_PROGRAMS[name])
     p = Program(img)
     assert p.compile()
-    coop = "coop_sum" in p.jit_asm(2)
+    a = p.jit_asm(2)
+    coop = "coop_sum" in a
     p.close()
     if name != "offset":
         assert coop, name
+        assert ("coop_sum_compact" in a) == (kernel == "deep"), (name, kernel)
     rng = random.Random(zlib.crc32(name.encode()))
     for n in (700, 17000):
         lens = [rng.choice([0, 1, 127, 128, 129, 130, 143, 144, 200, 1500, 1500, rng.randrange(1501)])
@@ -697,3 +703,39 @@ def test_coop_byte_sum(cuda, oracle_mod, monkeypatch, name, kernel):
                 full = _run_full(img, pkts, cuda, mem_size=2048, r10=2048, **layout)
                 gen = _run_full(img, pkts, cuda, mem_size=2048, r10=2048, generic=True, **layout)
                 _same_outputs(full, gen, f"{name} {layout}")
+
+
+@pytest.mark.parametrize("name", ["sum", "start5_upper", "addr_copy"])
+def test_coop_compact_tile_densities(cuda, oracle_mod, name):
+    """coop_sum_compact picks 16, 8 or 4 lanes per packet from the number C of cooperating lanes
+    in a tile (C <= 16, <= 32, > 32): batch-order tiles with exactly C long packets (1..64, at
+    random positions, lengths 128-1500) among short ones, C across every threshold; production
+    outputs against the oracle, aligned and misaligned bases."""
+    import numpy as np
+
+    from ebpf_emu import Program
+    from ebpf_emu.asm import assemble
+
+    img = assemble(COOP_PROGRAMS[name])
+    p = Program(img)
+    assert p.compile()
+    assert "coop_sum_compact" in p.jit_asm(2)
+    p.close()
+    rng = random.Random(zlib.crc32(b"density" + name.encode()))
+    lens = []
+    for c in (1, 2, 15, 16, 17, 31, 32, 33, 48, 63, 64, 0, 5, 40):
+        tile = [rng.randrange(129, 1501) if i < c else rng.choice([0, 1, 64, 127, 128])
+                for i in range(64)]
+        rng.shuffle(tile)
+        lens += tile
+    pkts = [bytes(rng.getrandbits(8) for _ in range(ln)) for ln in lens]
+    for layout in (dict(offsets_layout=True, align=16), dict(offsets_layout=True, misalign=3)):
+        prod = _run_prod(img, pkts, cuda, mem_size=2048, r10=2048, **layout)
+        (frames, nn), kw = _oracle_batch(pkts)
+        r0, st, cnt = oracle_mod.Program(img).run_batch(frames, nn, mem_size=2048, r10=2048,
+                                                        threads=8, **kw)
+        assert np.array_equal(prod["status"], st), (name, layout)
+        assert np.array_equal(prod["r0"], np.asarray(r0, dtype=np.uint64)), (name, layout)
+        assert list(prod["counters"]) == [int(c) for c in cnt], (name, layout)
+        full = _run_full(img, pkts, cuda, mem_size=2048, r10=2048, **layout)
+        assert np.array_equal(full["r0"], prod["r0"]) and np.array_equal(full["status"], st)
