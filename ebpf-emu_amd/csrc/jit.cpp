@@ -2377,6 +2377,8 @@ struct Compiler {
                     "v_and_b32 v88, -16, v88\n"
                     "v_add_u32 v91, v90, v91\n"
                     "v_cndmask_b32_e64 v91, 0, v91, s[60:61]\n"
+                    "v_mov_b32 v94, 0\n" +
+                    coop_window_part(vI, vN, d, G) +
                     // ranks: v93 = cooperating lanes below this one; srcl (v92) by forward permute
                     "v_mbcnt_lo_u32_b32 v95, -1, 0\nv_mbcnt_hi_u32_b32 v95, -1, v95\n"
                     "v_mbcnt_lo_u32_b32 v93, s60, 0\nv_mbcnt_hi_u32_b32 v93, s61, v93\n"
@@ -2509,7 +2511,7 @@ struct Compiler {
     r += C + "fin:\n"
          // the cooperating lanes: v24 = the bytes' sum, v25 = n, v26 = the last byte
          "s_mov_b64 exec, s[60:61]\n"
-         "v_mov_b32 v24, v97\n"
+         "v_add_u32 v24, v97, v94\n"
          "v_sub_u32 v25, " + vN + ", " + vI + "\n"
          "v_add_u32 v26, " + vI + ", v25\n" +
          (d - 1 ? "v_add_u32 v26, " + num(d - 1) + ", v26\n" : std::string()) +
@@ -2531,6 +2533,52 @@ struct Compiler {
          "s_andn2_b64 exec, s[62:63], s[60:61]\n"
          "s_cbranch_execz .L" + P + "b" + std::to_string(J + 1) + "\n";
     coop_emitted = true;
+    return r;
+  }
+
+  // coop_sum_compact's use of the lane's LDS window: a cooperating lane whose window [WB, WB + 64)
+  // (v22 = WB, the packet offset the window holds; invalid tags are never within 64 of a0) covers
+  // a0 sums the window's bytes [a0 - WB, 64) here -- every one in the range, since n >= 128 --
+  // into v94, and its HBM range starts at WB + 64 instead (v[88:91] redone), so the bytes the
+  // tile's window DMA already brought are not fetched again. Runs with exec = -1, v[88:91] set.
+  std::string coop_window_part(const std::string& vI, const std::string& vN, int64_t d,
+                               const std::string& G) const {
+    if (getenv("EBPFEMU_COOP_NO_WINDOW")) return "";
+    std::string r = "; the window's part of the range\n" +
+                    (d ? "v_add_u32 v24, " + std::to_string(d) + ", " + vI + "\n"
+                       : "v_mov_b32 v24, " + vI + "\n") +
+                    "v_sub_u32 v25, v24, v22\n"  // off = a0 - WB
+                    "v_cmp_gt_u32 vcc, 64, v25\n"
+                    "s_and_b64 s[66:67], vcc, s[60:61]\n"
+                    "s_mov_b64 exec, s[66:67]\n"
+                    "s_cbranch_execz " + G + "nowin\n"
+                    "s_waitcnt lgkmcnt(0)\n";
+    for (int c = 0; c < 4; c++)
+      r += "v_xad_u32 v26, v35, " + std::to_string(16 * c) + ", v34\n"
+           "ds_read_b128 v[" + std::to_string(56 + 4 * c) + ":" + std::to_string(59 + 4 * c) + "], v26\n";
+    r += "s_waitcnt lgkmcnt(0)\n";
+    for (int j = 0; j < 16; j++) {
+      // dword j keeps its bytes at window offsets >= off: mask = low dword of (~0 << 8 m),
+      // m = clamp(off - 4 j, 0, 4)
+      const std::string Dw = "v" + std::to_string(56 + j);
+      r += "v_subrev_u32 v26, " + std::to_string(4 * j) + ", v25\n"
+           "v_med3_i32 v26, v26, 0, 4\n"
+           "v_lshlrev_b32 v26, 3, v26\n"
+           "v_lshlrev_b64 v[26:27], v26, -1\n"
+           "v_and_b32 " + Dw + ", " + Dw + ", v26\n"
+           "v_sad_u8 v94, " + Dw + ", 0, v94\n";
+    }
+    // the HBM range: [WB + 64, a0 + n)
+    r += "v_sub_u32 v27, " + vN + ", " + vI + "\n"  // n
+         "v_add_u32 v27, v27, v25\n"                  // n + off
+         "v_subrev_u32 v27, 64, v27\n"                // a0 + n - (WB + 64)
+         "v_add_u32 v88, 64, v22\n"
+         "v_mov_b32 v89, 0\n"
+         "v_lshl_add_u64 v[88:89], v[32:33], 0, v[88:89]\n"
+         "v_and_b32 v90, 15, v88\n"
+         "v_and_b32 v88, -16, v88\n"
+         "v_add_u32 v91, v90, v27\n" + G + "nowin:\n"
+         "s_mov_b64 exec, -1\n";
     return r;
   }
 
