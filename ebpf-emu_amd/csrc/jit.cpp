@@ -57,6 +57,11 @@ struct Marker {
 };
 
 bool inline_const(int64_t v) { return v >= -16 && v <= 64; }
+// rounds of coop_sum_compact's loads in flight (EBPFEMU_COOP_DEPTH=2|3, default 3)
+int coop_depth() {
+  const char* e = getenv("EBPFEMU_COOP_DEPTH");
+  return e && e[0] == '2' ? 2 : 3;
+}
 
 std::string hex32(uint32_t v) {
   char b[16];
@@ -2344,10 +2349,12 @@ struct Compiler {
   // chosen from C so that four load instructions cover every packet: C <= 16 -> 16 lanes (256
   // bytes per packet per round), C <= 32 -> 8 lanes (one 128-byte line), else 4 lanes (64 bytes).
   // So a tile of 32 long packets among 32 short ones fills every lane of every load instead of
-  // half. Two buffers (v[56:71], v[72:87]): the next round's loads are in flight while a round is
-  // summed. After the rounds, each packet's LPP partial sums are added (DPP within a row) and
-  // moved to the packet's lane by ds_bpermute. Uses (deep kernel only) v[88:100] for the
-  // per-lane range, ranks and results and s41 for C, besides coop_sum's v[23:71] and s[60:67].
+  // half. Three buffers (v[56:71], v[72:87], v[88:103]): the next two rounds' loads are in flight
+  // while a round is summed. After the rounds, each packet's LPP partial sums are added (DPP
+  // within a row) and moved to the packet's lane by ds_bpermute. Uses (deep kernel only; every
+  // prefetch stage is invalidated after) v[88:96] for the per-lane ranges and ranks before the
+  // rounds, v[97:100] after them, v104 for the window's part, s41 for C and s[46:47], besides
+  // coop_sum's v[23:71] and s[60:67].
   std::string coop_sum_compact(uint32_t J, uint32_t rI, uint32_t rN, int64_t d, int ld,
                                int sum_add, const std::string& G, const std::string& P) const {
     const std::string vI = "v" + std::to_string(2 * rI), vN = "v" + std::to_string(2 * rN),
@@ -2377,7 +2384,7 @@ struct Compiler {
                     "v_and_b32 v88, -16, v88\n"
                     "v_add_u32 v91, v90, v91\n"
                     "v_cndmask_b32_e64 v91, 0, v91, s[60:61]\n"
-                    "v_mov_b32 v94, 0\n" +
+                    "v_mov_b32 v104, 0\n" +
                     coop_window_part(vI, vN, d, G) +
                     // ranks: v93 = cooperating lanes below this one; srcl (v92) by forward permute
                     "v_mbcnt_lo_u32_b32 v95, -1, 0\nv_mbcnt_hi_u32_b32 v95, -1, v95\n"
@@ -2422,13 +2429,14 @@ struct Compiler {
              "v_sub_u32 " + v(44 + k) + ", " + v(44 + k) + ", v96\n"
              "v_sub_u32 " + v(48 + k) + ", " + v(48 + k) + ", v96\n"
              "v_mov_b32 " + v(52 + k) + ", 0\n";
-      auto loads = [&](uint32_t base, bool early) {
-        std::string q;
+      // the loads of round s64 + m T into the buffer at `base` (m > 0: s65 = s64 + m T)
+      auto loads = [&](uint32_t base, uint32_t m) {
+        std::string q = m ? "s_add_u32 s65, s64, " + num(m * T) + "\n" : std::string();
         for (uint32_t k = 0; k < 4; k++)
-          q += "v_cmp_lt_i32 vcc, " + std::string(early ? "s65" : "s64") + ", " + v(48 + k) + "\n"
+          q += "v_cmp_lt_i32 vcc, " + std::string(m ? "s65" : "s64") + ", " + v(48 + k) + "\n"
                "s_mov_b64 exec, vcc\n"
                "global_load_dwordx4 v[" + num(base + 4 * k) + ":" + num(base + 3 + 4 * k) + "], " +
-               vp(36 + 2 * k) + ", off" + (early ? " offset:" + num(T) : std::string()) + "\n"
+               vp(36 + 2 * k) + ", off" + (m ? " offset:" + num(m * T) : std::string()) + "\n"
                "s_mov_b64 exec, -1\n";
         return q;
       };
@@ -2474,12 +2482,20 @@ struct Compiler {
           "s_add_u32 s64, s64, " + num(T) + "\n"
           "v_max3_i32 v24, v48, v49, v50\nv_max_i32 v24, v24, v51\n"
           "v_cmp_lt_i32 vcc, s64, v24\n";
-      r += "s_mov_b32 s64, 0\ns_mov_b32 s46, " + num(T) + "\ns_mov_b32 s47, 0\n" + loads(56, false) +
-           K + "w:\n"
-           "s_add_u32 s65, s64, " + num(T) + "\n" + loads(72, true) + "s_waitcnt vmcnt(4)\n" +
-           sums(56, "a") + next + "s_cbranch_vccz " + K + "x\n"
-           "s_add_u32 s65, s64, " + num(T) + "\n" + loads(56, true) + "s_waitcnt vmcnt(4)\n" +
-           sums(72, "b") + next + "s_cbranch_vccnz " + K + "w\n" + K + "x:\ns_waitcnt vmcnt(0)\n";
+      // three rounds in flight (v[56:71], v[72:87], v[88:103]): a round is summed while the
+      // next two are loading (EBPFEMU_COOP_DEPTH=2: two buffers, A/B)
+      r += "s_mov_b32 s64, 0\ns_mov_b32 s46, " + num(T) + "\ns_mov_b32 s47, 0\n" + loads(56, 0);
+      if (coop_depth() == 2) {
+        r += K + "w:\n" + loads(72, 1) + "s_waitcnt vmcnt(4)\n" + sums(56, "a") + next +
+             "s_cbranch_vccz " + K + "x\n" + loads(56, 1) + "s_waitcnt vmcnt(4)\n" + sums(72, "b") +
+             next + "s_cbranch_vccnz " + K + "w\n";
+      } else {
+        r += loads(72, 1) + K + "w:\n" + loads(88, 2) + "s_waitcnt vmcnt(8)\n" + sums(56, "a") +
+             next + "s_cbranch_vccz " + K + "x\n" + loads(56, 2) + "s_waitcnt vmcnt(8)\n" +
+             sums(72, "b") + next + "s_cbranch_vccz " + K + "x\n" + loads(72, 2) +
+             "s_waitcnt vmcnt(8)\n" + sums(88, "c") + next + "s_cbranch_vccnz " + K + "w\n";
+      }
+      r += K + "x:\ns_waitcnt vmcnt(0)\n";
       // each packet's LPP partial sums: quads, then rows (lane LPP * j + src of packet j)
       for (uint32_t k = 0; k < 4; k++) {
         const std::string A = v(52 + k);
@@ -2496,7 +2512,8 @@ struct Compiler {
       }
       const uint32_t src_off = lpp == 16 ? 12 : lpp == 8 ? 4 : 0;
       // the cooperating lane of rank q: slot q / PPI, lane LPP * (q % PPI) + src_off
-      r += "v_and_b32 v24, " + num(ppi - 1) + ", v93\n"
+      r += "v_mbcnt_lo_u32_b32 v93, s60, 0\nv_mbcnt_hi_u32_b32 v93, s61, v93\n"  // (the ranks again)
+           "v_and_b32 v24, " + num(ppi - 1) + ", v93\n"
            "v_lshlrev_b32 v24, " + num(lg + 2) + ", v24\n" +
            (src_off ? "v_add_u32 v24, " + num(4 * src_off) + ", v24\n" : std::string());
       for (uint32_t k = 0; k < 4; k++)
@@ -2511,7 +2528,7 @@ struct Compiler {
     r += C + "fin:\n"
          // the cooperating lanes: v24 = the bytes' sum, v25 = n, v26 = the last byte
          "s_mov_b64 exec, s[60:61]\n"
-         "v_add_u32 v24, v97, v94\n"
+         "v_add_u32 v24, v97, v104\n"
          "v_sub_u32 v25, " + vN + ", " + vI + "\n"
          "v_add_u32 v26, " + vI + ", v25\n" +
          (d - 1 ? "v_add_u32 v26, " + num(d - 1) + ", v26\n" : std::string()) +
@@ -2539,7 +2556,7 @@ struct Compiler {
   // coop_sum_compact's use of the lane's LDS window: a cooperating lane whose window [WB, WB + 64)
   // (v22 = WB, the packet offset the window holds; invalid tags are never within 64 of a0) covers
   // a0 sums the window's bytes [a0 - WB, 64) here -- every one in the range, since n >= 128 --
-  // into v94, and its HBM range starts at WB + 64 instead (v[88:91] redone), so the bytes the
+  // into v104, and its HBM range starts at WB + 64 instead (v[88:91] redone), so the bytes the
   // tile's window DMA already brought are not fetched again. Runs with exec = -1, v[88:91] set.
   std::string coop_window_part(const std::string& vI, const std::string& vN, int64_t d,
                                const std::string& G) const {
@@ -2566,7 +2583,7 @@ struct Compiler {
            "v_lshlrev_b32 v26, 3, v26\n"
            "v_lshlrev_b64 v[26:27], v26, -1\n"
            "v_and_b32 " + Dw + ", " + Dw + ", v26\n"
-           "v_sad_u8 v94, " + Dw + ", 0, v94\n";
+           "v_sad_u8 v104, " + Dw + ", 0, v104\n";
     }
     // the HBM range: [WB + 64, a0 + n)
     r += "v_sub_u32 v27, " + vN + ", " + vI + "\n"  // n

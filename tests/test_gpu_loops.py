@@ -658,7 +658,7 @@ done:
 }
 
 
-@pytest.mark.parametrize("kernel", ["loop", "deep_strided", "deep"])
+@pytest.mark.parametrize("kernel", ["loop", "deep_strided", "deep2", "deep"])
 @pytest.mark.parametrize("name", sorted(COOP_PROGRAMS))
 def test_coop_byte_sum(cuda, oracle_mod, monkeypatch, name, kernel):
     """Counted byte-sum loops whose long ranges are summed cooperatively (coop_sum): production
@@ -676,6 +676,8 @@ def test_coop_byte_sum(cuda, oracle_mod, monkeypatch, name, kernel):
     elif kernel == "deep_strided":
         monkeypatch.setenv("EBPFEMU_LOOP_DEEP", "1")
         monkeypatch.setenv("EBPFEMU_COOP_STRIDED", "1")
+    elif kernel == "deep2":  # (two rounds of loads in flight instead of three)
+        monkeypatch.setenv("EBPFEMU_COOP_DEPTH", "2")
 
     img = assemble(COOP_PROGRAMS[name])
     p = Program(img)
@@ -685,7 +687,7 @@ def test_coop_byte_sum(cuda, oracle_mod, monkeypatch, name, kernel):
     p.close()
     if name != "offset":
         assert coop, name
-        assert ("coop_sum_compact" in a) == (kernel == "deep"), (name, kernel)
+        assert ("coop_sum_compact" in a) == (kernel in ("deep", "deep2")), (name, kernel)
     rng = random.Random(zlib.crc32(name.encode()))
     for n in (700, 17000):
         lens = [rng.choice([0, 1, 127, 128, 129, 130, 143, 144, 200, 1500, 1500, rng.randrange(1501)])
