@@ -283,6 +283,10 @@ def main():
                      "ebpf_lane_insts_per_s": None,
                      "source": os.path.relpath(pj, ROOT)}
 
+    kid = prog.batch_kernel(descs[0], out, local)
+    kernel_name = _lib.KERNEL_NAMES[kid]
+    if kid == _lib.EBPF_KERNEL_JIT_LOOP:  # (the loop program's kernel: plain or deep)
+        kernel_name = prog.jit_loop_kernel() + " (compiled loop program)"
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(args, img, batches[0], mixed, n, mem_size, r10)
@@ -328,7 +332,7 @@ def main():
                 "kernel_avg_us": round(kern_avg_ms * 1e3, 3),
                 # HIP events bracket one whole batch: one interpreter launch (with counters, its
                 # last workgroup folds the per-shard sums into them)
-                "kernel": _lib.KERNEL_NAMES[prog.batch_kernel(descs[0], out, local)],
+                "kernel": kernel_name,
             },
             "issue_roofline": issue,
             "counters": {"drop": cnt[1], "pass": cnt[2], "other": cnt[5], "faults": cnt[6],

@@ -89,6 +89,19 @@ class Program:
         L.ebpf_prog_jit_asm(self._h, variant, buf, n.value + 1, ctypes.byref(n))
         return buf.value.decode()
 
+    def jit_loop_kernel(self) -> str:
+        """The template kernel holding this program's compiled loop code (EBPF_KERNEL_JIT_LOOP
+        names either): "ebpf_tile_jit_loop_deep" when the loop program went to the deep kernel
+        (cooperative byte sums, or a deeper refill prefetch), else "ebpf_tile_jit_loop"."""
+        a = self.jit_asm(2)
+        at = 0
+        for ln in a.splitlines(keepends=True):
+            at += len(ln)
+            if ln.startswith("; JIT N=") and " loops=1" in ln and " stack=1" not in ln:
+                if "not this program's kernel" not in a[at:at + 80]:
+                    return "ebpf_tile_jit_loop_deep" if " deep=1" in ln else "ebpf_tile_jit_loop"
+        return "ebpf_tile_jit_loop"
+
     @property
     def instructions(self):
         return _decoded(self._h)
