@@ -1452,11 +1452,11 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
 
   uint32_t cnt[7] = {0, 0, 0, 0, 0, 0, 0};  // per wave: < 2^32 packets
   uint32_t retired = 0;                      // per lane: <= 63 steps per tile
-  // diagnostics (EBPFEMU_TRACE=1, tools/trace_loop.py; JIT kernels only): s_memrealtime stamps of
+  // diagnostics (EBPFEMU_TRACE=1, tools/trace_loop.py; the JIT loop kernels only): s_memrealtime stamps of
   // the wave's first tile -- entry, window ready, statement done, counters flushed -- its lane 0's
   // packet length and the hardware ids
   uint64_t* const trace =
-      JIT && a.trace && wave_slot < kTraceWaves ? a.trace + wave_slot * kTraceSlots : nullptr;
+      JIT && LOOPS && a.trace && wave_slot < kTraceWaves ? a.trace + wave_slot * kTraceSlots : nullptr;
   auto stamp = [&](uint32_t slot) {
     uint64_t ts;
     asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ts)::"memory");
