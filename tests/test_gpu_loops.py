@@ -741,3 +741,28 @@ def test_coop_compact_tile_densities(cuda, oracle_mod, name):
         assert list(prod["counters"]) == [int(c) for c in cnt], (name, layout)
         full = _run_full(img, pkts, cuda, mem_size=2048, r10=2048, **layout)
         assert np.array_equal(full["r0"], prod["r0"]) and np.array_equal(full["status"], st)
+
+
+@pytest.mark.parametrize("name", ["sum", "start5_upper"])
+def test_coop_budget_edges(cuda, oracle_mod, name):
+    """Step budgets around what the longest cooperating packets need (coop_sum_compact runs under
+    a budget the counted entry proved sufficient; one step less must end in ST_STEPS exactly
+    where the oracle stops): budgets = the largest packet's steps, one less, and the median --
+    production outputs, verdicts and counters against the oracle."""
+    from ebpf_emu import Program
+    from ebpf_emu.asm import assemble
+
+    img = assemble(COOP_PROGRAMS[name])
+    p = Program(img)
+    assert p.compile() and "coop_sum_compact" in p.jit_asm(2)
+    p.close()
+    rng = random.Random(zlib.crc32(b"budget" + name.encode()))
+    lens = [rng.choice([64, 127, 128, 600, 1499, 1500, rng.randrange(129, 1501)]) for _ in range(640)]
+    pkts = [bytes(rng.getrandbits(8) for _ in range(ln)) for ln in lens]
+    op = oracle_mod.Program(img)
+    steps = sorted(op.run_packet(q, 2048, 2048, 1 << 22)[2] for q in pkts)
+    for budget in (steps[-1], steps[-1] - 1, steps[len(steps) // 2]):
+        prod = _run_prod(img, pkts, cuda, mem_size=2048, r10=2048, max_steps=budget,
+                         offsets_layout=True, align=16)
+        _check_prod_against_oracle(oracle_mod, img, pkts, prod, mem_size=2048, r10=2048,
+                                   max_steps=budget, tag=f"{name} budget {budget}")

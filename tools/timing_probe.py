@@ -37,19 +37,27 @@ def main():
     res = {}
     s = torch.cuda.Stream(dev)
 
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipStreamSynchronize.argtypes = [ctypes.c_void_p]
+    null = torch.cuda.current_stream(dev)
+
     def run(K, mode, graph=None):
         ev0 = torch.cuda.Event(enable_timing=True)
         ev1 = torch.cuda.Event(enable_timing=True)
+        st = null if mode in ("null", "null_hipsync") else s
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
-        ev0.record(s)
+        ev0.record(st)
         if graph is not None:
             graph.replay()
         else:
             for i in range(K):
-                prog.launch(descs[i % 8], out, s)
-        ev1.record(s)
-        if mode != "sync":
+                prog.launch(descs[i % 8], out, st)
+        ev1.record(st)
+        if mode in ("hipsync", "null_hipsync"):
+            hip.hipStreamSynchronize(ctypes.c_void_p(st.cuda_stream))
+        elif mode not in ("sync", "null"):
             while not ev1.query():
                 pass
         torch.cuda.synchronize(dev)
@@ -60,7 +68,7 @@ def main():
         prog.launch(descs[i % 8], out, s)
     torch.cuda.synchronize(dev)
     for K in (1, 5, 20, 200):
-        for mode in ("sync", "poll", "graph"):
+        for mode in ("sync", "poll", "graph", "null", "hipsync", "null_hipsync"):
             g = None
             if mode == "graph":
                 g = torch.cuda.CUDAGraph()
