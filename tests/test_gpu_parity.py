@@ -658,3 +658,99 @@ def test_emu_any_image_length_and_frame_stack(cuda, oracle_mod):
             with pytest.raises(EmuPanic) as e:
                 emu.run()
             assert e.value.status == st, src
+
+
+@pytest.mark.parametrize("config", ["5tuple", "checksum"])
+@pytest.mark.parametrize("own_ws", [True, False])
+def test_concurrent_streams(cuda, config, own_ws):
+    """Consecutive batches on two streams (bench.py --streams 2): launches alternate over two
+    streams that run at once, each with its own workspace (explicit, or the library's per-stream
+    one) and verdict buffer, all folding into ONE counters array. Every stream's verdicts equal a
+    one-stream run's, and the shared counters equal the sum of the one-stream runs."""
+    import torch
+
+    from ebpf_emu import Program, _lib
+    from ebpf_emu import workloads as W
+
+    n = 1 << 16
+    prog = Program(W.program(config))
+    prog.upload(0)
+    keep = []  # (the device buffers the batch descriptors point into)
+    descs = []
+    for k in range(3):
+        if config == "checksum":
+            b, o, ln = W.frames_mixed(n, config_id=5 + 100 * k)
+            t = [torch.from_numpy(b).to(cuda), torch.from_numpy(o.view(np.int32)).to(cuda),
+                 torch.from_numpy(ln.view(np.int16)).to(cuda)]
+            descs.append(prog.make_batch(t[0], n=n, offsets=t[1], lens=t[2], mem_size=2048,
+                                         r10=2048))
+        else:
+            t = [torch.from_numpy(W.frames_fixed(n, 64, 3 + 100 * k)).to(cuda)]
+            descs.append(prog.make_batch(t[0], n=n, stride=64, mem_size=1024, r10=512))
+        keep += t
+    # one stream, one batch at a time: the reference verdicts and counters
+    ref_v, ref_c = [], []
+    for d in descs:
+        v = torch.empty(n, dtype=torch.uint8, device=cuda)
+        c = torch.zeros(8, dtype=torch.int64, device=cuda)
+        o = _lib.BatchOut()
+        o.verdict, o.counters = v.data_ptr(), c.data_ptr()
+        prog.launch(d, o, torch.cuda.current_stream(cuda))
+        torch.cuda.synchronize()
+        ref_v.append(v.cpu())
+        ref_c.append(c.cpu().numpy().view(np.uint64))
+    streams = [torch.cuda.current_stream(cuda), torch.cuda.Stream(cuda)]
+    sdescs = []
+    for si in range(2):
+        row = []
+        for d in descs:
+            d2 = type(d).from_buffer_copy(d)
+            if own_ws:
+                wb = prog.workspace_bytes(d, 0)
+                ws = torch.zeros(max(wb, 1), dtype=torch.uint8, device=cuda)
+                keep.append(ws)
+                d2.workspace, d2.workspace_bytes = ws.data_ptr(), wb
+            row.append(d2)
+        sdescs.append(row)
+    cnt = torch.zeros(8, dtype=torch.int64, device=cuda)
+    steps = 12
+    verd = [torch.empty(n, dtype=torch.uint8, device=cuda) for _ in range(steps)]
+    ev0 = torch.cuda.Event()
+    ev0.record(streams[0])
+    streams[1].wait_event(ev0)
+    for i in range(steps):
+        si = i % 2
+        o = _lib.BatchOut()
+        o.verdict, o.counters = verd[i].data_ptr(), cnt.data_ptr()
+        prog.launch(sdescs[si][i % 3], o, streams[si])
+    torch.cuda.synchronize()
+    want = np.zeros(8, dtype=np.uint64)
+    for i in range(steps):
+        assert torch.equal(verd[i].cpu(), ref_v[i % 3]), (config, own_ws, i)
+        want += ref_c[i % 3]
+    assert list(cnt.cpu().numpy().view(np.uint64)) == list(want), (config, own_ws)
+    prog.close()
+
+
+def test_bench_line(cuda):
+    """bench.py's contract line (two streams, the default) on a small run: one JSON line with the
+    driver's keys, the roofline and its stream fields, and counters that add up to the packets."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--steps", "6", "--warmup",
+                        "2", "--cpu-seconds", "0", "--packets", str(1 << 16), "--pool-mib", "8"],
+                       capture_output=True, text=True, timeout=170, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config", "roofline"):
+        assert k in d, k
+    assert d["steps"] == 6 and d["n_gpus"] == 1 and d["config"]["streams"] == 2
+    ro = d["roofline"]
+    assert ro["streams"] == 2 and ro["kernel_avg_us"] > 0 and ro["kernel_single_us"] > 0
+    c = d["counters"]
+    assert c["drop"] + c["pass"] + c["other"] + c["faults"] <= 6 * (1 << 16)
