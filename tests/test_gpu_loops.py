@@ -766,3 +766,93 @@ def test_coop_budget_edges(cuda, oracle_mod, name):
                          offsets_layout=True, align=16)
         _check_prod_against_oracle(oracle_mod, img, pkts, prod, mem_size=2048, r10=2048,
                                    max_steps=budget, tag=f"{name} budget {budget}")
+
+
+def gen_bytesum_program(rng):
+    """A random counted byte-sum loop around the shape coop_sum takes (and near misses): random
+    accumulator / byte / index / bound registers, start (constant or a packet byte), bound (len,
+    len - c), load offset d (at most c: in bounds, or more: some lanes fault), base direct or an
+    address copy, accumulator and byte register preloaded with random 64-bit values, a 32-bit add
+    or an add before the load now and then (not the idiom), and an epilogue that mixes every
+    register the loop leaves into r0."""
+    S = rng.choice(["r0", "r6", "r7"])
+    D = rng.choice(["r5", "r8"])
+    I = rng.choice(["r3", "r4"])
+    A = "r4" if I == "r3" else "r3"
+    # bound: len (unsigned), len >> 1 (unsigned), or len - c (signed compares; not a counted loop)
+    bk = rng.choices(["len", "half", "sub"], weights=[5, 2, 2])[0]
+    N = "r2" if bk == "len" else "r9"
+    c = rng.choice([0, 1, 2, 3, 7])
+    d = {"len": 0, "half": rng.choice([0, 0, 3]), "sub": rng.choice([0, 0, 1, 2, c, c + 1])}[bk]
+    lines = [f"lddw {S}, {rng.getrandbits(64):#x}" if rng.random() < 0.5 else f"mov {S}, {rng.randrange(100)}",
+             f"lddw {D}, {rng.getrandbits(64):#x}"]
+    if rng.random() < 0.7:
+        lines.append(f"mov {I}, {rng.choice([0, 0, 1, 5, 16, 33])}")
+    else:
+        lines += [f"ldxb {I}, [r1+{rng.randrange(8)}]", f"and {I}, {rng.choice([15, 31, 63])}"]
+    if bk == "sub":
+        lines += ["mov r9, r2", f"sub r9, {c}"]
+    elif bk == "half":
+        lines += ["mov r9, r2", "rsh r9, 1"]
+    signed = bk == "sub"
+    lines.append(f"{'jsge' if signed else 'jge'} {I}, {N}, done")
+    lines.append("loop:")
+    body = []
+    if rng.random() < 0.5:
+        body += [f"mov {A}, r1", f"add {A}, {I}", f"ldxb {D}, [{A}+{d}]"]
+    else:
+        body.append(f"ldxb {D}, [{I}+{d}]")
+    r = rng.random()
+    if r < 0.1:
+        body.append(f"add32 {S}, {D}")          # not the 64-bit idiom
+    elif r < 0.15:
+        body.insert(0, f"add {S}, {D}")         # the add before the load: the previous byte
+    else:
+        body.append(f"add {S}, {D}")
+    body.append(f"add {I}, 1")
+    lines += body
+    lines.append(f"{'jslt' if signed else 'jlt'} {I}, {N}, loop")
+    lines.append("done:")
+    if S != "r0":
+        lines.append(f"mov r0, {S}")
+    k = rng.randrange(1, 40)
+    lines += [f"xor r0, {D}", f"lsh {D}, {k}", f"xor r0, {D}", f"xor r0, {I}", f"mov r9, {I}",
+              f"rsh r9, 3", "add r0, r9"]
+    if rng.random() < 0.5:
+        lines += ["mov r6, r0", "rsh r6, 8", "xor r0, r6", "and r0, 7"]
+    lines.append("exit")
+    return "\n".join("    " + ln if not ln.endswith(":") else ln for ln in lines) + "\n"
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_fuzz_bytesum_loops(cuda, oracle_mod, seed):
+    """Random counted byte-sum loops (gen_bytesum_program) over packets of 0-1500 bytes, in batch
+    order (the deep kernel's compacted cooperative sums) and aligned / misaligned bases: production
+    outputs against the oracle, full outputs against the general interpreter for some; at least a
+    quarter of the programs take coop_sum."""
+    from ebpf_emu import Program
+    from ebpf_emu.asm import assemble
+
+    rng = random.Random(1000 + seed)
+    n_coop = 0
+    n_prog = 30
+    for it in range(n_prog):
+        src = gen_bytesum_program(rng)
+        img = assemble(src)
+        p = Program(img)
+        assert p.compile(), src
+        n_coop += "coop_sum" in p.jit_asm(2)
+        p.close()
+        lens = [rng.choice([0, 1, 5, 64, 127, 128, 129, 200, 700, 1500, rng.randrange(1501)])
+                for _ in range(rng.choice([300, 700]))]
+        pkts = [bytes(rng.getrandbits(8) for _ in range(ln)) for ln in lens]
+        layout = rng.choice([dict(offsets_layout=True, align=16), dict(offsets_layout=True, align=64),
+                             dict(offsets_layout=True, misalign=3)])
+        prod = _run_prod(img, pkts, cuda, mem_size=2048, r10=2048, **layout)
+        _check_prod_against_oracle(oracle_mod, img, pkts, prod, mem_size=2048, r10=2048,
+                                   tag=f"seed {seed} it {it}\n{src}")
+        if it % 4 == 0:
+            full = _run_full(img, pkts, cuda, mem_size=2048, r10=2048, **layout)
+            gen = _run_full(img, pkts, cuda, mem_size=2048, r10=2048, generic=True, **layout)
+            _same_outputs(full, gen, f"seed {seed} it {it}\n{src}")
+    assert n_coop * 4 >= n_prog, n_coop
