@@ -85,6 +85,9 @@ def parse():
                     help="HIP streams the steps alternate over (each with its own workspace and "
                          "verdict buffer): consecutive batches overlap, one's ramp under the "
                          "other's tail; 1 = one launch after another")
+    ap.add_argument("--settle-ms", type=float, default=0.0,
+                    help="untimed clock-settling run of the workload before the W warmup steps "
+                         "(host milliseconds; reported as settle_ms)")
     ap.add_argument("--no-counters", action="store_true", help="A/B: verdicts only")
     ap.add_argument("--generic", action="store_true",
                     help="run on the general interpreter (EBPF_BATCH_GENERIC), for comparison")
@@ -221,6 +224,14 @@ def main():
         si = i % S
         prog.launch(sdescs[si][i % len(descs)], outs[si], streams[si])
 
+    if args.settle_ms > 0:  # untimed: the GPU's clocks up to their steady state
+        ts, i = time.perf_counter(), 0
+        while (time.perf_counter() - ts) * 1e3 < args.settle_ms:
+            step(i)
+            i += 1
+            if i % 64 == 0:  # keep the queue short (enqueue is faster than a batch)
+                torch.cuda.synchronize(dev)
+        torch.cuda.synchronize(dev)
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize(dev)
@@ -352,6 +363,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "settle_ms": args.settle_ms,
             "ms_per_step": round(elapsed * 1e3 / args.steps, 5),
             "higher_is_better": True,
             "scaling": "strong" if args.total_packets else "weak",

@@ -1385,6 +1385,9 @@ hipError_t launch_xdp_stage(const uint8_t* frames, const uint32_t* offsets, cons
 // final-image output (a NIC ring of fixed slots): no packet metadata at all.
 // ============================================================================================
 constexpr uint32_t kTileWaveLds = kWinBytes + kDagMetaBytes;  // window + metadata, 4.5 KiB
+constexpr uint32_t kTileWaveLdsPipe = kWinBytes + 2 * kDagMetaBytes;  // two metadata buffers, 5 KiB
+// the var kernels' metadata pipeline: on unless the launch asks otherwise (A/B, LaunchArgs.var_pipe)
+__device__ __forceinline__ bool g_var_pipe(const LaunchArgs& a) { return a.var_nopipe == 0; }
 
 
 #define TILE_ASM_OUT [bkt] "=&v"(bkt), [nst] "=&v"(nst)
@@ -1440,12 +1443,21 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
     a.bin_counts[threadIdx.x] = 0;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t wv = rfl(threadIdx.x / kWave);  // wave-uniform: keeps LDS addresses scalar
+  // PIPE (the compiled kernels on offsets / lens batches): two metadata buffers per wave, the
+  // next tile's offsets and lengths DMA'd while this tile runs, so a tile waits for one HBM round
+  // trip (its windows) instead of two (metadata, then windows). Loop kernels: only in batch order
+  // (no perm) and with a persistent grid (EBPFEMU_LOOP_GRID=persist; one tile per wave has no
+  // next tile). The statement reads the metadata in its prologue only, and a DMA older than its
+  // own loads only makes its vmcnt waits stricter.
+  constexpr bool PIPE = JIT && !FIXED;
   WaveLds L;
-  L.win = smem + wv * kTileWaveLds;
+  L.win = smem + wv * (PIPE ? kTileWaveLdsPipe : kTileWaveLds);
   L.meta_off = (uint32_t*)(L.win + kWinBytes);
   L.meta_len = L.meta_off + kWave;
   const uint32_t winb = lds_addr(L.win);
-  const uint32_t metab = lds_addr(L.meta_off);
+  const uint32_t metab0 = lds_addr(L.meta_off);
+  const bool pipe = PIPE && g_var_pipe(a) && !(LOOPS && a.perm);
+  uint32_t mb = 0;  // PIPE: the metadata buffer of the current tile
   const uint64_t wave_slot = (uint64_t)blockIdx.x * WPB + wv;
   const uint64_t total_waves = (uint64_t)gridDim.x * WPB;
   const auto ka = __builtin_amdgcn_kernarg_segment_ptr();
@@ -1464,17 +1476,30 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
   };
   if (trace) stamp(0);
 
+  if (pipe && wave_slot < a.n_tiles) {  // the first tile's metadata
+    uint32_t lane;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+    dma_meta(a, L, 0, wave_slot, lane);
+  }
   for (uint64_t tile = wave_slot; tile < a.n_tiles;) {
     // the lane index is re-derived inside the loop (volatile: not hoistable), so no per-lane
     // address of the window DMA stays live across the asm statement
     uint32_t aligned = 1;  // every packet base of the tile 16-byte aligned (loop-mode refills)
+    WaveLds Lc = L;        // this tile's metadata buffer (PIPE: buffer mb, 512 bytes each)
+    if (PIPE) {
+      Lc.meta_off = L.meta_off + mb * 2 * kWave;
+      Lc.meta_len = Lc.meta_off + kWave;
+    }
+    const uint32_t metab = rfl(metab0 + (PIPE ? mb * kDagMetaBytes : 0u));
     if (!FIXED) {  // (FIXED: the asm statement DMAs the windows itself)
       uint32_t lane;
       asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
       const uint64_t pkt = tile * kWave + lane;
       const bool valid = pkt < a.n;
       const bool sw = stride_windows(a);
-      if (LOOPS && a.perm) {  // length-binned order: gather this tile's packet metadata
+      if (pipe) {
+        // (metadata already in flight: issued for this tile by the previous iteration)
+      } else if (LOOPS && a.perm) {  // length-binned order: gather this tile's packet metadata
         const uint64_t src = valid ? (uint64_t)a.perm[pkt] : 0ull;
         if (a.offsets)
           dma_x1(valid ? (uintptr_t)(a.offsets + src) : (uintptr_t)a.prog, lds_addr(L.meta_off));
@@ -1485,22 +1510,31 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
       }
       if (sw) dma_window_stride(a, L.win, tile, lane);
       dma_wait();
-      uintptr_t mb;
+      uintptr_t pb;
       uint32_t ml;
-      meta_of(a, L, 0, tile, lane, mb, ml);
-      const bool co = sw || ballot(valid && ml != 0 && (mb & 15) != 0) == 0;
+      meta_of(a, Lc, 0, tile, lane, pb, ml);
+      const bool co = sw || ballot(valid && ml != 0 && (pb & 15) != 0) == 0;
       aligned = co ? 1u : 0u;
       if (co) {
         if (!sw) {
-          dma_window(a, L, 0, 0, tile, lane);
+          dma_window(a, Lc, 0, 0, tile, lane);
           dma_wait();
         }
       } else {
-        stage_window_lane(L.win + lane * kWin, win_swz(lane), (const uint8_t*)mb,
+        stage_window_lane(L.win + lane * kWin, win_swz(lane), (const uint8_t*)pb,
                           valid ? ml : 0u, valid);
       }
       if (!LOOPS && a.xdp) xdp_window(L.win + lane * kWin, win_swz(lane), ml);
       __builtin_amdgcn_s_waitcnt(0xc07f);  // the window's LDS writes / metadata reads: done
+      // PIPE: the next tile's metadata into the other buffer (last read by the previous tile's
+      // statement, which has finished), landing while this tile runs
+      const uint64_t ntl = rfl64(tile) + total_waves;
+      if (pipe && ntl < a.n_tiles) {
+        WaveLds Ln = L;
+        Ln.meta_off = L.meta_off + (mb ^ 1u) * 2 * kWave;
+        Ln.meta_len = Ln.meta_off + kWave;
+        dma_meta(a, Ln, 0, ntl, lane);
+      }
     }
     const uint64_t t = rfl64(tile);
     const uint64_t nt = t + total_waves;
@@ -1510,7 +1544,7 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
       if (!FIXED && threadIdx.x % kWave == 0) {
         uintptr_t mb;
         uint32_t ml;
-        meta_of(a, L, 0, tile, 0, mb, ml);
+        meta_of(a, Lc, 0, tile, 0, mb, ml);
         trace[4] = ml;
       }
     }
@@ -1549,7 +1583,7 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
       if (slot < a.n) {
         uintptr_t mb;
         uint32_t ml;
-        meta_of(a, L, 0, tile, ln, mb, ml);
+        meta_of(a, Lc, 0, tile, ln, mb, ml);
         // (xdp_md in place: the image is the packet 8 bytes further on, behind its ctx)
         const uint32_t len = a.xdp ? min(ml, 0xffffu) + 8u : ml;
         const uint8_t* base = (const uint8_t*)mb - (a.xdp ? 8 : 0);
@@ -1571,6 +1605,7 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
     retired += nst;
     if (trace && t == wave_slot) stamp(2);
     tile = nt;
+    if (pipe) mb ^= 1u;  // (without the prefetch every tile's metadata is in buffer 0)
   }
   uint64_t cnt64[7];
 #pragma unroll
@@ -1788,8 +1823,9 @@ static uint32_t g_lds_pad = [] {
   return e ? (uint32_t)atoi(e) : 0u;
 }();
 
-static uint32_t lds_bytes_for(int kind, uint32_t n_uops) {
-  if (kind == kKindLoop) return g_lds_pad + kWavesPerBlock * kTileWaveLds;
+static uint32_t lds_bytes_for(int kind, uint32_t n_uops, bool jit_loop = false) {
+  if (kind == kKindLoop)  // (the compiled loop kernels: + the second metadata buffer)
+    return g_lds_pad + kWavesPerBlock * (jit_loop ? kTileWaveLdsPipe : kTileWaveLds);
   if (kind == kKindDag)  // the program is fetched by SMEM
     return g_lds_pad +
            kWavesPerBlock * (n_uops <= kTileMaxUops && !g_no_tile ? kTileWaveLds : kDagWaveLds);
@@ -1953,6 +1989,18 @@ int launch_kernel_id(int kind, const LaunchArgs& a, const JitFns* jit, bool stac
 // The compiled loop kernel's grid (A/B): EBPFEMU_LOOP_GRID=persist -- balanced persistent waves
 // at the kernel's own occupancy (each wave a run of tiles, one counter flush per wave) instead of
 // one tile per wave.
+static bool g_var_grid = [] {
+  const char* e = getenv("EBPFEMU_VAR_GRID");
+  return !(e && e[0] == 't');
+}();
+static bool g_var_pipe_host = [] {
+  const char* e = getenv("EBPFEMU_VAR_PIPE");
+  return !(e && e[0] == '0');
+}();
+static bool g_loop_pipe = [] {  // A/B: EBPFEMU_LOOP_PIPE=0
+  const char* e = getenv("EBPFEMU_LOOP_PIPE");
+  return !(e && e[0] == '0');
+}();
 static int g_loop_grid = [] {
   const char* e = getenv("EBPFEMU_LOOP_GRID");
   return e ? (e[0] == 'p' ? 1 : 0) : -1;
@@ -1960,10 +2008,18 @@ static int g_loop_grid = [] {
 
 hipError_t launch_interp(int kind, const LaunchArgs& a, int grid, hipStream_t stream,
                          const JitFns* jit, bool stack) {
-  const uint32_t lds = lds_bytes_for(kind, a.n_uops);
+  const uint32_t lds = lds_bytes_for(kind, a.n_uops, jit && jit->loop);
   if (jit && jit->loop && kind == kKindLoop && g_loop_grid == 1)
     grid = jit_grid(stack ? jit->loop_stack : jit->loop, lds, a.n_tiles);
+  // the compiled var kernels: balanced persistent waves at their own occupancy (interp_grid sizes
+  // for tile_kernel's, which is higher: its extra workgroups would run in a second round);
+  // EBPFEMU_VAR_GRID=tile keeps tile_kernel's grid (A/B)
+  const bool var = jit && jit->fixed && kind != kKindLoop && jit_forward_for(kind, a.n_uops) &&
+                   !jit_fixed_layout(&a);
+  const uint32_t vlds = g_lds_pad + kWavesPerBlock * kTileWaveLdsPipe;
+  if (var && g_var_grid) grid = jit_grid(stack ? jit->var_stack : jit->var, vlds, a.n_tiles);
   LaunchArgs b = a;
+  b.var_nopipe = (kind == kKindLoop ? g_loop_pipe : g_var_pipe_host) ? 0u : 1u;
   // a shard word's sum must stay below 2^48: bound it by packets x steps per packet; and its
   // arrival count (16 bits) must reach the shard's workgroups - 1: at most 65535 members (the
   // compiled fixed-slot kernel's grid is one workgroup per CU, every other grid is `grid`)
@@ -1983,8 +2039,8 @@ hipError_t launch_interp(int kind, const LaunchArgs& a, int grid, hipStream_t st
       const uint32_t dlds = g_lds_pad + kDbWaves * kTileWaveLdsDb;
       e = hipModuleLaunchKernel(jit->fixed, jit_grid(jit->fixed, dlds, a.n_tiles, kDbBlock), 1, 1,
                                 kDbBlock, 1, 1, dlds, stream, bargs, nullptr);
-    } else {  // (the tile kernel's window LDS, also for programs past kTileMaxUops)
-      const uint32_t vlds = g_lds_pad + kWavesPerBlock * kTileWaveLds;
+    } else {  // (the tile kernel's window LDS + a second metadata buffer, also for programs
+              // past kTileMaxUops)
       e = hipModuleLaunchKernel(stack ? jit->var_stack : jit->var, grid, 1, 1, kBlock, 1, 1, vlds,
                                 stream, bargs, nullptr);
     }

@@ -76,6 +76,8 @@ struct LaunchArgs {
                               //   [u32 data = 8][u32 data_end = 8 + len][packet]; the window is
                               //   shifted by 8 bytes in LDS and the ctx synthesised per lane, BASE
                               //   = packet - 8 and LEN = 8 + len (no staging copy)
+  uint32_t var_nopipe;        // A/B (EBPFEMU_VAR_PIPE=0): the compiled var kernels fetch each tile's
+                              //   metadata and then its windows, no metadata prefetch
 };
 
 constexpr int kTraceSlots = 16;

@@ -754,3 +754,50 @@ def test_bench_line(cuda):
     assert ro["streams"] == 2 and ro["kernel_avg_us"] > 0 and ro["kernel_single_us"] > 0
     c = d["counters"]
     assert c["drop"] + c["pass"] + c["other"] + c["faults"] <= 6 * (1 << 16)
+
+
+@pytest.mark.parametrize("slot,shift", [(64, 0), (80, 3)])
+def test_var_kernel_full_size_shuffled(cuda, slot, shift):
+    """The compiled var kernel at full size (1 Mi packets: several tiles per persistent wave, so
+    each tile's offsets and lengths arrive by the previous tile's metadata prefetch). The fixed
+    5-tuple fixture's frames, stored `slot` bytes apart at `shift` (3: misaligned, the per-lane
+    staging path) and listed in a shuffled order through offsets + lens: verdict i equals the
+    fixed-slot kernel's verdict of frame perm[i], whose CRC and counters are the fixture's; r0 and
+    status as well."""
+    import torch
+
+    from ebpf_emu import Program, _lib
+    from ebpf_emu import workloads as W
+
+    with open(os.path.join(GOLDEN, "workloads.json")) as f:
+        g = json.load(f)["5tuple"]
+    n = g["n"]
+    buf = W.frames_fixed(n, 64, g["config_id"])
+    prog = Program(W.program("5tuple"))
+    cnt = torch.zeros(8, dtype=torch.int64, device=cuda)
+    ref = prog.run(torch.from_numpy(buf).to(cuda), n=n, stride=64, counters=cnt, r0=True,
+                   status=True)
+    torch.cuda.synchronize()
+    vref = ref.verdict.cpu().numpy()
+    assert zlib.crc32(vref.tobytes()) == g["verdict_crc32"]
+    assert [int(x) for x in cnt.cpu().numpy().view(np.uint64)] == g["counters"]
+
+    big = np.zeros((n, slot), dtype=np.uint8)
+    big[:, shift:shift + 64] = buf.reshape(n, 64)
+    perm = np.random.default_rng(slot).permutation(n)
+    offs = (perm.astype(np.int64) * slot + shift).astype(np.uint32)
+    frames = torch.from_numpy(big.reshape(-1)).to(cuda)
+    kw = dict(n=n, offsets=torch.from_numpy(offs.view(np.int32)).to(cuda),
+              lens=torch.from_numpy(np.full(n, 64, dtype=np.int16)).to(cuda))
+    assert prog.batch_kernel(prog.make_batch(frames, **kw)) == _lib.EBPF_KERNEL_JIT_VAR
+    cnt2 = torch.zeros(8, dtype=torch.int64, device=cuda)
+    res = prog.run(frames, counters=cnt2, r0=True, status=True, **kw)
+    torch.cuda.synchronize()
+    assert np.array_equal(res.verdict.cpu().numpy(), vref[perm])
+    assert np.array_equal(res.r0.cpu().numpy(), ref.r0.cpu().numpy()[perm])
+    assert np.array_equal(res.status.cpu().numpy(), ref.status.cpu().numpy()[perm])
+    assert [int(x) for x in cnt2.cpu().numpy().view(np.uint64)] == g["counters"]
+    # the production outputs alone (verdicts + counters, liveness-pruned init)
+    res = prog.run(frames, **kw)
+    torch.cuda.synchronize()
+    assert np.array_equal(res.verdict.cpu().numpy(), vref[perm])
