@@ -1386,6 +1386,7 @@ hipError_t launch_xdp_stage(const uint8_t* frames, const uint32_t* offsets, cons
 // ============================================================================================
 constexpr uint32_t kTileWaveLds = kWinBytes + kDagMetaBytes;  // window + metadata, 4.5 KiB
 constexpr uint32_t kTileWaveLdsPipe = kWinBytes + 2 * kDagMetaBytes;  // two metadata buffers, 5 KiB
+constexpr uint32_t kTileWaveLdsDb3 = 2 * kWinBytes + 3 * kDagMetaBytes;  // DB: 9.5 KiB
 // the var kernels' metadata pipeline: on unless the launch asks otherwise (A/B, LaunchArgs.var_pipe)
 __device__ __forceinline__ bool g_var_pipe(const LaunchArgs& a) { return a.var_nopipe == 0; }
 
@@ -1449,15 +1450,45 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
   // (no perm) and with a persistent grid (EBPFEMU_LOOP_GRID=persist; one tile per wave has no
   // next tile). The statement reads the metadata in its prologue only, and a DMA older than its
   // own loads only makes its vmcnt waits stricter.
+  // DB (the forward var kernels, LaunchArgs.var_db, opt-in A/B): also two window buffers and
+  // three metadata buffers per wave -- tile i runs on window i % 2 while tile i+1's windows and
+  // tile i+2's metadata are in flight, so a tile waits for no HBM round trip of its own (the
+  // fixed-slot kernel's scheme, with the metadata one tile further ahead). Measured slower than
+  // the metadata prefetch alone: 9.5 KiB of LDS per wave leaves 4 waves per SIMD instead of 7.
   constexpr bool PIPE = JIT && !FIXED;
-  WaveLds L;
-  L.win = smem + wv * (PIPE ? kTileWaveLdsPipe : kTileWaveLds);
-  L.meta_off = (uint32_t*)(L.win + kWinBytes);
-  L.meta_len = L.meta_off + kWave;
-  const uint32_t winb = lds_addr(L.win);
-  const uint32_t metab0 = lds_addr(L.meta_off);
   const bool pipe = PIPE && g_var_pipe(a) && !(LOOPS && a.perm);
-  uint32_t mb = 0;  // PIPE: the metadata buffer of the current tile
+  const bool db = PIPE && !LOOPS && pipe && a.var_db != 0;
+  const uint32_t nmeta = db ? 3u : 2u;
+  WaveLds L;
+  L.win = smem + wv * (db ? kTileWaveLdsDb3 : PIPE ? kTileWaveLdsPipe : kTileWaveLds);
+  L.meta_off = (uint32_t*)(L.win + (db ? 2 : 1) * kWinBytes);
+  L.meta_len = L.meta_off + kWave;
+  // window buffer w and metadata buffer m of this wave (512 bytes each: offsets, then lengths)
+  auto bufs = [&](uint32_t w, uint32_t m) {
+    WaveLds x;
+    x.win = L.win + w * kWinBytes;
+    x.meta_off = L.meta_off + m * 2 * kWave;
+    x.meta_len = x.meta_off + kWave;
+    return x;
+  };
+  const bool sw0 = stride_windows(a);
+  // DB: DMA tile t's windows into X.win (its metadata landed in X's buffer); false when some
+  // packet base is not 16-byte aligned (its lanes stage the window themselves, at its turn)
+  auto issue_window = [&](uint64_t t, const WaveLds& X, uint32_t lane) {
+    if (sw0) {
+      dma_window_stride(a, X.win, t, lane);
+      return true;
+    }
+    uintptr_t pb;
+    uint32_t ml;
+    meta_of(a, X, 0, t, lane, pb, ml);
+    const bool ok = ballot(t * kWave + lane < a.n && ml != 0 && (pb & 15) != 0) == 0;
+    if (ok) dma_window(a, X, 0, 0, t, lane);
+    return ok;
+  };
+  uint32_t mb = 0;      // PIPE: the metadata buffer of the current tile (0 .. nmeta - 1)
+  uint32_t wi = 0;      // DB: its window buffer
+  bool cur_dma = true;  // DB: its windows were DMA'd (else staged per lane at its turn)
   const uint64_t wave_slot = (uint64_t)blockIdx.x * WPB + wv;
   const uint64_t total_waves = (uint64_t)gridDim.x * WPB;
   const auto ka = __builtin_amdgcn_kernarg_segment_ptr();
@@ -1476,22 +1507,46 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
   };
   if (trace) stamp(0);
 
-  if (pipe && wave_slot < a.n_tiles) {  // the first tile's metadata
+  if (pipe && wave_slot < a.n_tiles) {  // the first tile's metadata (DB: and its windows)
     uint32_t lane;
     asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
     dma_meta(a, L, 0, wave_slot, lane);
+    if (db) {
+      dma_wait();
+      cur_dma = issue_window(wave_slot, bufs(0, 0), lane);
+      if (wave_slot + total_waves < a.n_tiles) dma_meta(a, bufs(0, 1), 0, wave_slot + total_waves, lane);
+    }
   }
   for (uint64_t tile = wave_slot; tile < a.n_tiles;) {
     // the lane index is re-derived inside the loop (volatile: not hoistable), so no per-lane
     // address of the window DMA stays live across the asm statement
     uint32_t aligned = 1;  // every packet base of the tile 16-byte aligned (loop-mode refills)
-    WaveLds Lc = L;        // this tile's metadata buffer (PIPE: buffer mb, 512 bytes each)
-    if (PIPE) {
-      Lc.meta_off = L.meta_off + mb * 2 * kWave;
-      Lc.meta_len = Lc.meta_off + kWave;
-    }
-    const uint32_t metab = rfl(metab0 + (PIPE ? mb * kDagMetaBytes : 0u));
-    if (!FIXED) {  // (FIXED: the asm statement DMAs the windows itself)
+    // this tile's window and metadata buffers (without PIPE / DB: buffer 0)
+    const WaveLds Lc = bufs(db ? wi : 0u, PIPE ? mb : 0u);
+    const uint32_t winb = lds_addr(Lc.win);
+    const uint32_t metab = lds_addr(Lc.meta_off);
+    if (!FIXED && db) {
+      uint32_t lane;
+      asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+      dma_wait();  // this tile's windows, the next tile's metadata
+      const uint64_t t0 = rfl64(tile);
+      const bool valid = t0 * kWave + lane < a.n;
+      uintptr_t pb;
+      uint32_t ml;
+      meta_of(a, Lc, 0, t0, lane, pb, ml);
+      if (!cur_dma)
+        stage_window_lane(Lc.win + lane * kWin, win_swz(lane), (const uint8_t*)pb,
+                          valid ? ml : 0u, valid);
+      const uint64_t t1 = t0 + total_waves;
+      if (t1 < a.n_tiles) {  // tile t1's windows, tile t2's metadata: in flight while t0 runs
+        const uint32_t m1 = mb + 1 == nmeta ? 0u : mb + 1, m2 = m1 + 1 == nmeta ? 0u : m1 + 1;
+        const bool nxt = issue_window(t1, bufs(wi ^ 1u, m1), lane);
+        if (t1 + total_waves < a.n_tiles) dma_meta(a, bufs(0, m2), 0, t1 + total_waves, lane);
+        cur_dma = nxt;
+      }
+      if (a.xdp) xdp_window(Lc.win + lane * kWin, win_swz(lane), ml);
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // the window's LDS writes / metadata reads: done
+    } else if (!FIXED) {  // (FIXED: the asm statement DMAs the windows itself)
       uint32_t lane;
       asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
       const uint64_t pkt = tile * kWave + lane;
@@ -1529,12 +1584,7 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
       // PIPE: the next tile's metadata into the other buffer (last read by the previous tile's
       // statement, which has finished), landing while this tile runs
       const uint64_t ntl = rfl64(tile) + total_waves;
-      if (pipe && ntl < a.n_tiles) {
-        WaveLds Ln = L;
-        Ln.meta_off = L.meta_off + (mb ^ 1u) * 2 * kWave;
-        Ln.meta_len = Ln.meta_off + kWave;
-        dma_meta(a, Ln, 0, ntl, lane);
-      }
+      if (pipe && ntl < a.n_tiles) dma_meta(a, bufs(0, mb ^ 1u), 0, ntl, lane);
     }
     const uint64_t t = rfl64(tile);
     const uint64_t nt = t + total_waves;
@@ -1594,7 +1644,7 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
           uint32_t v;
           if (d * 4 >= m) v = 0u;
           else if (!LOOPS && d * 4 < (uint32_t)kWin)  // (loop mode may have moved the window)
-            v = (uint32_t)win_read(L.win + ln * kWin, win_swz(ln), d * 4, 4, len);
+            v = (uint32_t)win_read(Lc.win + ln * kWin, win_swz(ln), d * 4, 4, len);
           else v = (uint32_t)pkt_read(base, d * 4, 4, len);
           put_image(mo, d, v, mem_size);
         }
@@ -1605,7 +1655,8 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
     retired += nst;
     if (trace && t == wave_slot) stamp(2);
     tile = nt;
-    if (pipe) mb ^= 1u;  // (without the prefetch every tile's metadata is in buffer 0)
+    if (pipe) mb = mb + 1 == nmeta ? 0u : mb + 1;  // (without the prefetch: buffer 0 always)
+    wi ^= 1u;
   }
   uint64_t cnt64[7];
 #pragma unroll
@@ -1993,6 +2044,12 @@ static bool g_var_grid = [] {
   const char* e = getenv("EBPFEMU_VAR_GRID");
   return !(e && e[0] == 't');
 }();
+// A/B, opt-in: EBPFEMU_VAR_DB=1 (measured slower: the windows' second buffer halves the waves
+// per CU; profiles/r03_ab_var_db.json)
+static bool g_var_db = [] {
+  const char* e = getenv("EBPFEMU_VAR_DB");
+  return e && e[0] == '1';
+}();
 static bool g_var_pipe_host = [] {
   const char* e = getenv("EBPFEMU_VAR_PIPE");
   return !(e && e[0] == '0');
@@ -2016,10 +2073,12 @@ hipError_t launch_interp(int kind, const LaunchArgs& a, int grid, hipStream_t st
   // EBPFEMU_VAR_GRID=tile keeps tile_kernel's grid (A/B)
   const bool var = jit && jit->fixed && kind != kKindLoop && jit_forward_for(kind, a.n_uops) &&
                    !jit_fixed_layout(&a);
-  const uint32_t vlds = g_lds_pad + kWavesPerBlock * kTileWaveLdsPipe;
-  if (var && g_var_grid) grid = jit_grid(stack ? jit->var_stack : jit->var, vlds, a.n_tiles);
+  const bool vdb = g_var_db && g_var_pipe_host;
+  const uint32_t vlds = g_lds_pad + kWavesPerBlock * (vdb ? kTileWaveLdsDb3 : kTileWaveLdsPipe);
+  if (var && (g_var_grid || vdb)) grid = jit_grid(stack ? jit->var_stack : jit->var, vlds, a.n_tiles);
   LaunchArgs b = a;
   b.var_nopipe = (kind == kKindLoop ? g_loop_pipe : g_var_pipe_host) ? 0u : 1u;
+  b.var_db = var && vdb ? 1u : 0u;
   // a shard word's sum must stay below 2^48: bound it by packets x steps per packet; and its
   // arrival count (16 bits) must reach the shard's workgroups - 1: at most 65535 members (the
   // compiled fixed-slot kernel's grid is one workgroup per CU, every other grid is `grid`)

@@ -78,6 +78,8 @@ struct LaunchArgs {
                               //   = packet - 8 and LEN = 8 + len (no staging copy)
   uint32_t var_nopipe;        // A/B (EBPFEMU_VAR_PIPE=0): the compiled var kernels fetch each tile's
                               //   metadata and then its windows, no metadata prefetch
+  uint32_t var_db;            // the compiled var kernels: double-buffered windows, the next tile's
+                              //   windows in flight while a tile runs (A/B, EBPFEMU_VAR_DB=1)
 };
 
 constexpr int kTraceSlots = 16;
