@@ -757,13 +757,16 @@ def test_bench_line(cuda):
 
 
 @pytest.mark.parametrize("slot,shift", [(64, 0), (80, 3)])
-def test_var_kernel_full_size_shuffled(cuda, slot, shift):
-    """The compiled var kernel at full size (1 Mi packets: several tiles per persistent wave, so
+@pytest.mark.parametrize("name", ["5tuple", "5tuple_stack", "5tuple_xdp", "acl"])
+def test_var_kernel_full_size_shuffled(cuda, name, slot, shift):
+    """The compiled var kernels at full size (1 Mi packets: several tiles per persistent wave, so
     each tile's offsets and lengths arrive by the previous tile's metadata prefetch). The fixed
     5-tuple fixture's frames, stored `slot` bytes apart at `shift` (3: misaligned, the per-lane
-    staging path) and listed in a shuffled order through offsets + lens: verdict i equals the
-    fixed-slot kernel's verdict of frame perm[i], whose CRC and counters are the fixture's; r0 and
-    status as well."""
+    staging path) and listed in a shuffled order through offsets + lens: verdict, r0 and status i
+    equal the fixed-slot kernel's for frame perm[i] (for the 5-tuple: the fixture's CRC and
+    counters; the others run on fixed slots against the oracle in their own tests). Programs: the
+    5-tuple, its stack-window form (ebpf_tile_jit_var_stack), the standard-XDP form over xdp_md
+    contexts (the ctx synthesised in the window), the 97-instruction ACL."""
     import torch
 
     from ebpf_emu import Program, _lib
@@ -773,14 +776,16 @@ def test_var_kernel_full_size_shuffled(cuda, slot, shift):
         g = json.load(f)["5tuple"]
     n = g["n"]
     buf = W.frames_fixed(n, 64, g["config_id"])
-    prog = Program(W.program("5tuple"))
+    prog = Program(W.program(name))
+    xdp = name == "5tuple_xdp"
     cnt = torch.zeros(8, dtype=torch.int64, device=cuda)
     ref = prog.run(torch.from_numpy(buf).to(cuda), n=n, stride=64, counters=cnt, r0=True,
-                   status=True)
+                   status=True, xdp_md=xdp)
     torch.cuda.synchronize()
     vref = ref.verdict.cpu().numpy()
-    assert zlib.crc32(vref.tobytes()) == g["verdict_crc32"]
-    assert [int(x) for x in cnt.cpu().numpy().view(np.uint64)] == g["counters"]
+    if name != "acl":  # the same verdicts as the 5-tuple's fixture
+        assert zlib.crc32(vref.tobytes()) == g["verdict_crc32"]
+        assert [int(x) for x in cnt.cpu().numpy().view(np.uint64)] == g["counters"]
 
     big = np.zeros((n, slot), dtype=np.uint8)
     big[:, shift:shift + 64] = buf.reshape(n, 64)
@@ -788,15 +793,16 @@ def test_var_kernel_full_size_shuffled(cuda, slot, shift):
     offs = (perm.astype(np.int64) * slot + shift).astype(np.uint32)
     frames = torch.from_numpy(big.reshape(-1)).to(cuda)
     kw = dict(n=n, offsets=torch.from_numpy(offs.view(np.int32)).to(cuda),
-              lens=torch.from_numpy(np.full(n, 64, dtype=np.int16)).to(cuda))
-    assert prog.batch_kernel(prog.make_batch(frames, **kw)) == _lib.EBPF_KERNEL_JIT_VAR
+              lens=torch.from_numpy(np.full(n, 64, dtype=np.int16)).to(cuda), xdp_md=xdp)
+    want = _lib.EBPF_KERNEL_JIT_VAR_STACK if name == "5tuple_stack" else _lib.EBPF_KERNEL_JIT_VAR
+    assert prog.batch_kernel(prog.make_batch(frames, **kw)) == want
     cnt2 = torch.zeros(8, dtype=torch.int64, device=cuda)
     res = prog.run(frames, counters=cnt2, r0=True, status=True, **kw)
     torch.cuda.synchronize()
     assert np.array_equal(res.verdict.cpu().numpy(), vref[perm])
     assert np.array_equal(res.r0.cpu().numpy(), ref.r0.cpu().numpy()[perm])
     assert np.array_equal(res.status.cpu().numpy(), ref.status.cpu().numpy()[perm])
-    assert [int(x) for x in cnt2.cpu().numpy().view(np.uint64)] == g["counters"]
+    assert torch.equal(cnt2, cnt)
     # the production outputs alone (verdicts + counters, liveness-pruned init)
     res = prog.run(frames, **kw)
     torch.cuda.synchronize()
