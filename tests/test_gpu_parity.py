@@ -783,9 +783,11 @@ def test_var_kernel_full_size_shuffled(cuda, name, slot, shift):
                    status=True, xdp_md=xdp)
     torch.cuda.synchronize()
     vref = ref.verdict.cpu().numpy()
-    if name != "acl":  # the same verdicts as the 5-tuple's fixture
+    if name != "acl":  # the same verdicts as the 5-tuple's fixture (other instruction counts)
         assert zlib.crc32(vref.tobytes()) == g["verdict_crc32"]
-        assert [int(x) for x in cnt.cpu().numpy().view(np.uint64)] == g["counters"]
+        got = [int(x) for x in cnt.cpu().numpy().view(np.uint64)]
+        assert got[:7] == g["counters"][:7]
+        assert name != "5tuple" or got == g["counters"]
 
     big = np.zeros((n, slot), dtype=np.uint8)
     big[:, shift:shift + 64] = buf.reshape(n, 64)
