@@ -13,9 +13,12 @@ batch's ramp under the previous one's tail, as a NIC's queues would feed them (D
 `roofline.kernel_avg_us` is then the device time per batch; `kernel_single_us` one launch at a
 time (measured after the timed region; `--streams 1` times that way throughout).
 
-Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): one rank per GPU, each rank
-owns its own shard of packets (weak scaling: per-GPU work fixed); the only collective is one
-RCCL all-reduce of the 8 per-verdict counters per job. value = packets of all ranks / max time.
+Multi-GPU (`bench.py --gpus N`, which starts N rank processes itself, or the same under
+python -m torch.distributed.run --nproc-per-node N): one rank per GPU, each rank owns its own
+shard of packets (weak scaling: per-GPU work fixed; pool batch k of rank r is seeded chunk
+k*N + r); the only collective is one RCCL all-reduce of the 8 per-verdict counters per job.
+value = packets of all ranks / max time. The reduced counters are checked against the oracle's
+counters of those chunks (tests/golden/bench_pins.json): `parity_pinned`.
 
 Prints ONE JSON line on rank 0.
 """
@@ -62,7 +65,10 @@ PROGRAM_OF = {"stack": "5tuple_stack", "tier1": "mac_swap_tx", "xdp": "5tuple_xd
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU). Without WORLD_SIZE in the environment, N > 1 "
+                         "starts N rank processes itself (before any GPU call); under torchrun "
+                         "it must equal WORLD_SIZE. Default: WORLD_SIZE, else 1")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", choices=sorted(CONFIGS), default="5tuple")
@@ -98,8 +104,137 @@ def parse():
     return ap.parse_args()
 
 
+def launch_ranks(n: int) -> int:
+    """`bench.py --gpus N` without a launcher: start N rank processes of this script (RANK =
+    LOCAL_RANK = r, WORLD_SIZE = N, rendezvous on 127.0.0.1), as torch.distributed.run would.
+    The parent never touches the GPU (no HIP call before or after the spawn, no exec); rank 0
+    prints the line. If a rank fails, the others are terminated (their exact PIDs). Returns the
+    first nonzero exit status, else 0."""
+    import socket
+    import subprocess
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 128 - c
+                for q in live:  # a peer blocked in a collective would wait forever
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+# ---- the weak-scaling pool: which seeded chunks each rank times, and the fixture that pins them --
+PIN_FIXTURE = os.path.join(ROOT, "tests", "golden", "bench_pins.json")
+
+
+def chunk_id(k: int, rank: int, world: int) -> int:
+    """Pool batch k of rank r of W is chunk k*W + r: the ranks' pools are disjoint, and at any W
+    the timed chunks are 0 .. B*W-1 (tests/golden/bench_pins.json holds their oracle counters)."""
+    return k * world + rank
+
+
+def chunk_seed(c: int, mixed: bool) -> int:
+    """config_id of chunk c: 64-byte frames are the config-4 chunks (dist.chunk_seed); mixed
+    64/1500-byte batches use 5 + 100c (chunk 0 = tests/golden/workloads.json's checksum batch)."""
+    return 5 + 100 * c if mixed else 3 + 100 * c
+
+
+def pin_weak(prog_name: str, mixed: bool, frame_bytes: int, n: int, world: int, pool: int,
+             steps: int, cnt):
+    """Expected global counters of a weak-scaling run (K steps; step i runs pool batch i mod B on
+    every rank), from the committed oracle fixture -> (want u64[8], source) or (None, reason)."""
+    if n != 1 << 20 or (not mixed and frame_bytes != 64):
+        return None, "no fixture for this batch shape (pinned: 1 Mi packets of 64 B or mixed)"
+    if not os.path.exists(PIN_FIXTURE):
+        return None, f"{os.path.relpath(PIN_FIXTURE, ROOT)} missing"
+    with open(PIN_FIXTURE) as f:
+        fx = json.load(f)
+    p = fx["programs"].get(prog_name)
+    if p is None or p["frames"] != ("mixed" if mixed else "fixed64"):
+        return None, f"no fixture for program {prog_name}"
+    cc = p["chunk_counters"]
+    if pool * world > len(cc):
+        return None, f"pool of {pool} x {world} ranks exceeds the fixture's {len(cc)} chunks"
+    want = [0] * 8
+    for i in range(steps):
+        for r in range(world):
+            row = cc[chunk_id(i % pool, r, world)]
+            for j in range(8):
+                want[j] += row[j]
+    want = [w & ((1 << 64) - 1) for w in want]
+    src = (f"{os.path.relpath(PIN_FIXTURE, ROOT)}: counters == the oracle's counters of chunks "
+           f"k*{world}+r over {steps} steps x {world} ranks")
+    return want, src
+
+
+def stub_rank(args, world, rank):
+    """EBPFEMU_BENCH_STUB=1 (CPU test of the launcher, no GPU): every rank takes the counters of
+    its own pool chunks from the fixture instead of running kernels, then the same gloo
+    reduction, max-over-ranks time and pin check as a real run; rank 0 prints the line."""
+    import torch
+    import torch.distributed as dist
+
+    if os.environ.get("EBPFEMU_BENCH_STUB_FAIL") == str(rank):  # (test: a rank that dies)
+        sys.exit(3)
+    dist.init_process_group("gloo")
+    prog_name = PROGRAM_OF.get(args.config, args.config)
+    mixed = args.config in ("checksum", "checksum_stack")
+    with open(PIN_FIXTURE) as f:
+        cc = json.load(f)["programs"][prog_name]["chunk_counters"]
+    # (the pool size bench's loop below reaches for 1 Mi packets per batch)
+    pool = 1 if mixed else min(16, -(-args.pool_mib // 64))
+    t0 = time.perf_counter()
+    mine = [0] * 8
+    for i in range(args.steps):
+        row = cc[chunk_id(i % pool, rank, world)]
+        mine = [a + b for a, b in zip(mine, row)]
+    counters = torch.tensor([m - (1 << 64) if m >= 1 << 63 else m for m in mine],
+                            dtype=torch.int64)
+    dist.all_reduce(counters)
+    elapsed = torch.tensor([time.perf_counter() - t0 + 1e-6], dtype=torch.float64)
+    dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    cnt = [int(c) & ((1 << 64) - 1) for c in counters.tolist()]
+    want, src = pin_weak(prog_name, mixed, 64, 1 << 20, world, pool, args.steps, cnt)
+    assert cnt == want, ("counters differ from the fixture", cnt, want)
+    if rank == 0:
+        n = 1 << 20
+        print(json.dumps({"metric": "stub", "value": n * world * args.steps / float(elapsed) / 1e6,
+                          "unit": "Mpkt/s", "n_gpus": world, "steps": args.steps,
+                          "counters": {"drop": cnt[1], "pass": cnt[2], "insns_retired": cnt[7]},
+                          "parity_pinned": src, "stub": True}), flush=True)
+    dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None:
+        if (args.gpus or 1) > 1:
+            sys.exit(launch_ranks(args.gpus))
+    elif args.gpus is not None and int(env_world) != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world}")
+    world = int(env_world or "1")
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("EBPFEMU_BENCH_STUB") == "1":
+        return stub_rank(args, world, rank)
+
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -107,17 +242,31 @@ def main():
     from ebpf_emu import Program
     from ebpf_emu import workloads as W
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     # EBPFEMU_BENCH_DIST=1: the process-group path (RCCL init, barriers, counter all-reduce, max
-    # over ranks) even for one rank, to exercise it on a one-GPU box
+    # over ranks) even for one rank, to exercise it on a one-GPU box. EBPFEMU_BENCH_BACKEND=gloo
+    # rehearses N ranks on one GPU (ranks share device LOCAL_RANK mod count; RCCL refuses two
+    # ranks on one device): the plumbing and the pins, not a scaling number.
     use_dist = world > 1 or os.environ.get("EBPFEMU_BENCH_DIST") == "1"
+    backend = os.environ.get("EBPFEMU_BENCH_BACKEND", "nccl")
+    if backend == "gloo":
+        local %= max(1, torch.cuda.device_count())
     if use_dist:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+
+    def all_reduce(t, op=None):
+        op = op or dist.ReduceOp.SUM
+        if backend == "nccl":
+            dist.all_reduce(t, op=op)
+        else:
+            h = t.cpu()
+            dist.all_reduce(h, op=op)
+            t.copy_(h)
 
     cfg_idx, desc = CONFIGS[args.config]
     if args.total_packets:
@@ -154,9 +303,10 @@ def main():
         pool_bytes = buf.nbytes
     k = 0
     while not args.total_packets:
-        # weak scaling: a pool of distinct batches per rank (rank-distinct seeds), larger than
-        # the Infinity Cache so that every step streams from HBM
-        cid = cfg_idx + 1 + 1000 * rank + 100 * k
+        # weak scaling: a pool of distinct batches per rank (pool batch k of rank r is seeded
+        # chunk k*W + r, chunk_id), larger than the Infinity Cache so that every step streams from
+        # HBM; tests/golden/bench_pins.json holds the oracle's counters of every such chunk
+        cid = chunk_seed(chunk_id(k, rank, world), mixed)
         if mixed:
             buf, offs, lens = W.frames_mixed(n, config_id=cid)
             batches.append(dict(frames=torch.from_numpy(buf).to(dev),
@@ -263,7 +413,8 @@ def main():
         ej.record(streams[si])
         stream.wait_event(ej)
     ev1.record(stream)
-    D.reduce_counters(counters)  # the one exchange step: per-verdict counters, RCCL / xGMI
+    if use_dist:  # the one exchange step: per-verdict counters, RCCL / xGMI
+        all_reduce(counters)
     torch.cuda.synchronize(dev)
     if use_dist:
         dist.barrier()
@@ -271,7 +422,7 @@ def main():
     elapsed = t1 - t0
     if use_dist:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        all_reduce(tt, dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     kern_avg_ms = ev0.elapsed_time(ev1) / args.steps
 
@@ -292,6 +443,17 @@ def main():
                 assert cnt == want, ("config-4 counters differ from tests/golden/config4.json",
                                      cnt, want)
                 pinned = "tests/golden/config4.json: counters == steps x fixture"
+    pin_note = None
+    if not args.total_packets and not args.no_counters:
+        # parity of the timed weak-scaling work at any rank count: the global counters of the K
+        # steps equal the oracle's counters of the chunks every rank timed (checked after timing)
+        want, src = pin_weak(PROGRAM_OF.get(args.config, args.config), mixed, fb, n, world,
+                             len(batches), args.steps, cnt)
+        if want is None:
+            pin_note = src
+        else:
+            assert cnt == want, ("timed counters differ from the oracle's fixture", src, cnt, want)
+            pinned = src
     mpps = total_pkts / elapsed / 1e6
     # the device's rate: the algorithmic bytes of a step over the HIP-event time per step (with
     # S > 1 streams consecutive launches overlap, so this is the time between batches, not one
@@ -419,6 +581,7 @@ def main():
             "wall_fixed_us": round((elapsed - kern_avg_ms * 1e-3 * args.steps) * 1e6, 2),
             "pmc_note": pmc_note,
             "parity_pinned": pinned,
+            "pin_note": pin_note,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -277,6 +277,13 @@ static const bool g_no_jit = [] {
   return e && e[0] == '1';
 }();
 
+// EBPFEMU_TEST_FAIL_STACK_JIT=1 (tests): every stack-window program's compilation fails, so
+// that the fallback to the general interpreter is exercised.
+static const bool g_fail_stack_jit = [] {
+  const char* e = getenv("EBPFEMU_TEST_FAIL_STACK_JIT");
+  return e && e[0] == '1';
+}();
+
 // Compile both table variants (caller holds p->mu). Returns the C ABI code of ebpf_prog_compile.
 static int jit_compile_locked(ebpf_prog* p) {
   if (p->jit_state == 0) {
@@ -290,19 +297,25 @@ static int jit_compile_locked(ebpf_prog* p) {
       p->jit_state = 1;
       for (int v = 0; v < kJitVariants && p->jit_state == 1; v++) {
         if (!p->jit_has[v]) continue;
-        const bool ok = v == 2 ? jit_compile_loop(p->xuops, p->ltuops, p->ltuopsx, p->jit_co[v],
+        const bool ok = !(g_fail_stack_jit && p->stack.k) &&
+                        (v == 2 ? jit_compile_loop(p->xuops, p->ltuops, p->ltuopsx, p->jit_co[v],
                                                   &p->jit_err, &p->jit_asm[v],
                                                   p->stack.k ? &p->stack : nullptr, &p->jit_deep)
                                : jit_compile(p->xuops,
                                              v == 3 ? p->tuopsk_xdp : v ? p->tuopsk : p->tuops,
                                              p->jit_co[v],
                                              &p->jit_err, &p->jit_asm[v],
-                                             p->stack.k ? &p->stack : nullptr);
+                                             p->stack.k ? &p->stack : nullptr));
         if (!ok && v >= 1 && p->stack.k && !p->jit_has[0]) {
           // a stack-window program whose code does not assemble (e.g. branches past the
-          // assembler's reach in a huge program): it stays on the general interpreter
+          // assembler's reach in a huge program): it stays on the general interpreter. Its
+          // stack tables are dropped too (batch_kind also routes tier-1 programs only there:
+          // the tables may already be on a device, and tile_kernel runs no stores)
           p->stack = StackPlan();
           p->kloads.clear();
+          p->tuopsk.clear();
+          p->ltuops.clear();
+          p->ltuopsx.clear();
           p->jit_has[1] = p->jit_has[2] = false;
           p->jit_co[1].clear();
           p->jit_co[2].clear();
@@ -1335,7 +1348,7 @@ static int batch_kind(const ebpf_prog* p, const ebpf_batch* b, const ebpf_batch_
     return batch_tier(p, b);
   }
   return (p->dev_duops[device] && b->max_steps >= p->xuops.size() && !generic) ? kKindDag
-         : (p->dev_ltuops[device] && !generic && !g_no_loop && !p->stack.k &&
+         : (p->dev_ltuops[device] && !generic && !g_no_loop && !p->stack.k && p->xtier == 0 &&
             (p->xuops.size() <= kTileMaxUops ||  // tile_kernel's loop mode, or compiled only
              (p->jit_mod[device][2] && !(b->flags & EBPF_BATCH_NO_JIT))))          ? kKindLoop
                                                                          : batch_tier(p, b);

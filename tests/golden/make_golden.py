@@ -9,7 +9,10 @@ fuzz vector is cross-checked against the independent Python restatement before i
                       seeded 1 Mi-packet chunks (chunk k: ebpf_emu.dist.chunk_frames(k, size), the
                       one definition bench.py --total-packets also builds its shards with) ->
                       per-chunk counters and verdict CRC32s, and the global counters
-Usage: python tests/golden/make_golden.py [config4]
+  bench_pins.json   : bench.py's weak-scaling pools at any rank count -> per-chunk counters of
+                      every 1 Mi-packet chunk a pool can hold, for each bench program (so that the
+                      default bench line pins its timed counters at N = 1..8)
+Usage: python tests/golden/make_golden.py [config4 | bench_pins]
 """
 import json
 import os
@@ -108,7 +111,69 @@ def config4(total=100_000_000):
             "counters": tot}
 
 
+# bench.py's weak-scaling pool: rank r of W, pool batch k -> chunk k*W + r (bench.chunk_id), so
+# the chunks of any rank count are 0 .. B*W-1. 64-byte chunks: dist.chunk_frames(c) (seed 3 + 100c,
+# the config-4 chunks); mixed chunks: workloads.frames_mixed(1Mi, config_id=5 + 100c).
+PIN_CHUNKS_64 = 128  # 16 pool batches x 8 ranks
+PIN_CHUNKS_MIXED = 16  # 2 pool batches x 8 ranks (a 1 Mi mixed batch is ~840 MB: one per rank)
+PIN_PROGRAMS_64 = ("5tuple", "drop", "5tuple_stack", "mac_swap_tx", "acl", "5tuple_xdp",
+                   "5tuple_call")
+PIN_PROGRAMS_MIXED = ("checksum", "checksum_stack")
+
+
+def _pin_chunk(args):
+    from ebpf_emu import dist as D
+
+    kind, c = args
+    out = {}
+    if kind == "64":
+        buf = D.chunk_frames(c, D.CHUNK)
+        for name in PIN_PROGRAMS_64:
+            p = oracle.Program(W.program(name))
+            _, _, cnt = p.run_batch(buf, D.CHUNK, stride=64, mem_size=1024, r10=512, threads=1,
+                                    xdp_md=name == "5tuple_xdp")
+            out[name] = [int(x) for x in cnt]
+    else:
+        buf, offs, lens = W.frames_mixed(D.CHUNK, config_id=5 + 100 * c)
+        for name in PIN_PROGRAMS_MIXED:
+            p = oracle.Program(W.program(name))
+            _, _, cnt = p.run_batch(buf, D.CHUNK, offsets=offs, lens=lens, mem_size=2048,
+                                    r10=2048, threads=1)
+            out[name] = [int(x) for x in cnt]
+    return kind, c, out
+
+
+def bench_pins():
+    from multiprocessing import Pool
+
+    from ebpf_emu import dist as D
+
+    jobs = [("64", c) for c in range(PIN_CHUNKS_64)] + [("mixed", c) for c in range(PIN_CHUNKS_MIXED)]
+    with Pool(max(1, min(8, os.cpu_count() or 1) - 1)) as pool:
+        res = pool.map(_pin_chunk, jobs)
+    progs = {}
+    for name in PIN_PROGRAMS_64 + PIN_PROGRAMS_MIXED:
+        mixed = name in PIN_PROGRAMS_MIXED
+        rows = sorted((c, o[name]) for kind, c, o in res if (kind == "mixed") == mixed)
+        for _, cnt in rows:
+            assert sum(cnt[:7]) == D.CHUNK
+        progs[name] = {"frames": "mixed" if mixed else "fixed64", "xdp_md": name == "5tuple_xdp",
+                       "program": W.program(name).hex(),
+                       "mem_size": 2048 if mixed else 1024, "r10": 2048 if mixed else 512,
+                       "chunk_counters": [cnt for _, cnt in rows]}
+    return {"chunk": D.CHUNK,
+            "chunk_of": "rank r of W, pool batch k -> chunk k*W + r",
+            "seed_fixed64": "dist.chunk_frames(c, 1Mi) = workloads.frames_fixed(1Mi, 64, "
+                            "config_id=3 + 100*c)",
+            "seed_mixed": "workloads.frames_mixed(1Mi, config_id=5 + 100*c)",
+            "programs": progs}
+
+
 if __name__ == "__main__":
+    if sys.argv[1:] == ["bench_pins"]:
+        with open(os.path.join(HERE, "bench_pins.json"), "w") as f:
+            json.dump(bench_pins(), f, indent=0)
+        sys.exit(0)
     if sys.argv[1:] == ["config4"]:
         with open(os.path.join(HERE, "config4.json"), "w") as f:
             json.dump(config4(), f, indent=0)

@@ -756,6 +756,36 @@ def test_bench_line(cuda):
     assert c["drop"] + c["pass"] + c["other"] + c["faults"] <= 6 * (1 << 16)
 
 
+@pytest.mark.parametrize("extra,env", [
+    ([], {}),
+    # two ranks on this one GPU through bench.py's own launcher (gloo: RCCL refuses two ranks on
+    # one device): spawn, rendezvous, counter reduction, max over ranks, per-rank chunk pins
+    (["--gpus", "2"], {"EBPFEMU_BENCH_BACKEND": "gloo"}),
+    (["--config", "xdp", "--layout", "offsets"], {}),
+])
+def test_bench_line_pinned(cuda, extra, env):
+    """The default weak-scaling line at full batch size (1 Mi packets, the pool of 8 chunks per
+    rank) pins its timed counters to the oracle's fixture (tests/golden/bench_pins.json)."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    e = dict(os.environ, **env)
+    e.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--steps", "11",
+                        "--warmup", "2", "--cpu-seconds", "0"] + extra,
+                       capture_output=True, text=True, timeout=170, cwd=root, env=e)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    n = 2 if "--gpus" in extra else 1
+    assert d["n_gpus"] == n and d["config"]["pool_batches"] == 8
+    assert d["parity_pinned"] and f"k*{n}+r" in d["parity_pinned"], d.get("pin_note")
+    c = d["counters"]
+    assert c["drop"] + c["pass"] + c["other"] + c["faults"] == 11 * n * (1 << 20)
+
+
 @pytest.mark.parametrize("slot,shift", [(64, 0), (80, 3)])
 @pytest.mark.parametrize("name", ["5tuple", "5tuple_stack", "5tuple_xdp", "acl"])
 def test_var_kernel_full_size_shuffled(cuda, name, slot, shift):

@@ -575,3 +575,68 @@ def test_stack_loop_programs(cuda, oracle_mod, layout):
             _vs_oracle(oracle_mod, img, _images_of(pkts, xdp), got, tag=f"{layout} it {it}",
                        max_steps=steps)
     assert n_stack >= 12, n_stack
+
+
+_FALLBACK_CHILD = r"""
+import json, sys, random
+import numpy as np, torch
+sys.path[:0] = sys.argv[1:3]
+from ebpf_emu import Program, _lib
+from ebpf_emu import workloads as W
+from ebpf_emu.asm import assemble
+from fuzzgen import gen_stack_loop_program, gen_stack_program
+rng = random.Random(4242)
+progs = [assemble(src) for src, k in DIRECTED if k] + [W.program("5tuple_stack"),
+         W.program("checksum_stack"), W.program("mac_swap_tx")]
+progs += [gen_stack_loop_program(rng) for _ in range(4)] + [gen_stack_program(rng) for _ in range(4)]
+dev = torch.device("cuda", 0)
+out = []
+for img in progs:
+    p = Program(img)
+    compiled = p.compile()
+    pkts = [bytes(rng.getrandbits(8) for _ in range(64)) for _ in range(70)]
+    buf = np.frombuffer(b"".join(pkts), dtype=np.uint8)
+    frames = torch.tensor(buf, device=dev)
+    b = p.make_batch(frames, n=len(pkts), stride=64, max_steps=20000)
+    kern = p.batch_kernel(b, _lib.BatchOut(), 0)
+    cnt = torch.zeros(8, dtype=torch.int64, device=dev)
+    res = p.run(frames, n=len(pkts), stride=64, max_steps=20000, r0=True, status=True, regs=True,
+                counters=cnt)
+    torch.cuda.synchronize()
+    out.append(dict(img=img.hex(), kernel=int(kern), window=p.stack_window, pkts=[x.hex() for x in pkts],
+                    status=res.status.cpu().tolist(),
+                    regs=res.regs.cpu().numpy().view(np.uint64).tolist(),
+                    counters=cnt.cpu().numpy().view(np.uint64).tolist()))
+    p.close()
+print(json.dumps(out))
+"""
+
+
+@pytest.mark.gpu
+def test_stack_compile_failure_falls_back(cuda, oracle_mod):
+    """A stack-window program whose compilation fails (EBPFEMU_TEST_FAIL_STACK_JIT=1 forces it)
+    runs on the general interpreter's tier 1 -- never on tile_kernel's loop mode, whose tables
+    may already be on the device and which has no stores -- with the oracle's results."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    from ebpf_emu import _lib
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    code = "DIRECTED = %r\n" % (DIRECTED,) + _FALLBACK_CHILD
+    env = dict(os.environ, EBPFEMU_TEST_FAIL_STACK_JIT="1")
+    r = subprocess.run([sys.executable, "-c", code, os.path.join(root, "ebpf-emu_amd"), here],
+                       capture_output=True, text=True, timeout=150, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert len(res) >= 20
+    for d in res:
+        assert d["window"] == 0, d["img"]  # the fallback dropped the stack plan
+        assert d["kernel"] == _lib.EBPF_KERNEL_GENERAL_T1, (d["img"], d["kernel"])
+        got = dict(status=np.array(d["status"]), regs=np.array(d["regs"], dtype=np.uint64),
+                   counters=np.array(d["counters"], dtype=np.uint64))
+        _vs_oracle(oracle_mod, bytes.fromhex(d["img"]), [bytes.fromhex(x) for x in d["pkts"]],
+                   got, tag="fallback", max_steps=20000)
