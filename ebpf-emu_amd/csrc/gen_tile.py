@@ -1054,7 +1054,9 @@ s_addc_u32 {SLOTBH}, {SLOTBH}, 0
 .p2align 8
 .Lslots%=:"""
 
-# bucket: 0..4 r0, 5 r0 >= 5, 6 fault, 7 not a packet; stores of the valid lanes
+# bucket: 0..4 r0, 5 r0 >= 5, 6 fault, 7 not a packet, 8 deoptimized (status 0x80, jit.h kStDeopt:
+# a compiled store-mode lane that left for the general interpreter -- no outputs, no steps, its
+# packet listed by the C++ after the statement); stores of the valid lanes
 EPILOGUE = """.Ldone%=:
 s_mov_b64 exec, {EXEC0}
 v_cmp_gt_u64 vcc, 5, {RF}
@@ -1063,6 +1065,11 @@ v_cmp_ne_u32 vcc, 0, {ST}
 v_cndmask_b32_e64 %[bkt], %[bkt], 6, vcc
 v_cndmask_b32_e64 %[bkt], 7, %[bkt], {VM}
 v_cndmask_b32_e64 %[nst], 0, {NST}, {VM}
+v_cmp_eq_u32 vcc, 0x80, {ST}
+s_and_b64 vcc, vcc, {VM}
+v_cndmask_b32_e64 %[bkt], %[bkt], 8, vcc
+v_cndmask_b32_e64 %[nst], %[nst], 0, vcc
+s_andn2_b64 {VM}, {VM}, vcc
 s_mov_b64 exec, {VM}
 s_cmp_lg_u64 exec, 0
 s_cbranch_scc0 .Lend%=

@@ -527,7 +527,8 @@ static std::vector<TUop> build_tile(const std::vector<Uop>& uops, const std::vec
     u.imm = o.imm;
     u.width = o.width;
     u.blen = start[i] ? rem[i] : 0;
-    if (h == H_LDX || h == H_ARSH64_IMM || h == H_ARSH64_REG || (stack && uops[i].op == U_ATOMIC))
+    if (h == H_LDX || h == H_ARSH64_IMM || h == H_ARSH64_REG ||
+        (stack && (uops[i].op == U_ATOMIC || uops[i].op == U_ST || uops[i].op == U_STX)))
       u.a0 = rem[i];  // REMX
     if (h == H_LDX && o.width == 1) id = chained ? T_LDX1_C : T_LDX1_E;  // one byte: one dword
     if (h == H_LDXK || h == H_LDXK_FAR) {
@@ -900,7 +901,8 @@ static StackAnalysis analyze_stack(const std::vector<Uop>& uops) {
   };
   std::vector<int32_t> off(n, kNoStack), pw(n, kNoStack);
   std::vector<char> dyn(n, 0);  // LDX with an unknown base
-  bool any_pw = false;
+  std::vector<char> dyns(n, 0);  // ST/STX with an unknown base (store mode)
+  bool any_pw = false, any_dyn = false;
   int64_t lo = 0, hi = INT64_MIN;  // store bytes relative to r10: [lo, hi)
   // passes in pc order until the states stop changing (one pass without back edges; with them
   // each join only moves a register towards unknown, so this ends), the last one collecting
@@ -909,7 +911,8 @@ static StackAnalysis analyze_stack(const std::vector<Uop>& uops) {
   std::fill(off.begin(), off.end(), kNoStack);
   std::fill(pw.begin(), pw.end(), kNoStack);
   std::fill(dyn.begin(), dyn.end(), 0);
-  any_pw = false;
+  std::fill(dyns.begin(), dyns.end(), 0);
+  any_pw = any_dyn = false;
   lo = 0, hi = INT64_MIN;
   for (uint32_t i = 0; i < n; i++) {
     if (!in[i].reached) continue;
@@ -924,6 +927,9 @@ static StackAnalysis analyze_stack(const std::vector<Uop>& uops) {
         if (c < 0 || c + w > (int64_t)kWin) return res;
         pw[i] = (int32_t)c;
         any_pw = true;
+      } else if (D.k == TOP && u.op != U_ATOMIC) {  // through a packet pointer: store mode
+        dyns[i] = 1;
+        any_dyn = true;
       } else {
         if (D.k != FP) return res;
         const int64_t d = D.v + (int64_t)u.x;
@@ -976,11 +982,23 @@ static StackAnalysis analyze_stack(const std::vector<Uop>& uops) {
   }
   // (loop programs run on the loop kernel, whose loads are not constant-folded: no packet-window
   // stores there)
-  if (loops && any_pw) return res;
+  if (loops && (any_pw || any_dyn)) return res;
+  // store mode (register-address stores): the header window lives in LDS, where every packet
+  // load reads it; a constant-address load straddling the window's end would read its low bytes
+  // from HBM (register-address ones deoptimize their lane at run time)
+  if (any_dyn)
+    for (uint32_t i = 0; i < n; i++) {
+      const Uop& u = uops[i];
+      if (u.op != U_LDX || !in[i].reached || off[i] != kNoStack || dyn[i]) continue;
+      const Val S = in[i].r[u.src];
+      if (S.k != CONST) continue;
+      const int64_t a = S.v + (int64_t)u.x;
+      if (a < (int64_t)kWin && a + u.aux > (int64_t)kWin) return res;
+    }
   // packet-window stores: every load must be a constant-address one (fold_const_loads reads the
   // stored bytes from the window registers) or a stack-window one, none straddling the window's
   // end (its bytes below kWin would come from HBM)
-  if (any_pw)
+  if (any_pw && !any_dyn)
     for (uint32_t i = 0; i < n; i++) {
       const Uop& u = uops[i];
       if (u.op != U_LDX || !in[i].reached || off[i] != kNoStack) continue;
@@ -989,7 +1007,7 @@ static StackAnalysis analyze_stack(const std::vector<Uop>& uops) {
       if (dyn[i] || S.k != CONST || (a < (int64_t)kWin && a + u.aux > (int64_t)kWin)) return res;
     }
   // (a plan with packet-window stores only keeps a 4-byte stack window)
-  const uint32_t k = std::max<uint32_t>((uint32_t)((-lo + 3) & ~3), any_pw ? 4u : 0u);
+  const uint32_t k = std::max<uint32_t>((uint32_t)((-lo + 3) & ~3), any_pw || any_dyn ? 4u : 0u);
   if (hi > 0 || k == 0 || k > kStackMax) return res;
   for (uint32_t i = 0; i < n; i++) {
     const Uop& u = uops[i];
@@ -997,7 +1015,7 @@ static StackAnalysis analyze_stack(const std::vector<Uop>& uops) {
     const int64_t d = off[i];
     if (d >= -(int64_t)k && d + u.aux <= 0) continue;       // inside the window
     if (d + u.aux <= -(int64_t)k || d >= 0) {                 // disjoint: an ordinary load at a
-      if (any_pw) return res;                                 // uniform address, checked at run
+      if (any_pw && !any_dyn) return res;                     // uniform address, checked at run
       off[i] = kNoStack;                                      // time like any other (not with
       continue;                                               // packet stores: LDS is stale)
     }
@@ -1007,6 +1025,8 @@ static StackAnalysis analyze_stack(const std::vector<Uop>& uops) {
   res.plan.off = std::move(off);
   res.plan.pw = std::move(pw);
   res.plan.any_pw = any_pw;
+  res.plan.dyn = std::move(dyns);
+  res.plan.any_dyn = any_dyn;
   return res;
 }
 
@@ -1081,7 +1101,7 @@ int ebpf_prog_load(const uint8_t* code, size_t nbytes, ebpf_prog** out, size_t* 
         sa.plan.k && forward ? fold_const_loads(xu, build_dag(xu)) : std::vector<DUop>();
     // packet-window stores: every load outside the stack window must be a constant-address one
     // (read from the window registers the stores update)
-    for (size_t i = 0; sa.plan.k && sa.plan.any_pw && forward && i < xu.size(); i++)
+    for (size_t i = 0; sa.plan.k && sa.plan.any_pw && !sa.plan.any_dyn && forward && i < xu.size(); i++)
       if (xu[i].op == U_LDX && sa.plan.off[i] == kNoStack && (dk[i].opaux & 0xff) != U_LDXK)
         sa.plan.k = 0;
     if (sa.plan.k) {
@@ -1092,7 +1112,7 @@ int ebpf_prog_load(const uint8_t* code, size_t nbytes, ebpf_prog** out, size_t* 
       }
       // the loop kernel's stack variant (back edges, or a step budget that can bind; not with
       // packet-window stores, which need the forward kernels' preloaded window)
-      if (!sa.plan.any_pw) {
+      if (!sa.plan.any_pw && !sa.plan.any_dyn) {
         const std::vector<DUop> d = build_dag(xu);
         p->ltuops = build_tile(xu, d, false, true);
         p->ltuopsx = build_tile(xu, d, true, true);
@@ -1230,6 +1250,7 @@ int ebpf_prog_upload(ebpf_prog* p, int device) {
           rc = EBPF_EHIP;
         else if (v == 2 && p->jit_deep)  // (the code is in the deep-prefetch loop kernel)
           p->jit_fn[device][v].loop = p->jit_fn[device][v].loop_deep;
+        p->jit_fn[device][v].var_only = p->stack.any_dyn;
       }
   }
   if (rc == EBPF_OK) {
@@ -1310,9 +1331,12 @@ static bool stack_launch_ok(const ebpf_prog* p, const ebpf_batch* b, const ebpf_
   la.lens = b->lens;
   la.stride = b->stride;
   la.mem_out = out->mem;
-  const bool fixed = launch_fixed_layout(la);
+  // (store mode runs on the var kernel whatever the layout: its window init covers any packet;
+  // its header-window loads read LDS without a bounds check, so the image must cover the window)
+  const bool fixed = launch_fixed_layout(la) && !p->stack.any_dyn;
   const uint64_t img_len = b->stride + ((b->flags & EBPF_BATCH_XDP_MD) ? 8 : 0);
   if (fixed ? r10 - k < img_len : !stack_var_ok(p, b)) return false;
+  if (p->stack.any_dyn && b->mem_size < (uint64_t)kWin) return false;
   for (const auto& kl : p->kloads) {
     if (kl.first < r10 && kl.first + kl.second > r10 - k) return false;
     // packet-window stores: the compiled code has only the copy whose window loads read the
@@ -1383,6 +1407,9 @@ static const bool g_xdp_stage = [] {
 static bool xdp_in_place(ebpf_prog* p, const ebpf_batch* b, bool mem_out, int device, int kind,
                          bool stk) {
   if (!(b->flags & EBPF_BATCH_XDP_MD) || g_xdp_stage || kind != kKindDag) return false;
+  // store mode: a deoptimized lane re-runs on the general interpreter, which reads the images
+  // xdp_stage writes (the ctx is not in the frames)
+  if (stk && p->stack.any_dyn) return false;
   LaunchArgs a{};
   a.n_uops = kind_uops(p, kind);
   a.frames = b->frames;
@@ -1397,20 +1424,34 @@ static bool xdp_in_place(ebpf_prog* p, const ebpf_batch* b, bool mem_out, int de
          (id == EBPF_KERNEL_TILE && !launch_fixed_layout(a));
 }
 
+// The general interpreter's tier-1 grid for a batch (its wave slots' images: the workspace).
+static int tier1_grid(const ebpf_prog* p, const ebpf_batch* b, int device) {
+  int cur = device_of_current();
+  hipSetDevice(device);
+  int grid = 0;
+  interp_grid(kKindTier1, (uint32_t)p->uops.size(), p->tiny, (b->n + 63) / 64, &grid);
+  hipSetDevice(cur);
+  return grid;
+}
+
+// The deopt pass of a store-mode batch: at most this many workgroups (the pass usually finds an
+// empty list; each of its workgroups stages the program and flushes its counters)
+constexpr int kDeoptMaxGrid = 256;
+
+// Bytes of the tier-1 wave slots (workspace, from kWsSlotsOff).
+static uint64_t tier1_slots_bytes(const ebpf_prog* p, const ebpf_batch* b, int device) {
+  if (batch_tier(p, b) != 1) return 0;
+  return (uint64_t)tier1_grid(p, b, device) * kWavesPerBlock * tier1_slot_bytes(b->mem_size);
+}
+
 uint64_t ebpf_workspace_bytes(const ebpf_prog* p, const ebpf_batch* b, int device) {
   if (!p || !b) return 0;
   const uint64_t x = (b->flags & EBPF_BATCH_XDP_MD) ? xdp_region_bytes(b) : 0;
   uint64_t bytes = kWsSlotsOff + x;
   if (use_binning(p, b))  // the binned packet order, then the per-workgroup class counts
     bytes += b->n * 4 + 4ull * kBinMaxWgs * kBinClasses;
-  if (batch_tier(p, b) == 1) {
-    int cur = device_of_current();
-    hipSetDevice(device);
-    int grid = 0;
-    interp_grid(kKindTier1, (uint32_t)p->uops.size(), p->tiny, (b->n + 63) / 64, &grid);
-    hipSetDevice(cur);
-    bytes += (uint64_t)grid * kWavesPerBlock * tier1_slot_bytes(b->mem_size);
-  }
+  bytes += align16(tier1_slots_bytes(p, b, device));
+  if (p->stack.any_dyn) bytes += align16(b->n * 4);  // the deopt list's indices (past the slots)
   return bytes;  // (the xdp_md region, when present, is the last x bytes)
 }
 
@@ -1571,7 +1612,25 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* bin, const ebpf_batch_out* ou
     }
   }
   const JitFns* jit = batch_jit(p, b, kind, stk, device);
+  // store mode (register-address packet stores, StackPlan::any_dyn): lanes the compiled kernel
+  // cannot finish are listed, then re-run from the start by the general interpreter (tier 1)
+  const bool deopt = stk && p->stack.any_dyn && kind == kKindDag && jit &&
+                     launch_kernel_id(kind, a, jit, stk) == EBPF_KERNEL_JIT_VAR_STACK;
+  if (deopt) {
+    a.deopt = (uint32_t*)(ws + kWsDeoptOff);
+    a.deopt_idx = (uint32_t*)(ws + kWsSlotsOff + align16(tier1_slots_bytes(p, b, device)));
+  }
   hipError_t e = launch_interp(kind, a, grid, s, jit, stk);
+  if (deopt && e == hipSuccess) {
+    LaunchArgs d = a;
+    d.deopt_pass = 1;
+    d.n_uops = (uint32_t)p->uops.size();
+    d.tprog = d.tprog_exact = nullptr;
+    d.dprog = nullptr;
+    d.xdp = 0;
+    const int g1 = std::min(tier1_grid(p, b, device), kDeoptMaxGrid);
+    e = launch_interp(kKindTier1, d, g1, s, nullptr, false);
+  }
   if (cur != device) hipSetDevice(cur);
   return e == hipSuccess ? EBPF_OK : EBPF_EHIP;
 }

@@ -530,9 +530,18 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
     }
   }
 
-  for (uint64_t tile = wave_slot; tile < a.n_tiles; tile += total_waves) {
-    const uint64_t pkt = tile * kWave + lane;
-    const bool valid = pkt < a.n;
+  // the deopt pass (tier 1, LaunchArgs::deopt_pass): the packets the compiled store-mode kernel
+  // listed, idx[0 .. count), each run from the start with its outputs at its own index
+  const bool dpass = TIER == 1 && a.deopt_pass != 0;
+  uint64_t n_run = a.n, tiles_run = a.n_tiles;
+  if (dpass) {
+    n_run = rfl(__hip_atomic_load(a.deopt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    tiles_run = (n_run + kWave - 1) / kWave;
+  }
+  for (uint64_t tile = wave_slot; tile < tiles_run; tile += total_waves) {
+    const uint64_t slot = tile * kWave + lane;
+    const bool valid = slot < n_run;
+    const uint64_t pkt = !dpass ? slot : valid ? (uint64_t)a.deopt_idx[slot] : 0ull;
     const uint8_t* base = nullptr;
     uint32_t len = 0;
     uint8_t* const my_win = L.win + (DB ? b : 0u) * kWinBytes + lane * kWin;
@@ -906,6 +915,15 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
   if (TIER == 0) dma_wait();  // no LDS-DMA may still target this workgroup's LDS at exit
 
   flush_counters(a, cnt, retired, smem, lane, wv);
+  if (dpass) {  // the last workgroup to finish clears the list for the next batch on the stream
+    __syncthreads();
+    if (threadIdx.x == 0 &&
+        __hip_atomic_fetch_add(a.deopt + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+            gridDim.x - 1) {
+      __hip_atomic_store(a.deopt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(a.deopt + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 }
 
 // ============================================================================================
@@ -1650,6 +1668,25 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
         }
       }
     }
+    if (JIT && a.deopt) {  // store mode: lanes that left for the general interpreter (bucket 8)
+      const uint64_t dm = ballot(bkt == 8u);
+      if (dm) {
+        uint32_t ln;
+        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(dm >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)dm, 0u));
+        const uint32_t first = (uint32_t)__builtin_ctzll(dm);
+        uint32_t base = 0;
+        if (ln == first)
+          base = __hip_atomic_fetch_add(a.deopt, (uint32_t)__builtin_popcountll(dm),
+                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        base = __builtin_amdgcn_readlane(base, first);
+        const uint64_t slot = t * kWave + ln;
+        if (bkt == 8u)
+          a.deopt_idx[base + rank] =
+              (uint32_t)(LOOPS && a.perm ? (uint64_t)a.perm[slot] : slot);
+      }
+    }
 #pragma unroll
     for (int b = 0; b < 7; b++) cnt[b] += __builtin_popcountll(ballot(bkt == (uint32_t)b));
     retired += nst;
@@ -2029,7 +2066,8 @@ int launch_kernel_id(int kind, const LaunchArgs& a, const JitFns* jit, bool stac
   if (jit && jit->loop && kind == kKindLoop)
     return stack ? EBPF_KERNEL_JIT_LOOP_STACK : EBPF_KERNEL_JIT_LOOP;
   if (jit && jit->fixed && jit_forward_for(kind, a.n_uops))
-    return jit_fixed_layout(&a) ? (stack ? EBPF_KERNEL_JIT_STACK : EBPF_KERNEL_JIT_FIXED)
+    return jit_fixed_layout(&a) && !jit->var_only
+               ? (stack ? EBPF_KERNEL_JIT_STACK : EBPF_KERNEL_JIT_FIXED)
                                 : (stack ? EBPF_KERNEL_JIT_VAR_STACK : EBPF_KERNEL_JIT_VAR);
   if (kind == kKindDag)
     return tile_kernel_for(kind, a.n_uops) ? EBPF_KERNEL_TILE : EBPF_KERNEL_DAG;
@@ -2072,7 +2110,7 @@ hipError_t launch_interp(int kind, const LaunchArgs& a, int grid, hipStream_t st
   // for tile_kernel's, which is higher: its extra workgroups would run in a second round);
   // EBPFEMU_VAR_GRID=tile keeps tile_kernel's grid (A/B)
   const bool var = jit && jit->fixed && kind != kKindLoop && jit_forward_for(kind, a.n_uops) &&
-                   !jit_fixed_layout(&a);
+                   (!jit_fixed_layout(&a) || jit->var_only);
   const bool vdb = g_var_db && g_var_pipe_host;
   const uint32_t vlds = g_lds_pad + kWavesPerBlock * (vdb ? kTileWaveLdsDb3 : kTileWaveLdsPipe);
   if (var && (g_var_grid || vdb)) grid = jit_grid(stack ? jit->var_stack : jit->var, vlds, a.n_tiles);
@@ -2094,7 +2132,7 @@ hipError_t launch_interp(int kind, const LaunchArgs& a, int grid, hipStream_t st
     e = hipModuleLaunchKernel(stack ? jit->loop_stack : jit->loop, grid, 1, 1, kBlock, 1, 1, lds,
                               stream, bargs, nullptr);
   } else if (jit && jit->fixed && jit_forward_for(kind, a.n_uops)) {
-    if (jit_fixed_layout(&a)) {  // double-buffered windows: its own LDS size and grid
+    if (jit_fixed_layout(&a) && !jit->var_only) {  // double-buffered windows: its own LDS size and grid
       const uint32_t dlds = g_lds_pad + kDbWaves * kTileWaveLdsDb;
       e = hipModuleLaunchKernel(jit->fixed, jit_grid(jit->fixed, dlds, a.n_tiles, kDbBlock), 1, 1,
                                 kDbBlock, 1, 1, dlds, stream, bargs, nullptr);

@@ -978,6 +978,183 @@ struct Compiler {
     return s;
   }
 
+  // ---- store mode (StackPlan::any_dyn): the lane's header window in LDS is the image's bytes
+  // [0, 64) -- packet bytes, zeros at or past LEN, and whatever the program stored there. Window
+  // byte b of the lane is at LDS address (b ^ SWZ) + WIN (v35 = SWZ, v34 = WIN: the 16-byte chunks
+  // swizzled per lane, interp.hip win_off), so a run of bytes inside one chunk is contiguous. ----
+
+  // The value register pair of a store (STX: src) or, for ST, "" (constant bytes of o.k, Q8).
+  // The low `nb` bytes of value bytes [q, q + nb) in a VGPR: a source register itself, or v42
+  // (shifted / materialized). hi16: the bytes sit in bits 16.. of the returned register instead.
+  std::string store_value(const Uop& o, uint32_t q, uint32_t nb, std::string& s, bool* hi16) const {
+    *hi16 = false;
+    if (o.op == U_ST) {
+      uint32_t c = 0;
+      for (uint32_t b = 0; b < nb; b++) c |= (uint32_t)((((uint64_t)o.k) >> (8 * (q + b))) & 0xff) << (8 * b);
+      s += "v_mov_b32 v42, " + hex32(c) + "\n";
+      return "v42";
+    }
+    const std::string V = "v" + std::to_string(2 * o.src + (q >= 4 ? 1 : 0));
+    const uint32_t r = q & 3;
+    if (r == 0) return V;
+    if (r == 2 && nb <= 2) {
+      *hi16 = true;
+      return V;
+    }
+    if (r + nb <= 4) {
+      s += "v_lshrrev_b32 v42, " + std::to_string(8 * r) + ", " + V + "\n";
+    } else {  // (crosses into the high word: q < 4 < q + nb)
+      s += "v_alignbyte_b32 v42, v" + std::to_string(2 * o.src + 1) + ", v" +
+           std::to_string(2 * o.src) + ", " + std::to_string(r) + "\n";
+    }
+    return "v42";
+  }
+
+  // ST / STX at the constant image address p = pw[i] (inside the window): LDS writes of the
+  // widest naturally aligned pieces inside each 16-byte chunk (emu.rs:354-372, little-endian).
+  std::string lds_store_const(uint32_t i) const {
+    const Uop& o = uops[i];
+    const uint32_t p = (uint32_t)stk->pw[i], w = o.aux;
+    std::string s = "; store [" + std::to_string(p) + ", +" + std::to_string(w) + ") into the window\n";
+    int32_t chunk = -1;
+    for (uint32_t b = p; b < p + w;) {
+      if ((int32_t)(b >> 4) != chunk) {
+        chunk = (int32_t)(b >> 4);
+        s += "v_xad_u32 v43, v35, " + std::to_string(16 * chunk) + ", v34\n";
+      }
+      const uint32_t q = b - p, left = std::min(p + w - b, 16 - (b & 15));
+      uint32_t nb = 1;
+      if ((b & 3) == 0 && (q & 3) == 0 && left >= 4) nb = 4;
+      else if ((b & 1) == 0 && (q & 1) == 0 && left >= 2) nb = 2;
+      bool hi = false;
+      const std::string V = store_value(o, q, nb, s, &hi);
+      const std::string op = nb == 4 ? "ds_write_b32" : nb == 2 ? (hi ? "ds_write_b16_d16_hi" : "ds_write_b16")
+                                                                : (hi ? "ds_write_b8_d16_hi" : "ds_write_b8");
+      s += op + " v43, " + V + " offset:" + std::to_string(b & 15) + "\n";
+      b += nb;
+    }
+    return s;
+  }
+
+  // ST / STX through a register (StackPlan::dyn): the address a = dst + off with the reference's
+  // bounds (a >= mem -> ST_MEM, a + w > mem -> ST_MEM_UB: only the first byte is checked, Q16,
+  // mmu.rs:23-30); lanes storing past the window [0, 64) deoptimize (status kStDeopt: the
+  // general interpreter re-runs their packets); the rest write their bytes into LDS one by one.
+  std::string lds_store_dyn(uint32_t i, const std::string& P) const {
+    const Uop& o = uops[i];
+    const uint32_t w = o.aux;
+    const std::string U = P + "u" + std::to_string(i), next = entry_label(P, next_start(i));
+    const int64_t off = (int64_t)(int32_t)o.x;
+    std::string s = "; store through r" + std::to_string(o.dst) + " (store mode)\n", offs;
+    if (inline_const(off)) {
+      offs = std::to_string(off);
+    } else {
+      s += "s_mov_b32 s48, " + hex32((uint32_t)off) + "\ns_mov_b32 s49, " +
+           hex32((uint32_t)((uint64_t)off >> 32)) + "\n";
+      offs = "s[48:49]";
+    }
+    s += "v_lshl_add_u64 v[36:37], " + vpair(2 * o.dst, 0, 1) + ", 0, " + offs + "\n"
+         "v_cmp_gt_u64_e64 s[60:61], s[52:53], v[36:37]\n"
+         "v_add_u32 v38, " + std::to_string(w) + ", v36\n"
+         "v_cmp_ge_u32_e64 s[62:63], s52, v38\n"
+         "s_and_b64 vcc, s[60:61], s[62:63]\n"
+         "s_andn2_b64 s[64:65], exec, vcc\n"
+         "s_cbranch_scc0 .Lsok" + U + "\n"
+         "s_mov_b64 s[66:67], exec\ns_mov_b64 exec, s[64:65]\n"
+         "v_cndmask_b32_e64 v30, 1, 2, s[60:61]\n"
+         "v_mov_b32 v28, -1\n"
+         "v_subrev_u32 v29, " + std::to_string(t[i].a0) + ", v29\n"
+         "s_andn2_b64 exec, s[66:67], s[64:65]\n"
+         "s_cbranch_execz " + next + "\n"
+         ".Lsok" + U + ":\n"
+         "v_cmp_lt_u32 vcc, 64, v38\n"
+         "s_and_b64 vcc, vcc, exec\n"
+         "s_cbranch_vccz .Lsin" + U + "\n"
+         "s_mov_b64 s[66:67], exec\ns_mov_b64 exec, vcc\n"
+         "v_mov_b32 v30, 0x80\nv_mov_b32 v28, -1\n"
+         "s_andn2_b64 exec, s[66:67], vcc\n"
+         "s_cbranch_execz " + next + "\n"
+         ".Lsin" + U + ":\n";
+    for (uint32_t j = 0; j < w; j++) {
+      std::string A = "v36";
+      if (j) {
+        s += "v_add_u32 v39, " + std::to_string(j) + ", v36\n";
+        A = "v39";
+      }
+      s += "v_xad_u32 v40, " + A + ", v35, v34\n";
+      bool hi = false;
+      const std::string V = store_value(o, j, 1, s, &hi);
+      s += std::string(hi ? "ds_write_b8_d16_hi" : "ds_write_b8") + " v40, " + V + "\n";
+    }
+    return s;
+  }
+
+  // A constant-address load inside the window (LDXK) in store mode: the window dwords from LDS
+  // (no LEN mask: the bytes at or past LEN are zeros there, or stored ones), merged into dst (Q1).
+  std::string ldxk_lds(uint32_t i) const {
+    const TUop& u = t[i];
+    const uint32_t a0 = u.a0, w = u.x - u.a0, d = a0 & ~3u, sh = a0 & 3;
+    const uint32_t nd = (sh + w + 3) / 4;
+    std::string s;
+    for (uint32_t k = 0; k < nd; k++)
+      s += "v_xad_u32 v" + std::to_string(43 + k) + ", v35, " + std::to_string(d + 4 * k) +
+           ", v34\nds_read_b32 v" + std::to_string(49 + k) + ", v" + std::to_string(43 + k) + "\n";
+    s += "s_waitcnt lgkmcnt(0)\n";
+    if (nd == 1) s += "v_lshrrev_b32 v26, " + std::to_string(8 * sh) + ", v49\n";
+    else s += "v_alignbyte_b32 v26, v50, v49, " + std::to_string(sh) + "\n";
+    if (w == 8) s += nd == 3 ? "v_alignbyte_b32 v27, v51, v50, " + std::to_string(sh) + "\n"
+                             : std::string("v_mov_b32 v27, v50\n");
+    const std::string D0 = "v" + std::to_string(u.dst2);
+    if (w == 1 || w == 2)
+      s += "s_mov_b32 s42, " + std::string(w == 1 ? "0xff" : "0xffff") + "\nv_bfi_b32 " + D0 +
+           ", s42, v26, " + D0 + "\n";
+    else if (w == 4)
+      s += "v_mov_b32 " + D0 + ", v26\n";
+    else
+      s += "v_mov_b64 " + vpair(u.dst2, 0, 1) + ", v[26:27]\n";
+    return s;
+  }
+
+  // The store-mode program (the var kernel's stack statement only; every other statement is
+  // never launched for it, host.cpp JitFns::var_only): the stack window in VGPRs as before; the
+  // header window's bytes at or past LEN zeroed in LDS once (lanes with LEN < 64 only), so loads
+  // and stores address one image; then the program's one (checked) copy.
+  bool body_store(const Marker& m, std::string& out) {
+    const std::string P = "J" + m.n + "_";
+    ovl_tag = m.n;
+    overlay_widths = 0;
+    if (!m.stack) {
+      out = "s_mov_b64 exec, 0  ; (store mode: the var kernel's stack statement only)\n";
+      return true;
+    }
+    std::string ool;
+    std::string main = "; compiled eBPF program (store mode): " + std::to_string(n) + " micro-ops\n"
+                       "s_mov_b32 s52, s33\ns_mov_b32 s53, 0\n" + stack_zero() + stack_init(P, ool);
+    const std::string Z = ".L" + P + "zdone";
+    main += "s_mov_b64 s[64:65], exec\ns_mov_b64 exec, -1\n"
+            "v_cmp_gt_u32 vcc, 64, v31\ns_cbranch_vccz " + Z + "\n";
+    for (uint32_t c = 0; c < 4; c++)
+      main += "v_xad_u32 v" + std::to_string(36 + c) + ", v35, " + std::to_string(16 * c) +
+              ", v34\nds_read_b128 v[" + std::to_string(64 + 4 * c) + ":" + std::to_string(67 + 4 * c) +
+              "], v" + std::to_string(36 + c) + "\n";
+    main += "s_waitcnt lgkmcnt(0)\n";
+    for (uint32_t j = 0; j < 16; j++)  // dword j keeps its bytes below LEN
+      main += "v_subrev_u32 v40, " + std::to_string(4 * j) + ", v31\n"
+              "v_med3_i32 v40, v40, 0, 4\nv_lshlrev_b32 v40, 3, v40\n"
+              "v_lshlrev_b64 v[40:41], v40, 1\nv_add_u32 v40, -1, v40\n"
+              "v_and_b32 v" + std::to_string(64 + j) + ", v40, v" + std::to_string(64 + j) + "\n";
+    for (uint32_t c = 0; c < 4; c++)
+      main += "ds_write_b128 v" + std::to_string(36 + c) + ", v[" + std::to_string(64 + 4 * c) + ":" +
+              std::to_string(67 + 4 * c) + "]\n";
+    main += Z + ":\ns_mov_b64 exec, s[64:65]\ns_mov_b64 exec, 0\n";
+    if (!copy(m, P, false, main, ool)) return false;
+    main += ".L" + P + "end:\n";
+    ool += overlay_routines();
+    if (!ool.empty()) main += "s_branch .Ldone" + m.n + "\n" + ool;
+    out = main;
+    return true;
+  }
+
   // ATOMIC on the stack window at byte p = k + off (static, 4-aligned; 8 bytes read and written,
   // emu.rs:373-437 as oracle/ebpf_oracle.c restates it): orig = the window qword; the 32-bit form
   // works on its low word, the operand's and r0's low words, and adds the high word back after
@@ -1724,6 +1901,10 @@ struct Compiler {
   // moved by the one-byte loads' refills); this load reads it at a - WB and never refills.
   std::string ldx_fixed(uint32_t i, bool one, const std::string& P, std::string& ool,
                         bool var = false, bool loop = false) const {
+    // store mode: the window's bytes at or past LEN are zeros in LDS and may have been stored to,
+    // so only bytes read from the packet past the window are masked by LEN; an access that starts
+    // inside the window and ends past it deoptimizes its lane (its low bytes may be stored ones)
+    const bool smode = stk && stk->any_dyn && !loop;
     const TUop& u = t[i];
     const uint32_t w = one ? 1u : u.width;
     const std::string U = P + "u" + std::to_string(i), next = entry_label(P, next_start(i));
@@ -1772,13 +1953,15 @@ struct Compiler {
       if (w == 8) win += "v_alignbyte_b32 v27, v51, v50, v36\n";
     }
     s += win + ".Lmrg" + U + ":\n";
-    if (var)  // the valid bytes: min(8, LEN - a) (0 when a >= LEN), the rest shifted out
-      s += std::string(w <= 4 ? "v_mov_b32 v27, 0\n" : "") +
-           "v_sub_u32 v46, v31, v36\nv_cmp_lt_u32 vcc, v36, v31\nv_cndmask_b32 v46, 0, v46, vcc\n"
-           "v_min_u32 v46, 8, v46\nv_lshlrev_b32 v46, 3, v46\nv_sub_u32 v46, 64, v46\n"
-           "v_lshlrev_b64 v[26:27], v46, v[26:27]\nv_lshrrev_b64 v[26:27], v46, v[26:27]\n"
-           // (a shift by 64 is one by 0: an access at or past LEN is zeroed by the select)
-           "v_cndmask_b32 v26, 0, v26, vcc\nv_cndmask_b32 v27, 0, v27, vcc\n";
+    // the valid bytes: min(8, LEN - a) (0 when a >= LEN), the rest shifted out
+    const std::string lenmask =
+        std::string(w <= 4 ? "v_mov_b32 v27, 0\n" : "") +
+        "v_sub_u32 v46, v31, v36\nv_cmp_lt_u32 vcc, v36, v31\nv_cndmask_b32 v46, 0, v46, vcc\n"
+        "v_min_u32 v46, 8, v46\nv_lshlrev_b32 v46, 3, v46\nv_sub_u32 v46, 64, v46\n"
+        "v_lshlrev_b64 v[26:27], v46, v[26:27]\nv_lshrrev_b64 v[26:27], v46, v[26:27]\n"
+        // (a shift by 64 is one by 0: an access at or past LEN is zeroed by the select)
+        "v_cndmask_b32 v26, 0, v26, vcc\nv_cndmask_b32 v27, 0, v27, vcc\n";
+    if (var && !smode) s += lenmask;
     if (stk) s += stack_overlay(U, w, ool);
     if (w == 1 || w == 2)
       s += "s_mov_b32 s42, " + std::string(w == 1 ? "0xff" : "0xffff") + "\nv_bfi_b32 " + D0 +
@@ -1790,8 +1973,13 @@ struct Compiler {
     // out of line: lanes whose access ends past the window (in bounds: their bytes come from
     // the packet's dwords that hold a packet byte, zeros past its end)
     std::string far = ".Lfar" + U + ":\n" + (loop ? "v_min_u32 v41, 63, v41\n" : "") + win +
-                      "s_mov_b64 s[66:67], exec\ns_mov_b64 exec, s[68:69]\n"
-                      "v_mov_b32 v26, 0\nv_mov_b32 v27, 0\n"
+                      "s_mov_b64 s[66:67], exec\ns_mov_b64 exec, s[68:69]\n";
+    if (smode)  // straddling the window's end: deoptimize (they leave both lane sets)
+      far += "v_cmp_gt_u32 vcc, 64, v36\ns_and_b64 vcc, vcc, exec\ns_cbranch_vccz .Lnd" + U + "\n"
+             "s_andn2_b64 s[66:67], s[66:67], vcc\ns_andn2_b64 s[68:69], s[68:69], vcc\n"
+             "s_mov_b64 exec, vcc\nv_mov_b32 v30, 0x80\nv_mov_b32 v28, -1\n"
+             "s_mov_b64 exec, s[68:69]\n.Lnd" + U + ":\n";
+    far += "v_mov_b32 v26, 0\nv_mov_b32 v27, 0\n"
                       "v_cmp_lt_u32 vcc, v36, v31\ns_and_b64 exec, s[68:69], vcc\n"
                       "s_cbranch_execz .Lfd" + U + "\n"
                       "v_and_b32 v46, -4, v36\nv_mov_b32 v47, 0\n"
@@ -1811,6 +1999,7 @@ struct Compiler {
     else
       far += "v_alignbyte_b32 v26, v50, v49, v36\n" +
              std::string(w == 8 ? "v_alignbyte_b32 v27, v51, v50, v36\n" : "");
+    if (smode) far += lenmask;  // (exec: the far lanes inside the image and before LEN)
     far += ".Lfd" + U + ":\ns_mov_b64 exec, s[66:67]\ns_branch .Lmrg" + U + "\n";
     ool += far;
     return s;
@@ -2613,6 +2802,19 @@ struct Compiler {
       err = "bad handler id";
       return false;
     }
+    if (stk && stk->any_dyn) {  // store mode: the header window lives in LDS
+      const Uop& o = uops[i];
+      if ((o.op == U_ST || o.op == U_STX) && stk->off[i] == kNoStack) {
+        main += stk->pw[i] != kNoStack ? lds_store_const(i)
+                : stk->dyn[i]          ? lds_store_dyn(i, P)
+                                       : std::string("; unreachable store\n");
+        return true;
+      }
+      if (is_ldxk(id)) {
+        main += ldxk_lds(i);
+        return true;
+      }
+    }
     if (stk && (uops[i].op == U_ST || uops[i].op == U_STX)) {
       // (a store the load-time dataflow never reached has no offset: no lane executes it)
       main += stk->pw[i] != kNoStack    ? pw_store(i)
@@ -2733,6 +2935,7 @@ struct Compiler {
   // ops. The fast copy runs when mem_size covers every such load's end (so none can fault);
   // otherwise the handlers' copy, with its per-load bounds checks.
   bool body(const Marker& m, std::string& out) {
+    if (stk && stk->any_dyn) return body_store(m, out);
     const std::string P = "J" + m.n + "_";
     ovl_tag = m.n;
     overlay_widths = 0;
@@ -3040,7 +3243,7 @@ bool compile_into_template(Compiler& c, Compiler* xc, std::vector<char>& code_ob
     // (stack-window programs: the fixed-slot kernel and the var kernel's stack statement; other
     // programs: every statement but that one)
     if (loop_marker != (xc != nullptr) || (loop_marker && m.deep != deep) ||
-        (c.stk ? !(m.stack || (!loop_marker && m.fixed == "1")) : m.stack))
+        (c.stk ? !(m.stack || (!loop_marker && m.fixed == "1" && !c.stk->any_dyn)) : m.stack))
       b = "s_mov_b64 exec, 0  ; (not this program's kernel)\n";
     else
       ok = xc ? c.body_loop(m, *xc, b) : c.body(m, b);
@@ -3067,7 +3270,8 @@ bool jit_compile(const std::vector<Uop>& uops, const std::vector<TUop>& t,
                  const StackPlan* stk) {
   if (uops.empty() || uops.size() > kJitMaxUops || t.size() < uops.size() ||
       (stk && (stk->k == 0 || stk->k > kStackMax || stk->k % 4 || stk->off.size() != uops.size() ||
-               stk->pw.size() != uops.size()))) {
+               stk->pw.size() != uops.size() ||
+               (stk->any_dyn && stk->dyn.size() != uops.size())))) {
     if (err) *err = "not a tile program";
     return false;
   }
@@ -3082,7 +3286,7 @@ bool jit_compile_loop(const std::vector<Uop>& uops, const std::vector<TUop>& t,
   if (uops.empty() || uops.size() > kJitMaxUops || t.size() < uops.size() ||
       tx.size() < uops.size() ||
       (stk && (stk->k == 0 || stk->k > kStackMax || stk->k % 4 || stk->off.size() != uops.size() ||
-               stk->any_pw))) {
+               stk->any_pw || stk->any_dyn))) {
     if (err) *err = "not a tile program";
     return false;
   }

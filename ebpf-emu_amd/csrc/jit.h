@@ -20,6 +20,9 @@ struct JitFns {
   hipFunction_t var_stack = nullptr;  // stack-window programs, other layouts (ebpf_tile_jit_var_stack)
   hipFunction_t loop_stack = nullptr;  // stack-window loop programs (ebpf_tile_jit_loop_stack)
   hipFunction_t loop_deep = nullptr;  // loop programs with the deep refill prefetch
+  // the program's code exists for the var kernels only (store mode: register-address stores into
+  // the packet, StackPlan::any_dyn), whatever the batch layout
+  bool var_only = false;
 };
 
 // Stack-window programs (memory tier 0.5, host.cpp analyze_stack): every store or atomic writes
@@ -41,7 +44,19 @@ struct StackPlan {
   std::vector<int32_t> pw;   // per micro-op: ST/STX into the packet's header window at a constant
                              // image address [0, kWin - width] (r1 = 0, main.rs:28); else kNoStack
   bool any_pw = false;
+  // store mode: ST/STX through a register whose value is not known at load time (a packet
+  // pointer: a TTL / port / checksum rewrite behind a variable-length header). The packet's header
+  // window then lives in LDS only (every packet load and store goes through it, bytes at or past
+  // LEN zeroed); a lane whose store leaves the window [0, 64) -- or whose load straddles its end
+  // -- deoptimizes: its packet is re-run from the start by the general interpreter (tier 1) after
+  // the compiled launch (host.cpp, the deopt list). Forward programs on the var kernels only.
+  std::vector<char> dyn;     // per micro-op: a register-address ST/STX
+  bool any_dyn = false;
 };
+
+// Status of a lane that leaves the compiled kernel for the general interpreter (never reported:
+// the tile epilogue lists the packet instead of writing its outputs, tile bucket 8).
+constexpr uint32_t kStDeopt = 0x80;
 
 // Compiles a forward-only program of <= kTileMaxUops micro-ops (its tile table `t`, built by
 // build_tile) into the assembly of the two template kernels, then assembles and links it

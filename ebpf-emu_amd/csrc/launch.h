@@ -20,7 +20,7 @@ constexpr int kWinStride = kWin + 4;  // padded per-lane LDS stride: 17 dwords, 
 constexpr int kMaxLdsUops = 4096;     // programs up to this many micro-ops are staged in LDS
 constexpr int kCallDepth = 64;        // EBPF_MAX_CALL_DEPTH
 constexpr int kCounterShards = 64;    // device-atomic counter shards (spread contention)
-// workspace layout: [(unused) | multi-GPU counter sums u64[8] @256 | xdp_md cursor u64 @320 |
+// workspace layout: [deopt count, done u32[2] @0 | (unused) | multi-GPU counter sums u64[8] @256 | xdp_md cursor u64 @320 |
 // length-bin counts u32[16] @384 | bin cursors u32[16] @448, 512 B][shards u64[64][8]][tier-1
 // wave slots, or the length-binned packet order u32[n]]; bin counts/cursors and shards are zero
 // between batches
@@ -28,6 +28,7 @@ constexpr uint64_t kWsBinCountsOff = 384;
 constexpr uint64_t kWsBinCursorOff = 448;
 constexpr int kBinClasses = 16;  // packets are binned by ceil(len / 128), capped
 constexpr int kBinMaxWgs = 1024;  // binning grid cap; per-workgroup class counts follow the order
+constexpr uint64_t kWsDeoptOff = 0;  // u32 count, done: the deopt list (LaunchArgs::deopt)
 constexpr uint64_t kWsXdpCursorOff = 320;  // u64: bytes staged by xdp_stage (reset per batch)
 constexpr uint64_t kWsMultiOff = 256;  // u64[8]: ebpf_run_batch_multi's per-shard counter sums
 constexpr uint64_t kWsShardsOff = 512;
@@ -80,6 +81,14 @@ struct LaunchArgs {
                               //   metadata and then its windows, no metadata prefetch
   uint32_t var_db;            // the compiled var kernels: double-buffered windows, the next tile's
                               //   windows in flight while a tile runs (A/B, EBPFEMU_VAR_DB=1)
+  // store-mode programs (jit.h StackPlan::any_dyn): the deopt list in the workspace -- u32
+  // [count, done] at kWsDeoptOff (zero between batches), idx[n] past the tier-1 slots. The
+  // compiled kernel appends the packet index of every lane that deoptimized (status kStDeopt: no
+  // outputs, not counted); then the general interpreter runs with deopt_pass = 1 over
+  // idx[0 .. count) (outputs at those indices), and its last workgroup zeroes count and done.
+  uint32_t* deopt;
+  uint32_t* deopt_idx;
+  uint32_t deopt_pass;
 };
 
 constexpr int kTraceSlots = 16;

@@ -185,6 +185,59 @@ drop:
     exit
 """
 
+# a NAT / router rewrite (memory store mode): IPv4 TTL decremented in place with the header
+# checksum adjusted (RFC 1624: + 0x0100 with the end-around carry), and TCP/UDP destination ports
+# 53 and 80 redirected to 8053 / 8080 -- the L4 header sits behind the variable-length IPv4
+# header (IHL), so the port store goes through a register (host.cpp analyze_stack: store mode,
+# the header window in LDS). Verdicts: XDP_TX for redirected frames, PASS otherwise, DROP at TTL <= 1
+# or IHL < 5. Same frames as the 5-tuple.
+NAT_REWRITE = """
+    mov r0, 2                 # XDP_PASS
+    jlt r2, 34, out
+    ldxh r3, [r1+12]          # EtherType (a little-endian load of big-endian bytes)
+    jne r3, 0x0008, out       # IPv4 only
+    ldxb r4, [r1+22]          # TTL
+    jle r4, 1, drop
+    sub r4, 1
+    stxb [r1+22], r4          # TTL - 1, in place
+    ldxh r5, [r1+24]          # header checksum
+    be16 r5
+    add r5, 0x100             # RFC 1624 for the TTL byte (the high byte of its word)
+    mov r6, r5
+    rsh r6, 16
+    and r5, 0xffff
+    add r5, r6
+    be16 r5
+    stxh [r1+24], r5
+    ldxb r6, [r1+14]          # version / IHL
+    and r6, 15
+    jlt r6, 5, drop           # malformed
+    lsh r6, 2
+    mov r7, r1
+    add r7, r6
+    add r7, 14                # the L4 header, behind the IPv4 options
+    ldxb r8, [r1+23]          # protocol
+    jeq r8, 6, l4
+    jne r8, 17, out
+l4:
+    ldxh r9, [r7+2]           # destination port
+    be16 r9
+    jeq r9, 53, redirect
+    jne r9, 80, out
+redirect:
+    add r9, 8000              # 53 -> 8053, 80 -> 8080
+    be16 r9
+    stxh [r7+2], r9           # a register-address store into the packet
+    ldxh r3, [r7+2]           # read back through the pointer
+    jne r3, r9, drop          # (never taken)
+    mov r0, 3                 # XDP_TX
+    exit
+drop:
+    mov r0, 1
+out:
+    exit
+"""
+
 # a firewall of ~100 instructions (past the tile interpreter's 62 micro-ops: compiled by the
 # forward-program compiler instead of interpreted by dag_kernel): 802.1Q, IPv4 sanity (version,
 # IHL, TTL, fragments), source and destination address rules, TCP flag and port rules, UDP
@@ -403,7 +456,7 @@ l4_out:
 PROGRAMS = {"drop": DROP_ALL, "5tuple": FIVE_TUPLE, "checksum": CHECKSUM,
             "5tuple_stack": FIVE_TUPLE_STACK, "mac_swap_tx": MAC_SWAP_TX, "acl": ACL,
             "5tuple_xdp": FIVE_TUPLE_XDP, "checksum_stack": CHECKSUM_STACK,
-            "5tuple_call": FIVE_TUPLE_CALL}
+            "5tuple_call": FIVE_TUPLE_CALL, "nat": NAT_REWRITE}
 
 
 def program(name: str) -> bytes:

@@ -306,3 +306,70 @@ def gen_stack_loop_program(rng: random.Random, k: int = 32) -> bytes:
     words.append(encode(0xAF, 0, 3, 0, 0))                     # xor r0, r3
     words.append(encode(0x95))
     return b"".join(words)
+
+
+def gen_store_program(rng: random.Random, n: int | None = None) -> bytes:
+    """Store-mode programs (register-address stores into the packet, host.cpp analyze_stack
+    StackPlan::any_dyn; emu.rs:354-372): r8 = r1 + (a packet byte & m) + c -- a packet pointer the
+    load-time dataflow cannot resolve -- and r7 = r8 + c2 (sometimes far past the image: faults);
+    then ST/STX of every width through r8 / r7 (mostly inside the 64-byte header window, some
+    past it or straddling its end: those lanes deoptimize to the general interpreter), loads
+    through the same pointers (reading stored bytes back), constant-address loads and stores of
+    the window, stack stores / loads / atomics at r10 - 8 .. r10 - 1, ALU and forward jumps; the
+    registers folded into r0 at the end."""
+    n = n or rng.randrange(8, 40)
+    words: list[bytes] = [
+        encode(0x71, 8, 1, 0, 0) if rng.random() < 0.2 else encode(0x71, 8, 1, rng.randrange(0, 64)),
+        encode(0x57, 8, 0, 0, rng.choice([7, 15, 31, 63, 127])),      # and r8, m
+        encode(0x07, 8, 0, 0, rng.randrange(0, 48)),                   # add r8, c
+        encode(0x0F, 8, 1, 0, 0),                                      # add r8, r1
+        encode(0xBF, 7, 8, 0, 0),                                      # mov r7, r8
+        encode(0x07, 7, 0, 0, rng.choice([0, 2, 4, 8, 20, 40, 60, 1000, 1019, 2000])),
+    ]
+    regs = [0, 2, 3, 4, 5, 6]
+    while len(words) < n:
+        q = rng.random()
+        size = rng.choice([0x00, 0x08, 0x10, 0x18])
+        w = {0x00: 4, 0x08: 2, 0x10: 1, 0x18: 8}[size]
+        dst, src = rng.choice(regs), rng.randrange(10)
+        ptr = rng.choice([8, 8, 7])
+        if q < 0.30:  # store through a pointer
+            off = rng.choice([rng.randrange(-4, 64), rng.randrange(-4, 24), 60, 62, 70])
+            if rng.random() < 0.35:
+                words.append(encode(0x62 | size, ptr, 0, off, _imm(rng)))
+            else:
+                words.append(encode(0x63 | size, ptr, src, off))
+        elif q < 0.48:  # load through a pointer
+            words.append(encode(0x61 | size, dst, ptr, rng.choice([rng.randrange(-4, 64), 58, 61, 66])))
+        elif q < 0.56:  # constant-address store into the window
+            off = rng.randrange(0, 64 - w + 1)
+            if rng.random() < 0.4:
+                words.append(encode(0x62 | size, 1, 0, off, _imm(rng)))
+            else:
+                words.append(encode(0x63 | size, 1, src, off))
+        elif q < 0.66:  # constant-address load (inside the window, or past it)
+            off = rng.choice([rng.randrange(0, 64 - w + 1), rng.randrange(64, 90)])
+            words.append(encode(0x61 | size, dst, 1, off))
+        elif q < 0.72:  # the stack
+            d = -rng.randrange(w, 9)
+            if rng.random() < 0.5:
+                words.append(encode(0x63 | size, 10, src, d))
+            elif rng.random() < 0.5:
+                words.append(encode(0x61 | size, dst, 10, d))
+            else:
+                words.append(encode(0xDB, 10, src, -8, 0x00))            # lock add [r10-8]
+        elif q < 0.86:  # ALU (never on r1, r7 .. r10)
+            cls = rng.choice([0x04, 0x07])
+            op = rng.choice([0, 1, 2, 4, 5, 6, 7, 10, 11, 12])
+            words.append(encode((op << 4) | rng.choice([0, 0x08]) | cls, dst, src, 0, _imm(rng)))
+        elif q < 0.97:  # forward jumps
+            cls = rng.choice([0x05, 0x06])
+            op = rng.choice([0, 1, 2, 3, 4, 5, 6, 7, 10, 11, 12, 13])
+            off = rng.randrange(0, max(1, n - len(words)) + 1)
+            words.append(encode((op << 4) | rng.choice([0, 0x08]) | cls, dst, src, off, _imm(rng)))
+        else:
+            words.append(encode(0x95))
+    for r in (3, 4, 5, 6):
+        words.append(encode(0xAF, 0, r, 0, 0))                            # xor r0, r
+    words.append(encode(0x95))
+    return b"".join(words)

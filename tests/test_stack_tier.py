@@ -35,8 +35,10 @@ DIRECTED = [
     ("stxw [r1+8], r2\nmov r3, r2\nldxb r0, [r3+0]\nexit", 0),    # + a register-address load
     ("stxw [r1+8], r2\nldxw r0, [r1+62]\nexit", 0),               # + a load across byte 64
     ("stxw [r1+8], r2\nldxw r0, [r10-8]\nexit", 0),               # + a load outside the window
-    ("mov r3, r2\nstxw [r3+0], r2\nexit", 0),                     # through an unknown pointer
-    ("jeq r2, 60, +2\nmov r3, r10\nja +1\nmov r3, r1\nstxb [r3-4], r0\nexit", 0),  # join differs
+    ("mov r3, r2\nstxw [r3+0], r2\nexit", 4),                     # through an unknown pointer:
+                                                                   # store mode (test_store_mode.py)
+    ("jeq r2, 60, +2\nmov r3, r10\nja +1\nmov r3, r1\nstxb [r3-4], r0\nexit", 4),  # join differs:
+                                                                   # store mode
     ("jeq r2, 60, +2\nmov r3, r10\nja +1\nmov r3, r10\nstxb [r3-4], r0\nexit", 4),  # join agrees
     ("stxdw [r10-8], r1\nldxw r0, [r10-10]\nexit", 0),             # a load straddling the edge
     ("stxdw [r10-8], r1\nldxw r0, [r10-16]\nexit", 8),             # a load below the window
@@ -47,7 +49,7 @@ DIRECTED = [
     ("stxdw [r10-8], r1\ncall 0\nexit", 8),                        # calls (flatten_calls)
     ("mov r0, 0\nstxb [r10-1], r0\nadd r0, 1\njlt r0, 5, -3\nexit", 4),  # a loop (loop kernel)
     ("mov r0, 0\nstxb [r1+3], r0\nadd r0, 1\njlt r0, 5, -3\nexit", 0),  # + packet store
-    ("mov32 r2, r10\nstxb [r2-1], r0\nexit", 0),                   # a truncated pointer
+    ("mov32 r2, r10\nstxb [r2-1], r0\nexit", 4),                   # a truncated pointer: store mode
     ("mov r0, 1\nexit", 0),                                        # no store: tier 0
 ]
 

@@ -1,0 +1,179 @@
+"""Store mode: register-address stores into the packet on the compiled kernel (host.cpp
+analyze_stack StackPlan::any_dyn, jit.cpp body_store / lds_store_dyn; reference emu.rs:354-372,
+mmu.rs:23-30).
+
+A store through a register whose value the load-time dataflow cannot resolve -- a TTL, port or
+checksum rewrite behind the variable-length IPv4 header -- used to send the whole program to the
+general interpreter's tier 1 (per-packet images in scratch). In store mode the program runs on the
+var kernel's stack statement with the lane's 64-byte header window in LDS as the image's bytes
+[0, 64): every packet load and store goes through it. A lane whose store leaves the window (or
+whose load straddles its end) deoptimizes: the compiled kernel lists its packet, and the general
+interpreter re-runs that packet from the start after the launch (the deopt pass), writing its
+outputs and counters. Programs are pure functions of the packet image, so the results are the
+reference's either way.
+
+CPU: which programs are store mode, and every one of them compiles and assembles.
+GPU: compiled == general interpreter == oracle, every output (status, r0, registers, verdicts,
+counters, production verdicts), over random store programs on fixed slots, offsets + lens with
+short packets, stride + lens and xdp_md batches -- with lanes that deoptimize, fault, or store
+past the packet's length -- and the NAT rewrite workload (workloads.NAT_REWRITE) with packets whose
+IPv4 options push the port past the window.
+"""
+import random
+import struct
+import zlib
+
+import numpy as np
+import pytest
+
+from fuzzgen import gen_store_program
+
+STEPS = 20000
+
+
+def test_store_mode_programs_compile(product_lib):
+    from ebpf_emu import Program
+    from ebpf_emu import workloads as W
+
+    p = Program(W.program("nat"))
+    assert p.tier == 1 and p.stack_window == 4 and p.compile()
+    assert "store mode" in p.jit_asm(1)
+    p.close()
+    rng = random.Random(77)
+    n = 0
+    for _ in range(120):
+        img = gen_store_program(rng)
+        try:
+            p = Program(img)
+        except Exception:
+            continue
+        if p.stack_window:
+            assert p.compile(), img.hex()
+            n += 1
+        p.close()
+    assert n >= 80, n
+
+
+def _nat_packets(rng, n, long_options=0.2):
+    """Ethernet/IPv4/TCP-UDP frames: TTL 0..255, IHL 5..15 (IHL >= 13 puts the port past the
+    64-byte window: those lanes deoptimize), ports 53 / 80 / random, lengths 34..200."""
+    out = []
+    for _ in range(n):
+        ihl = rng.choice([5, 5, 5, 6]) if rng.random() > long_options else rng.randrange(7, 16)
+        plen = max(34, 14 + 4 * ihl + rng.choice([0, 2, 4, 8, 20])) + rng.randrange(0, 60)
+        b = bytearray(rng.getrandbits(8) for _ in range(plen))
+        b[12:14] = b"\x08\x00" if rng.random() < 0.9 else b"\x86\xdd"
+        b[14] = 0x40 | ihl
+        b[22] = rng.choice([0, 1, 2, 64, 255])
+        b[23] = rng.choice([6, 17, 1])
+        l4 = 14 + 4 * ihl
+        if l4 + 4 <= plen:
+            b[l4 + 2:l4 + 4] = struct.pack(">H", rng.choice([53, 80, 80, 443, rng.randrange(65536)]))
+        out.append(bytes(b))
+    return out
+
+
+def _check(oracle_mod, img, pkts, got, ref, xdp, tag):
+    from test_stack_tier import _images_of, _vs_oracle
+
+    ok = got["status"] != 7  # (ST_BADPKT lanes have no registers: main.rs:20-21 panics)
+    for key in ("status", "verdict", "counters", "prod_verdict"):
+        assert np.array_equal(got[key], ref[key]), (key, tag, img.hex())
+    for key in ("r0", "regs"):
+        assert np.array_equal(got[key][ok], ref[key][ok]), (key, tag, img.hex())
+    _vs_oracle(oracle_mod, img, _images_of(pkts, xdp), got, tag=tag)
+
+
+LAYOUTS = ["fixed64", "fixed128", "offsets16", "offsets_mis3", "stride_lens", "xdp_offsets"]
+
+
+def _run_layout(img, pkts, dev, layout, generic=False):
+    from test_stack_tier import VAR_LAYOUTS, _fixed_frames, _run, _run_var
+
+    if layout.startswith("fixed"):
+        stride = int(layout[5:])
+        pk = [p[:stride].ljust(stride, b"\0") for p in pkts]
+        frames = _fixed_frames(pk, stride, dev)
+        return _run(img, frames, len(pk), dev, generic=generic, stride=stride), False, pk
+    out, xdp = _run_var(img, pkts, dev, VAR_LAYOUTS[layout], generic=generic)
+    return out, xdp, pkts
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layout", LAYOUTS)
+def test_store_mode_fuzz(cuda, oracle_mod, layout):
+    """Random store-mode programs: the compiled var kernel (+ its deopt pass) == the general
+    interpreter == the oracle on every output; the route asserted."""
+    from ebpf_emu import Program, _lib
+    from test_stack_tier import _var_packets
+
+    rng = random.Random(zlib.crc32(b"store" + layout.encode()))
+    n_run = 0
+    for it in range(28):
+        img = gen_store_program(rng)
+        try:
+            oracle_mod.Program(img)
+        except oracle_mod.OracleDecodeError:
+            continue
+        p = Program(img)
+        k = p.stack_window
+        p.close()
+        if not k:
+            continue
+        pkts = _var_packets(rng, rng.choice([64, 100, 130]))
+        got, xdp, pk = _run_layout(img, pkts, cuda, layout)
+        assert got["kernel"] == _lib.EBPF_KERNEL_JIT_VAR_STACK, (layout, img.hex())
+        ref, _, _ = _run_layout(img, pkts, cuda, layout, generic=True)
+        assert ref["kernel"] == _lib.EBPF_KERNEL_GENERAL_T1
+        _check(oracle_mod, img, pk, got, ref, xdp, f"{layout} it {it}")
+        n_run += 1
+    assert n_run >= 15, n_run
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layout", ["fixed128", "offsets_mis3", "xdp_offsets"])
+def test_nat_rewrite_vs_oracle(cuda, oracle_mod, layout):
+    """The NAT rewrite workload over frames with IPv4 options (ports past the window: deopt),
+    TTLs that drop, short and long frames: compiled == general interpreter == oracle."""
+    from ebpf_emu import _lib
+    from ebpf_emu import workloads as W
+
+    img = W.program("nat")
+    rng = random.Random(5150 + len(layout))
+    pkts = _nat_packets(rng, 3000)
+    got, xdp, pk = _run_layout(img, pkts, cuda, layout)
+    assert got["kernel"] == _lib.EBPF_KERNEL_JIT_VAR_STACK
+    ref, _, _ = _run_layout(img, pkts, cuda, layout, generic=True)
+    _check(oracle_mod, img, pk, got, ref, xdp, f"nat {layout}")
+    # the workload exercised every path: TX (redirected), PASS, DROP
+    v = got["verdict"]
+    assert (v == 3).sum() > 50 and (v == 2).sum() > 50 and (v == 1).sum() > 50
+
+
+@pytest.mark.gpu
+def test_nat_workload_full_size(cuda, oracle_mod):
+    """The bench's NAT batch (the 5-tuple frames, 1 Mi x 64 B fixed slots, chunk 0 of the pinned
+    pool) against the oracle: verdict counters and retired instructions, then the same batch with
+    every 16th frame's IHL set to 15 (the port past the window: 1/16 of the lanes deoptimize)."""
+    import torch
+
+    from ebpf_emu import Program
+    from ebpf_emu import workloads as W
+    from ebpf_emu import dist as D
+
+    img = W.program("nat")
+    n = 1 << 20
+    for deopt in (False, True):
+        buf = D.chunk_frames(0, n).copy()
+        if deopt:
+            v = buf.reshape(n, 64)
+            v[::16, 14] = (v[::16, 14] & 0xF0) | 0x0F
+        prog = Program(img)
+        cnt = torch.zeros(8, dtype=torch.int64, device=cuda)
+        res = prog.run(torch.from_numpy(buf).to(cuda), n=n, stride=64, counters=cnt)
+        torch.cuda.synchronize()
+        r0, st, ocnt = oracle_mod.Program(img).run_batch(buf, n, stride=64, threads=8)
+        verdict = np.where(st != 0, 0xFF, np.where(r0 < 5, r0, 0xFE)).astype(np.uint8)
+        assert np.array_equal(res.verdict.cpu().numpy(), verdict), deopt
+        assert list(cnt.cpu().numpy().view(np.uint64)) == list(ocnt), deopt
+        prog.close()
