@@ -58,6 +58,11 @@ CONFIGS = {
     # the 5-tuple with its L4 decision in a local function (CALL / EXIT flattened at load time onto
     # the compiled kernel; --generic: the general interpreter's frame stack), same verdicts
     "call": (2, "IPv4 5-tuple with the L4 decision as a local call (35 insns) over 1Mi x 64B frames"),
+    # a NAT / router rewrite: TTL - 1 with the header checksum, ports 53/80 redirected through the
+    # L4 header pointer behind the IPv4 options (a register-address store: store mode, the var
+    # kernel with the header window in LDS; --generic: the general interpreter's tier 1)
+    "nat": (2, "IPv4 NAT rewrite: TTL - 1 + checksum, port redirect through the L4 pointer (40 insns) "
+               "over 1Mi x 64B frames"),
 }
 PROGRAM_OF = {"stack": "5tuple_stack", "tier1": "mac_swap_tx", "xdp": "5tuple_xdp",
               "call": "5tuple_call"}

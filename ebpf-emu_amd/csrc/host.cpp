@@ -259,6 +259,16 @@ struct ebpf_prog {
   // loads through rD are constant-address loads (fold_const_loads xdp); variant 3 when it
   // differs from tuopsk
   std::vector<TUop> tuopsk_xdp;
+  // stack-slot promotion (promote_slots): a stack-window loop program whose window holds whole
+  // 8-byte slots becomes a tier-0 loop program with each slot in a free register (variant 4 of
+  // the compiled program, the loop kernels' full byte-loop machinery); its lanes whose packet
+  // reaches the window (LEN > r10 - k) deoptimize to the general interpreter
+  std::vector<Uop> puops;
+  std::vector<TUop> pltuops, pltuopsx;
+  TUop* dev_pltuops[kMaxDevices] = {};
+  TUop* dev_pltuopsx[kMaxDevices] = {};
+  uint32_t pguard_k = 0;
+  bool pjit_deep = false;  // variant 4 compiled into ebpf_tile_jit_loop_deep
 };
 
 // Diagnostics: EBPFEMU_TRACE=1 gives the compiled fixed-slot kernel a per-device stamp buffer
@@ -277,6 +287,13 @@ static const bool g_no_jit = [] {
   return e && e[0] == '1';
 }();
 
+// EBPFEMU_NO_PROMOTE=1 (A/B): stack-window loop programs keep their slots in the stack window
+// (the loop kernel's stack variant) instead of promote_slots' registers.
+static const bool g_no_promote = [] {
+  const char* e = getenv("EBPFEMU_NO_PROMOTE");
+  return e && e[0] == '1';
+}();
+
 // EBPFEMU_TEST_FAIL_STACK_JIT=1 (tests): every stack-window program's compilation fails, so
 // that the fallback to the general interpreter is exercised.
 static const bool g_fail_stack_jit = [] {
@@ -290,6 +307,7 @@ static int jit_compile_locked(ebpf_prog* p) {
     p->jit_has[0] = p->jit_has[1] = !p->tuops.empty() && !p->tuopsk.empty();
     p->jit_has[2] = !p->ltuops.empty() && !p->ltuopsx.empty();
     p->jit_has[3] = !p->tuopsk_xdp.empty() && !p->stack.k;
+    p->jit_has[4] = !p->pltuops.empty() && !p->pltuopsx.empty();
     if (p->stack.k) p->jit_has[1] = !p->tuopsk.empty();  // (the main.rs layout only)
     if (g_no_jit || (!p->jit_has[0] && !p->jit_has[1] && !p->jit_has[2])) {
       p->jit_state = 2;
@@ -297,6 +315,17 @@ static int jit_compile_locked(ebpf_prog* p) {
       p->jit_state = 1;
       for (int v = 0; v < kJitVariants && p->jit_state == 1; v++) {
         if (!p->jit_has[v]) continue;
+        if (v == 4) {  // the promoted program: dropped (the stack loop kernel stays) if it fails
+          if (!jit_compile_loop(p->puops, p->pltuops, p->pltuopsx, p->jit_co[4], &p->jit_err,
+                                &p->jit_asm[4], nullptr, &p->pjit_deep, p->pguard_k)) {
+            p->jit_has[4] = false;
+            p->jit_co[4].clear();
+            p->puops.clear();
+            p->pltuops.clear();
+            p->pltuopsx.clear();
+          }
+          continue;
+        }
         const bool ok = !(g_fail_stack_jit && p->stack.k) &&
                         (v == 2 ? jit_compile_loop(p->xuops, p->ltuops, p->ltuopsx, p->jit_co[v],
                                                   &p->jit_err, &p->jit_asm[v],
@@ -316,6 +345,10 @@ static int jit_compile_locked(ebpf_prog* p) {
           p->tuopsk.clear();
           p->ltuops.clear();
           p->ltuopsx.clear();
+          p->jit_has[4] = false;  // (the promoted program needs the stack plan's launch checks)
+          p->puops.clear();
+          p->pltuops.clear();
+          p->pltuopsx.clear();
           p->jit_has[1] = p->jit_has[2] = false;
           p->jit_co[1].clear();
           p->jit_co[2].clear();
@@ -1030,6 +1063,115 @@ static StackAnalysis analyze_stack(const std::vector<Uop>& uops) {
   return res;
 }
 
+// Stack-slot promotion: a stack-window loop program (analyze_stack's plan, no packet stores, no
+// atomics) whose window accesses are all whole 8-byte slots -- a spilled accumulator, as
+// compiled C keeps one (`ldxdw rT, [r10-8]; add rT, rD; stxdw [r10-8], rT`) -- becomes a tier-0
+// loop program with each slot in a register the program never names: `stdw [slot], imm` ->
+// `lddw rS, imm`, `stxdw [slot], rX` -> `mov rS, rX`, `ldxdw rX, [slot]` -> `mov rX, rS`. One
+// micro-op each, so steps, faults and budgets are the reference's (emu.rs:354-372 on a slot the
+// loads then read back, emu.rs:341-349). The accumulator triple `mov rT, rS; add rT, rD;
+// mov rS, rT` with rT dead after it becomes `nop; add rS, rD; nop` (the loop kernel's byte-sum
+// idiom then applies, jit.cpp counted_group). It is exact for the lanes whose packet loads
+// cannot read the slots' bytes (the slots start as the image's zeros and only the slots hold the
+// stores): the compiled code requires every packet load proven inside the packet (jit.cpp
+// all_loads_proven) and deoptimizes lanes with LEN > r10 - k (promo_guard); the final registers
+// and image differ (the slot registers, the slots' bytes), so batches that ask for them, or set
+// init_regs, run the stack loop kernel instead (promo_ok). Returns false if not applicable.
+static bool promote_slots(const std::vector<Uop>& xu, const StackPlan& plan, std::vector<Uop>& out) {
+  const uint32_t n = (uint32_t)xu.size();
+  if (!plan.k || plan.any_pw || plan.any_dyn || plan.off.size() != n) return false;
+  std::vector<int32_t> slots;
+  uint32_t used = 1u << 2 | 1u << 10 | 1u;  // r2 = LEN and r10 never; r0 always named
+  for (uint32_t i = 0; i < n; i++) {
+    const Uop& u = xu[i];
+    used |= 1u << (u.dst & 15) | 1u << (u.src & 15);
+    if (u.op == U_ATOMIC || u.op == U_CALL) return false;
+    const bool acc = u.op == U_ST || u.op == U_STX || (u.op == U_LDX && plan.off[i] != kNoStack);
+    if (!acc) continue;
+    if (plan.off[i] == kNoStack || u.aux != 8) return false;
+    if (std::find(slots.begin(), slots.end(), plan.off[i]) == slots.end()) slots.push_back(plan.off[i]);
+  }
+  std::sort(slots.begin(), slots.end());
+  for (size_t j = 1; j < slots.size(); j++)
+    if (slots[j] - slots[j - 1] < 8) return false;  // (partly overlapping slots)
+  std::vector<uint8_t> reg(slots.size());
+  uint32_t r = 9;
+  for (size_t j = 0; j < slots.size(); j++) {
+    while (r >= 1 && ((used >> r) & 1)) r--;
+    if (r < 1) return false;  // no free register left
+    reg[j] = (uint8_t)r--;
+  }
+  auto slot_reg = [&](int32_t off) {
+    return reg[std::find(slots.begin(), slots.end(), off) - slots.begin()];
+  };
+  out = xu;
+  for (uint32_t i = 0; i < n; i++) {
+    const Uop& u = xu[i];
+    const bool acc = u.op == U_ST || u.op == U_STX || (u.op == U_LDX && plan.off[i] != kNoStack);
+    if (!acc) continue;
+    Uop v{};
+    if (u.op == U_ST) {
+      v.op = U_LDIMM, v.dst = slot_reg(plan.off[i]), v.k = u.k;
+    } else if (u.op == U_STX) {
+      v.op = U_MOV64, v.dst = slot_reg(plan.off[i]), v.src = u.src, v.aux = F_SRC;
+    } else {
+      v.op = U_MOV64, v.dst = u.dst, v.src = slot_reg(plan.off[i]), v.aux = F_SRC;
+    }
+    out[i] = v;
+  }
+  // the accumulator triple, inside one basic block, rT dead after it
+  std::vector<char> tgt(n + 1, 0);
+  for (uint32_t i = 0; i < n; i++)
+    if (out[i].op >= U_JA && out[i].op <= U_JLE32 && (uint32_t)out[i].x <= n) tgt[(uint32_t)out[i].x] = 1;
+  // liveness of r0..r10 (r0 live at exits and faults; conservative for calls: none here)
+  std::vector<uint32_t> lin(n + 1, 0);
+  lin[n] = 1u;
+  auto rw = [&](const Uop& u, uint32_t& rd, uint32_t& wr) {
+    const uint32_t d = 1u << u.dst, sr = (u.aux & F_SRC) ? 1u << u.src : 0u;
+    rd = wr = 0;
+    if (u.op <= U_ARSH32) { wr = d; rd = sr | ((u.op == U_MOV64 || u.op == U_MOV32) ? 0u : d); }
+    else if (u.op <= U_BSWAP64) { rd = wr = d; }
+    else if (u.op >= U_JA && u.op <= U_JLE32) { rd = u.op == U_JA ? 0u : (d | sr); }
+    else if (u.op == U_LDIMM) { wr = d; }
+    else if (u.op == U_LDX) { rd = d | (1u << u.src); wr = d; }
+    else if (u.op == U_EXIT || u.op == U_FAULT) { rd = 1u; }
+    else { rd = 0x7ffu; }  // (anything else: everything live)
+  };
+  for (bool ch = true; ch;) {
+    ch = false;
+    for (uint32_t i = n; i-- > 0;) {
+      const Uop& u = out[i];
+      uint32_t rd, wr, o = 0;
+      rw(u, rd, wr);
+      if (u.op == U_EXIT || u.op == U_FAULT) o = 0;
+      else if (u.op >= U_JA && u.op <= U_JLE32) {
+        o = lin[std::min<uint32_t>((uint32_t)u.x, n)];
+        if (u.op != U_JA) o |= lin[i + 1];
+      } else o = lin[i + 1];
+      const uint32_t v = rd | (o & ~wr);
+      if (v != lin[i]) lin[i] = v, ch = true;
+    }
+  }
+  for (uint32_t i = 0; i + 2 < n; i++) {
+    const Uop &a = out[i], &b = out[i + 1], &c = out[i + 2];
+    if (a.op != U_MOV64 || !(a.aux & F_SRC) || b.op != U_ADD64 || !(b.aux & F_SRC) ||
+        c.op != U_MOV64 || !(c.aux & F_SRC))
+      continue;
+    const uint32_t rT = a.dst, rS = a.src, rD = b.src;
+    if (std::find(reg.begin(), reg.end(), (uint8_t)rS) == reg.end() || rT == rS || b.dst != rT ||
+        rD == rT || rD == rS || c.dst != rS || c.src != rT || tgt[i + 1] || tgt[i + 2] ||
+        ((lin[i + 3] >> rT) & 1))
+      continue;
+    Uop nop{};
+    nop.op = U_NOP, nop.dst = (uint8_t)rS;
+    Uop add = b;
+    add.dst = (uint8_t)rS;
+    out[i] = nop, out[i + 1] = add, out[i + 2] = nop;
+    i += 2;
+  }
+  return true;
+}
+
 extern "C" {
 
 void ebpf_batch_init(ebpf_batch* b) {
@@ -1116,6 +1258,15 @@ int ebpf_prog_load(const uint8_t* code, size_t nbytes, ebpf_prog** out, size_t* 
         const std::vector<DUop> d = build_dag(xu);
         p->ltuops = build_tile(xu, d, false, true);
         p->ltuopsx = build_tile(xu, d, true, true);
+        // loops with whole-slot accumulators: also the promoted tier-0 program (variant 4)
+        std::vector<Uop> pu;
+        if (!forward && !g_no_promote && promote_slots(xu, sa.plan, pu)) {
+          const std::vector<DUop> pd = build_dag(pu);
+          p->pltuops = build_tile(pu, pd);
+          p->pltuopsx = build_tile(pu, pd, true);
+          p->puops = std::move(pu);
+          p->pguard_k = sa.plan.k;
+        }
       }
       p->stack = std::move(sa.plan);
     }
@@ -1147,6 +1298,8 @@ void ebpf_prog_free(ebpf_prog* p) {
       if (p->dev_tuopsk[d]) hipFree(p->dev_tuopsk[d]);
       if (p->dev_ltuops[d]) hipFree(p->dev_ltuops[d]);
       if (p->dev_ltuopsx[d]) hipFree(p->dev_ltuopsx[d]);
+      if (p->dev_pltuops[d]) hipFree(p->dev_pltuops[d]);
+      if (p->dev_pltuopsx[d]) hipFree(p->dev_pltuopsx[d]);
     }
     for (int v = 0; v < kJitVariants; v++)
       if (p->jit_mod[d][v]) {
@@ -1248,12 +1401,20 @@ int ebpf_prog_upload(ebpf_prog* p, int device) {
       if (p->jit_has[v]) {
         if (!jit_load(p->jit_co[v], &p->jit_mod[device][v], &p->jit_fn[device][v]))
           rc = EBPF_EHIP;
-        else if (v == 2 && p->jit_deep)  // (the code is in the deep-prefetch loop kernel)
-          p->jit_fn[device][v].loop = p->jit_fn[device][v].loop_deep;
+        else if ((v == 2 && p->jit_deep) || (v == 4 && p->pjit_deep))  // (the code is in the
+          p->jit_fn[device][v].loop = p->jit_fn[device][v].loop_deep;     // deep-prefetch kernel)
         p->jit_fn[device][v].var_only = p->stack.any_dyn;
       }
   }
+  TUop* tp = nullptr;
+  TUop* tpx = nullptr;
+  if (rc == EBPF_OK && p->jit_has[4]) {  // (the promoted tables: known once compiled)
+    putt(p->pltuops, &tp);
+    putt(p->pltuopsx, &tpx);
+  }
   if (rc == EBPF_OK) {
+    p->dev_pltuops[device] = tp;
+    p->dev_pltuopsx[device] = tpx;
     p->dev_uops[device] = d;
     p->dev_duops[device] = dd;
     p->dev_duopsk[device] = ddk;
@@ -1262,7 +1423,8 @@ int ebpf_prog_upload(ebpf_prog* p, int device) {
     p->dev_ltuops[device] = tl;
     p->dev_ltuopsx[device] = tlx;
   } else {
-    for (void* q : {(void*)d, (void*)dd, (void*)ddk, (void*)td, (void*)tdk, (void*)tl, (void*)tlx})
+    for (void* q : {(void*)d, (void*)dd, (void*)ddk, (void*)td, (void*)tdk, (void*)tl, (void*)tlx,
+                    (void*)tp, (void*)tpx})
       if (q) hipFree(q);
   }
   hipSetDevice(cur);
@@ -1271,14 +1433,14 @@ int ebpf_prog_upload(ebpf_prog* p, int device) {
 
 // Whether a loop-mode batch runs in length-binned order (an xdp_md batch is staged as offsets +
 // lens).
-static bool use_binning(const ebpf_prog* p, const ebpf_batch* b) {
+static bool use_binning(const ebpf_prog* p, const ebpf_batch* b, bool promo = false) {
   const bool ol = (b->offsets && b->lens) || (b->flags & EBPF_BATCH_XDP_MD);
   if (p->ltuops.empty() || !ol || (b->flags & EBPF_BATCH_GENERIC) || b->init_fp_len) return false;
   // (a program on the deep loop kernel -- its long byte sums cooperative, coop_sum_compact -- runs
   // in batch order: a tile's short packets need no binning away from its long ones, and spreading
   // the long packets over every tile balances the waves; config 5, A/B on one box: 169.7 us
   // unbinned vs 191.3 binned per 1 Mi batch)
-  if (p->jit_deep && g_bin < 0) return false;
+  if ((promo ? p->pjit_deep : p->jit_deep) && g_bin < 0) return false;
   return g_bin >= 0 ? g_bin == 1 : b->n >= kBinMinPackets;
 }
 
@@ -1355,6 +1517,16 @@ static bool stack_loop_ok(const ebpf_prog* p, const ebpf_batch* b, const ebpf_ba
   return stack_common_ok(p, b, out) && p->jit_mod[device][2] && !g_no_loop && stack_var_ok(p, b);
 }
 
+// The stack-slot promoted program (variant 4, promote_slots) on this batch: the production
+// outputs only (verdict, r0, status, counters: the final registers and image differ) and the
+// main.rs layout; the window's launch checks of the stack kernels (stack_common_ok).
+static bool promo_ok(const ebpf_prog* p, const ebpf_batch* b, const ebpf_batch_out* out,
+                     int device) {
+  if (p->puops.empty() || !p->jit_mod[device][4] || !p->dev_pltuops[device]) return false;
+  if (!stack_common_ok(p, b, out) || out->regs || out->fp || out->fp_len) return false;
+  return !g_no_loop;
+}
+
 // The kernel kind of a batch (uploaded program): dag_kernel needs no step budget (a lane of a
 // forward-only program retires <= n_uops steps); the tile kernel in loop mode runs loops, or a
 // step budget that can bind (exact budget); a stack-window batch runs the compiled stack kernels
@@ -1368,6 +1540,7 @@ static int batch_kind(const ebpf_prog* p, const ebpf_batch* b, const ebpf_batch_
   *stk = false;
   if (p->stack.k && !generic) {
     if (stack_launch_ok(p, b, out, device)) return *stk = true, kKindDag;
+    if (promo_ok(p, b, out, device)) return kKindLoop;  // (stk false: the promoted program)
     if (stack_loop_ok(p, b, out, device)) return *stk = true, kKindLoop;
     return batch_tier(p, b);
   }
@@ -1381,6 +1554,9 @@ static int batch_kind(const ebpf_prog* p, const ebpf_batch* b, const ebpf_batch_
 // The compiled program, where it applies (tile-kernel programs; same tables, same results).
 static const JitFns* batch_jit(ebpf_prog* p, const ebpf_batch* b, int kind, bool stk, int device) {
   if (stk) return &p->jit_fn[device][kind == kKindLoop ? 2 : 1];
+  // (batch_kind routes a stack-window program to the loop kind without the stack flag only for
+  // its promoted program)
+  if (kind == kKindLoop && p->stack.k) return &p->jit_fn[device][4];
   if (b->flags & EBPF_BATCH_NO_JIT) return nullptr;
   if (kind == kKindDag && p->jit_mod[device][0])
     return &p->jit_fn[device][b->init_regs ? 0
@@ -1448,10 +1624,13 @@ uint64_t ebpf_workspace_bytes(const ebpf_prog* p, const ebpf_batch* b, int devic
   if (!p || !b) return 0;
   const uint64_t x = (b->flags & EBPF_BATCH_XDP_MD) ? xdp_region_bytes(b) : 0;
   uint64_t bytes = kWsSlotsOff + x;
-  if (use_binning(p, b))  // the binned packet order, then the per-workgroup class counts
-    bytes += b->n * 4 + 4ull * kBinMaxWgs * kBinClasses;
+  // the binned packet order, then the per-workgroup class counts (either loop program of a
+  // promoted stack program may run)
+  if (use_binning(p, b) || (!p->puops.empty() && use_binning(p, b, true)))
+    bytes += align16(b->n * 4 + 4ull * kBinMaxWgs * kBinClasses);
   bytes += align16(tier1_slots_bytes(p, b, device));
-  if (p->stack.any_dyn) bytes += align16(b->n * 4);  // the deopt list's indices (past the slots)
+  if (p->stack.any_dyn || !p->puops.empty())  // the deopt list's indices (past the slots)
+    bytes += align16(b->n * 4);
   return bytes;  // (the xdp_md region, when present, is the last x bytes)
 }
 
@@ -1558,9 +1737,12 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* bin, const ebpf_batch_out* ou
   a.prog = p->dev_uops[device];
   // constant-address loads are resolved for the main.rs register layout only
   a.dprog = b->init_regs ? p->dev_duops[device] : p->dev_duopsk[device];
-  a.tprog = kind == kKindLoop ? p->dev_ltuops[device]
+  // (the stack-slot promoted program: batch_kind's loop kind without the stack flag)
+  const bool promo = kind == kKindLoop && !stk && p->stack.k;
+  a.tprog = promo ? p->dev_pltuops[device]
+           : kind == kKindLoop ? p->dev_ltuops[device]
            : b->init_regs      ? p->dev_tuops[device] : p->dev_tuopsk[device];
-  a.tprog_exact = p->dev_ltuopsx[device];
+  a.tprog_exact = promo ? p->dev_pltuopsx[device] : p->dev_ltuopsx[device];
   a.n_uops = kind_uops(p, kind);
   a.mem_size = b->mem_size;
   a.frames = b->frames;
@@ -1602,7 +1784,7 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* bin, const ebpf_batch_out* ou
     if (cur != device) hipSetDevice(cur);
     return EBPF_EHIP;
   }
-  if (kind == kKindLoop && use_binning(p, b)) {
+  if (kind == kKindLoop && use_binning(p, b, promo)) {
     a.perm = (const uint32_t*)(ws + kWsSlotsOff);
     a.bin_counts = (uint32_t*)(ws + kWsBinCountsOff);
     if (launch_binning(b->lens, b->n, (uint32_t*)a.perm + b->n, (uint32_t*)a.perm, s) !=
@@ -1614,11 +1796,16 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* bin, const ebpf_batch_out* ou
   const JitFns* jit = batch_jit(p, b, kind, stk, device);
   // store mode (register-address packet stores, StackPlan::any_dyn): lanes the compiled kernel
   // cannot finish are listed, then re-run from the start by the general interpreter (tier 1)
-  const bool deopt = stk && p->stack.any_dyn && kind == kKindDag && jit &&
-                     launch_kernel_id(kind, a, jit, stk) == EBPF_KERNEL_JIT_VAR_STACK;
+  // (the promoted program: lanes whose packet reaches the slots, jit.cpp promo_guard)
+  const bool deopt = (stk && p->stack.any_dyn && kind == kKindDag && jit &&
+                      launch_kernel_id(kind, a, jit, stk) == EBPF_KERNEL_JIT_VAR_STACK) ||
+                     (promo && jit);
   if (deopt) {
     a.deopt = (uint32_t*)(ws + kWsDeoptOff);
-    a.deopt_idx = (uint32_t*)(ws + kWsSlotsOff + align16(tier1_slots_bytes(p, b, device)));
+    // (past the tier-1 slots, or the binned order and its class counts when the batch is binned)
+    const uint64_t bin_bytes = a.perm ? b->n * 4 + 4ull * kBinMaxWgs * kBinClasses : 0;
+    a.deopt_idx = (uint32_t*)(ws + kWsSlotsOff +
+                              align16(std::max<uint64_t>(tier1_slots_bytes(p, b, device), bin_bytes)));
   }
   hipError_t e = launch_interp(kind, a, grid, s, jit, stk);
   if (deopt && e == hipSuccess) {

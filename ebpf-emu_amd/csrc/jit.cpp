@@ -244,6 +244,7 @@ struct Compiler {
   bool prefetch = false;  // zwin refills take the prefetched next window (refill_prefetch)
   int pf = 1;  // windows prefetched ahead (ebpf_tile_jit_loop_deep for 2, 3)
   bool deep_regs = false;  // compiled for ebpf_tile_jit_loop_deep: v[72:105] are the program's
+  uint32_t guard_k = 0;  // a stack-slot promoted program (host.cpp promote_slots): the guard
   mutable bool coop_emitted = false;  // a coop_sum entry was emitted (compile_into_template:
                                       // such programs go to the deep kernel, unbinned)
 
@@ -308,6 +309,7 @@ struct Compiler {
   using AbsRegs = std::array<AbsVal, 11>;
   static constexpr uint64_t kLenMax = 1ull << 24;  // mem_size bound (include/ebpf_emu.h)
   std::vector<char> inb;   // inb[i]: the one-byte LDX i is proven in bounds
+  std::vector<char> reached;  // prove_loads' fixpoint: the micro-ops some path reaches
   std::vector<AbsRegs> ranges;  // the registers' abstract values at each reached micro-op
   // counted loops: a one-byte load's base read from this register instead (-1: its own)
   std::vector<int> addr_src = std::vector<int>(64, -1);
@@ -530,6 +532,7 @@ struct Compiler {
       flow(i + 1, nt);
     }
     if (!work.empty()) return;  // (no fixpoint within the bound: prove nothing)
+    reached = seen;
     ranges.assign(n, AbsRegs());
     for (uint32_t i = 0; i < n; i++)
       if (seen[i]) ranges[i] = in[i];
@@ -687,6 +690,15 @@ struct Compiler {
     if (x <= i && x < n) back = x;
     if (!ja && np <= i && np < n) back = std::min(back, np);
     return s + "s_mov_b64 exec, 0\ns_branch " + entry_label(P, back) + "\n";
+  }
+
+  // Every reachable packet load is a one-byte load proven inside the packet (prove_loads).
+  bool all_loads_proven() {
+    prove_loads();
+    if (reached.size() != n) return false;
+    for (uint32_t i = 0; i < n; i++)
+      if (reached[i] && uops[i].op == U_LDX && !inb[i]) return false;
+    return true;
   }
 
   // A VOP3 operand for an LPC value: an inline constant, or (programs above 64 micro-ops) a
@@ -2214,6 +2226,7 @@ struct Compiler {
       for (uint32_t i = L; i < J; i++) {
         if (skip[i] || (int)i == inc || (int)i == ld) continue;
         const Uop& u = uops[i];
+        if (u.op == U_NOP) continue;  // (promote_slots' folded slot accesses)
         others++;
         if ((int)i > ld && u.op == U_ADD64 && (u.aux & F_SRC) && u.src == uops[ld].dst &&
             u.dst != uops[ld].dst && u.dst != rI && u.dst != rN)  // (the add after the load)
@@ -3043,6 +3056,27 @@ struct Compiler {
     return true;
   }
 
+  // A stack-slot promoted program (guard_k): the lanes about to run (LPC 0) whose packet reaches
+  // the stack window (LEN > r10 - guard_k: a packet load could read a slot's bytes, which the
+  // promoted program keeps in a register) deoptimize before their first step -- the general
+  // interpreter runs their packets after the launch (host.cpp, the deopt pass).
+  std::string promo_guard(const std::string& P) const {
+    if (!guard_k) return "";
+    const std::string G = ".L" + P + "pguard";
+    // (r10 from s48, the statement's copy of LaunchArgs::r10: the promoted program may never
+    // read r10, so its register can be left uninitialised by the live-in init)
+    return "; stack-slot promotion guard: LEN <= r10 - " + std::to_string(guard_k) + "\n"
+           "s_mov_b64 s[64:65], exec\ns_mov_b64 exec, -1\n"
+           "v_mov_b32 v36, s48\nv_subrev_u32 v36, " + std::to_string(guard_k) + ", v36\n"
+           "v_cmp_gt_u32 vcc, v31, v36\n"
+           "v_cmp_eq_u32 s[60:61], 0, v28\n"
+           "s_and_b64 vcc, vcc, s[60:61]\n"
+           "s_cbranch_vccz " + G + "\n"
+           "s_mov_b64 exec, vcc\n"
+           "v_mov_b32 v30, 0x80\nv_mov_b32 v28, -1\n" + G + ":\n"
+           "s_mov_b64 exec, s[64:65]\n";
+  }
+
   // s70 (set by the statement's prologue, tile_jit.inc): bit 0 = exact mode (the step-budget
   // restart), bit 1 = registers not in the main.rs layout (init_regs) or requested as outputs.
   // With bit 1 clear, a program with loads proven in bounds (prove_loads) runs its proven copy.
@@ -3061,7 +3095,7 @@ struct Compiler {
                        ", v29\n"
                        "v_mov_b32 v55, 0x80000000\n" + window_zero_prologue(m, P) +
                        prefetch_prologue(m, P) +
-                       (stk ? stack_zero() + stack_init(P, ool) : std::string()) +
+                       (stk ? stack_zero() + stack_init(P, ool) : std::string()) + promo_guard(P) +
                        "s_bitcmp1_b32 s70, 0\ns_cbranch_scc1 .L" + PX + "start\n";
     prove_loads();
     const bool any = std::find(inb.begin(), inb.end(), 1) != inb.end();
@@ -3282,7 +3316,7 @@ bool jit_compile(const std::vector<Uop>& uops, const std::vector<TUop>& t,
 bool jit_compile_loop(const std::vector<Uop>& uops, const std::vector<TUop>& t,
                       const std::vector<TUop>& tx, std::vector<char>& code_object,
                       std::string* err, std::string* asm_out, const StackPlan* stk,
-                      bool* deep) {
+                      bool* deep, uint32_t guard_k) {
   if (uops.empty() || uops.size() > kJitMaxUops || t.size() < uops.size() ||
       tx.size() < uops.size() ||
       (stk && (stk->k == 0 || stk->k > kStackMax || stk->k % 4 || stk->off.size() != uops.size() ||
@@ -3291,6 +3325,13 @@ bool jit_compile_loop(const std::vector<Uop>& uops, const std::vector<TUop>& t,
     return false;
   }
   Compiler c(uops, t, true, false, stk), xc(uops, tx, true, true, stk);
+  if (guard_k) {  // a promoted program: its packet loads cannot reach the window of any lane
+    if (stk || !c.all_loads_proven()) {  // whose LEN <= r10 - guard_k
+      if (err) *err = "promoted program: a load not proven inside the packet";
+      return false;
+    }
+    c.guard_k = xc.guard_k = guard_k;
+  }
   return compile_into_template(c, &xc, code_object, err, asm_out, deep);
 }
 

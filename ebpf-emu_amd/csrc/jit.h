@@ -31,8 +31,8 @@ struct JitFns {
 // packet's header window at constant addresses (the preloaded window dwords v[64 : 79]).
 // compiled variants of a program: 0 init_regs batches, 1 the main.rs layout (constant-address
 // loads resolved), 2 the loop kernel, 3 xdp_md batches (the ctx's data field known, host.cpp
-// fold_const_loads)
-constexpr int kJitVariants = 4;
+// fold_const_loads), 4 the stack-slot promoted loop program (host.cpp promote_slots)
+constexpr int kJitVariants = 5;
 constexpr uint32_t kStackMax = 64;    // window bytes
 constexpr uint32_t kStackVgpr = 80;   // first VGPR of the window (ebpf_tile_jit_fixed)
 constexpr int32_t kNoStack = INT32_MIN;
@@ -70,10 +70,13 @@ bool jit_compile(const std::vector<Uop>& uops, const std::vector<TUop>& t,
 // Loop programs (back edges, or budgets that can bind; tile tables of build_tile: `t` the block
 // table, `tx` the exact one-micro-op-per-block table) for ebpf_tile_jit_loop. *deep (if given):
 // the code went into ebpf_tile_jit_loop_deep instead (refills prefetching pf_depth() windows).
+// guard_k > 0 (a stack-slot promoted program, host.cpp promote_slots): every packet load must be
+// a one-byte load proven inside the packet (prove_loads; else the compile fails), and lanes whose
+// packet reaches the window (LEN > r10 - guard_k) deoptimize at the start (jit.h kStDeopt).
 bool jit_compile_loop(const std::vector<Uop>& uops, const std::vector<TUop>& t,
                       const std::vector<TUop>& tx, std::vector<char>& code_object,
                       std::string* err, std::string* asm_out = nullptr,
-                      const StackPlan* stk = nullptr, bool* deep = nullptr);
+                      const StackPlan* stk = nullptr, bool* deep = nullptr, uint32_t guard_k = 0);
 
 // Windows the refills of byte-scanning loop programs prefetch ahead: 1 (ebpf_tile_jit_loop, 5
 // waves per SIMD) or 2-3 (ebpf_tile_jit_loop_deep, 4 waves); EBPFEMU_PF_DEPTH overrides.

@@ -89,11 +89,31 @@ class Program:
         L.ebpf_prog_jit_asm(self._h, variant, buf, n.value + 1, ctypes.byref(n))
         return buf.value.decode()
 
+    @property
+    def store_mode(self) -> bool:
+        """Register-address stores into the packet (host.cpp analyze_stack, StackPlan::any_dyn):
+        the compiled var kernel with its header window in LDS and the deopt pass."""
+        try:
+            return "(store mode)" in self.jit_asm(1)
+        except _lib.EbpfError:
+            return False
+
+    @property
+    def promoted(self) -> bool:
+        """A stack-window loop program with its 8-byte slots promoted to registers (host.cpp
+        promote_slots): production batches run that tier-0 program (compiled variant 4) on the
+        loop kernels, EBPF_KERNEL_JIT_LOOP."""
+        try:
+            return bool(self.jit_asm(4))
+        except _lib.EbpfError:
+            return False
+
     def jit_loop_kernel(self) -> str:
         """The template kernel holding this program's compiled loop code (EBPF_KERNEL_JIT_LOOP
         names either): "ebpf_tile_jit_loop_deep" when the loop program went to the deep kernel
-        (cooperative byte sums, or a deeper refill prefetch), else "ebpf_tile_jit_loop"."""
-        a = self.jit_asm(2)
+        (cooperative byte sums, or a deeper refill prefetch), else "ebpf_tile_jit_loop". (For a
+        promoted stack program: its promoted program's kernel.)"""
+        a = self.jit_asm(4 if self.promoted else 2)
         at = 0
         for ln in a.splitlines(keepends=True):
             at += len(ln)

@@ -373,3 +373,39 @@ def gen_store_program(rng: random.Random, n: int | None = None) -> bytes:
         words.append(encode(0xAF, 0, r, 0, 0))                            # xor r0, r
     words.append(encode(0x95))
     return b"".join(words)
+
+
+def gen_slot_loop_program(rng: random.Random) -> bytes:
+    """Loop programs that keep their accumulators in 8-byte stack slots, the way compiled C spills
+    them (host.cpp promote_slots): `stdw [r10-8*k], c` before a byte loop over the packet
+    (`ldxb rD, [r1 + rI]`, rI = start .. N, N = the packet length r2 or a constant), a body that
+    reloads a slot, adds the byte (or xors / mixes it), stores it back -- sometimes through a
+    second slot or with the accumulator register read after the store -- and a tail that folds
+    the slots into r0. Some loops run through r2 + 16 (byte loads past the packet: not provable,
+    no promotion)."""
+    from ebpf_emu.asm import assemble
+
+    nslots = rng.choice([1, 1, 2])
+    start = rng.choice([0, 0, 1, 13])
+    bound = rng.choice(["r2", "r2", "r2", "20", "r6"])
+    acc = rng.choice(["r0", "r6", "r7"]) if bound != "r6" else rng.choice(["r0", "r7"])
+    lines = [f"stdw [r10-{8 * (k + 1)}], {rng.choice([0, 0, 1, 0x55])}" for k in range(nslots)]
+    if bound == "r6":
+        lines += ["mov r6, r2", "add r6, 16"]
+    lines += [f"mov r3, {start}", f"jge r3, {bound}, done", "loop:", "mov r4, r1", "add r4, r3",
+              "ldxb r5, [r4+0]"]
+    kind = rng.random()
+    if kind < 0.6:  # the accumulator triple
+        lines += [f"ldxdw {acc}, [r10-8]", f"add {acc}, r5", f"stxdw [r10-8], {acc}"]
+    elif kind < 0.8:  # the register read again after the store (not foldable: rT live)
+        lines += [f"ldxdw {acc}, [r10-8]", f"xor {acc}, r5", f"stxdw [r10-8], {acc}",
+                  f"add {acc}, 1"]
+    else:  # a mix
+        lines += [f"ldxdw {acc}, [r10-8]", f"mul {acc}, 31", f"add {acc}, r5", f"stxdw [r10-8], {acc}"]
+    if nslots == 2:
+        lines += ["ldxdw r8, [r10-16]", "add r8, 1", "stxdw [r10-16], r8"]
+    lines += ["add r3, 1", f"jlt r3, {bound}, loop", "done:", "ldxdw r0, [r10-8]"]
+    if nslots == 2:
+        lines += ["ldxdw r9, [r10-16]", "xor r0, r9"]
+    lines += ["exit"]
+    return assemble("\n".join(lines))

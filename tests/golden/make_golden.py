@@ -12,7 +12,7 @@ fuzz vector is cross-checked against the independent Python restatement before i
   bench_pins.json   : bench.py's weak-scaling pools at any rank count -> per-chunk counters of
                       every 1 Mi-packet chunk a pool can hold, for each bench program (so that the
                       default bench line pins its timed counters at N = 1..8)
-Usage: python tests/golden/make_golden.py [config4 | bench_pins]
+Usage: python tests/golden/make_golden.py [config4 | bench_pins | bench_pins_add NAME...]
 """
 import json
 import os
@@ -117,7 +117,7 @@ def config4(total=100_000_000):
 PIN_CHUNKS_64 = 128  # 16 pool batches x 8 ranks
 PIN_CHUNKS_MIXED = 16  # 2 pool batches x 8 ranks (a 1 Mi mixed batch is ~840 MB: one per rank)
 PIN_PROGRAMS_64 = ("5tuple", "drop", "5tuple_stack", "mac_swap_tx", "acl", "5tuple_xdp",
-                   "5tuple_call")
+                   "5tuple_call", "nat")
 PIN_PROGRAMS_MIXED = ("checksum", "checksum_stack")
 
 
@@ -141,6 +141,26 @@ def _pin_chunk(args):
                                     r10=2048, threads=1)
             out[name] = [int(x) for x in cnt]
     return kind, c, out
+
+
+def bench_pins_add(names):
+    """Adds programs' 64-byte chunk counters to the committed bench_pins.json (same chunks)."""
+    from multiprocessing import Pool
+
+    global PIN_PROGRAMS_64
+    path = os.path.join(HERE, "bench_pins.json")
+    with open(path) as f:
+        pins = json.load(f)
+    PIN_PROGRAMS_64 = tuple(names)
+    with Pool(max(1, min(8, os.cpu_count() or 1) - 1)) as pool:
+        res = pool.map(_pin_chunk, [("64", c) for c in range(PIN_CHUNKS_64)])
+    for name in names:
+        rows = sorted((c, o[name]) for _, c, o in res)
+        pins["programs"][name] = {"frames": "fixed64", "xdp_md": False,
+                                  "program": W.program(name).hex(), "mem_size": 1024, "r10": 512,
+                                  "chunk_counters": [cnt for _, cnt in rows]}
+    with open(path, "w") as f:
+        json.dump(pins, f, indent=0)
 
 
 def bench_pins():
@@ -170,6 +190,9 @@ def bench_pins():
 
 
 if __name__ == "__main__":
+    if sys.argv[1:2] == ["bench_pins_add"]:
+        bench_pins_add(sys.argv[2:])
+        sys.exit(0)
     if sys.argv[1:] == ["bench_pins"]:
         with open(os.path.join(HERE, "bench_pins.json"), "w") as f:
             json.dump(bench_pins(), f, indent=0)
