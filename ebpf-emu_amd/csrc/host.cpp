@@ -1582,10 +1582,11 @@ static const bool g_xdp_stage = [] {
 
 static bool xdp_in_place(ebpf_prog* p, const ebpf_batch* b, bool mem_out, int device, int kind,
                          bool stk) {
-  if (!(b->flags & EBPF_BATCH_XDP_MD) || g_xdp_stage || kind != kKindDag) return false;
-  // store mode: a deoptimized lane re-runs on the general interpreter, which reads the images
-  // xdp_stage writes (the ctx is not in the frames)
-  if (stk && p->stack.any_dyn) return false;
+  if (!(b->flags & EBPF_BATCH_XDP_MD) || g_xdp_stage) return false;
+  // the general interpreter's tier 1 builds each lane's image [ctx][packet] itself (interp.hip);
+  // so does its deopt pass after a store-mode launch
+  if (kind == kKindTier1) return true;
+  if (kind != kKindDag) return false;
   LaunchArgs a{};
   a.n_uops = kind_uops(p, kind);
   a.frames = b->frames;
@@ -1814,7 +1815,7 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* bin, const ebpf_batch_out* ou
     d.n_uops = (uint32_t)p->uops.size();
     d.tprog = d.tprog_exact = nullptr;
     d.dprog = nullptr;
-    d.xdp = 0;
+    d.xdp = a.xdp;  // (in place: tier 1 builds the ctx-prefixed images itself)
     const int g1 = std::min(tier1_grid(p, b, device), kDeoptMaxGrid);
     e = launch_interp(kKindTier1, d, g1, s, nullptr, false);
   }

@@ -564,6 +564,10 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
       base = a.frames + (a.offsets ? (uint64_t)a.offsets[pkt] : pkt * a.stride);
       len = a.lens ? (uint32_t)a.lens[pkt] : stride_len(a);
     }
+    // the xdp_md convention in place (tier 1): the image is [u32 data = 8][u32 data_end =
+    // 8 + len][packet] (xdp.rs:16-20), r2 = its length 8 + len -- built below, no staging copy
+    const uint32_t plen = len;  // (the packet's own length)
+    if (TIER == 1 && a.xdp && valid) len = min(plen, 0xffffu) + 8u;
 
     // ---- Emu::default() + main.rs:14-31 register/memory layout ----
     uint32_t rlo[11], rhi[11];
@@ -587,8 +591,14 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
     if (TIER == 1) {
       const uint32_t md = (mem_size + 3) / 4;
       const uint32_t m = (pc != PC_DONE) ? len : 0u;
-      for (uint32_t d = 0; d < md; d++)
-        img[(size_t)d * kWave] = (d * 4 < m) ? (uint32_t)pkt_read(base, d * 4, 4, len) : 0u;
+      if (a.xdp) {
+        for (uint32_t d = 0; d < md; d++)
+          img[(size_t)d * kWave] = d * 4 >= m ? 0u : d == 0 ? 8u : d == 1 ? len
+                                 : (uint32_t)pkt_read(base, d * 4 - 8, 4, plen);
+      } else {
+        for (uint32_t d = 0; d < md; d++)
+          img[(size_t)d * kWave] = (d * 4 < m) ? (uint32_t)pkt_read(base, d * 4, 4, len) : 0u;
+      }
       // the caller's initial frame stack (Emu.fp, emu.rs:26): an EXIT pops it (emu.rs:273-279)
       csp = a.init_fp_len;
       for (uint32_t i = 0; i < csp; i++) cstack[(size_t)i * kWave] = a.init_fp[i];
