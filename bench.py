@@ -325,8 +325,11 @@ def main():
                 batches[-1]["offsets"] = torch.from_numpy(
                     (np.arange(n, dtype=np.int64) * fb).astype(np.uint32).view(np.int32)).to(dev)
                 batches[-1]["lens"] = torch.from_numpy(np.full(n, fb, dtype=np.int16)).to(dev)
-            # the bytes a header program touches: its 64-byte window (+ offset and length)
-            algo_bytes = n * (64 + 1 + (6 if args.layout == "offsets" else 0))
+            # the bytes a header program's launch must read: its header window (+ offset and
+            # length) -- on fixed slots only the 16-byte chunks its loads reach (jit.cpp
+            # window_chunks: 16 for drop-all, the whole 64 with a register-address load)
+            wb = prog.window_bytes if args.layout == "fixed" and not args.generic else 64
+            algo_bytes = n * (wb + 1 + (6 if args.layout == "offsets" else 0))
         else:  # large slots: copies of the first batch at other addresses (host RNG is slow)
             batches.append(dict(frames=batches[0]["frames"].clone()))
         # (the bytes a launch touches decide whether the pool outgrows the Infinity Cache)

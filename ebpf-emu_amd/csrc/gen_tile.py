@@ -882,8 +882,10 @@ def fixed_dma_db(winb, tag):
     (l/4) * stride + its swizzled chunk * 16, computed once per wave) and a scalar tile base --
     one VALU per round instead of five; a partial tile takes fixed_dma's per-lane checks.
     64-byte slots: one address and the four 1 KiB rows by the instruction offset, which the
-    LDS-DMA adds to both the global and the LDS address."""
-    return f"""s_add_u32 {{T5L}}, {{T0L}}, 64
+    LDS-DMA adds to both the global and the LDS address. `; @DMAX@` / `; @DMAXE@` (jit.cpp
+    window_chunks): exec = the lanes of the window chunks the compiled program reads, then all."""
+    return f"""; @DMAX@
+s_add_u32 {{T5L}}, {{T0L}}, 64
 s_addc_u32 {{T5H}}, {{T0H}}, 0
 s_sub_u32 {{T5L}}, {{KNL}}, {{T5L}}
 s_subb_u32 {{T5H}}, {{KNH}}, {{T5H}}
@@ -918,7 +920,8 @@ s_addc_u32 {{T7H}}, {{T7H}}, {{T1H}}""" for r in range(4)) + f"""
 s_branch .Ldmaok{tag}%=
 .Lpart{tag}%=:
 """ + fixed_dma(winb) + f"""
-.Ldmaok{tag}%=:"""
+.Ldmaok{tag}%=:
+; @DMAXE@"""
 
 
 # ---- prologue / epilogue ----
@@ -1288,10 +1291,12 @@ s_mul_hi_u32 {{T7H}}, {tidx}, %[tbytes]
 s_add_u32 {{T7L}}, {{T7L}}, %[fr_lo]
 s_addc_u32 {{T7H}}, {{T7H}}, %[fr_hi]
 v_lshl_add_u64 {{T1213}}, %[dmaoff], 0, {{T7}}
+; @DMAX@
 s_mov_b32 m0, {winb}
 s_nop 0
 """ + "\n".join(f"global_load_lds_dwordx4 {{T1213}}, off offset:{1024 * r} ; @DMAPOLICY@"
                 for r in range(4)) + f"""
+; @DMAXE@
 .Ld{tag}%=:
 """
     ool = f""".Lx{tag}%=:

@@ -245,6 +245,7 @@ struct Compiler {
   int pf = 1;  // windows prefetched ahead (ebpf_tile_jit_loop_deep for 2, 3)
   bool deep_regs = false;  // compiled for ebpf_tile_jit_loop_deep: v[72:105] are the program's
   uint32_t guard_k = 0;  // a stack-slot promoted program (host.cpp promote_slots): the guard
+  uint32_t dma_chunks = 4;  // the fixed-slot window DMA's chunks (compile_into_template)
   mutable bool coop_emitted = false;  // a coop_sum entry was emitted (compile_into_template:
                                       // such programs go to the deep kernel, unbinned)
 
@@ -690,6 +691,24 @@ struct Compiler {
     if (x <= i && x < n) back = x;
     if (!ja && np <= i && np < n) back = std::min(back, np);
     return s + "s_mov_b64 exec, 0\ns_branch " + entry_label(P, back) + "\n";
+  }
+
+  // The 16-byte chunks of the header window the compiled fixed-slot code can read: 4 with any
+  // register-address load (its address is a run-time value), else enough to cover every
+  // constant-address load and packet-window store ending inside the window (loads past it read
+  // HBM directly), at least one. The fixed-slot kernel's window DMA moves only those chunks.
+  uint32_t window_chunks() const {
+    uint32_t maxend = 0;
+    for (uint32_t i = 0; i < n; i++) {
+      const uint32_t id = t[i].hoff / TILE_SLOT;
+      if (uops[i].op == U_LDX && stk && stk->off[i] != kNoStack) continue;  // (the stack window)
+      if (id == T_LDX_C || id == T_LDX_E || id == T_LDX1_C || id == T_LDX1_E) return 4;
+      if (is_ldxk(id)) maxend = std::max<uint32_t>(maxend, t[i].x);
+      else if (uops[i].op == U_LDX && id != T_LDXK_FAR_C && id != T_LDXK_FAR_E) return 4;
+      if (stk && i < stk->pw.size() && stk->pw[i] != kNoStack)
+        maxend = std::max<uint32_t>(maxend, (uint32_t)stk->pw[i] + uops[i].aux);
+    }
+    return std::max<uint32_t>(1, std::min<uint32_t>(4, (maxend + 15) / 16));
   }
 
   // Every reachable packet load is a one-byte load proven inside the packet (prove_loads).
@@ -3243,6 +3262,24 @@ bool compile_into_template(Compiler& c, Compiler* xc, std::vector<char>& code_ob
     const std::string key = " ; @DMAPOLICY@", val = std::string(" ") + (pol ? pol : "nt");
     size_t q;
     while ((q = tmpl.find(key)) != std::string::npos) tmpl.replace(q, key.size(), val);
+  }
+  // the fixed-slot statement's window DMA: only the lanes of the chunks the program reads
+  // (EBPFEMU_DMA_CHUNKS=4 keeps the whole window, A/B)
+  {
+    const char* e = getenv("EBPFEMU_DMA_CHUNKS");
+    const uint32_t C = xc ? 4u : e ? std::max(1, std::min(4, atoi(e))) : c.window_chunks();
+    uint64_t mask = 0;  // lane l DMAs logical chunk (l & 3) ^ ((l >> 4) & 3) (gen_tile fixed_dma)
+    for (uint32_t l = 0; l < 64; l++)
+      if ((((l & 3) ^ ((l >> 4) & 3))) < C) mask |= 1ull << l;
+    const std::string on = C >= 4 ? "" : "s_mov_b32 exec_lo, " + hex32((uint32_t)mask) +
+                                             "\ns_mov_b32 exec_hi, " + hex32((uint32_t)(mask >> 32));
+    const std::string off = C >= 4 ? "" : "s_mov_b64 exec, -1";
+    for (const auto& kv : {std::make_pair(std::string("; @DMAXE@"), off),
+                           std::make_pair(std::string("; @DMAX@"), on)}) {
+      size_t q;
+      while ((q = tmpl.find(kv.first)) != std::string::npos) tmpl.replace(q, kv.first.size(), kv.second);
+    }
+    c.dma_chunks = C;
   }
   std::vector<Marker> marks;
   if (!find_markers(tmpl, marks)) {

@@ -90,6 +90,23 @@ class Program:
         return buf.value.decode()
 
     @property
+    def window_bytes(self) -> int:
+        """Bytes of each packet's 64-byte header window the compiled fixed-slot kernel DMAs
+        (jit.cpp window_chunks: the 16-byte chunks its constant-address loads and stores reach;
+        all 64 with a register-address load)."""
+        import re
+
+        try:
+            a = self.jit_asm(1)
+        except _lib.EbpfError:
+            return 64
+        m = re.search(r"s_mov_b32 exec_lo, (0x[0-9a-f]+)\ns_mov_b32 exec_hi, (0x[0-9a-f]+)", a)
+        if not m:
+            return 64
+        lanes = bin(int(m.group(1), 16)).count("1") + bin(int(m.group(2), 16)).count("1")
+        return lanes  # (16 lanes per chunk, 16 bytes each, per 16 packets: 1 byte per lane)
+
+    @property
     def store_mode(self) -> bool:
         """Register-address stores into the packet (host.cpp analyze_stack, StackPlan::any_dyn):
         the compiled var kernel with its header window in LDS and the deopt pass."""
