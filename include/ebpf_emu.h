@@ -120,7 +120,10 @@ typedef struct ebpf_batch {
 /* Outputs (device pointers; any may be NULL). */
 typedef struct ebpf_batch_out {
   uint8_t* verdict;   /* u8[n]: r0 < 5 ? r0 : 0xFE; 0xFF on fault */
-  uint64_t* r0;       /* u64[n]: raw r0 (two's complement of the reference's i64, main.rs:43) */
+  uint64_t* r0;       /* u64[n]: raw r0 (two's complement of the reference's i64, main.rs:43);
+                         for a packet with status != EBPF_ST_OK (the reference panics) r0 is the
+                         register at the fault, except on a stack-slot promoted program's kernel,
+                         where it is unspecified */
   uint8_t* status;    /* u8[n]: EBPF_ST_* */
   uint64_t* counters; /* u64[EBPF_NCOUNTERS], ADDED to (not overwritten) */
   uint8_t* mem;       /* u8[n][mem_size]: final memory image per packet (Emu.state.mmu.memory) */

@@ -10,6 +10,8 @@ GPU: the production outputs of promoted batches (route EBPF_KERNEL_JIT_LOOP) aga
 interpreter and the oracle, on every var layout, with packets long enough to reach the slots
 (LEN > r10 - k: those lanes deoptimize to the general interpreter) and step budgets that bind;
 batches asking for the final registers keep the stack loop kernel (EBPF_KERNEL_JIT_LOOP_STACK).
+r0 is compared where the packet completes: a faulted packet's r0 is not a reference output (the
+reference panics), and the folded accumulator (`nop; add rS, rD; nop`) leaves it elsewhere.
 """
 import random
 import zlib
@@ -115,8 +117,12 @@ def test_promoted_vs_oracle(cuda, oracle_mod, layout):
                 assert got["kernel"] == _lib.EBPF_KERNEL_JIT_LOOP, (layout, it)
                 n_prom += 1
             ref, _ = _prod(img, pkts, cuda, layout, generic=True, max_steps=steps)
-            for key in ("status", "verdict", "counters", "r0"):
+            for key in ("status", "verdict", "counters"):
                 assert np.array_equal(got[key], ref[key]), (key, layout, it, steps, img.hex())
+            # r0 of a packet that faulted (ST_STEPS here) is not an output of the reference, which
+            # panics there; the promoted program's folded accumulator leaves it elsewhere
+            okr = got["status"] == 0
+            assert np.array_equal(got["r0"][okr], ref["r0"][okr]), (layout, it, steps, img.hex())
             st, r0, cnt = _oracle(oracle_mod, img, pkts, xdp, 2048, 1024, steps)
             assert np.array_equal(got["status"], st), (layout, it, steps)
             ok = st == 0

@@ -175,8 +175,9 @@ def test_stack_window_fuzz(cuda, oracle_mod, seed):
         got = _run(img, frames, len(pkts), cuda, stride=stride)
         # (a constant-address load into the window: the loop kernel's stack variant, whose loads
         # all take the store-forwarding overlay)
+        # (store mode: the var kernel's stack statement, test_store_mode.py)
         assert got["kernel"] in (_lib.EBPF_KERNEL_JIT_STACK, _lib.EBPF_KERNEL_JIT_LOOP_STACK,
-                                 _lib.EBPF_KERNEL_GENERAL_T1)
+                                 _lib.EBPF_KERNEL_JIT_VAR_STACK, _lib.EBPF_KERNEL_GENERAL_T1)
         n_stack += got["kernel"] == _lib.EBPF_KERNEL_JIT_STACK
         ref = _run(img, frames, len(pkts), cuda, generic=True, stride=stride)
         assert ref["kernel"] == _lib.EBPF_KERNEL_GENERAL_T1
@@ -343,7 +344,8 @@ def test_stack_atomics_fuzz(cuda, oracle_mod, seed):
         pkts = [bytes(rng.getrandbits(8) for _ in range(stride)) for _ in range(rng.choice([64, 100]))]
         frames = _fixed_frames(pkts, stride, cuda)
         got = _run(img, frames, len(pkts), cuda, stride=stride)
-        n_stack += got["kernel"] == _lib.EBPF_KERNEL_JIT_STACK
+        # (a store through an unknown pointer: store mode, the var kernel's stack statement)
+        n_stack += got["kernel"] in (_lib.EBPF_KERNEL_JIT_STACK, _lib.EBPF_KERNEL_JIT_VAR_STACK)
         ref = _run(img, frames, len(pkts), cuda, generic=True, stride=stride)
         for key in ("status", "r0", "verdict", "regs", "counters", "prod_verdict"):
             assert np.array_equal(got[key], ref[key]), (key, seed, it, img.hex())
@@ -556,7 +558,7 @@ def test_stack_loop_programs(cuda, oracle_mod, layout):
     n_stack = 0
     for it, img in enumerate(progs):
         p = Program(img)
-        k = p.stack_window
+        k, prom = p.stack_window, p.promoted
         p.close()
         if not k:
             continue
@@ -566,7 +568,10 @@ def test_stack_loop_programs(cuda, oracle_mod, layout):
             if it == 2 and steps == 3000:  # (forward, budget that cannot bind: forward kernels)
                 assert got["kernel"] in (_lib.EBPF_KERNEL_JIT_VAR_STACK,), layout
             else:
-                assert got["kernel"] == _lib.EBPF_KERNEL_JIT_LOOP_STACK, (layout, it, img.hex())
+                # (the route of the production outputs: a promoted program's own loop kernel,
+                # test_promote.py; every output asked for below runs the stack loop kernel)
+                want = _lib.EBPF_KERNEL_JIT_LOOP if prom else _lib.EBPF_KERNEL_JIT_LOOP_STACK
+                assert got["kernel"] == want, (layout, it, img.hex())
                 n_stack += 1
             ref, _ = _run_var(img, pkts, cuda, VAR_LAYOUTS[layout], generic=True, max_steps=steps)
             ok = got["status"] != 7

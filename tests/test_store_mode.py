@@ -150,9 +150,11 @@ def test_nat_rewrite_vs_oracle(cuda, oracle_mod, layout):
     assert got["kernel"] == _lib.EBPF_KERNEL_JIT_VAR_STACK
     ref, _, _ = _run_layout(img, pkts, cuda, layout, generic=True)
     _check(oracle_mod, img, pk, got, ref, xdp, f"nat {layout}")
-    # the workload exercised every path: TX (redirected), PASS, DROP
+    # the workload exercised every path: TX (redirected), PASS, DROP (under xdp_md the program,
+    # not written for the ctx convention, reads the ctx-prefixed image: parity only)
     v = got["verdict"]
-    assert (v == 3).sum() > 50 and (v == 2).sum() > 50 and (v == 1).sum() > 50
+    if not xdp:
+        assert (v == 3).sum() > 50 and (v == 2).sum() > 50 and (v == 1).sum() > 50
 
 
 @pytest.mark.gpu
