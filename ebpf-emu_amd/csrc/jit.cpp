@@ -2933,15 +2933,26 @@ struct Compiler {
   // Other layouts: lanes whose packet reaches into the window take its bytes there, byte by
   // byte, out of line (the launch checked S0 >= 64, so they are never header-window bytes).
   std::string stack_init(const std::string& P, std::string& ool) const {
+    // per window dword j (image address b = S0 + 4j, 4-aligned): the lanes whose packet holds
+    // byte b load the aligned packet dwords around it -- the second only if it holds a packet
+    // byte too (no access leaves the page of a packet byte, interp.hip pkt_read) -- and keep the
+    // bytes below LEN; one wait per dword (the byte-by-byte form waited once per byte)
     ool += ".L" + P + "skinit:\ns_mov_b64 s[66:67], exec\ns_mov_b64 s[68:69], vcc\n";
-    for (uint32_t b = 0; b < stk->k; b++) {
-      const std::string L = ".L" + P + "sk" + std::to_string(b);
-      ool += "s_mov_b64 exec, s[68:69]\nv_add_u32_e64 v36, s57, " + std::to_string(b) +
-             "\nv_cmp_gt_u32 vcc, v31, v36\ns_and_b64 exec, exec, vcc\ns_cbranch_execz " + L +
-             "\nv_mov_b32 v37, 0\nv_lshl_add_u64 v[38:39], v[32:33], 0, v[36:37]\n"
-             "global_load_ubyte v40, v[38:39], off\ns_waitcnt vmcnt(0)\n"
-             "v_lshl_or_b32 " + sv(b / 4) + ", v40, " + std::to_string(8 * (b % 4)) + ", " +
-             sv(b / 4) + "\n" + L + ":\n";
+    for (uint32_t j = 0; j < stk->k / 4; j++) {
+      const std::string L = ".L" + P + "sk" + std::to_string(j);
+      ool += "s_mov_b64 exec, s[68:69]\nv_add_u32_e64 v36, s57, " + std::to_string(4 * j) +
+             "\nv_cmp_gt_u32 vcc, v31, v36\ns_and_b64 exec, exec, vcc\ns_cbranch_execz " + L + "\n"
+             "v_mov_b32 v37, 0\nv_lshl_add_u64 v[38:39], v[32:33], 0, v[36:37]\n"
+             "v_and_b32 v40, 3, v38\nv_and_b32 v38, -4, v38\n"
+             "global_load_dword v41, v[38:39], off\nv_mov_b32 v42, 0\n"
+             "v_sub_u32 v43, v36, v40\nv_add_u32 v43, 4, v43\nv_cmp_gt_u32 vcc, v31, v43\n"
+             "s_and_saveexec_b64 s[64:65], vcc\n"
+             "global_load_dword v42, v[38:39], off offset:4\n"
+             "s_mov_b64 exec, s[64:65]\ns_waitcnt vmcnt(0)\n"
+             "v_lshlrev_b32 v40, 3, v40\nv_alignbit_b32 v41, v42, v41, v40\n"
+             "v_sub_u32 v43, v31, v36\nv_min_u32 v43, 4, v43\nv_lshlrev_b32 v43, 3, v43\n"
+             "v_lshlrev_b64 v[44:45], v43, 1\nv_add_u32 v44, -1, v44\n"
+             "v_and_b32 " + sv(j) + ", v44, v41\n" + L + ":\n";
     }
     ool += "s_mov_b64 exec, s[66:67]\ns_branch .L" + P + "skdone\n";
     return "v_cmp_lt_u32 vcc, s57, v31\ns_cbranch_vccnz .L" + P + "skinit\n.L" + P + "skdone:\n";
