@@ -1526,8 +1526,11 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
   // diagnostics (EBPFEMU_TRACE=1, tools/trace_loop.py; the JIT loop kernels only): s_memrealtime stamps of
   // the wave's first tile -- entry, window ready, statement done, counters flushed -- its lane 0's
   // packet length and the hardware ids
+  // (the forward var kernels, tools/trace_var.py: window ready / statement done of each of the
+  // wave's first five tiles in slots 1 + 2i / 2 + 2i, its tile count in slot 15)
   uint64_t* const trace =
-      JIT && LOOPS && a.trace && wave_slot < kTraceWaves ? a.trace + wave_slot * kTraceSlots : nullptr;
+      JIT && a.trace && wave_slot < kTraceWaves ? a.trace + wave_slot * kTraceSlots : nullptr;
+  uint32_t ti = 0;  // (var trace: the wave's tile ordinal)
   auto stamp = [&](uint32_t slot) {
     uint64_t ts;
     asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ts)::"memory");
@@ -1617,7 +1620,8 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
     const uint64_t t = rfl64(tile);
     const uint64_t nt = t + total_waves;
     uint32_t bkt, nst;
-    if (trace && t == wave_slot) {
+    if (trace && !LOOPS && ti < 5) stamp(1 + 2 * ti);
+    if (trace && LOOPS && t == wave_slot) {
       stamp(1);
       if (!FIXED && threadIdx.x % kWave == 0) {
         uintptr_t mb;
@@ -1700,7 +1704,9 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
 #pragma unroll
     for (int b = 0; b < 7; b++) cnt[b] += __builtin_popcountll(ballot(bkt == (uint32_t)b));
     retired += nst;
-    if (trace && t == wave_slot) stamp(2);
+    if (trace && LOOPS && t == wave_slot) stamp(2);
+    if (trace && !LOOPS && ti < 5) stamp(2 + 2 * ti);
+    ti++;
     tile = nt;
     if (pipe) mb = mb + 1 == nmeta ? 0u : mb + 1;  // (without the prefetch: buffer 0 always)
     wi ^= 1u;
@@ -1716,6 +1722,7 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)\n\ts_getreg_b32 %1, hwreg(HW_REG_HW_ID)"
                  : "=s"(xcc), "=s"(hw));
     if (ln == 0) trace[14] = ((uint64_t)xcc << 32) | hw;
+    if (!LOOPS && ln == 0) trace[15] = ti;
   }
   flush_counters<WPB>(a, cnt64, retired, smem, ln, wv);
   if (trace) stamp(13);
