@@ -3055,6 +3055,14 @@ struct Compiler {
   // ebpf_tile_jit_loop: s70 = 0 runs the block copy, whose budget failure restarts the tile
   // (.Lreinit of the statement's prologue) with s70 = 1, which runs the exact copy.
   bool body_loop(const Marker& m, Compiler& xc, std::string& out) {
+    // (compile_into_template may run this twice -- a dry run finds a cooperative sum, then the
+    // real one: every piece of state a run writes is reset here, so the two agree)
+    for (Compiler* k : {this, &xc}) {
+      std::fill(k->addr_src.begin(), k->addr_src.end(), -1);
+      k->err.clear();
+      k->coop_emitted = false;
+      k->proven = false;
+    }
     // opt-in (EBPFEMU_BYTE_CACHE=1): A/B on one MI355X, checksum config, 1 Mi packets: 474 us
     // with the cache vs 466 without -- the LDS instructions drop 7.5x and the bank-conflict
     // cycles 14x, but the extra selects and the miss path's SALU turn the waits into issue
