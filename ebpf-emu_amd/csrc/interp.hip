@@ -474,6 +474,11 @@ __device__ __forceinline__ void flush_counters(const LaunchArgs& a, const uint64
 
 template <int TIER, bool LDSP, int NW, bool DB>
 __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
+  // the deopt pass with an empty list (the usual case): every workgroup leaves at once -- no
+  // program staging, no counter flush, nothing to clear (the list cannot grow during the pass)
+  if (TIER == 1 && a.deopt_pass &&
+      rfl(__hip_atomic_load(a.deopt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0)
+    return;
   counters_init();
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t nu = a.n_uops;
