@@ -927,7 +927,8 @@ s_branch .Ldmaok{tag}%=
 # ---- prologue / epilogue ----
 # %[ka]: the kernel-argument segment (LaunchArgs at offset 0; LA_* offsets are "i" operands);
 # %[tile]: the tile index (64-bit SGPR pair); %[winb]: this wave's window region (LDS byte
-# address); %[metab]: this wave's metadata region (offsets u32[64], lengths u32[64]).
+# address); %[metab]: this wave's metadata region (offsets u32[64], lengths u32[64]; with %[plen],
+# the compiled forward var kernels, lengths u16[64]: interp.hip dma_meta<true>).
 # the main.rs:28-31 register layout (r1 = 0, r2 = len, r10 = the batch's r10, the rest 0)
 DEFAULT_INIT = "\n".join(f"v_mov_b64 v[{i}:{i + 1}], 0" for i in range(0, 20, 2) if i != 4) + """
 v_mov_b32 v4, {LEN}
@@ -971,7 +972,13 @@ v_lshl_add_u64 {T23}, {T01}, 0, {T0}
 v_lshlrev_b32 {t5}, 2, {t0}
 v_add_u32 {t5}, %[metab], {t5}
 ds_read_b32 {t6}, {t5}
+.if %[plen]
+v_lshlrev_b32 {t7}, 1, {t0}
+v_add_u32 {t7}, %[metab], {t7}
+ds_read_u16 {t7}, {t7} offset:256
+.else
 ds_read_b32 {t7}, {t5} offset:256
+.endif
 .endif
 s_waitcnt lgkmcnt(0)
 """ + FIXED_DMA + """v_cmp_gt_u64 vcc, {KN}, {T23}
@@ -1469,6 +1476,255 @@ s_waitcnt lgkmcnt(0)
     return main + ool
 
 
+# ---- the compiled var kernel's tile loop (ebpf_tile_jit_varl) ----
+# offsets + lens batches (a capture's or a NIC ring's layout) whose length array is 4-byte aligned
+# (or absent). One statement runs up to %[cdn] (511) of the wave's tiles (tile, tile + W, ...: W =
+# the grid's waves) as the fixed-slot kernel's loop does, with two window buffers and two metadata
+# buffers per wave (interp.hip kVarlWaveLds: offsets u32[64], then the lengths as u16[64]). On
+# entry and at the top of every tile the tile's windows (DMA'd or staged by the C++) and the next
+# tile's metadata are in flight or landed; per tile:
+#   * wait; this lane's offset / length from the metadata (BASE, LEN, xdp_md: BASE - 8, 8 + len);
+#   * the next tile nt = tile + W: a whole tile whose packets are all 16-byte aligned (lanes of
+#     length 0 excepted) has its four window DMAs issued into the other window buffer (packet
+#     16r + l/4's chunk (l & 3) ^ ((l >> 4) & 3), chunks wholly past the packet from a dummy
+#     address); any other tile -- misaligned packets, the batch's partial last tile -- ends the
+#     statement after this one (%[stage] = 1): the C++ stages its windows lane by lane and comes
+#     back;
+#   * the metadata of nt + W (a whole tile) into this tile's metadata buffer, read above;
+#   * the compiled program, the verdict byte and the packed counter bucket as the fixed-slot loop.
+# The program's code is the var flavour with the preloaded window (jit.cpp body, marker varl=1):
+# window loads from v[64:79], bytes at or past LEN zero.
+def jit_statement_varl():
+    out_tail = EPILOGUE[EPILOGUE.index("s_cmp_lg_u64 {ER0}, 0"):EPILOGUE.index(".Lend%=:")]
+    out_tail = out_tail.replace(".Lend%=", ".Loutd%=") + "s_branch .Loutd%="
+    rounds = "\n".join(f"""v_mov_b32 {{t{13 + 2 * r}}}, 0
+v_mov_b32 {{t{12 + 2 * r}}}, {{t{2 + r}}}
+v_lshl_add_u64 {{T{12 + 2 * r}{13 + 2 * r}}}, {{T{12 + 2 * r}{13 + 2 * r}}}, 0, %[k_frames]
+v_add_co_u32 {{t{12 + 2 * r}}}, vcc, {{t{12 + 2 * r}}}, %[c16]
+v_addc_co_u32 {{t{13 + 2 * r}}}, vcc, 0, {{t{13 + 2 * r}}}, vcc
+v_cmp_lt_u32 vcc, %[c16], {{t{8 + r}}}
+v_cndmask_b32 {{t{12 + 2 * r}}}, {{t0}}, {{t{12 + 2 * r}}}, vcc
+v_cndmask_b32 {{t{13 + 2 * r}}}, {{t1}}, {{t{13 + 2 * r}}}, vcc""" for r in range(4))
+    dmas = "\n".join(f"""s_add_u32 m0, %[nwinb], {1024 * r}
+s_nop 0
+global_load_lds_dwordx4 {{T{12 + 2 * r}{13 + 2 * r}}}, off ; @DMAPOLICY@""" for r in range(4))
+    main = """s_mov_b32 {M0S}, m0
+s_movk_i32 %[cdn], 511
+s_mov_b32 %[stage], 0
+.Lloop%=:
+; this tile's windows and the next tile's metadata: landed
+s_waitcnt vmcnt(0)
+v_add_u32 {t0}, %[metab], %[lane4]
+ds_read_b32 {t6}, {t0}
+s_cmp_eq_u32 %[haslen], 0
+s_cbranch_scc1 .Lnl%=
+v_add_u32 {t1}, %[metab], %[lane2]
+ds_read_u16 {t7}, {t1}
+s_branch .Lnld%=
+.Lnl%=:
+v_mov_b32 {t7}, %[lenc]
+.Lnld%=:
+s_mov_b32 {T1L}, %[tile]
+s_mov_b32 {T1H}, 0
+s_lshl_b64 {T1}, {T1}, 6
+v_lshl_add_u64 {T23}, %[lanep], 0, {T1}
+v_cmp_gt_u64 vcc, %[k_n], {T23}
+s_mov_b64 {VM}, vcc
+s_waitcnt lgkmcnt(0)
+v_mov_b32 {LEN}, {t7}
+v_mov_b32 {t7}, 0
+v_lshl_add_u64 {BASE}, %[k_frames], 0, {T67}
+s_cmp_lg_u32 %[xdpf], 0
+s_cbranch_scc0 .Lnx%=
+v_min_u32 {LEN}, 0xffff, {LEN}
+v_add_u32 {LEN}, 8, {LEN}
+v_lshl_add_u64 {BASE}, {BASE}, 0, -8
+.Lnx%=:
+v_cndmask_b32 {LEN}, 0, {LEN}, vcc
+; the next tile
+s_add_u32 {T3}, %[tile], %[W]
+s_cmp_lt_u32 {T3}, %[ntiles]
+s_cbranch_scc0 .Lnonext%=
+s_cmp_lt_u32 {T3}, %[nfull]
+s_cbranch_scc0 .Lstg%=
+v_add_u32 {t0}, %[nmetab], %[lane4]
+ds_read_b32 {t8}, {t0}
+v_add_u32 {t0}, %[nmetab], %[moff]
+ds_read_b32 {t2}, {t0}
+ds_read_b32 {t3}, {t0} offset:64
+ds_read_b32 {t4}, {t0} offset:128
+ds_read_b32 {t5}, {t0} offset:192
+s_cmp_eq_u32 %[haslen], 0
+s_cbranch_scc1 .Lnl2%=
+v_add_u32 {t1}, %[nmetab], %[lane2]
+ds_read_u16 {t9}, {t1}
+v_add_u32 {t1}, %[nmetab], %[loff]
+ds_read_u16 {t10}, {t1}
+ds_read_u16 {t11}, {t1} offset:32
+ds_read_u16 {t12}, {t1} offset:64
+ds_read_u16 {t13}, {t1} offset:96
+s_waitcnt lgkmcnt(0)
+v_mov_b32 {t14}, {t10}
+v_mov_b32 {t15}, {t11}
+v_mov_b32 {t16}, {t12}
+v_mov_b32 {t17}, {t13}
+s_branch .Lnl2d%=
+.Lnl2%=:
+v_mov_b32 {t9}, %[lenc]
+v_mov_b32 {t14}, %[lenc]
+v_mov_b32 {t15}, %[lenc]
+v_mov_b32 {t16}, %[lenc]
+v_mov_b32 {t17}, %[lenc]
+s_waitcnt lgkmcnt(0)
+.Lnl2d%=:
+; every packet of the next tile 16-byte aligned (lanes of length 0 excepted), else stage it
+v_add_u32 {t0}, %[fr_lo], {t8}
+v_and_b32 {t0}, 15, {t0}
+v_cmp_ne_u32 vcc, 0, {t0}
+v_cmp_ne_u32_e64 {T0}, 0, {t9}
+s_and_b64 vcc, vcc, {T0}
+s_cbranch_vccnz .Lstg%=
+v_mov_b32 {t8}, {t14}
+v_mov_b32 {t9}, {t15}
+v_mov_b32 {t10}, {t16}
+v_mov_b32 {t11}, {t17}
+; (chunks wholly past the packet read a dummy address: the micro-op table)
+v_mov_b32 {t0}, %[tp_lo]
+v_mov_b32 {t1}, %[tp_hi]
+""" + rounds + """
+""" + dmas + """
+s_branch .Lmeta%=
+.Lstg%=:
+s_mov_b32 %[stage], 1
+.Lmeta%=:
+; the metadata of nt + W (a whole tile) into this tile's metadata buffer
+s_add_u32 {T3}, {T3}, %[W]
+s_cmp_lt_u32 {T3}, %[nfull]
+s_cbranch_scc0 .Lnonext%=
+s_mov_b32 {T1L}, {T3}
+s_mov_b32 {T1H}, 0
+s_lshl_b64 {T1}, {T1}, 8
+s_add_u32 {T1L}, {T1L}, %[of_lo]
+s_addc_u32 {T1H}, {T1H}, %[of_hi]
+v_mov_b32 {t1}, 0
+v_mov_b32 {t0}, %[lane4]
+v_lshl_add_u64 {T01}, {T01}, 0, {T1}
+s_mov_b32 m0, %[metab]
+s_nop 0
+global_load_lds_dword {T01}, off
+s_cmp_eq_u32 %[haslen], 0
+s_cbranch_scc1 .Lnonext%=
+s_mov_b32 {T1L}, {T3}
+s_mov_b32 {T1H}, 0
+s_lshl_b64 {T1}, {T1}, 7
+s_add_u32 {T1L}, {T1L}, %[ln_lo]
+s_addc_u32 {T1H}, {T1H}, %[ln_hi]
+v_mov_b32 {t1}, 0
+v_mov_b32 {t0}, %[lane4]
+v_lshl_add_u64 {T01}, {T01}, 0, {T1}
+s_add_u32 m0, %[metab], 256
+s_mov_b32 exec_hi, 0
+s_nop 0
+global_load_lds_dword {T01}, off
+s_mov_b64 exec, -1
+.Lnonext%=:
+; this tile's lanes
+s_mov_b32 {KMEM}, %[k_mem]
+s_mov_b64 {KR10}, %[k_r10]
+v_add_u32 {WIN}, %[winb], %[lane64]
+v_mov_b32 {SWZ}, %[swz]
+v_mov_b32 {NST}, 0
+v_mov_b32 {ST}, 0
+v_mov_b32 {LPC}, -1
+s_mov_b64 exec, {VM}
+v_mov_b32 {LPC}, 0
+v_cmp_lt_u32 vcc, {KMEM}, {LEN}
+s_and_b64 exec, exec, vcc
+v_mov_b32 {ST}, 7
+v_mov_b32 {LPC}, -1
+s_mov_b64 exec, -1
+s_cmp_lg_u32 %[initx], 0
+s_cbranch_scc1 .Linitx%=
+;@@JITINIT@@
+.Linitd%=:
+
+; JIT N=%= fixed=0 loops=0 aligned=%[aligned] xdp=%[xdpf] varl=1
+;@@JIT@@
+.Ldone%=:
+; verdict byte, the lane's counter bucket (verdict 0..4, 0xfe -> 5, 0xff -> 6) into %[acc]
+s_mov_b64 exec, {VM}
+v_cmp_gt_u64 vcc, 5, {RF}
+v_mov_b32 {t5}, 0xfe
+v_cndmask_b32 {t4}, {t5}, {RF0}, vcc
+v_cmp_eq_u32 vcc, 0, {ST}
+v_mov_b32 {t5}, 0xff
+v_cndmask_b32 {t4}, {t5}, {t4}, vcc
+v_subrev_u32 {t5}, 0xf9, {t4}
+v_min_u32 {t5}, {t4}, {t5}
+v_mul_u32_u24 {t5}, 9, {t5}
+v_lshlrev_b64 {T67}, {t5}, 1
+v_lshl_add_u64 %[acc], %[acc], 0, {T67}
+v_add_u32 %[ret], %[ret], {NST}
+s_cmp_lg_u64 %[k_verdict], 0
+s_cbranch_scc0 .Lnov%=
+s_lshl_b32 {T0L}, %[tile], 6
+s_lshr_b32 {T0H}, %[tile], 26
+s_add_u32 {T0L}, {T0L}, %[vd_lo]
+s_addc_u32 {T0H}, {T0H}, %[vd_hi]
+v_lshl_add_u64 {T67}, %[lanep], 0, {T0}
+global_store_byte {T67}, {t4}, off
+.Lnov%=:
+s_cmp_lg_u32 %[oflags], 0
+s_cbranch_scc1 .Lout%=
+.Loutd%=:
+s_mov_b64 exec, -1
+s_sub_u32 %[cdn], %[cdn], 1
+s_add_u32 %[tile], %[tile], %[W]
+s_xor_b32 %[winb], %[winb], %[wx]
+s_xor_b32 %[nwinb], %[nwinb], %[wx]
+s_xor_b32 %[metab], %[metab], %[mx]
+s_xor_b32 %[nmetab], %[nmetab], %[mx]
+s_cmp_ge_u32 %[tile], %[ntiles]
+s_cbranch_scc1 .Lexit%=
+s_cmp_lg_u32 %[stage], 0
+s_cbranch_scc1 .Lexit%=
+s_cmp_eq_u32 %[cdn], 0
+s_cbranch_scc0 .Lloop%=
+.Lexit%=:
+s_waitcnt lgkmcnt(0)
+s_mov_b32 m0, {M0S}
+s_branch .Lend%=
+"""
+    ool = """.Linitx%=:
+s_bitcmp1_b32 %[k_flags], 0
+s_cbranch_scc1 .Linitc%=
+""" + DEFAULT_INIT + """s_branch .Linitd%=
+.Linitc%=:
+s_load_dwordx2 {T5}, %[ka], %[o_init]
+s_waitcnt lgkmcnt(0)
+s_load_dwordx16 {UOP}, {T5}, 0x0
+s_waitcnt lgkmcnt(0)
+""" + "\n".join(f"v_mov_b32 v{i}, s{UB + i}" for i in range(16)) + """
+s_load_dwordx4 s[36:39], {T5}, 0x40
+s_load_dwordx2 s[40:41], {T5}, 0x50
+s_waitcnt lgkmcnt(0)
+""" + "\n".join(f"v_mov_b32 v{16 + i}, s{UB + i}" for i in range(6)) + """
+s_branch .Linitd%=
+.Lout%=:
+s_mov_b32 {T1L}, %[tile]
+s_mov_b32 {T1H}, 0
+s_lshl_b64 {T1}, {T1}, 6
+v_lshl_add_u64 {T23}, %[lanep], 0, {T1}
+s_load_dwordx2 {ER0}, %[ka], %[o_r0]
+s_load_dwordx2 {EST}, %[ka], %[o_status]
+s_load_dwordx2 {ERG}, %[ka], %[o_regs]
+s_waitcnt lgkmcnt(0)
+""" + out_tail + """
+.Lend%=:
+"""
+    return main + ool
+
+
 def handler_table():
     """Handler names in slot order and their id: every "alu"/"div"/"ool" kind has a chained (_C)
     and a block-end (_E) form; the others one form (_E); then DONE."""
@@ -1569,6 +1825,13 @@ def main():
         f.write("// GENERATED by gen_tile.py -- do not edit. The compiled fixed-slot kernel's tile "
                 "loop (one statement, many tiles).\n// clang-format off\n" + cstr(text) +
                 "\n// clang-format on\n")
+    # the compiled var kernel's tile loop (jit_statement_varl)
+    text = F(jit_statement_varl())
+    assert "{" not in text, "unsubstituted register name: " + text[text.index("{"):][:40]
+    with open(os.path.join(HERE, "tile_jit_varl.inc"), "w") as f:
+        f.write("// GENERATED by gen_tile.py -- do not edit. The compiled var kernel's tile loop "
+                "(offsets + lens batches, one statement, many tiles).\n// clang-format off\n" +
+                cstr(text) + "\n// clang-format on\n")
     out = ["// GENERATED by gen_tile.py -- do not edit. Per-handler JIT templates (jit.cpp), indexed",
            "// by tile id (tile_ids.h): {main text, out-of-line text}.", "#pragma once",
            "// clang-format off", "static const char* const kJitTemplates[T_COUNT][2] = {"]

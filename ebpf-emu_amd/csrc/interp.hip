@@ -277,29 +277,43 @@ __device__ __forceinline__ uint32_t stride_len(const LaunchArgs& a) {
 }
 
 // DMA the offsets / lengths of tile t into meta buffer b (lanes past the batch read a dummy).
+// PK (the compiled forward var kernels, tile_body PLEN): the buffer holds the offsets, then the
+// lengths packed as u16[64] (128 bytes instead of 64 zero-extended dword slots); b must be 0 (L
+// names the buffer). A whole tile of 4-byte aligned lengths moves as 32 dwords (lanes 0..31);
+// the batch's partial last tile and unaligned length arrays store them lane by lane.
+template <bool PK = false>
 __device__ __forceinline__ void dma_meta(const LaunchArgs& a, const WaveLds& L, uint32_t b,
                                          uint64_t t, uint32_t lane) {
   const uint64_t pkt = t * kWave + lane;
   const bool ok = t < a.n_tiles && pkt < a.n;
   if (a.offsets)
     dma_x1(ok ? (uintptr_t)(a.offsets + pkt) : (uintptr_t)a.prog, lds_addr(L.meta_off + b * kWave));
-  if (a.lens)
+  if (!a.lens) return;
+  if (!PK) {
     dma_u16(ok ? (uintptr_t)(a.lens + pkt) : (uintptr_t)a.prog, lds_addr(L.meta_len + b * kWave));
+  } else if (t < a.n_tiles && (t + 1) * kWave <= a.n && ((uintptr_t)a.lens & 3) == 0) {
+    if (lane < kWave / 2) dma_x1((uintptr_t)(a.lens + t * kWave) + 4 * lane, lds_addr(L.meta_len));
+  } else {
+    ((uint16_t*)L.meta_len)[lane] = ok ? a.lens[pkt] : (uint16_t)0;
+  }
 }
 
 // Packet j of tile t, from meta buffer b: base address and length (0 for j past the batch).
+template <bool PK = false>
 __device__ __forceinline__ void meta_of(const LaunchArgs& a, const WaveLds& L, uint32_t b,
                                         uint64_t t, uint32_t j, uintptr_t& base, uint32_t& len) {
   const uint64_t pkt = t * kWave + j;
   const bool ok = pkt < a.n;
   base = (uintptr_t)a.frames + (a.offsets ? (uint64_t)L.meta_off[b * kWave + j] : pkt * a.stride);
-  len = ok ? (a.lens ? (L.meta_len[b * kWave + j] & 0xffffu) : stride_len(a)) : 0u;
+  const uint32_t ml = PK ? (uint32_t)((const uint16_t*)L.meta_len)[j] : L.meta_len[b * kWave + j];
+  len = ok ? (a.lens ? (ml & 0xffffu) : stride_len(a)) : 0u;
 }
 
 // DMA tile t's 64 header windows (metadata in buffer mb) into window buffer wb: round r moves
 // packets 16r..16r+15, lane l filling chunk slot (l & 3) of packet 16r + l/4 from logical chunk
 // (l & 3) ^ swz. Chunks wholly past the packet's end read a dummy address instead (never a byte
 // past a valid 16-byte chunk).
+template <bool PK = false>
 __device__ __forceinline__ void dma_window(const LaunchArgs& a, const WaveLds& L, uint32_t mb,
                                            uint32_t wb, uint64_t t, uint32_t lane) {
 #pragma unroll
@@ -307,7 +321,7 @@ __device__ __forceinline__ void dma_window(const LaunchArgs& a, const WaveLds& L
     const uint32_t j = r * 16 + (lane >> 2);
     uintptr_t bj;
     uint32_t lj;
-    meta_of(a, L, mb, t, j, bj, lj);
+    meta_of<PK>(a, L, mb, t, j, bj, lj);
     const uint32_t c = (lane & 3) ^ win_swz(j);
     const uintptr_t src = (c * 16 < lj) ? bj + c * 16 : (uintptr_t)a.prog;
     dma_x4(src, lds_addr(L.win + wb * kWinBytes + r * 1024));
@@ -1420,6 +1434,16 @@ hipError_t launch_xdp_stage(const uint8_t* frames, const uint32_t* offsets, cons
 constexpr uint32_t kTileWaveLds = kWinBytes + kDagMetaBytes;  // window + metadata, 4.5 KiB
 constexpr uint32_t kTileWaveLdsPipe = kWinBytes + 2 * kDagMetaBytes;  // two metadata buffers, 5 KiB
 constexpr uint32_t kTileWaveLdsDb3 = 2 * kWinBytes + 3 * kDagMetaBytes;  // DB: 9.5 KiB
+// the compiled forward var kernels (tile_body PLEN): metadata buffers with packed u16 lengths
+// (dma_meta<true>), 384 bytes each -- a wave's window and two buffers take 4864 bytes, so eight
+// 4-wave workgroups and their 80 bytes of static counters fit a CU's 160 KiB of LDS (5 KiB buffers
+// left room for seven)
+constexpr uint32_t kVarMetaBytes = kWave * 4 + kWave * 2;
+constexpr uint32_t kVarWaveLds = kWinBytes + 2 * kVarMetaBytes;       // 4.75 KiB
+constexpr uint32_t kVarWaveLdsDb3 = 2 * kWinBytes + 3 * kVarMetaBytes;  // DB: 9.1 KiB
+// ebpf_tile_jit_varl: two windows and two packed metadata buffers per wave, 8.75 KiB (4 workgroups
+// of 4 waves per CU)
+constexpr uint32_t kVarlWaveLds = 2 * kWinBytes + 2 * kVarMetaBytes;
 // the var kernels' metadata pipeline: on unless the launch asks otherwise (A/B, LaunchArgs.var_pipe)
 __device__ __forceinline__ bool g_var_pipe(const LaunchArgs& a) { return a.var_nopipe == 0; }
 
@@ -1428,6 +1452,7 @@ __device__ __forceinline__ bool g_var_pipe(const LaunchArgs& a) { return a.var_n
 #define TILE_ASM_IN \
           [ka] "s"(ka), [tile] "s"(t), [winb] "s"(winb), [metab] "s"(metab), \
           [fixed] "i"(FIXED ? 1 : 0), [loops] "i"(LOOPS ? 1 : 0), [aligned] "s"(rfl(aligned)), \
+          [plen] "i"(PLEN ? 1 : 0), \
           [o_xdp] "i"(offsetof(LaunchArgs, xdp)), \
           [o_tprog] "i"(offsetof(LaunchArgs, tprog)), \
           [o_tprog_exact] "i"(offsetof(LaunchArgs, tprog_exact)), \
@@ -1489,18 +1514,24 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
   // fixed-slot kernel's scheme, with the metadata one tile further ahead). Measured slower than
   // the metadata prefetch alone: 9.5 KiB of LDS per wave leaves 4 waves per SIMD instead of 7.
   constexpr bool PIPE = JIT && !FIXED;
+  // PLEN: the compiled forward var kernels' packed-length metadata buffers (dma_meta<true>; the
+  // statement's prologue reads the lengths as u16, gen_tile.py %[plen])
+  constexpr bool PLEN = JIT && !FIXED && !LOOPS;
   const bool pipe = PIPE && g_var_pipe(a) && !(LOOPS && a.perm);
   const bool db = PIPE && !LOOPS && pipe && a.var_db != 0;
   const uint32_t nmeta = db ? 3u : 2u;
+  constexpr uint32_t kMetaStride = PLEN ? kVarMetaBytes / 4 : 2 * kWave;  // (u32 units)
   WaveLds L;
-  L.win = smem + wv * (db ? kTileWaveLdsDb3 : PIPE ? kTileWaveLdsPipe : kTileWaveLds);
+  L.win = smem + wv * (PLEN ? (db ? kVarWaveLdsDb3 : kVarWaveLds)
+                            : db ? kTileWaveLdsDb3 : PIPE ? kTileWaveLdsPipe : kTileWaveLds);
   L.meta_off = (uint32_t*)(L.win + (db ? 2 : 1) * kWinBytes);
   L.meta_len = L.meta_off + kWave;
-  // window buffer w and metadata buffer m of this wave (512 bytes each: offsets, then lengths)
+  // window buffer w and metadata buffer m of this wave (offsets, then lengths: 512 bytes each, or
+  // 384 with PLEN)
   auto bufs = [&](uint32_t w, uint32_t m) {
     WaveLds x;
     x.win = L.win + w * kWinBytes;
-    x.meta_off = L.meta_off + m * 2 * kWave;
+    x.meta_off = L.meta_off + m * kMetaStride;
     x.meta_len = x.meta_off + kWave;
     return x;
   };
@@ -1514,9 +1545,9 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
     }
     uintptr_t pb;
     uint32_t ml;
-    meta_of(a, X, 0, t, lane, pb, ml);
+    meta_of<PLEN>(a, X, 0, t, lane, pb, ml);
     const bool ok = ballot(t * kWave + lane < a.n && ml != 0 && (pb & 15) != 0) == 0;
-    if (ok) dma_window(a, X, 0, 0, t, lane);
+    if (ok) dma_window<PLEN>(a, X, 0, 0, t, lane);
     return ok;
   };
   uint32_t mb = 0;      // PIPE: the metadata buffer of the current tile (0 .. nmeta - 1)
@@ -1533,8 +1564,14 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
   // packet length and the hardware ids
   // (the forward var kernels, tools/trace_var.py: window ready / statement done of each of the
   // wave's first five tiles in slots 1 + 2i / 2 + 2i, its tile count in slot 15)
+  // (the var kernels' stamps cost registers: built only with -DEBPFEMU_VAR_TRACE, tools/trace_var.py)
+#ifdef EBPFEMU_VAR_TRACE
+  constexpr bool kTraceHere = JIT;
+#else
+  constexpr bool kTraceHere = JIT && LOOPS;
+#endif
   uint64_t* const trace =
-      JIT && a.trace && wave_slot < kTraceWaves ? a.trace + wave_slot * kTraceSlots : nullptr;
+      kTraceHere && a.trace && wave_slot < kTraceWaves ? a.trace + wave_slot * kTraceSlots : nullptr;
   uint32_t ti = 0;  // (var trace: the wave's tile ordinal)
   auto stamp = [&](uint32_t slot) {
     uint64_t ts;
@@ -1546,11 +1583,11 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
   if (pipe && wave_slot < a.n_tiles) {  // the first tile's metadata (DB: and its windows)
     uint32_t lane;
     asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
-    dma_meta(a, L, 0, wave_slot, lane);
+    dma_meta<PLEN>(a, L, 0, wave_slot, lane);
     if (db) {
       dma_wait();
       cur_dma = issue_window(wave_slot, bufs(0, 0), lane);
-      if (wave_slot + total_waves < a.n_tiles) dma_meta(a, bufs(0, 1), 0, wave_slot + total_waves, lane);
+      if (wave_slot + total_waves < a.n_tiles) dma_meta<PLEN>(a, bufs(0, 1), 0, wave_slot + total_waves, lane);
     }
   }
   for (uint64_t tile = wave_slot; tile < a.n_tiles;) {
@@ -1569,7 +1606,7 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
       const bool valid = t0 * kWave + lane < a.n;
       uintptr_t pb;
       uint32_t ml;
-      meta_of(a, Lc, 0, t0, lane, pb, ml);
+      meta_of<PLEN>(a, Lc, 0, t0, lane, pb, ml);
       if (!cur_dma)
         stage_window_lane(Lc.win + lane * kWin, win_swz(lane), (const uint8_t*)pb,
                           valid ? ml : 0u, valid);
@@ -1577,7 +1614,7 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
       if (t1 < a.n_tiles) {  // tile t1's windows, tile t2's metadata: in flight while t0 runs
         const uint32_t m1 = mb + 1 == nmeta ? 0u : mb + 1, m2 = m1 + 1 == nmeta ? 0u : m1 + 1;
         const bool nxt = issue_window(t1, bufs(wi ^ 1u, m1), lane);
-        if (t1 + total_waves < a.n_tiles) dma_meta(a, bufs(0, m2), 0, t1 + total_waves, lane);
+        if (t1 + total_waves < a.n_tiles) dma_meta<PLEN>(a, bufs(0, m2), 0, t1 + total_waves, lane);
         cur_dma = nxt;
       }
       if (a.xdp) xdp_window(Lc.win + lane * kWin, win_swz(lane), ml);
@@ -1597,18 +1634,18 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
         if (a.lens)
           dma_u16(valid ? (uintptr_t)(a.lens + src) : (uintptr_t)a.prog, lds_addr(L.meta_len));
       } else {
-        dma_meta(a, L, 0, tile, lane);
+        dma_meta<PLEN>(a, L, 0, tile, lane);
       }
       if (sw) dma_window_stride(a, L.win, tile, lane);
       dma_wait();
       uintptr_t pb;
       uint32_t ml;
-      meta_of(a, Lc, 0, tile, lane, pb, ml);
+      meta_of<PLEN>(a, Lc, 0, tile, lane, pb, ml);
       const bool co = sw || ballot(valid && ml != 0 && (pb & 15) != 0) == 0;
       aligned = co ? 1u : 0u;
       if (co) {
         if (!sw) {
-          dma_window(a, Lc, 0, 0, tile, lane);
+          dma_window<PLEN>(a, Lc, 0, 0, tile, lane);
           dma_wait();
         }
       } else {
@@ -1620,7 +1657,7 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
       // PIPE: the next tile's metadata into the other buffer (last read by the previous tile's
       // statement, which has finished), landing while this tile runs
       const uint64_t ntl = rfl64(tile) + total_waves;
-      if (pipe && ntl < a.n_tiles) dma_meta(a, bufs(0, mb ^ 1u), 0, ntl, lane);
+      if (pipe && ntl < a.n_tiles) dma_meta<PLEN>(a, bufs(0, mb ^ 1u), 0, ntl, lane);
     }
     const uint64_t t = rfl64(tile);
     const uint64_t nt = t + total_waves;
@@ -1631,7 +1668,7 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
       if (!FIXED && threadIdx.x % kWave == 0) {
         uintptr_t mb;
         uint32_t ml;
-        meta_of(a, Lc, 0, tile, 0, mb, ml);
+        meta_of<PLEN>(a, Lc, 0, tile, 0, mb, ml);
         trace[4] = ml;
       }
     }
@@ -1670,7 +1707,7 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
       if (slot < a.n) {
         uintptr_t mb;
         uint32_t ml;
-        meta_of(a, Lc, 0, tile, ln, mb, ml);
+        meta_of<PLEN>(a, Lc, 0, tile, ln, mb, ml);
         // (xdp_md in place: the image is the packet 8 bytes further on, behind its ctx)
         const uint32_t len = a.xdp ? min(ml, 0xffffu) + 8u : ml;
         const uint8_t* base = (const uint8_t*)mb - (a.xdp ? 8 : 0);
@@ -1851,6 +1888,129 @@ extern "C" __global__ __launch_bounds__(kDbBlock, 1) void ebpf_tile_jit_fixed(La
 }
 extern "C" __global__ __launch_bounds__(kBlock, 7) void ebpf_tile_jit_var(LaunchArgs a) {
   tile_body<false, false, true>(a);
+}
+// ebpf_tile_jit_varl: offsets + lens batches (varl_ok in launch_interp: offsets present, lengths
+// 4-byte aligned or absent, no final images, n_tiles < 2^31) -- the wave's tiles tile, tile + W,
+// ... in one asm statement (tile_jit_varl.inc, gen_tile.py jit_statement_varl) with two window
+// buffers and two packed metadata buffers per wave (kVarlWaveLds; 4 workgroups of 4 waves per
+// CU), so a tile's windows are in flight while the one before it runs. The C++ here only starts
+// the wave's first tile, stages the windows of a tile the statement hands back (misaligned
+// packets, the batch's partial last tile) and unpacks the per-lane packed counter buckets.
+extern "C" __global__ __launch_bounds__(kBlock, 4) void ebpf_tile_jit_varl(LaunchArgs a) {
+  counters_init();
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint32_t wv = rfl(threadIdx.x / kWave);
+  uint8_t* const wbase = smem + wv * kVarlWaveLds;  // [window 0][window 1][metadata 0][metadata 1]
+  uint32_t winb = lds_addr(wbase), nwinb = winb + kWinBytes;
+  uint32_t metab = lds_addr(wbase + 2 * kWinBytes), nmetab = metab + kVarMetaBytes;
+  const uint32_t win0 = winb, meta0 = metab;
+  const uint32_t wx = winb ^ nwinb, mx = metab ^ nmetab;
+  uint32_t lane;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+  // per-lane constants of the statement: its own metadata (offset, packed length), the window
+  // DMA's (packet 16r + l/4's offset and length at +64r / +32r, the chunk it moves), its window
+  const uint32_t lane4 = lane * 4, lane2 = 256 + lane * 2, moff = lane & ~3u;
+  const uint32_t loff = 256 + ((lane >> 2) << 1), c16 = ((lane & 3u) ^ ((lane >> 4) & 3u)) * 16u;
+  const uint32_t lane64 = lane << 6, swz = ((lane >> 2) & 3u) << 4;
+  const uint64_t lanep = lane;
+  const uint32_t W = gridDim.x * kWavesPerBlock;
+  const uint32_t ntiles = rfl((uint32_t)a.n_tiles), nfull = rfl((uint32_t)(a.n / kWave));
+  const uint32_t haslen = rfl(a.lens ? 1u : 0u), xdpf = rfl(a.xdp);
+  const uint32_t lenc = rfl(stride_len(a));
+  const uint32_t kflags = rfl((a.init_regs ? 1u : 0u) | (a.r0 ? 2u : 0u) | (a.status ? 4u : 0u) |
+                              (a.regs_out ? 8u : 0u));
+  const uint32_t initx = rfl(kflags & 9u), oflags = rfl(kflags & 14u), one = 1;
+  const uint64_t ka = (uint64_t)__builtin_amdgcn_kernarg_segment_ptr();
+  // the wave's current window / metadata buffers as generic pointers (staging)
+  auto buf = [&](uint32_t wb, uint32_t mb) {
+    WaveLds x;
+    x.win = wbase + (wb == win0 ? 0u : kWinBytes);
+    x.meta_off = (uint32_t*)(wbase + 2 * kWinBytes + (mb == meta0 ? 0u : kVarMetaBytes));
+    x.meta_len = x.meta_off + kWave;
+    return x;
+  };
+  // tile t's windows into X, lane by lane (its metadata in X; a partial tile's is fetched here)
+  auto stage = [&](uint32_t t, const WaveLds& X) {
+    if ((uint64_t)(t + 1) * kWave > a.n) {
+      dma_meta<true>(a, X, 0, t, lane);
+      dma_wait();
+    }
+    uintptr_t pb;
+    uint32_t ml;
+    meta_of<true>(a, X, 0, t, lane, pb, ml);
+    const bool valid = (uint64_t)t * kWave + lane < a.n;
+    stage_window_lane(X.win + lane * kWin, win_swz(lane), (const uint8_t*)pb, valid ? ml : 0u,
+                      valid);
+  };
+
+  uint32_t cnt[7] = {0, 0, 0, 0, 0, 0, 0};
+  uint64_t retired = 0;
+  uint32_t tile = blockIdx.x * kWavesPerBlock + wv;
+  if (tile < ntiles) {
+    // the first tile: its metadata, then its windows (DMA'd when whole and aligned), then the
+    // next tile's metadata, in flight at the statement's first wait
+    const WaveLds X = buf(winb, metab);
+    dma_meta<true>(a, X, 0, tile, lane);
+    dma_wait();
+    uintptr_t pb;
+    uint32_t ml;
+    meta_of<true>(a, X, 0, tile, lane, pb, ml);
+    const bool whole = (uint64_t)(tile + 1) * kWave <= a.n;
+    if (whole && ballot(ml != 0 && (pb & 15) != 0) == 0) dma_window<true>(a, X, 0, 0, tile, lane);
+    else stage(tile, X);
+    if (tile + W < ntiles) dma_meta<true>(a, buf(nwinb, nmetab), 0, tile + W, lane);
+  }
+  while (tile < ntiles) {
+    uint64_t acc = 0;
+    uint32_t ret = 0, cdn, stg;
+    asm volatile(
+#include "tile_jit_varl.inc"
+        : [tile] "+s"(tile), [winb] "+s"(winb), [nwinb] "+s"(nwinb), [metab] "+s"(metab),
+          [nmetab] "+s"(nmetab), [acc] "+v"(acc), [ret] "+v"(ret), [cdn] "=&s"(cdn),
+          [stage] "=&s"(stg)
+        : [ka] "s"(ka), [k_frames] "s"(a.frames), [fr_lo] "s"((uint32_t)(uintptr_t)a.frames),
+          [of_lo] "s"((uint32_t)(uintptr_t)a.offsets),
+          [of_hi] "s"((uint32_t)((uintptr_t)a.offsets >> 32)),
+          [ln_lo] "s"((uint32_t)(uintptr_t)a.lens), [ln_hi] "s"((uint32_t)((uintptr_t)a.lens >> 32)),
+          [tp_lo] "s"((uint32_t)(uintptr_t)a.tprog), [tp_hi] "s"((uint32_t)((uintptr_t)a.tprog >> 32)),
+          [k_n] "s"(a.n), [k_mem] "s"(a.mem_size), [k_r10] "s"(a.r10), [k_verdict] "s"(a.verdict),
+          [vd_lo] "s"((uint32_t)(uintptr_t)a.verdict),
+          [vd_hi] "s"((uint32_t)((uintptr_t)a.verdict >> 32)), [k_flags] "s"(kflags),
+          [initx] "s"(initx), [oflags] "s"(oflags), [W] "s"(W), [ntiles] "s"(ntiles),
+          [nfull] "s"(rfl(nfull)), [haslen] "s"(rfl(haslen)), [lenc] "s"(rfl(lenc)),
+          [xdpf] "s"(rfl(xdpf)),
+          [wx] "s"(wx), [mx] "s"(mx), [lane4] "v"(lane4), [lane2] "v"(lane2), [moff] "v"(moff),
+          [loff] "v"(loff), [c16] "v"(c16), [lane64] "v"(lane64), [swz] "v"(swz),
+          [lanep] "v"(lanep), [aligned] "s"(rfl(one)), [fixed] "i"(0), [loops] "i"(0),
+          [o_init] "i"(offsetof(LaunchArgs, init_regs)), [o_r0] "i"(offsetof(LaunchArgs, r0)),
+          [o_status] "i"(offsetof(LaunchArgs, status)),
+          [o_regs] "i"(offsetof(LaunchArgs, regs_out))
+        : TILE_ASM_CLOBBER, TILE_ASM_CLOBBER_WINDOW);
+    // (scalar loop state back through readfirstlane: the statement has VGPR outputs)
+    tile = rfl(tile);
+    winb = rfl(winb);
+    nwinb = rfl(nwinb);
+    metab = rfl(metab);
+    nmetab = rfl(nmetab);
+    stg = rfl(stg);
+#pragma unroll
+    for (int b = 0; b < 7; b += 2) {
+      const uint32_t q = (uint32_t)(acc >> (9 * b)) & 511u;
+      const uint32_t s =
+          wave_sum_u32(b < 6 ? q | ((uint32_t)(acc >> (9 * b + 9)) & 511u) << 16 : q);
+      cnt[b] += s & 0xffffu;
+      if (b < 6) cnt[b + 1] += s >> 16;
+    }
+    retired += wave_sum_u32(ret);
+    if (tile < ntiles && stg) {  // a tile the statement hands back: stage its windows
+      dma_wait();                // (the next tile's metadata)
+      stage(tile, buf(winb, metab));
+    }
+  }
+  uint64_t cnt64[7];
+#pragma unroll
+  for (int b = 0; b < 7; b++) cnt64[b] = cnt[b];
+  flush_counters<kWavesPerBlock, true>(a, cnt64, retired, smem, lane, wv);
 }
 // stack-window programs (memory tier 0.5) on offsets + lens, stride + lens and xdp_md batches:
 // the var kernel with the preloaded header window and the stack window in v[64:95]
@@ -2084,9 +2244,24 @@ static bool jit_forward_for(int kind, uint32_t n_uops) {
   return kind == kKindDag && (n_uops > kTileMaxUops || tile_kernel_for(kind, n_uops));
 }
 
+// The var tile loop (ebpf_tile_jit_varl) takes a compiled forward program's var-kernel batches
+// with offsets (4-byte aligned), lengths 4-byte aligned or absent, no final images or deopt list,
+// and tile indices in 31 bits. EBPFEMU_VARL=0 keeps ebpf_tile_jit_var (A/B).
+static bool g_varl = [] {
+  const char* e = getenv("EBPFEMU_VARL");
+  return !(e && e[0] == '0');
+}();
+static bool varl_ok(int kind, const LaunchArgs& a, const JitFns* jit, bool stack) {
+  return g_varl && jit && jit->varl && !stack && !jit->var_only && kind == kKindDag &&
+         jit_forward_for(kind, a.n_uops) && a.offsets && ((uintptr_t)a.offsets & 3) == 0 &&
+         ((uintptr_t)a.lens & 3) == 0 && !a.mem_out && !a.deopt && !a.perm &&
+         a.n_tiles < (1ull << 31);
+}
+
 int launch_kernel_id(int kind, const LaunchArgs& a, const JitFns* jit, bool stack) {
   if (jit && jit->loop && kind == kKindLoop)
     return stack ? EBPF_KERNEL_JIT_LOOP_STACK : EBPF_KERNEL_JIT_LOOP;
+  if (varl_ok(kind, a, jit, stack)) return EBPF_KERNEL_JIT_VARL;
   if (jit && jit->fixed && jit_forward_for(kind, a.n_uops))
     return jit_fixed_layout(&a) && !jit->var_only
                ? (stack ? EBPF_KERNEL_JIT_STACK : EBPF_KERNEL_JIT_FIXED)
@@ -2134,8 +2309,17 @@ hipError_t launch_interp(int kind, const LaunchArgs& a, int grid, hipStream_t st
   const bool var = jit && jit->fixed && kind != kKindLoop && jit_forward_for(kind, a.n_uops) &&
                    (!jit_fixed_layout(&a) || jit->var_only);
   const bool vdb = g_var_db && g_var_pipe_host;
-  const uint32_t vlds = g_lds_pad + kWavesPerBlock * (vdb ? kTileWaveLdsDb3 : kTileWaveLdsPipe);
+  const uint32_t vlds = g_lds_pad + kWavesPerBlock * (vdb ? kVarWaveLdsDb3 : kVarWaveLds);
   if (var && (g_var_grid || vdb)) grid = jit_grid(stack ? jit->var_stack : jit->var, vlds, a.n_tiles);
+  const bool vl = varl_ok(kind, a, jit, stack);
+  const uint32_t llds = g_lds_pad + kWavesPerBlock * kVarlWaveLds;
+  if (vl) {
+    grid = jit_grid(jit->varl, llds, a.n_tiles);
+    // (tests: EBPFEMU_VARL_WGS caps the workgroups, so a moderate batch gives each wave more than
+    // the 511 tiles of one statement entry)
+    const char* cap = getenv("EBPFEMU_VARL_WGS");
+    if (cap && atoi(cap) > 0 && atoi(cap) < grid) grid = atoi(cap);
+  }
   LaunchArgs b = a;
   b.var_nopipe = (kind == kKindLoop ? g_loop_pipe : g_var_pipe_host) ? 0u : 1u;
   b.var_db = var && vdb ? 1u : 0u;
@@ -2153,6 +2337,8 @@ hipError_t launch_interp(int kind, const LaunchArgs& a, int grid, hipStream_t st
   if (jit && jit->loop && kind == kKindLoop) {  // the compiled loop program
     e = hipModuleLaunchKernel(stack ? jit->loop_stack : jit->loop, grid, 1, 1, kBlock, 1, 1, lds,
                               stream, bargs, nullptr);
+  } else if (vl) {  // offsets + lens batches: the var tile loop
+    e = hipModuleLaunchKernel(jit->varl, grid, 1, 1, kBlock, 1, 1, llds, stream, bargs, nullptr);
   } else if (jit && jit->fixed && jit_forward_for(kind, a.n_uops)) {
     if (jit_fixed_layout(&a) && !jit->var_only) {  // double-buffered windows: its own LDS size and grid
       const uint32_t dlds = g_lds_pad + kDbWaves * kTileWaveLdsDb;

@@ -54,6 +54,8 @@ struct Marker {
   std::string xdp;  // the SGPR holding LaunchArgs::xdp (the xdp_md convention in place)
   bool stack = false;  // the var kernel's statement for stack-window programs
   bool deep = false;   // the deep-prefetch loop kernel's statement
+  bool varl = false;   // the var tile loop's statement (ebpf_tile_jit_varl): the var flavour of
+                       // loads with the preloaded window, as the stack statement's
 };
 
 bool inline_const(int64_t v) { return v >= -16 && v <= 64; }
@@ -94,6 +96,7 @@ bool find_markers(const std::string& s, std::vector<Marker>& out) {
     m.xdp = field("xdp=");
     m.stack = field("stack=") == "1";
     m.deep = field("deep=") == "1";
+    m.varl = field("varl=") == "1";
     const size_t mk = s.find(";@@JIT@@", eol);
     if (mk == std::string::npos || m.n.empty()) return false;
     const size_t ik = s.rfind(";@@JITINIT@@", pos);
@@ -2866,10 +2869,10 @@ struct Compiler {
       main += ldxk_fast(i);
       return true;
     }
-    if (!loops && (m.fixed == "1" || m.stack) &&
+    if (!loops && (m.fixed == "1" || m.stack || m.varl) &&
         (id == T_LDX_C || id == T_LDX_E || id == T_LDX1_C || id == T_LDX1_E)) {
       std::string ot;
-      main += ldx_fixed(i, id == T_LDX1_C || id == T_LDX1_E, P, ot, m.stack);
+      main += ldx_fixed(i, id == T_LDX1_C || id == T_LDX1_E, P, ot, m.stack || m.varl);
       ool += ot;
       return true;
     }
@@ -2991,13 +2994,13 @@ struct Compiler {
     // LDS, before any window read (LDS operations of a wave complete in order)
     bool reads_window = false;
     for (const Uop& o : uops) reads_window = reads_window || o.op == U_LDX;
-    if (m.fixed == "1" && reads_window && !m.xdp.empty())
+    if ((m.fixed == "1" || m.varl) && reads_window && !m.xdp.empty())
       main += "s_cmp_lg_u32 " + m.xdp + ", 0\ns_cbranch_scc0 .L" + P + "noxdp\n" + xdp_shift() +
               ".L" + P + "noxdp:\n";
     std::string ool;
     if (stk && m.stack) main += stack_init(P, ool);
     uint32_t chunks = 0, maxend = 0;
-    if (m.fixed == "1" || m.stack)
+    if (m.fixed == "1" || m.stack || m.varl)
       for (uint32_t i = 0; i < n; i++) {
         const TUop& u = t[i];
         if (!is_ldxk(u.hoff / TILE_SLOT)) continue;
@@ -3023,7 +3026,7 @@ struct Compiler {
           main += "v_xad_u32 v36, v35, " + std::to_string(16 * c) + ", v34\nds_read_b128 v[" +
                   std::to_string(64 + 4 * c) + ":" + std::to_string(67 + 4 * c) + "], v36\n";
       main += "s_waitcnt lgkmcnt(0)\n";
-      if (m.stack) {  // var layouts: the preloaded bytes at or past LEN are zeros (main.rs:16),
+      if (m.stack || m.varl) {  // var layouts: the preloaded bytes at or past LEN are zeros (main.rs:16),
                       // skipped when every lane's packet covers the window
         const std::string D = ".L" + F + "pmd";
         main += "v_cmp_gt_u32 vcc, 64, v31\ns_cbranch_vccz " + D + "\n";
@@ -3407,7 +3410,8 @@ bool jit_load(const std::vector<char>& co, hipModule_t* mod, JitFns* fns) {
       hipModuleGetFunction(&f.loop, m, "ebpf_tile_jit_loop") != hipSuccess ||
       hipModuleGetFunction(&f.var_stack, m, "ebpf_tile_jit_var_stack") != hipSuccess ||
       hipModuleGetFunction(&f.loop_stack, m, "ebpf_tile_jit_loop_stack") != hipSuccess ||
-      hipModuleGetFunction(&f.loop_deep, m, "ebpf_tile_jit_loop_deep") != hipSuccess) {
+      hipModuleGetFunction(&f.loop_deep, m, "ebpf_tile_jit_loop_deep") != hipSuccess ||
+      hipModuleGetFunction(&f.varl, m, "ebpf_tile_jit_varl") != hipSuccess) {
     (void)hipModuleUnload(m);
     return false;
   }

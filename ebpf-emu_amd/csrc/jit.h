@@ -20,6 +20,7 @@ struct JitFns {
   hipFunction_t var_stack = nullptr;  // stack-window programs, other layouts (ebpf_tile_jit_var_stack)
   hipFunction_t loop_stack = nullptr;  // stack-window loop programs (ebpf_tile_jit_loop_stack)
   hipFunction_t loop_deep = nullptr;  // loop programs with the deep refill prefetch
+  hipFunction_t varl = nullptr;  // offsets + lens batches: the var tile loop (ebpf_tile_jit_varl)
   // the program's code exists for the var kernels only (store mode: register-address stores into
   // the packet, StackPlan::any_dyn), whatever the batch layout
   bool var_only = false;

@@ -219,6 +219,9 @@ int ebpf_run_batch(ebpf_prog* prog, const ebpf_batch* batch, const ebpf_batch_ou
                                         (ebpf_tile_jit_var_stack) */
 #define EBPF_KERNEL_JIT_LOOP_STACK 10 /* compiled stack-window loop program
                                          (ebpf_tile_jit_loop_stack) */
+#define EBPF_KERNEL_JIT_VARL   11 /* compiled program, offsets + lens batches: the var tile loop
+                                    (ebpf_tile_jit_varl; offsets and lens 4-byte aligned, no
+                                    final images) */
 int ebpf_batch_kernel(ebpf_prog* prog, const ebpf_batch* batch, const ebpf_batch_out* out,
                       int device);
 

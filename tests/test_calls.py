@@ -87,7 +87,7 @@ def test_call_programs_directed(cuda, oracle_mod):
 
     rng = random.Random(1)
     pkts = [gen_packet(rng) for _ in range(130)]
-    fwd = (_lib.EBPF_KERNEL_JIT_VAR, _lib.EBPF_KERNEL_JIT_FIXED)
+    fwd = (_lib.EBPF_KERNEL_JIT_VAR, _lib.EBPF_KERNEL_JIT_VARL, _lib.EBPF_KERNEL_JIT_FIXED)
     for src, kern in ((NESTED, fwd), (RECURSE, fwd), (RECURSE_BIG, (_lib.EBPF_KERNEL_GENERAL_T1,))):
         img = assemble(src)
         p = Program(img)

@@ -1,0 +1,231 @@
+"""The var tile loop (ebpf_tile_jit_varl): offsets + lens batches -- a capture's
+or a NIC ring's layout -- of compiled forward programs, the wave's tiles in one asm statement with
+double-buffered windows. Every output against the C oracle (oracle/, restating emu.rs / mmu.rs /
+main.rs) and against the general interpreter on the same batch, bit-exact: aligned tiles (LDS-DMA
+windows), misaligned and partial tiles (handed back to the C++ and staged lane by lane), packets
+shorter than the window, lengths absent, init_regs / r0 / status / register outputs, xdp_md in
+place, and a wave running more than the 511 tiles of one statement entry."""
+import os
+import random
+
+import numpy as np
+import pytest
+
+from fuzzgen import gen_packet, gen_program
+from test_gpu_parity import STEPS, _check_prod_against_oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _mixed(pkts, dev, bad_every=0, lens=True):
+    """Offsets layout, every packet 16-byte aligned except each bad_every-th one (at +3): a tile
+    holding one is staged. Returns (frames, kwargs)."""
+    import torch
+
+    offs, pos, chunks = [], 0, []
+    for i, p in enumerate(pkts):
+        want = 3 if bad_every and i % bad_every == bad_every - 1 else 0
+        pad = (want - pos) % 16
+        chunks.append(bytes(pad))
+        pos += pad
+        offs.append(pos)
+        chunks.append(p)
+        pos += len(p)
+    buf = b"".join(chunks) + bytes(16)
+    frames = torch.tensor(np.frombuffer(buf, dtype=np.uint8).copy(), device=dev)
+    kw = dict(n=len(pkts), offsets=torch.tensor(np.array(offs, dtype=np.uint32).view(np.int32),
+                                                 device=dev))
+    if lens:
+        ln = np.array([len(p) for p in pkts], dtype=np.uint16)
+        kw["lens"] = torch.tensor(ln.view(np.int16), device=dev)
+    return frames, kw
+
+
+def _route(prog, frames, kw, **extra):
+    return prog.batch_kernel(prog.make_batch(frames, **kw, **extra))
+
+
+def _outputs(prog, frames, kw, dev, generic=False, regs=False, **extra):
+    import torch
+
+    cnt = torch.zeros(8, dtype=torch.int64, device=dev)
+    v = prog.run(frames, max_steps=STEPS, verdict=True, counters=cnt, generic=generic, **kw,
+                 **extra)
+    rs = prog.run(frames, max_steps=STEPS, verdict=False, r0=True, status=True, regs=regs,
+                  generic=generic, **kw, **extra)
+    torch.cuda.synchronize()
+    out = dict(verdict=v.verdict.cpu().numpy(), counters=cnt.cpu().numpy().view(np.uint64),
+               r0=rs.r0.cpu().numpy().view(np.uint64), status=rs.status.cpu().numpy())
+    if regs:
+        out["regs"] = rs.regs.cpu().numpy().view(np.uint64)
+    return out
+
+
+def _same(a, b, ctx):
+    for k in a:
+        assert np.array_equal(a[k], b[k]), f"{ctx}: {k} differs"
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_varl_fuzz(cuda, oracle_mod, seed):
+    """Random forward programs over random packets (0..80 bytes) in offsets + lens batches of
+    64..300 packets: aligned, every tile staged, and mixed; the route is the var tile loop; every
+    output == the oracle's and == the general interpreter's, registers included."""
+    from ebpf_emu import Program, _lib
+
+    rng = random.Random(7100 + seed)
+    done = 0
+    for it in range(30):
+        img = gen_program(rng, allow_loops=False, tier0=True)
+        try:
+            oracle_mod.Program(img)
+        except oracle_mod.OracleDecodeError:
+            continue
+        prog = Program(img)
+        if not prog.forward_only:
+            prog.close()
+            continue
+        pkts = [gen_packet(rng) for _ in range(rng.choice([64, 65, 100, 130, 300]))]
+        bad = rng.choice([0, 0, 1, 37])
+        frames, kw = _mixed(pkts, cuda, bad_every=bad)
+        k = _route(prog, frames, kw, max_steps=STEPS)
+        if k != _lib.EBPF_KERNEL_JIT_VARL:  # (a program the compiler does not take)
+            prog.close()
+            continue
+        got = _outputs(prog, frames, kw, cuda, regs=True)
+        ref = _outputs(prog, frames, kw, cuda, generic=True, regs=True)
+        ctx = f"seed {seed} it {it} bad {bad} prog {img.hex()}"
+        _same(got, ref, ctx)
+        _check_prod_against_oracle(oracle_mod, img, pkts, got, tag=ctx)
+        prog.close()
+        done += 1
+    assert done >= 15
+
+
+@pytest.mark.parametrize("name", ["5tuple", "drop", "acl"])
+def test_varl_workloads_vs_fixed(cuda, name):
+    """The bench programs over 200 013 of the workload's frames as an offsets + lens batch
+    (80-byte slots, every 5th packet misaligned in a quarter of the tiles) and with lengths
+    absent: verdicts, r0, status and counters == the compiled fixed-slot kernel's on the same
+    frames."""
+    import torch
+
+    from ebpf_emu import Program, _lib
+    from ebpf_emu import workloads as W
+
+    n = 200_000 + 13  # (a partial last tile)
+    prog = Program(W.program(name))
+    buf = W.frames_fixed(n, 64, 3)
+    fr = torch.from_numpy(buf).to(cuda)
+    ref = _outputs(prog, fr, dict(n=n, stride=64), cuda)
+    assert _route(prog, fr, dict(n=n, stride=64)) == _lib.EBPF_KERNEL_JIT_FIXED
+    # the same frames at offsets: slots of 80 bytes, packet i at 80 i (+3 for some)
+    slot = 80
+    big = np.zeros((n, slot), dtype=np.uint8)
+    shift = np.zeros(n, dtype=np.int64)
+    tiles = np.arange(n) // 64
+    shift[(tiles % 4 == 1) & (np.arange(n) % 5 == 0)] = 3
+    for s in (0, 3):
+        m = shift == s
+        big[m, s:s + 64] = buf.reshape(n, 64)[m]
+    offs = (np.arange(n, dtype=np.int64) * slot + shift).astype(np.uint32)
+    frames = torch.from_numpy(big.reshape(-1)).to(cuda)
+    o = torch.from_numpy(offs.view(np.int32)).to(cuda)
+    ln = torch.from_numpy(np.full(n, 64, dtype=np.int16)).to(cuda)
+    for kw in (dict(n=n, offsets=o, lens=ln), dict(n=n, offsets=o, stride=64)):
+        assert _route(prog, frames, kw) == _lib.EBPF_KERNEL_JIT_VARL
+        got = _outputs(prog, frames, kw, cuda)
+        _same(got, ref, f"{name} {sorted(kw)}")
+    prog.close()
+
+
+def test_varl_statement_reentry(cuda):
+    """One workgroup (EBPFEMU_VARL_WGS=1: 4 waves) over 3000 tiles: each wave runs 750 tiles, so
+    the statement returns after 511 and comes back (the packed counter buckets are unpacked in
+    between); misaligned tiles on both sides of the return. Against the fixed-slot kernel."""
+    import torch
+
+    from ebpf_emu import Program, _lib
+    from ebpf_emu import workloads as W
+
+    n = 3000 * 64 - 7
+    prog = Program(W.program("5tuple"))
+    buf = W.frames_fixed(n, 64, 5)
+    fr = torch.from_numpy(buf).to(cuda)
+    ref = _outputs(prog, fr, dict(n=n, stride=64), cuda)
+    pkts_shift = np.zeros(n, dtype=np.int64)
+    pkts_shift[np.isin(np.arange(n) // 64, [3, 510, 511, 512, 2043, 2044, 2045, 2999])] = 1
+    slot = 80
+    big = np.zeros((n, slot), dtype=np.uint8)
+    for s in (0, 1):
+        m = pkts_shift == s
+        big[m, s:s + 64] = buf.reshape(n, 64)[m]
+    offs = (np.arange(n, dtype=np.int64) * slot + pkts_shift).astype(np.uint32)
+    frames = torch.from_numpy(big.reshape(-1)).to(cuda)
+    kw = dict(n=n, offsets=torch.from_numpy(offs.view(np.int32)).to(cuda),
+              lens=torch.from_numpy(np.full(n, 64, dtype=np.int16)).to(cuda))
+    os.environ["EBPFEMU_VARL_WGS"] = "1"
+    try:
+        assert _route(prog, frames, kw) == _lib.EBPF_KERNEL_JIT_VARL
+        got = _outputs(prog, frames, kw, cuda)
+    finally:
+        del os.environ["EBPFEMU_VARL_WGS"]
+    _same(got, ref, "reentry")
+    prog.close()
+
+
+def test_varl_layout_routes(cuda, oracle_mod):
+    """Which batches take the var tile loop: offsets with lengths (4-byte aligned) or without;
+    not a length array at a 2-byte offset, not final images (the var kernel) -- same outputs
+    either way, against the oracle."""
+    import torch
+
+    from ebpf_emu import Program, _lib
+    from ebpf_emu import workloads as W
+
+    rng = random.Random(5)
+    pkts = [gen_packet(rng, 120) for _ in range(333)]
+    img = W.program("5tuple")
+    prog = Program(img)
+    frames, kw = _mixed(pkts, cuda, bad_every=0)
+    assert _route(prog, frames, kw) == _lib.EBPF_KERNEL_JIT_VARL
+    got = _outputs(prog, frames, kw, cuda)
+    _check_prod_against_oracle(oracle_mod, img, pkts, got, tag="aligned lens")
+    # lengths at a 2-byte aligned address: the var kernel
+    ln2 = torch.zeros(len(pkts) + 1, dtype=torch.int16, device=cuda)
+    ln2[1:] = kw["lens"]
+    kw2 = dict(kw, lens=ln2[1:])
+    assert kw2["lens"].data_ptr() % 4 == 2
+    assert _route(prog, frames, kw2) == _lib.EBPF_KERNEL_JIT_VAR
+    _same(_outputs(prog, frames, kw2, cuda), got, "lens at +2")
+    # final images (the var kernel): the same r0
+    res = prog.run(frames, mem=True, r0=True, status=True, max_steps=STEPS, **kw)
+    torch.cuda.synchronize()
+    assert np.array_equal(res.r0.cpu().numpy().view(np.uint64), got["r0"])
+    # no lengths: every packet `stride` bytes long (here 64)
+    pk64 = [p[:64].ljust(64, b"\0") for p in pkts]
+    frames, kw = _mixed(pk64, cuda, bad_every=7, lens=False)
+    kw["stride"] = 64
+    assert _route(prog, frames, kw) == _lib.EBPF_KERNEL_JIT_VARL
+    _check_prod_against_oracle(oracle_mod, img, pk64, _outputs(prog, frames, kw, cuda),
+                               tag="no lens")
+    prog.close()
+
+
+def test_varl_xdp_md(cuda):
+    """xdp_md batches in place on the var tile loop (the ctx synthesised in the preloaded window,
+    BASE = packet - 8, LEN = 8 + len): == the general interpreter's in-place images."""
+    from ebpf_emu import Program, _lib
+    from ebpf_emu import workloads as W
+
+    rng = random.Random(11)
+    pkts = [gen_packet(rng, 100) for _ in range(260)]
+    prog = Program(W.program("5tuple_xdp"))
+    for bad in (0, 9):
+        frames, kw = _mixed(pkts, cuda, bad_every=bad)
+        kw["xdp_md"] = True
+        assert _route(prog, frames, kw) == _lib.EBPF_KERNEL_JIT_VARL
+        got = _outputs(prog, frames, kw, cuda, regs=True)
+        ref = _outputs(prog, frames, kw, cuda, generic=True, regs=True)
+        _same(got, ref, f"xdp bad {bad}")
+    prog.close()

@@ -9,6 +9,8 @@ and compute (done - ready), of the wave's end, and the tiles per wave.
 
   python tools/trace_var.py [--program 5tuple] [--layout offsets|stride_lens] [--launches K]
 The stamps' own waits slow the kernel a little: read shares and spreads, not the length.
+The var kernels' stamps are compiled in only on request (they cost the kernel registers):
+  make -C ebpf-emu_amd clean all EXTRA_HIPFLAGS=-DEBPFEMU_VAR_TRACE
 """
 import argparse
 import ctypes
