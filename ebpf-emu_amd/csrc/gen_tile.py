@@ -1825,13 +1825,20 @@ def main():
         f.write("// GENERATED by gen_tile.py -- do not edit. The compiled fixed-slot kernel's tile "
                 "loop (one statement, many tiles).\n// clang-format off\n" + cstr(text) +
                 "\n// clang-format on\n")
-    # the compiled var kernel's tile loop (jit_statement_varl)
+    # the compiled var kernel's tile loop (jit_statement_varl), and its statement for
+    # stack-window programs (ebpf_tile_jit_varl_stack: the stack window in v[80:95] too)
     text = F(jit_statement_varl())
     assert "{" not in text, "unsubstituted register name: " + text[text.index("{"):][:40]
     with open(os.path.join(HERE, "tile_jit_varl.inc"), "w") as f:
         f.write("// GENERATED by gen_tile.py -- do not edit. The compiled var kernel's tile loop "
                 "(offsets + lens batches, one statement, many tiles).\n// clang-format off\n" +
                 cstr(text) + "\n// clang-format on\n")
+    text = text.replace(" varl=1\n", " varl=1 stack=1\n")
+    assert "stack=1" in text
+    with open(os.path.join(HERE, "tile_jit_varl_stack.inc"), "w") as f:
+        f.write("// GENERATED by gen_tile.py -- do not edit. The var tile loop's statement for "
+                "stack-window programs.\n// clang-format off\n" + cstr(text) +
+                "\n// clang-format on\n")
     out = ["// GENERATED by gen_tile.py -- do not edit. Per-handler JIT templates (jit.cpp), indexed",
            "// by tile id (tile_ids.h): {main text, out-of-line text}.", "#pragma once",
            "// clang-format off", "static const char* const kJitTemplates[T_COUNT][2] = {"]

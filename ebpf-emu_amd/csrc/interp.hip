@@ -1896,7 +1896,30 @@ extern "C" __global__ __launch_bounds__(kBlock, 7) void ebpf_tile_jit_var(Launch
 // CU), so a tile's windows are in flight while the one before it runs. The C++ here only starts
 // the wave's first tile, stages the windows of a tile the statement hands back (misaligned
 // packets, the batch's partial last tile) and unpacks the per-lane packed counter buckets.
-extern "C" __global__ __launch_bounds__(kBlock, 4) void ebpf_tile_jit_varl(LaunchArgs a) {
+#define VARL_OPERANDS \
+        : [tile] "+s"(tile), [winb] "+s"(winb), [nwinb] "+s"(nwinb), [metab] "+s"(metab), \
+          [nmetab] "+s"(nmetab), [acc] "+v"(acc), [ret] "+v"(ret), [cdn] "=&s"(cdn), \
+          [stage] "=&s"(stg) \
+        : [ka] "s"(ka), [k_frames] "s"(a.frames), [fr_lo] "s"((uint32_t)(uintptr_t)a.frames), \
+          [of_lo] "s"((uint32_t)(uintptr_t)a.offsets), \
+          [of_hi] "s"((uint32_t)((uintptr_t)a.offsets >> 32)), \
+          [ln_lo] "s"((uint32_t)(uintptr_t)a.lens), [ln_hi] "s"((uint32_t)((uintptr_t)a.lens >> 32)), \
+          [tp_lo] "s"((uint32_t)(uintptr_t)a.tprog), [tp_hi] "s"((uint32_t)((uintptr_t)a.tprog >> 32)), \
+          [k_n] "s"(a.n), [k_mem] "s"(a.mem_size), [k_r10] "s"(a.r10), [k_verdict] "s"(a.verdict), \
+          [vd_lo] "s"((uint32_t)(uintptr_t)a.verdict), \
+          [vd_hi] "s"((uint32_t)((uintptr_t)a.verdict >> 32)), [k_flags] "s"(kflags), \
+          [initx] "s"(initx), [oflags] "s"(oflags), [W] "s"(W), [ntiles] "s"(ntiles), \
+          [nfull] "s"(rfl(nfull)), [haslen] "s"(rfl(haslen)), [lenc] "s"(rfl(lenc)), \
+          [xdpf] "s"(rfl(xdpf)), \
+          [wx] "s"(wx), [mx] "s"(mx), [lane4] "v"(lane4), [lane2] "v"(lane2), [moff] "v"(moff), \
+          [loff] "v"(loff), [c16] "v"(c16), [lane64] "v"(lane64), [swz] "v"(swz), \
+          [lanep] "v"(lanep), [aligned] "s"(rfl(one)), [fixed] "i"(0), [loops] "i"(0), \
+          [o_init] "i"(offsetof(LaunchArgs, init_regs)), [o_r0] "i"(offsetof(LaunchArgs, r0)), \
+          [o_status] "i"(offsetof(LaunchArgs, status)), \
+          [o_regs] "i"(offsetof(LaunchArgs, regs_out)) \
+        : TILE_ASM_CLOBBER, TILE_ASM_CLOBBER_WINDOW
+template <bool STACK>
+__device__ __forceinline__ void varl_body(LaunchArgs& a) {
   counters_init();
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t wv = rfl(threadIdx.x / kWave);
@@ -1963,29 +1986,15 @@ extern "C" __global__ __launch_bounds__(kBlock, 4) void ebpf_tile_jit_varl(Launc
   while (tile < ntiles) {
     uint64_t acc = 0;
     uint32_t ret = 0, cdn, stg;
-    asm volatile(
+    if constexpr (STACK) {
+      asm volatile(
+#include "tile_jit_varl_stack.inc"
+          VARL_OPERANDS);
+    } else {
+      asm volatile(
 #include "tile_jit_varl.inc"
-        : [tile] "+s"(tile), [winb] "+s"(winb), [nwinb] "+s"(nwinb), [metab] "+s"(metab),
-          [nmetab] "+s"(nmetab), [acc] "+v"(acc), [ret] "+v"(ret), [cdn] "=&s"(cdn),
-          [stage] "=&s"(stg)
-        : [ka] "s"(ka), [k_frames] "s"(a.frames), [fr_lo] "s"((uint32_t)(uintptr_t)a.frames),
-          [of_lo] "s"((uint32_t)(uintptr_t)a.offsets),
-          [of_hi] "s"((uint32_t)((uintptr_t)a.offsets >> 32)),
-          [ln_lo] "s"((uint32_t)(uintptr_t)a.lens), [ln_hi] "s"((uint32_t)((uintptr_t)a.lens >> 32)),
-          [tp_lo] "s"((uint32_t)(uintptr_t)a.tprog), [tp_hi] "s"((uint32_t)((uintptr_t)a.tprog >> 32)),
-          [k_n] "s"(a.n), [k_mem] "s"(a.mem_size), [k_r10] "s"(a.r10), [k_verdict] "s"(a.verdict),
-          [vd_lo] "s"((uint32_t)(uintptr_t)a.verdict),
-          [vd_hi] "s"((uint32_t)((uintptr_t)a.verdict >> 32)), [k_flags] "s"(kflags),
-          [initx] "s"(initx), [oflags] "s"(oflags), [W] "s"(W), [ntiles] "s"(ntiles),
-          [nfull] "s"(rfl(nfull)), [haslen] "s"(rfl(haslen)), [lenc] "s"(rfl(lenc)),
-          [xdpf] "s"(rfl(xdpf)),
-          [wx] "s"(wx), [mx] "s"(mx), [lane4] "v"(lane4), [lane2] "v"(lane2), [moff] "v"(moff),
-          [loff] "v"(loff), [c16] "v"(c16), [lane64] "v"(lane64), [swz] "v"(swz),
-          [lanep] "v"(lanep), [aligned] "s"(rfl(one)), [fixed] "i"(0), [loops] "i"(0),
-          [o_init] "i"(offsetof(LaunchArgs, init_regs)), [o_r0] "i"(offsetof(LaunchArgs, r0)),
-          [o_status] "i"(offsetof(LaunchArgs, status)),
-          [o_regs] "i"(offsetof(LaunchArgs, regs_out))
-        : TILE_ASM_CLOBBER, TILE_ASM_CLOBBER_WINDOW);
+          VARL_OPERANDS);
+    }
     // (scalar loop state back through readfirstlane: the statement has VGPR outputs)
     tile = rfl(tile);
     winb = rfl(winb);
@@ -2011,6 +2020,14 @@ extern "C" __global__ __launch_bounds__(kBlock, 4) void ebpf_tile_jit_varl(Launc
 #pragma unroll
   for (int b = 0; b < 7; b++) cnt64[b] = cnt[b];
   flush_counters<kWavesPerBlock, true>(a, cnt64, retired, smem, lane, wv);
+}
+#undef VARL_OPERANDS
+extern "C" __global__ __launch_bounds__(kBlock, 4) void ebpf_tile_jit_varl(LaunchArgs a) {
+  varl_body<false>(a);
+}
+// stack-window programs (memory tier 0.5, not store mode): the stack window in v[80:95] too
+extern "C" __global__ __launch_bounds__(kBlock, 4) void ebpf_tile_jit_varl_stack(LaunchArgs a) {
+  varl_body<true>(a);
 }
 // stack-window programs (memory tier 0.5) on offsets + lens, stride + lens and xdp_md batches:
 // the var kernel with the preloaded header window and the stack window in v[64:95]
@@ -2252,7 +2269,7 @@ static bool g_varl = [] {
   return !(e && e[0] == '0');
 }();
 static bool varl_ok(int kind, const LaunchArgs& a, const JitFns* jit, bool stack) {
-  return g_varl && jit && jit->varl && !stack && !jit->var_only && kind == kKindDag &&
+  return g_varl && jit && jit->varl && !jit->var_only && kind == kKindDag &&
          jit_forward_for(kind, a.n_uops) && a.offsets && ((uintptr_t)a.offsets & 3) == 0 &&
          ((uintptr_t)a.lens & 3) == 0 && !a.mem_out && !a.deopt && !a.perm &&
          a.n_tiles < (1ull << 31);
@@ -2261,7 +2278,8 @@ static bool varl_ok(int kind, const LaunchArgs& a, const JitFns* jit, bool stack
 int launch_kernel_id(int kind, const LaunchArgs& a, const JitFns* jit, bool stack) {
   if (jit && jit->loop && kind == kKindLoop)
     return stack ? EBPF_KERNEL_JIT_LOOP_STACK : EBPF_KERNEL_JIT_LOOP;
-  if (varl_ok(kind, a, jit, stack)) return EBPF_KERNEL_JIT_VARL;
+  if (varl_ok(kind, a, jit, stack))
+    return stack ? EBPF_KERNEL_JIT_VARL_STACK : EBPF_KERNEL_JIT_VARL;
   if (jit && jit->fixed && jit_forward_for(kind, a.n_uops))
     return jit_fixed_layout(&a) && !jit->var_only
                ? (stack ? EBPF_KERNEL_JIT_STACK : EBPF_KERNEL_JIT_FIXED)
@@ -2314,7 +2332,7 @@ hipError_t launch_interp(int kind, const LaunchArgs& a, int grid, hipStream_t st
   const bool vl = varl_ok(kind, a, jit, stack);
   const uint32_t llds = g_lds_pad + kWavesPerBlock * kVarlWaveLds;
   if (vl) {
-    grid = jit_grid(jit->varl, llds, a.n_tiles);
+    grid = jit_grid(stack ? jit->varl_stack : jit->varl, llds, a.n_tiles);
     // (tests: EBPFEMU_VARL_WGS caps the workgroups, so a moderate batch gives each wave more than
     // the 511 tiles of one statement entry)
     const char* cap = getenv("EBPFEMU_VARL_WGS");
@@ -2338,7 +2356,8 @@ hipError_t launch_interp(int kind, const LaunchArgs& a, int grid, hipStream_t st
     e = hipModuleLaunchKernel(stack ? jit->loop_stack : jit->loop, grid, 1, 1, kBlock, 1, 1, lds,
                               stream, bargs, nullptr);
   } else if (vl) {  // offsets + lens batches: the var tile loop
-    e = hipModuleLaunchKernel(jit->varl, grid, 1, 1, kBlock, 1, 1, llds, stream, bargs, nullptr);
+    e = hipModuleLaunchKernel(stack ? jit->varl_stack : jit->varl, grid, 1, 1, kBlock, 1, 1, llds,
+                              stream, bargs, nullptr);
   } else if (jit && jit->fixed && jit_forward_for(kind, a.n_uops)) {
     if (jit_fixed_layout(&a) && !jit->var_only) {  // double-buffered windows: its own LDS size and grid
       const uint32_t dlds = g_lds_pad + kDbWaves * kTileWaveLdsDb;

@@ -3411,7 +3411,8 @@ bool jit_load(const std::vector<char>& co, hipModule_t* mod, JitFns* fns) {
       hipModuleGetFunction(&f.var_stack, m, "ebpf_tile_jit_var_stack") != hipSuccess ||
       hipModuleGetFunction(&f.loop_stack, m, "ebpf_tile_jit_loop_stack") != hipSuccess ||
       hipModuleGetFunction(&f.loop_deep, m, "ebpf_tile_jit_loop_deep") != hipSuccess ||
-      hipModuleGetFunction(&f.varl, m, "ebpf_tile_jit_varl") != hipSuccess) {
+      hipModuleGetFunction(&f.varl, m, "ebpf_tile_jit_varl") != hipSuccess ||
+      hipModuleGetFunction(&f.varl_stack, m, "ebpf_tile_jit_varl_stack") != hipSuccess) {
     (void)hipModuleUnload(m);
     return false;
   }

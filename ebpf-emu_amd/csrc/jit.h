@@ -21,6 +21,7 @@ struct JitFns {
   hipFunction_t loop_stack = nullptr;  // stack-window loop programs (ebpf_tile_jit_loop_stack)
   hipFunction_t loop_deep = nullptr;  // loop programs with the deep refill prefetch
   hipFunction_t varl = nullptr;  // offsets + lens batches: the var tile loop (ebpf_tile_jit_varl)
+  hipFunction_t varl_stack = nullptr;  // ... for stack-window programs (ebpf_tile_jit_varl_stack)
   // the program's code exists for the var kernels only (store mode: register-address stores into
   // the packet, StackPlan::any_dyn), whatever the batch layout
   bool var_only = false;

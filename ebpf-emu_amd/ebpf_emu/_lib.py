@@ -32,7 +32,7 @@ MAX_CALL_DEPTH = 64
 (EBPF_KERNEL_GENERAL_T0, EBPF_KERNEL_GENERAL_T1, EBPF_KERNEL_DAG, EBPF_KERNEL_TILE,
  EBPF_KERNEL_TILE_LOOP, EBPF_KERNEL_JIT_FIXED, EBPF_KERNEL_JIT_VAR, EBPF_KERNEL_JIT_LOOP,
  EBPF_KERNEL_JIT_STACK, EBPF_KERNEL_JIT_VAR_STACK, EBPF_KERNEL_JIT_LOOP_STACK,
- EBPF_KERNEL_JIT_VARL) = range(12)
+ EBPF_KERNEL_JIT_VARL, EBPF_KERNEL_JIT_VARL_STACK) = range(13)
 KERNEL_NAMES = ["ebpfemu::interp_kernel<0>", "ebpfemu::interp_kernel<1>", "ebpfemu::dag_kernel",
                 "ebpfemu::tile_kernel<forward>", "ebpfemu::tile_kernel<loops>",
                 "ebpf_tile_jit_fixed (compiled program)", "ebpf_tile_jit_var (compiled program)",
@@ -40,7 +40,8 @@ KERNEL_NAMES = ["ebpfemu::interp_kernel<0>", "ebpfemu::interp_kernel<1>", "ebpfe
                 "ebpf_tile_jit_fixed (compiled stack-window program)",
                 "ebpf_tile_jit_var_stack (compiled stack-window program)",
                 "ebpf_tile_jit_loop_stack (compiled stack-window loop program)",
-                "ebpf_tile_jit_varl (compiled program, var tile loop)"]
+                "ebpf_tile_jit_varl (compiled program, var tile loop)",
+                "ebpf_tile_jit_varl_stack (compiled stack-window program, var tile loop)"]
 
 EXPORTS = ["ebpf_batch_init", "ebpf_prog_load", "ebpf_prog_load_hex", "ebpf_prog_free",
            "ebpf_prog_len", "ebpf_prog_insn", "ebpf_prog_tier", "ebpf_prog_forward_only",

@@ -222,6 +222,8 @@ int ebpf_run_batch(ebpf_prog* prog, const ebpf_batch* batch, const ebpf_batch_ou
 #define EBPF_KERNEL_JIT_VARL   11 /* compiled program, offsets + lens batches: the var tile loop
                                     (ebpf_tile_jit_varl; offsets and lens 4-byte aligned, no
                                     final images) */
+#define EBPF_KERNEL_JIT_VARL_STACK 12 /* the var tile loop for stack-window programs
+                                         (ebpf_tile_jit_varl_stack; not store mode) */
 int ebpf_batch_kernel(ebpf_prog* prog, const ebpf_batch* batch, const ebpf_batch_out* out,
                       int device);
 

@@ -827,7 +827,7 @@ def test_var_kernel_full_size_shuffled(cuda, name, slot, shift):
     kw = dict(n=n, offsets=torch.from_numpy(offs.view(np.int32)).to(cuda),
               lens=torch.from_numpy(np.full(n, 64, dtype=np.int16)).to(cuda), xdp_md=xdp)
     # (offsets + lens: the var tile loop, ebpf_tile_jit_varl; stack-window programs the var kernel)
-    want = _lib.EBPF_KERNEL_JIT_VAR_STACK if name == "5tuple_stack" else _lib.EBPF_KERNEL_JIT_VARL
+    want = _lib.EBPF_KERNEL_JIT_VARL_STACK if name == "5tuple_stack" else _lib.EBPF_KERNEL_JIT_VARL
     assert prog.batch_kernel(prog.make_batch(frames, **kw)) == want
     cnt2 = torch.zeros(8, dtype=torch.int64, device=cuda)
     res = prog.run(frames, counters=cnt2, r0=True, status=True, **kw)

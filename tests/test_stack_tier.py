@@ -177,7 +177,8 @@ def test_stack_window_fuzz(cuda, oracle_mod, seed):
         # all take the store-forwarding overlay)
         # (store mode: the var kernel's stack statement, test_store_mode.py)
         assert got["kernel"] in (_lib.EBPF_KERNEL_JIT_STACK, _lib.EBPF_KERNEL_JIT_LOOP_STACK,
-                                 _lib.EBPF_KERNEL_JIT_VAR_STACK, _lib.EBPF_KERNEL_GENERAL_T1)
+                                 _lib.EBPF_KERNEL_JIT_VAR_STACK, _lib.EBPF_KERNEL_JIT_VARL_STACK,
+                                 _lib.EBPF_KERNEL_GENERAL_T1)
         n_stack += got["kernel"] == _lib.EBPF_KERNEL_JIT_STACK
         ref = _run(img, frames, len(pkts), cuda, generic=True, stride=stride)
         assert ref["kernel"] == _lib.EBPF_KERNEL_GENERAL_T1
@@ -215,7 +216,8 @@ def test_stack_window_fallbacks(cuda, oracle_mod):
         _vs_oracle(oracle_mod, img, pkts, got, r10=r10, tag=str(kw))
     lens = torch.tensor(np.full(len(pkts), 128, dtype=np.int16), device=cuda)
     offs = torch.tensor(np.arange(len(pkts), dtype=np.int32) * 128, device=cuda)
-    got = _run(img, frames, len(pkts), cuda, kernel=_lib.EBPF_KERNEL_JIT_VAR_STACK, offsets=offs,
+    # (offsets + lens: the var tile loop's stack statement)
+    got = _run(img, frames, len(pkts), cuda, kernel=_lib.EBPF_KERNEL_JIT_VARL_STACK, offsets=offs,
                lens=lens)
     _vs_oracle(oracle_mod, img, pkts, got, tag="offsets")
     got = _run(img, frames, len(pkts), cuda, kernel=_lib.EBPF_KERNEL_GENERAL_T1, offsets=offs,
@@ -345,7 +347,8 @@ def test_stack_atomics_fuzz(cuda, oracle_mod, seed):
         frames = _fixed_frames(pkts, stride, cuda)
         got = _run(img, frames, len(pkts), cuda, stride=stride)
         # (a store through an unknown pointer: store mode, the var kernel's stack statement)
-        n_stack += got["kernel"] in (_lib.EBPF_KERNEL_JIT_STACK, _lib.EBPF_KERNEL_JIT_VAR_STACK)
+        n_stack += got["kernel"] in (_lib.EBPF_KERNEL_JIT_STACK, _lib.EBPF_KERNEL_JIT_VAR_STACK,
+                                     _lib.EBPF_KERNEL_JIT_VARL_STACK)
         ref = _run(img, frames, len(pkts), cuda, generic=True, stride=stride)
         for key in ("status", "r0", "verdict", "regs", "counters", "prod_verdict"):
             assert np.array_equal(got[key], ref[key]), (key, seed, it, img.hex())
@@ -426,9 +429,9 @@ def test_stack_window_fuzz_var(cuda, oracle_mod, layout):
             continue
         pkts = _var_packets(rng, rng.choice([64, 100, 130]))
         got, xdp = _run_var(img, pkts, cuda, VAR_LAYOUTS[layout])
-        assert got["kernel"] in (_lib.EBPF_KERNEL_JIT_VAR_STACK, _lib.EBPF_KERNEL_JIT_LOOP_STACK,
-                                 _lib.EBPF_KERNEL_GENERAL_T1)
-        n_stack += got["kernel"] == _lib.EBPF_KERNEL_JIT_VAR_STACK
+        assert got["kernel"] in (_lib.EBPF_KERNEL_JIT_VAR_STACK, _lib.EBPF_KERNEL_JIT_VARL_STACK,
+                                 _lib.EBPF_KERNEL_JIT_LOOP_STACK, _lib.EBPF_KERNEL_GENERAL_T1)
+        n_stack += got["kernel"] in (_lib.EBPF_KERNEL_JIT_VAR_STACK, _lib.EBPF_KERNEL_JIT_VARL_STACK)
         ref, _ = _run_var(img, pkts, cuda, VAR_LAYOUTS[layout], generic=True)
         assert ref["kernel"] == _lib.EBPF_KERNEL_GENERAL_T1
         ok = got["status"] != 7  # (ST_BADPKT lanes have no registers: main.rs:20-21 panics)
@@ -454,7 +457,8 @@ def test_stack_workloads_var(cuda, oracle_mod, layout):
         img = assemble(src)
         pkts = _var_packets(rng, 150)
         got, xdp = _run_var(img, pkts, cuda, VAR_LAYOUTS[layout])
-        assert got["kernel"] == _lib.EBPF_KERNEL_JIT_VAR_STACK, src
+        # (offsets + lens: the var tile loop's stack statement; stride + lens the var kernel's)
+        assert got["kernel"] in (_lib.EBPF_KERNEL_JIT_VAR_STACK, _lib.EBPF_KERNEL_JIT_VARL_STACK), src
         ref, _ = _run_var(img, pkts, cuda, VAR_LAYOUTS[layout], generic=True)
         for key in ("status", "verdict", "counters"):
             assert np.array_equal(got[key], ref[key]), (key, layout, src)
@@ -508,7 +512,8 @@ def test_large_stack_programs(cuda, oracle_mod, layout):
             got, xdp = _run_var(img, pkts, cuda, VAR_LAYOUTS[layout])
             ref, _ = _run_var(img, pkts, cuda, VAR_LAYOUTS[layout], generic=True)
             want = _lib.EBPF_KERNEL_JIT_VAR_STACK
-        n_stack += got["kernel"] in (want, _lib.EBPF_KERNEL_JIT_LOOP_STACK)
+        n_stack += got["kernel"] in (want, _lib.EBPF_KERNEL_JIT_VARL_STACK,
+                                     _lib.EBPF_KERNEL_JIT_LOOP_STACK)
         ok = got["status"] != 7
         for key in ("status", "verdict", "counters", "prod_verdict"):
             assert np.array_equal(got[key], ref[key]), (key, layout, it, img.hex())
@@ -566,7 +571,8 @@ def test_stack_loop_programs(cuda, oracle_mod, layout):
             pkts = _var_packets(rng, rng.choice([64, 100]))
             got, xdp = _run_var(img, pkts, cuda, VAR_LAYOUTS[layout], max_steps=steps)
             if it == 2 and steps == 3000:  # (forward, budget that cannot bind: forward kernels)
-                assert got["kernel"] in (_lib.EBPF_KERNEL_JIT_VAR_STACK,), layout
+                assert got["kernel"] in (_lib.EBPF_KERNEL_JIT_VAR_STACK,
+                                         _lib.EBPF_KERNEL_JIT_VARL_STACK), layout
             else:
                 # (the route of the production outputs: a promoted program's own loop kernel,
                 # test_promote.py; every output asked for below runs the stack loop kernel)

@@ -102,9 +102,10 @@ def test_varl_fuzz(cuda, oracle_mod, seed):
     assert done >= 15
 
 
-@pytest.mark.parametrize("name", ["5tuple", "drop", "acl"])
+@pytest.mark.parametrize("name", ["5tuple", "drop", "acl", "5tuple_stack", "mac_swap_tx"])
 def test_varl_workloads_vs_fixed(cuda, name):
-    """The bench programs over 200 013 of the workload's frames as an offsets + lens batch
+    """The bench programs (the stack-window ones on the stack statement) over 200 013 of the
+    workload's frames as an offsets + lens batch
     (80-byte slots, every 5th packet misaligned in a quarter of the tiles) and with lengths
     absent: verdicts, r0, status and counters == the compiled fixed-slot kernel's on the same
     frames."""
@@ -118,7 +119,9 @@ def test_varl_workloads_vs_fixed(cuda, name):
     buf = W.frames_fixed(n, 64, 3)
     fr = torch.from_numpy(buf).to(cuda)
     ref = _outputs(prog, fr, dict(n=n, stride=64), cuda)
-    assert _route(prog, fr, dict(n=n, stride=64)) == _lib.EBPF_KERNEL_JIT_FIXED
+    stack = name in ("5tuple_stack", "mac_swap_tx")  # (memory tier 0.5: the stack statements)
+    assert _route(prog, fr, dict(n=n, stride=64)) == (_lib.EBPF_KERNEL_JIT_STACK if stack
+                                                      else _lib.EBPF_KERNEL_JIT_FIXED)
     # the same frames at offsets: slots of 80 bytes, packet i at 80 i (+3 for some)
     slot = 80
     big = np.zeros((n, slot), dtype=np.uint8)
@@ -133,7 +136,8 @@ def test_varl_workloads_vs_fixed(cuda, name):
     o = torch.from_numpy(offs.view(np.int32)).to(cuda)
     ln = torch.from_numpy(np.full(n, 64, dtype=np.int16)).to(cuda)
     for kw in (dict(n=n, offsets=o, lens=ln), dict(n=n, offsets=o, stride=64)):
-        assert _route(prog, frames, kw) == _lib.EBPF_KERNEL_JIT_VARL
+        assert _route(prog, frames, kw) == (_lib.EBPF_KERNEL_JIT_VARL_STACK if stack
+                                            else _lib.EBPF_KERNEL_JIT_VARL)
         got = _outputs(prog, frames, kw, cuda)
         _same(got, ref, f"{name} {sorted(kw)}")
     prog.close()
