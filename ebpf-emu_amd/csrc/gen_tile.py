@@ -1497,17 +1497,19 @@ s_waitcnt lgkmcnt(0)
 def jit_statement_varl():
     out_tail = EPILOGUE[EPILOGUE.index("s_cmp_lg_u64 {ER0}, 0"):EPILOGUE.index(".Lend%=:")]
     out_tail = out_tail.replace(".Lend%=", ".Loutd%=") + "s_branch .Loutd%="
+    # round r: packet 16r + l/4's offset (in the low word of the address pair) + frames + the
+    # lane's chunk (%[fc]); the lanes whose chunk starts before the packet's end (mask in
+    # MASKS[r]) issue the DMA -- the others leave their slot stale: bytes at or past LEN are
+    # masked wherever the program reads them
+    masks = ["{T0}", "{T1}", "{T4}", "{T5}"]
     rounds = "\n".join(f"""v_mov_b32 {{t{13 + 2 * r}}}, 0
-v_mov_b32 {{t{12 + 2 * r}}}, {{t{2 + r}}}
-v_lshl_add_u64 {{T{12 + 2 * r}{13 + 2 * r}}}, {{T{12 + 2 * r}{13 + 2 * r}}}, 0, %[k_frames]
-v_add_co_u32 {{t{12 + 2 * r}}}, vcc, {{t{12 + 2 * r}}}, %[c16]
-v_addc_co_u32 {{t{13 + 2 * r}}}, vcc, 0, {{t{13 + 2 * r}}}, vcc
-v_cmp_lt_u32 vcc, %[c16], {{t{8 + r}}}
-v_cndmask_b32 {{t{12 + 2 * r}}}, {{t0}}, {{t{12 + 2 * r}}}, vcc
-v_cndmask_b32 {{t{13 + 2 * r}}}, {{t1}}, {{t{13 + 2 * r}}}, vcc""" for r in range(4))
-    dmas = "\n".join(f"""s_add_u32 m0, %[nwinb], {1024 * r}
+v_lshl_add_u64 {{T{12 + 2 * r}{13 + 2 * r}}}, {{T{12 + 2 * r}{13 + 2 * r}}}, 0, %[fc]
+v_cmp_lt_u32_e64 {masks[r]}, %[c16], {{t{8 + r}}}""" for r in range(4))
+    dmas = "\n".join(f"""s_mov_b64 exec, {masks[r]}
+s_add_u32 m0, %[nwinb], {1024 * r}
 s_nop 0
-global_load_lds_dwordx4 {{T{12 + 2 * r}{13 + 2 * r}}}, off ; @DMAPOLICY@""" for r in range(4))
+global_load_lds_dwordx4 {{T{12 + 2 * r}{13 + 2 * r}}}, off ; @DMAPOLICY@""" for r in range(4)) + \
+        "\ns_mov_b64 exec, -1"
     main = """s_mov_b32 {M0S}, m0
 s_movk_i32 %[cdn], 511
 s_mov_b32 %[stage], 0
@@ -1548,49 +1550,37 @@ s_cbranch_scc0 .Lnonext%=
 s_cmp_lt_u32 {T3}, %[nfull]
 s_cbranch_scc0 .Lstg%=
 v_add_u32 {t0}, %[nmetab], %[lane4]
-ds_read_b32 {t8}, {t0}
+ds_read_b32 {t6}, {t0}
 v_add_u32 {t0}, %[nmetab], %[moff]
-ds_read_b32 {t2}, {t0}
-ds_read_b32 {t3}, {t0} offset:64
-ds_read_b32 {t4}, {t0} offset:128
-ds_read_b32 {t5}, {t0} offset:192
+ds_read_b32 {t12}, {t0}
+ds_read_b32 {t14}, {t0} offset:64
+ds_read_b32 {t16}, {t0} offset:128
+ds_read_b32 {t18}, {t0} offset:192
 s_cmp_eq_u32 %[haslen], 0
 s_cbranch_scc1 .Lnl2%=
 v_add_u32 {t1}, %[nmetab], %[lane2]
-ds_read_u16 {t9}, {t1}
+ds_read_u16 {t7}, {t1}
 v_add_u32 {t1}, %[nmetab], %[loff]
-ds_read_u16 {t10}, {t1}
-ds_read_u16 {t11}, {t1} offset:32
-ds_read_u16 {t12}, {t1} offset:64
-ds_read_u16 {t13}, {t1} offset:96
-s_waitcnt lgkmcnt(0)
-v_mov_b32 {t14}, {t10}
-v_mov_b32 {t15}, {t11}
-v_mov_b32 {t16}, {t12}
-v_mov_b32 {t17}, {t13}
+ds_read_u16 {t8}, {t1}
+ds_read_u16 {t9}, {t1} offset:32
+ds_read_u16 {t10}, {t1} offset:64
+ds_read_u16 {t11}, {t1} offset:96
 s_branch .Lnl2d%=
 .Lnl2%=:
+v_mov_b32 {t7}, %[lenc]
+v_mov_b32 {t8}, %[lenc]
 v_mov_b32 {t9}, %[lenc]
-v_mov_b32 {t14}, %[lenc]
-v_mov_b32 {t15}, %[lenc]
-v_mov_b32 {t16}, %[lenc]
-v_mov_b32 {t17}, %[lenc]
-s_waitcnt lgkmcnt(0)
+v_mov_b32 {t10}, %[lenc]
+v_mov_b32 {t11}, %[lenc]
 .Lnl2d%=:
+s_waitcnt lgkmcnt(0)
 ; every packet of the next tile 16-byte aligned (lanes of length 0 excepted), else stage it
-v_add_u32 {t0}, %[fr_lo], {t8}
+v_add_u32 {t0}, %[fr_lo], {t6}
 v_and_b32 {t0}, 15, {t0}
 v_cmp_ne_u32 vcc, 0, {t0}
-v_cmp_ne_u32_e64 {T0}, 0, {t9}
+v_cmp_ne_u32_e64 {T0}, 0, {t7}
 s_and_b64 vcc, vcc, {T0}
 s_cbranch_vccnz .Lstg%=
-v_mov_b32 {t8}, {t14}
-v_mov_b32 {t9}, {t15}
-v_mov_b32 {t10}, {t16}
-v_mov_b32 {t11}, {t17}
-; (chunks wholly past the packet read a dummy address: the micro-op table)
-v_mov_b32 {t0}, %[tp_lo]
-v_mov_b32 {t1}, %[tp_hi]
 """ + rounds + """
 """ + dmas + """
 s_branch .Lmeta%=

@@ -1598,6 +1598,7 @@ static bool xdp_in_place(ebpf_prog* p, const ebpf_batch* b, bool mem_out, int de
   const int id = launch_kernel_id(kind, a, batch_jit(p, b, kind, stk, device), stk);
   return id == EBPF_KERNEL_JIT_FIXED || id == EBPF_KERNEL_JIT_VAR ||
          id == EBPF_KERNEL_JIT_STACK || id == EBPF_KERNEL_JIT_VAR_STACK ||
+         id == EBPF_KERNEL_JIT_VARL || id == EBPF_KERNEL_JIT_VARL_STACK ||
          (id == EBPF_KERNEL_TILE && !launch_fixed_layout(a));
 }
 

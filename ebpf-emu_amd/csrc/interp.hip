@@ -1904,7 +1904,7 @@ extern "C" __global__ __launch_bounds__(kBlock, 7) void ebpf_tile_jit_var(Launch
           [of_lo] "s"((uint32_t)(uintptr_t)a.offsets), \
           [of_hi] "s"((uint32_t)((uintptr_t)a.offsets >> 32)), \
           [ln_lo] "s"((uint32_t)(uintptr_t)a.lens), [ln_hi] "s"((uint32_t)((uintptr_t)a.lens >> 32)), \
-          [tp_lo] "s"((uint32_t)(uintptr_t)a.tprog), [tp_hi] "s"((uint32_t)((uintptr_t)a.tprog >> 32)), \
+          [fc] "v"(fc), \
           [k_n] "s"(a.n), [k_mem] "s"(a.mem_size), [k_r10] "s"(a.r10), [k_verdict] "s"(a.verdict), \
           [vd_lo] "s"((uint32_t)(uintptr_t)a.verdict), \
           [vd_hi] "s"((uint32_t)((uintptr_t)a.verdict >> 32)), [k_flags] "s"(kflags), \
@@ -1936,6 +1936,7 @@ __device__ __forceinline__ void varl_body(LaunchArgs& a) {
   const uint32_t loff = 256 + ((lane >> 2) << 1), c16 = ((lane & 3u) ^ ((lane >> 4) & 3u)) * 16u;
   const uint32_t lane64 = lane << 6, swz = ((lane >> 2) & 3u) << 4;
   const uint64_t lanep = lane;
+  const uint64_t fc = (uint64_t)(uintptr_t)a.frames + c16;  // (the window DMA: frames + chunk)
   const uint32_t W = gridDim.x * kWavesPerBlock;
   const uint32_t ntiles = rfl((uint32_t)a.n_tiles), nfull = rfl((uint32_t)(a.n / kWave));
   const uint32_t haslen = rfl(a.lens ? 1u : 0u), xdpf = rfl(a.xdp);

@@ -127,6 +127,7 @@ def test_store_mode_fuzz(cuda, oracle_mod, layout):
             n_sm += 1
         else:
             assert got["kernel"] in (_lib.EBPF_KERNEL_JIT_STACK, _lib.EBPF_KERNEL_JIT_VAR_STACK,
+                                     _lib.EBPF_KERNEL_JIT_VARL_STACK,
                                      _lib.EBPF_KERNEL_GENERAL_T1), (layout, img.hex())
         ref, _, _ = _run_layout(img, pkts, cuda, layout, generic=True)
         assert ref["kernel"] == _lib.EBPF_KERNEL_GENERAL_T1
