@@ -1505,6 +1505,10 @@ def jit_statement_varl():
     rounds = "\n".join(f"""v_mov_b32 {{t{13 + 2 * r}}}, 0
 v_lshl_add_u64 {{T{12 + 2 * r}{13 + 2 * r}}}, {{T{12 + 2 * r}{13 + 2 * r}}}, 0, %[fc]
 v_cmp_lt_u32_e64 {masks[r]}, %[c16], {{t{8 + r}}}""" for r in range(4))
+    srounds = "\n".join(f"""v_lshl_add_u64 {{T{12 + 2 * r}{13 + 2 * r}}}, %[db], 0, {{T7}}
+s_add_u32 {{T7L}}, {{T7L}}, %[s16]
+s_addc_u32 {{T7H}}, {{T7H}}, 0""" for r in range(4))
+    smasks = "\n".join(f"v_cmp_lt_u32_e64 {masks[r]}, %[c16], {{t{8 + r}}}" for r in range(4))
     dmas = "\n".join(f"""s_mov_b64 exec, {masks[r]}
 s_add_u32 m0, %[nwinb], {1024 * r}
 s_nop 0
@@ -1518,8 +1522,8 @@ s_mov_b32 %[stage], 0
 s_waitcnt vmcnt(0)
 v_add_u32 {t0}, %[metab], %[lane4]
 ds_read_b32 {t6}, {t0}
-s_cmp_eq_u32 %[haslen], 0
-s_cbranch_scc1 .Lnl%=
+s_bitcmp1_b32 %[fl], 6
+s_cbranch_scc0 .Lnl%=
 v_add_u32 {t1}, %[metab], %[lane2]
 ds_read_u16 {t7}, {t1}
 s_branch .Lnld%=
@@ -1534,9 +1538,18 @@ v_cmp_gt_u64 vcc, %[k_n], {T23}
 s_mov_b64 {VM}, vcc
 s_waitcnt lgkmcnt(0)
 v_mov_b32 {LEN}, {t7}
+s_bitcmp1_b32 %[fl], 8
+s_cbranch_scc1 .Lsb%=
 v_mov_b32 {t7}, 0
 v_lshl_add_u64 {BASE}, %[k_frames], 0, {T67}
-s_cmp_lg_u32 %[xdpf], 0
+s_branch .Lsbd%=
+.Lsb%=:
+; (stride layout: packet tile * 64 + lane at frames + lane * stride + tile * 64 * stride)
+s_mul_i32 {T5L}, %[tile], %[tbytes]
+s_mul_hi_u32 {T5H}, %[tile], %[tbytes]
+v_lshl_add_u64 {BASE}, %[lb], 0, {T5}
+.Lsbd%=:
+s_bitcmp1_b32 %[fl], 7
 s_cbranch_scc0 .Lnx%=
 v_min_u32 {LEN}, 0xffff, {LEN}
 v_add_u32 {LEN}, 8, {LEN}
@@ -1549,6 +1562,8 @@ s_cmp_lt_u32 {T3}, %[ntiles]
 s_cbranch_scc0 .Lnonext%=
 s_cmp_lt_u32 {T3}, %[nfull]
 s_cbranch_scc0 .Lstg%=
+s_bitcmp1_b32 %[fl], 8
+s_cbranch_scc1 .Lsn%=
 v_add_u32 {t0}, %[nmetab], %[lane4]
 ds_read_b32 {t6}, {t0}
 v_add_u32 {t0}, %[nmetab], %[moff]
@@ -1556,8 +1571,8 @@ ds_read_b32 {t12}, {t0}
 ds_read_b32 {t14}, {t0} offset:64
 ds_read_b32 {t16}, {t0} offset:128
 ds_read_b32 {t18}, {t0} offset:192
-s_cmp_eq_u32 %[haslen], 0
-s_cbranch_scc1 .Lnl2%=
+s_bitcmp1_b32 %[fl], 6
+s_cbranch_scc0 .Lnl2%=
 v_add_u32 {t1}, %[nmetab], %[lane2]
 ds_read_u16 {t7}, {t1}
 v_add_u32 {t1}, %[nmetab], %[loff]
@@ -1584,6 +1599,30 @@ s_cbranch_vccnz .Lstg%=
 """ + rounds + """
 """ + dmas + """
 s_branch .Lmeta%=
+.Lsn%=:
+; stride layout (16-byte aligned slots): round r's packet 16r + l/4 at frames + its chunk +
+; (l/4) * stride (%[db]) + nt * 64 * stride + r * 16 * stride
+s_bitcmp1_b32 %[fl], 6
+s_cbranch_scc0 .Lsl%=
+v_add_u32 {t1}, %[nmetab], %[loff]
+ds_read_u16 {t8}, {t1}
+ds_read_u16 {t9}, {t1} offset:32
+ds_read_u16 {t10}, {t1} offset:64
+ds_read_u16 {t11}, {t1} offset:96
+s_branch .Lsld%=
+.Lsl%=:
+v_mov_b32 {t8}, %[lenc]
+v_mov_b32 {t9}, %[lenc]
+v_mov_b32 {t10}, %[lenc]
+v_mov_b32 {t11}, %[lenc]
+.Lsld%=:
+s_mul_i32 {T7L}, {T3}, %[tbytes]
+s_mul_hi_u32 {T7H}, {T3}, %[tbytes]
+""" + srounds + """
+s_waitcnt lgkmcnt(0)
+""" + smasks + """
+""" + dmas + """
+s_branch .Lmeta%=
 .Lstg%=:
 s_mov_b32 %[stage], 1
 .Lmeta%=:
@@ -1591,6 +1630,8 @@ s_mov_b32 %[stage], 1
 s_add_u32 {T3}, {T3}, %[W]
 s_cmp_lt_u32 {T3}, %[nfull]
 s_cbranch_scc0 .Lnonext%=
+s_bitcmp1_b32 %[fl], 8
+s_cbranch_scc1 .Lml%=
 s_mov_b32 {T1L}, {T3}
 s_mov_b32 {T1H}, 0
 s_lshl_b64 {T1}, {T1}, 8
@@ -1602,8 +1643,9 @@ v_lshl_add_u64 {T01}, {T01}, 0, {T1}
 s_mov_b32 m0, %[metab]
 s_nop 0
 global_load_lds_dword {T01}, off
-s_cmp_eq_u32 %[haslen], 0
-s_cbranch_scc1 .Lnonext%=
+.Lml%=:
+s_bitcmp1_b32 %[fl], 6
+s_cbranch_scc0 .Lnonext%=
 s_mov_b32 {T1L}, {T3}
 s_mov_b32 {T1H}, 0
 s_lshl_b64 {T1}, {T1}, 7
@@ -1633,7 +1675,7 @@ s_and_b64 exec, exec, vcc
 v_mov_b32 {ST}, 7
 v_mov_b32 {LPC}, -1
 s_mov_b64 exec, -1
-s_cmp_lg_u32 %[initx], 0
+s_bitcmp1_b32 %[fl], 4
 s_cbranch_scc1 .Linitx%=
 ;@@JITINIT@@
 .Linitd%=:
@@ -1641,7 +1683,34 @@ s_cbranch_scc1 .Linitx%=
 ; JIT N=%= fixed=0 loops=0 aligned=%[aligned] xdp=%[xdpf] varl=1
 ;@@JIT@@
 .Ldone%=:
-; verdict byte, the lane's counter bucket (verdict 0..4, 0xfe -> 5, 0xff -> 6) into %[acc]
+; store mode: lanes that left for the general interpreter (status 0x80, jit.h kStDeopt) produce
+; nothing here; their packet indices go to the deopt list (one returning atomic per wave)
+s_mov_b64 exec, {VM}
+v_cmp_eq_u32 vcc, 0x80, {ST}
+s_cbranch_vccz .Lnodo%=
+s_andn2_b64 {VM}, {VM}, vcc
+s_mov_b64 {T0}, vcc
+s_mov_b64 exec, vcc
+v_mbcnt_lo_u32_b32 {t5}, {T0L}, 0
+v_mbcnt_hi_u32_b32 {t5}, {T0H}, {t5}
+s_bcnt1_i32_b64 {T3}, {T0}
+s_ff1_i32_b64 {T1L}, {T0}
+s_lshl_b64 {T1}, 1, {T1L}
+s_mov_b64 exec, {T1}
+v_mov_b32 {t6}, {T3}
+v_mov_b64 {T89}, %[k_deopt]
+global_atomic_add {t4}, {T89}, {t6}, off sc0
+s_waitcnt vmcnt(0)
+v_readfirstlane_b32 {T3}, {t4}
+s_mov_b64 exec, {T0}
+v_add_u32 {t10}, {T3}, {t5}
+v_mov_b32 {t11}, 0
+v_lshlrev_b64 {T1011}, 2, {T1011}
+v_lshl_add_u64 {T89}, {T1011}, 0, %[k_dix]
+s_lshl_b32 {T1L}, %[tile], 6
+v_add_u32 {t4}, {T1L}, %[lane]
+global_store_dword {T89}, {t4}, off
+.Lnodo%=:
 s_mov_b64 exec, {VM}
 v_cmp_gt_u64 vcc, 5, {RF}
 v_mov_b32 {t5}, 0xfe
@@ -1655,7 +1724,7 @@ v_mul_u32_u24 {t5}, 9, {t5}
 v_lshlrev_b64 {T67}, {t5}, 1
 v_lshl_add_u64 %[acc], %[acc], 0, {T67}
 v_add_u32 %[ret], %[ret], {NST}
-s_cmp_lg_u64 %[k_verdict], 0
+s_bitcmp1_b32 %[fl], 9
 s_cbranch_scc0 .Lnov%=
 s_lshl_b32 {T0L}, %[tile], 6
 s_lshr_b32 {T0H}, %[tile], 26
@@ -1664,7 +1733,7 @@ s_addc_u32 {T0H}, {T0H}, %[vd_hi]
 v_lshl_add_u64 {T67}, %[lanep], 0, {T0}
 global_store_byte {T67}, {t4}, off
 .Lnov%=:
-s_cmp_lg_u32 %[oflags], 0
+s_bitcmp1_b32 %[fl], 5
 s_cbranch_scc1 .Lout%=
 .Loutd%=:
 s_mov_b64 exec, -1
@@ -1686,7 +1755,7 @@ s_mov_b32 m0, {M0S}
 s_branch .Lend%=
 """
     ool = """.Linitx%=:
-s_bitcmp1_b32 %[k_flags], 0
+s_bitcmp1_b32 %[fl], 0
 s_cbranch_scc1 .Linitc%=
 """ + DEFAULT_INIT + """s_branch .Linitd%=
 .Linitc%=:

@@ -1799,8 +1799,9 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* bin, const ebpf_batch_out* ou
   // store mode (register-address packet stores, StackPlan::any_dyn): lanes the compiled kernel
   // cannot finish are listed, then re-run from the start by the general interpreter (tier 1)
   // (the promoted program: lanes whose packet reaches the slots, jit.cpp promo_guard)
+  const int kid = jit ? launch_kernel_id(kind, a, jit, stk) : -1;
   const bool deopt = (stk && p->stack.any_dyn && kind == kKindDag && jit &&
-                      launch_kernel_id(kind, a, jit, stk) == EBPF_KERNEL_JIT_VAR_STACK) ||
+                      (kid == EBPF_KERNEL_JIT_VAR_STACK || kid == EBPF_KERNEL_JIT_VARL_STACK)) ||
                      (promo && jit);
   if (deopt) {
     a.deopt = (uint32_t*)(ws + kWsDeoptOff);

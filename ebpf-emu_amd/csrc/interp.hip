@@ -1904,12 +1904,13 @@ extern "C" __global__ __launch_bounds__(kBlock, 7) void ebpf_tile_jit_var(Launch
           [of_lo] "s"((uint32_t)(uintptr_t)a.offsets), \
           [of_hi] "s"((uint32_t)((uintptr_t)a.offsets >> 32)), \
           [ln_lo] "s"((uint32_t)(uintptr_t)a.lens), [ln_hi] "s"((uint32_t)((uintptr_t)a.lens >> 32)), \
-          [fc] "v"(fc), \
-          [k_n] "s"(a.n), [k_mem] "s"(a.mem_size), [k_r10] "s"(a.r10), [k_verdict] "s"(a.verdict), \
+          [fc] "v"(fc), [lb] "v"(lb), [db] "v"(db), \
+          [tbytes] "s"(rfl(tbytes)), [s16] "s"(rfl(s16)), [lane] "v"(lane), \
+          [k_deopt] "s"(a.deopt), [k_dix] "s"(a.deopt_idx), \
+          [k_n] "s"(a.n), [k_mem] "s"(a.mem_size), [k_r10] "s"(a.r10), \
           [vd_lo] "s"((uint32_t)(uintptr_t)a.verdict), \
-          [vd_hi] "s"((uint32_t)((uintptr_t)a.verdict >> 32)), [k_flags] "s"(kflags), \
-          [initx] "s"(initx), [oflags] "s"(oflags), [W] "s"(W), [ntiles] "s"(ntiles), \
-          [nfull] "s"(rfl(nfull)), [haslen] "s"(rfl(haslen)), [lenc] "s"(rfl(lenc)), \
+          [vd_hi] "s"((uint32_t)((uintptr_t)a.verdict >> 32)), [fl] "s"(rfl(fl)), \
+          [W] "s"(W), [ntiles] "s"(ntiles), [nfull] "s"(rfl(nfull)), [lenc] "s"(rfl(lenc)), \
           [xdpf] "s"(rfl(xdpf)), \
           [wx] "s"(wx), [mx] "s"(mx), [lane4] "v"(lane4), [lane2] "v"(lane2), [moff] "v"(moff), \
           [loff] "v"(loff), [c16] "v"(c16), [lane64] "v"(lane64), [swz] "v"(swz), \
@@ -1937,6 +1938,11 @@ __device__ __forceinline__ void varl_body(LaunchArgs& a) {
   const uint32_t lane64 = lane << 6, swz = ((lane >> 2) & 3u) << 4;
   const uint64_t lanep = lane;
   const uint64_t fc = (uint64_t)(uintptr_t)a.frames + c16;  // (the window DMA: frames + chunk)
+  // the stride layout (no offsets, 16-byte aligned slots of 64 bytes or more): lane l's packet at
+  // lb + tile * 64 * stride, round r's DMA source at db + tile * 64 * stride + r * 16 * stride
+  const uint64_t lb = (uint64_t)(uintptr_t)a.frames + (uint64_t)lane * a.stride;
+  const uint64_t db = (uint64_t)(uintptr_t)a.frames + (uint64_t)(lane >> 2) * a.stride + c16;
+  const uint32_t tbytes = (uint32_t)(a.stride * kWave), s16 = (uint32_t)(a.stride * 16);
   const uint32_t W = gridDim.x * kWavesPerBlock;
   const uint32_t ntiles = rfl((uint32_t)a.n_tiles), nfull = rfl((uint32_t)(a.n / kWave));
   const uint32_t haslen = rfl(a.lens ? 1u : 0u), xdpf = rfl(a.xdp);
@@ -1944,6 +1950,9 @@ __device__ __forceinline__ void varl_body(LaunchArgs& a) {
   const uint32_t kflags = rfl((a.init_regs ? 1u : 0u) | (a.r0 ? 2u : 0u) | (a.status ? 4u : 0u) |
                               (a.regs_out ? 8u : 0u));
   const uint32_t initx = rfl(kflags & 9u), oflags = rfl(kflags & 14u), one = 1;
+  // the statement's flags (gen_tile.py jit_statement_varl)
+  const uint32_t fl = kflags | (initx ? 16u : 0u) | (oflags ? 32u : 0u) | (haslen ? 64u : 0u) |
+                      (xdpf ? 128u : 0u) | (a.offsets ? 0u : 256u) | (a.verdict ? 512u : 0u);
   const uint64_t ka = (uint64_t)__builtin_amdgcn_kernarg_segment_ptr();
   // the wave's current window / metadata buffers as generic pointers (staging)
   auto buf = [&](uint32_t wb, uint32_t mb) {
@@ -1971,10 +1980,13 @@ __device__ __forceinline__ void varl_body(LaunchArgs& a) {
   uint64_t retired = 0;
   uint32_t tile = blockIdx.x * kWavesPerBlock + wv;
   if (tile < ntiles) {
-    // the first tile: its metadata, then its windows (DMA'd when whole and aligned), then the
-    // next tile's metadata, in flight at the statement's first wait
+    // the first two tiles' metadata at once, then the first tile's windows (DMA'd when whole and
+    // aligned): the statement's first wait is for those windows alone. (Tried: both first tiles'
+    // windows in flight from the start, as the fixed-slot kernel's opening burst -- 17.6 vs
+    // 16.6 us per 1 Mi-packet 5-tuple batch, A/B on one box.)
     const WaveLds X = buf(winb, metab);
     dma_meta<true>(a, X, 0, tile, lane);
+    if (tile + W < ntiles) dma_meta<true>(a, buf(nwinb, nmetab), 0, tile + W, lane);
     dma_wait();
     uintptr_t pb;
     uint32_t ml;
@@ -1982,7 +1994,6 @@ __device__ __forceinline__ void varl_body(LaunchArgs& a) {
     const bool whole = (uint64_t)(tile + 1) * kWave <= a.n;
     if (whole && ballot(ml != 0 && (pb & 15) != 0) == 0) dma_window<true>(a, X, 0, 0, tile, lane);
     else stage(tile, X);
-    if (tile + W < ntiles) dma_meta<true>(a, buf(nwinb, nmetab), 0, tile + W, lane);
   }
   while (tile < ntiles) {
     uint64_t acc = 0;
@@ -2262,18 +2273,24 @@ static bool jit_forward_for(int kind, uint32_t n_uops) {
   return kind == kKindDag && (n_uops > kTileMaxUops || tile_kernel_for(kind, n_uops));
 }
 
-// The var tile loop (ebpf_tile_jit_varl) takes a compiled forward program's var-kernel batches
-// with offsets (4-byte aligned), lengths 4-byte aligned or absent, no final images or deopt list,
-// and tile indices in 31 bits. EBPFEMU_VARL=0 keeps ebpf_tile_jit_var (A/B).
+// The var tile loop (ebpf_tile_jit_varl) takes a compiled forward program's var-kernel batches:
+// offsets (4-byte aligned) or 16-byte aligned slots of >= 64 bytes, lengths 4-byte aligned or
+// absent, no final images, tile indices in 31 bits (store-mode programs with their deopt list
+// included). EBPFEMU_VARL=0 keeps ebpf_tile_jit_var (A/B).
 static bool g_varl = [] {
   const char* e = getenv("EBPFEMU_VARL");
   return !(e && e[0] == '0');
 }();
 static bool varl_ok(int kind, const LaunchArgs& a, const JitFns* jit, bool stack) {
-  return g_varl && jit && jit->varl && !jit->var_only && kind == kKindDag &&
-         jit_forward_for(kind, a.n_uops) && a.offsets && ((uintptr_t)a.offsets & 3) == 0 &&
-         ((uintptr_t)a.lens & 3) == 0 && !a.mem_out && !a.deopt && !a.perm &&
-         a.n_tiles < (1ull << 31);
+  const bool layout = a.offsets ? ((uintptr_t)a.offsets & 3) == 0
+                                : a.stride >= (uint64_t)kWin && a.stride < (1ull << 26) &&
+                                      (((uintptr_t)a.frames | (uintptr_t)a.stride) & 15) == 0;
+  // (the fixed-slot layout's programs keep ebpf_tile_jit_fixed; store-mode programs, which run
+  // on the var kernels only, are stack-window programs)
+  return g_varl && jit && jit->varl && kind == kKindDag && jit_forward_for(kind, a.n_uops) &&
+         layout && ((uintptr_t)a.lens & 3) == 0 && !a.mem_out && !a.perm &&
+         a.n_tiles < (1ull << 31) && (!jit_fixed_layout(&a) || jit->var_only) &&
+         (!jit->var_only || stack);
 }
 
 int launch_kernel_id(int kind, const LaunchArgs& a, const JitFns* jit, bool stack) {

@@ -1163,7 +1163,13 @@ struct Compiler {
     }
     std::string ool;
     std::string main = "; compiled eBPF program (store mode): " + std::to_string(n) + " micro-ops\n"
-                       "s_mov_b32 s52, s33\ns_mov_b32 s53, 0\n" + stack_zero() + stack_init(P, ool);
+                       "s_mov_b32 s52, s33\ns_mov_b32 s53, 0\n";
+    // (the var tile loop's windows hold packet bytes [0, 64): the xdp_md ctx shifted in first, as
+    // body does; the var kernel's C++ shifts them itself)
+    if (m.varl && !m.xdp.empty())
+      main += "s_cmp_lg_u32 " + m.xdp + ", 0\ns_cbranch_scc0 .L" + P + "noxdp\n" + xdp_shift() +
+              ".L" + P + "noxdp:\n";
+    main += stack_zero() + stack_init(P, ool);
     const std::string Z = ".L" + P + "zdone";
     main += "s_mov_b64 s[64:65], exec\ns_mov_b64 exec, -1\n"
             "v_cmp_gt_u32 vcc, 64, v31\ns_cbranch_vccz " + Z + "\n";

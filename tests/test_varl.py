@@ -233,3 +233,40 @@ def test_varl_xdp_md(cuda):
         ref = _outputs(prog, frames, kw, cuda, generic=True, regs=True)
         _same(got, ref, f"xdp bad {bad}")
     prog.close()
+
+
+@pytest.mark.parametrize("name", ["5tuple", "5tuple_stack", "nat"])
+def test_varl_stride_lens(cuda, oracle_mod, name):
+    """Stride + lens batches (16-byte aligned slots of 80 bytes, packets 0..80 bytes long) on the
+    var tile loop's stride mode (no offsets: addresses from the slot index): == the oracle and the
+    general interpreter; the NAT rewrite in store mode with lanes that deoptimize (ports past the
+    window) and their deopt pass."""
+    from ebpf_emu import Program, _lib
+    from ebpf_emu import workloads as W
+    from test_store_mode import _nat_packets
+
+    rng = random.Random(404)
+    img = W.program(name)
+    pkts = (_nat_packets(rng, 700) if name == "nat" else [gen_packet(rng) for _ in range(700)])
+    pkts = [p[:80] for p in pkts]
+    prog = Program(img)
+    import torch
+
+    buf = np.zeros((len(pkts), 80), dtype=np.uint8)
+    for i, p in enumerate(pkts):
+        buf[i, :len(p)] = np.frombuffer(p, dtype=np.uint8)
+    frames = torch.from_numpy(buf.reshape(-1)).to(cuda)
+    ln = np.array([len(p) for p in pkts], dtype=np.uint16)
+    kw = dict(n=len(pkts), stride=80, lens=torch.from_numpy(ln.view(np.int16)).to(cuda))
+    stack = name != "5tuple"
+    assert _route(prog, frames, kw) == (_lib.EBPF_KERNEL_JIT_VARL_STACK if stack
+                                        else _lib.EBPF_KERNEL_JIT_VARL)
+    got = _outputs(prog, frames, kw, cuda, regs=True)
+    ref = _outputs(prog, frames, kw, cuda, generic=True, regs=True)
+    ok = got["status"] != 7  # (ST_BADPKT lanes: no registers, main.rs:20-21 panics)
+    for k in ("verdict", "counters", "status"):
+        assert np.array_equal(got[k], ref[k]), (name, k)
+    for k in ("r0", "regs"):
+        assert np.array_equal(got[k][ok], ref[k][ok]), (name, k)
+    _check_prod_against_oracle(oracle_mod, img, pkts, got, tag=name)
+    prog.close()
