@@ -1786,9 +1786,22 @@ __global__ __launch_bounds__(kBlock, 8) void tile_kernel(LaunchArgs a) {
 // counter buckets. Launch conditions (jit_fixed_ok): the fixed-slot layout, n_tiles < 2^31 and
 // 64 * stride < 2^32, so tile indices and tile byte offsets are 32-bit scalars.
 extern "C" __global__ __launch_bounds__(kDbBlock, 1) void ebpf_tile_jit_fixed(LaunchArgs a) {
-  counters_init();
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t wv = rfl(threadIdx.x / kWave);
+  // the wave's first tile's windows go out before the workgroup's start barrier (counters_init:
+  // the 16 waves of a workgroup do not start together), the statement then skips that DMA
+  // (A/B: LaunchArgs::fixed_late)
+  uint32_t first = 1;
+  {
+    const uint32_t t0 = blockIdx.x + wv * gridDim.x;
+    if (!a.fixed_late && t0 < a.n_tiles) {
+      uint32_t ln;
+      asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+      dma_window_stride(a, smem + wv * kTileWaveLdsDb, t0, ln);
+      first = 0;
+    }
+  }
+  counters_init();
   uint32_t winb = lds_addr(smem + wv * kTileWaveLdsDb), nwinb = winb + kWinBytes;
   const uint32_t wx = winb ^ nwinb;
   uint32_t lane;
@@ -1826,7 +1839,7 @@ extern "C" __global__ __launch_bounds__(kDbBlock, 1) void ebpf_tile_jit_fixed(La
   if (trace) stamp(0);
 
   uint32_t cnt[7] = {0, 0, 0, 0, 0, 0, 0};
-  uint32_t ret = 0, ordv = 0, first = 1, tile = wg + wv * grid, rounds = 0;
+  uint32_t ret = 0, ordv = 0, tile = wg + wv * grid, rounds = 0;
   uint64_t retired = 0;
   while (tile < ntiles) {
     uint64_t acc = 0;
@@ -2321,6 +2334,10 @@ static bool g_var_db = [] {
   const char* e = getenv("EBPFEMU_VAR_DB");
   return e && e[0] == '1';
 }();
+static bool g_fixed_late = [] {  // A/B: EBPFEMU_FIXED_EARLY=0
+  const char* e = getenv("EBPFEMU_FIXED_EARLY");
+  return e && e[0] == '0';
+}();
 static bool g_var_pipe_host = [] {
   const char* e = getenv("EBPFEMU_VAR_PIPE");
   return !(e && e[0] == '0');
@@ -2359,6 +2376,7 @@ hipError_t launch_interp(int kind, const LaunchArgs& a, int grid, hipStream_t st
   LaunchArgs b = a;
   b.var_nopipe = (kind == kKindLoop ? g_loop_pipe : g_var_pipe_host) ? 0u : 1u;
   b.var_db = var && vdb ? 1u : 0u;
+  b.fixed_late = g_fixed_late ? 1u : 0u;
   // a shard word's sum must stay below 2^48: bound it by packets x steps per packet; and its
   // arrival count (16 bits) must reach the shard's workgroups - 1: at most 65535 members (the
   // compiled fixed-slot kernel's grid is one workgroup per CU, every other grid is `grid`)

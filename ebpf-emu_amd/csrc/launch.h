@@ -81,6 +81,8 @@ struct LaunchArgs {
                               //   metadata and then its windows, no metadata prefetch
   uint32_t var_db;            // the compiled var kernels: double-buffered windows, the next tile's
                               //   windows in flight while a tile runs (A/B, EBPFEMU_VAR_DB=1)
+  uint32_t fixed_late;        // A/B (EBPFEMU_FIXED_EARLY=0): the compiled fixed-slot kernel issues
+                              //   its first tile's windows after the workgroup's start barrier
   // store-mode programs (jit.h StackPlan::any_dyn): the deopt list in the workspace -- u32
   // [count, done] at kWsDeoptOff (zero between batches), idx[n] past the tier-1 slots. The
   // compiled kernel appends the packet index of every lane that deoptimized (status kStDeopt: no
