@@ -1934,7 +1934,6 @@ extern "C" __global__ __launch_bounds__(kBlock, 7) void ebpf_tile_jit_var(Launch
         : TILE_ASM_CLOBBER, TILE_ASM_CLOBBER_WINDOW
 template <bool STACK>
 __device__ __forceinline__ void varl_body(LaunchArgs& a) {
-  counters_init();
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t wv = rfl(threadIdx.x / kWave);
   uint8_t* const wbase = smem + wv * kVarlWaveLds;  // [window 0][window 1][metadata 0][metadata 1]
@@ -1992,14 +1991,18 @@ __device__ __forceinline__ void varl_body(LaunchArgs& a) {
   uint32_t cnt[7] = {0, 0, 0, 0, 0, 0, 0};
   uint64_t retired = 0;
   uint32_t tile = blockIdx.x * kWavesPerBlock + wv;
+  // the first two tiles' metadata at once, before the workgroup's start barrier (as the
+  // fixed-slot kernel's first DMA); then the first tile's windows (DMA'd when whole and aligned):
+  // the statement's first wait is for those windows alone. (Tried: both first tiles' windows in
+  // flight from the start, as the fixed-slot kernel's opening burst -- 17.6 vs 16.6 us per 1
+  // Mi-packet 5-tuple batch, A/B on one box.)
+  const WaveLds X = buf(winb, metab);
   if (tile < ntiles) {
-    // the first two tiles' metadata at once, then the first tile's windows (DMA'd when whole and
-    // aligned): the statement's first wait is for those windows alone. (Tried: both first tiles'
-    // windows in flight from the start, as the fixed-slot kernel's opening burst -- 17.6 vs
-    // 16.6 us per 1 Mi-packet 5-tuple batch, A/B on one box.)
-    const WaveLds X = buf(winb, metab);
     dma_meta<true>(a, X, 0, tile, lane);
     if (tile + W < ntiles) dma_meta<true>(a, buf(nwinb, nmetab), 0, tile + W, lane);
+  }
+  counters_init();
+  if (tile < ntiles) {
     dma_wait();
     uintptr_t pb;
     uint32_t ml;
