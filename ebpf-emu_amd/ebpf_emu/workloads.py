@@ -86,6 +86,28 @@ done:
     exit
 """
 
+# config 5 as a standard XDP program under the xdp_md calling convention (xdp.rs:16-20): the sum
+# over ctx->data .. ctx->data_end. Same verdicts as CHECKSUM on the same packets. A loop program:
+# its xdp_md batches are staged (interp.hip xdp_stage) for the compiled loop kernels.
+CHECKSUM_XDP = """
+    ldxw r2, [r1+0]           # ctx->data
+    ldxw r3, [r1+4]           # ctx->data_end
+    mov r0, 0
+    jge r2, r3, done
+loop:
+    ldxb r5, [r2+0]
+    add r0, r5
+    add r2, 1
+    jlt r2, r3, loop
+done:
+    mov r6, r0
+    rsh r6, 8
+    xor r0, r6
+    and r0, 1
+    add r0, 1                 # DROP (1) or PASS (2) by parity
+    exit
+"""
+
 # config 5 with its running sum kept in a stack slot (r10 - 8) instead of a register, the way
 # compiled C keeps a spilled accumulator: memory tier 0.5 with a loop (the loop kernel's stack
 # variant). Same verdicts as CHECKSUM.
@@ -456,7 +478,7 @@ l4_out:
 PROGRAMS = {"drop": DROP_ALL, "5tuple": FIVE_TUPLE, "checksum": CHECKSUM,
             "5tuple_stack": FIVE_TUPLE_STACK, "mac_swap_tx": MAC_SWAP_TX, "acl": ACL,
             "5tuple_xdp": FIVE_TUPLE_XDP, "checksum_stack": CHECKSUM_STACK,
-            "5tuple_call": FIVE_TUPLE_CALL, "nat": NAT_REWRITE}
+            "5tuple_call": FIVE_TUPLE_CALL, "nat": NAT_REWRITE, "checksum_xdp": CHECKSUM_XDP}
 
 
 def program(name: str) -> bytes:

@@ -277,3 +277,32 @@ def test_xdp_md_loop_programs_staged(cuda):
     prog.close()
     del torch
 
+
+
+def test_xdp_md_checksum_loop_full_size(cuda):
+    """The per-byte checksum as a standard XDP program (workloads.CHECKSUM_XDP: the sum over
+    ctx->data .. ctx->data_end, a loop program: its batch staged by xdp_stage for the compiled
+    loop kernels) over a 256 Ki slice of config 5's mixed 64/1500-byte frames with 2048-byte
+    images: the same verdicts and verdict counters as the plain checksum (CHECKSUM, main.rs
+    layout) on the same packets, which test_workload_golden_full_size pins to the oracle."""
+    import torch
+
+    from ebpf_emu import Program
+    from ebpf_emu import workloads as W
+
+    n = 1 << 18
+    buf, offs, lens = W.frames_mixed(n)
+    frames = torch.from_numpy(buf).to(cuda)
+    kw = dict(n=n, offsets=torch.from_numpy(offs.view(np.int32)).to(cuda),
+              lens=torch.from_numpy(lens.view(np.int16)).to(cuda), mem_size=2048, r10=2048)
+    out = {}
+    for name, xdp in (("checksum", False), ("checksum_xdp", True)):
+        prog = Program(W.program(name))
+        cnt = torch.zeros(8, dtype=torch.int64, device=cuda)
+        res = prog.run(frames, counters=cnt, xdp_md=xdp, **kw)
+        torch.cuda.synchronize()
+        out[name] = (res.verdict.cpu().numpy(), cnt.cpu().numpy().view(np.uint64))
+        prog.close()
+    assert np.array_equal(out["checksum"][0], out["checksum_xdp"][0])
+    assert list(out["checksum"][1][:7]) == list(out["checksum_xdp"][1][:7])
+    assert (out["checksum"][0] == 1).sum() > 1000 and (out["checksum"][0] == 2).sum() > 1000
