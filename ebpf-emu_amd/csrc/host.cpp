@@ -269,6 +269,7 @@ struct ebpf_prog {
   TUop* dev_pltuopsx[kMaxDevices] = {};
   uint32_t pguard_k = 0;
   bool pjit_deep = false;  // variant 4 compiled into ebpf_tile_jit_loop_deep
+  bool xjit_deep = false;  // variant 5 likewise
 };
 
 // Diagnostics: EBPFEMU_TRACE=1 gives the compiled fixed-slot kernel a per-device stamp buffer
@@ -308,6 +309,12 @@ static int jit_compile_locked(ebpf_prog* p) {
     p->jit_has[2] = !p->ltuops.empty() && !p->ltuopsx.empty();
     p->jit_has[3] = !p->tuopsk_xdp.empty() && !p->stack.k;
     p->jit_has[4] = !p->pltuops.empty() && !p->pltuopsx.empty();
+    // variant 5: a loop program that reads a 4-byte word through r1 (an xdp_md program's ctx
+    // loads) gets a copy for xdp_md batches, whose staged images' ctx the range analysis knows
+    p->jit_has[5] = false;
+    if (p->jit_has[2] && !p->stack.k)
+      for (const Uop& u : p->xuops)
+        p->jit_has[5] = p->jit_has[5] || (u.op == U_LDX && u.aux == 4 && u.src == 1);
     if (p->stack.k) p->jit_has[1] = !p->tuopsk.empty();  // (the main.rs layout only)
     if (g_no_jit || (!p->jit_has[0] && !p->jit_has[1] && !p->jit_has[2])) {
       p->jit_state = 2;
@@ -315,6 +322,14 @@ static int jit_compile_locked(ebpf_prog* p) {
       p->jit_state = 1;
       for (int v = 0; v < kJitVariants && p->jit_state == 1; v++) {
         if (!p->jit_has[v]) continue;
+        if (v == 5) {  // the xdp_md copy: dropped (the plain loop program runs) if it fails
+          if (!jit_compile_loop(p->xuops, p->ltuops, p->ltuopsx, p->jit_co[5], &p->jit_err,
+                                &p->jit_asm[5], nullptr, &p->xjit_deep, 0, true)) {
+            p->jit_has[5] = false;
+            p->jit_co[5].clear();
+          }
+          continue;
+        }
         if (v == 4) {  // the promoted program: dropped (the stack loop kernel stays) if it fails
           if (!jit_compile_loop(p->puops, p->pltuops, p->pltuopsx, p->jit_co[4], &p->jit_err,
                                 &p->jit_asm[4], nullptr, &p->pjit_deep, p->pguard_k)) {
@@ -1401,7 +1416,8 @@ int ebpf_prog_upload(ebpf_prog* p, int device) {
       if (p->jit_has[v]) {
         if (!jit_load(p->jit_co[v], &p->jit_mod[device][v], &p->jit_fn[device][v]))
           rc = EBPF_EHIP;
-        else if ((v == 2 && p->jit_deep) || (v == 4 && p->pjit_deep))  // (the code is in the
+        else if ((v == 2 && p->jit_deep) || (v == 4 && p->pjit_deep) ||
+                 (v == 5 && p->xjit_deep))                              // (the code is in the
           p->jit_fn[device][v].loop = p->jit_fn[device][v].loop_deep;     // deep-prefetch kernel)
         p->jit_fn[device][v].var_only = p->stack.any_dyn;
       }
@@ -1796,6 +1812,11 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* bin, const ebpf_batch_out* ou
     }
   }
   const JitFns* jit = batch_jit(p, b, kind, stk, device);
+  // an xdp_md batch of a loop program runs staged: variant 5, whose range analysis knows the
+  // staged images' ctx (data = 8, data_end = LEN)
+  if (jit == &p->jit_fn[device][2] && (bin->flags & EBPF_BATCH_XDP_MD) && !xdp_direct &&
+      p->jit_mod[device][5])
+    jit = &p->jit_fn[device][5];
   // store mode (register-address packet stores, StackPlan::any_dyn): lanes the compiled kernel
   // cannot finish are listed, then re-run from the start by the general interpreter (tier 1)
   // (the promoted program: lanes whose packet reaches the slots, jit.cpp promo_guard)

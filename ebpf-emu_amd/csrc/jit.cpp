@@ -249,6 +249,55 @@ struct Compiler {
   bool deep_regs = false;  // compiled for ebpf_tile_jit_loop_deep: v[72:105] are the program's
   uint32_t guard_k = 0;  // a stack-slot promoted program (host.cpp promote_slots): the guard
   uint32_t dma_chunks = 4;  // the fixed-slot window DMA's chunks (compile_into_template)
+  // xdp_md batches of loop programs run on their staged images (interp.hip xdp_stage): image
+  // dwords 0 and 4 are the ctx, data = 8 and data_end = 8 + len = LEN (xdp.rs:16-20), so the
+  // range analysis gives `ldxw rX, [ctx + 0]` the constant 8 and `ldxw rX, [ctx + 4]` LEN -- the
+  // loop over data .. data_end is then a loop below LEN, as the main.rs layout's over r2
+  bool xdp_ctx = false;
+  // (xdp_ctx) the ctx loads: `ldxw rX, [r1 + 0 / 4]` with r1 still the initial r1 (the image's
+  // start) on every path -- the value is the staged ctx's data (8) or data_end (LEN), a 4-byte
+  // load that cannot fault in an image of >= 8 bytes; compiled as one move into rX's low word
+  // (the load's merge, Q1), and not a load for the byte-loop machinery (zero windows, prefetch)
+  mutable std::vector<int> ctx_off;  // per micro-op: 0 / 4, or -1
+  int ctx_load(uint32_t i) const {
+    if (!xdp_ctx) return -1;
+    if (ctx_off.empty()) {
+      std::vector<char> seen(n, 0), init(n, 0);  // init[i]: r1 unmodified on every path to i
+      std::vector<uint32_t> work{0};
+      seen[0] = init[0] = 1;
+      auto flow = [&](uint32_t to, bool v) {
+        if (to >= n) return;
+        if (!seen[to]) {
+          seen[to] = 1, init[to] = v, work.push_back(to);
+        } else if (init[to] && !v) {
+          init[to] = 0, work.push_back(to);
+        }
+      };
+      while (!work.empty()) {
+        const uint32_t i = work.back();
+        work.pop_back();
+        const Uop& u = uops[i];
+        const bool writes1 = u.dst == 1 && u.op != U_ST && u.op != U_STX && !is_jump(u) &&
+                             u.op != U_EXIT && u.op != U_FAULT;
+        const bool v = init[i] && !writes1 && u.op != U_CALL &&
+                       !(u.op == U_ATOMIC && u.src == 1);
+        if (u.op == U_EXIT || u.op == U_FAULT) continue;
+        if (u.op == U_JA) {
+          flow((uint32_t)u.x, v);
+          continue;
+        }
+        if (is_jump(u)) flow((uint32_t)u.x, v);
+        flow(i + 1, v);
+      }
+      ctx_off.assign(n, -1);
+      for (uint32_t i = 0; i < n; i++) {
+        const Uop& u = uops[i];
+        if (seen[i] && init[i] && u.op == U_LDX && u.aux == 4 && u.src == 1 && (u.x == 0 || u.x == 4))
+          ctx_off[i] = u.x;
+      }
+    }
+    return ctx_off[i];
+  }
   mutable bool coop_emitted = false;  // a coop_sum entry was emitted (compile_into_template:
                                       // such programs go to the deep kernel, unbinned)
 
@@ -355,7 +404,8 @@ struct Compiler {
   }
 
   // Transfer of micro-op u over s; jumps also give the taken successor's state (tk).
-  static void av_step(const Uop& u, const AbsRegs& s, AbsRegs& nt, AbsRegs& tk) {
+  static void av_step(const Uop& u, const AbsRegs& s, AbsRegs& nt, AbsRegs& tk,
+                      bool xdp_ctx = false) {
     nt = s;
     tk = s;
     const bool reg = (u.aux & F_SRC) != 0;
@@ -412,6 +462,18 @@ struct Compiler {
       case U_LDX: {  // the loaded bytes replace the low aux bytes; the rest of dst stays (Q1)
         d = AbsVal();
         if (u.aux < 8 && a.hi < (1ull << (8 * u.aux))) d.hi = (1ull << (8 * u.aux)) - 1;
+        // (xdp_ctx: a 4-byte load of image dword 0 or 4 into a register whose upper half is
+        // zero is the ctx's data = 8 or data_end = LEN)
+        const AbsVal& base = s[u.src];
+        if (xdp_ctx && u.aux == 4 && a.hi < (1ull << 32) && base.lo == base.hi) {
+          const uint64_t addr = base.lo + (uint64_t)(int64_t)(int32_t)u.x;
+          if (addr == 0) {
+            d = av_const(8);
+          } else if (addr == 4) {
+            d = AbsVal();
+            d.hi = kLenMax, d.slack = 0, d.is_len = true;
+          }
+        }
         return;
       }
       default: break;
@@ -526,7 +588,7 @@ struct Compiler {
       work.pop_back();
       const Uop& u = uops[i];
       AbsRegs nt, tk;
-      av_step(u, in[i], nt, tk);
+      av_step(u, in[i], nt, tk, xdp_ctx);
       if (u.op == U_EXIT || u.op == U_FAULT) continue;
       if (u.op == U_JA) {
         flow((uint32_t)u.x, tk);
@@ -2875,6 +2937,10 @@ struct Compiler {
       main += ldxk_fast(i);
       return true;
     }
+    if (const int co = ctx_load(i); co >= 0) {  // (xdp_ctx: the staged ctx's data / data_end)
+      main += "v_mov_b32 v" + std::to_string(2 * uops[i].dst) + ", " + (co ? "v31" : "8") + "\n";
+      return true;
+    }
     if (!loops && (m.fixed == "1" || m.stack || m.varl) &&
         (id == T_LDX_C || id == T_LDX_E || id == T_LDX1_C || id == T_LDX1_E)) {
       std::string ot;
@@ -3081,7 +3147,8 @@ struct Compiler {
     // (stack-window programs: the plain refillable windows, the loads' store-forwarding overlay)
     bool only_bytes = !getenv("EBPFEMU_NO_ZERO_WINDOW") && !stk;
     if (stk) cache = xc.cache = false;
-    for (const Uop& o : uops) only_bytes = only_bytes && (o.op != U_LDX || o.aux == 1);
+    for (uint32_t i = 0; i < n; i++)
+      only_bytes = only_bytes && (uops[i].op != U_LDX || uops[i].aux == 1 || ctx_load(i) >= 0);
     zwin = xc.zwin = only_bytes && !cache;
     qcache = xc.qcache = zwin && !getenv("EBPFEMU_NO_QCACHE");
     prefetch = xc.prefetch = zwin && !getenv("EBPFEMU_NO_PREFETCH");
@@ -3098,8 +3165,8 @@ struct Compiler {
     const char* bc = getenv("EBPFEMU_BYTE_CACHE");
     if (stk || (bc && bc[0] == '1') || getenv("EBPFEMU_NO_ZERO_WINDOW") || getenv("EBPFEMU_NO_PREFETCH"))
       return false;
-    for (const Uop& o : uops)
-      if (o.op == U_LDX && o.aux != 1) return false;
+    for (uint32_t i = 0; i < n; i++)
+      if (uops[i].op == U_LDX && uops[i].aux != 1 && ctx_load(i) < 0) return false;
     return true;
   }
 
@@ -3381,7 +3448,7 @@ bool jit_compile(const std::vector<Uop>& uops, const std::vector<TUop>& t,
 bool jit_compile_loop(const std::vector<Uop>& uops, const std::vector<TUop>& t,
                       const std::vector<TUop>& tx, std::vector<char>& code_object,
                       std::string* err, std::string* asm_out, const StackPlan* stk,
-                      bool* deep, uint32_t guard_k) {
+                      bool* deep, uint32_t guard_k, bool xdp_ctx) {
   if (uops.empty() || uops.size() > kJitMaxUops || t.size() < uops.size() ||
       tx.size() < uops.size() ||
       (stk && (stk->k == 0 || stk->k > kStackMax || stk->k % 4 || stk->off.size() != uops.size() ||
@@ -3390,6 +3457,7 @@ bool jit_compile_loop(const std::vector<Uop>& uops, const std::vector<TUop>& t,
     return false;
   }
   Compiler c(uops, t, true, false, stk), xc(uops, tx, true, true, stk);
+  c.xdp_ctx = xc.xdp_ctx = xdp_ctx;
   if (guard_k) {  // a promoted program: its packet loads cannot reach the window of any lane
     if (stk || !c.all_loads_proven()) {  // whose LEN <= r10 - guard_k
       if (err) *err = "promoted program: a load not proven inside the packet";

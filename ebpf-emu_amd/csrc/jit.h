@@ -33,8 +33,10 @@ struct JitFns {
 // packet's header window at constant addresses (the preloaded window dwords v[64 : 79]).
 // compiled variants of a program: 0 init_regs batches, 1 the main.rs layout (constant-address
 // loads resolved), 2 the loop kernel, 3 xdp_md batches (the ctx's data field known, host.cpp
-// fold_const_loads), 4 the stack-slot promoted loop program (host.cpp promote_slots)
-constexpr int kJitVariants = 5;
+// fold_const_loads), 4 the stack-slot promoted loop program (host.cpp promote_slots), 5 the loop
+// program for xdp_md batches (staged images: the ctx's data and data_end known to the range
+// analysis, jit.cpp Compiler::xdp_ctx)
+constexpr int kJitVariants = 6;
 constexpr uint32_t kStackMax = 64;    // window bytes
 constexpr uint32_t kStackVgpr = 80;   // first VGPR of the window (ebpf_tile_jit_fixed)
 constexpr int32_t kNoStack = INT32_MIN;
@@ -78,7 +80,8 @@ bool jit_compile(const std::vector<Uop>& uops, const std::vector<TUop>& t,
 bool jit_compile_loop(const std::vector<Uop>& uops, const std::vector<TUop>& t,
                       const std::vector<TUop>& tx, std::vector<char>& code_object,
                       std::string* err, std::string* asm_out = nullptr,
-                      const StackPlan* stk = nullptr, bool* deep = nullptr, uint32_t guard_k = 0);
+                      const StackPlan* stk = nullptr, bool* deep = nullptr, uint32_t guard_k = 0,
+                      bool xdp_ctx = false);
 
 // Windows the refills of byte-scanning loop programs prefetch ahead: 1 (ebpf_tile_jit_loop, 5
 // waves per SIMD) or 2-3 (ebpf_tile_jit_loop_deep, 4 waves); EBPFEMU_PF_DEPTH overrides.

@@ -49,12 +49,51 @@ done:
 """
 
 
+# the loop bound reloaded from the ctx every iteration (a compiled xdp_md loop program's ctx
+# loads, jit.cpp ctx_load, inside the loop)
+XDP_SUM_RELOAD = """
+    ldxw r2, [r1+0]
+    mov r0, 0
+loop:
+    ldxw r3, [r1+4]
+    jge r2, r3, done
+    ldxb r5, [r2+0]
+    add r0, r5
+    add r2, 1
+    ja loop
+done:
+    exit
+"""
+
+# a ctx-shaped load that is not the ctx on every path (r1 moved on one of them): compiled as a
+# load, not as the ctx's data_end
+XDP_R1_MOVED = """
+    ldxw r2, [r1+0]
+    ldxw r3, [r1+4]
+    mov r0, 0
+    ldxb r4, [r2+0]
+    jeq r4, 0, skip
+    add r1, 4
+skip:
+    ldxw r6, [r1+4]
+    add r0, r6
+loop:
+    jge r2, r3, done
+    ldxb r5, [r2+0]
+    add r0, r5
+    add r2, 1
+    ja loop
+done:
+    exit
+"""
+
+
 def _images(pkts):
     return [struct.pack("<II", 8, 8 + len(p)) + p for p in pkts]
 
 
 @pytest.mark.parametrize("layout", [dict(), dict(offsets_layout=True, misalign=3)])
-@pytest.mark.parametrize("src", [XDP_PARSE, XDP_SUM])
+@pytest.mark.parametrize("src", [XDP_PARSE, XDP_SUM, XDP_SUM_RELOAD, XDP_R1_MOVED])
 def test_xdp_md_images_match_oracle(cuda, oracle_mod, layout, src):
     import torch
 
@@ -103,7 +142,7 @@ def _xdp_packets(rng, n, lens=(0, 1, 7, 10, 14, 33, 34, 60, 64, 100, 1010, 1016,
 
 @pytest.mark.parametrize("layout", [dict(), dict(offsets_layout=True, align=16),
                                     dict(offsets_layout=True, misalign=3)])
-@pytest.mark.parametrize("src", [XDP_PARSE, XDP_SUM])
+@pytest.mark.parametrize("src", [XDP_PARSE, XDP_SUM, XDP_SUM_RELOAD, XDP_R1_MOVED])
 def test_xdp_md_production_outputs(cuda, oracle_mod, layout, src):
     """The outputs a production caller asks for, no registers and no image: a verdict + counters
     launch, then an r0 + status launch -- the compiled kernels' liveness-pruned register init

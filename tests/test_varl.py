@@ -270,3 +270,36 @@ def test_varl_stride_lens(cuda, oracle_mod, name):
         assert np.array_equal(got[k][ok], ref[k][ok]), (name, k)
     _check_prod_against_oracle(oracle_mod, img, pkts, got, tag=name)
     prog.close()
+
+
+def test_varl_init_regs(cuda):
+    """Caller-set registers (Emu.state.regs, emu.rs:14-17: batch.init_regs) on the var tile loop
+    (the statement's out-of-line initialisation): every output == the general interpreter's, for
+    random forward programs and register sets."""
+    import torch
+
+    from ebpf_emu import Program, _lib
+
+    rng = random.Random(77)
+    done = 0
+    for it in range(12):
+        img = gen_program(rng, allow_loops=False, tier0=True)
+        prog = Program(img)
+        if not prog.forward_only:
+            prog.close()
+            continue
+        pkts = [gen_packet(rng) for _ in range(130)]
+        frames, kw = _mixed(pkts, cuda, bad_every=rng.choice([0, 29]))
+        regs = [rng.choice([0, 1, 7, 64, 1 << 33, (1 << 64) - 5, rng.getrandbits(64)])
+                for _ in range(11)]
+        regs[10] = 512
+        ir = torch.tensor(np.array(regs, dtype=np.uint64).view(np.int64), device=cuda)
+        if _route(prog, frames, kw, init_regs=ir, max_steps=STEPS) != _lib.EBPF_KERNEL_JIT_VARL:
+            prog.close()
+            continue
+        got = _outputs(prog, frames, kw, cuda, regs=True, init_regs=ir)
+        ref = _outputs(prog, frames, kw, cuda, generic=True, regs=True, init_regs=ir)
+        _same(got, ref, f"init_regs it {it} prog {img.hex()}")
+        prog.close()
+        done += 1
+    assert done >= 5
