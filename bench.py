@@ -63,6 +63,10 @@ CONFIGS = {
     # kernel with the header window in LDS; --generic: the general interpreter's tier 1)
     "nat": (2, "IPv4 NAT rewrite: TTL - 1 + checksum, port redirect through the L4 pointer (40 insns) "
                "over 1Mi x 64B frames"),
+    # config 5 as a standard XDP program: the sum over ctx->data .. ctx->data_end (a loop program's
+    # xdp_md batch: staged images, compiled with the staged ctx known -- DESIGN 3.17)
+    "checksum_xdp": (4, "per-byte checksum as a standard XDP program (xdp_md ctx) over 1Mi mixed "
+                        "64B/1500B frames"),
 }
 PROGRAM_OF = {"stack": "5tuple_stack", "tier1": "mac_swap_tx", "xdp": "5tuple_xdp",
               "call": "5tuple_call"}
@@ -199,7 +203,7 @@ def stub_rank(args, world, rank):
         sys.exit(3)
     dist.init_process_group("gloo")
     prog_name = PROGRAM_OF.get(args.config, args.config)
-    mixed = args.config in ("checksum", "checksum_stack")
+    mixed = args.config in ("checksum", "checksum_stack", "checksum_xdp")
     with open(PIN_FIXTURE) as f:
         cc = json.load(f)["programs"][prog_name]["chunk_counters"]
     # (the pool size bench's loop below reaches for 1 Mi packets per batch)
@@ -282,7 +286,7 @@ def main():
         desc = desc.replace("64B frames", f"{(max(64, args.frame_bytes) + 15) // 16 * 16}B frame slots")
     if args.layout == "offsets":
         desc += " (offsets + lens batch)"
-        assert not args.total_packets and args.config not in ("checksum", "checksum_stack")
+        assert not args.total_packets and args.config not in ("checksum", "checksum_stack", "checksum_xdp")
     n = args.packets
     img = W.program(PROGRAM_OF.get(args.config, args.config))
     prog = Program(img)
@@ -291,7 +295,7 @@ def main():
     # ---- synthetic device-resident batches ----
     from ebpf_emu import dist as D
 
-    mixed = args.config in ("checksum", "checksum_stack")
+    mixed = args.config in ("checksum", "checksum_stack", "checksum_xdp")
     fb = (max(64, args.frame_bytes) + 15) // 16 * 16  # fixed slots: 16-byte aligned, >= 64
     batches = []
     pool_bytes = 0
@@ -347,7 +351,8 @@ def main():
     for b in batches:
         if mixed:
             bd = prog.make_batch(b["frames"], n=n, offsets=b["offsets"], lens=b["lens"],
-                                 mem_size=mem_size, r10=r10, generic=args.generic)
+                                 mem_size=mem_size, r10=r10, generic=args.generic,
+                                 xdp_md=args.config == "checksum_xdp")
         else:
             bd = prog.make_batch(b["frames"], n=n, stride=fb, offsets=b.get("offsets"),
                                  lens=b.get("lens"), mem_size=mem_size, r10=r10,
@@ -642,7 +647,8 @@ def cpu_baseline(args, img, batch0, mixed, n, mem_size, r10):
     stride = (max(64, args.frame_bytes) + 15) // 16 * 16
 
     def rate(nthreads, seconds):
-        kw = dict(mem_size=mem_size, r10=r10, threads=nthreads, xdp_md=args.config == "xdp")
+        kw = dict(mem_size=mem_size, r10=r10, threads=nthreads,
+                  xdp_md=args.config in ("xdp", "checksum_xdp"))
         # chunks sized to ~0.2 s of work so the time budget is met closely
         chunk = max(4096, min(n, int((1 << 14 if mixed else 1 << 20) * nthreads / 8)))
         done = 0

@@ -118,7 +118,7 @@ PIN_CHUNKS_64 = 128  # 16 pool batches x 8 ranks
 PIN_CHUNKS_MIXED = 16  # 2 pool batches x 8 ranks (a 1 Mi mixed batch is ~840 MB: one per rank)
 PIN_PROGRAMS_64 = ("5tuple", "drop", "5tuple_stack", "mac_swap_tx", "acl", "5tuple_xdp",
                    "5tuple_call", "nat")
-PIN_PROGRAMS_MIXED = ("checksum", "checksum_stack")
+PIN_PROGRAMS_MIXED = ("checksum", "checksum_stack", "checksum_xdp")
 
 
 def _pin_chunk(args):
@@ -138,26 +138,35 @@ def _pin_chunk(args):
         for name in PIN_PROGRAMS_MIXED:
             p = oracle.Program(W.program(name))
             _, _, cnt = p.run_batch(buf, D.CHUNK, offsets=offs, lens=lens, mem_size=2048,
-                                    r10=2048, threads=1)
+                                    r10=2048, threads=1, xdp_md=name == "checksum_xdp")
             out[name] = [int(x) for x in cnt]
     return kind, c, out
 
 
 def bench_pins_add(names):
-    """Adds programs' 64-byte chunk counters to the committed bench_pins.json (same chunks)."""
+    """Adds programs' chunk counters to the committed bench_pins.json (same chunks): names from
+    PIN_PROGRAMS_MIXED get the mixed chunks, the rest the 64-byte chunks."""
     from multiprocessing import Pool
 
-    global PIN_PROGRAMS_64
+    global PIN_PROGRAMS_64, PIN_PROGRAMS_MIXED
     path = os.path.join(HERE, "bench_pins.json")
     with open(path) as f:
         pins = json.load(f)
-    PIN_PROGRAMS_64 = tuple(names)
+    mixed_names = tuple(n for n in names if n in PIN_PROGRAMS_MIXED)
+    PIN_PROGRAMS_64 = tuple(n for n in names if n not in PIN_PROGRAMS_MIXED)
+    PIN_PROGRAMS_MIXED = mixed_names
+    jobs = ([("64", c) for c in range(PIN_CHUNKS_64)] if PIN_PROGRAMS_64 else []) + \
+        ([("mixed", c) for c in range(PIN_CHUNKS_MIXED)] if mixed_names else [])
     with Pool(max(1, min(8, os.cpu_count() or 1) - 1)) as pool:
-        res = pool.map(_pin_chunk, [("64", c) for c in range(PIN_CHUNKS_64)])
+        res = pool.map(_pin_chunk, jobs)
     for name in names:
-        rows = sorted((c, o[name]) for _, c, o in res)
-        pins["programs"][name] = {"frames": "fixed64", "xdp_md": False,
-                                  "program": W.program(name).hex(), "mem_size": 1024, "r10": 512,
+        mixed = name in mixed_names
+        rows = sorted((c, o[name]) for kind, c, o in res if (kind == "mixed") == mixed)
+        pins["programs"][name] = {"frames": "mixed" if mixed else "fixed64",
+                                  "xdp_md": name in ("5tuple_xdp", "checksum_xdp"),
+                                  "program": W.program(name).hex(),
+                                  "mem_size": 2048 if mixed else 1024,
+                                  "r10": 2048 if mixed else 512,
                                   "chunk_counters": [cnt for _, cnt in rows]}
     with open(path, "w") as f:
         json.dump(pins, f, indent=0)
@@ -177,7 +186,8 @@ def bench_pins():
         rows = sorted((c, o[name]) for kind, c, o in res if (kind == "mixed") == mixed)
         for _, cnt in rows:
             assert sum(cnt[:7]) == D.CHUNK
-        progs[name] = {"frames": "mixed" if mixed else "fixed64", "xdp_md": name == "5tuple_xdp",
+        progs[name] = {"frames": "mixed" if mixed else "fixed64",
+                       "xdp_md": name in ("5tuple_xdp", "checksum_xdp"),
                        "program": W.program(name).hex(),
                        "mem_size": 2048 if mixed else 1024, "r10": 2048 if mixed else 512,
                        "chunk_counters": [cnt for _, cnt in rows]}

@@ -30,7 +30,8 @@ def _pins():
         return json.load(f)
 
 
-@pytest.mark.parametrize("n,config", [(2, "5tuple"), (3, "acl"), (2, "checksum")])
+@pytest.mark.parametrize("n,config", [(2, "5tuple"), (3, "acl"), (2, "checksum"),
+                                           (2, "checksum_xdp")])
 def test_launcher_spawns_ranks_and_pins(n, config):
     steps = 5
     r = _bench(["--gpus", str(n), "--steps", str(steps), "--config", config], {})
@@ -42,7 +43,7 @@ def test_launcher_spawns_ranks_and_pins(n, config):
     assert d["parity_pinned"] and f"k*{n}+r" in d["parity_pinned"]
     # the summed counters are the fixture's counters of chunks k*n + r, computed independently
     cc = _pins()["programs"][config]["chunk_counters"]
-    pool = 1 if config == "checksum" else 8
+    pool = 1 if config.startswith("checksum") else 8
     want = [0] * 8
     for i in range(steps):
         for rank in range(n):
