@@ -270,6 +270,7 @@ struct ebpf_prog {
   uint32_t pguard_k = 0;
   bool pjit_deep = false;  // variant 4 compiled into ebpf_tile_jit_loop_deep
   bool xjit_deep = false;  // variant 5 likewise
+  bool rjit_deep = false;  // variant 6 likewise
 };
 
 // Diagnostics: EBPFEMU_TRACE=1 gives the compiled fixed-slot kernel a per-device stamp buffer
@@ -315,6 +316,9 @@ static int jit_compile_locked(ebpf_prog* p) {
     if (p->jit_has[2] && !p->stack.k)
       for (const Uop& u : p->xuops)
         p->jit_has[5] = p->jit_has[5] || (u.op == U_LDX && u.aux == 4 && u.src == 1);
+    // variant 6: the same program for xdp_md batches in place (rebased, jit.cpp
+    // Compiler::xdp_rebase) when every packet load is proven past the ctx
+    p->jit_has[6] = p->jit_has[5];
     if (p->stack.k) p->jit_has[1] = !p->tuopsk.empty();  // (the main.rs layout only)
     if (g_no_jit || (!p->jit_has[0] && !p->jit_has[1] && !p->jit_has[2])) {
       p->jit_state = 2;
@@ -322,11 +326,13 @@ static int jit_compile_locked(ebpf_prog* p) {
       p->jit_state = 1;
       for (int v = 0; v < kJitVariants && p->jit_state == 1; v++) {
         if (!p->jit_has[v]) continue;
-        if (v == 5) {  // the xdp_md copy: dropped (the plain loop program runs) if it fails
-          if (!jit_compile_loop(p->xuops, p->ltuops, p->ltuopsx, p->jit_co[5], &p->jit_err,
-                                &p->jit_asm[5], nullptr, &p->xjit_deep, 0, true)) {
-            p->jit_has[5] = false;
-            p->jit_co[5].clear();
+        if (v == 5 || v == 6) {  // the xdp_md copies: dropped (staged / the plain loop program
+                                 // runs) if they fail
+          std::string e;
+          if (!jit_compile_loop(p->xuops, p->ltuops, p->ltuopsx, p->jit_co[v], &e, &p->jit_asm[v],
+                                nullptr, v == 5 ? &p->xjit_deep : &p->rjit_deep, 0, true, v == 6)) {
+            p->jit_has[v] = false;
+            p->jit_co[v].clear();
           }
           continue;
         }
@@ -1417,7 +1423,7 @@ int ebpf_prog_upload(ebpf_prog* p, int device) {
         if (!jit_load(p->jit_co[v], &p->jit_mod[device][v], &p->jit_fn[device][v]))
           rc = EBPF_EHIP;
         else if ((v == 2 && p->jit_deep) || (v == 4 && p->pjit_deep) ||
-                 (v == 5 && p->xjit_deep))                              // (the code is in the
+                 (v == 5 && p->xjit_deep) || (v == 6 && p->rjit_deep))  // (the code is in the
           p->jit_fn[device][v].loop = p->jit_fn[device][v].loop_deep;     // deep-prefetch kernel)
         p->jit_fn[device][v].var_only = p->stack.any_dyn;
       }
@@ -1618,6 +1624,23 @@ static bool xdp_in_place(ebpf_prog* p, const ebpf_batch* b, bool mem_out, int de
          (id == EBPF_KERNEL_TILE && !launch_fixed_layout(a));
 }
 
+// An xdp_md batch of a loop program in place (no staging copy): variant 6, the program rebased
+// (jit.cpp Compiler::xdp_rebase; compiled only when every packet load is proven past the ctx),
+// runs the batch as the main.rs layout over the packets with mem_size - 8 (rebased_batch). Not
+// with final images (they hold the ctx) or caller-set registers (the proofs assume r1 = the ctx).
+static bool xdp_rebased(ebpf_prog* p, const ebpf_batch* b, const ebpf_batch_out* out, int device,
+                        int kind, bool stk) {
+  if (!(b->flags & EBPF_BATCH_XDP_MD) || g_xdp_stage || kind != kKindLoop || stk) return false;
+  if (!p->jit_mod[device][6] || out->mem || b->init_regs || b->mem_size < 8) return false;
+  return batch_jit(p, b, kind, stk, device) == &p->jit_fn[device][2];
+}
+static ebpf_batch rebased_batch(const ebpf_batch* b) {
+  ebpf_batch r = *b;
+  r.flags &= ~EBPF_BATCH_XDP_MD;
+  r.mem_size -= 8;
+  return r;
+}
+
 // The general interpreter's tier-1 grid for a batch (its wave slots' images: the workspace).
 static int tier1_grid(const ebpf_prog* p, const ebpf_batch* b, int device) {
   int cur = device_of_current();
@@ -1723,16 +1746,21 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* bin, const ebpf_batch_out* ou
     if (cur != device) hipSetDevice(cur);
     return EBPF_EHIP;
   }
+  const bool xdp_direct = xdp_in_place(p, bin, out->mem != nullptr, device, kind, stk);
+  const bool xdp_rb = !xdp_direct && xdp_rebased(p, bin, out, device, kind, stk);
+  if (xdp_rb) {  // (the batch run as the main.rs layout: no staging region)
+    staged = rebased_batch(bin);
+    b = &staged;
+  }
   // scratch: caller-provided or library-owned per (device, stream)
-  const uint64_t need = ebpf_workspace_bytes(p, bin, device);
+  const uint64_t need = ebpf_workspace_bytes(p, b, device);
   uint8_t* ws = nullptr;
   rc = batch_workspace(bin, need, device, s, &ws);
   if (rc) {
     if (cur != device) hipSetDevice(cur);
     return rc;
   }
-  const bool xdp_direct = xdp_in_place(p, bin, out->mem != nullptr, device, kind, stk);
-  if ((bin->flags & EBPF_BATCH_XDP_MD) && !xdp_direct) {
+  if ((bin->flags & EBPF_BATCH_XDP_MD) && !xdp_direct && !xdp_rb) {
     uint8_t* x = ws + need - xdp_region_bytes(bin);
     uint32_t* doffs = (uint32_t*)x;
     uint16_t* dlens = (uint16_t*)(x + align16(bin->n * 4));
@@ -1811,7 +1839,7 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* bin, const ebpf_batch_out* ou
       return EBPF_EHIP;
     }
   }
-  const JitFns* jit = batch_jit(p, b, kind, stk, device);
+  const JitFns* jit = xdp_rb ? &p->jit_fn[device][6] : batch_jit(p, b, kind, stk, device);
   // an xdp_md batch of a loop program runs staged: variant 5, whose range analysis knows the
   // staged images' ctx (data = 8, data_end = LEN)
   if (jit == &p->jit_fn[device][2] && (bin->flags & EBPF_BATCH_XDP_MD) && !xdp_direct &&
@@ -1855,8 +1883,11 @@ int ebpf_batch_kernel(ebpf_prog* p, const ebpf_batch* bin, const ebpf_batch_out*
   bool stk = false;
   const int kind = batch_kind(p, bin, out, device, &stk);
   ebpf_batch staged = *bin;  // xdp_md batches not run in place run as offsets + lens batches
-  if ((bin->flags & EBPF_BATCH_XDP_MD) &&
-      !xdp_in_place(p, bin, out->mem != nullptr, device, kind, stk)) {
+  const bool rb = xdp_rebased(p, bin, out, device, kind, stk);
+  if (rb) {
+    staged = rebased_batch(bin);
+  } else if ((bin->flags & EBPF_BATCH_XDP_MD) &&
+             !xdp_in_place(p, bin, out->mem != nullptr, device, kind, stk)) {
     staged.offsets = (const uint32_t*)16;
     staged.lens = (const uint16_t*)16;
     staged.stride = 0;
@@ -1869,7 +1900,23 @@ int ebpf_batch_kernel(ebpf_prog* p, const ebpf_batch* bin, const ebpf_batch_out*
   a.lens = staged.lens;
   a.stride = staged.stride;
   a.mem_out = out->mem;
-  return launch_kernel_id(kind, a, batch_jit(p, &staged, kind, stk, device), stk);
+  return launch_kernel_id(kind, a, rb ? &p->jit_fn[device][6] : batch_jit(p, &staged, kind, stk, device),
+                          stk);
+}
+
+int ebpf_batch_staged(ebpf_prog* p, const ebpf_batch* bin, const ebpf_batch_out* out, int device) {
+  if (!p || !out || device < 0 || device >= kMaxDevices) return EBPF_EINVAL;
+  int rc = check_batch(bin);
+  if (rc) return rc;
+  rc = ebpf_prog_upload(p, device);
+  if (rc) return rc;
+  if (!(bin->flags & EBPF_BATCH_XDP_MD)) return 0;
+  bool stk = false;
+  const int kind = batch_kind(p, bin, out, device, &stk);
+  return xdp_in_place(p, bin, out->mem != nullptr, device, kind, stk) ||
+                 xdp_rebased(p, bin, out, device, kind, stk)
+             ? 0
+             : 1;
 }
 
 int ebpf_run_batch_multi(ebpf_prog* p, int nshards, const int* devices, const ebpf_batch* batches,

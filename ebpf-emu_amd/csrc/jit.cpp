@@ -298,6 +298,13 @@ struct Compiler {
     }
     return ctx_off[i];
   }
+  // (xdp_ctx) xdp_md in place, rebased (variant 6): the batch runs as the main.rs layout over
+  // the packets themselves -- BASE the packet, LEN = len, mem_size - 8 (host.cpp) -- and every
+  // packet load's offset is 8 lower (t / tx rebased by jit_compile_loop): image byte a (>= 8, the
+  // range analysis proved it for every load) is packet byte a - 8, its bounds a + w <= 8 + len
+  // are a - 8 + w <= len, and mem_size's likewise. The registers keep the image's values: r2 and
+  // the ctx's data_end are 8 + LEN, data 8 (xdp.rs:16-20).
+  bool xdp_rebase = false;
   mutable bool coop_emitted = false;  // a coop_sum entry was emitted (compile_into_template:
                                       // such programs go to the deep kernel, unbinned)
 
@@ -689,7 +696,8 @@ struct Compiler {
     const uint32_t live = live_in() | 1u;
     std::string s = "; registers read before written: " + std::to_string(live) + "\n";
     for (int r = 0; r < 11; r++)
-      if (live & (1u << r)) s += kJitInitReg[r];
+      if (live & (1u << r)) s += r == 2 && xdp_rebase ? std::string("v_add_u32 v4, 8, v31\nv_mov_b32 v5, 0\n")
+                                                      : std::string(kJitInitReg[r]);
     return s;
   }
 
@@ -777,6 +785,27 @@ struct Compiler {
   }
 
   // Every reachable packet load is a one-byte load proven inside the packet (prove_loads).
+  // (xdp_ctx) Whether the program runs rebased (xdp_rebase): its range analysis reaches a fixpoint
+  // and every load it reaches, but the ctx loads, is a register-address load (T_LDX / T_LDX1, the
+  // offset in TUop::imm) whose address is >= 8 on every path -- so it never reads the ctx, which
+  // is not in memory there.
+  bool rebase_ok(const std::vector<TUop>& tx) {
+    prove_loads();
+    if (reached.size() != n) return false;
+    for (uint32_t i = 0; i < n; i++) {
+      if (!reached[i] || uops[i].op != U_LDX || ctx_load(i) >= 0) continue;
+      for (const std::vector<TUop>* tt : {&t, &tx}) {
+        const uint32_t id = (*tt)[i].hoff / TILE_SLOT;
+        if (id != T_LDX_C && id != T_LDX_E && id != T_LDX1_C && id != T_LDX1_E) return false;
+        if ((int64_t)(*tt)[i].imm != (int64_t)(int32_t)uops[i].x) return false;
+      }
+      const AbsVal& b = ranges[i][uops[i].src];
+      const int64_t off = (int64_t)(int32_t)uops[i].x;
+      if (b.hi >= (1ull << 62) || (int64_t)b.lo + off < 8) return false;
+    }
+    return true;
+  }
+
   bool all_loads_proven() {
     prove_loads();
     if (reached.size() != n) return false;
@@ -2938,7 +2967,9 @@ struct Compiler {
       return true;
     }
     if (const int co = ctx_load(i); co >= 0) {  // (xdp_ctx: the staged ctx's data / data_end)
-      main += "v_mov_b32 v" + std::to_string(2 * uops[i].dst) + ", " + (co ? "v31" : "8") + "\n";
+      main += co && xdp_rebase ? "v_add_u32 v" + std::to_string(2 * uops[i].dst) + ", 8, v31\n"
+                               : "v_mov_b32 v" + std::to_string(2 * uops[i].dst) + ", " +
+                                     (co ? "v31" : "8") + "\n";
       return true;
     }
     if (!loops && (m.fixed == "1" || m.stack || m.varl) &&
@@ -3348,6 +3379,11 @@ namespace {
 bool compile_into_template(Compiler& c, Compiler* xc, std::vector<char>& code_object,
                            std::string* err, std::string* asm_out, bool* deep_out = nullptr) {
   std::string tmpl(kJitTemplateAsm);
+  if (c.xdp_rebase) {  // (the all-registers init: r2 = 8 + LEN, the image's length)
+    const std::string from = "v_mov_b32 v4, v31\n", to = "v_add_u32 v4, 8, v31\n";
+    for (size_t q = 0; (q = tmpl.find(from, q)) != std::string::npos; q += to.size())
+      tmpl.replace(q, from.size(), to);
+  }
   // cache policy of the window DMA (the fixed-slot kernel's whole tiles): non-temporal -- every
   // packet byte is read once (MI355X guide, nt-weights: issued -> landed ~18 % shorter). A/B, one
   // box, 1 Mi packets: 5-tuple 16.5 vs 17.3 us, drop-all 13.7 vs 14.7; 8 Mi: 94.5 vs 103.8.
@@ -3448,7 +3484,7 @@ bool jit_compile(const std::vector<Uop>& uops, const std::vector<TUop>& t,
 bool jit_compile_loop(const std::vector<Uop>& uops, const std::vector<TUop>& t,
                       const std::vector<TUop>& tx, std::vector<char>& code_object,
                       std::string* err, std::string* asm_out, const StackPlan* stk,
-                      bool* deep, uint32_t guard_k, bool xdp_ctx) {
+                      bool* deep, uint32_t guard_k, bool xdp_ctx, bool xdp_rebase) {
   if (uops.empty() || uops.size() > kJitMaxUops || t.size() < uops.size() ||
       tx.size() < uops.size() ||
       (stk && (stk->k == 0 || stk->k > kStackMax || stk->k % 4 || stk->off.size() != uops.size() ||
@@ -3456,8 +3492,22 @@ bool jit_compile_loop(const std::vector<Uop>& uops, const std::vector<TUop>& t,
     if (err) *err = "not a tile program";
     return false;
   }
-  Compiler c(uops, t, true, false, stk), xc(uops, tx, true, true, stk);
+  // (xdp_rebase: the tables with every packet load's offset 8 lower, Compiler::xdp_rebase)
+  std::vector<TUop> tr, txr;
+  if (xdp_rebase) {
+    Compiler probe(uops, t, true, false, nullptr);
+    probe.xdp_ctx = true;
+    if (stk || guard_k || !xdp_ctx || !probe.rebase_ok(tx)) {
+      if (err) *err = "xdp_md rebase: a load not proven past the ctx";
+      return false;
+    }
+    tr = t, txr = tx;
+    for (uint32_t i = 0; i < uops.size(); i++)
+      if (probe.reached[i] && uops[i].op == U_LDX && probe.ctx_load(i) < 0) tr[i].imm -= 8, txr[i].imm -= 8;
+  }
+  Compiler c(uops, xdp_rebase ? tr : t, true, false, stk), xc(uops, xdp_rebase ? txr : tx, true, true, stk);
   c.xdp_ctx = xc.xdp_ctx = xdp_ctx;
+  c.xdp_rebase = xc.xdp_rebase = xdp_rebase;
   if (guard_k) {  // a promoted program: its packet loads cannot reach the window of any lane
     if (stk || !c.all_loads_proven()) {  // whose LEN <= r10 - guard_k
       if (err) *err = "promoted program: a load not proven inside the packet";

@@ -35,8 +35,10 @@ struct JitFns {
 // loads resolved), 2 the loop kernel, 3 xdp_md batches (the ctx's data field known, host.cpp
 // fold_const_loads), 4 the stack-slot promoted loop program (host.cpp promote_slots), 5 the loop
 // program for xdp_md batches (staged images: the ctx's data and data_end known to the range
-// analysis, jit.cpp Compiler::xdp_ctx)
-constexpr int kJitVariants = 6;
+// analysis, jit.cpp Compiler::xdp_ctx), 6 the same program for xdp_md batches in place (rebased:
+// the packet loads 8 bytes lower, the batch run as the main.rs layout over the packets,
+// Compiler::xdp_rebase)
+constexpr int kJitVariants = 7;
 constexpr uint32_t kStackMax = 64;    // window bytes
 constexpr uint32_t kStackVgpr = 80;   // first VGPR of the window (ebpf_tile_jit_fixed)
 constexpr int32_t kNoStack = INT32_MIN;
@@ -81,7 +83,7 @@ bool jit_compile_loop(const std::vector<Uop>& uops, const std::vector<TUop>& t,
                       const std::vector<TUop>& tx, std::vector<char>& code_object,
                       std::string* err, std::string* asm_out = nullptr,
                       const StackPlan* stk = nullptr, bool* deep = nullptr, uint32_t guard_k = 0,
-                      bool xdp_ctx = false);
+                      bool xdp_ctx = false, bool xdp_rebase = false);
 
 // Windows the refills of byte-scanning loop programs prefetch ahead: 1 (ebpf_tile_jit_loop, 5
 // waves per SIMD) or 2-3 (ebpf_tile_jit_loop_deep, 4 waves); EBPFEMU_PF_DEPTH overrides.

@@ -47,7 +47,8 @@ EXPORTS = ["ebpf_batch_init", "ebpf_prog_load", "ebpf_prog_load_hex", "ebpf_prog
            "ebpf_prog_len", "ebpf_prog_insn", "ebpf_prog_tier", "ebpf_prog_forward_only",
            "ebpf_prog_stack_window",
            "ebpf_workspace_bytes", "ebpf_prog_compile", "ebpf_prog_jit_asm", "ebpf_debug_trace",
-           "ebpf_prog_upload", "ebpf_run_batch", "ebpf_run_batch_multi", "ebpf_batch_kernel", "ebpf_pcap_index",
+           "ebpf_prog_upload", "ebpf_run_batch", "ebpf_run_batch_multi", "ebpf_batch_kernel", "ebpf_batch_staged",
+           "ebpf_pcap_index",
            "ebpf_strerror", "ebpf_version"]
 
 
@@ -120,6 +121,7 @@ def lib():
     L.ebpf_prog_upload.argtypes = [vp, ctypes.c_int]
     L.ebpf_run_batch.argtypes = [vp, ctypes.POINTER(Batch), ctypes.POINTER(BatchOut), vp]
     L.ebpf_batch_kernel.argtypes = [vp, ctypes.POINTER(Batch), ctypes.POINTER(BatchOut), ctypes.c_int]
+    L.ebpf_batch_staged.argtypes = [vp, ctypes.POINTER(Batch), ctypes.POINTER(BatchOut), ctypes.c_int]
     L.ebpf_run_batch_multi.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
                                        ctypes.POINTER(Batch), ctypes.POINTER(BatchOut),
                                        ctypes.POINTER(vp)]

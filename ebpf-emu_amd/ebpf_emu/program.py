@@ -197,6 +197,16 @@ class Program:
             raise _lib.EbpfError(rc, "ebpf_batch_kernel")
         return rc
 
+    def batch_staged(self, batch: _lib.Batch, out: _lib.BatchOut | None = None,
+                     device: int = 0) -> bool:
+        """Whether ebpf_run_batch stages this xdp_md batch's images before the program's kernel
+        (ebpf_batch_staged); False when it runs in place or is not an xdp_md batch."""
+        o = out if out is not None else _lib.BatchOut()
+        rc = _lib.lib().ebpf_batch_staged(self._h, ctypes.byref(batch), ctypes.byref(o), device)
+        if rc < 0:
+            raise _lib.EbpfError(rc, "ebpf_batch_staged")
+        return rc == 1
+
     def workspace_bytes(self, batch: _lib.Batch, device: int) -> int:
         return int(_lib.lib().ebpf_workspace_bytes(self._h, ctypes.byref(batch), device))
 

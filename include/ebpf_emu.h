@@ -227,6 +227,12 @@ int ebpf_run_batch(ebpf_prog* prog, const ebpf_batch* batch, const ebpf_batch_ou
 int ebpf_batch_kernel(ebpf_prog* prog, const ebpf_batch* batch, const ebpf_batch_out* out,
                       int device);
 
+/* Whether ebpf_run_batch stages this EBPF_BATCH_XDP_MD batch's images (one copy kernel writing
+ * [ctx][packet] per packet into the workspace before the program's kernel, xdp.rs:16-20) on
+ * `device`: 1 staged, 0 in place (or not an xdp_md batch), < 0 = EBPF_E*. */
+int ebpf_batch_staged(ebpf_prog* prog, const ebpf_batch* batch, const ebpf_batch_out* out,
+                      int device);
+
 /* Multi-GPU: shard s runs on devices[s] / streams[s] (distinct devices); the shards' counters are
  * summed with one RCCL all-reduce over xGMI, and the global totals of this call are ADDED to
  * every outs[s].counters (accumulated as in ebpf_run_batch, never overwritten; the per-shard sums

@@ -302,26 +302,97 @@ def test_xdp_md_var_in_place(cuda, oracle_mod, layout):
         prog.close()
 
 
-def test_xdp_md_loop_programs_staged(cuda):
-    """Loop programs still run the staged images (their window refills read packet bytes by
-    image address): the route is the compiled loop kernel."""
+# the sum in words, halves and bytes (loads of every width, none at a fixed window position)
+XDP_SUM_WIDE = """
+    ldxw r2, [r1+0]
+    ldxw r3, [r1+4]
+    mov r0, 0
+    mov r4, r2
+    add r4, 4
+loop4:
+    jgt r4, r3, tail
+    ldxw r5, [r4-4]
+    add r0, r5
+    ldxh r6, [r4-2]
+    xor r0, r6
+    add r4, 4
+    add r2, 4
+    ja loop4
+tail:
+    jge r2, r3, done
+    ldxb r5, [r2+0]
+    add r0, r5
+    add r2, 1
+    ja tail
+done:
+    exit
+"""
+
+
+@pytest.mark.parametrize("layout", [dict(), dict(offsets_layout=True, align=16),
+                                    dict(offsets_layout=True, misalign=3)])
+def test_xdp_md_loop_programs_in_place(cuda, oracle_mod, layout):
+    """Loop programs whose every packet load is proven past the ctx run the xdp_md batch in place
+    (no staging kernel): variant 6, the program rebased -- packet loads 8 bytes lower, the batch
+    run as the main.rs layout over the packets with mem_size - 8, r2 and the ctx's data_end 8 + LEN
+    (jit.cpp Compiler::xdp_rebase). Status, r0, every register, verdicts and counters against the
+    oracle on the ctx-prefixed images (xdp.rs:16-20), short packets, ST_BADPKT and a step budget
+    that binds (the exact copy) included. A program with a load that may read the ctx, and a batch
+    asking for the final images, stay staged."""
     import torch
 
     from ebpf_emu import Program, _lib
+    from ebpf_emu import workloads as W
     from ebpf_emu.asm import assemble
 
-    prog = Program(assemble(XDP_SUM))
-    frames, kw = _stage([bytes(100)] * 70, cuda)
-    assert _route(prog, frames, kw) == _lib.EBPF_KERNEL_JIT_LOOP
+    rng = random.Random(29)
+    pkts = _xdp_packets(rng, 400)
+    frames, kw = _stage(pkts, cuda, **layout)
+    for src in (XDP_SUM, XDP_SUM_RELOAD, XDP_SUM_WIDE, W.CHECKSUM_XDP):
+        img = assemble(src) if isinstance(src, str) else src
+        prog = Program(img)
+        assert prog.compile()
+        b = prog.make_batch(frames, xdp_md=True, **kw)
+        assert prog.batch_kernel(b) == _lib.EBPF_KERNEL_JIT_LOOP
+        assert not prog.batch_staged(b), src
+        op = oracle_mod.Program(img)
+        for steps in (1 << 22, 50):
+            cnt = torch.zeros(8, dtype=torch.int64, device=cuda)
+            res = prog.run(frames, r0=True, status=True, regs=True, counters=cnt, xdp_md=True,
+                           max_steps=steps, **kw)
+            torch.cuda.synchronize()
+            status = res.status.cpu().numpy()
+            regs = res.regs.cpu().numpy().view(np.uint64)
+            verdict = res.verdict.cpu().numpy()
+            want = np.zeros(8, dtype=np.uint64)
+            for i, im in enumerate(_images(pkts)):
+                st, oregs, _, nst = op.run_full(im, 1024, 512, steps)
+                want[7] += nst
+                assert status[i] == st, (i, len(pkts[i]), steps)
+                if st == 0:
+                    assert [int(x) for x in regs[i]] == oregs, (i, steps)
+                    assert verdict[i] == (oregs[0] if oregs[0] < 5 else 0xFE)
+                    want[oregs[0] if oregs[0] < 5 else 5] += 1
+                else:
+                    assert verdict[i] == 0xFF
+                    want[6] += 1
+            assert list(cnt.cpu().numpy().view(np.uint64)) == list(want), steps
+            assert (status == 7).sum() == sum(len(p) + 8 > 1024 for p in pkts)
+            if steps == 50:
+                assert (status == 5).sum() > 0  # (ST_STEPS: the budget bound)
+        # final images: the staged images (they hold the ctx)
+        o = _lib.BatchOut()
+        o.mem = 16
+        assert prog.batch_staged(b, o)
+        prog.close()
+    prog = Program(assemble(XDP_R1_MOVED))  # (ldxw r6, [r1+4] may read the ctx's data_end)
+    assert prog.compile() and prog.batch_staged(prog.make_batch(frames, xdp_md=True, **kw))
     prog.close()
-    del torch
-
 
 
 def test_xdp_md_checksum_loop_full_size(cuda):
     """The per-byte checksum as a standard XDP program (workloads.CHECKSUM_XDP: the sum over
-    ctx->data .. ctx->data_end, a loop program: its batch staged by xdp_stage for the compiled
-    loop kernels) over a 256 Ki slice of config 5's mixed 64/1500-byte frames with 2048-byte
+    ctx->data .. ctx->data_end, a loop program run in place, rebased) over a 256 Ki slice of config 5's mixed 64/1500-byte frames with 2048-byte
     images: the same verdicts and verdict counters as the plain checksum (CHECKSUM, main.rs
     layout) on the same packets, which test_workload_golden_full_size pins to the oracle."""
     import torch
@@ -337,6 +408,8 @@ def test_xdp_md_checksum_loop_full_size(cuda):
     out = {}
     for name, xdp in (("checksum", False), ("checksum_xdp", True)):
         prog = Program(W.program(name))
+        if xdp:
+            assert not prog.batch_staged(prog.make_batch(frames, xdp_md=True, **kw))
         cnt = torch.zeros(8, dtype=torch.int64, device=cuda)
         res = prog.run(frames, counters=cnt, xdp_md=xdp, **kw)
         torch.cuda.synchronize()

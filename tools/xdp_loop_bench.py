@@ -1,10 +1,10 @@
 #!/usr/bin/env python3
 """Per-batch time of an xdp_md loop program (diagnostic, not the driver's bench): the per-byte
 checksum as a standard XDP program (workloads.CHECKSUM_XDP) vs the plain checksum (CHECKSUM) on
-the same 1 Mi mixed 64/1500-byte batch (config 5's frames, offsets + lens). The difference is the
-xdp_md staging pass (interp.hip xdp_stage) the loop kernels still need. HIP events around K
-back-to-back batches on one stream.
-  python tools/xdp_loop_bench.py [--packets N] [--steps K]
+the same 1 Mi mixed 64/1500-byte batch (config 5's frames, offsets + lens): in place (variant 6,
+the program rebased, jit.cpp Compiler::xdp_rebase), or staged with EBPFEMU_XDP_STAGE=1 (the
+xdp_stage copy, then variant 5). HIP events around K back-to-back batches on one stream.
+  [EBPFEMU_XDP_STAGE=1] python tools/xdp_loop_bench.py [--packets N] [--steps K]
 """
 import argparse
 import json
@@ -53,9 +53,10 @@ def main():
         torch.cuda.synchronize()
         res[name] = {"us_per_batch": round(e0.elapsed_time(e1) * 1e3 / args.steps, 2),
                      "kernel": _lib.KERNEL_NAMES[prog.batch_kernel(desc, out)],
+                     "staged": prog.batch_staged(desc, out),
                      "verdict_crc": int(np.bitwise_xor.reduce(verdict.cpu().numpy().astype(np.uint64)))}
         prog.close()
-    res["xdp_staging_us"] = round(res["checksum_xdp"]["us_per_batch"] - res["checksum"]["us_per_batch"], 2)
+    res["xdp_minus_plain_us"] = round(res["checksum_xdp"]["us_per_batch"] - res["checksum"]["us_per_batch"], 2)
     print(json.dumps(res))
 
 
