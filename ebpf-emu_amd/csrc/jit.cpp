@@ -562,6 +562,10 @@ struct Compiler {
     // program's non-negative constants and their neighbours, LEN's bound, then no bound), so a
     // counter compared against a constant keeps that bound; a finite ladder, so it terminates
     std::vector<uint64_t> ladder{kLenMax, ~0ull};
+    // (xdp_ctx: also INT64_MAX, so a pointer stepping by more than one byte under a signed
+    // compare with data_end can settle non-negative -- the compare then bounds it below LEN -- and
+    // keep its lower bound past the ctx, which a bound of 2^64 - 1 loses to the add's wrap)
+    if (xdp_ctx) ladder.push_back((uint64_t)INT64_MAX);
     for (const Uop& u : uops)
       if (!(u.aux & F_SRC) && u.k >= 0 && (uint64_t)u.k < (1ull << 62))
         for (int64_t d = -1; d <= 1; d++)
@@ -799,9 +803,11 @@ struct Compiler {
         if (id != T_LDX_C && id != T_LDX_E && id != T_LDX1_C && id != T_LDX1_E) return false;
         if ((int64_t)(*tt)[i].imm != (int64_t)(int32_t)uops[i].x) return false;
       }
+      // a = r + off >= 8 on every path: r >= 8 - off, and r + off does not wrap
       const AbsVal& b = ranges[i][uops[i].src];
       const int64_t off = (int64_t)(int32_t)uops[i].x;
-      if (b.hi >= (1ull << 62) || (int64_t)b.lo + off < 8) return false;
+      if (b.lo >= (1ull << 62) || (int64_t)b.lo + off < 8 || (off > 0 && b.hi > ~0ull - (uint64_t)off))
+        return false;
     }
     return true;
   }

@@ -60,6 +60,33 @@ def test_workloads_compile():
         if name in ("checksum", "checksum_stack"):
             with pytest.raises(Exception):
                 p.jit_asm(1)
+        if name == "checksum_xdp":  # the xdp_md copies: the ctx known (5), rebased in place (6)
+            assert "v_add_u32 v4, 8, v31" not in p.jit_asm(5)
+            assert "v_add_u32 v4, 8, v31" in p.jit_asm(6)
+        p.close()
+
+
+def test_xdp_loop_rebase_eligibility():
+    """Variant 6 (xdp_md loop programs in place, jit.cpp Compiler::xdp_rebase) is compiled only
+    when the range analysis proves every packet load past the ctx: the byte sum, the bound
+    reloaded from the ctx, word + half loads behind a pointer compared with data_end; not a
+    program whose ctx-shaped load may read the ctx, nor a load at a fixed offset below 8."""
+    import test_gpu_xdp_md as X
+    from ebpf_emu import Program
+    from ebpf_emu.asm import assemble
+
+    for src, rebased in ((X.XDP_SUM, True), (X.XDP_SUM_RELOAD, True), (X.XDP_SUM_WIDE, True),
+                         (X.XDP_R1_MOVED, False),
+                         (X.XDP_SUM.replace("mov r0, 0", "ldxb r0, [r1+2]"), False)):
+        p = Program(assemble(src))
+        assert p.compile()
+        p.jit_asm(5)
+        if rebased:
+            text = p.jit_asm(6)
+            assert "v_add_u32 v4, 8, v31" in text  # (r2 = 8 + LEN)
+        else:
+            with pytest.raises(Exception):
+                p.jit_asm(6)
         p.close()
 
 

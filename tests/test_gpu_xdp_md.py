@@ -316,14 +316,16 @@ loop4:
     ldxh r6, [r4-2]
     xor r0, r6
     add r4, 4
-    add r2, 4
     ja loop4
 tail:
+    mov r2, r4
+    sub r2, 4
+loop1:
     jge r2, r3, done
     ldxb r5, [r2+0]
     add r0, r5
     add r2, 1
-    ja tail
+    ja loop1
 done:
     exit
 """
