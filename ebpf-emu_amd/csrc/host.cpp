@@ -1455,14 +1455,16 @@ int ebpf_prog_upload(ebpf_prog* p, int device) {
 
 // Whether a loop-mode batch runs in length-binned order (an xdp_md batch is staged as offsets +
 // lens).
-static bool use_binning(const ebpf_prog* p, const ebpf_batch* b, bool promo = false) {
+// deep: the loop program that runs is compiled into the deep kernel (its variant's *jit_deep flag;
+// false sizes the workspace for any variant)
+static bool use_binning(const ebpf_prog* p, const ebpf_batch* b, bool deep = false) {
   const bool ol = (b->offsets && b->lens) || (b->flags & EBPF_BATCH_XDP_MD);
   if (p->ltuops.empty() || !ol || (b->flags & EBPF_BATCH_GENERIC) || b->init_fp_len) return false;
   // (a program on the deep loop kernel -- its long byte sums cooperative, coop_sum_compact -- runs
   // in batch order: a tile's short packets need no binning away from its long ones, and spreading
   // the long packets over every tile balances the waves; config 5, A/B on one box: 169.7 us
   // unbinned vs 191.3 binned per 1 Mi batch)
-  if ((promo ? p->pjit_deep : p->jit_deep) && g_bin < 0) return false;
+  if (deep && g_bin < 0) return false;
   return g_bin >= 0 ? g_bin == 1 : b->n >= kBinMinPackets;
 }
 
@@ -1667,7 +1669,7 @@ uint64_t ebpf_workspace_bytes(const ebpf_prog* p, const ebpf_batch* b, int devic
   uint64_t bytes = kWsSlotsOff + x;
   // the binned packet order, then the per-workgroup class counts (either loop program of a
   // promoted stack program may run)
-  if (use_binning(p, b) || (!p->puops.empty() && use_binning(p, b, true)))
+  if (use_binning(p, b))
     bytes += align16(b->n * 4 + 4ull * kBinMaxWgs * kBinClasses);
   bytes += align16(tier1_slots_bytes(p, b, device));
   if (p->stack.any_dyn || !p->puops.empty())  // the deopt list's indices (past the slots)
@@ -1830,7 +1832,18 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* bin, const ebpf_batch_out* ou
     if (cur != device) hipSetDevice(cur);
     return EBPF_EHIP;
   }
-  if (kind == kKindLoop && use_binning(p, b, promo)) {
+  // the compiled variant that runs: variant 4 for the promoted program, 6 for an xdp_md batch in
+  // place (rebased), 5 for a staged one (its range analysis knows the staged images' ctx)
+  const JitFns* jit = xdp_rb ? &p->jit_fn[device][6] : batch_jit(p, b, kind, stk, device);
+  if (jit == &p->jit_fn[device][2] && (bin->flags & EBPF_BATCH_XDP_MD) && !xdp_direct &&
+      p->jit_mod[device][5])
+    jit = &p->jit_fn[device][5];
+  const bool deep = jit == &p->jit_fn[device][2]   ? p->jit_deep
+                    : jit == &p->jit_fn[device][4] ? p->pjit_deep
+                    : jit == &p->jit_fn[device][5] ? p->xjit_deep
+                    : jit == &p->jit_fn[device][6] ? p->rjit_deep
+                                                   : false;
+  if (kind == kKindLoop && use_binning(p, b, deep)) {
     a.perm = (const uint32_t*)(ws + kWsSlotsOff);
     a.bin_counts = (uint32_t*)(ws + kWsBinCountsOff);
     if (launch_binning(b->lens, b->n, (uint32_t*)a.perm + b->n, (uint32_t*)a.perm, s) !=
@@ -1839,12 +1852,6 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* bin, const ebpf_batch_out* ou
       return EBPF_EHIP;
     }
   }
-  const JitFns* jit = xdp_rb ? &p->jit_fn[device][6] : batch_jit(p, b, kind, stk, device);
-  // an xdp_md batch of a loop program runs staged: variant 5, whose range analysis knows the
-  // staged images' ctx (data = 8, data_end = LEN)
-  if (jit == &p->jit_fn[device][2] && (bin->flags & EBPF_BATCH_XDP_MD) && !xdp_direct &&
-      p->jit_mod[device][5])
-    jit = &p->jit_fn[device][5];
   // store mode (register-address packet stores, StackPlan::any_dyn): lanes the compiled kernel
   // cannot finish are listed, then re-run from the start by the general interpreter (tier 1)
   // (the promoted program: lanes whose packet reaches the slots, jit.cpp promo_guard)

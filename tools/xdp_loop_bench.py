@@ -4,7 +4,7 @@ checksum as a standard XDP program (workloads.CHECKSUM_XDP) vs the plain checksu
 the same 1 Mi mixed 64/1500-byte batch (config 5's frames, offsets + lens): in place (variant 6,
 the program rebased, jit.cpp Compiler::xdp_rebase), or staged with EBPFEMU_XDP_STAGE=1 (the
 xdp_stage copy, then variant 5). HIP events around K back-to-back batches on one stream.
-  [EBPFEMU_XDP_STAGE=1] python tools/xdp_loop_bench.py [--packets N] [--steps K]
+  python tools/xdp_loop_bench.py [--packets N] [--steps K] [--stage]
 """
 import argparse
 import json
@@ -16,6 +16,8 @@ sys.path.insert(0, os.path.join(ROOT, "ebpf-emu_amd"))
 
 
 def main():
+    if "--stage" in sys.argv:  # (read by the library when it loads)
+        os.environ["EBPFEMU_XDP_STAGE"] = "1"
     import numpy as np
     import torch
 
@@ -25,6 +27,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--packets", type=int, default=1 << 20)
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--stage", action="store_true", help="stage every xdp_md batch (A/B)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     n = args.packets
