@@ -418,6 +418,14 @@ static const bool g_no_dag = [] {
   return e && e[0] == '1';
 }();
 
+// EBPFEMU_XDP_STAGE=1 (A/B): every xdp_md batch goes through xdp_stage (xdp_in_place). (Outside the
+// extern "C" block below: a lambda initializer there was given the same closure as g_trace's by
+// the host compiler, so the flag read EBPFEMU_TRACE.)
+static const bool g_xdp_stage = [] {
+  const char* e = getenv("EBPFEMU_XDP_STAGE");
+  return e && e[0] == '1';
+}();
+
 // Width mask of an access of w bytes.
 static uint64_t width_mask(uint32_t w) { return w >= 8 ? ~0ull : ((1ull << (8 * w)) - 1); }
 
@@ -1598,11 +1606,8 @@ static uint32_t kind_uops(const ebpf_prog* p, int kind) {
 // The xdp_md convention in place (no staging copy): the compiled forward kernels and the tile
 // interpreter on the general layouts synthesise each packet's ctx in its window (interp.hip
 // xdp_window, jit.cpp xdp_shift) and read the packet 8 bytes further on; every other kernel runs
-// the images xdp_stage writes into the workspace. EBPFEMU_XDP_STAGE=1 stages always (A/B runs).
-static const bool g_xdp_stage = [] {
-  const char* e = getenv("EBPFEMU_XDP_STAGE");
-  return e && e[0] == '1';
-}();
+// the images xdp_stage writes into the workspace. EBPFEMU_XDP_STAGE=1 stages always (A/B runs:
+// g_xdp_stage, defined outside this extern "C" block).
 
 static bool xdp_in_place(ebpf_prog* p, const ebpf_batch* b, bool mem_out, int device, int kind,
                          bool stk) {

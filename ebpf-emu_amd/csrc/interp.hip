@@ -460,6 +460,10 @@ __device__ __forceinline__ void flush_counters(const LaunchArgs& a, const uint64
   const uint32_t g = blockIdx.x % kCounterShards;
   if (lane >= 8) return;
   const uint64_t sum = w->acc[lane];
+  if (a.fold_kernel == 2) {  // (A/B) no shards: a non-returning add to the caller's counter
+    if (sum) __hip_atomic_fetch_add(&a.counters[lane], sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
   uint64_t* word = &a.shards[g * 8 + lane];
   if (a.fold_kernel) {  // fold_counters runs next on the stream
     if (sum) __hip_atomic_fetch_add(word, sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2119,7 +2123,7 @@ hipError_t launch_counters_add(const uint64_t* src, uint64_t* dst, hipStream_t s
 // (EBPFEMU_FOLD=kernel for A/B runs, and launches whose per-shard sums could reach 2^48).
 static int g_fold_mode = [] {
   const char* e = getenv("EBPFEMU_FOLD");
-  return !e ? -1 : e[0] == 'i' ? 0 : 1;
+  return !e ? -1 : e[0] == 'i' ? 0 : e[0] == 'd' ? 2 : 1;
 }();
 // A/B: EBPFEMU_FIXED=0 disables the fixed-slot variants
 static bool g_fixed = [] {
@@ -2395,6 +2399,7 @@ hipError_t launch_interp(int kind, const LaunchArgs& a, int grid, hipStream_t st
                     members < (1ull << (64 - kShardCountShift));
   const bool fold_kernel = g_fold_mode >= 0 ? (g_fold_mode == 1 || !fits) : !fits;
   b.fold_kernel = fold_kernel ? 1u : 0u;
+  if (g_fold_mode == 2) b.fold_kernel = 2u;  // (A/B: EBPFEMU_FOLD=d, straight to the counters)
   void* bargs[] = {(void*)&b};
   hipError_t e;
   if (jit && jit->loop && kind == kKindLoop) {  // the compiled loop program
