@@ -1362,14 +1362,30 @@ hipError_t launch_binning(const uint16_t* lens, uint64_t n, uint32_t* wgc, uint3
 // [packet bytes] -- the bytes main.rs would be handed for a standard XDP program. One workgroup
 // stages 256 packets: it sizes their 16-byte aligned slots, reserves its range with one device
 // atomic (workgroups pack in arrival order; every packet keeps its index through the offsets),
-// then copies packet by packet with all 256 threads (coalesced bytes). An image longer than
-// mem_size is not copied: its length alone makes the batch fault it ST_BADPKT (main.rs:20-21).
+// then copies them: images of at most kStageShort bytes one per thread, longer ones one per wave
+// (its lanes on consecutive 16-byte chunks). An image longer than mem_size is not copied: its
+// length alone makes the batch fault it ST_BADPKT (main.rs:20-21).
+constexpr uint32_t kStageShort = 256;
+
+// Image chunk c (16 bytes at image offset 16c) of a packet of len bytes at src: the ctx {data =
+// 8, data_end = 8 + len} in its first 8 bytes, then packet bytes (pkt_read: aligned dwords that
+// hold a packet byte, never past one; zeros at or past len).
+__device__ __forceinline__ uint4 xdp_image_chunk(const uint8_t* src, uint32_t len, uint32_t c) {
+  uint32_t w[4];
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const uint32_t b = 16 * c + 4 * q;
+    w[q] = b == 0 ? 8u : b == 4 ? 8u + len : b - 8 < len ? (uint32_t)pkt_read(src, b - 8, 4, len) : 0u;
+  }
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
 // ============================================================================================
 __global__ __launch_bounds__(256) void xdp_stage(const uint8_t* frames, const uint32_t* offsets,
                                                  const uint16_t* lens, uint64_t stride, uint64_t n,
                                                  uint32_t mem_size, uint8_t* dst, uint32_t* doffs,
                                                  uint16_t* dlens, unsigned long long* cursor) {
-  __shared__ uint32_t pre[256];
+  __shared__ uint32_t pre[256], copy_s[256];
   __shared__ const uint8_t* src_s[256];
   __shared__ unsigned long long base;
   const uint32_t t = threadIdx.x;
@@ -1382,6 +1398,7 @@ __global__ __launch_bounds__(256) void xdp_stage(const uint8_t* frames, const ui
     src_s[t] = frames + (offsets ? (uint64_t)offsets[i] : i * stride);
   }
   pre[t] = slot;
+  copy_s[t] = copy;
   __syncthreads();
   for (uint32_t d = 1; d < 256; d <<= 1) {  // inclusive scan of the slot sizes
     const uint32_t v = t >= d ? pre[t - d] : 0u;
@@ -1396,25 +1413,21 @@ __global__ __launch_bounds__(256) void xdp_stage(const uint8_t* frames, const ui
     doffs[i] = (uint32_t)(base + excl);
     dlens[i] = (uint16_t)(len + 8 < 0xFFFF ? len + 8 : 0xFFFF);
   }
-  // each thread writes its own packet's image, 16 bytes at a time into the 16-byte aligned slot:
-  // image dword b = the ctx (b < 8) or packet bytes [b - 8, b - 4) read by pkt_read (aligned
-  // dwords that hold a packet byte, never past one; zeros at or past len). (The round-3 form
-  // copied byte by byte, a block's 256 packets one after another: 225 us for a 1 Mi batch of
-  // 64-byte frames.)
-  if (i < n && copy) {
+  // short images: each thread its own packet's, 16 bytes at a time into the 16-byte aligned slot
+  // (the round-3 form copied byte by byte, a block's 256 packets one after another: 225 us for a
+  // 1 Mi batch of 64-byte frames); long ones: one wave per packet, lane l on chunks l, l + 64, ...
+  // (a thread per 1500-byte packet strides 1.5 KB between lanes: 2.5 ms for config 5's batch)
+  if (i < n && copy && copy <= kStageShort) {
     uint8_t* const o = dst + base + excl;
-    const uint8_t* const src = src_s[t];
-    const uint32_t data_end = 8 + len;
-    for (uint32_t c = 0; c < copy; c += 16) {
-      uint32_t w[4];
-#pragma unroll
-      for (int q = 0; q < 4; q++) {
-        const uint32_t b = c + 4 * q;
-        w[q] = b == 0 ? 8u : b == 4 ? data_end
-               : b - 8 < len ? (uint32_t)pkt_read(src, b - 8, 4, len) : 0u;
-      }
-      *(uint4*)(o + c) = make_uint4(w[0], w[1], w[2], w[3]);
-    }
+    for (uint32_t c = 0; c < copy; c += 16) *(uint4*)(o + c) = xdp_image_chunk(src_s[t], len, c / 16);
+  }
+  __syncthreads();  // (pre[] holds the inclusive offsets, copy_s[] the image lengths)
+  const uint32_t wv = t / kWave, ln = t % kWave;
+  for (uint32_t j = wv; j < 256; j += 256 / kWave) {
+    const uint32_t cj = copy_s[j];
+    if (cj <= kStageShort) continue;  // (wave-uniform)
+    uint8_t* const o = dst + base + pre[j] - ((cj + 15u) & ~15u);
+    for (uint32_t c = ln; 16 * c < cj; c += kWave) *(uint4*)(o + 16 * c) = xdp_image_chunk(src_s[j], cj - 8, c);
   }
 }
 
