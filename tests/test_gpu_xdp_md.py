@@ -420,3 +420,65 @@ def test_xdp_md_checksum_loop_full_size(cuda):
     assert np.array_equal(out["checksum"][0], out["checksum_xdp"][0])
     assert list(out["checksum"][1][:7]) == list(out["checksum_xdp"][1][:7])
     assert (out["checksum"][0] == 1).sum() > 1000 and (out["checksum"][0] == 2).sum() > 1000
+
+
+def _xdp_loop_program(rng):
+    """A random xdp_md loop over data .. data_end: the pointer itself compared with data_end
+    (shape A) or an end pointer r4 = p + K (shape B); loads of every width at offsets inside the
+    step's span; r0 mixed with xor / add / shifts; data_end optionally reloaded from the ctx."""
+    w, suffix = rng.choice([(1, "b"), (2, "h"), (4, "w"), (8, "dw")])
+    reload = rng.random() < 0.3
+    mix = rng.choice(["xor r0, r5", "add r0, r5", "lsh r0, 1\n    xor r0, r5", "add r0, r5\n    rsh r0, 3"])
+    lines = ["ldxw r2, [r1+0]", "ldxw r3, [r1+4]", f"mov r0, {rng.randrange(256)}"]
+    if rng.random() < 0.5:
+        step = rng.randrange(1, 9)
+        off = rng.randrange(0, 8)
+        lines += ["loop:"] + (["ldxw r3, [r1+4]"] if reload else []) + [
+            "jge r2, r3, done", f"ldx{suffix} r5, [r2+{off}]", mix, f"add r2, {step}", "ja loop"]
+    else:
+        K = rng.randrange(w, 17)
+        step = rng.randrange(1, K + 1)
+        off = rng.randrange(0, K - w + 1)
+        lines += ["mov r4, r2", f"add r4, {K}", "loop:"] + (["ldxw r3, [r1+4]"] if reload else []) + [
+            "jgt r4, r3, done", f"ldx{suffix} r5, [r4-{K - off}]", mix, f"add r4, {step}", "ja loop"]
+    lines += ["done:", "exit"]
+    return "\n".join("    " + ln if not ln.endswith(":") else ln for ln in lines) + "\n"
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_xdp_md_loop_fuzz_in_place(cuda, oracle_mod, seed):
+    """Random xdp_md loop programs (_xdp_loop_program) on an offsets + lens batch of short and
+    long packets: run in place (rebased) where the range analysis proves every load past the ctx,
+    else staged; either way status, r0 and every register against the oracle on the ctx-prefixed
+    images (xdp.rs:16-20), with a budget that binds on the long packets too. Most programs must
+    run in place."""
+    import torch
+
+    from ebpf_emu import Program
+    from ebpf_emu.asm import assemble
+
+    rng = random.Random(1000 + seed)
+    pkts = _xdp_packets(rng, 200)
+    frames, kw = _stage(pkts, cuda, offsets_layout=True, align=16 if seed != 2 else 1,
+                        misalign=0 if seed != 2 else 5)
+    in_place = 0
+    for k in range(10):
+        src = _xdp_loop_program(rng)
+        img = assemble(src)
+        prog = Program(img)
+        assert prog.compile(), src
+        in_place += not prog.batch_staged(prog.make_batch(frames, xdp_md=True, **kw))
+        op = oracle_mod.Program(img)
+        for steps in (1 << 22, 300):
+            res = prog.run(frames, r0=True, status=True, regs=True, xdp_md=True, max_steps=steps,
+                           **kw)
+            torch.cuda.synchronize()
+            status = res.status.cpu().numpy()
+            regs = res.regs.cpu().numpy().view(np.uint64)
+            for i, im in enumerate(_images(pkts)):
+                st, oregs, _, _ = op.run_full(im, 1024, 512, steps)
+                assert status[i] == st, (src, i, len(pkts[i]), steps)
+                if st == 0:
+                    assert [int(x) for x in regs[i]] == oregs, (src, i, steps)
+        prog.close()
+    assert in_place >= 6, in_place
