@@ -464,7 +464,7 @@ __device__ __forceinline__ void flush_counters(const LaunchArgs& a, const uint64
     if (sum) __hip_atomic_fetch_add(&a.counters[lane], sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
   }
-  uint64_t* word = &a.shards[(g * 8 + lane) * a.shard_stride];
+  uint64_t* word = &a.shards[g * 8 + lane];
   if (a.fold_kernel) {  // fold_counters runs next on the stream
     if (sum) __hip_atomic_fetch_add(word, sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
@@ -2108,11 +2108,10 @@ extern "C" __global__ __launch_bounds__(kBlock, 4) void ebpf_tile_jit_loop_stack
 // Folds the shards into the caller's counters (EBPFEMU_FOLD=kernel A/B mode): one workgroup,
 // launched after the interpreter on the same stream.
 __global__ __launch_bounds__(kCounterShards * 8) void fold_counters(uint64_t* shards,
-                                                                     uint64_t* counters,
-                                                                     uint32_t stride) {
+                                                                     uint64_t* counters) {
   __shared__ uint64_t fold[kCounterShards * 8];
-  fold[threadIdx.x] = __hip_atomic_exchange(&shards[threadIdx.x * stride], 0ull, __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_AGENT);
+  fold[threadIdx.x] =
+      __hip_atomic_exchange(&shards[threadIdx.x], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   if (threadIdx.x < 8) {
     uint64_t t = 0;
@@ -2138,12 +2137,6 @@ hipError_t launch_counters_add(const uint64_t* src, uint64_t* dst, hipStream_t s
 static int g_fold_mode = [] {
   const char* e = getenv("EBPFEMU_FOLD");
   return !e ? -1 : e[0] == 'i' ? 0 : e[0] == 'd' ? 2 : 1;
-}();
-// EBPFEMU_SHARD_STRIDE (A/B): u64 words between counter shard words, 1 .. kShardStrideMax
-static uint32_t g_shard_stride = [] {
-  const char* e = getenv("EBPFEMU_SHARD_STRIDE");
-  const int v = e ? atoi(e) : 1;
-  return (uint32_t)(v < 1 ? 1 : v > (int)kShardStrideMax ? (int)kShardStrideMax : v);
 }();
 // A/B: EBPFEMU_FIXED=0 disables the fixed-slot variants
 static bool g_fixed = [] {
@@ -2420,7 +2413,6 @@ hipError_t launch_interp(int kind, const LaunchArgs& a, int grid, hipStream_t st
   const bool fold_kernel = g_fold_mode >= 0 ? (g_fold_mode == 1 || !fits) : !fits;
   b.fold_kernel = fold_kernel ? 1u : 0u;
   if (g_fold_mode == 2) b.fold_kernel = 2u;  // (A/B: EBPFEMU_FOLD=d, straight to the counters)
-  b.shard_stride = g_shard_stride;
   void* bargs[] = {(void*)&b};
   hipError_t e;
   if (jit && jit->loop && kind == kKindLoop) {  // the compiled loop program
@@ -2445,8 +2437,7 @@ hipError_t launch_interp(int kind, const LaunchArgs& a, int grid, hipStream_t st
   if (e != hipSuccess || a.counters == nullptr || !fold_kernel) return e;
   uint64_t* shards = a.shards;
   uint64_t* counters = a.counters;
-  uint32_t stride = g_shard_stride;
-  void* fargs[] = {(void*)&shards, (void*)&counters, (void*)&stride};
+  void* fargs[] = {(void*)&shards, (void*)&counters};
   return hipLaunchKernel((const void*)fold_counters, dim3(1), dim3(kCounterShards * 8), fargs, 0,
                          stream);
 }

@@ -32,8 +32,7 @@ constexpr uint64_t kWsDeoptOff = 0;  // u32 count, done: the deopt list (LaunchA
 constexpr uint64_t kWsXdpCursorOff = 320;  // u64: bytes staged by xdp_stage (reset per batch)
 constexpr uint64_t kWsMultiOff = 256;  // u64[8]: ebpf_run_batch_multi's per-shard counter sums
 constexpr uint64_t kWsShardsOff = 512;
-constexpr uint64_t kShardStrideMax = 16;  // (128-byte lines)
-constexpr uint64_t kWsSlotsOff = kWsShardsOff + kCounterShards * 8 * 8 * kShardStrideMax;
+constexpr uint64_t kWsSlotsOff = kWsShardsOff + kCounterShards * 8 * 8;
 
 // Kernel kinds: the two memory tiers of interp_kernel, and dag_kernel (tier-0 programs whose
 // jumps all go forward, run with max_steps >= n_uops so no step budget can bind).
@@ -66,8 +65,6 @@ struct LaunchArgs {
   uint64_t* regs_out;         // optional [n][11] final registers
   uint32_t fold_kernel;       // 1: shards are folded by fold_counters after the launch, 0:
                               //    in-kernel (counted shard words, flush_counters)
-  uint32_t shard_stride;      // u64 words between consecutive shard words (1, or up to
-                              // kShardStrideMax: each word on a cache line of its own)
   const uint32_t* perm;       // loop mode: packet index of tile slot i (length-binned), else null
   uint32_t* bin_counts;       // with perm: bin counts + cursors, zeroed again by the tile kernel
   uint64_t* trace;            // diagnostics (EBPFEMU_TRACE=1): per-wave s_memrealtime stamps of
