@@ -204,6 +204,8 @@ def stub_rank(args, world, rank):
     dist.init_process_group("gloo")
     prog_name = PROGRAM_OF.get(args.config, args.config)
     mixed = args.config in ("checksum", "checksum_stack", "checksum_xdp")
+    if args.total_packets:
+        return stub_rank_strong(args, world, rank)
     with open(PIN_FIXTURE) as f:
         cc = json.load(f)["programs"][prog_name]["chunk_counters"]
     # (the pool size bench's loop below reaches for 1 Mi packets per batch)
@@ -227,6 +229,47 @@ def stub_rank(args, world, rank):
                           "unit": "Mpkt/s", "n_gpus": world, "steps": args.steps,
                           "counters": {"drop": cnt[1], "pass": cnt[2], "insns_retired": cnt[7]},
                           "parity_pinned": src, "stub": True}), flush=True)
+    dist.destroy_process_group()
+
+
+def stub_rank_strong(args, world, rank):
+    """The stub for --total-packets (BASELINE config 4, strong scaling): rank r takes the counters
+    of its contiguous shard of the global batch's seeded chunks (dist.shard_chunks) from
+    tests/golden/config4.json, then the same gloo reduction, max-over-ranks time and the config-4
+    pin as a real run."""
+    import torch
+    import torch.distributed as dist
+
+    sys.path.insert(0, os.path.join(ROOT, "ebpf-emu_amd"))
+    from ebpf_emu import dist as D
+
+    with open(os.path.join(ROOT, "tests", "golden", "config4.json")) as f:
+        g4 = json.load(f)
+    assert args.config == "5tuple" and g4["total_packets"] == args.total_packets
+    sizes = D.chunk_sizes(args.total_packets, D.CHUNK)
+    mine = D.shard_chunks(len(sizes), world, rank)
+    t0 = time.perf_counter()
+    own = [0] * 8
+    for _ in range(args.steps):
+        for k in mine:
+            own = [a + b for a, b in zip(own, g4["chunk_counters"][k])]
+    counters = torch.tensor([m - (1 << 64) if m >= 1 << 63 else m for m in own],
+                            dtype=torch.int64)
+    dist.all_reduce(counters)
+    elapsed = torch.tensor([time.perf_counter() - t0 + 1e-6], dtype=torch.float64)
+    dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    cnt = [int(c) & ((1 << 64) - 1) for c in counters.tolist()]
+    want = [(c * args.steps) & ((1 << 64) - 1) for c in g4["counters"]]
+    assert cnt == want, ("config-4 counters differ from tests/golden/config4.json", cnt, want)
+    if rank == 0:
+        print(json.dumps({"metric": "stub", "value": args.total_packets * args.steps /
+                          float(elapsed) / 1e6, "unit": "Mpkt/s", "n_gpus": world,
+                          "steps": args.steps, "scaling": "strong",
+                          "packets_per_rank": [sum(sizes[k] for k in D.shard_chunks(len(sizes), world, r))
+                                               for r in range(world)],
+                          "counters": {"drop": cnt[1], "pass": cnt[2], "insns_retired": cnt[7]},
+                          "parity_pinned": "tests/golden/config4.json: counters == steps x fixture",
+                          "stub": True}), flush=True)
     dist.destroy_process_group()
 
 
@@ -383,8 +426,16 @@ def main():
     out = outs[0]
     stream = streams[0]
 
-    def step(i):
-        si = i % S
+    # step i of the K timed steps runs on stream (K-1-i) mod S: consecutive steps alternate, and
+    # the last one runs on stream 0, whose end event closes the timed region. With the last step
+    # on another stream the end join waits on that stream's completion signal from stream 0's
+    # queue, which measured 11 us more per run (tools/fixed_cost_ab.py "cur" vs "last0":
+    # profiles/r05_fixed_cost_ab.json)
+    def sof(i, k):
+        return (k - 1 - i) % S
+
+    def step(i, k=None):
+        si = sof(i, k if k is not None else S)
         prog.launch(sdescs[si][i % len(descs)], outs[si], streams[si])
 
     if args.settle_ms > 0:  # untimed: the GPU's clocks up to their steady state
@@ -412,16 +463,19 @@ def main():
     ev1 = torch.cuda.Event(enable_timing=True)
     if use_dist:
         dist.barrier()
+    K = args.steps
+    first = sof(0, K)  # (the stream of the first step: the start event is recorded there)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    ev0.record(stream)
-    for i in range(args.steps):
+    ev0.record(streams[first])
+    for i in range(K):
         if i == 1:  # (after the first launch: its enqueue is the first thing the GPU waits for)
-            for si in range(1, S):
-                streams[si].wait_event(ev0)
-        step(i)
+            for si in range(S):
+                if si != first:
+                    streams[si].wait_event(ev0)
+        step(i, K)
     t_enq = time.perf_counter() - t0  # host time to enqueue the K steps (launch-bound check)
-    for si in range(1, S):  # stream 0 joins the others before the end event
+    for si in range(1, S):  # stream 0 (the last step's) joins the others before the end event
         ej = torch.cuda.Event()
         ej.record(streams[si])
         stream.wait_event(ej)

@@ -1840,8 +1840,10 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* bin, const ebpf_batch_out* ou
   // the compiled variant that runs: variant 4 for the promoted program, 6 for an xdp_md batch in
   // place (rebased), 5 for a staged one (its range analysis knows the staged images' ctx)
   const JitFns* jit = xdp_rb ? &p->jit_fn[device][6] : batch_jit(p, b, kind, stk, device);
+  // (variant 5 compiles ctx loads through r1 as the ctx's constants: only with the main.rs
+  // registers, r1 = the image start)
   if (jit == &p->jit_fn[device][2] && (bin->flags & EBPF_BATCH_XDP_MD) && !xdp_direct &&
-      p->jit_mod[device][5])
+      !b->init_regs && p->jit_mod[device][5])
     jit = &p->jit_fn[device][5];
   const bool deep = jit == &p->jit_fn[device][2]   ? p->jit_deep
                     : jit == &p->jit_fn[device][4] ? p->pjit_deep
@@ -1881,6 +1883,9 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* bin, const ebpf_batch_out* ou
     d.xdp = a.xdp;  // (in place: tier 1 builds the ctx-prefixed images itself)
     const int g1 = std::min(tier1_grid(p, b, device), kDeoptMaxGrid);
     e = launch_interp(kKindTier1, d, g1, s, nullptr, false);
+    // a failed pass leaves the list's count behind: the next batch's pass would re-run its stale
+    // indices (the pass's last workgroup clears count and done)
+    if (e != hipSuccess) (void)hipMemsetAsync(a.deopt, 0, 8, s);
   }
   if (cur != device) hipSetDevice(cur);
   return e == hipSuccess ? EBPF_OK : EBPF_EHIP;

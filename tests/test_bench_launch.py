@@ -31,7 +31,7 @@ def _pins():
 
 
 @pytest.mark.parametrize("n,config", [(2, "5tuple"), (3, "acl"), (2, "checksum"),
-                                           (2, "checksum_xdp")])
+                                           (2, "checksum_xdp"), (8, "5tuple")])
 def test_launcher_spawns_ranks_and_pins(n, config):
     steps = 5
     r = _bench(["--gpus", str(n), "--steps", str(steps), "--config", config], {})
@@ -94,3 +94,25 @@ def test_pin_weak_logic():
     for w in (1, 2, 4, 8):
         ids = sorted(bench.chunk_id(k, r, w) for k in range(8) for r in range(w))
         assert ids == list(range(8 * w))
+
+
+def test_launcher_strong_scaling_8_ranks():
+    """The driver's strong-scaling shape: `bench.py --gpus 8 --total-packets 100000000` (BASELINE
+    config 4): 8 rank processes, each its contiguous shard of the 96 seeded chunks; the reduced
+    counters equal steps x the config-4 fixture (the pin a real run asserts), and every packet is
+    owned by exactly one rank."""
+    steps = 2
+    r = _bench(["--gpus", "8", "--steps", str(steps), "--total-packets", "100000000"], {},
+               timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    with open(os.path.join(GOLDEN, "config4.json")) as f:
+        c4 = json.load(f)
+    assert d["n_gpus"] == 8 and d["scaling"] == "strong" and d["parity_pinned"]
+    assert sum(d["packets_per_rank"]) == 100000000
+    assert max(d["packets_per_rank"]) - min(d["packets_per_rank"]) <= 2 * (1 << 20)
+    assert d["counters"]["drop"] == steps * c4["counters"][1]
+    assert d["counters"]["pass"] == steps * c4["counters"][2]
+    assert d["counters"]["insns_retired"] == steps * c4["counters"][7]

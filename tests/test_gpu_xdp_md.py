@@ -482,3 +482,58 @@ def test_xdp_md_loop_fuzz_in_place(cuda, oracle_mod, seed):
                     assert [int(x) for x in regs[i]] == oregs, (src, i, steps)
         prog.close()
     assert in_place >= 6, in_place
+
+
+@pytest.mark.parametrize("r1", [8, 4, 0])
+def test_xdp_md_loop_init_regs(cuda, oracle_mod, r1):
+    """Caller-set registers (batch.init_regs, emu.rs:14-17) on an xdp_md batch of loop programs:
+    with r1 != 0 the program's `ldxw rX, [r1+0/4]` are packet loads, not the ctx's data /
+    data_end, so neither the staged-ctx variant (5, which compiles them as the ctx's constants)
+    nor the rebased one (6) may run. Every packet's status / r0 / registers against the oracle on
+    the ctx-prefixed images with the same registers, and against the general interpreter.
+    The packets' first 8 bytes are in-image offsets, so with r1 = 8 the loops run over them."""
+    import torch
+
+    from ebpf_emu import Program
+    from ebpf_emu.asm import assemble
+
+    rng = random.Random(77 + r1)
+    pkts = []
+    for p in _xdp_packets(rng, 240, lens=(8, 9, 16, 40, 64, 100, 600)):
+        p = bytearray(p)
+        k = rng.randrange(0, len(p) + 1)
+        p[0:4] = struct.pack("<I", 8 + k)
+        p[4:8] = struct.pack("<I", 8 + len(p) - rng.randrange(0, 3))
+        pkts.append(bytes(p))
+    regs0 = [0, r1, 0, 0, 0, 0, 0, 0, 0, 0, 512]
+    ir = torch.tensor(np.array(regs0, dtype=np.uint64).view(np.int64), device=cuda)
+    frames, kw = _stage(pkts, cuda, offsets_layout=True, align=16)
+    for src in (XDP_SUM, XDP_SUM_RELOAD, XDP_SUM_WIDE, W_CHECKSUM_XDP()):
+        img = assemble(src) if isinstance(src, str) else src
+        prog = Program(img)
+        op = oracle_mod.Program(img)
+        for steps in (1 << 22, 200):
+            got = prog.run(frames, r0=True, status=True, regs=True, xdp_md=True, init_regs=ir,
+                           max_steps=steps, **kw)
+            gen = prog.run(frames, r0=True, status=True, regs=True, xdp_md=True, init_regs=ir,
+                           max_steps=steps, generic=True, **kw)
+            prod = prog.run(frames, r0=True, status=True, xdp_md=True, init_regs=ir,
+                            max_steps=steps, **kw)
+            torch.cuda.synchronize()
+            for k in ("r0", "status", "regs"):
+                assert torch.equal(getattr(got, k), getattr(gen, k)), (k, r1, steps)
+            assert torch.equal(prod.status, got.status) and torch.equal(prod.r0, got.r0)
+            status = got.status.cpu().numpy()
+            regs = got.regs.cpu().numpy().view(np.uint64)
+            for i, im in enumerate(_images(pkts)):
+                st, oregs, _, _ = op.run_full(im, 1024, 512, steps, init_regs=regs0)
+                assert status[i] == st, (i, r1, steps)
+                if st == 0:
+                    assert [int(x) for x in regs[i]] == oregs, (i, r1, steps)
+        prog.close()
+
+
+def W_CHECKSUM_XDP():
+    from ebpf_emu import workloads as W
+
+    return W.program("checksum_xdp")

@@ -66,6 +66,30 @@ def _same(a, b, ctx):
         assert np.array_equal(a[k], b[k]), f"{ctx}: {k} differs"
 
 
+def _eq_sensitive(got, want, ctx):
+    """got == want, and the comparison is live: the same check fails once one bit of the
+    expected array is flipped."""
+    got, want = np.asarray(got), np.asarray(want)
+    assert np.array_equal(got, want), ctx
+    if want.size:
+        w2 = want.copy()
+        w2.reshape(-1).view(np.uint8)[0] ^= 1
+        assert not np.array_equal(got, w2), f"{ctx}: a flipped bit went unnoticed"
+
+
+def _vs_oracle_batch(oracle_mod, img, buf, n, got, ctx, **kw):
+    """Every production output of `got` (verdict, r0 where the packet completed, status,
+    counters) against the C oracle's run_batch of the same packets (oracle/ebpf_oracle.c, which
+    restates emu.rs / mmu.rs / main.rs)."""
+    r0, st, cnt = oracle_mod.Program(img).run_batch(buf, n, threads=8, max_steps=STEPS, **kw)
+    _eq_sensitive(got["status"], st, f"{ctx}: status")
+    ok = st == 0
+    _eq_sensitive(got["r0"][ok], r0[ok], f"{ctx}: r0")
+    want_v = np.where(st != 0, 0xFF, np.where(r0 < 5, r0, 0xFE)).astype(np.uint8)
+    _eq_sensitive(got["verdict"], want_v, f"{ctx}: verdict")
+    _eq_sensitive(got["counters"], cnt, f"{ctx}: counters")
+
+
 @pytest.mark.parametrize("seed", range(4))
 def test_varl_fuzz(cuda, oracle_mod, seed):
     """Random forward programs over random packets (0..80 bytes) in offsets + lens batches of
@@ -103,12 +127,12 @@ def test_varl_fuzz(cuda, oracle_mod, seed):
 
 
 @pytest.mark.parametrize("name", ["5tuple", "drop", "acl", "5tuple_stack", "mac_swap_tx"])
-def test_varl_workloads_vs_fixed(cuda, name):
+def test_varl_workloads_vs_fixed(cuda, oracle_mod, name):
     """The bench programs (the stack-window ones on the stack statement) over 200 013 of the
     workload's frames as an offsets + lens batch
     (80-byte slots, every 5th packet misaligned in a quarter of the tiles) and with lengths
-    absent: verdicts, r0, status and counters == the compiled fixed-slot kernel's on the same
-    frames."""
+    absent: verdicts, r0, status and counters == the C oracle's on the same frames, and == the
+    compiled fixed-slot kernel's."""
     import torch
 
     from ebpf_emu import Program, _lib
@@ -119,6 +143,7 @@ def test_varl_workloads_vs_fixed(cuda, name):
     buf = W.frames_fixed(n, 64, 3)
     fr = torch.from_numpy(buf).to(cuda)
     ref = _outputs(prog, fr, dict(n=n, stride=64), cuda)
+    _vs_oracle_batch(oracle_mod, W.program(name), buf, n, ref, f"{name} fixed", stride=64)
     stack = name in ("5tuple_stack", "mac_swap_tx")  # (memory tier 0.5: the stack statements)
     assert _route(prog, fr, dict(n=n, stride=64)) == (_lib.EBPF_KERNEL_JIT_STACK if stack
                                                       else _lib.EBPF_KERNEL_JIT_FIXED)
@@ -139,14 +164,19 @@ def test_varl_workloads_vs_fixed(cuda, name):
         assert _route(prog, frames, kw) == (_lib.EBPF_KERNEL_JIT_VARL_STACK if stack
                                             else _lib.EBPF_KERNEL_JIT_VARL)
         got = _outputs(prog, frames, kw, cuda)
+        _vs_oracle_batch(oracle_mod, W.program(name), big.reshape(-1), n, got,
+                         f"{name} {sorted(kw)}", offsets=offs,
+                         lens=np.full(n, 64, dtype=np.uint16) if "lens" in kw else None,
+                         stride=0 if "lens" in kw else 64)
         _same(got, ref, f"{name} {sorted(kw)}")
     prog.close()
 
 
-def test_varl_statement_reentry(cuda):
+def test_varl_statement_reentry(cuda, oracle_mod):
     """One workgroup (EBPFEMU_VARL_WGS=1: 4 waves) over 3000 tiles: each wave runs 750 tiles, so
     the statement returns after 511 and comes back (the packed counter buckets are unpacked in
-    between); misaligned tiles on both sides of the return. Against the fixed-slot kernel."""
+    between); misaligned tiles on both sides of the return. Against the C oracle and the
+    fixed-slot kernel."""
     import torch
 
     from ebpf_emu import Program, _lib
@@ -174,6 +204,8 @@ def test_varl_statement_reentry(cuda):
         got = _outputs(prog, frames, kw, cuda)
     finally:
         del os.environ["EBPFEMU_VARL_WGS"]
+    _vs_oracle_batch(oracle_mod, W.program("5tuple"), big.reshape(-1), n, got, "reentry",
+                     offsets=offs, lens=np.full(n, 64, dtype=np.uint16))
     _same(got, ref, "reentry")
     prog.close()
 
@@ -216,21 +248,42 @@ def test_varl_layout_routes(cuda, oracle_mod):
     prog.close()
 
 
-def test_varl_xdp_md(cuda):
+def test_varl_xdp_md(cuda, oracle_mod):
     """xdp_md batches in place on the var tile loop (the ctx synthesised in the preloaded window,
-    BASE = packet - 8, LEN = 8 + len): == the general interpreter's in-place images."""
+    BASE = packet - 8, LEN = 8 + len): every output, registers included, == the C oracle's on the
+    ctx-prefixed images [u32 8][u32 8 + len][packet] (xdp.rs:16-20 handed to main.rs), and == the
+    general interpreter's in-place images."""
+    import struct
+
     from ebpf_emu import Program, _lib
     from ebpf_emu import workloads as W
 
     rng = random.Random(11)
     pkts = [gen_packet(rng, 100) for _ in range(260)]
-    prog = Program(W.program("5tuple_xdp"))
+    img = W.program("5tuple_xdp")
+    prog = Program(img)
+    op = oracle_mod.Program(img)
+    images = [struct.pack("<II", 8, 8 + len(p)) + p for p in pkts]
     for bad in (0, 9):
         frames, kw = _mixed(pkts, cuda, bad_every=bad)
         kw["xdp_md"] = True
         assert _route(prog, frames, kw) == _lib.EBPF_KERNEL_JIT_VARL
         got = _outputs(prog, frames, kw, cuda, regs=True)
         ref = _outputs(prog, frames, kw, cuda, generic=True, regs=True)
+        want = dict(status=[], r0=[], regs=[], counters=np.zeros(8, dtype=np.uint64))
+        for im in images:
+            st, oregs, _, steps = op.run_full(im, 1024, 512, STEPS)
+            want["status"].append(st)
+            want["regs"].append(oregs if st == 0 else [0] * 11)
+            want["counters"][(oregs[0] if oregs[0] < 5 else 5) if st == 0 else 6] += 1
+            want["counters"][7] += steps
+        st = np.array(want["status"], dtype=np.uint8)
+        ok = st == 0
+        oregs = np.array(want["regs"], dtype=np.uint64)
+        _eq_sensitive(got["status"], st, f"xdp bad {bad}: status")
+        _eq_sensitive(got["regs"][ok], oregs[ok], f"xdp bad {bad}: regs")
+        _eq_sensitive(got["r0"][ok], oregs[ok, 0], f"xdp bad {bad}: r0")
+        _eq_sensitive(got["counters"], want["counters"], f"xdp bad {bad}: counters")
         _same(got, ref, f"xdp bad {bad}")
     prog.close()
 
@@ -272,10 +325,11 @@ def test_varl_stride_lens(cuda, oracle_mod, name):
     prog.close()
 
 
-def test_varl_init_regs(cuda):
+def test_varl_init_regs(cuda, oracle_mod):
     """Caller-set registers (Emu.state.regs, emu.rs:14-17: batch.init_regs) on the var tile loop
-    (the statement's out-of-line initialisation): every output == the general interpreter's, for
-    random forward programs and register sets."""
+    (the statement's out-of-line initialisation): every output == the C oracle's run with the
+    same registers (oracle run_full init_regs), and == the general interpreter's, for random
+    forward programs and register sets."""
     import torch
 
     from ebpf_emu import Program, _lib
@@ -299,6 +353,17 @@ def test_varl_init_regs(cuda):
             continue
         got = _outputs(prog, frames, kw, cuda, regs=True, init_regs=ir)
         ref = _outputs(prog, frames, kw, cuda, generic=True, regs=True, init_regs=ir)
+        op = oracle_mod.Program(img)
+        ost, oregs = [], []
+        for p in pkts:
+            st, rr, _, _ = op.run_full(p, 1024, 512, STEPS, init_regs=regs)
+            ost.append(st)
+            oregs.append(rr if st == 0 else [0] * 11)
+        ost = np.array(ost, dtype=np.uint8)
+        ok = ost == 0
+        oregs = np.array(oregs, dtype=np.uint64)
+        _eq_sensitive(got["status"], ost, f"init_regs it {it}: status")
+        _eq_sensitive(got["regs"][ok], oregs[ok], f"init_regs it {it}: regs")
         _same(got, ref, f"init_regs it {it} prog {img.hex()}")
         prog.close()
         done += 1
