@@ -46,7 +46,7 @@ CONFIGS = {
     # packet-window stores; --generic: the general interpreter's tier 1)
     "tier1": (2, "XDP_TX MAC-swap reflector with packet stores and a stack atomic (17 insns) over 1Mi x 64B frames"),
     # a ~100-instruction firewall (past the tile interpreter's 62 micro-ops: the forward-program
-    # compiler; EBPFEMU_NO_JIT=1: dag_kernel), same frames as 5tuple
+    # compiler), same frames as 5tuple
     "acl": (2, "IPv4/IPv6 ACL firewall (97 insns) over 1Mi x 64B frames"),
     # the 5-tuple as a standard XDP program under the xdp_md calling convention (xdp.rs:16-20:
     # r1 = ctx, data / data_end read from it), same frames as 5tuple; the ctx is synthesised in
@@ -352,6 +352,7 @@ def main():
         buf = np.concatenate([D.chunk_frames(k, sizes[k]) for k in mine])
         batches.append(dict(frames=torch.from_numpy(buf).to(dev)))
         algo_bytes = n * (64 + 1)
+        floor_bytes = n * (64 + 1)
         pool_bytes = buf.nbytes
     k = 0
     while not args.total_packets:
@@ -365,6 +366,7 @@ def main():
                                 offsets=torch.from_numpy(offs.view(np.int32)).to(dev),
                                 lens=torch.from_numpy(lens.view(np.int16)).to(dev)))
             algo_bytes = int(lens.astype(np.int64).sum()) + n * (4 + 2 + 1)
+            floor_bytes = line_floor_bytes(offs.astype(np.int64), lens.astype(np.int64)) + n * (4 + 2 + 1)
         elif fb == 64 or k == 0:
             buf = W.frames_fixed(n, fb, cid)
             batches.append(dict(frames=torch.from_numpy(buf).to(dev)))
@@ -372,11 +374,16 @@ def main():
                 batches[-1]["offsets"] = torch.from_numpy(
                     (np.arange(n, dtype=np.int64) * fb).astype(np.uint32).view(np.int32)).to(dev)
                 batches[-1]["lens"] = torch.from_numpy(np.full(n, fb, dtype=np.int16)).to(dev)
-            # the bytes a header program's launch must read: its header window (+ offset and
-            # length) -- on fixed slots only the 16-byte chunks its loads reach (jit.cpp
-            # window_chunks: 16 for drop-all, the whole 64 with a register-address load)
+            # a header program's algorithmic bytes are its packet's 64-byte header
+            # window + the verdict byte (+ offset and length) = 65 B per 64-byte frame. The floor
+            # is what HBM must move for them: the 128-byte lines the bytes the launch reads touch
+            # (on fixed slots only the 16-byte chunks the program's loads reach, jit.cpp
+            # window_chunks: 16 for drop-all, all 64 with a register-address load)
             wb = prog.window_bytes if args.layout == "fixed" and not args.generic else 64
-            algo_bytes = n * (wb + 1 + (6 if args.layout == "offsets" else 0))
+            meta = 6 if args.layout == "offsets" else 0
+            algo_bytes = n * (64 + 1 + meta)
+            st = np.arange(n, dtype=np.int64) * fb
+            floor_bytes = line_floor_bytes(st, np.full(n, wb, dtype=np.int64)) + n * (1 + meta)
         else:  # large slots: copies of the first batch at other addresses (host RNG is slow)
             batches.append(dict(frames=batches[0]["frames"].clone()))
         # (the bytes a launch touches decide whether the pool outgrows the Infinity Cache)
@@ -526,6 +533,7 @@ def main():
     # S > 1 streams consecutive launches overlap, so this is the time between batches, not one
     # kernel's duration), and the same bytes over the wall-clock step time that `value` uses
     achieved_gbs = algo_bytes / (kern_avg_ms * 1e-3) / 1e9
+    floor_gbs = floor_bytes / (kern_avg_ms * 1e-3) / 1e9
     wall_gbs = algo_bytes * args.steps / elapsed / 1e9
     # one launch at a time, after the timed region (not part of `value`): the kernel's own
     # duration, which rocprof's per-kernel average of a --streams 1 run reports
@@ -623,6 +631,14 @@ def main():
                 "achieved_wall": round(wall_gbs, 2),
                 "frac_wall": round(wall_gbs / HBM_PEAK_GBS, 5),
                 "algo_bytes_per_launch": algo_bytes,
+                # the HBM line floor of those bytes (128-byte lines touched: a 64-byte window in
+                # a 1504-byte slot straddles two lines in one case of four) and its fraction;
+                # the PMC traffic per launch over the same time (null without a PMC summary)
+                "floor_bytes_per_launch": floor_bytes,
+                "floor_bytes_per_packet": round(floor_bytes / max(n, 1), 2),
+                "frac_floor": round(floor_gbs / HBM_PEAK_GBS, 5),
+                "frac_traffic": (round(traffic / (kern_avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
+                                 if traffic else None),
                 # HIP-event time per step over the timed region: one event pair around the K
                 # launches (each one whole batch; with counters, its last workgroup folds the
                 # per-shard sums into them). With S > 1 streams the launches overlap: rocprof's
@@ -654,6 +670,21 @@ def main():
         print(json.dumps(line), flush=True)
     if use_dist:
         dist.destroy_process_group()
+
+
+def line_floor_bytes(starts, lengths, line=128):
+    """Bytes of the distinct 128-byte HBM lines that byte ranges [start, start + length) touch
+    (the MI355X L2 line: a read of any byte of a line moves the line)."""
+    import numpy as np
+
+    starts = np.asarray(starts, dtype=np.int64)
+    lengths = np.asarray(lengths, dtype=np.int64)
+    keep = lengths > 0
+    a = starts[keep] // line
+    b = (starts[keep] + lengths[keep] - 1) // line
+    span = b - a + 1
+    idx = np.repeat(a, span) + (np.arange(int(span.sum())) - np.repeat(np.cumsum(span) - span, span))
+    return int(np.unique(idx).size) * line
 
 
 def host_cpus():

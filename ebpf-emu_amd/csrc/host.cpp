@@ -283,19 +283,6 @@ static const bool g_trace = [] {
 static uint64_t* g_trace_buf[kMaxDevices] = {};
 static uint32_t g_trace_launch[kMaxDevices] = {};
 
-// EBPFEMU_NO_JIT=1: forward-only programs run on the tile interpreter (A/B runs).
-static const bool g_no_jit = [] {
-  const char* e = getenv("EBPFEMU_NO_JIT");
-  return e && e[0] == '1';
-}();
-
-// EBPFEMU_NO_PROMOTE=1 (A/B): stack-window loop programs keep their slots in the stack window
-// (the loop kernel's stack variant) instead of promote_slots' registers.
-static const bool g_no_promote = [] {
-  const char* e = getenv("EBPFEMU_NO_PROMOTE");
-  return e && e[0] == '1';
-}();
-
 // EBPFEMU_TEST_FAIL_STACK_JIT=1 (tests): every stack-window program's compilation fails, so
 // that the fallback to the general interpreter is exercised.
 static const bool g_fail_stack_jit = [] {
@@ -320,7 +307,7 @@ static int jit_compile_locked(ebpf_prog* p) {
     // Compiler::xdp_rebase) when every packet load is proven past the ctx
     p->jit_has[6] = p->jit_has[5];
     if (p->stack.k) p->jit_has[1] = !p->tuopsk.empty();  // (the main.rs layout only)
-    if (g_no_jit || (!p->jit_has[0] && !p->jit_has[1] && !p->jit_has[2])) {
+    if (!p->jit_has[0] && !p->jit_has[1] && !p->jit_has[2]) {
       p->jit_state = 2;
     } else {
       p->jit_state = 1;
@@ -379,8 +366,6 @@ static int jit_compile_locked(ebpf_prog* p) {
       }
       if (p->jit_state == 1 && !p->jit_has[0] && !p->jit_has[1] && !p->jit_has[2])
         p->jit_state = 2;
-      if (p->jit_state == EBPF_EJIT && getenv("EBPFEMU_JIT_VERBOSE"))
-        fprintf(stderr, "ebpfemu: program compiler: %s\n", p->jit_err.c_str());
     }
   }
   return p->jit_state == 1 ? 1 : p->jit_state == 2 ? 0 : p->jit_state;
@@ -393,30 +378,6 @@ static const int g_bin = [] {
   return e ? (e[0] == '1' ? 1 : 0) : -1;
 }();
 constexpr uint64_t kBinMinPackets = 16384;
-
-// A/B: EBPFEMU_NO_LOOP=1 runs loop programs on the general interpreter (interp_kernel).
-static const bool g_no_loop = [] {
-  const char* e = getenv("EBPFEMU_NO_LOOP");
-  return e && e[0] == '1';
-}();
-
-// EBPFEMU_NO_STACK=1: no memory tier 0.5 (stack-window programs run on interp_kernel tier 1).
-static const bool g_no_stack = [] {
-  const char* e = getenv("EBPFEMU_NO_STACK");
-  return e && e[0] == '1';
-}();
-
-// EBPFEMU_NO_FLATTEN=1: programs with CALL keep the general interpreter's frame stack.
-static const bool g_no_flatten = [] {
-  const char* e = getenv("EBPFEMU_NO_FLATTEN");
-  return e && e[0] == '1';
-}();
-
-// EBPFEMU_NO_DAG=1 runs every tier-0 program on interp_kernel (A/B runs, differential tests).
-static const bool g_no_dag = [] {
-  const char* e = getenv("EBPFEMU_NO_DAG");
-  return e && e[0] == '1';
-}();
 
 // EBPFEMU_XDP_STAGE=1 (A/B): every xdp_md batch goes through xdp_stage (xdp_in_place). (Outside the
 // extern "C" block below: a lambda initializer there was given the same closure as g_trace's by
@@ -1229,10 +1190,9 @@ int ebpf_prog_load(const uint8_t* code, size_t nbytes, ebpf_prog** out, size_t* 
     p->uops.push_back(u);
   }
   // CALL / EXIT: the frame stacks as program copies (flatten_calls) for every kernel but the
-  // general interpreter, unless EBPFEMU_NO_FLATTEN=1 or the program does not flatten
+  // general interpreter, unless the program does not flatten
   p->xuops = p->uops;
-  if (std::any_of(p->uops.begin(), p->uops.end(), [](const Uop& u) { return u.op == U_CALL; }) &&
-      !g_no_flatten) {
+  if (std::any_of(p->uops.begin(), p->uops.end(), [](const Uop& u) { return u.op == U_CALL; })) {
     std::vector<Uop> f;
     if (flatten_calls(p->uops, f)) {
       p->xuops = std::move(f);
@@ -1266,7 +1226,7 @@ int ebpf_prog_load(const uint8_t* code, size_t nbytes, ebpf_prog** out, size_t* 
     p->ltuops = build_tile(xu, d);
     p->ltuopsx = build_tile(xu, d, true);
   }
-  if (p->xtier == 1 && !g_no_stack) {  // memory tier 0.5: the compiled fixed-slot kernel only
+  if (p->xtier == 1) {  // memory tier 0.5: the compiled fixed-slot kernel only
     StackAnalysis sa = analyze_stack(xu);
     const std::vector<DUop> dk =
         sa.plan.k && forward ? fold_const_loads(xu, build_dag(xu)) : std::vector<DUop>();
@@ -1289,7 +1249,7 @@ int ebpf_prog_load(const uint8_t* code, size_t nbytes, ebpf_prog** out, size_t* 
         p->ltuopsx = build_tile(xu, d, true, true);
         // loops with whole-slot accumulators: also the promoted tier-0 program (variant 4)
         std::vector<Uop> pu;
-        if (!forward && !g_no_promote && promote_slots(xu, sa.plan, pu)) {
+        if (!forward && promote_slots(xu, sa.plan, pu)) {
           const std::vector<DUop> pd = build_dag(pu);
           p->pltuops = build_tile(pu, pd);
           p->pltuopsx = build_tile(pu, pd, true);
@@ -1546,7 +1506,7 @@ static bool stack_launch_ok(const ebpf_prog* p, const ebpf_batch* b, const ebpf_
 // variant.
 static bool stack_loop_ok(const ebpf_prog* p, const ebpf_batch* b, const ebpf_batch_out* out,
                           int device) {
-  return stack_common_ok(p, b, out) && p->jit_mod[device][2] && !g_no_loop && stack_var_ok(p, b);
+  return stack_common_ok(p, b, out) && p->jit_mod[device][2] && stack_var_ok(p, b);
 }
 
 // The stack-slot promoted program (variant 4, promote_slots) on this batch: the production
@@ -1556,7 +1516,7 @@ static bool promo_ok(const ebpf_prog* p, const ebpf_batch* b, const ebpf_batch_o
                      int device) {
   if (p->puops.empty() || !p->jit_mod[device][4] || !p->dev_pltuops[device]) return false;
   if (!stack_common_ok(p, b, out) || out->regs || out->fp || out->fp_len) return false;
-  return !g_no_loop;
+  return true;
 }
 
 // The kernel kind of a batch (uploaded program): dag_kernel needs no step budget (a lane of a
@@ -1567,7 +1527,7 @@ static int batch_kind(const ebpf_prog* p, const ebpf_batch* b, const ebpf_batch_
                       int device, bool* stk) {
   // (the final frame stacks of a flattened program are its copies' stacks: the general
   // interpreter's frame stack writes them)
-  const bool generic = g_no_dag || (b->flags & EBPF_BATCH_GENERIC) || b->init_fp_len ||
+  const bool generic = (b->flags & EBPF_BATCH_GENERIC) || b->init_fp_len ||
                        (p->flattened && (out->fp || out->fp_len));
   *stk = false;
   if (p->stack.k && !generic) {
@@ -1577,7 +1537,7 @@ static int batch_kind(const ebpf_prog* p, const ebpf_batch* b, const ebpf_batch_
     return batch_tier(p, b);
   }
   return (p->dev_duops[device] && b->max_steps >= p->xuops.size() && !generic) ? kKindDag
-         : (p->dev_ltuops[device] && !generic && !g_no_loop && !p->stack.k && p->xtier == 0 &&
+         : (p->dev_ltuops[device] && !generic && !p->stack.k && p->xtier == 0 &&
             (p->xuops.size() <= kTileMaxUops ||  // tile_kernel's loop mode, or compiled only
              (p->jit_mod[device][2] && !(b->flags & EBPF_BATCH_NO_JIT))))          ? kKindLoop
                                                                          : batch_tier(p, b);

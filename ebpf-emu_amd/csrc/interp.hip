@@ -261,10 +261,8 @@ __device__ __forceinline__ void img_write(uint32_t* img, uint32_t a, uint32_t w,
 // per lane, so the 16-bit lengths land in 4-byte slots.)
 constexpr uint32_t kWinBytes = kWave * kWin;                          // one buffer, 4 KiB
 constexpr uint32_t kMetaBytes = 2 * kWave * 4 + 2 * kWave * 4;             // 1 KiB
-// per-wave LDS bytes: double-buffered windows (DB) or one window buffer
-__host__ __device__ constexpr uint32_t wave_lds0(bool db) {
-  return (db ? 2 : 1) * kWinBytes + kMetaBytes;
-}
+// per-wave LDS bytes of the general interpreter's tier 0: one window buffer + metadata
+constexpr uint32_t kWaveLds0 = kWinBytes + kMetaBytes;
 
 struct WaveLds {
   uint8_t* win;        // [2][kWinBytes]
@@ -460,10 +458,6 @@ __device__ __forceinline__ void flush_counters(const LaunchArgs& a, const uint64
   const uint32_t g = blockIdx.x % kCounterShards;
   if (lane >= 8) return;
   const uint64_t sum = w->acc[lane];
-  if (a.fold_kernel == 2) {  // (A/B) no shards: a non-returning add to the caller's counter
-    if (sum) __hip_atomic_fetch_add(&a.counters[lane], sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
   uint64_t* word = &a.shards[g * 8 + lane];
   if (a.fold_kernel) {  // fold_counters runs next on the stream
     if (sum) __hip_atomic_fetch_add(word, sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -490,7 +484,7 @@ __device__ __forceinline__ void flush_counters(const LaunchArgs& a, const uint64
     rhi[i] = (uint32_t)(v_ >> 32);       \
   } while (0)
 
-template <int TIER, bool LDSP, int NW, bool DB>
+template <int TIER, bool LDSP, int NW>
 __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
   // the deopt pass with an empty list (the usual case): every workgroup leaves at once -- no
   // program staging, no counter flush, nothing to clear (the list cannot grow during the pass)
@@ -502,7 +496,7 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
   const uint32_t nu = a.n_uops;
   const uint32_t prog_bytes = LDSP ? nu * (uint32_t)sizeof(Uop) : 0u;
   Uop* sprog = (Uop*)smem;
-  uint8_t* const wave_region = smem + prog_bytes;  // tier 0: wave_lds0(DB) per wave
+  uint8_t* const wave_region = smem + prog_bytes;  // tier 0: kWaveLds0 per wave
 
   // stage the program once per workgroup (emu.instructions, emu.rs:24)
   if (LDSP) {
@@ -515,8 +509,8 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
   const uint32_t lane = threadIdx.x & (kWave - 1);
   const uint32_t wv = threadIdx.x / kWave;
   WaveLds L;
-  L.win = wave_region + (size_t)wv * wave_lds0(DB);
-  L.meta_off = (uint32_t*)(L.win + (DB ? 2 : 1) * kWinBytes);
+  L.win = wave_region + (size_t)wv * kWaveLds0;
+  L.meta_off = (uint32_t*)(L.win + kWinBytes);
   L.meta_len = L.meta_off + 2 * kWave;
   const uint32_t my_swz = win_swz(lane);
   const uint64_t wave_slot = (uint64_t)blockIdx.x * kWavesPerBlock + wv;
@@ -532,25 +526,15 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
   uint64_t cnt[7] = {0, 0, 0, 0, 0, 0, 0};  // wave-uniform verdict buckets + faults
   uint64_t retired = 0;                     // per lane
 
-  // Tier 0 pipeline (W = total waves; buffers alternate per tile of this wave).
-  //  DB (double-buffered windows): at the top of tile t the windows of t (buffer b) and the
-  //  metadata of t + W (buffer b ^ 1) have landed; the wave DMAs the windows of t + W into buffer
-  //  b ^ 1 and the metadata of t + 2W into buffer b, and interprets t while both are in flight.
-  //  !DB (one window buffer, half the LDS, more resident waves): the windows of t are DMA'd and
-  //  waited for at the top of t; only the metadata of t + W is in flight during t.
+  // Tier 0 pipeline (W = total waves; metadata buffers alternate per tile of this wave): the
+  // windows of t are DMA'd and waited for at the top of t; the metadata of t + W is in flight
+  // during t. (Double-buffered windows -- the next tile's windows in flight as well -- were an
+  // opt-in A/B variant until round 5: half the resident waves, not faster.)
   uint32_t b = 0;
   bool co_cur = false;  // tile t's windows were DMA'd (all packet bases 16-byte aligned)
   if (TIER == 0 && wave_slot < a.n_tiles) {
     dma_meta(a, L, 0, wave_slot, lane);
     dma_wait();
-    if (DB) {
-      uintptr_t mb;
-      uint32_t ml;
-      meta_of(a, L, 0, wave_slot, lane, mb, ml);
-      co_cur = ballot(ml != 0 && (mb & 15) != 0) == 0;
-      if (co_cur) dma_window(a, L, 0, 0, wave_slot, lane);
-      if (wave_slot + total_waves < a.n_tiles) dma_meta(a, L, 1, wave_slot + total_waves, lane);
-    }
   }
 
   // the deopt pass (tier 1, LaunchArgs::deopt_pass): the packets the compiled store-mode kernel
@@ -567,20 +551,18 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
     const uint64_t pkt = !dpass ? slot : valid ? (uint64_t)a.deopt_idx[slot] : 0ull;
     const uint8_t* base = nullptr;
     uint32_t len = 0;
-    uint8_t* const my_win = L.win + (DB ? b : 0u) * kWinBytes + lane * kWin;
+    uint8_t* const my_win = L.win + lane * kWin;
     if (TIER == 0) {
-      dma_wait();  // DB: windows of this tile + metadata of the next; !DB: this tile's metadata
+      dma_wait();  // this tile's metadata
       uintptr_t mb;
       uint32_t ml;
       meta_of(a, L, b, tile, lane, mb, ml);
       base = (const uint8_t*)mb;
       len = valid ? ml : 0u;
-      if (!DB) {
-        co_cur = ballot(valid && ml != 0 && (mb & 15) != 0) == 0;
-        if (co_cur) {
-          dma_window(a, L, b, 0, tile, lane);
-          dma_wait();
-        }
+      co_cur = ballot(valid && ml != 0 && (mb & 15) != 0) == 0;
+      if (co_cur) {
+        dma_window(a, L, b, 0, tile, lane);
+        dma_wait();
       }
       if (!co_cur) stage_window_lane(my_win, my_swz, base, len, valid);
     } else if (valid) {
@@ -634,21 +616,7 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
       // which hipcc does not see.
       __builtin_amdgcn_s_waitcnt(0x0F70);
       const uint64_t tn = tile + total_waves;
-      if (DB) {
-        // next tile of this wave: its metadata is in buffer b ^ 1
-        bool co_nxt = false;
-        if (tn < a.n_tiles) {
-          uintptr_t nb;
-          uint32_t nl;
-          meta_of(a, L, b ^ 1, tn, lane, nb, nl);
-          co_nxt = ballot(nl != 0 && (nb & 15) != 0) == 0;
-          if (co_nxt) dma_window(a, L, b ^ 1, b ^ 1, tn, lane);
-        }
-        // the metadata reads of buffer b (top of this tile) returned before the DMA overwrites it
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (tn + total_waves < a.n_tiles) dma_meta(a, L, b, tn + total_waves, lane);
-        co_cur = co_nxt;
-      } else if (tn < a.n_tiles) {
+      if (tn < a.n_tiles) {
         dma_meta(a, L, b ^ 1, tn, lane);  // lands while this tile is interpreted
       }
     }
@@ -1456,19 +1424,15 @@ hipError_t launch_xdp_stage(const uint8_t* frames, const uint32_t* offsets, cons
 // ============================================================================================
 constexpr uint32_t kTileWaveLds = kWinBytes + kDagMetaBytes;  // window + metadata, 4.5 KiB
 constexpr uint32_t kTileWaveLdsPipe = kWinBytes + 2 * kDagMetaBytes;  // two metadata buffers, 5 KiB
-constexpr uint32_t kTileWaveLdsDb3 = 2 * kWinBytes + 3 * kDagMetaBytes;  // DB: 9.5 KiB
 // the compiled forward var kernels (tile_body PLEN): metadata buffers with packed u16 lengths
 // (dma_meta<true>), 384 bytes each -- a wave's window and two buffers take 4864 bytes, so eight
 // 4-wave workgroups and their 80 bytes of static counters fit a CU's 160 KiB of LDS (5 KiB buffers
 // left room for seven)
 constexpr uint32_t kVarMetaBytes = kWave * 4 + kWave * 2;
 constexpr uint32_t kVarWaveLds = kWinBytes + 2 * kVarMetaBytes;       // 4.75 KiB
-constexpr uint32_t kVarWaveLdsDb3 = 2 * kWinBytes + 3 * kVarMetaBytes;  // DB: 9.1 KiB
 // ebpf_tile_jit_varl: two windows and two packed metadata buffers per wave, 8.75 KiB (4 workgroups
 // of 4 waves per CU)
 constexpr uint32_t kVarlWaveLds = 2 * kWinBytes + 2 * kVarMetaBytes;
-// the var kernels' metadata pipeline: on unless the launch asks otherwise (A/B, LaunchArgs.var_pipe)
-__device__ __forceinline__ bool g_var_pipe(const LaunchArgs& a) { return a.var_nopipe == 0; }
 
 
 #define TILE_ASM_OUT [bkt] "=&v"(bkt), [nst] "=&v"(nst)
@@ -1528,26 +1492,20 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
   // PIPE (the compiled kernels on offsets / lens batches): two metadata buffers per wave, the
   // next tile's offsets and lengths DMA'd while this tile runs, so a tile waits for one HBM round
   // trip (its windows) instead of two (metadata, then windows). Loop kernels: only in batch order
-  // (no perm) and with a persistent grid (EBPFEMU_LOOP_GRID=persist; one tile per wave has no
-  // next tile). The statement reads the metadata in its prologue only, and a DMA older than its
-  // own loads only makes its vmcnt waits stricter.
-  // DB (the forward var kernels, LaunchArgs.var_db, opt-in A/B): also two window buffers and
-  // three metadata buffers per wave -- tile i runs on window i % 2 while tile i+1's windows and
-  // tile i+2's metadata are in flight, so a tile waits for no HBM round trip of its own (the
-  // fixed-slot kernel's scheme, with the metadata one tile further ahead). Measured slower than
-  // the metadata prefetch alone: 9.5 KiB of LDS per wave leaves 4 waves per SIMD instead of 7.
+  // (no perm; one tile per wave, so only a wave whose grid slot recurs has a next tile). The
+  // statement reads the metadata in its prologue only, and a DMA older than its own loads only
+  // makes its vmcnt waits stricter. (Double-buffered windows as well, with three metadata
+  // buffers, were measured slower: 9.5 KiB of LDS per wave leaves 4 waves per SIMD instead of 7,
+  // profiles/r03_ab_var_db.json; removed in round 5.)
   constexpr bool PIPE = JIT && !FIXED;
   // PLEN: the compiled forward var kernels' packed-length metadata buffers (dma_meta<true>; the
   // statement's prologue reads the lengths as u16, gen_tile.py %[plen])
   constexpr bool PLEN = JIT && !FIXED && !LOOPS;
-  const bool pipe = PIPE && g_var_pipe(a) && !(LOOPS && a.perm);
-  const bool db = PIPE && !LOOPS && pipe && a.var_db != 0;
-  const uint32_t nmeta = db ? 3u : 2u;
+  const bool pipe = PIPE && !(LOOPS && a.perm);
   constexpr uint32_t kMetaStride = PLEN ? kVarMetaBytes / 4 : 2 * kWave;  // (u32 units)
   WaveLds L;
-  L.win = smem + wv * (PLEN ? (db ? kVarWaveLdsDb3 : kVarWaveLds)
-                            : db ? kTileWaveLdsDb3 : PIPE ? kTileWaveLdsPipe : kTileWaveLds);
-  L.meta_off = (uint32_t*)(L.win + (db ? 2 : 1) * kWinBytes);
+  L.win = smem + wv * (PLEN ? kVarWaveLds : PIPE ? kTileWaveLdsPipe : kTileWaveLds);
+  L.meta_off = (uint32_t*)(L.win + kWinBytes);
   L.meta_len = L.meta_off + kWave;
   // window buffer w and metadata buffer m of this wave (offsets, then lengths: 512 bytes each, or
   // 384 with PLEN)
@@ -1558,24 +1516,7 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
     x.meta_len = x.meta_off + kWave;
     return x;
   };
-  const bool sw0 = stride_windows(a);
-  // DB: DMA tile t's windows into X.win (its metadata landed in X's buffer); false when some
-  // packet base is not 16-byte aligned (its lanes stage the window themselves, at its turn)
-  auto issue_window = [&](uint64_t t, const WaveLds& X, uint32_t lane) {
-    if (sw0) {
-      dma_window_stride(a, X.win, t, lane);
-      return true;
-    }
-    uintptr_t pb;
-    uint32_t ml;
-    meta_of<PLEN>(a, X, 0, t, lane, pb, ml);
-    const bool ok = ballot(t * kWave + lane < a.n && ml != 0 && (pb & 15) != 0) == 0;
-    if (ok) dma_window<PLEN>(a, X, 0, 0, t, lane);
-    return ok;
-  };
-  uint32_t mb = 0;      // PIPE: the metadata buffer of the current tile (0 .. nmeta - 1)
-  uint32_t wi = 0;      // DB: its window buffer
-  bool cur_dma = true;  // DB: its windows were DMA'd (else staged per lane at its turn)
+  uint32_t mb = 0;  // PIPE: the metadata buffer of the current tile (0 or 1)
   const uint64_t wave_slot = (uint64_t)blockIdx.x * WPB + wv;
   const uint64_t total_waves = (uint64_t)gridDim.x * WPB;
   const auto ka = __builtin_amdgcn_kernarg_segment_ptr();
@@ -1603,46 +1544,20 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
   };
   if (trace) stamp(0);
 
-  if (pipe && wave_slot < a.n_tiles) {  // the first tile's metadata (DB: and its windows)
+  if (pipe && wave_slot < a.n_tiles) {  // the first tile's metadata
     uint32_t lane;
     asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
     dma_meta<PLEN>(a, L, 0, wave_slot, lane);
-    if (db) {
-      dma_wait();
-      cur_dma = issue_window(wave_slot, bufs(0, 0), lane);
-      if (wave_slot + total_waves < a.n_tiles) dma_meta<PLEN>(a, bufs(0, 1), 0, wave_slot + total_waves, lane);
-    }
   }
   for (uint64_t tile = wave_slot; tile < a.n_tiles;) {
     // the lane index is re-derived inside the loop (volatile: not hoistable), so no per-lane
     // address of the window DMA stays live across the asm statement
     uint32_t aligned = 1;  // every packet base of the tile 16-byte aligned (loop-mode refills)
-    // this tile's window and metadata buffers (without PIPE / DB: buffer 0)
-    const WaveLds Lc = bufs(db ? wi : 0u, PIPE ? mb : 0u);
+    // this tile's window and metadata buffers (without PIPE: buffer 0)
+    const WaveLds Lc = bufs(0u, PIPE ? mb : 0u);
     const uint32_t winb = lds_addr(Lc.win);
     const uint32_t metab = lds_addr(Lc.meta_off);
-    if (!FIXED && db) {
-      uint32_t lane;
-      asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
-      dma_wait();  // this tile's windows, the next tile's metadata
-      const uint64_t t0 = rfl64(tile);
-      const bool valid = t0 * kWave + lane < a.n;
-      uintptr_t pb;
-      uint32_t ml;
-      meta_of<PLEN>(a, Lc, 0, t0, lane, pb, ml);
-      if (!cur_dma)
-        stage_window_lane(Lc.win + lane * kWin, win_swz(lane), (const uint8_t*)pb,
-                          valid ? ml : 0u, valid);
-      const uint64_t t1 = t0 + total_waves;
-      if (t1 < a.n_tiles) {  // tile t1's windows, tile t2's metadata: in flight while t0 runs
-        const uint32_t m1 = mb + 1 == nmeta ? 0u : mb + 1, m2 = m1 + 1 == nmeta ? 0u : m1 + 1;
-        const bool nxt = issue_window(t1, bufs(wi ^ 1u, m1), lane);
-        if (t1 + total_waves < a.n_tiles) dma_meta<PLEN>(a, bufs(0, m2), 0, t1 + total_waves, lane);
-        cur_dma = nxt;
-      }
-      if (a.xdp) xdp_window(Lc.win + lane * kWin, win_swz(lane), ml);
-      __builtin_amdgcn_s_waitcnt(0xc07f);  // the window's LDS writes / metadata reads: done
-    } else if (!FIXED) {  // (FIXED: the asm statement DMAs the windows itself)
+    if (!FIXED) {  // (FIXED: the asm statement DMAs the windows itself)
       uint32_t lane;
       asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
       const uint64_t pkt = tile * kWave + lane;
@@ -1773,8 +1688,7 @@ __device__ __forceinline__ void tile_body(LaunchArgs& a) {
     if (trace && !LOOPS && ti < 5) stamp(2 + 2 * ti);
     ti++;
     tile = nt;
-    if (pipe) mb = mb + 1 == nmeta ? 0u : mb + 1;  // (without the prefetch: buffer 0 always)
-    wi ^= 1u;
+    if (pipe) mb ^= 1u;  // (without the prefetch: buffer 0 always)
   }
   uint64_t cnt64[7];
 #pragma unroll
@@ -1813,11 +1727,11 @@ extern "C" __global__ __launch_bounds__(kDbBlock, 1) void ebpf_tile_jit_fixed(La
   const uint32_t wv = rfl(threadIdx.x / kWave);
   // the wave's first tile's windows go out before the workgroup's start barrier (counters_init:
   // the 16 waves of a workgroup do not start together), the statement then skips that DMA
-  // (A/B: LaunchArgs::fixed_late)
+  // (A/B, round 4: 14.17 vs 14.72 us one launch, profiles/r04_ab_fixed_early_dma.log)
   uint32_t first = 1;
   {
     const uint32_t t0 = blockIdx.x + wv * gridDim.x;
-    if (!a.fixed_late && t0 < a.n_tiles) {
+    if (t0 < a.n_tiles) {
       uint32_t ln;
       asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
       dma_window_stride(a, smem + wv * kTileWaveLdsDb, t0, ln);
@@ -2133,68 +2047,46 @@ hipError_t launch_counters_add(const uint64_t* src, uint64_t* dst, hipStream_t s
 }
 
 // Counter fold: in-kernel with counted shard words (default), or fold_counters after the launch
-// (EBPFEMU_FOLD=kernel for A/B runs, and launches whose per-shard sums could reach 2^48).
-static int g_fold_mode = [] {
+// (EBPFEMU_FOLD=kernel: fold_counters for every launch -- the test of the path that launches whose
+// per-shard sums could reach 2^48 take, tests/test_knobs.py)
+static bool g_fold_kernel = [] {
   const char* e = getenv("EBPFEMU_FOLD");
-  return !e ? -1 : e[0] == 'i' ? 0 : e[0] == 'd' ? 2 : 1;
-}();
-// A/B: EBPFEMU_FIXED=0 disables the fixed-slot variants
-static bool g_fixed = [] {
-  const char* e = getenv("EBPFEMU_FIXED");
-  return !e || e[0] != '0';
-}();
-
-static bool g_db = [] {  // tier-0 window double-buffering (EBPFEMU_TIER0_DB=0|1 for A/B runs)
-  const char* e = getenv("EBPFEMU_TIER0_DB");
-  return e ? e[0] == '1' : false;
-}();
-
-// A/B switch: EBPFEMU_NO_TILE=1 runs forward-only programs on dag_kernel instead of tile_kernel.
-static bool g_no_tile = [] {
-  const char* e = getenv("EBPFEMU_NO_TILE");
-  return e && e[0] == '1';
-}();
-
-// A/B knob (EBPFEMU_LDS_PAD=bytes): extra dynamic LDS per workgroup, to lower occupancy on purpose.
-static uint32_t g_lds_pad = [] {
-  const char* e = getenv("EBPFEMU_LDS_PAD");
-  return e ? (uint32_t)atoi(e) : 0u;
+  return e && e[0] == 'k';
 }();
 
 static uint32_t lds_bytes_for(int kind, uint32_t n_uops, bool jit_loop = false) {
   if (kind == kKindLoop)  // (the compiled loop kernels: + the second metadata buffer)
-    return g_lds_pad + kWavesPerBlock * (jit_loop ? kTileWaveLdsPipe : kTileWaveLds);
+    return kWavesPerBlock * (jit_loop ? kTileWaveLdsPipe : kTileWaveLds);
   if (kind == kKindDag)  // the program is fetched by SMEM
-    return g_lds_pad +
-           kWavesPerBlock * (n_uops <= kTileMaxUops && !g_no_tile ? kTileWaveLds : kDagWaveLds);
+    return kWavesPerBlock * (n_uops <= kTileMaxUops ? kTileWaveLds : kDagWaveLds);
   const uint32_t prog = n_uops <= (uint32_t)kMaxLdsUops ? n_uops * (uint32_t)sizeof(Uop) : 0u;
-  uint32_t rest = kind == kKindTier0 ? kWavesPerBlock * wave_lds0(g_db) : 0u;
+  uint32_t rest = kind == kKindTier0 ? kWavesPerBlock * kWaveLds0 : 0u;
   return prog + rest;
 }
 
 // Kernel variant for a program: tier (memory model), LDS-staged program, scheduler width.
-template <int TIER, bool DB>
+template <int TIER>
 static const void* variant(uint32_t n_uops) {
-  if (n_uops <= 64) return (const void*)interp_kernel<TIER, true, 1, DB>;
-  if (n_uops <= 256) return (const void*)interp_kernel<TIER, true, 4, DB>;
-  if (n_uops <= (uint32_t)kMaxLdsUops) return (const void*)interp_kernel<TIER, true, 0, DB>;
-  return (const void*)interp_kernel<TIER, false, 0, DB>;
+  if (n_uops <= 64) return (const void*)interp_kernel<TIER, true, 1>;
+  if (n_uops <= 256) return (const void*)interp_kernel<TIER, true, 4>;
+  if (n_uops <= (uint32_t)kMaxLdsUops) return (const void*)interp_kernel<TIER, true, 0>;
+  return (const void*)interp_kernel<TIER, false, 0>;
 }
 
 
 
 // Programs that run on tile_kernel (kKindLoop always does).
 static bool tile_kernel_for(int kind, uint32_t n_uops) {
-  return kind == kKindLoop || (kind == kKindDag && n_uops <= kTileMaxUops && !g_no_tile);
+  return kind == kKindLoop || (kind == kKindDag && n_uops <= kTileMaxUops);
 }
 
 // The tile kernel's lean variant serves the fixed-slot stride layout without image output.
 static bool fixed_layout(const LaunchArgs* a) {
-  return g_fixed && a && a->offsets == nullptr && a->lens == nullptr && a->mem_out == nullptr &&
+  return a && a->offsets == nullptr && a->lens == nullptr && a->mem_out == nullptr &&
          a->stride >= (uint64_t)kWin && (((uintptr_t)a->frames | (uintptr_t)a->stride) & 15) == 0;
 }
 
-bool launch_fixed_layout(const LaunchArgs& a) { return fixed_layout(&a) && !g_no_tile; }
+bool launch_fixed_layout(const LaunchArgs& a) { return fixed_layout(&a); }
 
 // The compiled fixed-slot kernel keeps tile indices and tile byte offsets in 32-bit scalars.
 static bool jit_fixed_layout(const LaunchArgs* a) {
@@ -2209,16 +2101,9 @@ static const void* kernel_for(int kind, uint32_t n_uops, const LaunchArgs* a = n
     return n_uops > 64 ? (const void*)dag_kernel<4> : (const void*)dag_kernel<1>;
   }
   if (kind == kKindLoop) return (const void*)tile_kernel<false, true>;
-  if (kind == kKindTier1) return variant<1, false>(n_uops);
-  return g_db ? variant<0, true>(n_uops) : variant<0, false>(n_uops);
+  if (kind == kKindTier1) return variant<1>(n_uops);
+  return variant<0>(n_uops);
 }
-
-// Grid policy override for A/B runs: EBPFEMU_GRID=balanced|full|tiles (default: per program).
-static int g_grid = [] {
-  const char* e = getenv("EBPFEMU_GRID");
-  if (!e) return -1;
-  return e[0] == 'f' ? 1 : e[0] == 't' ? 2 : 0;
-}();
 
 int interp_grid(int kind, uint32_t n_uops, bool tiny, uint64_t n_tiles, int* grid_out) {
   int dev = 0, cus = 256, per_cu = 1;
@@ -2247,8 +2132,7 @@ int interp_grid(int kind, uint32_t n_uops, bool tiny, uint64_t n_tiles, int* gri
   const uint64_t tiles = n_tiles ? n_tiles : 1;
   uint64_t waves;
   // tile_kernel: balanced persistent waves (few workgroups: cheap in-kernel counter fold)
-  const int policy = g_grid >= 0 ? g_grid
-                     : kind == kKindLoop ? 2  // divergent tiles: one per wave
+  const int policy = kind == kKindLoop ? 2  // divergent tiles: one per wave
                      : kind == kKindTier1 || tile_kernel_for(kind, n_uops) ? 0
                      : tiny ? 1 : 2;
   if (policy == 1) {
@@ -2315,18 +2199,14 @@ static bool jit_forward_for(int kind, uint32_t n_uops) {
 // The var tile loop (ebpf_tile_jit_varl) takes a compiled forward program's var-kernel batches:
 // offsets (4-byte aligned) or 16-byte aligned slots of >= 64 bytes, lengths 4-byte aligned or
 // absent, no final images, tile indices in 31 bits (store-mode programs with their deopt list
-// included). EBPFEMU_VARL=0 keeps ebpf_tile_jit_var (A/B).
-static bool g_varl = [] {
-  const char* e = getenv("EBPFEMU_VARL");
-  return !(e && e[0] == '0');
-}();
+// included).
 static bool varl_ok(int kind, const LaunchArgs& a, const JitFns* jit, bool stack) {
   const bool layout = a.offsets ? ((uintptr_t)a.offsets & 3) == 0
                                 : a.stride >= (uint64_t)kWin && a.stride < (1ull << 26) &&
                                       (((uintptr_t)a.frames | (uintptr_t)a.stride) & 15) == 0;
   // (the fixed-slot layout's programs keep ebpf_tile_jit_fixed; store-mode programs, which run
   // on the var kernels only, are stack-window programs)
-  return g_varl && jit && jit->varl && kind == kKindDag && jit_forward_for(kind, a.n_uops) &&
+  return jit && jit->varl && kind == kKindDag && jit_forward_for(kind, a.n_uops) &&
          layout && ((uintptr_t)a.lens & 3) == 0 && !a.mem_out && !a.perm &&
          a.n_tiles < (1ull << 31) && (!jit_fixed_layout(&a) || jit->var_only) &&
          (!jit->var_only || stack);
@@ -2347,51 +2227,17 @@ int launch_kernel_id(int kind, const LaunchArgs& a, const JitFns* jit, bool stac
   return kind == kKindTier1 ? EBPF_KERNEL_GENERAL_T1 : EBPF_KERNEL_GENERAL_T0;
 }
 
-// The compiled loop kernel's grid (A/B): EBPFEMU_LOOP_GRID=persist -- balanced persistent waves
-// at the kernel's own occupancy (each wave a run of tiles, one counter flush per wave) instead of
-// one tile per wave.
-static bool g_var_grid = [] {
-  const char* e = getenv("EBPFEMU_VAR_GRID");
-  return !(e && e[0] == 't');
-}();
-// A/B, opt-in: EBPFEMU_VAR_DB=1 (measured slower: the windows' second buffer halves the waves
-// per CU; profiles/r03_ab_var_db.json)
-static bool g_var_db = [] {
-  const char* e = getenv("EBPFEMU_VAR_DB");
-  return e && e[0] == '1';
-}();
-static bool g_fixed_late = [] {  // A/B: EBPFEMU_FIXED_EARLY=0
-  const char* e = getenv("EBPFEMU_FIXED_EARLY");
-  return e && e[0] == '0';
-}();
-static bool g_var_pipe_host = [] {
-  const char* e = getenv("EBPFEMU_VAR_PIPE");
-  return !(e && e[0] == '0');
-}();
-static bool g_loop_pipe = [] {  // A/B: EBPFEMU_LOOP_PIPE=0
-  const char* e = getenv("EBPFEMU_LOOP_PIPE");
-  return !(e && e[0] == '0');
-}();
-static int g_loop_grid = [] {
-  const char* e = getenv("EBPFEMU_LOOP_GRID");
-  return e ? (e[0] == 'p' ? 1 : 0) : -1;
-}();
-
 hipError_t launch_interp(int kind, const LaunchArgs& a, int grid, hipStream_t stream,
                          const JitFns* jit, bool stack) {
   const uint32_t lds = lds_bytes_for(kind, a.n_uops, jit && jit->loop);
-  if (jit && jit->loop && kind == kKindLoop && g_loop_grid == 1)
-    grid = jit_grid(stack ? jit->loop_stack : jit->loop, lds, a.n_tiles);
   // the compiled var kernels: balanced persistent waves at their own occupancy (interp_grid sizes
-  // for tile_kernel's, which is higher: its extra workgroups would run in a second round);
-  // EBPFEMU_VAR_GRID=tile keeps tile_kernel's grid (A/B)
+  // for tile_kernel's, which is higher: its extra workgroups would run in a second round)
   const bool var = jit && jit->fixed && kind != kKindLoop && jit_forward_for(kind, a.n_uops) &&
                    (!jit_fixed_layout(&a) || jit->var_only);
-  const bool vdb = g_var_db && g_var_pipe_host;
-  const uint32_t vlds = g_lds_pad + kWavesPerBlock * (vdb ? kVarWaveLdsDb3 : kVarWaveLds);
-  if (var && (g_var_grid || vdb)) grid = jit_grid(stack ? jit->var_stack : jit->var, vlds, a.n_tiles);
+  const uint32_t vlds = kWavesPerBlock * kVarWaveLds;
+  if (var) grid = jit_grid(stack ? jit->var_stack : jit->var, vlds, a.n_tiles);
   const bool vl = varl_ok(kind, a, jit, stack);
-  const uint32_t llds = g_lds_pad + kWavesPerBlock * kVarlWaveLds;
+  const uint32_t llds = kWavesPerBlock * kVarlWaveLds;
   if (vl) {
     grid = jit_grid(stack ? jit->varl_stack : jit->varl, llds, a.n_tiles);
     // (tests: EBPFEMU_VARL_WGS caps the workgroups, so a moderate batch gives each wave more than
@@ -2400,9 +2246,6 @@ hipError_t launch_interp(int kind, const LaunchArgs& a, int grid, hipStream_t st
     if (cap && atoi(cap) > 0 && atoi(cap) < grid) grid = atoi(cap);
   }
   LaunchArgs b = a;
-  b.var_nopipe = (kind == kKindLoop ? g_loop_pipe : g_var_pipe_host) ? 0u : 1u;
-  b.var_db = var && vdb ? 1u : 0u;
-  b.fixed_late = g_fixed_late ? 1u : 0u;
   // a shard word's sum must stay below 2^48: bound it by packets x steps per packet; and its
   // arrival count (16 bits) must reach the shard's workgroups - 1: at most 65535 members (the
   // compiled fixed-slot kernel's grid is one workgroup per CU, every other grid is `grid`)
@@ -2410,9 +2253,8 @@ hipError_t launch_interp(int kind, const LaunchArgs& a, int grid, hipStream_t st
   const uint64_t members = ((uint64_t)grid + kCounterShards - 1) / kCounterShards;
   const bool fits = a.n < (1ull << 40) && steps < (1ull << 47) / (a.n + 1) &&
                     members < (1ull << (64 - kShardCountShift));
-  const bool fold_kernel = g_fold_mode >= 0 ? (g_fold_mode == 1 || !fits) : !fits;
+  const bool fold_kernel = g_fold_kernel || !fits;
   b.fold_kernel = fold_kernel ? 1u : 0u;
-  if (g_fold_mode == 2) b.fold_kernel = 2u;  // (A/B: EBPFEMU_FOLD=d, straight to the counters)
   void* bargs[] = {(void*)&b};
   hipError_t e;
   if (jit && jit->loop && kind == kKindLoop) {  // the compiled loop program
@@ -2423,7 +2265,7 @@ hipError_t launch_interp(int kind, const LaunchArgs& a, int grid, hipStream_t st
                               stream, bargs, nullptr);
   } else if (jit && jit->fixed && jit_forward_for(kind, a.n_uops)) {
     if (jit_fixed_layout(&a) && !jit->var_only) {  // double-buffered windows: its own LDS size and grid
-      const uint32_t dlds = g_lds_pad + kDbWaves * kTileWaveLdsDb;
+      const uint32_t dlds = kDbWaves * kTileWaveLdsDb;
       e = hipModuleLaunchKernel(jit->fixed, jit_grid(jit->fixed, dlds, a.n_tiles, kDbBlock), 1, 1,
                                 kDbBlock, 1, 1, dlds, stream, bargs, nullptr);
     } else {  // (the tile kernel's window LDS + a second metadata buffer, also for programs

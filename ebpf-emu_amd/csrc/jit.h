@@ -75,7 +75,7 @@ bool jit_compile(const std::vector<Uop>& uops, const std::vector<TUop>& t,
 
 // Loop programs (back edges, or budgets that can bind; tile tables of build_tile: `t` the block
 // table, `tx` the exact one-micro-op-per-block table) for ebpf_tile_jit_loop. *deep (if given):
-// the code went into ebpf_tile_jit_loop_deep instead (refills prefetching pf_depth() windows).
+// the code went into ebpf_tile_jit_loop_deep instead (a loop with a cooperative byte sum).
 // guard_k > 0 (a stack-slot promoted program, host.cpp promote_slots): every packet load must be
 // a one-byte load proven inside the packet (prove_loads; else the compile fails), and lanes whose
 // packet reaches the window (LEN > r10 - guard_k) deoptimize at the start (jit.h kStDeopt).
@@ -87,7 +87,6 @@ bool jit_compile_loop(const std::vector<Uop>& uops, const std::vector<TUop>& t,
 
 // Windows the refills of byte-scanning loop programs prefetch ahead: 1 (ebpf_tile_jit_loop, 5
 // waves per SIMD) or 2-3 (ebpf_tile_jit_loop_deep, 4 waves); EBPFEMU_PF_DEPTH overrides.
-int pf_depth();
 
 // Loads a code object on the current device (the functions it does not hold stay null).
 bool jit_load(const std::vector<char>& code_object, hipModule_t* mod, JitFns* fns);

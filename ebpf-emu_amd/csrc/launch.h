@@ -77,12 +77,6 @@ struct LaunchArgs {
                               //   [u32 data = 8][u32 data_end = 8 + len][packet]; the window is
                               //   shifted by 8 bytes in LDS and the ctx synthesised per lane, BASE
                               //   = packet - 8 and LEN = 8 + len (no staging copy)
-  uint32_t var_nopipe;        // A/B (EBPFEMU_VAR_PIPE=0): the compiled var kernels fetch each tile's
-                              //   metadata and then its windows, no metadata prefetch
-  uint32_t var_db;            // the compiled var kernels: double-buffered windows, the next tile's
-                              //   windows in flight while a tile runs (A/B, EBPFEMU_VAR_DB=1)
-  uint32_t fixed_late;        // A/B (EBPFEMU_FIXED_EARLY=0): the compiled fixed-slot kernel issues
-                              //   its first tile's windows after the workgroup's start barrier
   // store-mode programs (jit.h StackPlan::any_dyn): the deopt list in the workspace -- u32
   // [count, done] at kWsDeoptOff (zero between batches), idx[n] past the tier-1 slots. The
   // compiled kernel appends the packet index of every lane that deoptimized (status kStDeopt: no

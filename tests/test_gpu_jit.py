@@ -475,26 +475,3 @@ def test_tile_loop_reentry(cuda, monkeypatch):
         prog.close()
 
 
-@pytest.mark.parametrize("depth", [2, 3, "pair"])
-def test_deep_prefetch_compiles(monkeypatch, depth):
-    """(CPU) With EBPFEMU_PF_DEPTH = 2, 3 the prefetching loop programs go to the deep kernel's
-    statement; stack-window loops and programs with wider loads keep ebpf_tile_jit_loop."""
-    from ebpf_emu import Program
-    from ebpf_emu import workloads as W
-    from ebpf_emu.asm import assemble
-
-    monkeypatch.setenv("EBPFEMU_PF_DEPTH", str(depth))
-    from test_gpu_loops import DEEP_SCANS
-
-    for src in [W.CHECKSUM] + DEEP_SCANS:
-        p = Program(assemble(src))
-        assert p.compile()
-        text = p.jit_asm(2)
-        assert "global_load_dwordx4 v[72:75]" in text
-        assert ("s_waitcnt vmcnt(1)" if depth == "pair" else f"s_waitcnt vmcnt({4 * (depth - 1)})") in text
-        p.close()
-    for name in ("checksum_stack",):
-        p = Program(W.program(name))
-        assert p.compile()
-        assert "global_load_dwordx4 v[72:75]" not in p.jit_asm(2)
-        p.close()

@@ -549,9 +549,9 @@ def test_counted_loop_passes(cuda, oracle_mod, seed):
                                        max_steps=100000, tag=f"seed {seed} it {it} {layout}")
 
 
-# Byte scans for the deep refill prefetch (jit.cpp refill_deep): sequential windows (lockstep
-# lanes hit their prefetched stage), strides that skip windows (every refill a miss: the window
-# loaded directly, the stages refilled), a backward scan, and lengths that differ per lane.
+# Byte scans for the refill prefetch (jit.cpp refill_prefetch): sequential windows (lockstep
+# lanes hit their prefetched window), strides that skip windows (every refill a miss: the window
+# loaded directly), a backward scan, and lengths that differ per lane.
 DEEP_SCANS = [FORWARD_SUM] + [FORWARD_SUM.replace("add r3, 1", f"add r3, {s}") for s in (5, 64, 100, 130)] + [
     """
     mov r0, 0
@@ -570,25 +570,23 @@ done:
 """]
 
 
-@pytest.mark.parametrize("depth", [2, 3, "pair"])
-def test_deep_prefetch(cuda, oracle_mod, monkeypatch, depth):
-    """The loop kernel whose refills prefetch 2 or 3 windows ahead (EBPFEMU_PF_DEPTH,
-    ebpf_tile_jit_loop_deep): the checksum and byte scans with window-skipping strides, a backward
-    scan and per-lane lengths, binned and unbinned batches, fixed and offsets layouts --
-    compiled == general interpreter == oracle."""
+def test_prefetch_scans(cuda, oracle_mod):
+    """The refill prefetch over the checksum and byte scans with window-skipping strides, a
+    backward scan and per-lane lengths, binned and unbinned batches, two alignments of the
+    offsets layout -- compiled == general interpreter == oracle."""
     import numpy as np
 
     from ebpf_emu import Program
     from ebpf_emu import workloads as W
     from ebpf_emu.asm import assemble
 
-    monkeypatch.setenv("EBPFEMU_PF_DEPTH", str(depth))
-    rng = random.Random(zlib.crc32(str(depth).encode()))
+    depth = 1
+    rng = random.Random(zlib.crc32(b"prefetch"))
     for i, src in enumerate([W.CHECKSUM] + DEEP_SCANS):
         img = assemble(src)
         p = Program(img)
         assert p.compile()
-        assert "global_load_dwordx4 v[72:75]" in p.jit_asm(2), src
+        assert "global_load_dwordx4 v[56:59]" in p.jit_asm(2), src
         p.close()
         n = 17000 if i < 2 else 700  # (>= 16384: length-binned order)
         lens = [rng.choice([0, 14, 64, 65, 200, 600, 1500, 1500, 1500, rng.randrange(1501)])
@@ -658,26 +656,16 @@ done:
 }
 
 
-@pytest.mark.parametrize("kernel", ["loop", "deep_strided", "deep2", "deep"])
 @pytest.mark.parametrize("name", sorted(COOP_PROGRAMS))
-def test_coop_byte_sum(cuda, oracle_mod, monkeypatch, name, kernel):
-    """Counted byte-sum loops whose long ranges are summed cooperatively (coop_sum): production
-    and full outputs against the oracle on packets of 0-1500 bytes (lengths around the 128-byte
-    threshold included), aligned and misaligned packet bases, binned and unbinned batches; on the
-    loop kernel (EBPFEMU_NO_COOP_DEEP), on the deep kernel with the strided sum (two rounds of
-    loads in flight) and with the compacted one (the default: coop_sum_compact)."""
+def test_coop_byte_sum(cuda, oracle_mod, name):
+    """Counted byte-sum loops whose long ranges are summed cooperatively (coop_sum_compact on the
+    deep kernel): production and full outputs against the oracle on packets of 0-1500 bytes
+    (lengths around the 128-byte threshold included), aligned and misaligned packet bases, binned
+    and unbinned batches."""
     import numpy as np
 
     from ebpf_emu import Program
     from ebpf_emu.asm import assemble
-
-    if kernel == "loop":
-        monkeypatch.setenv("EBPFEMU_NO_COOP_DEEP", "1")
-    elif kernel == "deep_strided":
-        monkeypatch.setenv("EBPFEMU_LOOP_DEEP", "1")
-        monkeypatch.setenv("EBPFEMU_COOP_STRIDED", "1")
-    elif kernel == "deep2":  # (two rounds of loads in flight instead of three)
-        monkeypatch.setenv("EBPFEMU_COOP_DEPTH", "2")
 
     img = assemble(COOP_PROGRAMS[name])
     p = Program(img)
@@ -687,7 +675,7 @@ def test_coop_byte_sum(cuda, oracle_mod, monkeypatch, name, kernel):
     p.close()
     if name != "offset":
         assert coop, name
-        assert ("coop_sum_compact" in a) == (kernel in ("deep", "deep2")), (name, kernel)
+        assert "coop_sum_compact" in a, name
     rng = random.Random(zlib.crc32(name.encode()))
     for n in (700, 17000):
         lens = [rng.choice([0, 1, 127, 128, 129, 130, 143, 144, 200, 1500, 1500, rng.randrange(1501)])

@@ -12,6 +12,8 @@ Variants (each: synchronize, t0, K launches, the variant's end sequence, synchro
             step's stream, the other stream waits on it after the first launch; join as cur)
   fast      nojoin with a pre-bound ctypes call per step (no per-call argument conversion)
   fastnw    fast + nowait
+  last0nw   last0 without the start wait
+  last0s3   last0 on three streams
 Prints the median wall and event us per step and the fixed part (wall - event) x K per variant.
 """
 import ctypes
@@ -34,6 +36,7 @@ def main():
     K = int(os.environ.get("K", "20"))
     reps = int(os.environ.get("REPS", "60"))
     modes = os.environ.get("MODES", "cur,nojoin,nowait,last0,fast,fastnw").split(",")
+    S = 3 if any(m.endswith("s3") for m in modes) else 2
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     n = 1 << 20
@@ -41,8 +44,7 @@ def main():
     prog.upload(0)
     batches = [torch.from_numpy(W.frames_fixed(n, 64, 3 + 100 * k)).to(dev) for k in range(8)]
     descs = [prog.make_batch(b, n=n, stride=64) for b in batches]
-    S = 2
-    streams = [torch.cuda.current_stream(dev), torch.cuda.Stream(dev)]
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
     ws_bytes = prog.workspace_bytes(descs[0], 0)
     counters = torch.zeros(8, dtype=torch.int64, device=dev)
     sd, outs, keep = [], [], []
@@ -79,10 +81,11 @@ def main():
     def run(mode):
         fast = mode.startswith("fast")
         step = step_fast if fast else step_slow
-        wait = mode not in ("nowait", "fastnw")
-        join = mode in ("cur", "last0")
-        rot = mode == "last0"
-        sof = (lambda i: (K - 1 - i) % S) if rot else (lambda i: i % S)
+        wait = mode not in ("nowait", "fastnw", "last0nw")
+        join = mode in ("cur", "last0", "last0nw", "last0s3")
+        rot = mode.startswith("last0")
+        SS = 3 if mode.endswith("s3") else 2
+        sof = (lambda i: (K - 1 - i) % SS) if rot else (lambda i: i % SS)
         first = sof(0)
         ev0 = torch.cuda.Event(enable_timing=True)
         ends = [torch.cuda.Event(enable_timing=True) for _ in range(S)]
@@ -91,13 +94,13 @@ def main():
         ev0.record(streams[first])
         for i in range(K):
             if i == 1 and wait:
-                for si in range(S):
+                for si in range(SS):
                     if si != first:
                         streams[si].wait_event(ev0)
             step(i, sof(i))
         last = sof(K - 1)
         if join:
-            for si in range(S):
+            for si in range(SS):
                 if si != last:
                     ej = torch.cuda.Event()
                     ej.record(streams[si])
@@ -105,16 +108,16 @@ def main():
             ends[0].record(streams[last])
             used = [ends[0]]
         else:
-            for si in range(S):
+            for si in range(SS):
                 ends[si].record(streams[si])
-            used = ends
+            used = ends[:SS]
         torch.cuda.synchronize(dev)
         t1 = time.perf_counter()
         ev = max(ev0.elapsed_time(e) for e in used) * 1e3
         return (t1 - t0) * 1e6, ev
 
     for i in range(40):
-        step_slow(i, i % S)
+        step_slow(i, i % 2)
     torch.cuda.synchronize(dev)
     res = {m: [] for m in modes}
     for r in range(reps):
