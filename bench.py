@@ -82,11 +82,16 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", choices=sorted(CONFIGS), default="5tuple")
     ap.add_argument("--packets", type=int, default=1 << 20, help="packets per batch per GPU")
-    ap.add_argument("--layout", choices=["fixed", "offsets"], default="fixed",
-                    help="64-byte-frame configs: fixed slots (a NIC ring), or the same frames as an "
-                         "offsets + lens batch (a pcap capture's layout: the var kernels)")
+    ap.add_argument("--layout", choices=["fixed", "offsets", "pcap"], default="fixed",
+                    help="64-byte-frame configs: fixed slots (a NIC ring), the same frames as an "
+                         "offsets + lens batch at 64-byte slots (the var kernels), or as a classic "
+                         "pcap capture (24-byte file header, a 16-byte record header before each "
+                         "frame: records at 8 mod 16) indexed in place by ebpf_pcap_index")
     ap.add_argument("--frame-bytes", type=int, default=64,
                     help="fixed-slot configs: bytes per frame slot (rounded up to 16; e.g. 1500)")
+    ap.add_argument("--long-options", type=int, default=0,
+                    help="64-byte-frame configs: every Nth frame's IPv4 IHL set to 15 (options up "
+                         "to byte 74: the NAT's port store past the 64-byte header window)")
     ap.add_argument("--total-packets", type=int, default=0,
                     help="strong scaling: one global batch of this many packets (BASELINE config 4"
                          " = 100000000), sharded over the ranks in seeded 1Mi-packet chunks")
@@ -327,8 +332,11 @@ def main():
         cfg_idx = 3 if args.config == "5tuple" else cfg_idx
     if args.frame_bytes != 64 and args.config != "checksum":
         desc = desc.replace("64B frames", f"{(max(64, args.frame_bytes) + 15) // 16 * 16}B frame slots")
-    if args.layout == "offsets":
-        desc += " (offsets + lens batch)"
+    if args.long_options:
+        desc += f" (every {args.long_options}th frame with IHL 15)"
+    if args.layout != "fixed":
+        desc += " (offsets + lens batch)" if args.layout == "offsets" else \
+            " (a pcap capture indexed in place: offsets + lens into the capture)"
         assert not args.total_packets and args.config not in ("checksum", "checksum_stack", "checksum_xdp")
     n = args.packets
     img = W.program(PROGRAM_OF.get(args.config, args.config))
@@ -369,20 +377,34 @@ def main():
             floor_bytes = line_floor_bytes(offs.astype(np.int64), lens.astype(np.int64)) + n * (4 + 2 + 1)
         elif fb == 64 or k == 0:
             buf = W.frames_fixed(n, fb, cid)
+            if args.long_options:
+                v = buf.reshape(n, fb)
+                v[::args.long_options, 14] = (v[::args.long_options, 14] & 0xF0) | 0x0F
             batches.append(dict(frames=torch.from_numpy(buf).to(dev)))
             if args.layout == "offsets":  # the same frames through u32 offsets + u16 lengths
                 batches[-1]["offsets"] = torch.from_numpy(
                     (np.arange(n, dtype=np.int64) * fb).astype(np.uint32).view(np.int32)).to(dev)
                 batches[-1]["lens"] = torch.from_numpy(np.full(n, fb, dtype=np.int16)).to(dev)
+            elif args.layout == "pcap":  # the same frames as a capture, indexed in place
+                cap = pcap_capture(buf.reshape(n, fb))
+                from ebpf_emu import pcap as PC
+
+                offs, lens, _ = PC.index(cap)
+                assert len(offs) == n and (lens == fb).all()
+                batches[-1] = dict(frames=torch.from_numpy(cap).to(dev),
+                                   offsets=torch.from_numpy(offs.view(np.int32)).to(dev),
+                                   lens=torch.from_numpy(lens.view(np.int16)).to(dev))
             # a header program's algorithmic bytes are its packet's 64-byte header
             # window + the verdict byte (+ offset and length) = 65 B per 64-byte frame. The floor
             # is what HBM must move for them: the 128-byte lines the bytes the launch reads touch
             # (on fixed slots only the 16-byte chunks the program's loads reach, jit.cpp
             # window_chunks: 16 for drop-all, all 64 with a register-address load)
             wb = prog.window_bytes if args.layout == "fixed" and not args.generic else 64
-            meta = 6 if args.layout == "offsets" else 0
+            meta = 6 if args.layout != "fixed" else 0
             algo_bytes = n * (64 + 1 + meta)
-            st = np.arange(n, dtype=np.int64) * fb
+            # (a capture's records: 16-byte record headers between the frames)
+            st = np.arange(n, dtype=np.int64) * ((fb + 16) if args.layout == "pcap" else fb) + \
+                (40 if args.layout == "pcap" else 0)
             floor_bytes = line_floor_bytes(st, np.full(n, wb, dtype=np.int64)) + n * (1 + meta)
         else:  # large slots: copies of the first batch at other addresses (host RNG is slow)
             batches.append(dict(frames=batches[0]["frames"].clone()))
@@ -412,7 +434,9 @@ def main():
     # (counter shards, zeroed once) and verdict buffer; every launch adds into the one counters
     # array (the library's fold is an atomic add). Stream 0 is the current stream.
     S = max(1, args.streams)
-    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
+    _order = os.environ.get("BENCH_ORDER", "last0")  # (A/B, temporary: old | last0 | side)
+    streams = ([torch.cuda.Stream(dev) for _ in range(S)] if _order == "side" else
+               [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)])
     ws_bytes = max(prog.workspace_bytes(bd, local) for bd in descs)
     verdicts = [verdict] + [torch.empty_like(verdict) for _ in range(S - 1)]
     workspaces, sdescs, outs = [], [], []
@@ -439,7 +463,7 @@ def main():
     # queue, which measured 11 us more per run (tools/fixed_cost_ab.py "cur" vs "last0":
     # profiles/r05_fixed_cost_ab.json)
     def sof(i, k):
-        return (k - 1 - i) % S
+        return i % S if _order == "old" else (k - 1 - i) % S
 
     def step(i, k=None):
         si = sof(i, k if k is not None else S)
@@ -482,11 +506,13 @@ def main():
                     streams[si].wait_event(ev0)
         step(i, K)
     t_enq = time.perf_counter() - t0  # host time to enqueue the K steps (launch-bound check)
-    for si in range(1, S):  # stream 0 (the last step's) joins the others before the end event
-        ej = torch.cuda.Event()
-        ej.record(streams[si])
-        stream.wait_event(ej)
-    ev1.record(stream)
+    last = sof(K - 1, K)
+    for si in range(S):  # the last step's stream joins the others before the end event
+        if si != last:
+            ej = torch.cuda.Event()
+            ej.record(streams[si])
+            streams[last].wait_event(ej)
+    ev1.record(streams[last])
     if use_dist:  # the one exchange step: per-verdict counters, RCCL / xGMI
         all_reduce(counters)
     torch.cuda.synchronize(dev)
@@ -518,7 +544,9 @@ def main():
                                      cnt, want)
                 pinned = "tests/golden/config4.json: counters == steps x fixture"
     pin_note = None
-    if not args.total_packets and not args.no_counters:
+    if args.long_options:
+        pin_note = "frames modified by --long-options: no fixture"
+    elif not args.total_packets and not args.no_counters:
         # parity of the timed weak-scaling work at any rank count: the global counters of the K
         # steps equal the oracle's counters of the chunks every rank timed (checked after timing)
         want, src = pin_weak(PROGRAM_OF.get(args.config, args.config), mixed, fb, n, world,
@@ -554,7 +582,7 @@ def main():
     # SQ_INSTS_VALU), collected by tools/pmc.sh into the committed summary
     traffic = None
     issue = None
-    suffix = ("" if mixed or fb == 64 else f"_{fb}B") + ("_offsets" if args.layout == "offsets" else "")
+    suffix = ("" if mixed or fb == 64 else f"_{fb}B") + ("" if args.layout == "fixed" else f"_{args.layout}")
     pj = args.pmc_json or os.path.join(ROOT, "profiles", f"pmc_{args.config}{suffix}.json")
     pmc_note = None
     if os.path.exists(pj) and not args.total_packets and n == 1 << 20 and not args.generic:
@@ -672,6 +700,25 @@ def main():
         dist.destroy_process_group()
 
 
+def pcap_capture(frames):
+    """A classic little-endian pcap capture (pcap.to_bytes's format, ebpf_emu/pcap.py) of the rows
+    of `frames` (u8[n][L]), built with numpy: 24-byte file header, then per frame a 16-byte record
+    header (ts = the record index, incl_len = orig_len = L) and the frame."""
+    import struct
+
+    import numpy as np
+
+    n, L = frames.shape
+    rec = np.zeros((n, 16 + L), dtype=np.uint8)
+    hdr = rec[:, :16].view(np.uint32)
+    hdr[:, 0] = np.arange(n, dtype=np.uint32)
+    hdr[:, 2] = L
+    hdr[:, 3] = L
+    rec[:, 16:] = frames
+    head = np.frombuffer(struct.pack("<IHHiIII", 0xA1B2C3D4, 2, 4, 0, 0, 65535, 1), dtype=np.uint8)
+    return np.concatenate([head, rec.reshape(-1)])
+
+
 def line_floor_bytes(starts, lengths, line=128):
     """Bytes of the distinct 128-byte HBM lines that byte ranges [start, start + length) touch
     (the MI355X L2 line: a read of any byte of a line moves the line)."""
@@ -726,7 +773,8 @@ def cpu_baseline(args, img, batch0, mixed, n, mem_size, r10):
     threads = args.cpu_threads or usable
     op = oracle.Program(img)
     frames = batch0["frames"].cpu().numpy()
-    if mixed:
+    indexed = "offsets" in batch0  # (mixed frames, or the offsets / pcap layouts)
+    if indexed:
         offs = batch0["offsets"].cpu().numpy().view(np.uint32)
         lens = batch0["lens"].cpu().numpy().view(np.uint16)
     stride = (max(64, args.frame_bytes) + 15) // 16 * 16
@@ -741,7 +789,7 @@ def cpu_baseline(args, img, batch0, mixed, n, mem_size, r10):
         while time.perf_counter() - t0 < seconds:
             lo = done % n
             hi = min(n, lo + chunk)
-            if mixed:
+            if indexed:
                 op.run_batch(frames, hi - lo, offsets=offs[lo:hi], lens=lens[lo:hi], **kw)
             else:
                 op.run_batch(frames[lo * stride:hi * stride], hi - lo, stride=stride, **kw)

@@ -1509,6 +1509,65 @@ v_cmp_lt_u32_e64 {masks[r]}, %[c16], {{t{8 + r}}}""" for r in range(4))
 s_add_u32 {{T7L}}, {{T7L}}, %[s16]
 s_addc_u32 {{T7H}}, {{T7H}}, 0""" for r in range(4))
     smasks = "\n".join(f"v_cmp_lt_u32_e64 {masks[r]}, %[c16], {{t{8 + r}}}" for r in range(4))
+    # a tile whose packets are not all 16-byte aligned (a capture's records: 24 + 16 + sum of the
+    # earlier records) is DMA'd from 16-byte aligned sources: round r's lane moves chunk c of
+    # (packet & ~15), so a window holds packet bytes [-m, 64 - m) (m = packet & 15; the chunk
+    # has packet bytes if 16 c < len + m), and each lane whose packet reaches past them loads the
+    # 16 bytes after (its packet's [64 - m, 80 - m)) into v[56:59]; at that tile's top the lanes
+    # with m != 0 shift their window by m in LDS (realign) before the program reads it.
+    mrounds = "\n".join(f"""v_add_u32 {{t1}}, %[fr_lo], {{t{12 + 2 * r}}}
+v_and_b32 {{t1}}, 15, {{t1}}
+v_add_u32 {{t{8 + r}}}, {{t{8 + r}}}, {{t1}}""" for r in range(4)) + "\n" + rounds + "\n" + \
+        "\n".join(f"v_and_b32 {{t{12 + 2 * r}}}, -16, {{t{12 + 2 * r}}}" for r in range(4))
+    d = [f"v{36 + k}" for k in range(16)] + ["v56", "v57", "v58", "v59"]  # the 20 dwords read
+    chunk_rd = "\n".join(f"v_xad_u32 {{t18}}, %[swz], {16 * c}, {{t17}}\n"
+                          f"ds_read_b128 v[{36 + 4 * c}:{39 + 4 * c}], {{t18}}" for c in range(4))
+    chunk_wr = "\n".join(f"v_xad_u32 {{t18}}, %[swz], {16 * c}, {{t17}}\n"
+                          f"ds_write_b128 {{t18}}, v[{36 + 4 * c}:{39 + 4 * c}]" for c in range(4))
+    # uniform dword shift q (every realigned lane's m >> 2 the same: records of one size) -- one
+    # v_alignbyte per dword; else a select network (q per lane) first, then the byte shift
+    uni = "\n".join(f".Lrq{q}%=:\n" + "\n".join(
+        f"v_alignbyte_b32 {d[j]}, {d[j + q + 1]}, {d[j + q]}, {{t16}}" for j in range(16)) +
+        "\ns_branch .Lraw%=" for q in range(4))
+    sel = "\n".join(
+        "\n".join(f"v_cndmask_b32_e64 {d[k]}, {d[k]}, {d[k + i]}, {m}"
+                   for i, m in ((1, "{T1}"), (2, "{T4}"), (3, "{T5}")) if k + i < 20)
+        for k in range(17)) + "\n" + "\n".join(
+        f"v_alignbyte_b32 {d[j]}, {d[j + 1]}, {d[j]}, {{t16}}" for j in range(16))
+    realign = f"""; this tile's windows came from 16-byte aligned sources: shift the lanes with m != 0
+s_bitcmp1_b32 %[mis], 0
+s_cbranch_scc0 .Lrad%=
+v_and_b32 {{t16}}, 15, {{BASEL}}
+v_cmp_ne_u32 vcc, 0, {{t16}}
+s_and_b64 vcc, vcc, {{VM}}
+s_cbranch_vccz .Lrad%=
+s_mov_b64 exec, vcc
+v_add_u32 {{t17}}, %[winb], %[lane64]
+{chunk_rd}
+v_lshrrev_b32 {{t19}}, 2, {{t16}}
+v_readfirstlane_b32 {{T3}}, {{t19}}
+v_cmp_ne_u32 vcc, {{T3}}, {{t19}}
+s_and_b64 vcc, vcc, exec
+s_waitcnt lgkmcnt(0)
+s_cbranch_vccnz .Lrqv%=
+s_cmp_eq_u32 {{T3}}, 0
+s_cbranch_scc1 .Lrq0%=
+s_cmp_eq_u32 {{T3}}, 1
+s_cbranch_scc1 .Lrq1%=
+s_cmp_eq_u32 {{T3}}, 2
+s_cbranch_scc1 .Lrq2%=
+s_branch .Lrq3%=
+{uni}
+.Lrqv%=:
+v_cmp_eq_u32_e64 {{T1}}, 1, {{t19}}
+v_cmp_eq_u32_e64 {{T4}}, 2, {{t19}}
+v_cmp_eq_u32_e64 {{T5}}, 3, {{t19}}
+{sel}
+.Lraw%=:
+{chunk_wr}
+s_mov_b64 exec, -1
+s_mov_b64 vcc, {{VM}}
+.Lrad%=:"""
     dmas = "\n".join(f"""s_mov_b64 exec, {masks[r]}
 s_add_u32 m0, %[nwinb], {1024 * r}
 s_nop 0
@@ -1517,6 +1576,7 @@ global_load_lds_dwordx4 {{T{12 + 2 * r}{13 + 2 * r}}}, off ; @DMAPOLICY@""" for 
     main = """s_mov_b32 {M0S}, m0
 s_movk_i32 %[cdn], 511
 s_mov_b32 %[stage], 0
+s_mov_b32 %[mis], 0
 .Lloop%=:
 ; this tile's windows and the next tile's metadata: landed
 s_waitcnt vmcnt(0)
@@ -1549,6 +1609,7 @@ s_mul_i32 {T5L}, %[tile], %[tbytes]
 s_mul_hi_u32 {T5H}, %[tile], %[tbytes]
 v_lshl_add_u64 {BASE}, %[lb], 0, {T5}
 .Lsbd%=:
+""" + realign + """
 s_bitcmp1_b32 %[fl], 7
 s_cbranch_scc0 .Lnx%=
 v_min_u32 {LEN}, 0xffff, {LEN}
@@ -1589,14 +1650,36 @@ v_mov_b32 {t10}, %[lenc]
 v_mov_b32 {t11}, %[lenc]
 .Lnl2d%=:
 s_waitcnt lgkmcnt(0)
-; every packet of the next tile 16-byte aligned (lanes of length 0 excepted), else stage it
+; every packet of the next tile 16-byte aligned (lanes of length 0 excepted): DMA'd as they are;
+; else from 16-byte aligned sources and realigned at its top -- or staged by the C++ when this
+; is the statement's last tile (v[56:59] do not survive the return)
 v_add_u32 {t0}, %[fr_lo], {t6}
 v_and_b32 {t0}, 15, {t0}
 v_cmp_ne_u32 vcc, 0, {t0}
 v_cmp_ne_u32_e64 {T0}, 0, {t7}
 s_and_b64 vcc, vcc, {T0}
-s_cbranch_vccnz .Lstg%=
+s_cbranch_vccnz .Lmis%=
 """ + rounds + """
+""" + dmas + """
+s_branch .Lmeta%=
+.Lmis%=:
+s_cmp_eq_u32 %[cdn], 1
+s_cbranch_scc1 .Lstg%=
+s_or_b32 %[mis], %[mis], 2
+; the lane's 16 bytes past its window: its packet's [64 - m, 80 - m), when it reaches them
+v_add_u32 {t1}, {t7}, {t0}
+v_cmp_lt_u32 vcc, 64, {t1}
+v_cmp_ne_u32_e64 {T1}, 0, {t0}
+s_and_b64 exec, vcc, {T1}
+s_cbranch_execz .Lmx%=
+v_mov_b32 {t2}, {t6}
+v_mov_b32 {t3}, 0
+v_lshl_add_u64 {T23}, %[k_frames], 0, {T23}
+v_and_b32 {t2}, -16, {t2}
+global_load_dwordx4 v[56:59], {T23}, off offset:64
+.Lmx%=:
+s_mov_b64 exec, -1
+""" + mrounds + """
 """ + dmas + """
 s_branch .Lmeta%=
 .Lsn%=:
@@ -1680,7 +1763,7 @@ s_cbranch_scc1 .Linitx%=
 ;@@JITINIT@@
 .Linitd%=:
 
-; JIT N=%= fixed=0 loops=0 aligned=%[aligned] xdp=%[xdpf] varl=1
+; JIT N=%= fixed=0 loops=0 aligned=%[aligned] xdp=%[xdpf] ovf=%[k_ovf] tile=%[tile] dm=%[dmask] varl=1
 ;@@JIT@@
 .Ldone%=:
 ; store mode: lanes that left for the general interpreter (status 0x80, jit.h kStDeopt) produce
@@ -1737,6 +1820,7 @@ s_bitcmp1_b32 %[fl], 5
 s_cbranch_scc1 .Lout%=
 .Loutd%=:
 s_mov_b64 exec, -1
+s_lshr_b32 %[mis], %[mis], 1
 s_sub_u32 %[cdn], %[cdn], 1
 s_add_u32 %[tile], %[tile], %[W]
 s_xor_b32 %[winb], %[winb], %[wx]

@@ -1639,6 +1639,8 @@ uint64_t ebpf_workspace_bytes(const ebpf_prog* p, const ebpf_batch* b, int devic
   bytes += align16(tier1_slots_bytes(p, b, device));
   if (p->stack.any_dyn || !p->puops.empty())  // the deopt list's indices (past the slots)
     bytes += align16(b->n * 4);
+  if (p->stack.any_dyn)  // store mode: the overflow images (past the indices)
+    bytes += b->n * 64 + 16;
   return bytes;  // (the xdp_md region, when present, is the last x bytes)
 }
 
@@ -1832,6 +1834,7 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* bin, const ebpf_batch_out* ou
     const uint64_t bin_bytes = a.perm ? b->n * 4 + 4ull * kBinMaxWgs * kBinClasses : 0;
     a.deopt_idx = (uint32_t*)(ws + kWsSlotsOff +
                               align16(std::max<uint64_t>(tier1_slots_bytes(p, b, device), bin_bytes)));
+    if (p->stack.any_dyn) a.ovf = (uint8_t*)a.deopt_idx + align16(b->n * 4);
   }
   hipError_t e = launch_interp(kind, a, grid, s, jit, stk);
   if (deopt && e == hipSuccess) {

@@ -389,13 +389,43 @@ __device__ __forceinline__ void xdp_window(uint8_t* pw, uint32_t swz, uint32_t l
       : "memory");
 }
 
-// Synchronous per-lane staging for tiles whose packet bases are not all 16-byte aligned.
+// The 16-byte aligned source block at a, or zeros when it holds no byte of [src, end): a block
+// holding a packet byte lies in that byte's page, so no load leaves the packet's pages.
+__device__ __forceinline__ u32x4 blk16(uintptr_t a, uintptr_t src, uintptr_t end) {
+  if (a + 16 <= src || a >= end) return u32x4{0u, 0u, 0u, 0u};
+  return *(g_u4*)a;
+}
+
+// Synchronous per-lane staging for tiles whose packet bases are not all 16-byte aligned: the
+// five 16-byte aligned blocks that cover the window's bytes (each only where it holds one of
+// them), funnel-shifted into place (v_alignbyte), bytes at or past min(len, 64) zero. Five load
+// instructions per wave, each over its 64 packets' lines (round 4 read the window as 16
+// bounds-checked dwords, two loads each: 32 such instructions).
 __device__ __forceinline__ void stage_window_lane(uint8_t* pw, uint32_t swz, const uint8_t* base,
                                                   uint32_t len, bool valid) {
   const uint32_t m = valid ? min(len, (uint32_t)kWin) : 0u;
+  const uintptr_t s0 = (uintptr_t)base, end = s0 + m, a0 = s0 & ~(uintptr_t)15;
+  const uint32_t sh = (uint32_t)(s0 & 15), q = sh >> 2;
+  uint32_t d[20];
 #pragma unroll
-  for (uint32_t bo = 0; bo < (uint32_t)kWin; bo += 4)
-    *(uint32_t*)(pw + win_off(bo, swz)) = (bo < m) ? (uint32_t)pkt_read(base, bo, 4, len) : 0u;
+  for (int k = 0; k < 5; k++) {
+    const u32x4 b = m ? blk16(a0 + 16 * k, s0, end) : u32x4{0u, 0u, 0u, 0u};
+    d[4 * k] = b.x, d[4 * k + 1] = b.y, d[4 * k + 2] = b.z, d[4 * k + 3] = b.w;
+  }
+#pragma unroll
+  for (uint32_t c = 0; c < 4; c++) {
+    uint32_t w[4];
+#pragma unroll
+    for (uint32_t e = 0; e < 4; e++) {
+      const uint32_t j = 4 * c + e;  // window dword j = bytes [4j + sh, 4j + sh + 4) of the blocks
+      const uint32_t l0 = (q & 1) ? d[j + 1] : d[j], l1 = (q & 1) ? d[j + 3] : d[j + 2];
+      const uint32_t h0 = (q & 1) ? d[j + 2] : d[j + 1], h1 = (q & 1) ? d[j + 4] : d[j + 3];
+      const uint32_t v = __builtin_amdgcn_alignbyte((q & 2) ? h1 : h0, (q & 2) ? l1 : l0, sh & 3);
+      const uint32_t valid_b = m > 4 * j ? min(m - 4 * j, 4u) : 0u;
+      w[e] = valid_b >= 4 ? v : v & ((1u << (8 * valid_b)) - 1u);
+    }
+    *(uint4*)(pw + win_off(16 * c, swz)) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
 }
 
 // ---- counters ----
@@ -489,8 +519,11 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
   // the deopt pass with an empty list (the usual case): every workgroup leaves at once -- no
   // program staging, no counter flush, nothing to clear (the list cannot grow during the pass)
   if (TIER == 1 && a.deopt_pass &&
-      rfl(__hip_atomic_load(a.deopt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0)
+      rfl(__hip_atomic_load(a.deopt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0) {
+    if (blockIdx.x == 0 && threadIdx.x == 0)  // (deopt[2]: packets the last pass re-ran, tests)
+      __hip_atomic_store(a.deopt + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
+  }
   counters_init();
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t nu = a.n_uops;
@@ -921,6 +954,7 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
     if (threadIdx.x == 0 &&
         __hip_atomic_fetch_add(a.deopt + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
             gridDim.x - 1) {
+      __hip_atomic_store(a.deopt + 2, (uint32_t)n_run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(a.deopt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(a.deopt + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -1330,30 +1364,47 @@ hipError_t launch_binning(const uint16_t* lens, uint64_t n, uint32_t* wgc, uint3
 // [packet bytes] -- the bytes main.rs would be handed for a standard XDP program. One workgroup
 // stages 256 packets: it sizes their 16-byte aligned slots, reserves its range with one device
 // atomic (workgroups pack in arrival order; every packet keeps its index through the offsets),
-// then copies them: images of at most kStageShort bytes one per thread, longer ones one per wave
-// (its lanes on consecutive 16-byte chunks). An image longer than mem_size is not copied: its
-// length alone makes the batch fault it ST_BADPKT (main.rs:20-21).
-constexpr uint32_t kStageShort = 256;
+// then writes the range's 16-byte chunks: thread t the chunks t, t + 256, ... of the range (each
+// mapped to its packet by a binary search over the slot prefix sums in LDS), so consecutive
+// threads store consecutive chunks whatever the packets' lengths. An image longer than mem_size
+// is not copied: its length alone makes the batch fault it ST_BADPKT (main.rs:20-21).
+// (Round 4 copied short images a thread each and long ones a wave each, every chunk from four
+// bounds-checked dword loads: 675 us for a 1 Mi mixed 64/1500-byte batch.)
 
-// Image chunk c (16 bytes at image offset 16c) of a packet of len bytes at src: the ctx {data =
-// 8, data_end = 8 + len} in its first 8 bytes, then packet bytes (pkt_read: aligned dwords that
-// hold a packet byte, never past one; zeros at or past len).
+// Image chunk c (image bytes [16c, 16c + 16)) of a packet of len bytes at src: the ctx {data = 8,
+// data_end = 8 + len} in its first 8 bytes, packet byte b at image byte 8 + b, zeros at or past
+// 8 + len. Two aligned 16-byte source blocks and a funnel shift (v_alignbyte) per dword.
 __device__ __forceinline__ uint4 xdp_image_chunk(const uint8_t* src, uint32_t len, uint32_t c) {
+  const uintptr_t s0 = (uintptr_t)src, end = s0 + len;
+  const uintptr_t p = s0 + 16ull * c - 8;  // the source address of image byte 16c
+  const uintptr_t a0 = p & ~(uintptr_t)15;
+  const uint32_t sh = (uint32_t)(p & 15), q = sh >> 2;
+  const u32x4 b0 = blk16(a0, s0, end);
+  const u32x4 b1 = sh ? blk16(a0 + 16, s0, end) : u32x4{0u, 0u, 0u, 0u};
+  const uint32_t d[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
   uint32_t w[4];
 #pragma unroll
-  for (int q = 0; q < 4; q++) {
-    const uint32_t b = 16 * c + 4 * q;
-    w[q] = b == 0 ? 8u : b == 4 ? 8u + len : b - 8 < len ? (uint32_t)pkt_read(src, b - 8, 4, len) : 0u;
+  for (int k = 0; k < 4; k++) {
+    // d[k + q] and d[k + q + 1] by selects (q per thread: no dynamic register indexing)
+    const uint32_t l0 = (q & 1) ? d[k + 1] : d[k], l1 = (q & 1) ? d[k + 3] : d[k + 2];
+    const uint32_t h0 = (q & 1) ? d[k + 2] : d[k + 1];
+    const uint32_t h1 = (q & 1) ? (k + 4 < 8 ? d[k + 4] : 0u) : d[k + 3];
+    const uint32_t lo = (q & 2) ? l1 : l0, hi = (q & 2) ? h1 : h0;
+    w[k] = __builtin_amdgcn_alignbyte(hi, lo, sh & 3);
+    const uint32_t b = 16 * c + 4 * k;  // image byte of the dword
+    const uint32_t valid = 8 + len > b ? min(8 + len - b, 4u) : 0u;
+    w[k] = b == 0 ? 8u : b == 4 ? 8u + len : valid >= 4 ? w[k] : w[k] & ((1u << (8 * valid)) - 1u);
   }
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
-// ============================================================================================
-__global__ __launch_bounds__(256) void xdp_stage(const uint8_t* frames, const uint32_t* offsets,
-                                                 const uint16_t* lens, uint64_t stride, uint64_t n,
-                                                 uint32_t mem_size, uint8_t* dst, uint32_t* doffs,
+__global__ __launch_bounds__(256) void xdp_stage(const uint8_t* __restrict__ frames,
+                                                 const uint32_t* __restrict__ offsets,
+                                                 const uint16_t* __restrict__ lens, uint64_t stride,
+                                                 uint64_t n, uint32_t mem_size,
+                                                 uint8_t* __restrict__ dst, uint32_t* doffs,
                                                  uint16_t* dlens, unsigned long long* cursor) {
-  __shared__ uint32_t pre[256], copy_s[256];
+  __shared__ uint32_t pre[256], len_s[256];
   __shared__ const uint8_t* src_s[256];
   __shared__ unsigned long long base;
   const uint32_t t = threadIdx.x;
@@ -1366,7 +1417,7 @@ __global__ __launch_bounds__(256) void xdp_stage(const uint8_t* frames, const ui
     src_s[t] = frames + (offsets ? (uint64_t)offsets[i] : i * stride);
   }
   pre[t] = slot;
-  copy_s[t] = copy;
+  len_s[t] = copy ? len : 0xFFFFFFFFu;  // (not copied: ST_BADPKT)
   __syncthreads();
   for (uint32_t d = 1; d < 256; d <<= 1) {  // inclusive scan of the slot sizes
     const uint32_t v = t >= d ? pre[t - d] : 0u;
@@ -1376,26 +1427,35 @@ __global__ __launch_bounds__(256) void xdp_stage(const uint8_t* frames, const ui
   }
   if (t == 255) base = atomicAdd(cursor, (unsigned long long)pre[255]);
   __syncthreads();
-  const uint32_t excl = pre[t] - slot;
   if (i < n) {
-    doffs[i] = (uint32_t)(base + excl);
+    doffs[i] = (uint32_t)(base + pre[t] - slot);
     dlens[i] = (uint16_t)(len + 8 < 0xFFFF ? len + 8 : 0xFFFF);
   }
-  // short images: each thread its own packet's, 16 bytes at a time into the 16-byte aligned slot
-  // (the round-3 form copied byte by byte, a block's 256 packets one after another: 225 us for a
-  // 1 Mi batch of 64-byte frames); long ones: one wave per packet, lane l on chunks l, l + 64, ...
-  // (a thread per 1500-byte packet strides 1.5 KB between lanes: 2.5 ms for config 5's batch)
-  if (i < n && copy && copy <= kStageShort) {
-    uint8_t* const o = dst + base + excl;
-    for (uint32_t c = 0; c < copy; c += 16) *(uint4*)(o + c) = xdp_image_chunk(src_s[t], len, c / 16);
-  }
-  __syncthreads();  // (pre[] holds the inclusive offsets, copy_s[] the image lengths)
-  const uint32_t wv = t / kWave, ln = t % kWave;
-  for (uint32_t j = wv; j < 256; j += 256 / kWave) {
-    const uint32_t cj = copy_s[j];
-    if (cj <= kStageShort) continue;  // (wave-uniform)
-    uint8_t* const o = dst + base + pre[j] - ((cj + 15u) & ~15u);
-    for (uint32_t c = ln; 16 * c < cj; c += kWave) *(uint4*)(o + 16 * c) = xdp_image_chunk(src_s[j], cj - 8, c);
+  uint8_t* const o = dst + base;
+  const uint32_t chunks = pre[255] / 16;
+  // four chunks per thread per round, their loads all in flight before any store (the chunks'
+  // packets: the first j with pre[j] > 16k, walked forward -- k only grows)
+  uint32_t j = 0;
+  for (uint32_t k0 = t; k0 < chunks; k0 += 4 * 256) {
+    uint4 v[4];
+    uint32_t kk[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const uint32_t k = k0 + 256 * u;
+      kk[u] = k;
+      v[u] = make_uint4(0u, 0u, 0u, 0u);
+      if (k >= chunks) continue;
+      while (pre[j] <= 16 * k) j++;
+      const uint32_t lj = len_s[j];
+      if (lj == 0xFFFFFFFFu) {
+        kk[u] = 0xFFFFFFFFu;  // (not copied: ST_BADPKT)
+        continue;
+      }
+      v[u] = xdp_image_chunk(src_s[j], lj, (16 * k - (j ? pre[j - 1] : 0u)) / 16);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++)
+      if (kk[u] < chunks) *(uint4*)(o + 16ull * kk[u]) = v[u];
   }
 }
 
@@ -1843,20 +1903,23 @@ extern "C" __global__ __launch_bounds__(kBlock, 7) void ebpf_tile_jit_var(Launch
 // 4-byte aligned or absent, no final images, n_tiles < 2^31) -- the wave's tiles tile, tile + W,
 // ... in one asm statement (tile_jit_varl.inc, gen_tile.py jit_statement_varl) with two window
 // buffers and two packed metadata buffers per wave (kVarlWaveLds; 4 workgroups of 4 waves per
-// CU), so a tile's windows are in flight while the one before it runs. The C++ here only starts
-// the wave's first tile, stages the windows of a tile the statement hands back (misaligned
-// packets, the batch's partial last tile) and unpacks the per-lane packed counter buckets.
+// CU), so a tile's windows are in flight while the one before it runs. Tiles whose packets are
+// not all 16-byte aligned (a capture's records) are DMA'd from aligned sources plus 16 bytes per
+// lane in v[56:59], and shifted into place in LDS at their turn (realign). The C++ here only
+// starts the wave's first tile, stages the windows of a tile the statement hands back (the
+// batch's partial last tile, a misaligned tile after the statement's last) and unpacks the
+// per-lane packed counter buckets.
 #define VARL_OPERANDS \
         : [tile] "+s"(tile), [winb] "+s"(winb), [nwinb] "+s"(nwinb), [metab] "+s"(metab), \
           [nmetab] "+s"(nmetab), [acc] "+v"(acc), [ret] "+v"(ret), [cdn] "=&s"(cdn), \
-          [stage] "=&s"(stg) \
+          [stage] "=&s"(stg), [mis] "=&s"(mis), [dmask] "=&s"(dmask) \
         : [ka] "s"(ka), [k_frames] "s"(a.frames), [fr_lo] "s"((uint32_t)(uintptr_t)a.frames), \
           [of_lo] "s"((uint32_t)(uintptr_t)a.offsets), \
           [of_hi] "s"((uint32_t)((uintptr_t)a.offsets >> 32)), \
           [ln_lo] "s"((uint32_t)(uintptr_t)a.lens), [ln_hi] "s"((uint32_t)((uintptr_t)a.lens >> 32)), \
           [fc] "v"(fc), [lb] "v"(lb), [db] "v"(db), \
           [tbytes] "s"(rfl(tbytes)), [s16] "s"(rfl(s16)), [lane] "v"(lane), \
-          [k_deopt] "s"(a.deopt), [k_dix] "s"(a.deopt_idx), \
+          [k_deopt] "s"(a.deopt), [k_dix] "s"(a.deopt_idx), [k_ovf] "s"(a.ovf), \
           [k_n] "s"(a.n), [k_mem] "s"(a.mem_size), [k_r10] "s"(a.r10), \
           [vd_lo] "s"((uint32_t)(uintptr_t)a.verdict), \
           [vd_hi] "s"((uint32_t)((uintptr_t)a.verdict >> 32)), [fl] "s"(rfl(fl)), \
@@ -1868,7 +1931,7 @@ extern "C" __global__ __launch_bounds__(kBlock, 7) void ebpf_tile_jit_var(Launch
           [o_init] "i"(offsetof(LaunchArgs, init_regs)), [o_r0] "i"(offsetof(LaunchArgs, r0)), \
           [o_status] "i"(offsetof(LaunchArgs, status)), \
           [o_regs] "i"(offsetof(LaunchArgs, regs_out)) \
-        : TILE_ASM_CLOBBER, TILE_ASM_CLOBBER_WINDOW
+        : TILE_ASM_CLOBBER, TILE_ASM_CLOBBER_WINDOW, "v56", "v57", "v58", "v59"
 template <bool STACK>
 __device__ __forceinline__ void varl_body(LaunchArgs& a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -1950,7 +2013,8 @@ __device__ __forceinline__ void varl_body(LaunchArgs& a) {
   }
   while (tile < ntiles) {
     uint64_t acc = 0;
-    uint32_t ret = 0, cdn, stg;
+    uint32_t ret = 0, cdn, stg, mis;
+    uint64_t dmask;  // (store mode: the lanes whose overflow image is live, per tile)
     if constexpr (STACK) {
       asm volatile(
 #include "tile_jit_varl_stack.inc"

@@ -56,6 +56,9 @@ struct Marker {
   bool deep = false;   // the deep-prefetch loop kernel's statement
   bool varl = false;   // the var tile loop's statement (ebpf_tile_jit_varl): the var flavour of
                        // loads with the preloaded window, as the stack statement's
+  // the var tile loop's store-mode state (gen_tile.py jit_statement_varl): the SGPR pair of
+  // LaunchArgs::ovf, the tile index's SGPR and the SGPR pair of the lanes' overflow-dirty mask
+  std::string ovf, tile, dm;
 };
 
 bool inline_const(int64_t v) { return v >= -16 && v <= 64; }
@@ -92,6 +95,9 @@ bool find_markers(const std::string& s, std::vector<Marker>& out) {
     m.stack = field("stack=") == "1";
     m.deep = field("deep=") == "1";
     m.varl = field("varl=") == "1";
+    m.ovf = field("ovf=");
+    m.tile = field("tile=");
+    m.dm = field("dm=");
     const size_t mk = s.find(";@@JIT@@", eol);
     if (mk == std::string::npos || m.n.empty()) return false;
     const size_t ik = s.rfind(";@@JITINIT@@", pos);
@@ -1152,11 +1158,53 @@ struct Compiler {
     return s;
   }
 
+  // ---- the overflow image (store mode on the var tile loop): image bytes [64, 128) of the
+  // lane's packet in the workspace (LaunchArgs::ovf + packet index * 64), filled from the packet
+  // (zeros at or past LEN) by the lane's first store past byte 64 (its bit in the dirty mask dm,
+  // cleared per tile); its later loads of those bytes read it (sc1: from L2, where the stores
+  // went). So a port or checksum rewrite behind long IPv4 options stays on the compiled kernel.
+  // v[44:45] = the lane's overflow image (s[48:49]: its tile's).
+  std::string ovf_addr() const {
+    return "s_lshl_b32 s48, " + tile_s + ", 12\ns_lshr_b32 s49, " + tile_s + ", 20\n"
+           "s_add_u32 s48, s48, " + ovf_lo + "\ns_addc_u32 s49, s49, " + ovf_hi + "\n"
+           "v_mbcnt_lo_u32_b32 v44, -1, 0\nv_mbcnt_hi_u32_b32 v44, -1, v44\n"
+           "v_lshlrev_b32 v44, 6, v44\nv_mov_b32 v45, 0\n"
+           "v_lshl_add_u64 v[44:45], v[44:45], 0, s[48:49]\n";
+  }
+  // The lanes of exec: their overflow images filled from the packet's dwords past byte 64 (those
+  // that hold a packet byte, as the far loads read them; bytes at or past LEN zero). Uses
+  // v[64:79] (the preloaded window registers, unused in store mode), v[40:41], v[44:45], s[62:63].
+  std::string ovf_fill() const {
+    std::string r = ovf_addr() + "s_mov_b64 s[62:63], exec\n";
+    for (uint32_t k = 0; k < 16; k++) r += "v_mov_b32 v" + std::to_string(64 + k) + ", 0\n";
+    for (uint32_t k = 0; k < 16; k++)
+      r += "v_cmp_lt_u32 vcc, " + std::to_string(64 + 4 * k) + ", v31\n"
+           "s_and_b64 exec, s[62:63], vcc\n"
+           "global_load_dword v" + std::to_string(64 + k) + ", v[32:33], off offset:" +
+           std::to_string(64 + 4 * k) + "\n";
+    r += "s_mov_b64 exec, s[62:63]\ns_waitcnt vmcnt(0)\n";
+    for (uint32_t k = 0; k < 16; k++)
+      r += "v_subrev_u32 v40, " + std::to_string(64 + 4 * k) + ", v31\n"
+           "v_med3_i32 v40, v40, 0, 4\nv_lshlrev_b32 v40, 3, v40\n"
+           "v_lshlrev_b64 v[40:41], v40, 1\nv_add_u32 v40, -1, v40\n"
+           "v_and_b32 v" + std::to_string(64 + k) + ", v40, v" + std::to_string(64 + k) + "\n";
+    for (uint32_t c = 0; c < 4; c++)
+      r += "global_store_dwordx4 v[44:45], v[" + std::to_string(64 + 4 * c) + ":" +
+           std::to_string(67 + 4 * c) + "], off offset:" + std::to_string(16 * c) + "\n";
+    return r + "s_waitcnt vmcnt(0)\n";
+  }
+  // Lanes of exec in the dirty mask deoptimize (before a load the overflow would not serve).
+  std::string ovf_dirty_deopt(const std::string& U, const std::string& next) const {
+    return "s_and_b64 vcc, exec, " + dm + "\ns_cbranch_vccz .Ldk" + U + "\n"
+           "s_mov_b64 s[66:67], exec\ns_mov_b64 exec, vcc\nv_mov_b32 v30, 0x80\nv_mov_b32 v28, -1\n"
+           "s_andn2_b64 exec, s[66:67], vcc\ns_cbranch_execz " + next + "\n.Ldk" + U + ":\n";
+  }
+
   // ST / STX through a register (StackPlan::dyn): the address a = dst + off with the reference's
   // bounds (a >= mem -> ST_MEM, a + w > mem -> ST_MEM_UB: only the first byte is checked, Q16,
   // mmu.rs:23-30); lanes storing past the window [0, 64) deoptimize (status kStDeopt: the
   // general interpreter re-runs their packets); the rest write their bytes into LDS one by one.
-  std::string lds_store_dyn(uint32_t i, const std::string& P) const {
+  std::string lds_store_dyn(uint32_t i, const std::string& P, std::string& ool) const {
     const Uop& o = uops[i];
     const uint32_t w = o.aux;
     const std::string U = P + "u" + std::to_string(i), next = entry_label(P, next_start(i));
@@ -1184,13 +1232,17 @@ struct Compiler {
          "s_cbranch_execz " + next + "\n"
          ".Lsok" + U + ":\n"
          "v_cmp_lt_u32 vcc, 64, v38\n"
-         "s_and_b64 vcc, vcc, exec\n"
-         "s_cbranch_vccz .Lsin" + U + "\n"
-         "s_mov_b64 s[66:67], exec\ns_mov_b64 exec, vcc\n"
-         "v_mov_b32 v30, 0x80\nv_mov_b32 v28, -1\n"
-         "s_andn2_b64 exec, s[66:67], vcc\n"
-         "s_cbranch_execz " + next + "\n"
-         ".Lsin" + U + ":\n";
+         "s_and_b64 vcc, vcc, exec\n";
+    if (!ovf_lo.empty()) {
+      s += "s_cbranch_vccnz .Lsov" + U + "\n";
+    } else {
+      s += "s_cbranch_vccz .Lsin" + U + "\n"
+           "s_mov_b64 s[66:67], exec\ns_mov_b64 exec, vcc\n"
+           "v_mov_b32 v30, 0x80\nv_mov_b32 v28, -1\n"
+           "s_andn2_b64 exec, s[66:67], vcc\n"
+           "s_cbranch_execz " + next + "\n";
+    }
+    s += ".Lsin" + U + ":\n";
     for (uint32_t j = 0; j < w; j++) {
       std::string A = "v36";
       if (j) {
@@ -1202,6 +1254,49 @@ struct Compiler {
       const std::string V = store_value(o, j, 1, s, &hi);
       s += std::string(hi ? "ds_write_b8_d16_hi" : "ds_write_b8") + " v40, " + V + "\n";
     }
+    if (ovf_lo.empty()) return s;
+    s += ".Lsdn" + U + ":\n";
+    // out of line: some lane's store ends past byte 64 (vcc). Lanes ending past min(128, S0 = the
+    // stack window's start, s57) deoptimize; the others fill their overflow image on their first
+    // such store, then write each byte to the window (< 64) or the overflow image.
+    std::string o2 = ".Lsov" + U + ":\n"
+        "v_mov_b32 v39, 0x80\nv_min_u32 v39, s57, v39\n"
+        "v_cmp_lt_u32_e64 s[60:61], v39, v38\n"
+        "s_and_b64 s[60:61], s[60:61], vcc\n"
+        "s_cbranch_scc0 .Lsnd" + U + "\n"
+        "s_mov_b64 s[66:67], exec\ns_mov_b64 exec, s[60:61]\n"
+        "v_mov_b32 v30, 0x80\nv_mov_b32 v28, -1\n"
+        "s_andn2_b64 exec, s[66:67], s[60:61]\n"
+        "s_andn2_b64 vcc, vcc, s[60:61]\n"
+        "s_cbranch_execz " + next + "\n"
+        ".Lsnd" + U + ":\n"
+        "s_andn2_b64 s[60:61], vcc, " + dm + "\n"
+        "s_cbranch_scc0 .Lsdi" + U + "\n"
+        "s_or_b64 " + dm + ", " + dm + ", s[60:61]\n"
+        "s_mov_b64 s[66:67], exec\ns_mov_b64 exec, s[60:61]\n" + ovf_fill() +
+        "s_mov_b64 exec, s[66:67]\n"
+        ".Lsdi" + U + ":\n" + ovf_addr() + "v_mov_b32 v41, 0\n";
+    for (uint32_t j = 0; j < w; j++) {
+      const std::string J = std::to_string(j);
+      o2 += (j ? "v_add_u32 v39, " + J + ", v36\n" : std::string("v_mov_b32 v39, v36\n")) +
+            "v_cmp_gt_u32_e64 s[60:61], 64, v39\n"
+            "s_mov_b64 s[66:67], exec\ns_and_b64 exec, s[66:67], s[60:61]\n"
+            "s_cbranch_execz .Lsw" + J + U + "\n"
+            "v_xad_u32 v40, v39, v35, v34\n";
+      bool hi = false;
+      std::string V = store_value(o, j, 1, o2, &hi);
+      o2 += std::string(hi ? "ds_write_b8_d16_hi" : "ds_write_b8") + " v40, " + V + "\n"
+            ".Lsw" + J + U + ":\n"
+            "s_andn2_b64 exec, s[66:67], s[60:61]\n"
+            "s_cbranch_execz .Lsg" + J + U + "\n"
+            "v_add_u32 v40, -64, v39\n"
+            "v_lshl_add_u64 v[46:47], v[44:45], 0, v[40:41]\n";
+      V = store_value(o, j, 1, o2, &hi);
+      o2 += std::string(hi ? "global_store_byte_d16_hi" : "global_store_byte") + " v[46:47], " + V +
+            ", off\n.Lsg" + J + U + ":\ns_mov_b64 exec, s[66:67]\n";
+    }
+    o2 += "s_waitcnt vmcnt(0)\ns_branch .Lsdn" + U + "\n";
+    ool += o2;
     return s;
   }
 
@@ -1239,6 +1334,16 @@ struct Compiler {
     const std::string P = "J" + m.n + "_";
     ovl_tag = m.n;
     overlay_widths = 0;
+    // (the var tile loop's statement: stores past byte 64 into the overflow image)
+    ovf_lo = ovf_hi = tile_s = dm = "";
+    unsigned a0 = 0, a1 = 0;
+    if (m.varl && m.stack && !m.tile.empty() && !m.dm.empty() &&
+        sscanf(m.ovf.c_str(), "s[%u:%u]", &a0, &a1) == 2 && a1 == a0 + 1) {
+      ovf_lo = "s" + std::to_string(a0);
+      ovf_hi = "s" + std::to_string(a1);
+      tile_s = m.tile;
+      dm = m.dm;
+    }
     if (!m.stack) {
       out = "s_mov_b64 exec, 0  ; (store mode: the var kernel's stack statement only)\n";
       return true;
@@ -1246,6 +1351,7 @@ struct Compiler {
     std::string ool;
     std::string main = "; compiled eBPF program (store mode): " + std::to_string(n) + " micro-ops\n"
                        "s_mov_b32 s52, s33\ns_mov_b32 s53, 0\n";
+    if (!dm.empty()) main += "s_mov_b64 " + dm + ", 0\n";
     // (the var tile loop's windows hold packet bytes [0, 64): the xdp_md ctx shifted in first, as
     // body does; the var kernel's C++ shifts them itself)
     if (m.varl && !m.xdp.empty())
@@ -1364,6 +1470,10 @@ struct Compiler {
   }
   std::string overlay_label(uint32_t w) const { return ".Lovr" + ovl_tag + "_" + std::to_string(w); }
   std::string ovl_tag;  // unique per statement (set by body)
+  // store mode on the var tile loop (body_store, marker fields ovf / tile / dm): stores into the
+  // image's bytes [64, 128) go to the packet's overflow image in the workspace instead of
+  // deoptimizing the lane; empty on the other statements
+  std::string ovf_lo, ovf_hi, tile_s, dm;
 
   // The overlay routines the statement's loads call (vcc = the lanes to patch).
   std::string overlay_routines() const {
@@ -1872,6 +1982,36 @@ struct Compiler {
              "s_andn2_b64 s[66:67], s[66:67], vcc\ns_andn2_b64 s[68:69], s[68:69], vcc\n"
              "s_mov_b64 exec, vcc\nv_mov_b32 v30, 0x80\nv_mov_b32 v28, -1\n"
              "s_mov_b64 exec, s[68:69]\n.Lnd" + U + ":\n";
+    if (smode && !dm.empty()) {
+      // lanes that stored past byte 64 (the dirty mask): their bytes [64, 128) from the overflow
+      // image; an access ending past 128 deoptimizes (its high bytes would be the packet's)
+      far += "s_and_b64 s[60:61], s[68:69], " + dm + "\n"
+             "s_cbranch_scc0 .Lnv" + U + "\n"
+             "v_cmp_lt_u32 vcc, 0x80, v38\n"
+             "s_and_b64 vcc, vcc, s[60:61]\n"
+             "s_cbranch_vccz .Lnq" + U + "\n"
+             "s_andn2_b64 s[60:61], s[60:61], vcc\n"
+             "s_andn2_b64 s[66:67], s[66:67], vcc\n"
+             "s_andn2_b64 s[68:69], s[68:69], vcc\n"
+             "s_mov_b64 exec, vcc\nv_mov_b32 v30, 0x80\nv_mov_b32 v28, -1\n"
+             ".Lnq" + U + ":\n"
+             "s_mov_b64 exec, s[60:61]\n"
+             "s_cbranch_execz .Lnv" + U + "\n" + ovf_addr() +
+             "v_add_u32 v46, -64, v36\nv_and_b32 v46, -4, v46\nv_mov_b32 v47, 0\n"
+             "v_lshl_add_u64 v[44:45], v[44:45], 0, v[46:47]\n"
+             "global_load_dword v49, v[44:45], off sc1\n";
+      if (w > 1) far += "global_load_dword v50, v[44:45], off offset:4 sc1\n";
+      if (w == 8) far += "global_load_dword v51, v[44:45], off offset:8 sc1\n";
+      far += "s_waitcnt vmcnt(0)\nv_mov_b32 v27, 0\n";
+      if (w == 1)
+        far += "v_and_b32 v48, 3, v36\nv_lshlrev_b32 v48, 3, v48\nv_bfe_u32 v26, v49, v48, 8\n";
+      else
+        far += "v_alignbyte_b32 v26, v50, v49, v36\n" +
+               std::string(w == 8 ? "v_alignbyte_b32 v27, v51, v50, v36\n" : "");
+      far += "s_andn2_b64 s[68:69], s[68:69], s[60:61]\n"
+             ".Lnv" + U + ":\n"
+             "s_mov_b64 exec, s[68:69]\n";
+    }
     far += "v_mov_b32 v26, 0\nv_mov_b32 v27, 0\n"
                       "v_cmp_lt_u32 vcc, v36, v31\ns_and_b64 exec, s[68:69], vcc\n"
                       "s_cbranch_execz .Lfd" + U + "\n"
@@ -2521,7 +2661,7 @@ struct Compiler {
       const Uop& o = uops[i];
       if ((o.op == U_ST || o.op == U_STX) && stk->off[i] == kNoStack) {
         main += stk->pw[i] != kNoStack ? lds_store_const(i)
-                : stk->dyn[i]          ? lds_store_dyn(i, P)
+                : stk->dyn[i]          ? lds_store_dyn(i, P, ool)
                                        : std::string("; unreachable store\n");
         return true;
       }
@@ -2529,6 +2669,10 @@ struct Compiler {
         main += ldxk_lds(i);
         return true;
       }
+      // (a constant-address load past the window reads the packet: a lane that has stored into
+      // its overflow image leaves for the general interpreter first)
+      if (!dm.empty() && (id == T_LDXK_FAR_C || id == T_LDXK_FAR_E))
+        main += ovf_dirty_deopt(P + "u" + std::to_string(i), entry_label(P, next_start(i)));
     }
     if (stk && (uops[i].op == U_ST || uops[i].op == U_STX)) {
       // (a store the load-time dataflow never reached has no offset: no lane executes it)
@@ -3021,6 +3165,12 @@ bool compile_into_template(Compiler& c, Compiler* xc, std::vector<char>& code_ob
       b = "s_mov_b64 exec, 0  ; (not this program's kernel)\n";
     else
       ok = xc ? c.body_loop(m, *xc, b) : c.body(m, b);
+    // (the var tile loop keeps a misaligned next tile's last 16 bytes per lane in v[56:59] across
+    // the program, gen_tile.py jit_statement_varl: its code must not name them)
+    if (ok && m.varl && Compiler::touches(b, 56, 59)) {
+      if (err) *err = "var tile loop program names v[56:59]";
+      return false;
+    }
     if (!ok) {
       if (err) *err = c.err;
       return false;

@@ -28,7 +28,8 @@ constexpr uint64_t kWsBinCountsOff = 384;
 constexpr uint64_t kWsBinCursorOff = 448;
 constexpr int kBinClasses = 16;  // packets are binned by ceil(len / 128), capped
 constexpr int kBinMaxWgs = 1024;  // binning grid cap; per-workgroup class counts follow the order
-constexpr uint64_t kWsDeoptOff = 0;  // u32 count, done: the deopt list (LaunchArgs::deopt)
+constexpr uint64_t kWsDeoptOff = 0;  // u32 count, done: the deopt list (LaunchArgs::deopt); u32
+                                     // at +8: how many packets the last deopt pass re-ran
 constexpr uint64_t kWsXdpCursorOff = 320;  // u64: bytes staged by xdp_stage (reset per batch)
 constexpr uint64_t kWsMultiOff = 256;  // u64[8]: ebpf_run_batch_multi's per-shard counter sums
 constexpr uint64_t kWsShardsOff = 512;
@@ -85,6 +86,9 @@ struct LaunchArgs {
   uint32_t* deopt;
   uint32_t* deopt_idx;
   uint32_t deopt_pass;
+  // store mode on the var tile loop: per packet its image's bytes [64, 128) once it stores there
+  // (u8[n][64] + 16 in the workspace past deopt_idx; jit.cpp ovf_fill), else null
+  uint8_t* ovf;
 };
 
 constexpr int kTraceSlots = 16;

@@ -786,13 +786,16 @@ def test_bench_line_pinned(cuda, extra, env):
     assert c["drop"] + c["pass"] + c["other"] + c["faults"] == 11 * n * (1 << 20)
 
 
-@pytest.mark.parametrize("slot,shift", [(64, 0), (80, 3)])
+@pytest.mark.parametrize("slot,shift", [(64, 0), (80, 3), (80, 8), (81, 5)])
 @pytest.mark.parametrize("name", ["5tuple", "5tuple_stack", "5tuple_xdp", "acl"])
 def test_var_kernel_full_size_shuffled(cuda, name, slot, shift):
     """The compiled var kernels at full size (1 Mi packets: several tiles per persistent wave, so
     each tile's offsets and lengths arrive by the previous tile's metadata prefetch). The fixed
-    5-tuple fixture's frames, stored `slot` bytes apart at `shift` (3: misaligned, the per-lane
-    staging path) and listed in a shuffled order through offsets + lens: verdict, r0 and status i
+    5-tuple fixture's frames, stored `slot` bytes apart at `shift` (3, 8: every packet misaligned
+    by the same amount -- 8 is a pcap capture's record layout -- so the var tile loop DMAs from
+    16-byte aligned sources and realigns with one shift per tile; slot 81: a different
+    misalignment per packet, the realign's per-lane select network) and listed in a shuffled
+    order through offsets + lens: verdict, r0 and status i
     equal the fixed-slot kernel's for frame perm[i] (for the 5-tuple: the fixture's CRC and
     counters; the others run on fixed slots against the oracle in their own tests). Programs: the
     5-tuple, its stack-window form (ebpf_tile_jit_var_stack), the standard-XDP form over xdp_md

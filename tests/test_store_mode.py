@@ -187,3 +187,65 @@ def test_nat_workload_full_size(cuda, oracle_mod):
         assert np.array_equal(res.verdict.cpu().numpy(), verdict), deopt
         assert list(cnt.cpu().numpy().view(np.uint64)) == list(ocnt), deopt
         prog.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layout", ["fixed128", "offsets_mis3", "xdp_offsets"])
+def test_nat_long_options_no_deopt(cuda, oracle_mod, layout):
+    """IPv4 options up to IHL 15 put the NAT's port store at image bytes 74..77, past the 64-byte
+    header window: on the var tile loop those stores (and the port loads after them) go to the
+    packet's overflow image (jit.cpp ovf_fill, image bytes [64, 128)) instead of deoptimizing --
+    the deopt pass re-runs no packet (the workspace word at +8, LaunchArgs::deopt[2]), and every
+    output == the general interpreter's == the oracle's."""
+    import torch
+
+    from ebpf_emu import Program, _lib
+    from ebpf_emu import workloads as W
+    from test_stack_tier import VAR_LAYOUTS, _fixed_frames
+
+    img = W.program("nat")
+    rng = random.Random(77 + len(layout))
+    pkts = _nat_packets(rng, 2000, long_options=1.0)
+    assert sum(14 + 4 * (p[14] & 15) + 4 > 64 for p in pkts) > 500
+    prog = Program(img)
+    if layout.startswith("fixed"):
+        stride = int(layout[5:])
+        pk = [p[:stride].ljust(stride, b"\0") for p in pkts]
+        frames = _fixed_frames(pk, stride, cuda)
+        kw = dict(n=len(pk), stride=stride)
+        xdp = False
+    else:
+        from test_gpu_parity import _stage
+
+        spec = dict(VAR_LAYOUTS[layout])
+        xdp = spec.pop("xdp", False)
+        pk = pkts
+        frames, kw = _stage(pkts, cuda, **spec)
+    b = prog.make_batch(frames, xdp_md=xdp, **kw)
+    ws = torch.full((prog.workspace_bytes(b, 0),), 0x55, dtype=torch.uint8, device=cuda)
+    ws[:512 + 64 * 8 * 8] = 0  # (launch.h: the deopt words and counter shards start zeroed)
+    b = prog.make_batch(frames, xdp_md=xdp, workspace=ws, **kw)
+    assert prog.batch_kernel(b) == _lib.EBPF_KERNEL_JIT_VARL_STACK
+    out = _lib.BatchOut()
+    r0 = torch.empty(len(pk), dtype=torch.int64, device=cuda)
+    st = torch.empty(len(pk), dtype=torch.uint8, device=cuda)
+    ws[8:12] = 0xFF
+    out.r0, out.status = r0.data_ptr(), st.data_ptr()
+    prog.launch(b, out, torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    assert ws[8:12].cpu().numpy().view(np.uint32)[0] == 0, "lanes deoptimized"
+    gen = prog.run(frames, r0=True, status=True, generic=True, xdp_md=xdp, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(st, gen.status)
+    ok = st == 0
+    assert torch.equal(r0[ok], gen.r0[ok])
+    from test_stack_tier import _images_of
+
+    op = oracle_mod.Program(img)
+    stn, r0n = st.cpu().numpy(), r0.cpu().numpy().view(np.uint64)
+    for i, im in enumerate(_images_of(pk, xdp)):
+        s, o0, _ = op.run_packet(im, 1024, 512, 1 << 22)
+        assert stn[i] == s, (layout, i)
+        if s == 0:
+            assert int(r0n[i]) == o0, (layout, i)
+    prog.close()
