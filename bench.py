@@ -434,9 +434,7 @@ def main():
     # (counter shards, zeroed once) and verdict buffer; every launch adds into the one counters
     # array (the library's fold is an atomic add). Stream 0 is the current stream.
     S = max(1, args.streams)
-    _order = os.environ.get("BENCH_ORDER", "last0")  # (A/B, temporary: old | last0 | side)
-    streams = ([torch.cuda.Stream(dev) for _ in range(S)] if _order == "side" else
-               [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)])
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
     ws_bytes = max(prog.workspace_bytes(bd, local) for bd in descs)
     verdicts = [verdict] + [torch.empty_like(verdict) for _ in range(S - 1)]
     workspaces, sdescs, outs = [], [], []
@@ -457,13 +455,9 @@ def main():
     out = outs[0]
     stream = streams[0]
 
-    # step i of the K timed steps runs on stream (K-1-i) mod S: consecutive steps alternate, and
-    # the last one runs on stream 0, whose end event closes the timed region. With the last step
-    # on another stream the end join waits on that stream's completion signal from stream 0's
-    # queue, which measured 11 us more per run (tools/fixed_cost_ab.py "cur" vs "last0":
-    # profiles/r05_fixed_cost_ab.json)
+    # step i of k runs on stream (k-1-i) mod S (the timed region's order, below)
     def sof(i, k):
-        return i % S if _order == "old" else (k - 1 - i) % S
+        return (k - 1 - i) % S
 
     def step(i, k=None):
         si = sof(i, k if k is not None else S)
@@ -477,42 +471,56 @@ def main():
             if i % 64 == 0:  # keep the queue short (enqueue is faster than a batch)
                 torch.cuda.synchronize(dev)
         torch.cuda.synchronize(dev)
-    for i in range(args.warmup):
-        step(i)
+
+    def region(k):
+        """k steps bracketed by an event pair: the start event on the first step's stream, the
+        other streams wait on it after the first launch; the last step's stream joins the others
+        before the end event. Returns (start event, end event, host seconds to enqueue)."""
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        first = sof(0, k)
+        ts = time.perf_counter()
+        e0.record(streams[first])
+        for i in range(k):
+            if i == 1:  # (after the first launch: its enqueue is the first thing the GPU waits for)
+                for si in range(S):
+                    if si != first:
+                        streams[si].wait_event(e0)
+            step(i, k)
+        te = time.perf_counter() - ts
+        last = sof(k - 1, k)
+        for si in range(S):  # the last step's stream joins the others before the end event
+            if si != last:
+                ej = torch.cuda.Event()
+                ej.record(streams[si])
+                streams[last].wait_event(ej)
+        e1.record(streams[last])
+        return e0, e1, te
+
+    # warmup: the timed region's own sequence (events, cross-stream waits and joins) untimed, so
+    # its first-use costs land here -- the first cross-stream wait of a process stalled the next
+    # launch by 130-210 us in about half of the driver-style runs (rocprof kernel traces,
+    # profiles/r05_first_wait_stall.log), 7 us per step over 20 steps
+    if args.warmup:
+        region(args.warmup)
     torch.cuda.synchronize(dev)
     counters.zero_()
 
     # ---- timed region: barrier + sync on both sides, K steps, max over ranks ----
-    # HIP events on the launch stream: one pair around the K back-to-back batches (a batch =
+    # HIP events on the launch streams: one pair around the K back-to-back batches (a batch =
     # every launch of one ebpf_run_batch), so the per-batch time includes the dispatch gaps
     # between launches but no event packets between them. The wall clock adds one host -> GPU ->
     # host round trip (the first launch's latency and the completion signal: ~13 us measured for
-    # an empty stream, tools/timing_probe.py), i.e. ~7 % of K = 20 steps of ~15 us; busy-polling
-    # the end event instead of synchronizing measured worse (35 vs 20 us), a graph of the K
-    # launches no better.
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
+    # an empty stream, tools/timing_probe.py). Step i runs on stream (K-1-i) mod S: consecutive
+    # steps alternate and the last one runs on stream 0; with the last step on another stream the
+    # end join waits on that stream's completion signal from stream 0's queue, which measured
+    # 11 us more per run (tools/fixed_cost_ab.py "cur" vs "last0": profiles/r05_fixed_cost_ab.json)
     if use_dist:
         dist.barrier()
     K = args.steps
-    first = sof(0, K)  # (the stream of the first step: the start event is recorded there)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    ev0.record(streams[first])
-    for i in range(K):
-        if i == 1:  # (after the first launch: its enqueue is the first thing the GPU waits for)
-            for si in range(S):
-                if si != first:
-                    streams[si].wait_event(ev0)
-        step(i, K)
-    t_enq = time.perf_counter() - t0  # host time to enqueue the K steps (launch-bound check)
-    last = sof(K - 1, K)
-    for si in range(S):  # the last step's stream joins the others before the end event
-        if si != last:
-            ej = torch.cuda.Event()
-            ej.record(streams[si])
-            streams[last].wait_event(ej)
-    ev1.record(streams[last])
+    ev0, ev1, t_enq = region(K)
     if use_dist:  # the one exchange step: per-verdict counters, RCCL / xGMI
         all_reduce(counters)
     torch.cuda.synchronize(dev)
