@@ -1510,61 +1510,60 @@ s_add_u32 {{T7L}}, {{T7L}}, %[s16]
 s_addc_u32 {{T7H}}, {{T7H}}, 0""" for r in range(4))
     smasks = "\n".join(f"v_cmp_lt_u32_e64 {masks[r]}, %[c16], {{t{8 + r}}}" for r in range(4))
     # a tile whose packets are not all 16-byte aligned (a capture's records: 24 + 16 + sum of the
-    # earlier records) is DMA'd from 16-byte aligned sources: round r's lane moves chunk c of
-    # (packet & ~15), so a window holds packet bytes [-m, 64 - m) (m = packet & 15; the chunk
-    # has packet bytes if 16 c < len + m), and each lane whose packet reaches past them loads the
-    # 16 bytes after (its packet's [64 - m, 80 - m)) into v[56:59]; at that tile's top the lanes
-    # with m != 0 shift their window by m in LDS (realign) before the program reads it.
-    mrounds = "\n".join(f"""v_add_u32 {{t1}}, %[fr_lo], {{t{12 + 2 * r}}}
+    # earlier records) is DMA'd straight from the packets: round r's lane moves packet bytes
+    # [16c, 16c + 16) from packet + 16c, whatever its alignment (the LDS side of the DMA is the
+    # lane's slot either way: tools/probe_dma_align.hip). Nothing may be read past the 16-byte block
+    # that holds the packet's last byte (the page the next block lies in may not be mapped), so a
+    # lane whose chunk would reach past it -- the last chunk of a packet shorter than the window,
+    # when 16c + 16 + m > ceil16(m + len), m = packet & 15 -- moves the aligned block below
+    # instead, (packet + 16c) & ~15, whose bytes hold the chunk's packet bytes m bytes higher; at
+    # the tile's top those lanes shift that one slot down by m in LDS (tailfix).
+    trounds = "\n".join(f"""v_add_u32 {{t1}}, %[fr_lo], {{t{12 + 2 * r}}}
 v_and_b32 {{t1}}, 15, {{t1}}
-v_add_u32 {{t{8 + r}}}, {{t{8 + r}}}, {{t1}}""" for r in range(4)) + "\n" + rounds + "\n" + \
-        "\n".join(f"v_and_b32 {{t{12 + 2 * r}}}, -16, {{t{12 + 2 * r}}}" for r in range(4))
-    d = [f"v{36 + k}" for k in range(16)] + ["v56", "v57", "v58", "v59"]  # the 20 dwords read
-    chunk_rd = "\n".join(f"v_xad_u32 {{t18}}, %[swz], {16 * c}, {{t17}}\n"
-                          f"ds_read_b128 v[{36 + 4 * c}:{39 + 4 * c}], {{t18}}" for c in range(4))
-    chunk_wr = "\n".join(f"v_xad_u32 {{t18}}, %[swz], {16 * c}, {{t17}}\n"
-                          f"ds_write_b128 {{t18}}, v[{36 + 4 * c}:{39 + 4 * c}]" for c in range(4))
-    # uniform dword shift q (every realigned lane's m >> 2 the same: records of one size) -- one
-    # v_alignbyte per dword; else a select network (q per lane) first, then the byte shift
-    uni = "\n".join(f".Lrq{q}%=:\n" + "\n".join(
-        f"v_alignbyte_b32 {d[j]}, {d[j + q + 1]}, {d[j + q]}, {{t16}}" for j in range(16)) +
-        "\ns_branch .Lraw%=" for q in range(4))
+v_add3_u32 {{t2}}, {{t1}}, {{t{8 + r}}}, 15
+v_and_b32 {{t2}}, -16, {{t2}}
+v_add3_u32 {{t3}}, %[c16], {{t1}}, 16
+v_cmp_gt_u32 vcc, {{t3}}, {{t2}}""" + "\n" + rounds.split("\n")[3 * r] + "\n" +
+        rounds.split("\n")[3 * r + 1] + "\n" + rounds.split("\n")[3 * r + 2] + f"""
+v_and_b32 {{t2}}, -16, {{t{12 + 2 * r}}}
+v_cndmask_b32 {{t{12 + 2 * r}}}, {{t{12 + 2 * r}}}, {{t2}}, vcc""" for r in range(4))
+    # the tail lanes of a tile DMA'd from unaligned packets (above): chunk c = (len - 1) >> 4 of a
+    # packet of 1..64 bytes whose 16c + 16 + m > ceil16(m + len); dword j of the slot becomes
+    # bytes [4j + m, 4j + m + 4) of it (bytes at or past 16 - m are past the packet: masked)
+    d = [f"v{36 + k}" for k in range(5)]
     sel = "\n".join(
         "\n".join(f"v_cndmask_b32_e64 {d[k]}, {d[k]}, {d[k + i]}, {m}"
-                   for i, m in ((1, "{T1}"), (2, "{T4}"), (3, "{T5}")) if k + i < 20)
-        for k in range(17)) + "\n" + "\n".join(
-        f"v_alignbyte_b32 {d[j]}, {d[j + 1]}, {d[j]}, {{t16}}" for j in range(16))
-    realign = f"""; this tile's windows came from 16-byte aligned sources: shift the lanes with m != 0
+                   for i, m in ((1, "{T1}"), (2, "{T4}"), (3, "{T5}")) if k + i < 5)
+        for k in range(4))
+    tailfix = f"""; this tile was DMA'd from unaligned packets: its tail lanes' last slot down by m bytes
 s_bitcmp1_b32 %[mis], 0
 s_cbranch_scc0 .Lrad%=
 v_and_b32 {{t16}}, 15, {{BASEL}}
-v_cmp_ne_u32 vcc, 0, {{t16}}
-s_and_b64 vcc, vcc, {{VM}}
-s_cbranch_vccz .Lrad%=
-s_mov_b64 exec, vcc
+v_add3_u32 {{t17}}, {{t16}}, {{LEN}}, 15
+v_and_b32 {{t17}}, -16, {{t17}}
+v_add_u32 {{t18}}, -1, {{LEN}}
+v_and_b32 {{t18}}, -16, {{t18}}
+v_add3_u32 {{t19}}, {{t18}}, {{t16}}, 16
+v_cmp_gt_u32_e64 {{T4}}, {{t19}}, {{t17}}
+v_cmp_ne_u32_e64 {{T1}}, 0, {{LEN}}
+s_and_b64 {{T4}}, {{T4}}, {{T1}}
+v_cmp_ge_u32_e64 {{T1}}, 64, {{LEN}}
+s_and_b64 {{T4}}, {{T4}}, {{T1}}
+s_and_b64 {{T4}}, {{T4}}, {{VM}}
+s_cbranch_scc0 .Lrad%=
+s_mov_b64 exec, {{T4}}
 v_add_u32 {{t17}}, %[winb], %[lane64]
-{chunk_rd}
+v_xad_u32 {{t18}}, %[swz], {{t18}}, {{t17}}
+ds_read_b128 v[36:39], {{t18}}
+v_mov_b32 v40, 0
 v_lshrrev_b32 {{t19}}, 2, {{t16}}
-v_readfirstlane_b32 {{T3}}, {{t19}}
-v_cmp_ne_u32 vcc, {{T3}}, {{t19}}
-s_and_b64 vcc, vcc, exec
-s_waitcnt lgkmcnt(0)
-s_cbranch_vccnz .Lrqv%=
-s_cmp_eq_u32 {{T3}}, 0
-s_cbranch_scc1 .Lrq0%=
-s_cmp_eq_u32 {{T3}}, 1
-s_cbranch_scc1 .Lrq1%=
-s_cmp_eq_u32 {{T3}}, 2
-s_cbranch_scc1 .Lrq2%=
-s_branch .Lrq3%=
-{uni}
-.Lrqv%=:
 v_cmp_eq_u32_e64 {{T1}}, 1, {{t19}}
 v_cmp_eq_u32_e64 {{T4}}, 2, {{t19}}
 v_cmp_eq_u32_e64 {{T5}}, 3, {{t19}}
+s_waitcnt lgkmcnt(0)
 {sel}
-.Lraw%=:
-{chunk_wr}
+""" + "\n".join(f"v_alignbyte_b32 {d[j]}, {d[j + 1]}, {d[j]}, {{t16}}" for j in range(4)) + f"""
+ds_write_b128 {{t18}}, v[36:39]
 s_mov_b64 exec, -1
 s_mov_b64 vcc, {{VM}}
 .Lrad%=:"""
@@ -1576,7 +1575,6 @@ global_load_lds_dwordx4 {{T{12 + 2 * r}{13 + 2 * r}}}, off ; @DMAPOLICY@""" for 
     main = """s_mov_b32 {M0S}, m0
 s_movk_i32 %[cdn], 511
 s_mov_b32 %[stage], 0
-s_mov_b32 %[mis], 0
 .Lloop%=:
 ; this tile's windows and the next tile's metadata: landed
 s_waitcnt vmcnt(0)
@@ -1609,7 +1607,7 @@ s_mul_i32 {T5L}, %[tile], %[tbytes]
 s_mul_hi_u32 {T5H}, %[tile], %[tbytes]
 v_lshl_add_u64 {BASE}, %[lb], 0, {T5}
 .Lsbd%=:
-""" + realign + """
+""" + tailfix + """
 s_bitcmp1_b32 %[fl], 7
 s_cbranch_scc0 .Lnx%=
 v_min_u32 {LEN}, 0xffff, {LEN}
@@ -1651,8 +1649,8 @@ v_mov_b32 {t11}, %[lenc]
 .Lnl2d%=:
 s_waitcnt lgkmcnt(0)
 ; every packet of the next tile 16-byte aligned (lanes of length 0 excepted): DMA'd as they are;
-; else from 16-byte aligned sources and realigned at its top -- or staged by the C++ when this
-; is the statement's last tile (v[56:59] do not survive the return)
+; else straight from the packets, the tail lanes from aligned blocks (fixed at its top: %[mis]
+; bit 1, bit 0 once it is this tile)
 v_add_u32 {t0}, %[fr_lo], {t6}
 v_and_b32 {t0}, 15, {t0}
 v_cmp_ne_u32 vcc, 0, {t0}
@@ -1663,23 +1661,15 @@ s_cbranch_vccnz .Lmis%=
 """ + dmas + """
 s_branch .Lmeta%=
 .Lmis%=:
-s_cmp_eq_u32 %[cdn], 1
-s_cbranch_scc1 .Lstg%=
+; (no packet shorter than the window: no tail lanes, the chunks straight from the packets)
+v_cmp_gt_u32 vcc, 64, {t7}
+s_cbranch_vccz .Lmnt%=
 s_or_b32 %[mis], %[mis], 2
-; the lane's 16 bytes past its window: its packet's [64 - m, 80 - m), when it reaches them
-v_add_u32 {t1}, {t7}, {t0}
-v_cmp_lt_u32 vcc, 64, {t1}
-v_cmp_ne_u32_e64 {T1}, 0, {t0}
-s_and_b64 exec, vcc, {T1}
-s_cbranch_execz .Lmx%=
-v_mov_b32 {t2}, {t6}
-v_mov_b32 {t3}, 0
-v_lshl_add_u64 {T23}, %[k_frames], 0, {T23}
-v_and_b32 {t2}, -16, {t2}
-global_load_dwordx4 v[56:59], {T23}, off offset:64
-.Lmx%=:
-s_mov_b64 exec, -1
-""" + mrounds + """
+""" + trounds + """
+""" + dmas + """
+s_branch .Lmeta%=
+.Lmnt%=:
+""" + rounds + """
 """ + dmas + """
 s_branch .Lmeta%=
 .Lsn%=:

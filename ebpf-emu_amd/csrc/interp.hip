@@ -326,6 +326,26 @@ __device__ __forceinline__ void dma_window(const LaunchArgs& a, const WaveLds& L
   }
 }
 
+// The same for packets at any 4-byte aligned address (the var tile loop, gen_tile.py
+// jit_statement_varl): chunk c straight from packet + 16c, except a chunk that would read past the
+// 16-byte block holding the packet's last byte (16c + 16 + m > ceil16(m + len), m = packet & 15),
+// which moves the aligned block below, (packet + 16c) & ~15 -- the statement shifts that slot into
+// place at the tile's top (its tailfix, %[mis] bit 0).
+__device__ __forceinline__ void dma_window_any(const LaunchArgs& a, const WaveLds& L, uint64_t t,
+                                               uint32_t lane) {
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const uint32_t j = r * 16 + (lane >> 2);
+    uintptr_t bj;
+    uint32_t lj;
+    meta_of<true>(a, L, 0, t, j, bj, lj);
+    const uint32_t c = (lane & 3) ^ win_swz(j), m = (uint32_t)(bj & 15);
+    uintptr_t src = bj + c * 16;
+    if (c * 16 + 16 + m > ((m + lj + 15) & ~15u)) src &= ~(uintptr_t)15;
+    dma_x4(c * 16 < lj ? src : (uintptr_t)a.prog, lds_addr(L.win + r * 1024));
+  }
+}
+
 // Stride layout with 16-byte aligned slots of >= kWin bytes: every packet's whole window is
 // inside its slot (the C ABI requires n * stride bytes of frames), so tile t's windows can be
 // DMA'd without its lengths -- i.e. in the same HBM round trip as the lengths. Bytes past a
@@ -1373,8 +1393,12 @@ hipError_t launch_binning(const uint16_t* lens, uint64_t n, uint32_t* wgc, uint3
 
 // Image chunk c (image bytes [16c, 16c + 16)) of a packet of len bytes at src: the ctx {data = 8,
 // data_end = 8 + len} in its first 8 bytes, packet byte b at image byte 8 + b, zeros at or past
-// 8 + len. Two aligned 16-byte source blocks and a funnel shift (v_alignbyte) per dword.
+// 8 + len. A chunk inside the packet is one 16-byte load at its (unaligned) address; the first
+// and the last: two aligned 16-byte source blocks and a funnel shift (v_alignbyte) per dword.
+typedef uint4 __attribute__((aligned(1))) uint4_any;  // (any address: tools/probe_dma_align.hip)
 __device__ __forceinline__ uint4 xdp_image_chunk(const uint8_t* src, uint32_t len, uint32_t c) {
+  // a chunk wholly inside the packet (packet bytes [16c - 8, 16c + 8)): one load, as it lies
+  if (c != 0 && 16 * c + 8 <= len) return *(const uint4_any*)(src + 16 * c - 8);
   const uintptr_t s0 = (uintptr_t)src, end = s0 + len;
   const uintptr_t p = s0 + 16ull * c - 8;  // the source address of image byte 16c
   const uintptr_t a0 = p & ~(uintptr_t)15;
@@ -1904,15 +1928,14 @@ extern "C" __global__ __launch_bounds__(kBlock, 7) void ebpf_tile_jit_var(Launch
 // ... in one asm statement (tile_jit_varl.inc, gen_tile.py jit_statement_varl) with two window
 // buffers and two packed metadata buffers per wave (kVarlWaveLds; 4 workgroups of 4 waves per
 // CU), so a tile's windows are in flight while the one before it runs. Tiles whose packets are
-// not all 16-byte aligned (a capture's records) are DMA'd from aligned sources plus 16 bytes per
-// lane in v[56:59], and shifted into place in LDS at their turn (realign). The C++ here only
-// starts the wave's first tile, stages the windows of a tile the statement hands back (the
-// batch's partial last tile, a misaligned tile after the statement's last) and unpacks the
-// per-lane packed counter buckets.
+// not all 16-byte aligned (a capture's records) are DMA'd straight from the packets (the last
+// chunk of a short packet from the aligned block below, shifted into place at the tile's top).
+// The C++ here only starts the wave's first tile, stages the windows of a tile the statement
+// hands back (the batch's partial last tile) and unpacks the per-lane packed counter buckets.
 #define VARL_OPERANDS \
         : [tile] "+s"(tile), [winb] "+s"(winb), [nwinb] "+s"(nwinb), [metab] "+s"(metab), \
           [nmetab] "+s"(nmetab), [acc] "+v"(acc), [ret] "+v"(ret), [cdn] "=&s"(cdn), \
-          [stage] "=&s"(stg), [mis] "=&s"(mis), [dmask] "=&s"(dmask) \
+          [stage] "=&s"(stg), [mis] "+s"(mis), [dmask] "=&s"(dmask) \
         : [ka] "s"(ka), [k_frames] "s"(a.frames), [fr_lo] "s"((uint32_t)(uintptr_t)a.frames), \
           [of_lo] "s"((uint32_t)(uintptr_t)a.offsets), \
           [of_hi] "s"((uint32_t)((uintptr_t)a.offsets >> 32)), \
@@ -1931,7 +1954,7 @@ extern "C" __global__ __launch_bounds__(kBlock, 7) void ebpf_tile_jit_var(Launch
           [o_init] "i"(offsetof(LaunchArgs, init_regs)), [o_r0] "i"(offsetof(LaunchArgs, r0)), \
           [o_status] "i"(offsetof(LaunchArgs, status)), \
           [o_regs] "i"(offsetof(LaunchArgs, regs_out)) \
-        : TILE_ASM_CLOBBER, TILE_ASM_CLOBBER_WINDOW, "v56", "v57", "v58", "v59"
+        : TILE_ASM_CLOBBER, TILE_ASM_CLOBBER_WINDOW
 template <bool STACK>
 __device__ __forceinline__ void varl_body(LaunchArgs& a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -1991,6 +2014,7 @@ __device__ __forceinline__ void varl_body(LaunchArgs& a) {
   uint32_t cnt[7] = {0, 0, 0, 0, 0, 0, 0};
   uint64_t retired = 0;
   uint32_t tile = blockIdx.x * kWavesPerBlock + wv;
+  uint32_t mis = 0;  // bit 0: the current tile's windows came from unaligned packets (tailfix)
   // the first two tiles' metadata at once, before the workgroup's start barrier (as the
   // fixed-slot kernel's first DMA); then the first tile's windows (DMA'd when whole and aligned):
   // the statement's first wait is for those windows alone. (Tried: both first tiles' windows in
@@ -2008,12 +2032,17 @@ __device__ __forceinline__ void varl_body(LaunchArgs& a) {
     uint32_t ml;
     meta_of<true>(a, X, 0, tile, lane, pb, ml);
     const bool whole = (uint64_t)(tile + 1) * kWave <= a.n;
-    if (whole && ballot(ml != 0 && (pb & 15) != 0) == 0) dma_window<true>(a, X, 0, 0, tile, lane);
-    else stage(tile, X);
+    if (whole) {
+      mis = ballot(ml != 0 && (pb & 15) != 0) != 0 ? 1u : 0u;
+      if (mis) dma_window_any(a, X, tile, lane);
+      else dma_window<true>(a, X, 0, 0, tile, lane);
+    } else {
+      stage(tile, X);
+    }
   }
   while (tile < ntiles) {
     uint64_t acc = 0;
-    uint32_t ret = 0, cdn, stg, mis;
+    uint32_t ret = 0, cdn, stg;
     uint64_t dmask;  // (store mode: the lanes whose overflow image is live, per tile)
     if constexpr (STACK) {
       asm volatile(
@@ -2040,9 +2069,11 @@ __device__ __forceinline__ void varl_body(LaunchArgs& a) {
       if (b < 6) cnt[b + 1] += s >> 16;
     }
     retired += wave_sum_u32(ret);
+    mis = rfl(mis);
     if (tile < ntiles && stg) {  // a tile the statement hands back: stage its windows
       dma_wait();                // (the next tile's metadata)
       stage(tile, buf(winb, metab));
+      mis = 0;
     }
   }
   uint64_t cnt64[7];

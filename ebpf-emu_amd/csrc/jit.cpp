@@ -3165,12 +3165,6 @@ bool compile_into_template(Compiler& c, Compiler* xc, std::vector<char>& code_ob
       b = "s_mov_b64 exec, 0  ; (not this program's kernel)\n";
     else
       ok = xc ? c.body_loop(m, *xc, b) : c.body(m, b);
-    // (the var tile loop keeps a misaligned next tile's last 16 bytes per lane in v[56:59] across
-    // the program, gen_tile.py jit_statement_varl: its code must not name them)
-    if (ok && m.varl && Compiler::touches(b, 56, 59)) {
-      if (err) *err = "var tile loop program names v[56:59]";
-      return false;
-    }
     if (!ok) {
       if (err) *err = c.err;
       return false;

@@ -249,3 +249,85 @@ def test_nat_long_options_no_deopt(cuda, oracle_mod, layout):
         if s == 0:
             assert int(r0n[i]) == o0, (layout, i)
     prog.close()
+
+
+# a packet byte picks where the program stores (r1 + 2 * byte: 0..510, through a register): in
+# the header window, in the overflow image [64, 128) or past it -- the last deoptimize (about
+# three lanes in four)
+DEOPT_PROG = """
+    ldxb r3, [r1+14]
+    lsh r3, 1
+    mov r4, r1
+    add r4, r3
+    stb [r4+0], 0x5a
+    ldxb r0, [r4+0]
+    ldxb r5, [r1+20]
+    add r0, r5
+    and r0, 3
+    exit
+"""
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layout", ["fixed128", "offsets_mis3", "big"])
+def test_deopt_list_rerun(cuda, oracle_mod, layout):
+    """A store-mode batch where most lanes deoptimize (a store at or past byte 128: past the
+    overflow image): the var tile loop lists them, the deopt pass re-runs them on the general
+    interpreter (host.cpp, LaunchArgs::deopt_pass). 128-byte slots, unaligned offsets + lens and
+    300 000 packets; two launches on one workspace (the pass resets the list's words for the
+    next); status, r0 and counters == the general interpreter's == the oracle's, and the re-run
+    count (workspace +8) == the lanes whose store lands at or past byte 128."""
+    import torch
+
+    from ebpf_emu import Program, _lib
+    from ebpf_emu.asm import assemble
+    from test_stack_tier import VAR_LAYOUTS, _fixed_frames
+
+    img = assemble(DEOPT_PROG)
+    rng = random.Random(404 + len(layout))
+    n = 300_000 if layout == "big" else 3000
+    pkts = [bytes(rng.getrandbits(8) for _ in range(rng.choice([0, 10, 15, 21, 60, 64, 100, 128])))
+            for _ in range(n)]
+    prog = Program(img)
+    if layout != "offsets_mis3":
+        stride = 128
+        pk = [p[:stride].ljust(stride, b"\0") for p in pkts]
+        frames = _fixed_frames(pk, stride, cuda)
+        kw = dict(n=len(pk), stride=stride)
+    else:
+        from test_gpu_parity import _stage
+
+        pk = pkts
+        frames, kw = _stage(pkts, cuda, **VAR_LAYOUTS[layout])
+    b = prog.make_batch(frames, **kw)
+    assert prog.batch_kernel(b) == _lib.EBPF_KERNEL_JIT_VARL_STACK
+    ws = torch.zeros(prog.workspace_bytes(b, 0), dtype=torch.uint8, device=cuda)
+    b = prog.make_batch(frames, workspace=ws, **kw)
+    gcnt = torch.zeros(8, dtype=torch.int64, device=cuda)
+    gen = prog.run(frames, r0=True, status=True, generic=True, counters=gcnt, **kw)
+    op = oracle_mod.Program(img)
+    want_rerun = sum(1 for p in pk if len(p) > 14 and 2 * p[14] >= 128)
+    assert want_rerun > n // 2
+    for rep in range(2):
+        out = _lib.BatchOut()
+        r0 = torch.empty(len(pk), dtype=torch.int64, device=cuda)
+        st = torch.empty(len(pk), dtype=torch.uint8, device=cuda)
+        cnt = torch.zeros(8, dtype=torch.int64, device=cuda)
+        out.r0, out.status, out.counters = r0.data_ptr(), st.data_ptr(), cnt.data_ptr()
+        prog.launch(b, out, torch.cuda.current_stream())
+        torch.cuda.synchronize()
+        words = ws[:16].cpu().numpy().view(np.uint32)
+        # the list's count and done words (launch.h kWsDeoptOff) reset for the next launch
+        assert words[0] == 0 and words[1] == 0, (rep, words)
+        assert words[2] == want_rerun, (rep, words[2], want_rerun)
+        assert torch.equal(st, gen.status), rep
+        ok = st == 0
+        assert torch.equal(r0[ok], gen.r0[ok]), rep
+        assert torch.equal(cnt, gcnt), (rep, cnt, gcnt)
+        stn, r0n = st.cpu().numpy(), r0.cpu().numpy().view(np.uint64)
+        for i in range(0, len(pk), 1 if n <= 3000 else 97):
+            s, o0, _ = op.run_packet(pk[i], 1024, 512, 1 << 22)
+            assert stn[i] == s, (layout, i)
+            if s == 0:
+                assert int(r0n[i]) == o0, (layout, i)
+    prog.close()

@@ -2,8 +2,9 @@
 or a NIC ring's layout -- of compiled forward programs, the wave's tiles in one asm statement with
 double-buffered windows. Every output against the C oracle (oracle/, restating emu.rs / mmu.rs /
 main.rs) and against the general interpreter on the same batch, bit-exact: aligned tiles (LDS-DMA
-windows), misaligned and partial tiles (handed back to the C++ and staged lane by lane), packets
-shorter than the window, lengths absent, init_regs / r0 / status / register outputs, xdp_md in
+windows), tiles of unaligned packets (DMA'd straight from the packets, a short packet's last chunk
+from the aligned block below and shifted in LDS), partial tiles (handed back to the C++ and
+staged lane by lane), packets shorter than the window, lengths absent, init_regs / r0 / status / register outputs, xdp_md in
 place, and a wave running more than the 511 tiles of one statement entry."""
 import os
 import random
@@ -17,14 +18,17 @@ from test_gpu_parity import STEPS, _check_prod_against_oracle
 pytestmark = pytest.mark.gpu
 
 
-def _mixed(pkts, dev, bad_every=0, lens=True):
+def _mixed(pkts, dev, bad_every=0, lens=True, align=None):
     """Offsets layout, every packet 16-byte aligned except each bad_every-th one (at +3): a tile
-    holding one is staged. Returns (frames, kwargs)."""
+    holding one is DMA'd straight from its unaligned packets. align(i) -> the packet's address
+    mod 16 instead, when given. Returns (frames, kwargs)."""
     import torch
 
     offs, pos, chunks = [], 0, []
     for i, p in enumerate(pkts):
         want = 3 if bad_every and i % bad_every == bad_every - 1 else 0
+        if align is not None:
+            want = align(i)
         pad = (want - pos) % 16
         chunks.append(bytes(pad))
         pos += pad
@@ -124,6 +128,52 @@ def test_varl_fuzz(cuda, oracle_mod, seed):
         prog.close()
         done += 1
     assert done >= 15
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_varl_any_alignment(cuda, oracle_mod, seed):
+    """Every packet at a random address mod 16 (0..15) and 0..80 bytes long, so most tiles are
+    DMA'd from unaligned packets and short packets' last chunks take the aligned-block path and
+    the shift at the tile's top (gen_tile.py tailfix): random forward programs and the bench
+    programs, every output == the oracle's and == the general interpreter's, registers included;
+    one capture-like batch (records at 8 mod 16) of the 5-tuple too."""
+    from ebpf_emu import Program, _lib
+    from ebpf_emu import workloads as W
+
+    rng = random.Random(7300 + seed)
+    imgs = [W.program(n) for n in ("5tuple", "acl", "mac_swap_tx", "5tuple_xdp", "nat")]
+    while len(imgs) < 16:
+        img = gen_program(rng, allow_loops=False, tier0=True)
+        try:
+            oracle_mod.Program(img)
+        except oracle_mod.OracleDecodeError:
+            continue
+        imgs.append(img)
+    done = 0
+    for it, img in enumerate(imgs):
+        prog = Program(img)
+        if not prog.forward_only:
+            prog.close()
+            continue
+        n = rng.choice([64, 128, 200, 640])
+        pkts = [(gen_packet(rng) + bytes(rng.getrandbits(8) for _ in range(80)))[
+            :rng.choice([0, 1, 7, 15, 16, 17, 33, 47, 48, 49, 63, 64, 65, 80])] for _ in range(n)]
+        fixed_m = rng.choice([None, 8, 4, 1])
+        frames, kw = _mixed(pkts, cuda, align=(lambda i: fixed_m) if fixed_m is not None
+                            else (lambda i: rng.randrange(16)))
+        k = _route(prog, frames, kw, max_steps=STEPS)
+        if k not in (_lib.EBPF_KERNEL_JIT_VARL, _lib.EBPF_KERNEL_JIT_VARL_STACK):
+            prog.close()
+            continue
+        regs = k == _lib.EBPF_KERNEL_JIT_VARL  # (store mode: the production outputs)
+        got = _outputs(prog, frames, kw, cuda, regs=regs)
+        ref = _outputs(prog, frames, kw, cuda, generic=True, regs=regs)
+        ctx = f"seed {seed} it {it} m {fixed_m} kernel {k} prog {img.hex()}"
+        _same(got, ref, ctx)
+        _check_prod_against_oracle(oracle_mod, img, pkts, got, tag=ctx)
+        prog.close()
+        done += 1
+    assert done >= 8
 
 
 @pytest.mark.parametrize("name", ["5tuple", "drop", "acl", "5tuple_stack", "mac_swap_tx"])
