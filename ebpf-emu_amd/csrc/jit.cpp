@@ -1977,11 +1977,57 @@ struct Compiler {
     // the packet's dwords that hold a packet byte, zeros past its end)
     std::string far = ".Lfar" + U + ":\n" + (loop ? "v_min_u32 v41, 63, v41\n" : "") + win +
                       "s_mov_b64 s[66:67], exec\ns_mov_b64 exec, s[68:69]\n";
-    if (smode)  // straddling the window's end: deoptimize (they leave both lane sets)
+    if (smode && dm.empty())  // straddling the window's end: deoptimize (they leave both lane sets)
       far += "v_cmp_gt_u32 vcc, 64, v36\ns_and_b64 vcc, vcc, exec\ns_cbranch_vccz .Lnd" + U + "\n"
              "s_andn2_b64 s[66:67], s[66:67], vcc\ns_andn2_b64 s[68:69], s[68:69], vcc\n"
              "s_mov_b64 exec, vcc\nv_mov_b32 v30, 0x80\nv_mov_b32 v28, -1\n"
              "s_mov_b64 exec, s[68:69]\n.Lnd" + U + ":\n";
+    if (smode && !dm.empty() && w > 1) {
+      // straddling the window's end (a < 64 < a + w, so 57 <= a <= 63): bytes [a, 64) from the
+      // window in LDS (stored ones included), bytes [64, a + w) from the overflow image (lanes
+      // that stored there: the dirty mask) or the packet (zeros at or past LEN); the value is the
+      // bytes [56, 72) shifted down by a - 56
+      far += "v_cmp_gt_u32 vcc, 64, v36\ns_and_b64 s[60:61], vcc, exec\n"
+             "s_cbranch_scc0 .Lnd" + U + "\n"
+             "s_mov_b64 exec, s[60:61]\n"
+             "v_mov_b32 v42, 56\nv_xad_u32 v43, v35, v42, v34\nds_read_b32 v49, v43\n"
+             "v_mov_b32 v42, 60\nv_xad_u32 v43, v35, v42, v34\nds_read_b32 v50, v43\n"
+             "v_mov_b32 v46, 0\nv_mov_b32 v47, 0\n"
+             // clean lanes: the packet's dwords at 64 and 68 that start before LEN
+             "s_andn2_b64 exec, s[60:61], " + dm + "\n"
+             "s_cbranch_execz .Lsc" + U + "\n"
+             "s_mov_b64 s[64:65], exec\n"
+             "v_cmp_lt_u32 vcc, 64, v31\ns_and_b64 exec, s[64:65], vcc\n"
+             "global_load_dword v46, v[32:33], off offset:64\n"
+             "v_cmp_lt_u32 vcc, 0x44, v31\ns_and_b64 exec, s[64:65], vcc\n"
+             "global_load_dword v47, v[32:33], off offset:68\n"
+             "s_mov_b64 exec, s[64:65]\ns_waitcnt vmcnt(0)\n"
+             // (the bytes at or past LEN: min(8, LEN - 64) valid, 0 when LEN <= 64)
+             "v_subrev_u32 v42, 64, v31\nv_cmp_lt_u32 vcc, 64, v31\nv_cndmask_b32 v42, 0, v42, vcc\n"
+             "v_min_u32 v42, 8, v42\nv_lshlrev_b32 v42, 3, v42\nv_sub_u32 v42, 64, v42\n"
+             "v_lshlrev_b64 v[46:47], v42, v[46:47]\nv_lshrrev_b64 v[46:47], v42, v[46:47]\n"
+             "v_cndmask_b32 v46, 0, v46, vcc\nv_cndmask_b32 v47, 0, v47, vcc\n"
+             ".Lsc" + U + ":\n"
+             // dirty lanes: the overflow image's first two dwords
+             "s_and_b64 exec, s[60:61], " + dm + "\n"
+             "s_cbranch_execz .Lsd" + U + "\n" + ovf_addr() +
+             "global_load_dword v46, v[44:45], off sc1\n"
+             "global_load_dword v47, v[44:45], off offset:4 sc1\n"
+             "s_waitcnt vmcnt(0)\n"
+             ".Lsd" + U + ":\n"
+             "s_mov_b64 exec, s[60:61]\n"
+             "s_waitcnt lgkmcnt(0)\n"
+             // dwords [56, 72) = v49 v50 v46 v47; a - 56 = 4q + (a & 3)
+             "v_cmp_gt_u32 vcc, 60, v36\n"
+             "v_cndmask_b32 v42, v50, v49, vcc\nv_cndmask_b32 v43, v46, v50, vcc\n"
+             "v_cndmask_b32 v48, v47, v46, vcc\n"
+             "v_alignbyte_b32 v26, v43, v42, v36\nv_alignbyte_b32 v27, v48, v43, v36\n"
+             // (these lanes are done: out of the far set; back with the others at the merge)
+             "s_andn2_b64 s[68:69], s[68:69], s[60:61]\n"
+             "s_mov_b64 exec, s[68:69]\n.Lnd" + U + ":\n";
+    } else if (smode && !dm.empty()) {
+      far += ".Lnd" + U + ":\n";
+    }
     if (smode && !dm.empty()) {
       // lanes that stored past byte 64 (the dirty mask): their bytes [64, 128) from the overflow
       // image; an access ending past 128 deoptimizes (its high bytes would be the packet's)

@@ -331,3 +331,89 @@ def test_deopt_list_rerun(cuda, oracle_mod, layout):
             if s == 0:
                 assert int(r0n[i]) == o0, (layout, i)
     prog.close()
+
+
+# a pointer to image byte 57..64 (a packet byte picks it); a store just below it into the window,
+# on every other packet a store past byte 64 (the overflow image: the lane is dirty), then 8-, 4-
+# and 2-byte loads through it that straddle the window's end
+STRADDLE_PROG = """
+    ldxb r3, [r1+14]
+    and r3, 7
+    mov r4, r1
+    add r4, r3
+    add r4, 57
+    stb [r4-1], 0x33
+    ldxb r5, [r1+15]
+    and r5, 1
+    jeq r5, 0, nost
+    stb [r4+8], 0x77
+nost:
+    ldxdw r0, [r4+0]
+    ldxw r6, [r4+0]
+    ldxh r7, [r4+1]
+    xor r0, r6
+    xor r0, r7
+    exit
+"""
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layout", ["fixed128", "offsets_mis3", "xdp_offsets"])
+def test_straddling_loads_no_deopt(cuda, oracle_mod, layout):
+    """Store mode on the var tile loop: a load that starts in the header window and ends past
+    byte 64 reads its low bytes from the window in LDS (stored ones included) and its high bytes
+    from the overflow image (lanes that stored there) or the packet (zeros at or past LEN) --
+    jit.cpp ldx_fixed -- instead of deoptimizing: the deopt pass re-runs no packet, and every
+    output == the general interpreter's == the oracle's. Packets of 0..100 bytes, so LEN falls
+    inside, before and after the straddled bytes."""
+    import torch
+
+    from ebpf_emu import Program, _lib
+    from ebpf_emu.asm import assemble
+    from test_stack_tier import VAR_LAYOUTS, _fixed_frames, _images_of
+
+    img = assemble(STRADDLE_PROG)
+    rng = random.Random(99 + len(layout))
+    pkts = [bytes(rng.getrandbits(8) for _ in range(rng.choice([0, 15, 16, 40, 60, 64, 65, 66, 68,
+                                                                  70, 71, 72, 80, 100])))
+            for _ in range(3000)]
+    prog = Program(img)
+    assert prog.store_mode
+    if layout.startswith("fixed"):
+        stride = int(layout[5:])
+        pk = [p[:stride].ljust(stride, b"\0") for p in pkts]
+        frames = _fixed_frames(pk, stride, cuda)
+        kw = dict(n=len(pk), stride=stride)
+        xdp = False
+    else:
+        from test_gpu_parity import _stage
+
+        spec = dict(VAR_LAYOUTS[layout])
+        xdp = spec.pop("xdp", False)
+        pk = pkts
+        frames, kw = _stage(pkts, cuda, **spec)
+    b = prog.make_batch(frames, xdp_md=xdp, **kw)
+    ws = torch.zeros(prog.workspace_bytes(b, 0), dtype=torch.uint8, device=cuda)
+    b = prog.make_batch(frames, xdp_md=xdp, workspace=ws, **kw)
+    assert prog.batch_kernel(b) == _lib.EBPF_KERNEL_JIT_VARL_STACK
+    out = _lib.BatchOut()
+    r0 = torch.empty(len(pk), dtype=torch.int64, device=cuda)
+    st = torch.empty(len(pk), dtype=torch.uint8, device=cuda)
+    ws[8:12] = 0xFF
+    out.r0, out.status = r0.data_ptr(), st.data_ptr()
+    prog.launch(b, out, torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    assert ws[8:12].cpu().numpy().view(np.uint32)[0] == 0, "lanes deoptimized"
+    gen = prog.run(frames, r0=True, status=True, generic=True, xdp_md=xdp, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(st, gen.status)
+    ok = st == 0
+    assert torch.equal(r0[ok], gen.r0[ok])
+    op = oracle_mod.Program(img)
+    stn, r0n = st.cpu().numpy(), r0.cpu().numpy().view(np.uint64)
+    for i, im in enumerate(_images_of(pk, xdp)):
+        s, o0, _ = op.run_packet(im, 1024, 512, 1 << 22)
+        assert stn[i] == s, (layout, i)
+        if s == 0:
+            assert int(r0n[i]) == o0, (layout, i)
+    prog.close()
