@@ -1384,10 +1384,11 @@ hipError_t launch_binning(const uint16_t* lens, uint64_t n, uint32_t* wgc, uint3
 // [packet bytes] -- the bytes main.rs would be handed for a standard XDP program. One workgroup
 // stages 256 packets: it sizes their 16-byte aligned slots, reserves its range with one device
 // atomic (workgroups pack in arrival order; every packet keeps its index through the offsets),
-// then writes the range's 16-byte chunks: thread t the chunks t, t + 256, ... of the range (each
-// mapped to its packet by a binary search over the slot prefix sums in LDS), so consecutive
-// threads store consecutive chunks whatever the packets' lengths. An image longer than mem_size
-// is not copied: its length alone makes the batch fault it ST_BADPKT (main.rs:20-21).
+// then writes the range's 16-byte chunks: each wave a quarter of the range, its lanes on
+// consecutive chunks (each mapped to its packet through the slot prefix sums in LDS), so a wave
+// stores 1 KB of contiguous chunks per instruction whatever the packets' lengths. An image
+// longer than mem_size is not copied: its length alone makes the batch fault it ST_BADPKT
+// (main.rs:20-21).
 // (Round 4 copied short images a thread each and long ones a wave each, every chunk from four
 // bounds-checked dword loads: 675 us for a 1 Mi mixed 64/1500-byte batch.)
 
@@ -1457,18 +1458,31 @@ __global__ __launch_bounds__(256) void xdp_stage(const uint8_t* __restrict__ fra
   }
   uint8_t* const o = dst + base;
   const uint32_t chunks = pre[255] / 16;
-  // four chunks per thread per round, their loads all in flight before any store (the chunks'
-  // packets: the first j with pre[j] > 16k, walked forward -- k only grows)
+  // wave w writes the w-th quarter of the range, lane l the chunks l, l + 64, ... of it, four in
+  // flight before any store (each chunk's packet: the first j with pre[j] > 16k, found by a binary
+  // search for the lane's first chunk, then walked forward -- k grows by 64 chunks, about one
+  // packet of the mixed batch)
+  const uint32_t wv = t >> 6, ln = t & 63, q = (chunks + 3) / 4;
+  const uint32_t kb = min(wv * q, chunks), ke = min(kb + q, chunks);
   uint32_t j = 0;
-  for (uint32_t k0 = t; k0 < chunks; k0 += 4 * 256) {
+  if (kb + ln < ke) {
+    uint32_t lo = 0, hi = 255;  // (pre[255] > 16 k for every k < chunks)
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (pre[mid] <= 16 * (kb + ln)) lo = mid + 1;
+      else hi = mid;
+    }
+    j = lo;
+  }
+  for (uint32_t k0 = kb + ln; k0 < ke; k0 += 4 * 64) {
     uint4 v[4];
     uint32_t kk[4];
 #pragma unroll
     for (int u = 0; u < 4; u++) {
-      const uint32_t k = k0 + 256 * u;
+      const uint32_t k = k0 + 64 * u;
       kk[u] = k;
       v[u] = make_uint4(0u, 0u, 0u, 0u);
-      if (k >= chunks) continue;
+      if (k >= ke) continue;
       while (pre[j] <= 16 * k) j++;
       const uint32_t lj = len_s[j];
       if (lj == 0xFFFFFFFFu) {
@@ -1479,7 +1493,7 @@ __global__ __launch_bounds__(256) void xdp_stage(const uint8_t* __restrict__ fra
     }
 #pragma unroll
     for (int u = 0; u < 4; u++)
-      if (kk[u] < chunks) *(uint4*)(o + 16ull * kk[u]) = v[u];
+      if (kk[u] < ke) *(uint4*)(o + 16ull * kk[u]) = v[u];
   }
 }
 
