@@ -1050,6 +1050,8 @@ static StackAnalysis analyze_stack(const std::vector<Uop>& uops) {
   res.plan.any_pw = any_pw;
   res.plan.dyn = std::move(dyns);
   res.plan.any_dyn = any_dyn;
+  // (store mode: whether the deopt pass can be left out for main.rs-layout batches, jit.cpp)
+  res.plan.no_deopt = any_dyn && store_mode_no_deopt(uops, res.plan);
   return res;
 }
 
@@ -1828,6 +1830,10 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* bin, const ebpf_batch_out* ou
   const bool deopt = (stk && p->stack.any_dyn && kind == kKindDag && jit &&
                       (kid == EBPF_KERNEL_JIT_VAR_STACK || kid == EBPF_KERNEL_JIT_VARL_STACK)) ||
                      (promo && jit);
+  // store mode on the var tile loop with no lane able to leave (StackPlan::no_deopt: the main.rs
+  // registers, the stack window at or past the overflow image's end): no deopt pass
+  const bool pass = deopt && !(kid == EBPF_KERNEL_JIT_VARL_STACK && p->stack.no_deopt &&
+                               !b->init_regs && b->r10 >= 128ull + p->stack.k);
   if (deopt) {
     a.deopt = (uint32_t*)(ws + kWsDeoptOff);
     // (past the tier-1 slots, or the binned order and its class counts when the batch is binned)
@@ -1837,7 +1843,7 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* bin, const ebpf_batch_out* ou
     if (p->stack.any_dyn) a.ovf = (uint8_t*)a.deopt_idx + align16(b->n * 4);
   }
   hipError_t e = launch_interp(kind, a, grid, s, jit, stk);
-  if (deopt && e == hipSuccess) {
+  if (pass && e == hipSuccess) {
     LaunchArgs d = a;
     d.deopt_pass = 1;
     d.n_uops = (uint32_t)p->uops.size();

@@ -1351,6 +1351,7 @@ struct Compiler {
     std::string ool;
     std::string main = "; compiled eBPF program (store mode): " + std::to_string(n) + " micro-ops\n"
                        "s_mov_b32 s52, s33\ns_mov_b32 s53, 0\n";
+    if (stk->no_deopt) main += "; store mode: no lane can deoptimize (store_mode_no_deopt)\n";
     if (!dm.empty()) main += "s_mov_b64 " + dm + ", 0\n";
     // (the var tile loop's windows hold packet bytes [0, 64): the xdp_md ctx shifted in first, as
     // body does; the var kernel's C++ shifts them itself)
@@ -3228,6 +3229,113 @@ bool compile_into_template(Compiler& c, Compiler* xc, std::vector<char>& code_ob
 }
 
 }  // namespace
+
+// Store mode on the var tile loop (ebpf_tile_jit_varl_stack): can any lane deoptimize? A forward
+// dataflow of the registers' value ranges (Compiler::av_step, the main.rs layout: r1 = 0 the
+// image's start, r2 = LEN; stores change no register, an atomic's fetch makes its registers
+// unknown) bounds every access's address at every reachable micro-op. No lane can leave when
+//   * every register-address store ends at or below byte 128 (the overflow image's end; the host
+//     also needs the stack window to start at or past 128), and
+//   * if any such store may end past byte 64 (a lane may be dirty: jit.cpp ovf_*), every
+//     register-address load ends at or below 128 and no constant-address load ends past 64 (a
+//     dirty lane would leave at either).
+// Loads straddling byte 64 are served (ldx_fixed); addresses below 0 or past mem_size fault,
+// which is not a deoptimization. Calls: no proof. (`why`: the first micro-op that failed.)
+bool store_mode_no_deopt(const std::vector<Uop>& uops, const StackPlan& stk, uint32_t* why) {
+  using AbsVal = Compiler::AbsVal;
+  using AbsRegs = Compiler::AbsRegs;
+  const uint32_t n = (uint32_t)uops.size();
+  if (why) *why = UINT32_MAX;
+  if (!stk.any_dyn || stk.dyn.size() != n || stk.off.size() != n || stk.pw.size() != n) return false;
+  for (uint32_t i = 0; i < n; i++)
+    if (uops[i].op == U_CALL) {
+      if (why) *why = i;
+      return false;
+    }
+  std::vector<AbsRegs> in(n);
+  std::vector<char> seen(n, 0);
+  AbsRegs init;
+  for (int r = 0; r < 11; r++) init[r] = Compiler::av_const(0);
+  init[2] = AbsVal();
+  init[2].hi = Compiler::kLenMax, init[2].slack = 0, init[2].is_len = true;  // r2 = LEN
+  init[10] = AbsVal();                                                      // r10: a launch value
+  std::vector<uint32_t> work{0};
+  in[0] = init;
+  seen[0] = 1;
+  auto flow = [&](uint32_t to, const AbsRegs& st) {
+    if (to >= n) return;
+    if (!seen[to]) {
+      in[to] = st, seen[to] = 1, work.push_back(to);
+      return;
+    }
+    AbsRegs m;
+    bool ch = false;
+    for (int r = 0; r < 11; r++) {
+      m[r] = Compiler::av_meet(in[to][r], st[r]);
+      ch = ch || !Compiler::av_eq(m[r], in[to][r]);
+    }
+    if (ch) in[to] = m, work.push_back(to);
+  };
+  for (size_t steps = 0; !work.empty(); steps++) {
+    if (steps > 100000) return false;  // (forward programs settle far sooner)
+    const uint32_t i = work.back();
+    work.pop_back();
+    const Uop& u = uops[i];
+    if ((u.op >= U_JA && u.op <= U_JLE32 && (uint32_t)u.x <= i) ) return false;  // (a back edge)
+    AbsRegs nt, tk;
+    Compiler::av_step(u, in[i], nt, tk, false);
+    if (u.op == U_ATOMIC) {  // (fetch forms write src, CMPXCHG writes r0)
+      nt[u.src] = AbsVal();
+      nt[0] = AbsVal();
+    }
+    if (u.op == U_EXIT || u.op == U_FAULT) continue;
+    if (u.op == U_JA) {
+      flow((uint32_t)u.x, tk);
+      continue;
+    }
+    if (u.op >= U_JEQ && u.op <= U_JLE32) flow((uint32_t)u.x, tk);
+    flow(i + 1, nt);
+  }
+  // the largest end of a register-address store / load, of a constant-address load
+  uint64_t st_end = 0, ld_end = 0, kld_end = 0;
+  uint32_t st_at = UINT32_MAX, ld_at = UINT32_MAX, kld_at = UINT32_MAX;
+  for (uint32_t i = 0; i < n; i++) {
+    if (!seen[i]) continue;
+    const Uop& u = uops[i];
+    const int64_t off = (int64_t)(int32_t)u.x;
+    auto end_of = [&](const AbsVal& b) -> uint64_t {  // (unbounded: UINT64_MAX)
+      if (b.hi >= (1ull << 40)) return UINT64_MAX;
+      const int64_t e = (int64_t)b.hi + off + (int64_t)u.aux;
+      return e < 0 ? 0 : (uint64_t)e;
+    };
+    if (u.op == U_ST || u.op == U_STX) {
+      if (stk.off[i] != kNoStack || stk.pw[i] != kNoStack || !stk.dyn[i]) continue;
+      const uint64_t e = end_of(in[i][u.dst]);
+      if (e > st_end) st_end = e, st_at = i;
+    } else if (u.op == U_LDX) {
+      if (stk.off[i] != kNoStack) continue;  // (the stack window)
+      const AbsVal& b = in[i][u.src];
+      const uint64_t e = end_of(b);
+      if (b.lo == b.hi) {
+        if (e > kld_end) kld_end = e, kld_at = i;
+      } else if (e > ld_end) {
+        ld_end = e, ld_at = i;
+      }
+    } else if (u.op == U_ATOMIC && stk.off[i] == kNoStack) {
+      if (why) *why = i;
+      return false;
+    }
+  }
+  if (st_end > 128) {
+    if (why) *why = st_at;
+    return false;
+  }
+  if (st_end > 64 && (ld_end > 128 || kld_end > 64)) {
+    if (why) *why = ld_end > 128 ? ld_at : kld_at;
+    return false;
+  }
+  return true;
+}
 
 bool jit_compile(const std::vector<Uop>& uops, const std::vector<TUop>& t,
                  std::vector<char>& code_object, std::string* err, std::string* asm_out,

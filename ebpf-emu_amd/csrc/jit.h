@@ -58,7 +58,13 @@ struct StackPlan {
   // the compiled launch (host.cpp, the deopt list). Forward programs on the var kernels only.
   std::vector<char> dyn;     // per micro-op: a register-address ST/STX
   bool any_dyn = false;
+  bool no_deopt = false;     // store_mode_no_deopt: no lane of a main.rs-layout batch can leave
 };
+
+// Store mode on the var tile loop: whether no lane of a main.rs-layout batch can deoptimize
+// (jit.cpp, a range analysis of every access; the host also needs the stack window at or past
+// byte 128). Then the deopt pass after the launch is not needed.
+bool store_mode_no_deopt(const std::vector<Uop>& uops, const StackPlan& stk, uint32_t* why = nullptr);
 
 // Status of a lane that leaves the compiled kernel for the general interpreter (never reported:
 // the tile epilogue lists the packet instead of writing its outputs, tile bucket 8).

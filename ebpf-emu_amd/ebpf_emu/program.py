@@ -116,6 +116,15 @@ class Program:
             return False
 
     @property
+    def store_mode_no_deopt(self) -> bool:
+        """Store mode with no lane able to deoptimize on the var tile loop (jit.cpp
+        store_mode_no_deopt): main.rs-layout batches run without the deopt pass."""
+        try:
+            return "no lane can deoptimize" in self.jit_asm(1)
+        except _lib.EbpfError:
+            return False
+
+    @property
     def promoted(self) -> bool:
         """A stack-window loop program with its 8-byte slots promoted to registers (host.cpp
         promote_slots): production batches run that tier-0 program (compiled variant 4) on the

@@ -83,6 +83,15 @@ def _check(oracle_mod, img, pkts, got, ref, xdp, tag):
     _vs_oracle(oracle_mod, img, _images_of(pkts, xdp), got, tag=tag)
 
 
+def _assert_no_deopt(ws, prog):
+    """No lane left for the general interpreter: the list's count (workspace +0) is 0, and the
+    deopt pass either re-ran nothing (+8 == 0) or, for a program proven deopt-free
+    (jit.cpp store_mode_no_deopt), was not launched (+8 keeps the test's 0xFFFFFFFF)."""
+    w = ws[:12].cpu().numpy().view(np.uint32)
+    assert w[0] == 0, ("lanes deoptimized", w)
+    assert w[2] == (0xFFFFFFFF if prog.store_mode_no_deopt else 0), w
+
+
 LAYOUTS = ["fixed64", "fixed128", "offsets16", "offsets_mis3", "stride_lens", "xdp_offsets"]
 
 
@@ -233,7 +242,7 @@ def test_nat_long_options_no_deopt(cuda, oracle_mod, layout):
     out.r0, out.status = r0.data_ptr(), st.data_ptr()
     prog.launch(b, out, torch.cuda.current_stream())
     torch.cuda.synchronize()
-    assert ws[8:12].cpu().numpy().view(np.uint32)[0] == 0, "lanes deoptimized"
+    _assert_no_deopt(ws, prog)
     gen = prog.run(frames, r0=True, status=True, generic=True, xdp_md=xdp, **kw)
     torch.cuda.synchronize()
     assert torch.equal(st, gen.status)
@@ -403,7 +412,7 @@ def test_straddling_loads_no_deopt(cuda, oracle_mod, layout):
     out.r0, out.status = r0.data_ptr(), st.data_ptr()
     prog.launch(b, out, torch.cuda.current_stream())
     torch.cuda.synchronize()
-    assert ws[8:12].cpu().numpy().view(np.uint32)[0] == 0, "lanes deoptimized"
+    _assert_no_deopt(ws, prog)
     gen = prog.run(frames, r0=True, status=True, generic=True, xdp_md=xdp, **kw)
     torch.cuda.synchronize()
     assert torch.equal(st, gen.status)
@@ -417,3 +426,76 @@ def test_straddling_loads_no_deopt(cuda, oracle_mod, layout):
         if s == 0:
             assert int(r0n[i]) == o0, (layout, i)
     prog.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layout", ["fixed128", "offsets_mis3"])
+def test_no_deopt_proof_fuzz(cuda, oracle_mod, layout):
+    """Store-mode programs that jit.cpp store_mode_no_deopt proves deopt-free (every
+    register-address store ends at or below byte 128, and -- when one may pass byte 64 -- every
+    register-address load too, no constant-address load past 64) run on the var tile loop without
+    the deopt pass. A wrong proof would leave listed lanes without outputs, so: the list stays
+    empty, the pass is not launched, and every output == the general interpreter's == the
+    oracle's. Also: the same program with r10 below 128 + the stack window keeps its pass."""
+    import torch
+
+    from ebpf_emu import Program, _lib
+    from test_stack_tier import VAR_LAYOUTS, _fixed_frames, _images_of, _var_packets
+
+    rng = random.Random(zlib.crc32(b"proof" + layout.encode()))
+    done = 0
+    for it in range(160):
+        img = gen_store_program(rng)
+        try:
+            oracle_mod.Program(img)
+            prog = Program(img)
+        except Exception:
+            continue
+        if not (prog.store_mode and prog.store_mode_no_deopt):
+            prog.close()
+            continue
+        pkts = _var_packets(rng, rng.choice([64, 100, 130]))
+        if layout.startswith("fixed"):
+            pk = [p[:128].ljust(128, b"\0") for p in pkts]
+            frames = _fixed_frames(pk, 128, cuda)
+            kw = dict(n=len(pk), stride=128)
+        else:
+            from test_gpu_parity import _stage
+
+            pk = pkts
+            frames, kw = _stage(pkts, cuda, **VAR_LAYOUTS[layout])
+        for r10 in (512, 100):
+            b = prog.make_batch(frames, r10=r10, **kw)
+            if prog.batch_kernel(b) != _lib.EBPF_KERNEL_JIT_VARL_STACK:
+                break
+            ws = torch.zeros(prog.workspace_bytes(b, 0), dtype=torch.uint8, device=cuda)
+            b = prog.make_batch(frames, r10=r10, workspace=ws, **kw)
+            out = _lib.BatchOut()
+            r0 = torch.empty(len(pk), dtype=torch.int64, device=cuda)
+            st = torch.empty(len(pk), dtype=torch.uint8, device=cuda)
+            ws[8:12] = 0xFF
+            out.r0, out.status = r0.data_ptr(), st.data_ptr()
+            prog.launch(b, out, torch.cuda.current_stream())
+            torch.cuda.synchronize()
+            w = ws[:12].cpu().numpy().view(np.uint32)
+            if r10 == 512:  # (the stack window at 512 - k: no pass)
+                assert w[0] == 0 and w[2] == 0xFFFFFFFF, (it, w, img.hex())
+            else:  # (r10 - k below 128: the pass runs)
+                assert w[0] == 0 and w[2] != 0xFFFFFFFF, (it, w, img.hex())
+            gen = prog.run(frames, r0=True, status=True, generic=True, r10=r10, **kw)
+            torch.cuda.synchronize()
+            assert torch.equal(st, gen.status), (it, r10, img.hex())
+            ok = st == 0
+            assert torch.equal(r0[ok], gen.r0[ok]), (it, r10, img.hex())
+            if r10 == 512:
+                op = oracle_mod.Program(img)
+                stn, r0n = st.cpu().numpy(), r0.cpu().numpy().view(np.uint64)
+                for i, im in enumerate(_images_of(pk, False)):
+                    s, o0, _ = op.run_packet(im, 1024, 512, 1 << 22)
+                    assert stn[i] == s, (it, i)
+                    if s == 0:
+                        assert int(r0n[i]) == o0, (it, i)
+        else:
+            done += 1
+        prog.close()
+    assert done >= 8, done
