@@ -67,6 +67,10 @@ CONFIGS = {
     # xdp_md batch: staged images, compiled with the staged ctx known -- DESIGN 3.17)
     "checksum_xdp": (4, "per-byte checksum as a standard XDP program (xdp_md ctx) over 1Mi mixed "
                         "64B/1500B frames"),
+    # a long program: a 128-rule firewall chain (workloads.acl_rules_source, 1013 insns, ~297 run
+    # per packet) -- compiled past the near-branch reach (jit.cpp far mode); issue-bound, not HBM
+    "acl_rules": (2, "IPv4 rule-table firewall, 128 rules (1013 insns, ~297 executed per packet) "
+                     "over 1Mi x 64B frames"),
 }
 PROGRAM_OF = {"stack": "5tuple_stack", "tier1": "mac_swap_tx", "xdp": "5tuple_xdp",
               "call": "5tuple_call"}

@@ -1210,7 +1210,8 @@ int ebpf_prog_load(const uint8_t* code, size_t nbytes, ebpf_prog** out, size_t* 
     if (u.op >= U_JA && u.op <= U_CALL && (uint32_t)u.x <= (uint32_t)i) forward = false;
   }
   p->tiny = forward && xu.size() <= kTinyUops;
-  if (forward && p->xtier == 0 && !xu.empty() && xu.size() <= kMaxDagUops) {
+  // (past kMaxDagUops the tables serve the compiler only: batch_kind)
+  if (forward && p->xtier == 0 && !xu.empty() && xu.size() <= kJitMaxUops) {
     p->duops = build_dag(xu);
     p->duopsk = fold_const_loads(xu, p->duops);
     if (xu.size() <= kJitMaxUops) {  // tile_kernel's (<= 62) and the compiler's tables
@@ -1319,6 +1320,7 @@ int ebpf_prog_insn(const ebpf_prog* p, size_t i, int32_t* imm, int64_t* imm64, i
 
 int ebpf_prog_tier(const ebpf_prog* p) { return p ? p->tier : -1; }
 
+static_assert(kJitMaxUops == EBPF_MAX_COMPILED_UOPS, "include/ebpf_emu.h names the compiler's limit");
 int ebpf_prog_forward_only(const ebpf_prog* p) { return p ? (p->duops.empty() ? 0 : 1) : -1; }
 
 int ebpf_prog_stack_window(const ebpf_prog* p) { return p ? (int)p->stack.k : -1; }
@@ -1538,7 +1540,10 @@ static int batch_kind(const ebpf_prog* p, const ebpf_batch* b, const ebpf_batch_
     if (stack_loop_ok(p, b, out, device)) return *stk = true, kKindLoop;
     return batch_tier(p, b);
   }
-  return (p->dev_duops[device] && b->max_steps >= p->xuops.size() && !generic) ? kKindDag
+  // (a forward program past dag_kernel's kMaxDagUops runs only compiled)
+  const bool dag_ok = p->xuops.size() <= kMaxDagUops ||
+                      (p->jit_mod[device][0] && !(b->flags & EBPF_BATCH_NO_JIT));
+  return (p->dev_duops[device] && b->max_steps >= p->xuops.size() && !generic && dag_ok) ? kKindDag
          : (p->dev_ltuops[device] && !generic && !p->stack.k && p->xtier == 0 &&
             (p->xuops.size() <= kTileMaxUops ||  // tile_kernel's loop mode, or compiled only
              (p->jit_mod[device][2] && !(b->flags & EBPF_BATCH_NO_JIT))))          ? kKindLoop

@@ -43,6 +43,9 @@ namespace ebpfemu {
 namespace {
 
 constexpr uint32_t kFieldSgpr = 36;  // TUop dword d lives in s[36 + d] (gen_tile.py UB)
+// far mode: an island of out-of-line code at the first block start past this many lines (a line
+// is at most 12 bytes: 36 KiB and the island's own code stay well inside s_branch's reach)
+constexpr size_t kIslandLines = 3000;
 
 struct Marker {
   size_t begin = 0, end = 0;  // the marker line ";@@JIT@@" (replaced)
@@ -62,6 +65,15 @@ struct Marker {
 };
 
 bool inline_const(int64_t v) { return v >= -16 && v <= 64; }
+
+// A jump to `label` from anywhere in the code object (s_branch reaches +-128 KiB), for far mode
+// (compile_into_template): through s[60:61] (the statement's T0, dead wherever a body is entered
+// or left and at every block entry) and SCC (s_add sets it). `tag` makes its label unique.
+std::string long_jump(const std::string& label, const std::string& tag) {
+  const std::string g = ".Lgp" + tag, d = "(" + label + "-" + g + ")";
+  return "s_getpc_b64 s[60:61]\n" + g + ":\ns_add_u32 s60, s60, " + d + "&4294967295\n"
+         "s_addc_u32 s61, s61, " + d + ">>32\ns_setpc_b64 s[60:61]\n";
+}
 
 std::string hex32(uint32_t v) {
   char b[16];
@@ -373,6 +385,24 @@ struct Compiler {
   // counted loops: a one-byte load's base read from this register instead (-1: its own)
   std::vector<int> addr_src = std::vector<int>(64, -1);
   bool proven = false;     // emitting the proven copy (ldx1_loop drops inb[i] loads' checks)
+  // far mode (compile_into_template): the body's long branches as long jumps, and its
+  // out-of-line code in islands between blocks (copy) so that every short branch stays in reach
+  bool far_mode = false;
+  mutable uint32_t far_tag = 0;
+  size_t island_from = 0;  // main's length after the last island
+  // A branch whose target may lie past s_branch's reach in far mode: `cond` "" for s_branch, else
+  // the s_cbranch_ condition (scc0, scc1, vccz, vccnz, execz, execnz).
+  std::string jmp(const std::string& cond, const std::string& label) const {
+    if (!far_mode) return (cond.empty() ? "s_branch " : "s_cbranch_" + cond + " ") + label + "\n";
+    const std::string t = "f" + ovl_tag + "_" + std::to_string(far_tag++);
+    if (cond.empty()) return long_jump(label, t);
+    static const char* inv[][2] = {{"scc0", "scc1"}, {"scc1", "scc0"}, {"vccz", "vccnz"},
+                                   {"vccnz", "vccz"}, {"execz", "execnz"}, {"execnz", "execz"}};
+    std::string ic;
+    for (const auto& p : inv)
+      if (cond == p[0]) ic = p[1];
+    return "s_cbranch_" + ic + " .Lfs" + t + "\n" + long_jump(label, t) + ".Lfs" + t + ":\n";
+  }
 
   static AbsVal av_const(uint64_t c) {
     AbsVal v;
@@ -1334,6 +1364,7 @@ struct Compiler {
     const std::string P = "J" + m.n + "_";
     ovl_tag = m.n;
     overlay_widths = 0;
+    island_from = 0;
     // (the var tile loop's statement: stores past byte 64 into the overflow image)
     ovf_lo = ovf_hi = tile_s = dm = "";
     unsigned a0 = 0, a1 = 0;
@@ -2089,6 +2120,14 @@ struct Compiler {
   bool copy(const Marker& m, const std::string& P, bool fast, std::string& main,
             std::string& ool) {
     for (uint32_t i = 0; i < n; i++) {
+      if (start[i] && far_mode && !ool.empty() &&
+          (size_t)std::count(main.begin() + std::min(island_from, main.size()), main.end(), '\n') >
+              kIslandLines) {
+        const std::string L = ".L" + P + "isl" + std::to_string(i);
+        main += "s_branch " + L + "\n" + ool + L + ":\n";
+        ool.clear();
+        island_from = main.size();
+      }
       if (start[i]) {
         main += ".L" + P + "b" + std::to_string(i) + ":\n";
         if (target[i])
@@ -2790,7 +2829,7 @@ struct Compiler {
   // the lanes whose steps pass max_steps (vcc).
   std::string budget_check(uint32_t i, const std::string& P) const {
     std::string s;
-    if (!exact) return s + "s_cbranch_vccnz .L" + P + "budget\n";
+    if (!exact) return s + jmp("vccnz", ".L" + P + "budget");
     const std::string ok = ".L" + P + "bok" + std::to_string(i);
     return s + "s_cbranch_vccz " + ok + "\ns_mov_b64 s[64:65], exec\ns_mov_b64 exec, vcc\n"
                "v_mov_b32 v30, 5\nv_mov_b32 v28, -1\nv_subrev_u32 v29, 1, v29\n"
@@ -2862,6 +2901,7 @@ struct Compiler {
     const std::string P = "J" + m.n + "_";
     ovl_tag = m.n;
     overlay_widths = 0;
+    island_from = 0;
     std::string main = "; compiled eBPF program: " + std::to_string(n) + " micro-ops\n"
                        "s_mov_b32 s52, s33\ns_mov_b32 s53, 0\n";
     if (stk) main += stack_zero();
@@ -2896,8 +2936,7 @@ struct Compiler {
     if (chunks) {
       const std::string F = "J" + m.n + "f_";
       if (!pw)
-        main += "s_cmp_gt_u32 " + std::to_string(maxend) + ", s33\ns_cbranch_scc1 .L" + P +
-                "slow\n";
+        main += "s_cmp_gt_u32 " + std::to_string(maxend) + ", s33\n" + jmp("scc1", ".L" + P + "slow");
       for (uint32_t c = 0; c < 4; c++)
         if (chunks & (1u << c))
           main += "v_xad_u32 v36, v35, " + std::to_string(16 * c) + ", v34\nds_read_b128 v[" +
@@ -2918,7 +2957,7 @@ struct Compiler {
       }
       main += "s_mov_b64 exec, 0\n";
       if (!copy(m, F, true, main, ool)) return false;
-      main += "s_branch .L" + P + "end\n" + (pw ? "" : ".L" + P + "slow:\n");
+      main += jmp("", ".L" + P + "end") + (pw ? "" : ".L" + P + "slow:\n");
     }
     if (!pw) {
       main += "s_mov_b64 exec, 0\n";
@@ -2998,6 +3037,7 @@ struct Compiler {
     ovl_tag = m.n;
     xc.ovl_tag = m.n + "x";
     overlay_widths = xc.overlay_widths = 0;
+    island_from = 0;
     std::string ool;
     // (stack-window programs keep the budget's bias in s54 -- the statement's table pointer, which
     // compiled code never reads -- s57 being the window's address)
@@ -3009,26 +3049,27 @@ struct Compiler {
                        "v_mov_b32 v55, 0x80000000\n" + window_zero_prologue(m, P) +
                        prefetch_prologue(m, P) +
                        (stk ? stack_zero() + stack_init(P, ool) : std::string()) + promo_guard(P) +
-                       "s_bitcmp1_b32 s70, 0\ns_cbranch_scc1 .L" + PX + "start\n";
+                       "s_bitcmp1_b32 s70, 0\n" + jmp("scc1", ".L" + PX + "start");
     prove_loads();
     const bool any = std::find(inb.begin(), inb.end(), 1) != inb.end();
     if (any) {
       main += "; one-byte loads proven in bounds: the proven copy unless s70 bit 1\n"
-              "s_bitcmp1_b32 s70, 1\ns_cbranch_scc1 .L" + PC + "go\ns_mov_b64 exec, 0\n";
+              "s_bitcmp1_b32 s70, 1\n" + jmp("scc1", ".L" + PC + "go") + "s_mov_b64 exec, 0\n";
       proven = true;
       const bool ok = copy(m, P, false, main, ool);
       proven = false;
       if (!ok) return false;
-      main += "s_branch .L" + P + "end\n.L" + PC + "go:\n";
+      main += jmp("", ".L" + P + "end") + ".L" + PC + "go:\n";
     }
     main += "s_mov_b64 exec, 0\n";
     const std::string PB = any ? PC : P;  // the checked block copy
     if (!copy(m, PB, false, main, ool)) return false;
-    main += "s_branch .L" + P + "end\n" + (any ? ".L" + PC + "budget:\n" : std::string()) +
+    main += jmp("", ".L" + P + "end") + (any ? ".L" + PC + "budget:\n" : std::string()) +
             ".L" + P + "budget:\ns_or_b32 s70, s70, 1\n"
             "s_cmp_eq_u32 " + m.aligned + ", 0\ns_cbranch_scc1 .L" + P + "bkeep\n"
             "v_mov_b32 v22, -64\n.L" + P + "bkeep:\ns_mov_b64 exec, -1\n"
             "s_branch .Lreinit" + m.n + "\n.L" + PX + "start:\ns_mov_b64 exec, 0\n";
+    xc.island_from = main.size();
     if (!xc.copy(m, PX, false, main, ool)) {
       err = xc.err;
       return false;
@@ -3141,9 +3182,35 @@ bool assemble(const std::string& src, std::vector<char>& co, std::string* err) {
 
 namespace {
 
+// Far mode (compile_into_template) past this many lines of code in one body: s_branch reaches
+// +-32 Ki dwords, and a line of the body is at most 12 bytes, most 4 or 8.
+constexpr size_t kFarLines = 8192;
+
+// A body moved out of line (far mode): its exits to the statement (.Ldone: the epilogue behind
+// the marker, .Lreinit: a loop program's exact-mode restart) become long jumps, and so does its
+// fall-through end.
+std::string relocated_body(const std::string& b, const std::string& n, uint32_t& tag) {
+  auto lj = [&](const std::string& l) { return long_jump(l, "r" + std::to_string(tag++)); };
+  std::string out = ".Lbody" + n + ":\n";
+  size_t p = 0;
+  while (p < b.size()) {
+    size_t e = b.find('\n', p);
+    if (e == std::string::npos) e = b.size();
+    const std::string ln = b.substr(p, e - p);
+    p = e + 1;
+    if (ln == "s_branch .Ldone" + n || ln == "s_branch .Lreinit" + n)
+      out += lj(ln.substr(9));
+    else
+      out += ln + "\n";
+  }
+  return out + lj(".Ldone" + n);
+}
+
 // Insert the compiled code at every marker of the template assembly (markers of the other kind of
 // kernel -- loop vs forward-only -- get an empty body: never launched for this program), then
-// assemble.
+// assemble. Far mode, when a body passes kFarLines: every body out of line, behind its kernel's
+// code (entered by a long jump), so that no branch of the template or of the statement around it
+// spans the program.
 bool compile_into_template(Compiler& c, Compiler* xc, std::vector<char>& code_object,
                            std::string* err, std::string* asm_out, bool* deep_out = nullptr) {
   std::string tmpl(kJitTemplateAsm);
@@ -3201,28 +3268,63 @@ bool compile_into_template(Compiler& c, Compiler* xc, std::vector<char>& code_ob
     c.coop_emitted = xc->coop_emitted = false;
   }
   c.deep_regs = xc ? (xc->deep_regs = deep) : false;
-  for (const Marker& m : marks) {
-    std::string b;
+  // (far: the relocated bodies wait for the end of their kernel's code, its .Lfunc_end label)
+  std::string pending;
+  uint32_t tag = 0;
+  bool far = false;
+  auto copy_tmpl = [&](size_t from, size_t to) {
+    for (size_t q; far && !pending.empty() && (q = tmpl.find("\n.Lfunc_end", from)) < to;) {
+      src += tmpl.substr(from, q + 1 - from) + pending;
+      pending.clear();
+      from = q + 1;
+    }
+    src += tmpl.substr(from, to - from);
+  };
+  std::vector<std::string> bodies(marks.size());
+  std::vector<char> live(marks.size(), 0);
+  for (int pass = 0; pass < 2; pass++) {
+  if (pass == 1 && !far) break;
+  c.far_mode = far;
+  if (xc) xc->far_mode = far;
+  for (size_t k = 0; k < marks.size(); k++) {
+    const Marker& m = marks[k];
+    std::string& b = bodies[k];
     const bool loop_marker = m.loops == "1";
-    bool ok = true;
     // (stack-window programs: the fixed-slot kernel and the var kernel's stack statement; other
     // programs: every statement but that one)
     if (loop_marker != (xc != nullptr) || (loop_marker && m.deep != deep) ||
-        (c.stk ? !(m.stack || (!loop_marker && m.fixed == "1" && !c.stk->any_dyn)) : m.stack))
+        (c.stk ? !(m.stack || (!loop_marker && m.fixed == "1" && !c.stk->any_dyn)) : m.stack)) {
       b = "s_mov_b64 exec, 0  ; (not this program's kernel)\n";
-    else
-      ok = xc ? c.body_loop(m, *xc, b) : c.body(m, b);
-    if (!ok) {
+      continue;
+    }
+    if (!(xc ? c.body_loop(m, *xc, b) : c.body(m, b))) {
       if (err) *err = c.err;
       return false;
     }
-    src += tmpl.substr(at, m.init_begin - at);
+    live[k] = 1;
+    far = far || (size_t)std::count(b.begin(), b.end(), '\n') > kFarLines;
+  }
+  }
+  for (size_t k = 0; k < marks.size(); k++) {
+    const Marker& m = marks[k];
+    const std::string& b = bodies[k];
+    copy_tmpl(at, m.init_begin);
     src += init;
-    src += tmpl.substr(m.init_end, m.begin - m.init_end);
-    src += b;
+    copy_tmpl(m.init_end, m.begin);
+    if (far && live[k]) {
+      src += "; the program's code: out of line\n" +
+             long_jump(".Lbody" + m.n, "e" + std::to_string(tag++));
+      pending += relocated_body(b, m.n, tag);
+    } else {
+      src += b;
+    }
     at = m.end;
   }
-  src += tmpl.substr(at);
+  copy_tmpl(at, tmpl.size());
+  if (!pending.empty()) {
+    if (err) *err = "far mode: no kernel end behind a marker";
+    return false;
+  }
   if (asm_out) *asm_out = src;
   if (deep_out) *deep_out = deep;
   return assemble(src, code_object, err);

@@ -119,7 +119,9 @@ struct alignas(64) TUop {
 static_assert(sizeof(TUop) == 64, "TUop must be 64 bytes");
 constexpr uint32_t kTileUops = 64;     // table entries: micro-ops, then the DONE sentinels 62, 63
 constexpr uint32_t kTileMaxUops = 62;  // programs the tile kernels run
-constexpr uint32_t kJitMaxUops = 256;  // forward-only programs the compiler takes (= kMaxDagUops)
+// programs the compiler takes (jit.cpp; flatten_calls' copies likewise). Past kMaxDagUops
+// (launch.h, dag_kernel's LDS table) a forward program runs compiled or on the general interpreter.
+constexpr uint32_t kJitMaxUops = 4096;
 static_assert(offsetof(DUop, opaux) == 128, "the C++ half starts at dword 32");
 
 }  // namespace ebpfemu

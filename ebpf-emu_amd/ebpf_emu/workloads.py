@@ -475,14 +475,60 @@ l4_out:
     exit
 """
 
+
+
+def acl_rules_source(rules: int = 128, seed: int = 11) -> str:
+    """A rule-table firewall of `rules` seeded rules (~9 instructions each: 1,200 instructions at
+    128 -- past the compiler's near-branch reach, jit.cpp far mode), the shape of an iptables-style
+    chain written as straight-line XDP: the Ethernet/IPv4 5-tuple loaded once (IHL 5; frames
+    without one pass), then rule k: (saddr & mask) == prefix, (daddr & mask) == prefix, protocol,
+    destination port in [lo, hi] -> its verdict, else rule k + 1; no rule: XDP_PASS. Prefixes are
+    /8 on saddr's first octet (10 or a seeded octet: the synthetic frames randomise the rest), or
+    wider; most packets match no rule and run every rule's first test."""
+    import random as _random
+
+    rng = _random.Random(seed)
+    out = ["    mov r0, 2", "    jlt r2, 38, out", "    ldxh r3, [r1+12]", "    jne r3, 0x0008, out",
+           "    ldxb r4, [r1+23]           # protocol", "    ldxw r5, [r1+26]           # saddr",
+           "    ldxw r6, [r1+30]           # daddr", "    ldxh r7, [r1+36]           # dport",
+           "    be16 r7"]
+    for k in range(rules):
+        nxt = f"r{k + 1}" if k + 1 < rules else "out"
+        out.append(f"r{k}:")
+        octet = 10 if rng.random() < 0.15 else rng.randrange(256)
+        kind = rng.random()
+        if kind < 0.6:  # saddr /8
+            out += ["    mov r8, r5", "    and r8, 0xff", f"    jne r8, {octet}, {nxt}"]
+        else:           # saddr /16 (the second octet is random in the frames: rare)
+            out += ["    mov r8, r5", "    and r8, 0xffff",
+                    f"    jne r8, {octet | (rng.randrange(256) << 8)}, {nxt}"]
+        if rng.random() < 0.3:  # daddr /8
+            out += ["    mov r8, r6", "    and r8, 0xff", f"    jne r8, {rng.randrange(256)}, {nxt}"]
+        proto = rng.choice([6, 17, None])
+        if proto is not None:
+            out.append(f"    jne r4, {proto}, {nxt}")
+            lo = rng.choice([0, 0, 53, 80, 443, 1024, rng.randrange(65536)])
+            hi = min(65535, lo + rng.choice([0, 0, 10, 1023, 30000]))
+            out += [f"    jlt r7, {lo}, {nxt}", f"    jgt r7, {hi}, {nxt}"]
+        out += [f"    mov r0, {1 if rng.random() < 0.7 else 2}", "    ja out"]
+    out += ["out:", "    exit"]
+    return "\n".join(out) + "\n"
+
+
+ACL_RULES = acl_rules_source()
+
 PROGRAMS = {"drop": DROP_ALL, "5tuple": FIVE_TUPLE, "checksum": CHECKSUM,
             "5tuple_stack": FIVE_TUPLE_STACK, "mac_swap_tx": MAC_SWAP_TX, "acl": ACL,
             "5tuple_xdp": FIVE_TUPLE_XDP, "checksum_stack": CHECKSUM_STACK,
             "5tuple_call": FIVE_TUPLE_CALL, "nat": NAT_REWRITE, "checksum_xdp": CHECKSUM_XDP}
 
 
+# long programs (far mode), kept apart from PROGRAMS (the compact benchmark programs)
+LONG_PROGRAMS = {"acl_rules": ACL_RULES}
+
+
 def program(name: str) -> bytes:
-    return assemble(PROGRAMS[name])
+    return assemble(PROGRAMS[name] if name in PROGRAMS else LONG_PROGRAMS[name])
 
 
 def _headers(rng: np.random.Generator, n: int, frame_len: np.ndarray, buf: np.ndarray,

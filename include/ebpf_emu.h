@@ -159,9 +159,10 @@ int ebpf_prog_insn(const ebpf_prog* prog, size_t i, int32_t* imm, int64_t* imm64
  * no calls), 1 = general per-packet image in device workspace. */
 int ebpf_prog_tier(const ebpf_prog* prog);
 
-/* 1 when the program (memory tier 0, every jump forward, <= 256 micro-ops) runs on the
- * forward-jump fast path -- for batches with max_steps >= its length and without
- * EBPF_BATCH_GENERIC -- else 0; -1 for NULL. */
+/* 1 when the program (memory tier 0, every jump forward, <= EBPF_MAX_COMPILED_UOPS micro-ops)
+ * runs on the forward-jump fast path -- for batches with max_steps >= its length and without
+ * EBPF_BATCH_GENERIC; past 256 micro-ops only compiled (ebpf_prog_compile), not with
+ * EBPF_BATCH_NO_JIT -- else 0; -1 for NULL. */
 int ebpf_prog_forward_only(const ebpf_prog* prog);
 
 /* Memory tier 0.5: the bytes of the stack window [r10 - k, r10) of a program whose memory writes
@@ -175,9 +176,13 @@ int ebpf_prog_forward_only(const ebpf_prog* prog);
  * 0 = not such a program; -1 for NULL. */
 int ebpf_prog_stack_window(const ebpf_prog* prog);
 
+/* Micro-ops (after local calls are flattened into one copy per frame stack) of the longest
+ * program the compiler takes; longer programs run on the general interpreter. */
+#define EBPF_MAX_COMPILED_UOPS 4096
+
 /* Compile the program to gfx950 machine code now, if it is one the tile kernels run (memory tier
  * 0): straight-line code in pc order with direct register operands, replacing the interpreter's
- * dispatch, for programs of <= 256 micro-ops. Forward-only programs get the forward kernels
+ * dispatch, for programs of <= EBPF_MAX_COMPILED_UOPS micro-ops. Forward-only programs get the forward kernels
  * (batches with max_steps >= the program length); every such program also gets the loop kernel
  * (back edges, or a step budget that can bind: the exact budget of the reference's step count). Needs no
  * GPU; done implicitly by the first upload. Returns 1 = compiled, 0 = not such a program (or

@@ -409,3 +409,85 @@ def gen_slot_loop_program(rng: random.Random) -> bytes:
         lines += ["ldxdw r9, [r10-16]", "xor r0, r9"]
     lines += ["exit"]
     return assemble("\n".join(lines))
+
+
+def gen_long_program(rng: random.Random, n: int, loops: bool = False, stack: bool = False,
+                     store: bool = False) -> bytes:
+    """Long tier-0 programs (hundreds to thousands of micro-ops, past the compiler's near-branch
+    reach: jit.cpp far mode) that lanes actually run through: ALU ops on seeded registers, packet
+    loads at r1 + 0..79 of every width, forward jumps over a few instructions, a rare early exit
+    of some lanes;
+    with loops=True also counted loops (r9 = 0 .. k) over a few instructions; with stack=True
+    stores and loads of every width in the stack window [r10 - 32, r10) (memory tier 0.5); with
+    store=True stores and loads through a packet pointer r8 = r1 + (a packet byte & 15) + c at
+    offsets 0..99 (store mode: past byte 64 the overflow image, past 128 the deopt list). r0 folds
+    the registers at the end."""
+    words: list[bytes] = []
+    for r in (0, 3, 4, 5, 6, 7, 8):
+        v = rng.choice(EDGE) if rng.random() < 0.5 else rng.getrandbits(64)
+        words.append(encode(0x18, r, 0, 0, v & 0xFFFFFFFF) + encode(0, 0, 0, 0, v >> 32))
+    if stack:  # (the window's lowest store first: every later access lies inside [r10 - 32, r10))
+        words.append(encode(0x7B, 10, 0, -32))                          # stxdw [r10-32], r0
+    if store:
+        words += [encode(0x71, 8, 1, rng.randrange(0, 64)),             # ldxb r8, [r1+c0]
+                  encode(0x57, 8, 0, 0, 15), encode(0x07, 8, 0, 0, rng.randrange(0, 16)),
+                  encode(0x0F, 8, 1, 0, 0)]                             # r8 = r1 + (b & 15) + c
+    regs = [0, 3, 4, 5, 6, 7] if store else [0, 3, 4, 5, 6, 7, 8]
+    while len(words) < n:
+        q = rng.random()
+        dst, src = rng.choice(regs), rng.choice([0, 2, 3, 4, 5, 6, 7, 8])
+        if q < 0.08 and store:
+            size = rng.choice([0x00, 0x08, 0x10, 0x18])
+            off = rng.randrange(0, 100)
+            k = rng.random()
+            if k < 0.45:
+                words.append(encode(0x63 | size, 8, src, off))           # stx [r8 + off], src
+            elif k < 0.65:
+                words.append(encode(0x62 | size, 8, 0, off, _imm(rng)))  # st [r8 + off], imm
+            else:
+                words.append(encode(0x61 | size, dst, 8, off))           # ldx dst, [r8 + off]
+        elif q < 0.55:
+            cls = rng.choice([0x04, 0x07])
+            op = rng.choice([0, 1, 2, 4, 5, 6, 7, 10, 11, 12] * 4 + [3, 9, 13])
+            srcbit = rng.choice([0, 0x08])
+            imm = rng.choice([16, 32, 64]) if op == 13 else _imm(rng)
+            words.append(encode((op << 4) | (0 if op == 13 else srcbit) | cls, dst,
+                                0 if op == 13 else src, 0, imm))
+        elif q < 0.75:
+            size = rng.choice([0x00, 0x08, 0x10, 0x18])
+            off = rng.randrange(0, 80)
+            if store:  # (store mode: no constant-address load straddles byte 64, analyze_stack)
+                w = {0x00: 4, 0x08: 2, 0x10: 1, 0x18: 8}[size]
+                off = off if off >= 64 or off + w <= 64 else 64 - w
+            words.append(encode(0x61 | size, dst, 1, off))
+        elif q < 0.93:
+            cls = rng.choice([0x05, 0x06])
+            op = rng.choice([1, 2, 3, 4, 5, 6, 7, 10, 11, 12, 13])
+            words.append(encode((op << 4) | rng.choice([0, 0x08]) | cls, dst, src,
+                                rng.randrange(0, 7), _imm(rng)))
+        elif q < 0.96 and stack:
+            size = rng.choice([0x00, 0x08, 0x10, 0x18])
+            w = {0x00: 4, 0x08: 2, 0x10: 1, 0x18: 8}[size]
+            d = -w * rng.randrange(1, 32 // w + 1)
+            k = rng.random()
+            if k < 0.35:
+                words.append(encode(0x63 | size, 10, src, d))           # stx [r10 + d], src
+            elif k < 0.5:
+                words.append(encode(0x62 | size, 10, 0, d, _imm(rng)))  # st [r10 + d], imm
+            else:
+                words.append(encode(0x61 | size, dst, 10, d))           # ldx dst, [r10 + d]
+        elif q < 0.96 and loops:
+            body = [encode(0x07 | (rng.choice([0, 1, 2, 10, 12]) << 4), rng.choice([3, 4, 5, 6]),
+                           0, 0, _imm(rng)) for _ in range(rng.randrange(1, 5))]
+            words.append(encode(0xB7, 9, 0, 0, 0))                      # mov r9, 0
+            words += body
+            words.append(encode(0x07, 9, 0, 0, 1))                      # add r9, 1
+            words.append(encode(0xA5, 9, 0, -(len(body) + 2), rng.randrange(1, 12)))  # jlt r9, k
+        elif q < 0.962:  # an exit for the lanes with dst == imm (the rest stays reachable)
+            words += [encode(0x55, dst, 0, 1, rng.choice([0, 1, 2, 7, 0xFF])), encode(0x95)]
+        else:
+            words.append(encode(0xB7 | rng.choice([0, 0x08]), dst, src, 0, _imm(rng)))
+    for r in (3, 4, 5, 6, 7, 8):
+        words.append(encode(0xAF, 0, r, 0, 0))                          # xor r0, r
+    words.append(encode(0x95))
+    return b"".join(words)

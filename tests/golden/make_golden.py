@@ -117,7 +117,7 @@ def config4(total=100_000_000):
 PIN_CHUNKS_64 = 128  # 16 pool batches x 8 ranks
 PIN_CHUNKS_MIXED = 16  # 2 pool batches x 8 ranks (a 1 Mi mixed batch is ~840 MB: one per rank)
 PIN_PROGRAMS_64 = ("5tuple", "drop", "5tuple_stack", "mac_swap_tx", "acl", "5tuple_xdp",
-                   "5tuple_call", "nat")
+                   "5tuple_call", "nat", "acl_rules")
 PIN_PROGRAMS_MIXED = ("checksum", "checksum_stack", "checksum_xdp")
 
 

@@ -31,7 +31,7 @@ def _pins():
 
 
 @pytest.mark.parametrize("n,config", [(2, "5tuple"), (3, "acl"), (2, "checksum"),
-                                           (2, "checksum_xdp"), (8, "5tuple")])
+                                           (2, "checksum_xdp"), (8, "5tuple"), (2, "acl_rules")])
 def test_launcher_spawns_ranks_and_pins(n, config):
     steps = 5
     r = _bench(["--gpus", str(n), "--steps", str(steps), "--config", config], {})

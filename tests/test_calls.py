@@ -3,7 +3,8 @@ runs on the compiled kernels as one copy per reachable frame stack -- a CALL a j
 callee's copy, an EXIT with a non-empty stack a jump to the popped pc (emu.rs:265-279, Q12: the
 pushed pc is the callee's entry + 1, no registers saved). Checked against the oracle (status,
 r0, registers, retired steps) and the general interpreter's frame stack (EBPF_BATCH_GENERIC),
-with binding step budgets; recursion keeps the general interpreter (ST_CALLDEPTH at 65 frames)."""
+with binding step budgets; recursion flattens too while its 65 frame stacks x the recursive
+body's pcs fit kJitMaxUops (ST_CALLDEPTH at 65 frames), else keeps the general interpreter."""
 import random
 
 import numpy as np
@@ -35,8 +36,9 @@ g:
 
 # unbounded recursion: every call jumps back to the program's start and pushes pc 1, so the
 # stack grows to 64 frames and the 65th push faults ST_CALLDEPTH. 65 stacks x 2 pcs fit the
-# compiled kernels (a forward-only program of 129 micro-ops); RECURSE_BIG's 65 x 5 do not (the
-# general interpreter's frame stack)
+# compiled kernels (a forward-only program of 129 micro-ops), and so do RECURSE_BIG's 65 x 5 (325
+# copies: past the 256 of rounds 1-4, inside kJitMaxUops = 4096); RECURSE_HUGE's 65 x 70 do not
+# (the general interpreter's frame stack)
 RECURSE = """
 top:
     add r0, 1
@@ -49,6 +51,10 @@ top:
     xor r0, r2
     lsh r0, 1
     add r0, r1
+    call top
+    exit
+"""
+RECURSE_HUGE = "top:\n" + "".join(f"    add r0, {k}\n    xor r0, r2\n" for k in range(34)) + """
     call top
     exit
 """
@@ -67,6 +73,9 @@ def test_flatten_compiles():
     assert p.forward_only and p.compile()
     p.close()
     p = Program(assemble(RECURSE_BIG))
+    assert p.forward_only and p.compile()
+    p.close()
+    p = Program(assemble(RECURSE_HUGE))
     assert not p.forward_only and not p.compile()
     p.close()
     rng = random.Random(5)
@@ -88,7 +97,8 @@ def test_call_programs_directed(cuda, oracle_mod):
     rng = random.Random(1)
     pkts = [gen_packet(rng) for _ in range(130)]
     fwd = (_lib.EBPF_KERNEL_JIT_VAR, _lib.EBPF_KERNEL_JIT_VARL, _lib.EBPF_KERNEL_JIT_FIXED)
-    for src, kern in ((NESTED, fwd), (RECURSE, fwd), (RECURSE_BIG, (_lib.EBPF_KERNEL_GENERAL_T1,))):
+    for src, kern in ((NESTED, fwd), (RECURSE, fwd), (RECURSE_BIG, fwd),
+                      (RECURSE_HUGE, (_lib.EBPF_KERNEL_GENERAL_T1,))):
         img = assemble(src)
         p = Program(img)
         frames = torch.zeros(64 * 64, dtype=torch.uint8, device=cuda)
@@ -99,7 +109,7 @@ def test_call_programs_directed(cuda, oracle_mod):
         _same_outputs(got, _run_full(img, pkts, cuda, generic=True), src[:20])
         prod = _run_prod(img, pkts, cuda)
         _check_prod_against_oracle(oracle_mod, img, pkts, prod, tag="prod " + src[:20])
-    assert (got["status"] == 6).all()  # RECURSE_BIG: ST_CALLDEPTH
+    assert (got["status"] == 6).all()  # RECURSE_HUGE: ST_CALLDEPTH
 
 
 @pytest.mark.gpu

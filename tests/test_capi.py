@@ -94,8 +94,8 @@ def test_forward_only_selection(product_lib):
     assert fwd(assemble("ja -1\nexit")) == 0                   # jump to itself
     assert fwd(assemble("jeq r1, 0, +5\nexit")) == 1           # target past the end
     assert fwd(assemble("stb [r10-1], 1\nexit")) == 0          # tier 1
-    assert fwd(assemble("mov r0, 0\n" * 255 + "exit")) == 1    # 256 micro-ops
-    assert fwd(assemble("mov r0, 0\n" * 256 + "exit")) == 0
+    assert fwd(assemble("mov r0, 0\n" * 4095 + "exit")) == 1   # EBPF_MAX_COMPILED_UOPS
+    assert fwd(assemble("mov r0, 0\n" * 4096 + "exit")) == 0
     assert product_lib.ebpf_prog_forward_only(None) == -1
 
 
