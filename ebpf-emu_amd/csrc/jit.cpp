@@ -333,7 +333,9 @@ struct Compiler {
       if (is_jump(o)) {
         const uint32_t x = t[i].x;  // the canonical taken target (PC_DONE past the end)
         const uint32_t np = t[i].npc;
-        if (x < n) target[x] = 1;
+        // (a successor at i + 1 keeps its lanes in exec -- jtail, ja -- and parks none there: no
+        // re-admission unless another jump targets it; a back edge parks both, below)
+        if (x < n && x != i + 1) target[x] = 1;
         if (np < n && np != i + 1) target[np] = 1;
         // a back edge parks both successors (the fall-through one at i + 1)
         if (loops && ((x <= i && x < n) || (np <= i && np < n)) && i + 1 < n) target[i + 1] = 1;
@@ -729,6 +731,15 @@ struct Compiler {
   uint32_t next_start(uint32_t i) const {
     uint32_t j = i + 1;
     while (j < n && !start[j]) j++;
+    return j;
+  }
+
+  // The next block after i whose entry can re-admit parked lanes (a jump target), or n: with no
+  // lane running, the blocks before it have nothing to do (a rule chain whose first test sent every
+  // lane to the next rule skips the rule's other blocks in one branch).
+  uint32_t next_target(uint32_t i) const {
+    uint32_t j = i + 1;
+    while (j < n && !target[j]) j++;
     return j;
   }
 
@@ -1411,7 +1422,7 @@ struct Compiler {
     main += ".L" + P + "end:\n";
     ool += overlay_routines();
     if (!ool.empty()) main += "s_branch .Ldone" + m.n + "\n" + ool;
-    out = main;
+    out = peephole(main);
     return true;
   }
 
@@ -2133,7 +2144,7 @@ struct Compiler {
         if (target[i])
           main += "s_or_saveexec_b64 s[64:65], -1\nv_cmp_eq_u32 vcc, " + std::to_string(i) +
                   ", v28\ns_or_b64 exec, s[64:65], vcc\n";
-        main += "s_cbranch_execz .L" + P + "b" + std::to_string(next_start(i)) + "\n";
+        main += "s_cbranch_execz .L" + P + "b" + std::to_string(next_target(i)) + "\n";
         if (loops && hoist[i] != -2) main += "v_mov_b32 v28, " + std::to_string(hoist[i]) + "\n";
         if (loops && proven && !counted_entry(m, i, P, main, ool)) return false;
         if (loops) main += ".L" + P + "body" + std::to_string(i) + ":\n";
@@ -2966,7 +2977,7 @@ struct Compiler {
     main += ".L" + P + "end:\n";
     ool += overlay_routines();
     if (!ool.empty()) main += "s_branch .Ldone" + m.n + "\n" + ool;
-    out = main;
+    out = peephole(main);
     return true;
   }
 
@@ -3083,7 +3094,9 @@ struct Compiler {
   }
 
   // mov + add of the same 64-bit destination in a row (e.g. `mov r4, r1; add r4, r3`, adjacent
-  // micro-ops with no block entry between them): one add from the moved source.
+  // micro-ops with no block entry between them): one add from the moved source. mov + and / or /
+  // xor with an operand that is not the destination (`mov r8, r5; and r8, 0xff`, a rule's mask):
+  // the two halves' ops from the moved source (an and with 0 a move of 0).
   static std::string peephole(const std::string& text) {
     std::vector<std::string> ln;
     for (size_t p = 0; p < text.size();) {
@@ -3106,6 +3119,59 @@ struct Compiler {
           out += "v_lshl_add_u64 " + D + ", v[" + std::to_string(s0) + ":" + std::to_string(s1) +
                  "], 0, " + ln[i + 1].substr(head.size()) + "\n";
           i++;
+          continue;
+        }
+        // (an s_mov of the op's constant may sit between: it touches no VGPR)
+        const size_t k = i + 1 < ln.size() && ln[i + 1].compare(0, 10, "s_mov_b32 ") == 0 ? i + 2 : i + 1;
+        auto half = [&](size_t j, uint32_t d, std::string& op, std::string& x) {
+          char o[16], a[64], b[32];
+          if (j >= ln.size() || sscanf(ln[j].c_str(), "%15s v%*u, %63[^,], %31s", o, a, b) != 3) return false;
+          op = o, x = a;
+          const std::string vd = "v" + std::to_string(d);
+          return (op == "v_and_b32" || op == "v_or_b32" || op == "v_xor_b32") &&
+                 ln[j] == op + " " + vd + ", " + x + ", " + vd && x.find('v') == std::string::npos;
+        };
+        std::string o0, x0, o1, x1;
+        if (d1 == d0 + 1 && s1 == s0 + 1 && half(k, d0, o0, x0) && half(k + 1, d1, o1, x1) && o0 == o1) {
+          if (k == i + 2) out += ln[i + 1] + "\n";
+          out += o0 + " v" + std::to_string(d0) + ", " + x0 + ", v" + std::to_string(s0) + "\n";
+          out += o0 == "v_and_b32" && x1 == "0"
+                     ? "v_mov_b32 v" + std::to_string(d1) + ", 0\n"
+                     : o0 + " v" + std::to_string(d1) + ", " + x1 + ", v" + std::to_string(s1) + "\n";
+          i = k + 1;
+          continue;
+        }
+      }
+      out += ln[i] + "\n";
+    }
+    return narrow_compares(out);
+  }
+
+  // A 64-bit compare of a register whose high half was just zeroed with a constant below 2^32
+  // (`v_mov_b32 vH, 0`, s[48:49] = {K, 0}, `v_cmp_<op>_[iu]64 vcc, s[48:49], v[L:H]`, in a row):
+  // both sides lie in [0, 2^32), where the signed and unsigned orders agree, so the 32-bit
+  // unsigned compare of the low halves gives the same vcc.
+  static std::string narrow_compares(const std::string& text) {
+    std::vector<std::string> ln;
+    for (size_t p = 0; p < text.size();) {
+      size_t e = text.find('\n', p);
+      if (e == std::string::npos) e = text.size();
+      ln.push_back(text.substr(p, e - p));
+      p = e + 1;
+    }
+    std::string out;
+    for (size_t i = 0; i < ln.size(); i++) {
+      char op[8], sg;
+      uint32_t lo, hi, h0;
+      if (i >= 3 && ln[i - 1] == "s_mov_b32 s49, 0x0" && ln[i - 2].compare(0, 15, "s_mov_b32 s48, ") == 0 &&
+          sscanf(ln[i - 3].c_str(), "v_mov_b32 v%u, 0", &h0) == 1 && ln[i - 3] == "v_mov_b32 v" + std::to_string(h0) + ", 0" &&
+          sscanf(ln[i].c_str(), "v_cmp_%2[a-z]_%c64 vcc, s[48:49], v[%u:%u]", op, &sg, &lo, &hi) == 4 &&
+          (sg == 'u' || sg == 'i') && hi == lo + 1 && hi == h0 &&
+          ln[i] == std::string("v_cmp_") + op + "_" + sg + "64 vcc, s[48:49], v[" + std::to_string(lo) +
+                       ":" + std::to_string(hi) + "]") {
+        const std::string o(op);
+        if (o == "eq" || o == "ne" || o == "gt" || o == "ge" || o == "lt" || o == "le") {
+          out += "v_cmp_" + o + "_u32 vcc, s48, v" + std::to_string(lo) + "\n";
           continue;
         }
       }
