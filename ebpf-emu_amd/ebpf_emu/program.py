@@ -71,7 +71,8 @@ class Program:
 
     def compile(self) -> bool:
         """Compile to gfx950 code now (ebpf_prog_compile): True if this is a compiled program
-        (tier 0, <= 256 micro-ops), False if it runs interpreted."""
+        (tier 0 or the stack / store tiers, <= EBPF_MAX_COMPILED_UOPS = 4096 micro-ops), False if it
+        runs interpreted."""
         rc = _lib.lib().ebpf_prog_compile(self._h)
         if rc < 0:
             raise _lib.EbpfError(rc, "ebpf_prog_compile")
