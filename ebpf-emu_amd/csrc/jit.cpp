@@ -3133,7 +3133,14 @@ struct Compiler {
         };
         std::string o0, x0, o1, x1;
         if (d1 == d0 + 1 && s1 == s0 + 1 && half(k, d0, o0, x0) && half(k + 1, d1, o1, x1) && o0 == o1) {
-          if (k == i + 2) out += ln[i + 1] + "\n";
+          // (the s_mov's constant straight into the low half's op -- a VOP2 literal -- when only
+          // that op reads it)
+          char sreg[16], kv[32];
+          if (k == i + 2 && sscanf(ln[i + 1].c_str(), "s_mov_b32 %15[^,], %31s", sreg, kv) == 2 &&
+              x0 == sreg && x1 != sreg)
+            x0 = kv;
+          else if (k == i + 2)
+            out += ln[i + 1] + "\n";
           out += o0 + " v" + std::to_string(d0) + ", " + x0 + ", v" + std::to_string(s0) + "\n";
           out += o0 == "v_and_b32" && x1 == "0"
                      ? "v_mov_b32 v" + std::to_string(d1) + ", 0\n"
@@ -3150,7 +3157,8 @@ struct Compiler {
   // A 64-bit compare of a register whose high half was just zeroed with a constant below 2^32
   // (`v_mov_b32 vH, 0`, s[48:49] = {K, 0}, `v_cmp_<op>_[iu]64 vcc, s[48:49], v[L:H]`, in a row):
   // both sides lie in [0, 2^32), where the signed and unsigned orders agree, so the 32-bit
-  // unsigned compare of the low halves gives the same vcc.
+  // unsigned compare of the low halves gives the same vcc -- with K as the VOPC's literal (the
+  // s_movs of s[48:49] go: a micro-op's code sets every field register it reads).
   static std::string narrow_compares(const std::string& text) {
     std::vector<std::string> ln;
     for (size_t p = 0; p < text.size();) {
@@ -3159,7 +3167,7 @@ struct Compiler {
       ln.push_back(text.substr(p, e - p));
       p = e + 1;
     }
-    std::string out;
+    std::vector<std::string> out;
     for (size_t i = 0; i < ln.size(); i++) {
       char op[8], sg;
       uint32_t lo, hi, h0;
@@ -3169,15 +3177,19 @@ struct Compiler {
           (sg == 'u' || sg == 'i') && hi == lo + 1 && hi == h0 &&
           ln[i] == std::string("v_cmp_") + op + "_" + sg + "64 vcc, s[48:49], v[" + std::to_string(lo) +
                        ":" + std::to_string(hi) + "]") {
-        const std::string o(op);
-        if (o == "eq" || o == "ne" || o == "gt" || o == "ge" || o == "lt" || o == "le") {
-          out += "v_cmp_" + o + "_u32 vcc, s48, v" + std::to_string(lo) + "\n";
+        const std::string o(op), k = ln[i - 2].substr(15);
+        if ((o == "eq" || o == "ne" || o == "gt" || o == "ge" || o == "lt" || o == "le") &&
+            out.size() >= 2 && out.back() == ln[i - 1] && out[out.size() - 2] == ln[i - 2]) {
+          out.resize(out.size() - 2);
+          out.push_back("v_cmp_" + o + "_u32 vcc, " + k + ", v" + std::to_string(lo));
           continue;
         }
       }
-      out += ln[i] + "\n";
+      out.push_back(ln[i]);
     }
-    return out;
+    std::string r;
+    for (const std::string& l : out) r += l + "\n";
+    return r;
   }
 };
 
