@@ -208,3 +208,55 @@ def test_long_stack_and_store_programs_vs_oracle(cuda, oracle_mod, kind):
         _same(got, ref, f"{kind} it {it}", keys=("status", "r0", "verdict", "counters"))
         full = _run(img, pkts, cuda, **kw)
         _vs_oracle(oracle_mod, img, pkts, full, tag=f"{kind} {it}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layout", ["fixed", "offsets"])
+def test_long_programs_xdp_md(cuda, oracle_mod, layout):
+    """Far-mode code on xdp_md batches (the ctx synthesised in the window, xdp.rs:16-20): the
+    production outputs and the counters == the oracle's, every output == the general
+    interpreter's, on a compiled kernel."""
+    import numpy as np
+    import torch
+
+    from ebpf_emu import Program, _lib
+    from test_gpu_parity import _stage
+
+    rng = random.Random(91 + (layout == "offsets"))
+    for it in range(2):
+        img = gen_long_program(rng, 1200)
+        prog = Program(img)
+        assert prog.compile()
+        if layout == "fixed":
+            n = 300
+            buf = np.frombuffer(bytes(rng.getrandbits(8) for _ in range(64 * n)), dtype=np.uint8)
+            frames = torch.from_numpy(buf.copy()).to(cuda)
+            kw = dict(n=n, stride=64)
+            okw = dict(stride=64)
+        else:
+            pkts = [gen_packet(rng, 100) for _ in range(300)]
+            frames, kw = _stage(pkts, cuda, offsets_layout=True)
+            n = len(pkts)
+            buf = frames.cpu().numpy()
+            okw = dict(offsets=kw["offsets"].cpu().numpy().view(np.uint32),
+                       lens=kw["lens"].cpu().numpy().view(np.uint16))
+        k = prog.batch_kernel(prog.make_batch(frames, xdp_md=True, mem_size=1024, **kw))
+        assert _lib.KERNEL_NAMES[k].startswith("ebpf_tile_jit"), _lib.KERNEL_NAMES[k]
+        cnt = torch.zeros(8, dtype=torch.int64, device=cuda)
+        v = prog.run(frames, mem_size=1024, counters=cnt, xdp_md=True, **kw)
+        rs = prog.run(frames, mem_size=1024, verdict=False, r0=True, status=True, xdp_md=True, **kw)
+        full = prog.run(frames, mem_size=1024, r0=True, status=True, regs=True, xdp_md=True, **kw)
+        gen = prog.run(frames, mem_size=1024, r0=True, status=True, regs=True, xdp_md=True,
+                       generic=True, **kw)
+        torch.cuda.synchronize()
+        r0, st, ocnt = oracle_mod.Program(img).run_batch(buf, n, mem_size=1024, xdp_md=True,
+                                                         threads=4, **okw)
+        assert np.array_equal(rs.status.cpu().numpy(), st), it
+        ok = st == 0
+        assert np.array_equal(rs.r0.cpu().numpy().view(np.uint64)[ok], r0[ok]), it
+        want_v = np.where(st != 0, 0xFF, np.where(r0 < 5, r0, 0xFE)).astype(np.uint8)
+        assert np.array_equal(v.verdict.cpu().numpy(), want_v), it
+        assert list(cnt.cpu().numpy().view(np.uint64)) == list(ocnt), it
+        for key in ("r0", "status", "regs"):
+            assert torch.equal(getattr(full, key), getattr(gen, key)), (it, key)
+        prog.close()
