@@ -734,6 +734,18 @@ struct Compiler {
     return j;
   }
 
+  // Whether micro-op j leaves no lane running into j + 1 in a forward program: an exit or fault
+  // (@EXIT@), a ja elsewhere, a conditional jump whose successors both lie elsewhere (jtail: both
+  // leave). Every branch to a block entry carries an empty exec too (s_cbranch_execz, the fault
+  // tails, KFAULT's exit), so a target there re-admits with exec = the parked lanes directly.
+  bool clears_exec(uint32_t j) const {
+    const Uop& o = uops[j];
+    if (o.op == U_EXIT || o.op == U_FAULT) return true;
+    if (!is_jump(o)) return false;
+    if (o.op == U_JA) return t[j].x != j + 1;
+    return t[j].x != j + 1 && t[j].npc != j + 1;
+  }
+
   // The next block after i whose entry can re-admit parked lanes (a jump target), or n: with no
   // lane running, the blocks before it have nothing to do (a rule chain whose first test sent every
   // lane to the next rule skips the rule's other blocks in one branch).
@@ -2141,7 +2153,9 @@ struct Compiler {
       }
       if (start[i]) {
         main += ".L" + P + "b" + std::to_string(i) + ":\n";
-        if (target[i])
+        if (target[i] && !loops && i > 0 && clears_exec(i - 1))  // (exec is empty here)
+          main += "s_mov_b64 exec, -1\nv_cmpx_eq_u32 vcc, " + std::to_string(i) + ", v28\n";
+        else if (target[i])
           main += "s_or_saveexec_b64 s[64:65], -1\nv_cmp_eq_u32 vcc, " + std::to_string(i) +
                   ", v28\ns_or_b64 exec, s[64:65], vcc\n";
         main += "s_cbranch_execz .L" + P + "b" + std::to_string(next_target(i)) + "\n";
