@@ -883,15 +883,20 @@ struct Compiler {
     // the leaving lanes' LPC by one select on vcc (the pcs are inline constants, or VGPRs above
     // 64), then exec
     std::string pre;
-    const std::string lx = vop3_lpc(lpc_of(x, x_done), "v37", pre),
-                      ln = vop3_lpc(lpc_of(np, n_done), "v38", pre);
-    if (n_next)  // taken lanes leave
+    if (n_next) {  // taken lanes leave
+      const std::string lx = vop3_lpc(lpc_of(x, x_done), "v37", pre);
       return pre + (lx.empty() ? "" : "v_cndmask_b32_e64 v28, v28, " + lx + ", vcc\n") +
              "s_andn2_b64 exec, exec, vcc\n";
-    if (x_next)  // not-taken lanes leave
+    }
+    if (x_next) {  // not-taken lanes leave (a literal pc cannot go in: vcc is the select's one
+                   // constant-bus read)
+      const std::string ln = vop3_lpc(lpc_of(np, n_done), "v38", pre);
       return pre + (ln.empty() ? "" : "v_cndmask_b32_e64 v28, " + ln + ", v28, vcc\n") +
              "s_and_b64 exec, exec, vcc\n";
+    }
     // both leave
+    const std::string lx = vop3_lpc(lpc_of(x, x_done), "v37", pre),
+                      ln = vop3_lpc(lpc_of(np, n_done), "v38", pre);
     std::string s = pre;
     if (!lx.empty() || !ln.empty())
       s += "v_cndmask_b32_e64 v28, " + (ln.empty() ? "v28" : ln) + ", " +
