@@ -1345,6 +1345,33 @@ int ebpf_prog_jit_asm(ebpf_prog* p, int variant, char* buf, size_t cap, size_t* 
   return EBPF_OK;
 }
 
+int ebpf_prog_jit_error(ebpf_prog* p, char* buf, size_t cap, size_t* len) {
+  if (!p) return EBPF_EINVAL;
+  std::lock_guard<std::mutex> lk(p->mu);
+  const int rc = jit_compile_locked(p);
+  std::string m;
+  if (rc < 0 || !p->jit_err.empty()) {
+    m = p->jit_err.empty() ? "the compiler failed" : p->jit_err;
+  } else if (rc == 0) {
+    const size_t n = p->xuops.size();
+    if (n > kJitMaxUops)
+      m = "not compiled: " + std::to_string(n) + " micro-ops (after flattening calls) past "
+          "EBPF_MAX_COMPILED_UOPS (" + std::to_string(kJitMaxUops) + ")";
+    else if (p->xtier == 1)
+      m = "not compiled: memory writes outside the stack window, a constant-address packet store "
+          "past the header window or an atomic outside the stack (the general interpreter's tier 1)";
+    else
+      m = "not compiled";
+  }
+  if (len) *len = m.size();
+  if (buf && cap) {
+    const size_t k = std::min(cap - 1, m.size());
+    std::memcpy(buf, m.data(), k);
+    buf[k] = 0;
+  }
+  return EBPF_OK;
+}
+
 int ebpf_prog_upload(ebpf_prog* p, int device) {
   if (!p || device < 0 || device >= kMaxDevices) return EBPF_EINVAL;
   std::lock_guard<std::mutex> lk(p->mu);

@@ -46,7 +46,7 @@ KERNEL_NAMES = ["ebpfemu::interp_kernel<0>", "ebpfemu::interp_kernel<1>", "ebpfe
 EXPORTS = ["ebpf_batch_init", "ebpf_prog_load", "ebpf_prog_load_hex", "ebpf_prog_free",
            "ebpf_prog_len", "ebpf_prog_insn", "ebpf_prog_tier", "ebpf_prog_forward_only",
            "ebpf_prog_stack_window",
-           "ebpf_workspace_bytes", "ebpf_prog_compile", "ebpf_prog_jit_asm", "ebpf_debug_trace",
+           "ebpf_workspace_bytes", "ebpf_prog_compile", "ebpf_prog_jit_asm", "ebpf_prog_jit_error", "ebpf_debug_trace",
            "ebpf_prog_upload", "ebpf_run_batch", "ebpf_run_batch_multi", "ebpf_batch_kernel", "ebpf_batch_staged",
            "ebpf_pcap_index",
            "ebpf_strerror", "ebpf_version"]
@@ -116,6 +116,7 @@ def lib():
     L.ebpf_prog_compile.argtypes = [vp]
     L.ebpf_debug_trace.argtypes = [ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(sz)]
     L.ebpf_prog_jit_asm.argtypes = [vp, ctypes.c_int, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
+    L.ebpf_prog_jit_error.argtypes = [vp, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
     L.ebpf_workspace_bytes.argtypes = [vp, ctypes.POINTER(Batch), ctypes.c_int]
     L.ebpf_workspace_bytes.restype = u64
     L.ebpf_prog_upload.argtypes = [vp, ctypes.c_int]

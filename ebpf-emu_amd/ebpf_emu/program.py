@@ -91,6 +91,19 @@ class Program:
         return buf.value.decode()
 
     @property
+    def jit_error(self) -> str:
+        """Why the program is not (wholly) compiled (ebpf_prog_jit_error): the compiler's or the
+        assembler's message, or why it is not a program the compiler takes; "" if compiled."""
+        L = _lib.lib()
+        n = ctypes.c_size_t(0)
+        rc = L.ebpf_prog_jit_error(self._h, None, 0, ctypes.byref(n))
+        if rc:
+            raise _lib.EbpfError(rc, "ebpf_prog_jit_error")
+        buf = ctypes.create_string_buffer(n.value + 1)
+        L.ebpf_prog_jit_error(self._h, buf, n.value + 1, ctypes.byref(n))
+        return buf.value.decode()
+
+    @property
     def window_bytes(self) -> int:
         """Bytes of each packet's 64-byte header window the compiled fixed-slot kernel DMAs
         (jit.cpp window_chunks: the 16-byte chunks its constant-address loads and stores reach;

@@ -185,8 +185,9 @@ int ebpf_prog_stack_window(const ebpf_prog* prog);
  * dispatch, for programs of <= EBPF_MAX_COMPILED_UOPS micro-ops. Forward-only programs get the forward kernels
  * (batches with max_steps >= the program length); every such program also gets the loop kernel
  * (back edges, or a step budget that can bind: the exact budget of the reference's step count). Needs no
- * GPU; done implicitly by the first upload. Returns 1 = compiled, 0 = not such a program (or
- * compilation disabled by EBPFEMU_NO_JIT=1), EBPF_EJIT on a compiler failure. */
+ * GPU; done implicitly by the first upload. Returns 1 = compiled, 0 = not such a program,
+ * EBPF_EJIT on a compiler failure (ebpf_prog_jit_error says why; EBPF_BATCH_NO_JIT runs a compiled
+ * program's batch interpreted). */
 int ebpf_prog_compile(ebpf_prog* prog);
 
 /* The compiled program's gfx950 assembly (variant 0: forward-only, batches with init_regs; 1:
@@ -194,6 +195,12 @@ int ebpf_prog_compile(ebpf_prog* prog);
  * loop-program kernel), for inspection: copies up to cap bytes (NUL-terminated) and sets *len to
  * the full length. EBPF_EINVAL if that variant is not compiled. */
 int ebpf_prog_jit_asm(ebpf_prog* prog, int variant, char* buf, size_t cap, size_t* len);
+
+/* Why the program is not (wholly) compiled: compiles it first, then copies up to cap bytes
+ * (NUL-terminated) of the reason -- the compiler's or assembler's error, or why the program is
+ * not one the compiler takes -- and sets *len to its length; "" when every variant compiled.
+ * (new: no reference counterpart; diagnostics for ebpf_prog_compile) */
+int ebpf_prog_jit_error(ebpf_prog* prog, char* buf, size_t cap, size_t* len);
 
 /* Device scratch a batch needs (counter shards; tier 1 adds per-wave memory images). */
 uint64_t ebpf_workspace_bytes(const ebpf_prog* prog, const ebpf_batch* batch, int device);

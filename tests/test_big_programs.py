@@ -84,11 +84,22 @@ def test_long_stack_and_store_programs_compile():
 
 
 def test_past_the_limit_interpreted():
-    """Past kJitMaxUops the program loads and runs on the general interpreter (not compiled)."""
+    """Past kJitMaxUops the program loads and runs on the general interpreter (not compiled), and
+    ebpf_prog_jit_error says so; a compiled program has no error."""
     from ebpf_emu import Program
+    from ebpf_emu import workloads as W
+    from ebpf_emu.asm import assemble
 
     p = Program(gen_long_program(random.Random(5), 4200))
     assert not p.compile()
+    assert "past EBPF_MAX_COMPILED_UOPS (4096)" in p.jit_error, p.jit_error
+    p.close()
+    p = Program(W.program("acl_rules"))
+    assert p.compile() and p.jit_error == ""
+    p.close()
+    # (a store at a constant address past the header window: the general interpreter's tier 1)
+    p = Program(assemble("mov r3, 100\nstxw [r3+0], r3\nmov r0, 2\nexit"))
+    assert not p.compile() and "tier 1" in p.jit_error, p.jit_error
     p.close()
 
 
