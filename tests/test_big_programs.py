@@ -271,3 +271,26 @@ def test_long_programs_xdp_md(cuda, oracle_mod, layout):
         for key in ("r0", "status", "regs"):
             assert torch.equal(getattr(full, key), getattr(gen, key)), (it, key)
         prog.close()
+
+
+@pytest.mark.gpu
+def test_long_programs_fuzz(cuda, oracle_mod):
+    """Random long programs of every form (forward, counted loops, stack window, packet-pointer
+    stores; 400-2500 instructions) on offsets + lens batches: production outputs and counters ==
+    the oracle's, every output == the general interpreter's, and each on a compiled kernel."""
+    from test_gpu_jit import _run, _same, _vs_oracle
+
+    rng = random.Random(20261018)
+    for it in range(12):
+        kind = ["fwd", "loop", "stack", "store"][it % 4]
+        n = rng.choice([400, 900, 1600, 2500])
+        img = gen_long_program(rng, n, loops=kind == "loop", stack=kind == "stack",
+                               store=kind == "store")
+        pkts = [gen_packet(rng, 100) for _ in range(rng.choice([64, 130]))]
+        name = _kernel(img, cuda, "offsets", pkts)
+        assert name.startswith("ebpf_tile_jit"), (kind, n, name)
+        prod = _run(img, pkts, cuda, prod=True, offsets_layout=True)
+        ref = _run(img, pkts, cuda, prod=True, no_jit=True, offsets_layout=True)
+        _same(prod, ref, f"{kind} {n} it {it}", keys=("status", "r0", "verdict", "counters"))
+        full = _run(img, pkts, cuda, offsets_layout=True)
+        _vs_oracle(oracle_mod, img, pkts, full, tag=f"{kind} {n} {it}")
