@@ -1322,9 +1322,14 @@ s_branch .Ld{tag}%=
     return main, ool
 
 
-def jit_statement_loop():
+def jit_statement_loop(single=False):
+    """single: the occupancy variant (ebpf_tile_jit_fixed_occ) -- one window buffer per wave, so
+    the next tile is claimed and its windows DMA'd only once this tile's code is done with the
+    buffer; the other waves of the SIMD (6 instead of 4) hide that DMA."""
     dma_f, ool_f = loop_dma("{T3}", "%[winb]", "f")
     dma_n, ool_n = loop_dma("%[ntile]", "%[nwinb]", "n")
+    if single:
+        dma_n, ool_n = loop_dma("{T3}", "%[winb]", "g")
     # the r0 / status / register outputs (%[oflags]): EPILOGUE's stores with T23 = packet index
     out_tail = EPILOGUE[EPILOGUE.index("s_cmp_lg_u64 {ER0}, 0"):EPILOGUE.index(".Lend%=:")]
     out_tail = out_tail.replace(".Lend%=", ".Loutd%=") + "s_branch .Loutd%="
@@ -1336,7 +1341,9 @@ s_mov_b32 {T3}, %[tile]
 """ + dma_f + """.Lent%=:
 s_movk_i32 %[cdn], 511
 .Lloop%=:
-; the next tile: nt = wg + (ordinal + waves) * grid, DMA'd into the other buffer
+""" + ("""; this tile's windows (one buffer: DMA'd at the end of the tile before)
+s_waitcnt vmcnt(0)
+""" if single else """; the next tile: nt = wg + (ordinal + waves) * grid, DMA'd into the other buffer
 s_mov_b64 exec, 1
 ds_add_rtn_u32 %[ordv], %[nxa], %[one]
 s_waitcnt lgkmcnt(0)
@@ -1352,7 +1359,7 @@ s_branch .Ldmad%=
 .Lnonext%=:
 s_waitcnt vmcnt(0)
 .Ldmad%=:
-; this tile's lanes (fixed slots: every lane of a whole tile is a packet of length %[lenc])
+""") + """; this tile's lanes (fixed slots: every lane of a whole tile is a packet of length %[lenc])
 s_mov_b32 {KMEM}, %[k_mem]
 s_mov_b64 {KR10}, %[k_r10]
 s_mov_b64 {VM}, -1
@@ -1378,7 +1385,7 @@ s_cbranch_scc1 .Linitx%=
 ;@@JITINIT@@
 .Linitd%=:
 
-; JIT N=%= fixed=%[fixed] loops=%[loops] aligned=%[aligned] xdp=%[xdpf]
+; JIT N=%= fixed=%[fixed] loops=%[loops] aligned=%[aligned] xdp=%[xdpf]""" + (" occ=1" if single else "") + """
 ;@@JIT@@
 .Ldone%=:
 ; verdict byte, the lane's counter bucket (verdict 0..4, 0xfe -> 5, 0xff -> 6) into %[acc]
@@ -1409,12 +1416,25 @@ s_cbranch_scc1 .Lout%=
 .Loutd%=:
 s_mov_b64 exec, -1
 s_sub_u32 %[cdn], %[cdn], 1
+""" + ("""; the next tile into the one buffer (every LDS read of this tile has returned: the wait below)
+s_mov_b64 exec, 1
+ds_add_rtn_u32 %[ordv], %[nxa], %[one]
+s_waitcnt lgkmcnt(0)
+s_mov_b64 exec, -1
+v_readfirstlane_b32 {T3}, %[ordv]
+s_add_u32 {T3}, {T3}, %[wpb]
+s_mul_i32 {T3}, {T3}, %[grid]
+s_add_u32 %[ntile], {T3}, %[wg]
 s_cmp_lt_u32 %[ntile], %[ntiles]
+s_cbranch_scc0 .Lfin%=
+s_mov_b32 %[tile], %[ntile]
+s_mov_b32 {T3}, %[ntile]
+""" + dma_n if single else """s_cmp_lt_u32 %[ntile], %[ntiles]
 s_cbranch_scc0 .Lfin%=
 s_mov_b32 %[tile], %[ntile]
 s_xor_b32 %[winb], %[winb], %[wx]
 s_xor_b32 %[nwinb], %[nwinb], %[wx]
-s_cmp_eq_u32 %[cdn], 0
+""") + """s_cmp_eq_u32 %[cdn], 0
 s_cbranch_scc0 .Lloop%=
 s_branch .Lexit%=
 .Lfin%=:
@@ -1761,6 +1781,8 @@ s_cbranch_scc1 .Linitx%=
 s_mov_b64 exec, {VM}
 v_cmp_eq_u32 vcc, 0x80, {ST}
 s_cbranch_vccz .Lnodo%=
+s_bitcmp1_b32 %[fl], 10
+s_cbranch_scc1 .Ldofail%=
 s_andn2_b64 {VM}, {VM}, vcc
 s_mov_b64 {T0}, vcc
 s_mov_b64 exec, vcc
@@ -1783,6 +1805,12 @@ v_lshl_add_u64 {T89}, {T1011}, 0, %[k_dix]
 s_lshl_b32 {T1L}, %[tile], 6
 v_add_u32 {t4}, {T1L}, %[lane]
 global_store_dword {T89}, {t4}, off
+s_branch .Lnodo%=
+.Ldofail%=:
+; (no deopt pass follows this launch, StackPlan::no_deopt: a lane that left anyway is a failed
+; load-time proof -- status EBPF_ST_JIT, counted as a fault, never silently dropped)
+s_mov_b64 exec, vcc
+v_mov_b32 {ST}, 8
 .Lnodo%=:
 s_mov_b64 exec, {VM}
 v_cmp_gt_u64 vcc, 5, {RF}
@@ -1958,6 +1986,13 @@ def main():
         f.write("// GENERATED by gen_tile.py -- do not edit. The compiled fixed-slot kernel's tile "
                 "loop (one statement, many tiles).\n// clang-format off\n" + cstr(text) +
                 "\n// clang-format on\n")
+    # ... its occupancy variant (ebpf_tile_jit_fixed_occ: one window buffer per wave)
+    text = F(jit_statement_loop(single=True))
+    assert "{" not in text, "unsubstituted register name: " + text[text.index("{"):][:40]
+    with open(os.path.join(HERE, "tile_jit_loop1.inc"), "w") as f:
+        f.write("// GENERATED by gen_tile.py -- do not edit. The compiled fixed-slot kernel's tile "
+                "loop, one window buffer per wave (ebpf_tile_jit_fixed_occ).\n// clang-format off\n" +
+                cstr(text) + "\n// clang-format on\n")
     # the compiled var kernel's tile loop (jit_statement_varl), and its statement for
     # stack-window programs (ebpf_tile_jit_varl_stack: the stack window in v[80:95] too)
     text = F(jit_statement_varl())

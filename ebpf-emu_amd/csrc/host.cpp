@@ -12,6 +12,7 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <thread>
 #include <set>
 #include <string>
 #include <vector>
@@ -202,6 +203,10 @@ int parse_hex_u64s(const char* hex, std::vector<uint8_t>& image) {
 struct DevWorkspace {
   void* ptr = nullptr;
   uint64_t bytes = 0;
+  // buffers outgrown by a larger batch: kept, not freed -- another host thread may have taken
+  // the old pointer for a batch on the same (device, stream) it has not launched yet (the growth
+  // doubles, so these add at most the current size)
+  std::vector<void*> retired;
 };
 
 std::mutex g_ws_mu;
@@ -248,6 +253,7 @@ struct ebpf_prog {
   // program, < 0 failed
   int jit_state = 0;
   bool jit_has[kJitVariants] = {};
+  bool jit_occ[kJitVariants] = {};  // the variant's code also went into ebpf_tile_jit_fixed_occ
   std::vector<char> jit_co[kJitVariants];
   bool jit_deep = false;  // variant 2 compiled into ebpf_tile_jit_loop_deep
   std::string jit_asm[kJitVariants];
@@ -311,21 +317,57 @@ static int jit_compile_locked(ebpf_prog* p) {
       p->jit_state = 2;
     } else {
       p->jit_state = 1;
+      // the variants are independent compiles (own Compiler, own code object; the program's
+      // tables are read-only here): all at once, one thread each, then their results in order
+      struct Res {
+        bool ok = false, deep = false, occ = false;
+        std::string err, text;
+        std::vector<char> co;
+      };
+      Res r[kJitVariants];
+      std::vector<std::thread> th;
+      for (int v = 0; v < kJitVariants; v++) {
+        if (!p->jit_has[v]) continue;
+        th.emplace_back([p, v, &r] {
+          Res& q = r[v];
+          if (v == 5 || v == 6)
+            q.ok = jit_compile_loop(p->xuops, p->ltuops, p->ltuopsx, q.co, &q.err, &q.text, nullptr,
+                                    &q.deep, 0, true, v == 6);
+          else if (v == 4)
+            q.ok = jit_compile_loop(p->puops, p->pltuops, p->pltuopsx, q.co, &q.err, &q.text,
+                                    nullptr, &q.deep, p->pguard_k);
+          else
+            q.ok = !(g_fail_stack_jit && p->stack.k) &&
+                   (v == 2 ? jit_compile_loop(p->xuops, p->ltuops, p->ltuopsx, q.co, &q.err, &q.text,
+                                              p->stack.k ? &p->stack : nullptr, &q.deep)
+                           : jit_compile(p->xuops, v == 3 ? p->tuopsk_xdp : v ? p->tuopsk : p->tuops,
+                                         q.co, &q.err, &q.text, p->stack.k ? &p->stack : nullptr,
+                                         &q.occ));
+        });
+      }
+      for (std::thread& t : th) t.join();
+      auto take = [&](int v) {
+        p->jit_co[v] = std::move(r[v].co);
+        p->jit_asm[v] = std::move(r[v].text);
+        p->jit_occ[v] = r[v].occ;
+        bool* deep = v == 2 ? &p->jit_deep : v == 4 ? &p->pjit_deep : v == 5 ? &p->xjit_deep
+                     : v == 6 ? &p->rjit_deep : nullptr;
+        if (deep) *deep = r[v].deep;
+      };
       for (int v = 0; v < kJitVariants && p->jit_state == 1; v++) {
         if (!p->jit_has[v]) continue;
+        take(v);
         if (v == 5 || v == 6) {  // the xdp_md copies: dropped (staged / the plain loop program
                                  // runs) if they fail
-          std::string e;
-          if (!jit_compile_loop(p->xuops, p->ltuops, p->ltuopsx, p->jit_co[v], &e, &p->jit_asm[v],
-                                nullptr, v == 5 ? &p->xjit_deep : &p->rjit_deep, 0, true, v == 6)) {
+          if (!r[v].ok) {
             p->jit_has[v] = false;
             p->jit_co[v].clear();
           }
           continue;
         }
         if (v == 4) {  // the promoted program: dropped (the stack loop kernel stays) if it fails
-          if (!jit_compile_loop(p->puops, p->pltuops, p->pltuopsx, p->jit_co[4], &p->jit_err,
-                                &p->jit_asm[4], nullptr, &p->pjit_deep, p->pguard_k)) {
+          if (!r[4].ok) {
+            p->jit_err = r[4].err;
             p->jit_has[4] = false;
             p->jit_co[4].clear();
             p->puops.clear();
@@ -334,15 +376,8 @@ static int jit_compile_locked(ebpf_prog* p) {
           }
           continue;
         }
-        const bool ok = !(g_fail_stack_jit && p->stack.k) &&
-                        (v == 2 ? jit_compile_loop(p->xuops, p->ltuops, p->ltuopsx, p->jit_co[v],
-                                                  &p->jit_err, &p->jit_asm[v],
-                                                  p->stack.k ? &p->stack : nullptr, &p->jit_deep)
-                               : jit_compile(p->xuops,
-                                             v == 3 ? p->tuopsk_xdp : v ? p->tuopsk : p->tuops,
-                                             p->jit_co[v],
-                                             &p->jit_err, &p->jit_asm[v],
-                                             p->stack.k ? &p->stack : nullptr));
+        const bool ok = r[v].ok;
+        if (!ok) p->jit_err = r[v].err;
         if (!ok && v >= 1 && p->stack.k && !p->jit_has[0]) {
           // a stack-window program whose code does not assemble (e.g. branches past the
           // assembler's reach in a huge program): it stays on the general interpreter. Its
@@ -360,6 +395,10 @@ static int jit_compile_locked(ebpf_prog* p) {
           p->jit_has[1] = p->jit_has[2] = false;
           p->jit_co[1].clear();
           p->jit_co[2].clear();
+          for (int w = v + 1; w < kJitVariants; w++) {  // (compiled alongside, never used)
+            p->jit_has[w] = false;
+            p->jit_co[w].clear();
+          }
           break;
         }
         if (!ok) p->jit_state = EBPF_EJIT;
@@ -1051,7 +1090,7 @@ static StackAnalysis analyze_stack(const std::vector<Uop>& uops) {
   res.plan.dyn = std::move(dyns);
   res.plan.any_dyn = any_dyn;
   // (store mode: whether the deopt pass can be left out for main.rs-layout batches, jit.cpp)
-  res.plan.no_deopt = any_dyn && store_mode_no_deopt(uops, res.plan);
+  res.plan.no_deopt = any_dyn && store_mode_no_deopt(uops, res.plan, nullptr, &res.plan.kld);
   return res;
 }
 
@@ -1321,9 +1360,24 @@ int ebpf_prog_insn(const ebpf_prog* p, size_t i, int32_t* imm, int64_t* imm64, i
 int ebpf_prog_tier(const ebpf_prog* p) { return p ? p->tier : -1; }
 
 static_assert(kJitMaxUops == EBPF_MAX_COMPILED_UOPS, "include/ebpf_emu.h names the compiler's limit");
-int ebpf_prog_forward_only(const ebpf_prog* p) { return p ? (p->duops.empty() ? 0 : 1) : -1; }
+int ebpf_prog_forward_only(const ebpf_prog* p) {
+  if (!p) return -1;
+  if (p->duops.empty()) return 0;
+  if (p->uops.size() <= (size_t)kMaxDagUops) return 1;
+  // past dag_kernel's table only the compiled forward kernels run it (batch_kind dag_ok): 1 only
+  // when they compiled (a compiler failure leaves every batch on the general interpreter)
+  ebpf_prog* q = const_cast<ebpf_prog*>(p);
+  std::lock_guard<std::mutex> lk(q->mu);
+  (void)jit_compile_locked(q);
+  return q->jit_state == 1 && (q->jit_has[0] || q->jit_has[1]) ? 1 : 0;
+}
 
 int ebpf_prog_stack_window(const ebpf_prog* p) { return p ? (int)p->stack.k : -1; }
+
+int ebpf_prog_store_mode(const ebpf_prog* p) {
+  if (!p) return -1;
+  return !p->stack.any_dyn ? 0 : p->stack.no_deopt ? 2 : 1;
+}
 
 int ebpf_prog_compile(ebpf_prog* p) {
   if (!p) return EBPF_EINVAL;
@@ -1425,6 +1479,7 @@ int ebpf_prog_upload(ebpf_prog* p, int device) {
                  (v == 5 && p->xjit_deep) || (v == 6 && p->rjit_deep))  // (the code is in the
           p->jit_fn[device][v].loop = p->jit_fn[device][v].loop_deep;     // deep-prefetch kernel)
         p->jit_fn[device][v].var_only = p->stack.any_dyn;
+        if (!p->jit_occ[v]) p->jit_fn[device][v].fixed_occ = nullptr;
       }
   }
   TUop* tp = nullptr;
@@ -1690,18 +1745,16 @@ static int batch_workspace(const ebpf_batch* b, uint64_t need, int device, hipSt
   std::lock_guard<std::mutex> lk(g_ws_mu);
   DevWorkspace& w = g_ws[{device, (void*)s}];
   if (w.bytes < need) {
-    if (w.ptr) {
-      hipStreamSynchronize(s);
-      hipFree(w.ptr);
-      w.ptr = nullptr;
-      w.bytes = 0;
+    const uint64_t grow = std::max(need, 2 * w.bytes);
+    void* np = nullptr;
+    if (hipMalloc(&np, grow) != hipSuccess) return EBPF_ENOMEM;
+    if (hipMemset(np, 0, kWsSlotsOff) != hipSuccess) {  // shards start at zero
+      hipFree(np);
+      return EBPF_EHIP;
     }
-    if (hipMalloc(&w.ptr, need) != hipSuccess) {
-      w.ptr = nullptr;
-      return EBPF_ENOMEM;
-    }
-    if (hipMemset(w.ptr, 0, kWsSlotsOff) != hipSuccess) return EBPF_EHIP;  // shards start at zero
-    w.bytes = need;
+    if (w.ptr) w.retired.push_back(w.ptr);
+    w.ptr = np;
+    w.bytes = grow;
   }
   *out = (uint8_t*)w.ptr;
   return EBPF_OK;
@@ -1873,6 +1926,7 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* bin, const ebpf_batch_out* ou
     a.deopt_idx = (uint32_t*)(ws + kWsSlotsOff +
                               align16(std::max<uint64_t>(tier1_slots_bytes(p, b, device), bin_bytes)));
     if (p->stack.any_dyn) a.ovf = (uint8_t*)a.deopt_idx + align16(b->n * 4);
+    if (!pass) a.deopt_pass = 2;  // (no pass follows: a lane that leaves faults EBPF_ST_JIT)
   }
   hipError_t e = launch_interp(kind, a, grid, s, jit, stk);
   if (pass && e == hipSuccess) {

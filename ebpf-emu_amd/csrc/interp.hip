@@ -222,20 +222,8 @@ __device__ __forceinline__ void put_image(uint8_t* row, uint32_t d, uint32_t v, 
   for (uint32_t i = 0; i < 4 && d * 4 + i < mem_size; i++) row[d * 4 + i] = (uint8_t)(v >> (8 * i));
 }
 
-// ---- tier-1 image: lane-interleaved dwords, dword d of this lane at img[d * 64] ----
-__device__ __forceinline__ uint64_t img_read(const uint32_t* img, uint32_t a, uint32_t w) {
-  const uint32_t* p = img + (size_t)(a >> 2) * kWave;
-  const uint32_t s = a & 3;
-  const uint32_t d0 = p[0];
-  const uint32_t d1 = (s + w > 4) ? p[kWave] : 0u;
-  uint64_t v = __builtin_amdgcn_alignbyte(d1, d0, s);
-  if (w == 8) {
-    const uint32_t d2 = s ? p[2 * kWave] : 0u;
-    v |= (uint64_t)__builtin_amdgcn_alignbyte(d2, d1, s) << 32;
-  }
-  return v & wmask(w);
-}
-
+// ---- tier-1 image: lane-interleaved dwords, dword d of this lane at img[d * 64] (materialised
+// lazily, interp_kernel: lazy_read / lazy_write) ----
 __device__ __forceinline__ void img_write(uint32_t* img, uint32_t a, uint32_t w, uint64_t v) {
   uint32_t* p = img + (size_t)(a >> 2) * kWave;
   const uint32_t s = a & 3;
@@ -646,17 +634,15 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
       st = EBPF_ST_BADPKT;
       pc = PC_DONE;
     }
+    // tier 1: the image (main.rs:16-27: the packet, then zeros to mem_size) is materialised in
+    // the lane's scratch lazily, a block at a time (32 blocks of 2^bsh dwords cover it: 32 bytes
+    // for the 1 KiB default): a block is written from the packet / zeros by the first store into
+    // it (bit b of `ib`), and reads of a block never stored to compute the initial bytes instead.
+    // The eager copy wrote mem_size bytes per packet (1 GiB per 1 Mi-packet batch at 1 KiB) where
+    // a program typically stores into one or two blocks.
+    const uint32_t m_img = (TIER == 1 && pc != PC_DONE) ? len : 0u;
+    uint32_t ib = 0;
     if (TIER == 1) {
-      const uint32_t md = (mem_size + 3) / 4;
-      const uint32_t m = (pc != PC_DONE) ? len : 0u;
-      if (a.xdp) {
-        for (uint32_t d = 0; d < md; d++)
-          img[(size_t)d * kWave] = d * 4 >= m ? 0u : d == 0 ? 8u : d == 1 ? len
-                                 : (uint32_t)pkt_read(base, d * 4 - 8, 4, plen);
-      } else {
-        for (uint32_t d = 0; d < md; d++)
-          img[(size_t)d * kWave] = (d * 4 < m) ? (uint32_t)pkt_read(base, d * 4, 4, len) : 0u;
-      }
       // the caller's initial frame stack (Emu.fp, emu.rs:26): an EXIT pops it (emu.rs:273-279)
       csp = a.init_fp_len;
       for (uint32_t i = 0; i < csp; i++) cstack[(size_t)i * kWave] = a.init_fp[i];
@@ -679,6 +665,43 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
     // there ("act"). The step is computed by all lanes and COMMITTED through selects on act,
     // so the eBPF register file (22 VGPRs, indexed by the scalar dst/src via s_set_gpr_idx)
     // is never inside divergent control flow; only memory accesses are predicated on act.
+    // (tier 1) dword d of the initial image; whether dword d is in a materialised block; a block
+    // materialised; the lazy image's reads and writes (img_read / img_write's layout)
+    const uint32_t img_md = (mem_size + 3) / 4;
+    const uint32_t bsh = img_md <= 32 ? 0u : 32u - __builtin_clz((img_md + 31) / 32 - 1);
+    auto vdw = [&](uint32_t d) -> uint32_t {
+      if (d * 4 >= m_img) return 0u;
+      if (a.xdp) return d == 0 ? 8u : d == 1 ? len : (uint32_t)pkt_read(base, d * 4 - 8, 4, plen);
+      return (uint32_t)pkt_read(base, d * 4, 4, len);
+    };
+    auto rdw = [&](uint32_t d) -> uint32_t {
+      return (ib >> (d >> bsh)) & 1u ? img[(size_t)d * kWave] : vdw(d);
+    };
+    auto own = [&](uint32_t d) {  // (d < img_md: the access was bounds-checked)
+      const uint32_t b = d >> bsh;
+      if ((ib >> b) & 1u) return;
+      const uint32_t e1 = min((b + 1) << bsh, img_md);
+      for (uint32_t e = b << bsh; e < e1; e++) img[(size_t)e * kWave] = vdw(e);
+      ib |= 1u << b;
+    };
+    auto lazy_read = [&](uint32_t a0, uint32_t w) -> uint64_t {
+      const uint32_t d = a0 >> 2, sft = a0 & 3;
+      const uint32_t d0 = rdw(d);
+      const uint32_t d1 = (sft + w > 4) ? rdw(d + 1) : 0u;
+      uint64_t v = __builtin_amdgcn_alignbyte(d1, d0, sft);
+      if (w == 8) {
+        const uint32_t d2 = sft ? rdw(d + 2) : 0u;
+        v |= (uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sft) << 32;
+      }
+      return v & wmask(w);
+    };
+    auto lazy_write = [&](uint32_t a0, uint32_t w, uint64_t v) {
+      const uint32_t d = a0 >> 2, dl = (a0 + w - 1) >> 2;
+      own(d);
+      if (dl != d) own(dl);
+      if (dl > d + 1) own(d + 1);
+      img_write(img, a0, w, v);
+    };
     uint32_t wsteps = 0;
     // Termination guard: every iteration retires >= 1 lane-step and a lane retires at most
     // max_steps, so 64 * max_steps + 64 iterations bound a correct run; the guard only turns a
@@ -825,7 +848,7 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
           const uint32_t a0 = (uint32_t)ua;
           uint64_t v = 0;
           if (act && !fault) {
-            if (TIER == 1) v = img_read(img, a0, aux);
+            if (TIER == 1) v = lazy_read(a0, aux);
             else if (a0 >= len) v = 0;
             else if (a0 + aux <= (uint32_t)kWin) v = win_read(my_win, my_swz, a0, aux, len);
             else v = pkt_read(base, a0, aux, len);
@@ -844,7 +867,7 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
             const bool ub = !oob && ua + aux > mem_size;
             fault = oob || ub;
             fst = oob ? EBPF_ST_MEM : EBPF_ST_MEM_UB;
-            if (act && !fault) img_write(img, (uint32_t)ua, aux, op == U_ST ? k : S);
+            if (act && !fault) lazy_write((uint32_t)ua, aux, op == U_ST ? k : S);
           } else {
             fault = true;
             fst = EBPF_ST_INSN;
@@ -859,7 +882,7 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
             fault = ovf || ua >= mem_size || ua + 8 > mem_size;
             fst = EBPF_ST_MEM;
             const bool go = act && !fault;
-            uint64_t orig = go ? img_read(img, (uint32_t)ua, 8) : 0;
+            uint64_t orig = go ? lazy_read((uint32_t)ua, 8) : 0;
             const bool fetch = aux & F_FETCH;
             const bool is32 = aux & F_ATOMIC32;
             uint64_t bak = fetch ? orig : 0;
@@ -888,7 +911,7 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
             int64_t t;
             const bool f3 = __builtin_add_overflow((int64_t)orig, (int64_t)(high << 32), &t);
             if (!fault && (f2 || f3)) { fault = true; fst = f2 ? fst2 : EBPF_ST_ARITH; }
-            if (act && !fault) img_write(img, (uint32_t)ua, 8, (uint64_t)t);
+            if (act && !fault) lazy_write((uint32_t)ua, 8, (uint64_t)t);
             w_src = fetch;
             side = bak;
           } else {
@@ -936,7 +959,7 @@ __global__ __launch_bounds__(kBlock) void interp_kernel(LaunchArgs a) {
       const uint32_t m = min(len, mem_size);
       for (uint32_t d = 0; d < (mem_size + 3) / 4; d++) {
         uint32_t v;
-        if (TIER == 1) v = img[(size_t)d * kWave];
+        if (TIER == 1) v = rdw(d);
         else if (d * 4 >= m) v = 0u;
         else if (d * 4 < (uint32_t)kWin) v = (uint32_t)win_read(my_win, my_swz, d * 4, 4, len);
         else v = (uint32_t)pkt_read(base, d * 4, 4, len);
@@ -1396,10 +1419,15 @@ hipError_t launch_binning(const uint16_t* lens, uint64_t n, uint32_t* wgc, uint3
 // data_end = 8 + len} in its first 8 bytes, packet byte b at image byte 8 + b, zeros at or past
 // 8 + len. A chunk inside the packet is one 16-byte load at its (unaligned) address; the first
 // and the last: two aligned 16-byte source blocks and a funnel shift (v_alignbyte) per dword.
-typedef uint4 __attribute__((aligned(1))) uint4_any;  // (any address: tools/probe_dma_align.hip)
+// (any address: tools/probe_dma_align.hip; a clang vector, not HIP_vector_type, whose 16-byte
+// aligned copy constructor would be handed the 1-byte aligned lvalue)
+typedef uint32_t u32x4_any __attribute__((ext_vector_type(4), aligned(1)));
 __device__ __forceinline__ uint4 xdp_image_chunk(const uint8_t* src, uint32_t len, uint32_t c) {
   // a chunk wholly inside the packet (packet bytes [16c - 8, 16c + 8)): one load, as it lies
-  if (c != 0 && 16 * c + 8 <= len) return *(const uint4_any*)(src + 16 * c - 8);
+  if (c != 0 && 16 * c + 8 <= len) {
+    const u32x4_any v = *(const u32x4_any*)(src + 16 * c - 8);
+    return make_uint4(v.x, v.y, v.z, v.w);
+  }
   const uintptr_t s0 = (uintptr_t)src, end = s0 + len;
   const uintptr_t p = s0 + 16ull * c - 8;  // the source address of image byte 16c
   const uintptr_t a0 = p & ~(uintptr_t)15;
@@ -1820,7 +1848,23 @@ __global__ __launch_bounds__(kBlock, 8) void tile_kernel(LaunchArgs a) {
 // gen_tile.py jit_statement_loop), re-entered only every 511 tiles to unpack the per-lane packed
 // counter buckets. Launch conditions (jit_fixed_ok): the fixed-slot layout, n_tiles < 2^31 and
 // 64 * stride < 2^32, so tile indices and tile byte offsets are 32-bit scalars.
-extern "C" __global__ __launch_bounds__(kDbBlock, 1) void ebpf_tile_jit_fixed(LaunchArgs a) {
+//
+// SINGLE (ebpf_tile_jit_fixed_occ, WAVES = kOccWaves): the occupancy variant for issue-bound
+// programs (a long rule chain: hundreds of steps per packet for 64 bytes of HBM) -- one window
+// buffer per wave (tile_jit_loop1.inc claims and DMAs the next tile when the current one is done),
+// and a statement that owns only v[0:21] and v[26:50] (the compiled code has no preloaded window,
+// jit.cpp Compiler::body occ), so 3 workgroups of 8 waves fit a CU: 6 waves per SIMD instead of 4
+// to hide the min-pc scheme's exec / vcc dependency chains.
+#define TILE_ASM_CLOBBER_OCC "s33", "s34", "s35", "s36", "s37", "s38", "s39", "s40", "s41", "s42", \
+    "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53", "s54", "s55", "s56", \
+    "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", \
+    "s71", "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11", "v12", "v13", \
+    "v14", "v15", "v16", "v17", "v18", "v19", "v20", "v21", "v26", "v27", "v28", "v29", "v30", "v31", \
+    "v32", "v33", "v34", "v35", "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "v44", "v45", \
+    "v46", "v47", "v48", "v49", "v50", "vcc", "scc", "memory"
+template <uint32_t WAVES, bool SINGLE>
+__device__ __forceinline__ void fixed_body(LaunchArgs& a) {
+  constexpr uint32_t kWaveLds = SINGLE ? kWinBytes : kTileWaveLdsDb;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t wv = rfl(threadIdx.x / kWave);
   // the wave's first tile's windows go out before the workgroup's start barrier (counters_init:
@@ -1832,12 +1876,12 @@ extern "C" __global__ __launch_bounds__(kDbBlock, 1) void ebpf_tile_jit_fixed(La
     if (t0 < a.n_tiles) {
       uint32_t ln;
       asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
-      dma_window_stride(a, smem + wv * kTileWaveLdsDb, t0, ln);
+      dma_window_stride(a, smem + wv * kWaveLds, t0, ln);
       first = 0;
     }
   }
   counters_init();
-  uint32_t winb = lds_addr(smem + wv * kTileWaveLdsDb), nwinb = winb + kWinBytes;
+  uint32_t winb = lds_addr(smem + wv * kWaveLds), nwinb = SINGLE ? winb : winb + kWinBytes;
   const uint32_t wx = winb ^ nwinb;
   uint32_t lane;
   asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
@@ -1864,8 +1908,8 @@ extern "C" __global__ __launch_bounds__(kDbBlock, 1) void ebpf_tile_jit_fixed(La
                               (a.regs_out ? 8u : 0u));
   const uint32_t initx = rfl(kflags & 9u), oflags = rfl(kflags & 14u);
   const uint64_t ka = (uint64_t)__builtin_amdgcn_kernarg_segment_ptr();
-  uint64_t* const trace = a.trace && (uint64_t)wg * kDbWaves + wv < kTraceWaves
-                              ? a.trace + ((uint64_t)wg * kDbWaves + wv) * kTraceSlots : nullptr;
+  uint64_t* const trace = a.trace && (uint64_t)wg * WAVES + wv < kTraceWaves
+                              ? a.trace + ((uint64_t)wg * WAVES + wv) * kTraceSlots : nullptr;
   auto stamp = [&](uint32_t slot) {
     uint64_t ts;
     asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ts)::"memory");
@@ -1879,25 +1923,35 @@ extern "C" __global__ __launch_bounds__(kDbBlock, 1) void ebpf_tile_jit_fixed(La
   while (tile < ntiles) {
     uint64_t acc = 0;
     uint32_t cdn, ntile;
-    asm volatile(
-#include "tile_jit_loop.inc"
-        : [tile] "+s"(tile), [winb] "+s"(winb), [nwinb] "+s"(nwinb), [ordv] "+v"(ordv),
-          [acc] "+v"(acc), [ret] "+v"(ret), [cdn] "=&s"(cdn), [ntile] "=&s"(ntile)
-        : [first] "s"(first), [ka] "s"(ka), [k_tprog] "s"(a.tprog), [k_frames] "s"(a.frames),
-          [fr_lo] "s"((uint32_t)(uintptr_t)a.frames), [fr_hi] "s"((uint32_t)((uintptr_t)a.frames >> 32)),
-          [k_stride] "s"(a.stride), [k_n] "s"(a.n), [k_mem] "s"(a.mem_size), [k_r10] "s"(a.r10),
-          [k_verdict] "s"(a.verdict), [vd_lo] "s"((uint32_t)(uintptr_t)a.verdict),
-          [vd_hi] "s"((uint32_t)((uintptr_t)a.verdict >> 32)), [k_flags] "s"(kflags),
-          [initx] "s"(initx), [oflags] "s"(oflags), [grid] "s"(grid), [wg] "s"(wg),
-          [wpb] "i"(kDbWaves), [ntiles] "s"(ntiles), [nfull] "s"(nfull), [nfast] "s"(nfast),
-          [tbytes] "s"(tbytes), [lenc] "s"(lenc), [wx] "s"(wx),
-          [dmaoff] "v"(dmaoff), [laneoff] "v"(laneoff), [lane64] "v"(lane64), [swz] "v"(swz),
-          [lanep] "v"(lanep), [nxa] "v"(nxa), [one] "v"(one), [aligned] "s"(one),
-          [fixed] "i"(1), [loops] "i"(0), [xdpf] "s"(xdpf),
-          [o_init] "i"(offsetof(LaunchArgs, init_regs)),
-          [o_r0] "i"(offsetof(LaunchArgs, r0)), [o_status] "i"(offsetof(LaunchArgs, status)),
+#define FIXED_OPERANDS \
+        : [tile] "+s"(tile), [winb] "+s"(winb), [nwinb] "+s"(nwinb), [ordv] "+v"(ordv), \
+          [acc] "+v"(acc), [ret] "+v"(ret), [cdn] "=&s"(cdn), [ntile] "=&s"(ntile) \
+        : [first] "s"(first), [ka] "s"(ka), [k_tprog] "s"(a.tprog), [k_frames] "s"(a.frames), \
+          [fr_lo] "s"((uint32_t)(uintptr_t)a.frames), [fr_hi] "s"((uint32_t)((uintptr_t)a.frames >> 32)), \
+          [k_stride] "s"(a.stride), [k_n] "s"(a.n), [k_mem] "s"(a.mem_size), [k_r10] "s"(a.r10), \
+          [k_verdict] "s"(a.verdict), [vd_lo] "s"((uint32_t)(uintptr_t)a.verdict), \
+          [vd_hi] "s"((uint32_t)((uintptr_t)a.verdict >> 32)), [k_flags] "s"(kflags), \
+          [initx] "s"(initx), [oflags] "s"(oflags), [grid] "s"(grid), [wg] "s"(wg), \
+          [wpb] "i"(WAVES), [ntiles] "s"(ntiles), [nfull] "s"(nfull), [nfast] "s"(nfast), \
+          [tbytes] "s"(tbytes), [lenc] "s"(lenc), [wx] "s"(wx), \
+          [dmaoff] "v"(dmaoff), [laneoff] "v"(laneoff), [lane64] "v"(lane64), [swz] "v"(swz), \
+          [lanep] "v"(lanep), [nxa] "v"(nxa), [one] "v"(one), [aligned] "s"(one), \
+          [fixed] "i"(1), [loops] "i"(0), [xdpf] "s"(xdpf), \
+          [o_init] "i"(offsetof(LaunchArgs, init_regs)), \
+          [o_r0] "i"(offsetof(LaunchArgs, r0)), [o_status] "i"(offsetof(LaunchArgs, status)), \
           [o_regs] "i"(offsetof(LaunchArgs, regs_out))
-        : TILE_ASM_CLOBBER, TILE_ASM_CLOBBER_WINDOW);
+    if constexpr (SINGLE) {
+      asm volatile(
+#include "tile_jit_loop1.inc"
+          FIXED_OPERANDS
+          : TILE_ASM_CLOBBER_OCC);
+    } else {
+      asm volatile(
+#include "tile_jit_loop.inc"
+          FIXED_OPERANDS
+          : TILE_ASM_CLOBBER, TILE_ASM_CLOBBER_WINDOW);
+    }
+#undef FIXED_OPERANDS
     // (an asm statement with VGPR outputs is divergent as a whole to the compiler: the scalar
     // loop state goes back through readfirstlane, which is free on an SGPR)
     tile = rfl(tile);
@@ -1931,8 +1985,14 @@ extern "C" __global__ __launch_bounds__(kDbBlock, 1) void ebpf_tile_jit_fixed(La
   uint64_t cnt64[7];
 #pragma unroll
   for (int b = 0; b < 7; b++) cnt64[b] = cnt[b];
-  flush_counters<kDbWaves, true>(a, cnt64, retired, smem, lane, wv);
+  flush_counters<WAVES, true>(a, cnt64, retired, smem, lane, wv);
   if (trace) stamp(13);
+}
+extern "C" __global__ __launch_bounds__(kDbBlock, 1) void ebpf_tile_jit_fixed(LaunchArgs a) {
+  fixed_body<kDbWaves, false>(a);
+}
+extern "C" __global__ __launch_bounds__(kOccBlock, 3) void ebpf_tile_jit_fixed_occ(LaunchArgs a) {
+  fixed_body<kOccWaves, true>(a);
 }
 extern "C" __global__ __launch_bounds__(kBlock, 7) void ebpf_tile_jit_var(LaunchArgs a) {
   tile_body<false, false, true>(a);
@@ -2001,7 +2061,8 @@ __device__ __forceinline__ void varl_body(LaunchArgs& a) {
   const uint32_t initx = rfl(kflags & 9u), oflags = rfl(kflags & 14u), one = 1;
   // the statement's flags (gen_tile.py jit_statement_varl)
   const uint32_t fl = kflags | (initx ? 16u : 0u) | (oflags ? 32u : 0u) | (haslen ? 64u : 0u) |
-                      (xdpf ? 128u : 0u) | (a.offsets ? 0u : 256u) | (a.verdict ? 512u : 0u);
+                      (xdpf ? 128u : 0u) | (a.offsets ? 0u : 256u) | (a.verdict ? 512u : 0u) |
+                      (a.deopt_pass == 2 ? 1024u : 0u);
   const uint64_t ka = (uint64_t)__builtin_amdgcn_kernarg_segment_ptr();
   // the wave's current window / metadata buffers as generic pointers (staging)
   auto buf = [&](uint32_t wb, uint32_t mb) {
@@ -2285,7 +2346,8 @@ static int jit_grid(hipFunction_t f, uint32_t lds, uint64_t n_tiles, int block =
   }
   const uint64_t tiles = n_tiles ? n_tiles : 1;
   const uint64_t wgs = (uint64_t)occ.first * occ.second;
-  if (wpb == (uint64_t)kDbWaves) {  // tiles handed out within the workgroup: >= 1 tile each
+  if (wpb == (uint64_t)kDbWaves || wpb == (uint64_t)kOccWaves) {  // tiles handed out within the
+                                                                   // workgroup: >= 1 tile each
     // (tests: EBPFEMU_FIXED_WGS caps the workgroups, so a moderate batch gives each wave more
     // than the 511 tiles one entry of the tile-loop statement runs)
     const char* cap = getenv("EBPFEMU_FIXED_WGS");
@@ -2321,11 +2383,20 @@ static bool varl_ok(int kind, const LaunchArgs& a, const JitFns* jit, bool stack
          (!jit->var_only || stack);
 }
 
+// The fixed-slot kernel's occupancy variant takes a compiled issue-bound program's fixed-slot
+// batches (jit_compile's *occ; not stack-window programs, not xdp_md in place: its code has no
+// preloaded window to shift the ctx into).
+static bool fixed_occ_ok(int kind, const LaunchArgs& a, const JitFns* jit, bool stack) {
+  return jit && jit->fixed_occ && !stack && !jit->var_only && !a.xdp && kind == kKindDag &&
+         jit_forward_for(kind, a.n_uops) && jit_fixed_layout(&a);
+}
+
 int launch_kernel_id(int kind, const LaunchArgs& a, const JitFns* jit, bool stack) {
   if (jit && jit->loop && kind == kKindLoop)
     return stack ? EBPF_KERNEL_JIT_LOOP_STACK : EBPF_KERNEL_JIT_LOOP;
   if (varl_ok(kind, a, jit, stack))
     return stack ? EBPF_KERNEL_JIT_VARL_STACK : EBPF_KERNEL_JIT_VARL;
+  if (fixed_occ_ok(kind, a, jit, stack)) return EBPF_KERNEL_JIT_FIXED_OCC;
   if (jit && jit->fixed && jit_forward_for(kind, a.n_uops))
     return jit_fixed_layout(&a) && !jit->var_only
                ? (stack ? EBPF_KERNEL_JIT_STACK : EBPF_KERNEL_JIT_FIXED)
@@ -2372,6 +2443,10 @@ hipError_t launch_interp(int kind, const LaunchArgs& a, int grid, hipStream_t st
   } else if (vl) {  // offsets + lens batches: the var tile loop
     e = hipModuleLaunchKernel(stack ? jit->varl_stack : jit->varl, grid, 1, 1, kBlock, 1, 1, llds,
                               stream, bargs, nullptr);
+  } else if (fixed_occ_ok(kind, a, jit, stack)) {  // one window buffer, 6 waves per SIMD
+    const uint32_t olds = kOccWaves * kWinBytes;
+    e = hipModuleLaunchKernel(jit->fixed_occ, jit_grid(jit->fixed_occ, olds, a.n_tiles, kOccBlock),
+                              1, 1, kOccBlock, 1, 1, olds, stream, bargs, nullptr);
   } else if (jit && jit->fixed && jit_forward_for(kind, a.n_uops)) {
     if (jit_fixed_layout(&a) && !jit->var_only) {  // double-buffered windows: its own LDS size and grid
       const uint32_t dlds = kDbWaves * kTileWaveLdsDb;

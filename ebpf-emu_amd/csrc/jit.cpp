@@ -46,6 +46,11 @@ constexpr uint32_t kFieldSgpr = 36;  // TUop dword d lives in s[36 + d] (gen_til
 // far mode: an island of out-of-line code at the first block start past this many lines (a line
 // is at most 12 bytes: 36 KiB and the island's own code stay well inside s_branch's reach)
 constexpr size_t kIslandLines = 3000;
+// far mode: a block entry's empty-exec skip past more micro-ops than this is a long jump
+constexpr uint32_t kFarSkipUops = 48;
+// forward programs of at least this many micro-ops get the fixed-slot kernel's occupancy variant
+// (occ_wanted)
+constexpr uint32_t kOccMinUops = 96;
 
 struct Marker {
   size_t begin = 0, end = 0;  // the marker line ";@@JIT@@" (replaced)
@@ -57,6 +62,8 @@ struct Marker {
   std::string xdp;  // the SGPR holding LaunchArgs::xdp (the xdp_md convention in place)
   bool stack = false;  // the var kernel's statement for stack-window programs
   bool deep = false;   // the deep-prefetch loop kernel's statement
+  bool occ = false;    // the fixed-slot kernel's occupancy variant (ebpf_tile_jit_fixed_occ): no
+                       // preloaded window, only v[0:21] and v[26:50] for the program's code
   bool varl = false;   // the var tile loop's statement (ebpf_tile_jit_varl): the var flavour of
                        // loads with the preloaded window, as the stack statement's
   // the var tile loop's store-mode state (gen_tile.py jit_statement_varl): the SGPR pair of
@@ -107,6 +114,7 @@ bool find_markers(const std::string& s, std::vector<Marker>& out) {
     m.stack = field("stack=") == "1";
     m.deep = field("deep=") == "1";
     m.varl = field("varl=") == "1";
+    m.occ = field("occ=") == "1";
     m.ovf = field("ovf=");
     m.tile = field("tile=");
     m.dm = field("dm=");
@@ -390,6 +398,8 @@ struct Compiler {
   // far mode (compile_into_template): the body's long branches as long jumps, and its
   // out-of-line code in islands between blocks (copy) so that every short branch stays in reach
   bool far_mode = false;
+  bool occ_ok = false;  // the occupancy variant's body compiled (compile_into_template)
+  mutable uint32_t wcache = 0;  // store mode: window chunks cached in v[64:79] here (ldxk_lds)
   mutable uint32_t far_tag = 0;
   size_t island_from = 0;  // main's length after the last island
   // A branch whose target may lie past s_branch's reach in far mode: `cond` "" for s_branch, else
@@ -1360,9 +1370,34 @@ struct Compiler {
 
   // A constant-address load inside the window (LDXK) in store mode: the window dwords from LDS
   // (no LEN mask: the bytes at or past LEN are zeros there, or stored ones), merged into dst (Q1).
+  // Store mode's constant-address loads read the window through a chunk cache in v[64:79] (the
+  // preloaded-window registers, free in store mode): a chunk's 16 bytes come from LDS with one
+  // ds_read_b128 at its first use and serve every later constant load of it. Every lane of a wave
+  // reading the same window byte with ds_read_b32 hit only 16 distinct banks (64-byte windows,
+  // chunk-swizzled: a 4-way conflict, PMC round 5: 3.4 conflict cycles per LDS instruction on
+  // NAT); a b128 read covers all 64 banks per 16 lanes. Validity (wcache, one bit per chunk) is
+  // known at compile time: cleared at every jump target (lanes parked elsewhere re-join, their
+  // registers never filled), after every register-address store (any byte may have changed; its
+  // overflow fill also uses v[64:79]); a constant-address store writes LDS and merges into the
+  // cached dwords (store_bytes).
   std::string ldxk_lds(uint32_t i) const {
     const TUop& u = t[i];
-    const uint32_t a0 = u.a0, w = u.x - u.a0, d = a0 & ~3u, sh = a0 & 3;
+    const uint32_t a0 = u.a0, w = u.x - u.a0, sh = a0 & 3;
+    const uint32_t last = w == 8 && sh ? (a0 >> 2) + 2 : (a0 + w - 1) >> 2;
+    if (last < 16) {
+      std::string s;
+      bool fill = false;
+      for (uint32_t c = a0 >> 4; c <= last >> 2; c++) {
+        if (wcache & (1u << c)) continue;
+        s += "v_xad_u32 v43, v35, " + std::to_string(16 * c) + ", v34\nds_read_b128 v[" +
+             std::to_string(64 + 4 * c) + ":" + std::to_string(67 + 4 * c) + "], v43\n";
+        wcache |= 1u << c;
+        fill = true;
+      }
+      if (fill) s += "s_waitcnt lgkmcnt(0)\n";
+      return s + ldxk_fast(i);
+    }
+    const uint32_t d = a0 & ~3u;
     const uint32_t nd = (sh + w + 3) / 4;
     std::string s;
     for (uint32_t k = 0; k < nd; k++)
@@ -2125,19 +2160,21 @@ struct Compiler {
                       "v_lshl_add_u64 v[44:45], v[32:33], 0, v[46:47]\n"
                       "s_mov_b64 s[64:65], exec\n"
                       "global_load_dword v49, v[44:45], off\n"
-                      "v_mov_b32 v50, 0\nv_mov_b32 v51, 0\n";
+                      "v_mov_b32 v50, 0\nv_mov_b32 v47, 0\n";
+    // (the packet's dwords in v49, v50, v47 -- v47 is free once the address is formed -- so the
+    // code stays inside v[0:50], the occupancy variant's registers)
     const int nd = w == 8 ? 3 : (w == 1 ? 1 : 2);
     for (int k = 1; k < nd; k++)
       far += "v_add_u32 v48, " + std::to_string(4 * k) + ", v46\nv_cmp_lt_u32 vcc, v48, v31\n"
              "s_and_b64 exec, s[64:65], vcc\n"
-             "global_load_dword v" + std::to_string(49 + k) + ", v[44:45], off offset:" +
+             "global_load_dword v" + std::string(k == 1 ? "50" : "47") + ", v[44:45], off offset:" +
              std::to_string(4 * k) + "\ns_mov_b64 exec, s[64:65]\n";
     far += "s_waitcnt vmcnt(0)\n";
     if (w == 1)
       far += "v_and_b32 v48, 3, v36\nv_lshlrev_b32 v48, 3, v48\nv_bfe_u32 v26, v49, v48, 8\n";
     else
       far += "v_alignbyte_b32 v26, v50, v49, v36\n" +
-             std::string(w == 8 ? "v_alignbyte_b32 v27, v51, v50, v36\n" : "");
+             std::string(w == 8 ? "v_alignbyte_b32 v27, v47, v50, v36\n" : "");
     if (smode) far += lenmask;  // (exec: the far lanes inside the image and before LEN)
     far += ".Lfd" + U + ":\ns_mov_b64 exec, s[66:67]\ns_branch .Lmrg" + U + "\n";
     ool += far;
@@ -2147,7 +2184,9 @@ struct Compiler {
   // One copy of the program. fast: window loads from preloaded registers (ldxk_fast).
   bool copy(const Marker& m, const std::string& P, bool fast, std::string& main,
             std::string& ool) {
+    wcache = 0;
     for (uint32_t i = 0; i < n; i++) {
+      if (start[i] && target[i]) wcache = 0;  // (store mode's chunk cache, ldxk_lds)
       if (start[i] && far_mode && !ool.empty() &&
           (size_t)std::count(main.begin() + std::min(island_from, main.size()), main.end(), '\n') >
               kIslandLines) {
@@ -2163,7 +2202,12 @@ struct Compiler {
         else if (target[i])
           main += "s_or_saveexec_b64 s[64:65], -1\nv_cmp_eq_u32 vcc, " + std::to_string(i) +
                   ", v28\ns_or_b64 exec, s[64:65], vcc\n";
-        main += "s_cbranch_execz .L" + P + "b" + std::to_string(next_target(i)) + "\n";
+        // (far mode: a skip past many micro-ops -- a long straight-line run with no target, e.g.
+        // the exact copy's one-micro-op blocks -- may pass s_cbranch's reach: a long jump)
+        const uint32_t nt = next_target(i);
+        const std::string skip = ".L" + P + "b" + std::to_string(nt);
+        main += far_mode && nt - i > kFarSkipUops ? jmp("execz", skip)
+                                                  : "s_cbranch_execz " + skip + "\n";
         if (loops && hoist[i] != -2) main += "v_mov_b32 v28, " + std::to_string(hoist[i]) + "\n";
         if (loops && proven && !counted_entry(m, i, P, main, ool)) return false;
         if (loops) main += ".L" + P + "body" + std::to_string(i) + ":\n";
@@ -2776,9 +2820,18 @@ struct Compiler {
     if (stk && stk->any_dyn) {  // store mode: the header window lives in LDS
       const Uop& o = uops[i];
       if ((o.op == U_ST || o.op == U_STX) && stk->off[i] == kNoStack) {
-        main += stk->pw[i] != kNoStack ? lds_store_const(i)
-                : stk->dyn[i]          ? lds_store_dyn(i, P, ool)
-                                       : std::string("; unreachable store\n");
+        if (stk->pw[i] != kNoStack) {
+          main += lds_store_const(i);
+          const uint32_t p = (uint32_t)stk->pw[i];  // (the cached chunks see the store too)
+          uint32_t ch = 0;
+          for (uint32_t b = p; b < p + o.aux; b++) ch |= 1u << (b >> 4);
+          if (wcache & ch) main += store_bytes(i, p, 64);
+        } else if (stk->dyn[i]) {
+          main += lds_store_dyn(i, P, ool);
+          wcache = 0;
+        } else {
+          main += "; unreachable store\n";
+        }
         return true;
       }
       if (is_ldxk(id)) {
@@ -2787,8 +2840,17 @@ struct Compiler {
       }
       // (a constant-address load past the window reads the packet: a lane that has stored into
       // its overflow image leaves for the general interpreter first)
-      if (!dm.empty() && (id == T_LDXK_FAR_C || id == T_LDXK_FAR_E))
+      if (!dm.empty() && (id == T_LDXK_FAR_C || id == T_LDXK_FAR_E)) {
+        // (the deopt-free proof judged constant-address loads by the range analysis: a load the
+        // folder made constant where the ranges saw several values would deoptimize dirty lanes
+        // the proof let through -- refuse to compile rather than run without the pass)
+        if (stk->no_deopt && (i >= stk->kld.size() || !stk->kld[i])) {
+          err = "store_mode_no_deopt: micro-op " + std::to_string(i) +
+                " compiled as a constant-address load the proof did not classify as one";
+          return false;
+        }
         main += ovf_dirty_deopt(P + "u" + std::to_string(i), entry_label(P, next_start(i)));
+      }
     }
     if (stk && (uops[i].op == U_ST || uops[i].op == U_STX)) {
       // (a store the load-time dataflow never reached has no offset: no lane executes it)
@@ -2941,13 +3003,13 @@ struct Compiler {
     // LDS, before any window read (LDS operations of a wave complete in order)
     bool reads_window = false;
     for (const Uop& o : uops) reads_window = reads_window || o.op == U_LDX;
-    if ((m.fixed == "1" || m.varl) && reads_window && !m.xdp.empty())
+    if ((m.fixed == "1" || m.varl) && reads_window && !m.xdp.empty() && !m.occ)
       main += "s_cmp_lg_u32 " + m.xdp + ", 0\ns_cbranch_scc0 .L" + P + "noxdp\n" + xdp_shift() +
               ".L" + P + "noxdp:\n";
     std::string ool;
     if (stk && m.stack) main += stack_init(P, ool);
     uint32_t chunks = 0, maxend = 0;
-    if (m.fixed == "1" || m.stack || m.varl)
+    if ((m.fixed == "1" && !m.occ) || m.stack || m.varl)
       for (uint32_t i = 0; i < n; i++) {
         const TUop& u = t[i];
         if (!is_ldxk(u.hoff / TILE_SLOT)) continue;
@@ -3308,6 +3370,38 @@ std::string relocated_body(const std::string& b, const std::string& n, uint32_t&
 // assemble. Far mode, when a body passes kFarLines: every body out of line, behind its kernel's
 // code (entered by a long jump), so that no branch of the template or of the statement around it
 // spans the program.
+// ebpf_tile_jit_fixed_occ: whether a compiled body names only the VGPRs its statement owns
+// (v[0:21], v[26:50]: TILE_ASM_CLOBBER_OCC in interp.hip); the others hold the kernel's own values.
+bool occ_regs_ok(const std::string& b) {
+  for (size_t q = 0; (q = b.find('v', q)) != std::string::npos; q++) {
+    if (q > 0 && (isalnum((unsigned char)b[q - 1]) || b[q - 1] == '_' || b[q - 1] == '.')) continue;
+    uint32_t lo = 0, hi = 0;
+    if (b[q + 1] == '[') {
+      if (sscanf(b.c_str() + q, "v[%u:%u]", &lo, &hi) != 2) continue;
+    } else if (isdigit((unsigned char)b[q + 1])) {
+      if (sscanf(b.c_str() + q, "v%u", &lo) != 1) continue;
+      hi = lo;
+    } else {
+      continue;
+    }
+    for (uint32_t r = lo; r <= hi; r++)
+      if (r > 50 || (r >= 22 && r <= 25)) return false;
+  }
+  return true;
+}
+
+// Programs the occupancy variant of the fixed-slot kernel takes (host.cpp routes their
+// fixed-slot batches there): issue-bound ones, judged by length -- a long program's rule chain
+// retires hundreds of steps per packet for the same 64 bytes of HBM. EBPFEMU_FIXED_OCC=0|1 (A/B)
+// turns it off / on for every program it can take.
+bool occ_wanted(uint32_t n_uops) {
+  static const int force = [] {
+    const char* e = getenv("EBPFEMU_FIXED_OCC");
+    return e ? (e[0] == '1' ? 1 : 0) : -1;
+  }();
+  return force >= 0 ? force == 1 : n_uops >= kOccMinUops;
+}
+
 bool compile_into_template(Compiler& c, Compiler* xc, std::vector<char>& code_object,
                            std::string* err, std::string* asm_out, bool* deep_out = nullptr) {
   std::string tmpl(kJitTemplateAsm);
@@ -3390,13 +3484,21 @@ bool compile_into_template(Compiler& c, Compiler* xc, std::vector<char>& code_ob
     // (stack-window programs: the fixed-slot kernel and the var kernel's stack statement; other
     // programs: every statement but that one)
     if (loop_marker != (xc != nullptr) || (loop_marker && m.deep != deep) ||
-        (c.stk ? !(m.stack || (!loop_marker && m.fixed == "1" && !c.stk->any_dyn)) : m.stack)) {
+        (c.stk ? !(m.stack || (!loop_marker && m.fixed == "1" && !c.stk->any_dyn)) : m.stack) ||
+        (m.occ && (c.stk || !occ_wanted(c.n)))) {
       b = "s_mov_b64 exec, 0  ; (not this program's kernel)\n";
       continue;
     }
     if (!(xc ? c.body_loop(m, *xc, b) : c.body(m, b))) {
       if (err) *err = c.err;
       return false;
+    }
+    if (m.occ) {
+      c.occ_ok = occ_regs_ok(b);
+      if (!c.occ_ok) {  // (code naming the kernel's own registers: never launched)
+        b = "s_mov_b64 exec, 0  ; (occupancy variant: the code needs more registers)\n";
+        continue;
+      }
     }
     live[k] = 1;
     far = far || (size_t)std::count(b.begin(), b.end(), '\n') > kFarLines;
@@ -3440,7 +3542,8 @@ bool compile_into_template(Compiler& c, Compiler* xc, std::vector<char>& code_ob
 //     dirty lane would leave at either).
 // Loads straddling byte 64 are served (ldx_fixed); addresses below 0 or past mem_size fault,
 // which is not a deoptimization. Calls: no proof. (`why`: the first micro-op that failed.)
-bool store_mode_no_deopt(const std::vector<Uop>& uops, const StackPlan& stk, uint32_t* why) {
+bool store_mode_no_deopt(const std::vector<Uop>& uops, const StackPlan& stk, uint32_t* why,
+                         std::vector<char>* kld) {
   using AbsVal = Compiler::AbsVal;
   using AbsRegs = Compiler::AbsRegs;
   const uint32_t n = (uint32_t)uops.size();
@@ -3498,8 +3601,12 @@ bool store_mode_no_deopt(const std::vector<Uop>& uops, const StackPlan& stk, uin
   // the largest end of a register-address store / load, of a constant-address load
   uint64_t st_end = 0, ld_end = 0, kld_end = 0;
   uint32_t st_at = UINT32_MAX, ld_at = UINT32_MAX, kld_at = UINT32_MAX;
+  if (kld) kld->assign(n, 0);
   for (uint32_t i = 0; i < n; i++) {
-    if (!seen[i]) continue;
+    if (!seen[i]) {  // (no lane reaches it: whatever its code, it never deoptimizes)
+      if (kld && uops[i].op == U_LDX) (*kld)[i] = 1;
+      continue;
+    }
     const Uop& u = uops[i];
     const int64_t off = (int64_t)(int32_t)u.x;
     auto end_of = [&](const AbsVal& b) -> uint64_t {  // (unbounded: UINT64_MAX)
@@ -3516,6 +3623,7 @@ bool store_mode_no_deopt(const std::vector<Uop>& uops, const StackPlan& stk, uin
       const AbsVal& b = in[i][u.src];
       const uint64_t e = end_of(b);
       if (b.lo == b.hi) {
+        if (kld) (*kld)[i] = 1;
         if (e > kld_end) kld_end = e, kld_at = i;
       } else if (e > ld_end) {
         ld_end = e, ld_at = i;
@@ -3538,7 +3646,7 @@ bool store_mode_no_deopt(const std::vector<Uop>& uops, const StackPlan& stk, uin
 
 bool jit_compile(const std::vector<Uop>& uops, const std::vector<TUop>& t,
                  std::vector<char>& code_object, std::string* err, std::string* asm_out,
-                 const StackPlan* stk) {
+                 const StackPlan* stk, bool* occ) {
   if (uops.empty() || uops.size() > kJitMaxUops || t.size() < uops.size() ||
       (stk && (stk->k == 0 || stk->k > kStackMax || stk->k % 4 || stk->off.size() != uops.size() ||
                stk->pw.size() != uops.size() ||
@@ -3547,7 +3655,9 @@ bool jit_compile(const std::vector<Uop>& uops, const std::vector<TUop>& t,
     return false;
   }
   Compiler c(uops, t, false, false, stk);
-  return compile_into_template(c, nullptr, code_object, err, asm_out);
+  const bool ok = compile_into_template(c, nullptr, code_object, err, asm_out);
+  if (occ) *occ = ok && c.occ_ok;
+  return ok;
 }
 
 bool jit_compile_loop(const std::vector<Uop>& uops, const std::vector<TUop>& t,
@@ -3598,7 +3708,8 @@ bool jit_load(const std::vector<char>& co, hipModule_t* mod, JitFns* fns) {
       hipModuleGetFunction(&f.loop_stack, m, "ebpf_tile_jit_loop_stack") != hipSuccess ||
       hipModuleGetFunction(&f.loop_deep, m, "ebpf_tile_jit_loop_deep") != hipSuccess ||
       hipModuleGetFunction(&f.varl, m, "ebpf_tile_jit_varl") != hipSuccess ||
-      hipModuleGetFunction(&f.varl_stack, m, "ebpf_tile_jit_varl_stack") != hipSuccess) {
+      hipModuleGetFunction(&f.varl_stack, m, "ebpf_tile_jit_varl_stack") != hipSuccess ||
+      hipModuleGetFunction(&f.fixed_occ, m, "ebpf_tile_jit_fixed_occ") != hipSuccess) {
     (void)hipModuleUnload(m);
     return false;
   }

@@ -22,6 +22,9 @@ struct JitFns {
   hipFunction_t loop_deep = nullptr;  // loop programs with the deep refill prefetch
   hipFunction_t varl = nullptr;  // offsets + lens batches: the var tile loop (ebpf_tile_jit_varl)
   hipFunction_t varl_stack = nullptr;  // ... for stack-window programs (ebpf_tile_jit_varl_stack)
+  // the fixed-slot layout's occupancy variant (ebpf_tile_jit_fixed_occ: issue-bound programs, one
+  // window buffer per wave); null unless this program's code went there (jit_compile *occ)
+  hipFunction_t fixed_occ = nullptr;
   // the program's code exists for the var kernels only (store mode: register-address stores into
   // the packet, StackPlan::any_dyn), whatever the batch layout
   bool var_only = false;
@@ -59,12 +62,17 @@ struct StackPlan {
   std::vector<char> dyn;     // per micro-op: a register-address ST/STX
   bool any_dyn = false;
   bool no_deopt = false;     // store_mode_no_deopt: no lane of a main.rs-layout batch can leave
+  // per micro-op: an LDX the proof took as constant-address (its range analysis found one value).
+  // Codegen checks that every load it compiles as a constant-address far load (whose dirty lanes
+  // deoptimize) is one of these, so the proof and the code cannot disagree silently.
+  std::vector<char> kld;
 };
 
 // Store mode on the var tile loop: whether no lane of a main.rs-layout batch can deoptimize
 // (jit.cpp, a range analysis of every access; the host also needs the stack window at or past
 // byte 128). Then the deopt pass after the launch is not needed.
-bool store_mode_no_deopt(const std::vector<Uop>& uops, const StackPlan& stk, uint32_t* why = nullptr);
+bool store_mode_no_deopt(const std::vector<Uop>& uops, const StackPlan& stk, uint32_t* why = nullptr,
+                         std::vector<char>* kld = nullptr);
 
 // Status of a lane that leaves the compiled kernel for the general interpreter (never reported:
 // the tile epilogue lists the packet instead of writing its outputs, tile bucket 8).
@@ -75,9 +83,11 @@ constexpr uint32_t kStDeopt = 0x80;
 // (amd_comgr) into a gfx950 code object. Returns false with a reason in *err on failure.
 // stk: a stack-window program (only the fixed-slot kernel and the var kernel's stack variant
 // get its code).
+// *occ (if given): the code also went into ebpf_tile_jit_fixed_occ (an issue-bound program whose
+// code fits that statement's registers).
 bool jit_compile(const std::vector<Uop>& uops, const std::vector<TUop>& t,
                  std::vector<char>& code_object, std::string* err, std::string* asm_out = nullptr,
-                 const StackPlan* stk = nullptr);
+                 const StackPlan* stk = nullptr, bool* occ = nullptr);
 
 // Loop programs (back edges, or budgets that can bind; tile tables of build_tile: `t` the block
 // table, `tx` the exact one-micro-op-per-block table) for ebpf_tile_jit_loop. *deep (if given):

@@ -15,6 +15,10 @@ constexpr int kWavesPerBlock = kBlock / kWave;
 // the waves by an LDS counter (interp.hip tile_body)
 constexpr int kDbWaves = 16;
 constexpr int kDbBlock = kDbWaves * kWave;
+// ebpf_tile_jit_fixed_occ (issue-bound programs): one window buffer per wave, 3 workgroups of 8
+// waves per CU (6 waves per SIMD, the limit of its ~103 SGPRs)
+constexpr int kOccWaves = 8;
+constexpr int kOccBlock = kOccWaves * kWave;
 constexpr int kWin = 64;              // packet bytes staged in LDS per lane (header window)
 constexpr int kWinStride = kWin + 4;  // padded per-lane LDS stride: 17 dwords, conflict-free b32
 constexpr int kMaxLdsUops = 4096;     // programs up to this many micro-ops are staged in LDS
@@ -83,6 +87,8 @@ struct LaunchArgs {
   // compiled kernel appends the packet index of every lane that deoptimized (status kStDeopt: no
   // outputs, not counted); then the general interpreter runs with deopt_pass = 1 over
   // idx[0 .. count) (outputs at those indices), and its last workgroup zeroes count and done.
+  // deopt_pass = 2 on a compiled store-mode launch that no pass follows (StackPlan::no_deopt): a
+  // lane that still leaves is not listed but gets status EBPF_ST_JIT (the proof failed).
   uint32_t* deopt;
   uint32_t* deopt_idx;
   uint32_t deopt_pass;

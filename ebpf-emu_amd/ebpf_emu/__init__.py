@@ -6,7 +6,7 @@ execution. Batched use: `Program(image).run(frames, ...)`.
 """
 from . import asm, ins, mmu, xdp  # noqa: F401
 from ._lib import (DEFAULT_MEM, DEFAULT_R10, DEFAULT_STEPS, STATUS_NAMES, ST_ARITH,  # noqa: F401
-                   ST_BADPKT, ST_CALLDEPTH, ST_INSN, ST_MEM, ST_MEM_UB, ST_OK, ST_STEPS,
+                   ST_BADPKT, ST_CALLDEPTH, ST_INSN, ST_JIT, ST_MEM, ST_MEM_UB, ST_OK, ST_STEPS,
                    EbpfError, lib)
 from .ins import DecodeError, HexError, hexs_to_instructions, hexs_to_u8s  # noqa: F401
 

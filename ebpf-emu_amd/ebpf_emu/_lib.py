@@ -19,8 +19,8 @@ EBPF_EINVAL, EBPF_ELEN, EBPF_EREG, EBPF_EOP, EBPF_EMODE = -1, -2, -3, -4, -5
 EBPF_ELDDW, EBPF_ELDDW_OVF, EBPF_EHEX, EBPF_ENOMEM, EBPF_EHIP = -6, -7, -8, -9, -10
 EBPF_ETOOBIG, EBPF_ERCCL, EBPF_EPCAP, EBPF_EJIT = -11, -12, -13, -14
 
-ST_OK, ST_MEM, ST_MEM_UB, ST_INSN, ST_ARITH, ST_STEPS, ST_CALLDEPTH, ST_BADPKT = range(8)
-STATUS_NAMES = ["OK", "MEM", "MEM_UB", "INSN", "ARITH", "STEPS", "CALLDEPTH", "BADPKT"]
+ST_OK, ST_MEM, ST_MEM_UB, ST_INSN, ST_ARITH, ST_STEPS, ST_CALLDEPTH, ST_BADPKT, ST_JIT = range(9)
+STATUS_NAMES = ["OK", "MEM", "MEM_UB", "INSN", "ARITH", "STEPS", "CALLDEPTH", "BADPKT", "JIT"]
 VERDICT_OTHER, VERDICT_FAULT = 0xFE, 0xFF
 NCOUNTERS = 8
 DEFAULT_MEM, DEFAULT_R10, DEFAULT_STEPS = 1024, 512, 1 << 22
@@ -41,11 +41,12 @@ KERNEL_NAMES = ["ebpfemu::interp_kernel<0>", "ebpfemu::interp_kernel<1>", "ebpfe
                 "ebpf_tile_jit_var_stack (compiled stack-window program)",
                 "ebpf_tile_jit_loop_stack (compiled stack-window loop program)",
                 "ebpf_tile_jit_varl (compiled program, var tile loop)",
-                "ebpf_tile_jit_varl_stack (compiled stack-window program, var tile loop)"]
+                "ebpf_tile_jit_varl_stack (compiled stack-window program, var tile loop)",
+                "ebpf_tile_jit_fixed_occ (compiled issue-bound program, fixed slots)"]
 
 EXPORTS = ["ebpf_batch_init", "ebpf_prog_load", "ebpf_prog_load_hex", "ebpf_prog_free",
            "ebpf_prog_len", "ebpf_prog_insn", "ebpf_prog_tier", "ebpf_prog_forward_only",
-           "ebpf_prog_stack_window",
+           "ebpf_prog_stack_window", "ebpf_prog_store_mode",
            "ebpf_workspace_bytes", "ebpf_prog_compile", "ebpf_prog_jit_asm", "ebpf_prog_jit_error", "ebpf_debug_trace",
            "ebpf_prog_upload", "ebpf_run_batch", "ebpf_run_batch_multi", "ebpf_batch_kernel", "ebpf_batch_staged",
            "ebpf_pcap_index",
@@ -113,6 +114,7 @@ def lib():
     L.ebpf_prog_tier.argtypes = [vp]
     L.ebpf_prog_forward_only.argtypes = [vp]
     L.ebpf_prog_stack_window.argtypes = [vp]
+    L.ebpf_prog_store_mode.argtypes = [vp]
     L.ebpf_prog_compile.argtypes = [vp]
     L.ebpf_debug_trace.argtypes = [ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(sz)]
     L.ebpf_prog_jit_asm.argtypes = [vp, ctypes.c_int, ctypes.c_char_p, sz, ctypes.POINTER(sz)]

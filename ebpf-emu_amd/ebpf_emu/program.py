@@ -124,19 +124,13 @@ class Program:
     def store_mode(self) -> bool:
         """Register-address stores into the packet (host.cpp analyze_stack, StackPlan::any_dyn):
         the compiled var kernel with its header window in LDS and the deopt pass."""
-        try:
-            return "(store mode)" in self.jit_asm(1)
-        except _lib.EbpfError:
-            return False
+        return _lib.lib().ebpf_prog_store_mode(self._h) > 0
 
     @property
     def store_mode_no_deopt(self) -> bool:
         """Store mode with no lane able to deoptimize on the var tile loop (jit.cpp
         store_mode_no_deopt): main.rs-layout batches run without the deopt pass."""
-        try:
-            return "no lane can deoptimize" in self.jit_asm(1)
-        except _lib.EbpfError:
-            return False
+        return _lib.lib().ebpf_prog_store_mode(self._h) == 2
 
     @property
     def promoted(self) -> bool:

@@ -49,6 +49,8 @@ typedef struct ihipStream_t* ebpf_stream_t; /* == hipStream_t */
 #define EBPF_ST_STEPS       5  /* step budget exhausted (reference: no limit, hangs; emu.rs:452) */
 #define EBPF_ST_CALLDEPTH   6  /* frame stack deeper than EBPF_MAX_CALL_DEPTH */
 #define EBPF_ST_BADPKT      7  /* packet longer than the memory image (main.rs:20-21) */
+#define EBPF_ST_JIT         8  /* a compiled kernel's load-time proof did not hold for this packet
+                                 (a library bug, never expected: the packet was not run) */
 
 /* ---- verdict byte (xdp_action, xdp.rs:3-9) ---- */
 #define EBPF_XDP_ABORTED    0
@@ -176,6 +178,15 @@ int ebpf_prog_forward_only(const ebpf_prog* prog);
  * 0 = not such a program; -1 for NULL. */
 int ebpf_prog_stack_window(const ebpf_prog* prog);
 
+/* Store mode: ST/STX through a register whose value is not known at load time (a packet pointer
+ * behind a variable-length header; reference emu.rs:354-372). Such a program runs on the compiled
+ * var kernels with its header window in LDS; a lane whose access leaves the image bytes the kernel
+ * holds is re-run by the general interpreter after the launch (the deopt pass). 0 = not store
+ * mode, 1 = store mode with the deopt pass, 2 = store mode proven at load time to need no pass
+ * for main.rs-layout batches (no lane can leave; a lane that did would fault EBPF_ST_JIT); -1 for
+ * NULL. */
+int ebpf_prog_store_mode(const ebpf_prog* prog);
+
 /* Micro-ops (after local calls are flattened into one copy per frame stack) of the longest
  * program the compiler takes; longer programs run on the general interpreter. */
 #define EBPF_MAX_COMPILED_UOPS 4096
@@ -236,6 +247,8 @@ int ebpf_run_batch(ebpf_prog* prog, const ebpf_batch* batch, const ebpf_batch_ou
                                     final images) */
 #define EBPF_KERNEL_JIT_VARL_STACK 12 /* the var tile loop for stack-window programs
                                          (ebpf_tile_jit_varl_stack; not store mode) */
+#define EBPF_KERNEL_JIT_FIXED_OCC 13 /* compiled program, fixed-slot layout, occupancy variant for
+                                        issue-bound programs (ebpf_tile_jit_fixed_occ) */
 int ebpf_batch_kernel(ebpf_prog* prog, const ebpf_batch* batch, const ebpf_batch_out* out,
                       int device);
 

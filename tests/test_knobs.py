@@ -11,6 +11,8 @@ were measured slower, and the overrides of defaults, are gone with their code pa
                                 per-shard sums could pass 2^48)
   EBPFEMU_FIXED_WGS=n           caps ebpf_tile_jit_fixed's grid (test_gpu_jit.py tile loop re-entry)
   EBPFEMU_VARL_WGS=n            caps ebpf_tile_jit_varl's grid (test_varl.py statement re-entry)
+  EBPFEMU_FIXED_OCC=0|1         the fixed-slot kernel's occupancy variant off / for every program
+                                (A/B; default: programs of >= 96 micro-ops, test_occ.py)
 The first five are read once when the library loads, so their tests run a child process
 (tests/knob_child.py); the last two are read per launch.
 """
@@ -27,7 +29,7 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(ROOT, "ebpf-emu_amd", "csrc")
 
 KNOBS = {"EBPFEMU_TRACE", "EBPFEMU_TEST_FAIL_STACK_JIT", "EBPFEMU_BIN", "EBPFEMU_XDP_STAGE",
-         "EBPFEMU_FOLD", "EBPFEMU_FIXED_WGS", "EBPFEMU_VARL_WGS"}
+         "EBPFEMU_FOLD", "EBPFEMU_FIXED_WGS", "EBPFEMU_VARL_WGS", "EBPFEMU_FIXED_OCC"}
 
 
 def test_knob_inventory():
@@ -91,3 +93,22 @@ def test_binned_deopt_default():
     a promoted program binned and deoptimizing at once; == the oracle."""
     d = _child("bin_default", {})
     assert d["deopt_lanes"] > 1000
+
+
+@pytest.mark.parametrize("val,want", [("0", [False, False]), ("1", [True, True])])
+def test_knob_fixed_occ(val, want):
+    """EBPFEMU_FIXED_OCC=0|1 (read once, at the first compile): acl_rules and the 5-tuple without /
+    with code in ebpf_tile_jit_fixed_occ (by default only acl_rules, test_occ.py)."""
+    code = ("import sys; sys.path[:0] = [sys.argv[1], sys.argv[2]]\n"
+            "from test_occ import _occ_body\n"
+            "from ebpf_emu import Program, workloads as W\n"
+            "out = []\n"
+            "for name in ('acl_rules', '5tuple'):\n"
+            "    p = Program(W.program(name)); p.compile()\n"
+            "    out.append(_occ_body(p.jit_asm(1)) is not None)\n"
+            "print(out)\n")
+    r = subprocess.run([sys.executable, "-c", code, os.path.join(ROOT, "ebpf-emu_amd"), HERE],
+                       capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, EBPFEMU_FIXED_OCC=val))
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.stdout.strip().splitlines()[-1] == str(want)
