@@ -71,6 +71,12 @@ CONFIGS = {
     # per packet) -- compiled past the near-branch reach (jit.cpp far mode); issue-bound, not HBM
     "acl_rules": (2, "IPv4 rule-table firewall, 128 rules (1013 insns, ~297 executed per packet) "
                      "over 1Mi x 64B frames"),
+    # a payload writer: ICMP echo replies in place, and every other IPv4 frame's 4-byte trailer
+    # (the frame's last bytes: r1 + r2 - 4) incremented -- register-address stores; with
+    # --frame-bytes 1504 the trailer is 1500 bytes in, past the header window: store mode's
+    # overflow image (jit.cpp ovf_fill, one 64-byte block per packet)
+    "responder": (2, "XDP responder: ICMP echo reply in place + a 4-byte telemetry trailer "
+                     "incremented at the frame's end (49 insns) over 1Mi x 64B frames"),
 }
 PROGRAM_OF = {"stack": "5tuple_stack", "tier1": "mac_swap_tx", "xdp": "5tuple_xdp",
               "call": "5tuple_call"}
@@ -177,13 +183,25 @@ def pin_weak(prog_name: str, mixed: bool, frame_bytes: int, n: int, world: int, 
              steps: int, cnt):
     """Expected global counters of a weak-scaling run (K steps; step i runs pool batch i mod B on
     every rank), from the committed oracle fixture -> (want u64[8], source) or (None, reason)."""
-    if n != 1 << 20 or (not mixed and frame_bytes != 64):
-        return None, "no fixture for this batch shape (pinned: 1 Mi packets of 64 B or mixed)"
     if not os.path.exists(PIN_FIXTURE):
         return None, f"{os.path.relpath(PIN_FIXTURE, ROOT)} missing"
     with open(PIN_FIXTURE) as f:
         fx = json.load(f)
     p = fx["programs"].get(prog_name)
+    if n == 1 << 20 and not mixed and frame_bytes == 1504 and p and "chunk_counters_1504" in p:
+        # (1504-byte slots: every pool batch of rank r is a copy of chunk r)
+        cc = p["chunk_counters_1504"]
+        if world > len(cc):
+            return None, f"{world} ranks exceed the fixture's {len(cc)} 1504-byte chunks"
+        want = [0] * 8
+        for r in range(world):
+            for j in range(8):
+                want[j] += steps * cc[r][j]
+        want = [w & ((1 << 64) - 1) for w in want]
+        return want, (f"{os.path.relpath(PIN_FIXTURE, ROOT)}: counters == the oracle's counters of "
+                      f"the 1504-byte chunks r over {steps} steps x {world} ranks")
+    if n != 1 << 20 or (not mixed and frame_bytes != 64):
+        return None, "no fixture for this batch shape (pinned: 1 Mi packets of 64 B or mixed)"
     if p is None or p["frames"] != ("mixed" if mixed else "fixed64"):
         return None, f"no fixture for program {prog_name}"
     cc = p["chunk_counters"]
@@ -410,6 +428,9 @@ def main():
             st = np.arange(n, dtype=np.int64) * ((fb + 16) if args.layout == "pcap" else fb) + \
                 (40 if args.layout == "pcap" else 0)
             floor_bytes = line_floor_bytes(st, np.full(n, wb, dtype=np.int64)) + n * (1 + meta)
+            if args.config == "responder" and fb > 64:  # (+ the 4-byte trailer at the frame's end:
+                algo_bytes += n * 4                      #  its 128-byte line, past the window)
+                floor_bytes += n * 128
         else:  # large slots: copies of the first batch at other addresses (host RNG is slow)
             batches.append(dict(frames=batches[0]["frames"].clone()))
         # (the bytes a launch touches decide whether the pool outgrows the Infinity Cache)
@@ -594,10 +615,11 @@ def main():
     # SQ_INSTS_VALU), collected by tools/pmc.sh into the committed summary
     traffic = None
     issue = None
-    suffix = ("" if mixed or fb == 64 else f"_{fb}B") + ("" if args.layout == "fixed" else f"_{args.layout}")
+    suffix = (("" if mixed or fb == 64 else f"_{fb}B") + ("" if args.layout == "fixed" else f"_{args.layout}")
+              + ("_generic" if args.generic else ""))
     pj = args.pmc_json or os.path.join(ROOT, "profiles", f"pmc_{args.config}{suffix}.json")
     pmc_note = None
-    if os.path.exists(pj) and not args.total_packets and n == 1 << 20 and not args.generic:
+    if os.path.exists(pj) and not args.total_packets and n == 1 << 20:
         with open(pj) as f:
             pmc = json.load(f)
         # a summary profiled on another build of the kernel does not describe this run: refuse

@@ -303,12 +303,13 @@ static int jit_compile_locked(ebpf_prog* p) {
     p->jit_has[2] = !p->ltuops.empty() && !p->ltuopsx.empty();
     p->jit_has[3] = !p->tuopsk_xdp.empty() && !p->stack.k;
     p->jit_has[4] = !p->pltuops.empty() && !p->pltuopsx.empty();
-    // variant 5: a loop program that reads a 4-byte word through r1 (an xdp_md program's ctx
-    // loads) gets a copy for xdp_md batches, whose staged images' ctx the range analysis knows
+    // variant 5: a loop program that reads a 4-byte word at offset 0 or 4 of a register (an
+    // xdp_md program's ctx loads, through r1 or a copy of it: jit.cpp ctx_load) gets a copy for
+    // xdp_md batches, whose staged images' ctx the range analysis knows
     p->jit_has[5] = false;
     if (p->jit_has[2] && !p->stack.k)
       for (const Uop& u : p->xuops)
-        p->jit_has[5] = p->jit_has[5] || (u.op == U_LDX && u.aux == 4 && u.src == 1);
+        p->jit_has[5] = p->jit_has[5] || (u.op == U_LDX && u.aux == 4 && (u.x == 0 || u.x == 4));
     // variant 6: the same program for xdp_md batches in place (rebased, jit.cpp
     // Compiler::xdp_rebase) when every packet load is proven past the ctx
     p->jit_has[6] = p->jit_has[5];
@@ -1090,7 +1091,8 @@ static StackAnalysis analyze_stack(const std::vector<Uop>& uops) {
   res.plan.dyn = std::move(dyns);
   res.plan.any_dyn = any_dyn;
   // (store mode: whether the deopt pass can be left out for main.rs-layout batches, jit.cpp)
-  res.plan.no_deopt = any_dyn && store_mode_no_deopt(uops, res.plan, nullptr, &res.plan.kld);
+  res.plan.no_deopt = any_dyn && store_mode_no_deopt(uops, res.plan, nullptr, &res.plan.kld,
+                                                     &res.plan.st_bound, &res.plan.len_bound);
   return res;
 }
 
@@ -1728,8 +1730,8 @@ uint64_t ebpf_workspace_bytes(const ebpf_prog* p, const ebpf_batch* b, int devic
   bytes += align16(tier1_slots_bytes(p, b, device));
   if (p->stack.any_dyn || !p->puops.empty())  // the deopt list's indices (past the slots)
     bytes += align16(b->n * 4);
-  if (p->stack.any_dyn)  // store mode: the overflow images (past the indices)
-    bytes += b->n * 64 + 16;
+  if (p->stack.any_dyn)  // store mode: the overflow images (past the indices; jit.h ovf_stride)
+    bytes += b->n * ovf_stride(b->mem_size) + 16;
   return bytes;  // (the xdp_md region, when present, is the last x bytes)
 }
 
@@ -1917,8 +1919,11 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* bin, const ebpf_batch_out* ou
                      (promo && jit);
   // store mode on the var tile loop with no lane able to leave (StackPlan::no_deopt: the main.rs
   // registers, the stack window at or past the overflow image's end): no deopt pass
+  const uint64_t s0 = b->r10 >= p->stack.k ? b->r10 - p->stack.k : 0;  // the stack window's start
   const bool pass = deopt && !(kid == EBPF_KERNEL_JIT_VARL_STACK && p->stack.no_deopt &&
-                               !b->init_regs && b->r10 >= 128ull + p->stack.k);
+                               !b->init_regs && s0 >= p->stack.st_bound &&
+                               (!p->stack.len_bound ||
+                                (b->mem_size <= kOvfEnd && s0 >= b->mem_size)));
   if (deopt) {
     a.deopt = (uint32_t*)(ws + kWsDeoptOff);
     // (past the tier-1 slots, or the binned order and its class counts when the batch is binned)

@@ -1852,16 +1852,9 @@ __global__ __launch_bounds__(kBlock, 8) void tile_kernel(LaunchArgs a) {
 // SINGLE (ebpf_tile_jit_fixed_occ, WAVES = kOccWaves): the occupancy variant for issue-bound
 // programs (a long rule chain: hundreds of steps per packet for 64 bytes of HBM) -- one window
 // buffer per wave (tile_jit_loop1.inc claims and DMAs the next tile when the current one is done),
-// and a statement that owns only v[0:21] and v[26:50] (the compiled code has no preloaded window,
-// jit.cpp Compiler::body occ), so 3 workgroups of 8 waves fit a CU: 6 waves per SIMD instead of 4
-// to hide the min-pc scheme's exec / vcc dependency chains.
-#define TILE_ASM_CLOBBER_OCC "s33", "s34", "s35", "s36", "s37", "s38", "s39", "s40", "s41", "s42", \
-    "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53", "s54", "s55", "s56", \
-    "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", \
-    "s71", "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11", "v12", "v13", \
-    "v14", "v15", "v16", "v17", "v18", "v19", "v20", "v21", "v26", "v27", "v28", "v29", "v30", "v31", \
-    "v32", "v33", "v34", "v35", "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "v44", "v45", \
-    "v46", "v47", "v48", "v49", "v50", "vcc", "scc", "memory"
+// and a statement that owns only v[0:55] (the compiled code has no preloaded window, jit.cpp
+// Compiler::body occ): under 80 VGPRs, so 3 workgroups of 8 waves fit a CU -- 6 waves per SIMD
+// (its ~100 SGPRs allow no more) instead of 4, to hide the min-pc scheme's exec / vcc chains.
 template <uint32_t WAVES, bool SINGLE>
 __device__ __forceinline__ void fixed_body(LaunchArgs& a) {
   constexpr uint32_t kWaveLds = SINGLE ? kWinBytes : kTileWaveLdsDb;
@@ -1944,7 +1937,7 @@ __device__ __forceinline__ void fixed_body(LaunchArgs& a) {
       asm volatile(
 #include "tile_jit_loop1.inc"
           FIXED_OPERANDS
-          : TILE_ASM_CLOBBER_OCC);
+          : TILE_ASM_CLOBBER);
     } else {
       asm volatile(
 #include "tile_jit_loop.inc"

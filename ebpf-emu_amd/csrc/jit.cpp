@@ -51,6 +51,8 @@ constexpr uint32_t kFarSkipUops = 48;
 // forward programs of at least this many micro-ops get the fixed-slot kernel's occupancy variant
 // (occ_wanted)
 constexpr uint32_t kOccMinUops = 96;
+// store mode's overflow image covers image bytes [64, min(mem_size rounded up to 64, this))
+// (jit.h kOvfEnd)
 
 struct Marker {
   size_t begin = 0, end = 0;  // the marker line ";@@JIT@@" (replaced)
@@ -63,7 +65,7 @@ struct Marker {
   bool stack = false;  // the var kernel's statement for stack-window programs
   bool deep = false;   // the deep-prefetch loop kernel's statement
   bool occ = false;    // the fixed-slot kernel's occupancy variant (ebpf_tile_jit_fixed_occ): no
-                       // preloaded window, only v[0:21] and v[26:50] for the program's code
+                       // preloaded window, only v[0:55] for the program's code
   bool varl = false;   // the var tile loop's statement (ebpf_tile_jit_varl): the var flavour of
                        // loads with the preloaded window, as the stack statement's
   // the var tile loop's store-mode state (gen_tile.py jit_statement_varl): the SGPR pair of
@@ -281,25 +283,38 @@ struct Compiler {
   int ctx_load(uint32_t i) const {
     if (!xdp_ctx) return -1;
     if (ctx_off.empty()) {
-      std::vector<char> seen(n, 0), init(n, 0);  // init[i]: r1 unmodified on every path to i
+      // init[i]: the registers (bit r) holding the initial r1 -- the image start, the ctx -- on
+      // every path to i: r1 unmodified, or a copy of it (mov rX, r1 / mov32: the start is 0)
+      std::vector<char> seen(n, 0);
+      std::vector<uint16_t> init(n, 0);
       std::vector<uint32_t> work{0};
-      seen[0] = init[0] = 1;
-      auto flow = [&](uint32_t to, bool v) {
+      seen[0] = 1;
+      init[0] = 1u << 1;
+      auto flow = [&](uint32_t to, uint16_t v) {
         if (to >= n) return;
         if (!seen[to]) {
           seen[to] = 1, init[to] = v, work.push_back(to);
-        } else if (init[to] && !v) {
-          init[to] = 0, work.push_back(to);
+        } else if ((init[to] & v) != init[to]) {
+          init[to] &= v, work.push_back(to);
         }
       };
       while (!work.empty()) {
         const uint32_t i = work.back();
         work.pop_back();
         const Uop& u = uops[i];
-        const bool writes1 = u.dst == 1 && u.op != U_ST && u.op != U_STX && !is_jump(u) &&
-                             u.op != U_EXIT && u.op != U_FAULT;
-        const bool v = init[i] && !writes1 && u.op != U_CALL &&
-                       !(u.op == U_ATOMIC && u.src == 1);
+        const bool writes = u.op != U_ST && u.op != U_STX && !is_jump(u) && u.op != U_EXIT &&
+                            u.op != U_FAULT && u.op != U_ATOMIC && u.op != U_NOP && u.dst <= 10;
+        uint16_t v = init[i];
+        if (u.op == U_CALL) v = 0;
+        if (u.op == U_ATOMIC) {  // (fetch forms write src, CMPXCHG r0)
+          if (u.aux & F_FETCH) v &= (uint16_t)~(1u << u.src);
+          if (u.k == 0xf0) v &= (uint16_t)~1u;
+        }
+        if (writes) {
+          const bool copy = (u.op == U_MOV64 || u.op == U_MOV32) && (u.aux & F_SRC) && u.src <= 10 &&
+                            ((init[i] >> u.src) & 1);
+          v = copy ? (uint16_t)(v | (1u << u.dst)) : (uint16_t)(v & ~(1u << u.dst));
+        }
         if (u.op == U_EXIT || u.op == U_FAULT) continue;
         if (u.op == U_JA) {
           flow((uint32_t)u.x, v);
@@ -311,7 +326,8 @@ struct Compiler {
       ctx_off.assign(n, -1);
       for (uint32_t i = 0; i < n; i++) {
         const Uop& u = uops[i];
-        if (seen[i] && init[i] && u.op == U_LDX && u.aux == 4 && u.src == 1 && (u.x == 0 || u.x == 4))
+        if (seen[i] && u.op == U_LDX && u.aux == 4 && u.src <= 10 && ((init[i] >> u.src) & 1) &&
+            (u.x == 0 || u.x == 4))
           ctx_off[i] = u.x;
       }
     }
@@ -1226,44 +1242,88 @@ struct Compiler {
     return s;
   }
 
-  // ---- the overflow image (store mode on the var tile loop): image bytes [64, 128) of the
-  // lane's packet in the workspace (LaunchArgs::ovf + packet index * 64), filled from the packet
-  // (zeros at or past LEN) by the lane's first store past byte 64 (its bit in the dirty mask dm,
-  // cleared per tile); its later loads of those bytes read it (sc1: from L2, where the stores
-  // went). So a port or checksum rewrite behind long IPv4 options stays on the compiled kernel.
-  // v[44:45] = the lane's overflow image (s[48:49]: its tile's).
+  // ---- the overflow image (store mode on the var tile loop): image bytes [64, E) of the lane's
+  // packet in the workspace, E = min(mem_size rounded up to 64, kOvfEnd = 2048) (LaunchArgs::ovf
+  // + packet index * (E - 64)), kept per 64-byte block b (bytes [64 + 64b, 128 + 64b)): a block
+  // is filled from the packet (zeros at or past LEN) by the lane's first store into it -- or by
+  // a load that spans it and a filled one -- and its bit b set in v23 (the lane's filled
+  // blocks; the dirty mask dm: the lanes with any, cleared per tile). Loads of filled blocks read
+  // the image (sc1: from L2, where the stores went), of the others the packet. So a rewrite of
+  // a 1500-byte frame's payload stays on the compiled kernel, and costs the blocks it touches.
+  // s48 = E (from the mem_size in s52).
+  static std::string ovf_end() {
+    return "s_add_u32 s48, s52, 63\ns_and_b32 s48, s48, 0xffffffc0\n"
+           "s_min_u32 s48, s48, " + std::to_string(kOvfEnd) + "\ns_max_u32 s48, s48, 64\n";
+  }
+  // v[44:45] = the lane's overflow image: ovf + (tile * 64 + lane) * (E - 64). Uses v40, v41,
+  // s[48:49], vcc.
   std::string ovf_addr() const {
-    return "s_lshl_b32 s48, " + tile_s + ", 12\ns_lshr_b32 s49, " + tile_s + ", 20\n"
-           "s_add_u32 s48, s48, " + ovf_lo + "\ns_addc_u32 s49, s49, " + ovf_hi + "\n"
-           "v_mbcnt_lo_u32_b32 v44, -1, 0\nv_mbcnt_hi_u32_b32 v44, -1, v44\n"
-           "v_lshlrev_b32 v44, 6, v44\nv_mov_b32 v45, 0\n"
-           "v_lshl_add_u64 v[44:45], v[44:45], 0, s[48:49]\n";
+    return ovf_end() + "s_sub_u32 s48, s48, 64\nv_mov_b32 v41, s48\n"
+           "s_lshl_b32 s48, " + tile_s + ", 6\n"
+           "v_mbcnt_lo_u32_b32 v40, -1, 0\nv_mbcnt_hi_u32_b32 v40, -1, v40\n"
+           "v_add_u32 v40, s48, v40\n"
+           "s_mov_b32 s48, " + ovf_lo + "\ns_mov_b32 s49, " + ovf_hi + "\n"
+           "v_mad_u64_u32 v[44:45], vcc, v40, v41, s[48:49]\n";
   }
-  // The lanes of exec: their overflow images filled from the packet's dwords past byte 64 (those
-  // that hold a packet byte, as the far loads read them; bytes at or past LEN zero). Uses
-  // v[64:79] (the preloaded window registers, unused in store mode), v[40:41], v[44:45], s[62:63].
-  std::string ovf_fill() const {
-    std::string r = ovf_addr() + "s_mov_b64 s[62:63], exec\n";
-    for (uint32_t k = 0; k < 16; k++) r += "v_mov_b32 v" + std::to_string(64 + k) + ", 0\n";
-    for (uint32_t k = 0; k < 16; k++)
-      r += "v_cmp_lt_u32 vcc, " + std::to_string(64 + 4 * k) + ", v31\n"
-           "s_and_b64 exec, s[62:63], vcc\n"
-           "global_load_dword v" + std::to_string(64 + k) + ", v[32:33], off offset:" +
-           std::to_string(64 + 4 * k) + "\n";
-    r += "s_mov_b64 exec, s[62:63]\ns_waitcnt vmcnt(0)\n";
-    for (uint32_t k = 0; k < 16; k++)
-      r += "v_subrev_u32 v40, " + std::to_string(64 + 4 * k) + ", v31\n"
-           "v_med3_i32 v40, v40, 0, 4\nv_lshlrev_b32 v40, 3, v40\n"
-           "v_lshlrev_b64 v[40:41], v40, 1\nv_add_u32 v40, -1, v40\n"
-           "v_and_b32 v" + std::to_string(64 + k) + ", v40, v" + std::to_string(64 + k) + "\n";
-    for (uint32_t c = 0; c < 4; c++)
-      r += "global_store_dwordx4 v[44:45], v[" + std::to_string(64 + 4 * c) + ":" +
-           std::to_string(67 + 4 * c) + "], off offset:" + std::to_string(16 * c) + "\n";
-    return r + "s_waitcnt vmcnt(0)\n";
+  // The fill routine (one per body, behind its code: ovf_routine; called with s_swappc, return
+  // address in s[62:63]): the lanes of exec (some) get block v39 of their overflow image filled
+  // from the packet's dwords (those before LEN; the bytes at or past it zero), 16 bytes at a time
+  // through v[52:55]; bit v39 set in v23, the lanes added to dm. Keeps v36-v39, v42, v43,
+  // s[60:61], s[66:69]; uses v40, v41, v44-v48, v50-v55, s[48:49], s[64:65], vcc.
+  mutable bool ovf_used = false;
+  std::string ovf_label() const { return ".Lovf" + ovl_tag; }
+  std::string ovf_routine() const {
+    if (!ovf_used) return "";
+    std::string r = ovf_label() + ":\ns_mov_b64 s[64:65], exec\ns_or_b64 " + dm + ", " + dm + ", exec\n" +
+                    ovf_addr() +
+                    "v_lshlrev_b32 v40, 6, v39\nv_mov_b32 v41, 0\n"
+                    "v_lshl_add_u64 v[44:45], v[44:45], 0, v[40:41]\n"
+                    "v_add_u32 v40, 64, v40\n"  // the block's image offset o
+                    "v_lshl_add_u64 v[46:47], v[32:33], 0, v[40:41]\n"
+                    "v_sub_u32 v48, v31, v40\n";  // LEN - o (signed)
+    for (uint32_t q = 0; q < 4; q++) {
+      for (uint32_t k = 0; k < 4; k++) {
+        const std::string K = std::to_string(16 * q + 4 * k), V = "v" + std::to_string(52 + k);
+        r += "v_mov_b32 " + V + ", 0\n"
+             "v_cmp_lt_i32 vcc, " + K + ", v48\ns_and_b64 exec, s[64:65], vcc\n"
+             "global_load_dword " + V + ", v[46:47], off offset:" + K + "\n"
+             "s_mov_b64 exec, s[64:65]\n";
+      }
+      r += "s_waitcnt vmcnt(0)\n";
+      for (uint32_t k = 0; k < 4; k++)
+        r += "v_subrev_u32 v50, " + std::to_string(16 * q + 4 * k) + ", v48\n"
+             "v_med3_i32 v50, v50, 0, 4\nv_lshlrev_b32 v50, 3, v50\n"
+             "v_lshlrev_b64 v[50:51], v50, 1\nv_add_u32 v50, -1, v50\n"
+             "v_and_b32 v" + std::to_string(52 + k) + ", v50, v" + std::to_string(52 + k) + "\n";
+      // (s_nop 1: a store of more than 64 bits reads its data VGPRs after issue -- the next
+      // round's moves into v[52:55] must wait, cdna_asm_programming.md 4.1)
+      r += "global_store_dwordx4 v[44:45], v[52:55], off offset:" + std::to_string(16 * q) +
+           "\ns_nop 1\n";
+    }
+    return r + "s_waitcnt vmcnt(0)\nv_lshlrev_b32 v40, v39, 1\nv_or_b32 v23, v23, v40\n"
+               "s_setpc_b64 s[62:63]\n";
   }
-  // Lanes of exec in the dirty mask deoptimize (before a load the overflow would not serve).
-  std::string ovf_dirty_deopt(const std::string& U, const std::string& next) const {
+  // The lanes of `lanes` whose block v39 is not filled yet: filled by the routine (exec is
+  // `lanes` after).
+  std::string ovf_ensure(const std::string& lanes, const std::string& tag) const {
+    ovf_used = true;
+    const std::string P = ".Lfp" + tag, L = ovf_label(), d = "(" + L + "-" + P + ")";
+    return "v_lshrrev_b32 v40, v39, v23\nv_and_b32 v40, 1, v40\nv_cmp_eq_u32 vcc, 0, v40\n"
+           "s_and_b64 exec, " + lanes + ", vcc\ns_cbranch_execz .Lfe" + tag + "\n"
+           "s_getpc_b64 s[48:49]\n" + P + ":\ns_add_u32 s48, s48, " + d + "&4294967295\n"
+           "s_addc_u32 s49, s49, " + d + ">>32\ns_swappc_b64 s[62:63], s[48:49]\n"
+           ".Lfe" + tag + ":\ns_mov_b64 exec, " + lanes + "\n";
+  }
+  // A constant-address load of [a, a + w) past the window: lanes of exec that filled a block it
+  // reads deoptimize first (the load reads the packet).
+  std::string ovf_dirty_deopt(const std::string& U, const std::string& next, uint32_t a,
+                              uint32_t w) const {
+    uint32_t bm = 0;
+    for (uint32_t b = std::max(a, 64u); b < a + w && b < kOvfEnd; b++) bm |= 1u << ((b - 64) >> 6);
+    if (!bm) return "";
     return "s_and_b64 vcc, exec, " + dm + "\ns_cbranch_vccz .Ldk" + U + "\n"
+           "v_and_b32 v40, " + hex32(bm) + ", v23\nv_cmp_ne_u32 vcc, 0, v40\n"
+           "s_and_b64 vcc, vcc, exec\ns_cbranch_vccz .Ldk" + U + "\n"
            "s_mov_b64 s[66:67], exec\ns_mov_b64 exec, vcc\nv_mov_b32 v30, 0x80\nv_mov_b32 v28, -1\n"
            "s_andn2_b64 exec, s[66:67], vcc\ns_cbranch_execz " + next + "\n.Ldk" + U + ":\n";
   }
@@ -1324,11 +1384,12 @@ struct Compiler {
     }
     if (ovf_lo.empty()) return s;
     s += ".Lsdn" + U + ":\n";
-    // out of line: some lane's store ends past byte 64 (vcc). Lanes ending past min(128, S0 = the
-    // stack window's start, s57) deoptimize; the others fill their overflow image on their first
-    // such store, then write each byte to the window (< 64) or the overflow image.
-    std::string o2 = ".Lsov" + U + ":\n"
-        "v_mov_b32 v39, 0x80\nv_min_u32 v39, s57, v39\n"
+    // out of line: some lane's store ends past byte 64 (vcc). Lanes ending past min(E, S0 = the
+    // stack window's start, s57) deoptimize; the others fill the blocks of their overflow image
+    // the store reaches (its first and last byte's: w <= 8) if not yet filled, then write each
+    // byte to the window (< 64) or the overflow image.
+    std::string o2 = ".Lsov" + U + ":\n" + ovf_end() +
+        "v_mov_b32 v39, s48\nv_min_u32 v39, s57, v39\n"
         "v_cmp_lt_u32_e64 s[60:61], v39, v38\n"
         "s_and_b64 s[60:61], s[60:61], vcc\n"
         "s_cbranch_scc0 .Lsnd" + U + "\n"
@@ -1338,12 +1399,11 @@ struct Compiler {
         "s_andn2_b64 vcc, vcc, s[60:61]\n"
         "s_cbranch_execz " + next + "\n"
         ".Lsnd" + U + ":\n"
-        "s_andn2_b64 s[60:61], vcc, " + dm + "\n"
-        "s_cbranch_scc0 .Lsdi" + U + "\n"
-        "s_or_b64 " + dm + ", " + dm + ", s[60:61]\n"
-        "s_mov_b64 s[66:67], exec\ns_mov_b64 exec, s[60:61]\n" + ovf_fill() +
-        "s_mov_b64 exec, s[66:67]\n"
-        ".Lsdi" + U + ":\n" + ovf_addr() + "v_mov_b32 v41, 0\n";
+        "s_mov_b64 s[68:69], vcc\ns_mov_b64 s[66:67], exec\n"
+        "v_max_u32 v39, 64, v36\nv_subrev_u32 v39, 64, v39\nv_lshrrev_b32 v39, 6, v39\n" +
+        ovf_ensure("s[68:69]", "f" + U) +
+        "v_add_u32 v39, -65, v38\nv_lshrrev_b32 v39, 6, v39\n" + ovf_ensure("s[68:69]", "l" + U) +
+        "s_mov_b64 exec, s[66:67]\n" + ovf_addr() + "v_mov_b32 v41, 0\n";
     for (uint32_t j = 0; j < w; j++) {
       const std::string J = std::to_string(j);
       o2 += (j ? "v_add_u32 v39, " + J + ", v36\n" : std::string("v_mov_b32 v39, v36\n")) +
@@ -1446,7 +1506,9 @@ struct Compiler {
     std::string main = "; compiled eBPF program (store mode): " + std::to_string(n) + " micro-ops\n"
                        "s_mov_b32 s52, s33\ns_mov_b32 s53, 0\n";
     if (stk->no_deopt) main += "; store mode: no lane can deoptimize (store_mode_no_deopt)\n";
-    if (!dm.empty()) main += "s_mov_b64 " + dm + ", 0\n";
+    if (!dm.empty())  // (no overflow block filled yet: v23, the lanes' block bits, and dm)
+      main += "s_mov_b64 " + dm + ", 0\ns_mov_b64 s[64:65], exec\ns_mov_b64 exec, -1\n"
+              "v_mov_b32 v23, 0\ns_mov_b64 exec, s[64:65]\n";
     // (the var tile loop's windows hold packet bytes [0, 64): the xdp_md ctx shifted in first, as
     // body does; the var kernel's C++ shifts them itself)
     if (m.varl && !m.xdp.empty())
@@ -1470,9 +1532,10 @@ struct Compiler {
       main += "ds_write_b128 v" + std::to_string(36 + c) + ", v[" + std::to_string(64 + 4 * c) + ":" +
               std::to_string(67 + 4 * c) + "]\n";
     main += Z + ":\ns_mov_b64 exec, s[64:65]\ns_mov_b64 exec, 0\n";
+    ovf_used = false;
     if (!copy(m, P, false, main, ool)) return false;
     main += ".L" + P + "end:\n";
-    ool += overlay_routines();
+    ool += overlay_routines() + ovf_routine();
     if (!ool.empty()) main += "s_branch .Ldone" + m.n + "\n" + ool;
     out = peephole(main);
     return true;
@@ -2085,11 +2148,13 @@ struct Compiler {
       far += "v_cmp_gt_u32 vcc, 64, v36\ns_and_b64 s[60:61], vcc, exec\n"
              "s_cbranch_scc0 .Lnd" + U + "\n"
              "s_mov_b64 exec, s[60:61]\n"
+             // (s[62:63]: the lanes whose overflow block 0 is filled)
+             "v_and_b32 v40, 1, v23\nv_cmp_ne_u32_e64 s[62:63], 0, v40\n"
              "v_mov_b32 v42, 56\nv_xad_u32 v43, v35, v42, v34\nds_read_b32 v49, v43\n"
              "v_mov_b32 v42, 60\nv_xad_u32 v43, v35, v42, v34\nds_read_b32 v50, v43\n"
              "v_mov_b32 v46, 0\nv_mov_b32 v47, 0\n"
              // clean lanes: the packet's dwords at 64 and 68 that start before LEN
-             "s_andn2_b64 exec, s[60:61], " + dm + "\n"
+             "s_andn2_b64 exec, s[60:61], s[62:63]\n"
              "s_cbranch_execz .Lsc" + U + "\n"
              "s_mov_b64 s[64:65], exec\n"
              "v_cmp_lt_u32 vcc, 64, v31\ns_and_b64 exec, s[64:65], vcc\n"
@@ -2104,7 +2169,7 @@ struct Compiler {
              "v_cndmask_b32 v46, 0, v46, vcc\nv_cndmask_b32 v47, 0, v47, vcc\n"
              ".Lsc" + U + ":\n"
              // dirty lanes: the overflow image's first two dwords
-             "s_and_b64 exec, s[60:61], " + dm + "\n"
+             "s_and_b64 exec, s[60:61], s[62:63]\n"
              "s_cbranch_execz .Lsd" + U + "\n" + ovf_addr() +
              "global_load_dword v46, v[44:45], off sc1\n"
              "global_load_dword v47, v[44:45], off offset:4 sc1\n"
@@ -2124,11 +2189,20 @@ struct Compiler {
       far += ".Lnd" + U + ":\n";
     }
     if (smode && !dm.empty()) {
-      // lanes that stored past byte 64 (the dirty mask): their bytes [64, 128) from the overflow
-      // image; an access ending past 128 deoptimizes (its high bytes would be the packet's)
+      // lanes that filled a block of their overflow image (the dirty mask) whose access touches
+      // one (the blocks bf = v39 and bl = v43 of its first and last byte): the other block filled
+      // too if it is not, then the bytes read from the image; an access ending past the image (E,
+      // mem_size > kOvfEnd) deoptimizes. The rest read the packet below.
       far += "s_and_b64 s[60:61], s[68:69], " + dm + "\n"
              "s_cbranch_scc0 .Lnv" + U + "\n"
-             "v_cmp_lt_u32 vcc, 0x80, v38\n"
+             "s_mov_b64 exec, s[60:61]\n"
+             "v_subrev_u32 v39, 64, v36\nv_lshrrev_b32 v39, 6, v39\n"
+             "v_add_u32 v43, -65, v38\nv_lshrrev_b32 v43, 6, v43\n"
+             "v_lshrrev_b32 v40, v39, v23\nv_lshrrev_b32 v42, v43, v23\nv_or_b32 v40, v40, v42\n"
+             "v_and_b32 v40, 1, v40\nv_cmp_ne_u32 vcc, 0, v40\n"
+             "s_and_b64 s[60:61], s[60:61], vcc\n"
+             "s_cbranch_scc0 .Lnv" + U + "\n" + ovf_end() +
+             "v_mov_b32 v42, s48\nv_cmp_lt_u32 vcc, v42, v38\n"
              "s_and_b64 vcc, vcc, s[60:61]\n"
              "s_cbranch_vccz .Lnq" + U + "\n"
              "s_andn2_b64 s[60:61], s[60:61], vcc\n"
@@ -2137,7 +2211,8 @@ struct Compiler {
              "s_mov_b64 exec, vcc\nv_mov_b32 v30, 0x80\nv_mov_b32 v28, -1\n"
              ".Lnq" + U + ":\n"
              "s_mov_b64 exec, s[60:61]\n"
-             "s_cbranch_execz .Lnv" + U + "\n" + ovf_addr() +
+             "s_cbranch_execz .Lnv" + U + "\n" + ovf_ensure("s[60:61]", "f" + U) +
+             "v_mov_b32 v39, v43\n" + ovf_ensure("s[60:61]", "l" + U) + ovf_addr() +
              "v_add_u32 v46, -64, v36\nv_and_b32 v46, -4, v46\nv_mov_b32 v47, 0\n"
              "v_lshl_add_u64 v[44:45], v[44:45], 0, v[46:47]\n"
              "global_load_dword v49, v[44:45], off sc1\n";
@@ -2849,7 +2924,8 @@ struct Compiler {
                 " compiled as a constant-address load the proof did not classify as one";
           return false;
         }
-        main += ovf_dirty_deopt(P + "u" + std::to_string(i), entry_label(P, next_start(i)));
+        main += ovf_dirty_deopt(P + "u" + std::to_string(i), entry_label(P, next_start(i)), t[i].a0,
+                                t[i].x - t[i].a0);
       }
     }
     if (stk && (uops[i].op == U_ST || uops[i].op == U_STX)) {
@@ -3371,7 +3447,7 @@ std::string relocated_body(const std::string& b, const std::string& n, uint32_t&
 // code (entered by a long jump), so that no branch of the template or of the statement around it
 // spans the program.
 // ebpf_tile_jit_fixed_occ: whether a compiled body names only the VGPRs its statement owns
-// (v[0:21], v[26:50]: TILE_ASM_CLOBBER_OCC in interp.hip); the others hold the kernel's own values.
+// (v[0:55], TILE_ASM_CLOBBER in interp.hip); the others hold the kernel's own values.
 bool occ_regs_ok(const std::string& b) {
   for (size_t q = 0; (q = b.find('v', q)) != std::string::npos; q++) {
     if (q > 0 && (isalnum((unsigned char)b[q - 1]) || b[q - 1] == '_' || b[q - 1] == '.')) continue;
@@ -3384,8 +3460,7 @@ bool occ_regs_ok(const std::string& b) {
     } else {
       continue;
     }
-    for (uint32_t r = lo; r <= hi; r++)
-      if (r > 50 || (r >= 22 && r <= 25)) return false;
+    if (hi >= 56) return false;
   }
   return true;
 }
@@ -3543,7 +3618,7 @@ bool compile_into_template(Compiler& c, Compiler* xc, std::vector<char>& code_ob
 // Loads straddling byte 64 are served (ldx_fixed); addresses below 0 or past mem_size fault,
 // which is not a deoptimization. Calls: no proof. (`why`: the first micro-op that failed.)
 bool store_mode_no_deopt(const std::vector<Uop>& uops, const StackPlan& stk, uint32_t* why,
-                         std::vector<char>* kld) {
+                         std::vector<char>* kld, uint64_t* st_bound, bool* len_bound) {
   using AbsVal = Compiler::AbsVal;
   using AbsRegs = Compiler::AbsRegs;
   const uint32_t n = (uint32_t)uops.size();
@@ -3601,6 +3676,10 @@ bool store_mode_no_deopt(const std::vector<Uop>& uops, const StackPlan& stk, uin
   // the largest end of a register-address store / load, of a constant-address load
   uint64_t st_end = 0, ld_end = 0, kld_end = 0;
   uint32_t st_at = UINT32_MAX, ld_at = UINT32_MAX, kld_at = UINT32_MAX;
+  // accesses proven to end inside the packet (base slack d >= off + width: r + off + width <=
+  // LEN <= mem_size) -- a write at the frame's tail, r1 + r2 - 4 -- are bounded by mem_size, not
+  // by the ranges: the host then needs mem_size <= kOvfEnd and the stack window past mem_size
+  bool len_st = false, len_ld = false;
   if (kld) kld->assign(n, 0);
   for (uint32_t i = 0; i < n; i++) {
     if (!seen[i]) {  // (no lane reaches it: whatever its code, it never deoptimizes)
@@ -3614,9 +3693,14 @@ bool store_mode_no_deopt(const std::vector<Uop>& uops, const StackPlan& stk, uin
       const int64_t e = (int64_t)b.hi + off + (int64_t)u.aux;
       return e < 0 ? 0 : (uint64_t)e;
     };
+    auto in_len = [&](const AbsVal& b) { return b.slack >= 0 && off + (int64_t)u.aux <= b.slack; };
     if (u.op == U_ST || u.op == U_STX) {
       if (stk.off[i] != kNoStack || stk.pw[i] != kNoStack || !stk.dyn[i]) continue;
       const uint64_t e = end_of(in[i][u.dst]);
+      if (e > kOvfEnd && in_len(in[i][u.dst])) {
+        len_st = true;
+        continue;
+      }
       if (e > st_end) st_end = e, st_at = i;
     } else if (u.op == U_LDX) {
       if (stk.off[i] != kNoStack) continue;  // (the stack window)
@@ -3625,6 +3709,8 @@ bool store_mode_no_deopt(const std::vector<Uop>& uops, const StackPlan& stk, uin
       if (b.lo == b.hi) {
         if (kld) (*kld)[i] = 1;
         if (e > kld_end) kld_end = e, kld_at = i;
+      } else if (e > kOvfEnd && in_len(b)) {
+        len_ld = true;
       } else if (e > ld_end) {
         ld_end = e, ld_at = i;
       }
@@ -3633,14 +3719,18 @@ bool store_mode_no_deopt(const std::vector<Uop>& uops, const StackPlan& stk, uin
       return false;
     }
   }
-  if (st_end > 128) {
+  // (the overflow image, jit.cpp ovf_fill: a store ending past kOvfEnd deoptimizes, and so may
+  // a load of a dirty lane ending past it, or a constant-address load of a filled block)
+  if (st_end > kOvfEnd) {
     if (why) *why = st_at;
     return false;
   }
-  if (st_end > 64 && (ld_end > 128 || kld_end > 64)) {
-    if (why) *why = ld_end > 128 ? ld_at : kld_at;
+  if ((st_end > 64 || len_st) && (ld_end > kOvfEnd || kld_end > 64)) {
+    if (why) *why = ld_end > kOvfEnd ? ld_at : kld_at;
     return false;
   }
+  if (st_bound) *st_bound = std::max<uint64_t>(st_end, 128);
+  if (len_bound) *len_bound = len_st || len_ld;
   return true;
 }
 

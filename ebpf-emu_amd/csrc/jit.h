@@ -42,6 +42,16 @@ struct JitFns {
 // the packet loads 8 bytes lower, the batch run as the main.rs layout over the packets,
 // Compiler::xdp_rebase)
 constexpr int kJitVariants = 7;
+// Store mode (the var tile loop): the overflow image holds image bytes [64, min(mem_size rounded
+// up to 64, kOvfEnd)) per packet, in 64-byte blocks filled on first use (jit.cpp ovf_fill); a
+// store ending past it (or past the stack window's start) deoptimizes.
+constexpr uint32_t kOvfEnd = 2048;
+// bytes of the overflow image per packet for a batch's mem_size (host.cpp workspace)
+inline uint64_t ovf_stride(uint32_t mem_size) {
+  uint64_t e = ((uint64_t)mem_size + 63) & ~63ull;
+  e = e < kOvfEnd ? e : kOvfEnd;
+  return e > 64 ? e - 64 : 0;
+}
 constexpr uint32_t kStackMax = 64;    // window bytes
 constexpr uint32_t kStackVgpr = 80;   // first VGPR of the window (ebpf_tile_jit_fixed)
 constexpr int32_t kNoStack = INT32_MIN;
@@ -66,13 +76,19 @@ struct StackPlan {
   // Codegen checks that every load it compiles as a constant-address far load (whose dirty lanes
   // deoptimize) is one of these, so the proof and the code cannot disagree silently.
   std::vector<char> kld;
+  uint64_t st_bound = 128;   // (no_deopt) every register-address store ends at or below this
+  bool len_bound = false;    // (no_deopt) ... or inside the packet (LEN <= mem_size)
 };
 
 // Store mode on the var tile loop: whether no lane of a main.rs-layout batch can deoptimize
 // (jit.cpp, a range analysis of every access; the host also needs the stack window at or past
 // byte 128). Then the deopt pass after the launch is not needed.
+// *st_bound: every register-address store ends at or below it (>= 128); the host runs a batch
+// without the pass when its stack window starts at or past it. *len_bound: some access is bounded
+// by the packet's length instead (then also mem_size <= kOvfEnd and the stack window past it).
 bool store_mode_no_deopt(const std::vector<Uop>& uops, const StackPlan& stk, uint32_t* why = nullptr,
-                         std::vector<char>* kld = nullptr);
+                         std::vector<char>* kld = nullptr, uint64_t* st_bound = nullptr,
+                         bool* len_bound = nullptr);
 
 // Status of a lane that leaves the compiled kernel for the general interpreter (never reported:
 // the tile epilogue lists the packet instead of writing its outputs, tile bucket 8).

@@ -260,6 +260,68 @@ out:
     exit
 """
 
+# an XDP responder over 1500-byte frames (memory store mode with the overflow image, jit.cpp
+# ovf_fill): ICMP echo requests answered in place -- Ethernet and IPv4 addresses swapped, type 8
+# -> 0 with the ICMP checksum adjusted (RFC 1624), XDP_TX -- and every other IPv4 frame's 4-byte
+# telemetry trailer (the frame's last 4 bytes: r1 + r2 - 4, byte 1500 of a 1504-byte slot)
+# incremented in place, read back, XDP_PASS. The ICMP header sits behind the IPv4 options, the
+# trailer at the packet's length: both register-address stores, the trailer far past the
+# 64-byte header window.
+RESPONDER = """
+    mov r0, 2                 # XDP_PASS
+    jlt r2, 42, out
+    ldxh r3, [r1+12]          # EtherType
+    jne r3, 0x0008, out
+    ldxb r6, [r1+14]          # version / IHL
+    and r6, 15
+    jlt r6, 5, drop
+    ldxb r4, [r1+23]          # protocol
+    jne r4, 1, trailer
+    lsh r6, 2
+    mov r7, r1
+    add r7, r6
+    add r7, 14                # the ICMP header, behind the IPv4 options
+    ldxb r5, [r7+0]           # type
+    jne r5, 8, trailer        # echo request only
+    ldxw r3, [r1+0]           # swap the MACs
+    ldxh r4, [r1+4]
+    ldxw r5, [r1+6]
+    ldxh r8, [r1+10]
+    stxw [r1+0], r5
+    stxh [r1+4], r8
+    stxw [r1+6], r3
+    stxh [r1+10], r4
+    ldxw r3, [r1+26]          # swap the IPv4 addresses
+    ldxw r4, [r1+30]
+    stxw [r1+26], r4
+    stxw [r1+30], r3
+    stb [r7+0], 0             # echo reply
+    ldxh r5, [r7+2]           # checksum + 0x0800 (RFC 1624, end-around carry)
+    be16 r5
+    add r5, 0x0800
+    mov r6, r5
+    rsh r6, 16
+    and r5, 0xffff
+    add r5, r6
+    be16 r5
+    stxh [r7+2], r5
+    mov r0, 3                 # XDP_TX
+    exit
+trailer:
+    mov r9, r1
+    add r9, r2                # the packet's end
+    ldxw r3, [r9-4]           # the telemetry trailer
+    add32 r3, 1
+    stxw [r9-4], r3           # a register-address store at the frame's tail
+    ldxw r4, [r9-4]           # read back through the pointer
+    jne r4, r3, drop          # (never taken)
+    exit
+drop:
+    mov r0, 1
+out:
+    exit
+"""
+
 # a firewall of ~100 instructions (past the tile interpreter's 62 micro-ops: compiled by the
 # forward-program compiler instead of interpreted by dag_kernel): 802.1Q, IPv4 sanity (version,
 # IHL, TTL, fragments), source and destination address rules, TCP flag and port rules, UDP
@@ -520,7 +582,8 @@ ACL_RULES = acl_rules_source()
 PROGRAMS = {"drop": DROP_ALL, "5tuple": FIVE_TUPLE, "checksum": CHECKSUM,
             "5tuple_stack": FIVE_TUPLE_STACK, "mac_swap_tx": MAC_SWAP_TX, "acl": ACL,
             "5tuple_xdp": FIVE_TUPLE_XDP, "checksum_stack": CHECKSUM_STACK,
-            "5tuple_call": FIVE_TUPLE_CALL, "nat": NAT_REWRITE, "checksum_xdp": CHECKSUM_XDP}
+            "5tuple_call": FIVE_TUPLE_CALL, "nat": NAT_REWRITE, "checksum_xdp": CHECKSUM_XDP,
+            "responder": RESPONDER}
 
 
 # long programs (far mode), kept apart from PROGRAMS (the compact benchmark programs)

@@ -375,6 +375,64 @@ def gen_store_program(rng: random.Random, n: int | None = None) -> bytes:
     return b"".join(words)
 
 
+def gen_far_store_program(rng: random.Random, n: int | None = None) -> bytes:
+    """Store-mode programs writing a 1500-byte frame's payload (jit.cpp's overflow image: image
+    bytes [64, 2048) in 64-byte blocks filled on first use; emu.rs:354-372): r8 = r1 + (a packet
+    byte << 2) + c (0 .. ~1400) and r7 = r8 + c2 -- pointers the load-time dataflow cannot resolve
+    -- then stores of every width through them (some straddling 64-byte blocks), loads through
+    them (stored bytes read back, other blocks read from the packet), loads at fixed payload
+    offsets, window and stack accesses, ALU and forward jumps; the registers folded into r0."""
+    n = n or rng.randrange(10, 40)
+    words: list[bytes] = [
+        encode(0x71, 8, 1, rng.randrange(0, 64)),                      # ldxb r8, [r1+k]
+        encode(0x67, 8, 0, 0, rng.choice([0, 1, 2, 2, 2])),             # lsh r8, s
+        encode(0x07, 8, 0, 0, rng.choice([0, 64, 100, 400, 700])),      # add r8, c
+        encode(0x0F, 8, 1, 0, 0),                                       # add r8, r1
+        encode(0xBF, 7, 8, 0, 0),                                       # mov r7, r8
+        encode(0x07, 7, 0, 0, rng.choice([0, 4, 61, 64, 200, 630, 1100])),
+    ]
+    regs = [0, 2, 3, 4, 5, 6]
+    while len(words) < n:
+        q = rng.random()
+        size = rng.choice([0x00, 0x08, 0x10, 0x18])
+        w = {0x00: 4, 0x08: 2, 0x10: 1, 0x18: 8}[size]
+        dst, src = rng.choice(regs), rng.randrange(10)
+        ptr = rng.choice([8, 8, 7])
+        if q < 0.32:  # store through a pointer
+            off = rng.choice([rng.randrange(-4, 70), 60, 62, 63, 127, 125])
+            if rng.random() < 0.35:
+                words.append(encode(0x62 | size, ptr, 0, off, _imm(rng)))
+            else:
+                words.append(encode(0x63 | size, ptr, src, off))
+        elif q < 0.52:  # load through a pointer
+            words.append(encode(0x61 | size, dst, ptr, rng.choice([rng.randrange(-4, 70), 61, 63, 126])))
+        elif q < 0.60:  # constant-address load past the window (the packet's payload)
+            words.append(encode(0x61 | size, dst, 1, rng.choice([rng.randrange(64, 200), 1000, 1490])))
+        elif q < 0.66:  # constant-address store / load in the window
+            off = rng.randrange(0, 64 - w + 1)
+            words.append(encode(0x63 | size, 1, src, off) if rng.random() < 0.5
+                         else encode(0x61 | size, dst, 1, off))
+        elif q < 0.72:  # the stack
+            d = -rng.randrange(w, 9)
+            words.append(encode(0x63 | size, 10, src, d) if rng.random() < 0.5
+                         else encode(0x61 | size, dst, 10, d))
+        elif q < 0.86:  # ALU (never on r1, r7 .. r10)
+            cls = rng.choice([0x04, 0x07])
+            op = rng.choice([0, 1, 2, 4, 5, 6, 7, 10, 11, 12])
+            words.append(encode((op << 4) | rng.choice([0, 0x08]) | cls, dst, src, 0, _imm(rng)))
+        elif q < 0.97:  # forward jumps
+            cls = rng.choice([0x05, 0x06])
+            op = rng.choice([0, 1, 2, 3, 4, 5, 6, 7, 10, 11, 12, 13])
+            off = rng.randrange(0, max(1, n - len(words)) + 1)
+            words.append(encode((op << 4) | rng.choice([0, 0x08]) | cls, dst, src, off, _imm(rng)))
+        else:
+            words.append(encode(0x95))
+    for r in (3, 4, 5, 6):
+        words.append(encode(0xAF, 0, r, 0, 0))                            # xor r0, r
+    words.append(encode(0x95))
+    return b"".join(words)
+
+
 def gen_slot_loop_program(rng: random.Random) -> bytes:
     """Loop programs that keep their accumulators in 8-byte stack slots, the way compiled C spills
     them (host.cpp promote_slots): `stdw [r10-8*k], c` before a byte loop over the packet

@@ -12,7 +12,8 @@ fuzz vector is cross-checked against the independent Python restatement before i
   bench_pins.json   : bench.py's weak-scaling pools at any rank count -> per-chunk counters of
                       every 1 Mi-packet chunk a pool can hold, for each bench program (so that the
                       default bench line pins its timed counters at N = 1..8)
-Usage: python tests/golden/make_golden.py [config4 | bench_pins | bench_pins_add NAME...]
+Usage: python tests/golden/make_golden.py [config4 | bench_pins | bench_pins_add NAME... |
+       bench_pins_add_1504]
 """
 import json
 import os
@@ -117,8 +118,12 @@ def config4(total=100_000_000):
 PIN_CHUNKS_64 = 128  # 16 pool batches x 8 ranks
 PIN_CHUNKS_MIXED = 16  # 2 pool batches x 8 ranks (a 1 Mi mixed batch is ~840 MB: one per rank)
 PIN_PROGRAMS_64 = ("5tuple", "drop", "5tuple_stack", "mac_swap_tx", "acl", "5tuple_xdp",
-                   "5tuple_call", "nat", "acl_rules")
+                   "5tuple_call", "nat", "acl_rules", "responder")
 PIN_PROGRAMS_MIXED = ("checksum", "checksum_stack", "checksum_xdp")
+# 1504-byte slots (bench.py --frame-bytes 1504: rank r's pool is copies of chunk r,
+# workloads.frames_fixed(1Mi, 1504, config_id=3 + 100r), mem_size = r10 = 2048)
+PIN_CHUNKS_1504 = 8
+PIN_PROGRAMS_1504 = ("responder",)
 
 
 def _pin_chunk(args):
@@ -141,6 +146,35 @@ def _pin_chunk(args):
                                     r10=2048, threads=1, xdp_md=name == "checksum_xdp")
             out[name] = [int(x) for x in cnt]
     return kind, c, out
+
+
+def _pin_chunk_1504(c):
+    buf = W.frames_fixed(1 << 20, 1504, 3 + 100 * c)
+    out = {}
+    for name in PIN_PROGRAMS_1504:
+        p = oracle.Program(W.program(name))
+        _, _, cnt = p.run_batch(buf, 1 << 20, stride=1504, mem_size=2048, r10=2048, threads=1)
+        out[name] = [int(x) for x in cnt]
+    return c, out
+
+
+def bench_pins_add_1504():
+    """Adds the 1504-byte chunks' counters (chunk_counters_1504) of PIN_PROGRAMS_1504."""
+    from multiprocessing import Pool
+
+    path = os.path.join(HERE, "bench_pins.json")
+    with open(path) as f:
+        pins = json.load(f)
+    with Pool(4) as pool:  # (a 1504-byte chunk is 1.5 GB)
+        res = sorted(pool.map(_pin_chunk_1504, range(PIN_CHUNKS_1504)))
+    for name in PIN_PROGRAMS_1504:
+        e = pins["programs"][name]
+        e["chunk_counters_1504"] = [o[name] for _, o in res]
+        e["frames_1504"] = "workloads.frames_fixed(1Mi, 1504, config_id=3 + 100*r), mem_size = r10 = 2048"
+        for cnt in e["chunk_counters_1504"]:
+            assert sum(cnt[:7]) == 1 << 20
+    with open(path, "w") as f:
+        json.dump(pins, f, indent=0)
 
 
 def bench_pins_add(names):
@@ -202,6 +236,9 @@ def bench_pins():
 if __name__ == "__main__":
     if sys.argv[1:2] == ["bench_pins_add"]:
         bench_pins_add(sys.argv[2:])
+        sys.exit(0)
+    if sys.argv[1:] == ["bench_pins_add_1504"]:
+        bench_pins_add_1504()
         sys.exit(0)
     if sys.argv[1:] == ["bench_pins"]:
         with open(os.path.join(HERE, "bench_pins.json"), "w") as f:

@@ -45,9 +45,9 @@ def test_workloads_compile():
         # (the stack programs: the main.rs layout's forward kernels, and the loop kernel's stack
         # variant unless they store into the packet; the ACL, past 62 micro-ops: the forward
         # kernels only, budgets that bind run dag_kernel / interp_kernel)
-        # (the NAT rewrite stores through a register: store mode, variant 1 only)
+        # (the NAT rewrite and the responder store through a register: store mode, variant 1 only)
         variants = ((2,) if name in ("checksum", "checksum_stack", "checksum_xdp")
-                    else (1,) if name in ("mac_swap_tx", "nat")
+                    else (1,) if name in ("mac_swap_tx", "nat", "responder")
                     else (1, 2) if name == "5tuple_stack" else (0, 1) if name == "acl"
                     else (0, 1, 2))
         for variant in variants:
@@ -69,14 +69,18 @@ def test_workloads_compile():
 def test_xdp_loop_rebase_eligibility():
     """Variant 6 (xdp_md loop programs in place, jit.cpp Compiler::xdp_rebase) is compiled only
     when the range analysis proves every packet load past the ctx: the byte sum, the bound
-    reloaded from the ctx, word + half loads behind a pointer compared with data_end; not a
+    reloaded from the ctx (through r1 or a saved copy of it), word + half loads behind a pointer
+    compared with data_end; not a
     program whose ctx-shaped load may read the ctx, nor a load at a fixed offset below 8."""
     import test_gpu_xdp_md as X
     from ebpf_emu import Program
     from ebpf_emu.asm import assemble
 
     for src, rebased in ((X.XDP_SUM, True), (X.XDP_SUM_RELOAD, True), (X.XDP_SUM_WIDE, True),
-                         (X.XDP_R1_MOVED, False),
+                         (X.XDP_SUM_CTX_SAVED, True), (X.XDP_R1_MOVED, False),
+                         # (a copy of r1 overwritten before its ctx-shaped load: not the ctx)
+                         (X.XDP_SUM_CTX_SAVED.replace("mov r0, 0", "mov r0, 0\n    add r7, 1"),
+                          False),
                          (X.XDP_SUM.replace("mov r0, 0", "ldxb r0, [r1+2]"), False)):
         p = Program(assemble(src))
         assert p.compile()

@@ -65,6 +65,24 @@ done:
     exit
 """
 
+# the bound reloaded every iteration through a saved ctx pointer (compilers keep ctx in r6: a
+# copy of r1, jit.cpp ctx_load's register set) -- in place, not staged
+XDP_SUM_CTX_SAVED = """
+    mov r6, r1
+    ldxw r2, [r6+0]
+    mov32 r7, r6
+    mov r0, 0
+loop:
+    ldxw r3, [r7+4]
+    jge r2, r3, done
+    ldxb r5, [r2+0]
+    add r0, r5
+    add r2, 1
+    ja loop
+done:
+    exit
+"""
+
 # a ctx-shaped load that is not the ctx on every path (r1 moved on one of them): compiled as a
 # load, not as the ctx's data_end
 XDP_R1_MOVED = """
@@ -350,7 +368,7 @@ def test_xdp_md_loop_programs_in_place(cuda, oracle_mod, layout):
     rng = random.Random(29)
     pkts = _xdp_packets(rng, 400)
     frames, kw = _stage(pkts, cuda, **layout)
-    for src in (XDP_SUM, XDP_SUM_RELOAD, XDP_SUM_WIDE, W.CHECKSUM_XDP):
+    for src in (XDP_SUM, XDP_SUM_RELOAD, XDP_SUM_CTX_SAVED, XDP_SUM_WIDE, W.CHECKSUM_XDP):
         img = assemble(src) if isinstance(src, str) else src
         prog = Program(img)
         assert prog.compile()

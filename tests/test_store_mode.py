@@ -261,8 +261,8 @@ def test_nat_long_options_no_deopt(cuda, oracle_mod, layout):
 
 
 # a packet byte picks where the program stores (r1 + 2 * byte: 0..510, through a register): in
-# the header window, in the overflow image [64, 128) or past it -- the last deoptimize (about
-# three lanes in four)
+# the header window, in the overflow image, or -- with the batch's r10 at 128 -- past the stack
+# window's start (r10 - k): those deoptimize (about three lanes in four)
 DEOPT_PROG = """
     ldxb r3, [r1+14]
     lsh r3, 1
@@ -280,12 +280,13 @@ DEOPT_PROG = """
 @pytest.mark.gpu
 @pytest.mark.parametrize("layout", ["fixed128", "offsets_mis3", "big"])
 def test_deopt_list_rerun(cuda, oracle_mod, layout):
-    """A store-mode batch where most lanes deoptimize (a store at or past byte 128: past the
-    overflow image): the var tile loop lists them, the deopt pass re-runs them on the general
-    interpreter (host.cpp, LaunchArgs::deopt_pass). 128-byte slots, unaligned offsets + lens and
-    300 000 packets; two launches on one workspace (the pass resets the list's words for the
-    next); status, r0 and counters == the general interpreter's == the oracle's, and the re-run
-    count (workspace +8) == the lanes whose store lands at or past byte 128."""
+    """A store-mode batch where most lanes deoptimize (r10 = 128: a store ending past the stack
+    window's start r10 - k, which the compiled kernel holds in registers): the var tile loop lists
+    them, the deopt pass re-runs them on the general interpreter (host.cpp,
+    LaunchArgs::deopt_pass). 128-byte slots, unaligned offsets + lens and 300 000 packets; two
+    launches on one workspace (the pass resets the list's words for the next); status, r0 and
+    counters == the general interpreter's == the oracle's, and the re-run count (workspace +8) ==
+    the lanes whose store ends past r10 - k."""
     import torch
 
     from ebpf_emu import Program, _lib
@@ -308,14 +309,15 @@ def test_deopt_list_rerun(cuda, oracle_mod, layout):
 
         pk = pkts
         frames, kw = _stage(pkts, cuda, **VAR_LAYOUTS[layout])
-    b = prog.make_batch(frames, **kw)
+    b = prog.make_batch(frames, r10=128, **kw)
     assert prog.batch_kernel(b) == _lib.EBPF_KERNEL_JIT_VARL_STACK
     ws = torch.zeros(prog.workspace_bytes(b, 0), dtype=torch.uint8, device=cuda)
-    b = prog.make_batch(frames, workspace=ws, **kw)
+    b = prog.make_batch(frames, r10=128, workspace=ws, **kw)
     gcnt = torch.zeros(8, dtype=torch.int64, device=cuda)
-    gen = prog.run(frames, r0=True, status=True, generic=True, counters=gcnt, **kw)
+    gen = prog.run(frames, r0=True, status=True, generic=True, counters=gcnt, r10=128, **kw)
     op = oracle_mod.Program(img)
-    want_rerun = sum(1 for p in pk if len(p) > 14 and 2 * p[14] >= 128)
+    s0 = 128 - prog.stack_window
+    want_rerun = sum(1 for p in pk if len(p) > 14 and 2 * p[14] + 1 > s0)
     assert want_rerun > n // 2
     for rep in range(2):
         out = _lib.BatchOut()
@@ -335,7 +337,7 @@ def test_deopt_list_rerun(cuda, oracle_mod, layout):
         assert torch.equal(cnt, gcnt), (rep, cnt, gcnt)
         stn, r0n = st.cpu().numpy(), r0.cpu().numpy().view(np.uint64)
         for i in range(0, len(pk), 1 if n <= 3000 else 97):
-            s, o0, _ = op.run_packet(pk[i], 1024, 512, 1 << 22)
+            s, o0, _ = op.run_packet(pk[i], 1024, 128, 1 << 22)
             assert stn[i] == s, (layout, i)
             if s == 0:
                 assert int(r0n[i]) == o0, (layout, i)
