@@ -1920,10 +1920,16 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* bin, const ebpf_batch_out* ou
   // store mode on the var tile loop with no lane able to leave (StackPlan::no_deopt: the main.rs
   // registers, the stack window at or past the overflow image's end): no deopt pass
   const uint64_t s0 = b->r10 >= p->stack.k ? b->r10 - p->stack.k : 0;  // the stack window's start
+  // (the longest image a lane can have: the slot of a batch without lengths, else mem_size --
+  // an access bounded by LEN must end before the stack window)
+  const uint64_t len_max = std::min<uint64_t>(
+      b->mem_size, !b->lens && !b->offsets ? b->stride + (a.xdp ? 8 : 0) : b->mem_size);
+  // (a store ending past mem_size faults before it could deoptimize: bounded by mem_size too)
   const bool pass = deopt && !(kid == EBPF_KERNEL_JIT_VARL_STACK && p->stack.no_deopt &&
-                               !b->init_regs && s0 >= p->stack.st_bound &&
+                               !b->init_regs &&
+                               s0 >= std::min<uint64_t>(p->stack.st_bound, b->mem_size) &&
                                (!p->stack.len_bound ||
-                                (b->mem_size <= kOvfEnd && s0 >= b->mem_size)));
+                                (b->mem_size <= kOvfEnd && s0 >= len_max)));
   if (deopt) {
     a.deopt = (uint32_t*)(ws + kWsDeoptOff);
     // (past the tier-1 slots, or the binned order and its class counts when the batch is binned)

@@ -19,6 +19,7 @@ constexpr int kDbBlock = kDbWaves * kWave;
 // waves per CU (6 waves per SIMD, the limit of its ~103 SGPRs)
 constexpr int kOccWaves = 8;
 constexpr int kOccBlock = kOccWaves * kWave;
+constexpr int kOccWgsPerCu = 3;
 constexpr int kWin = 64;              // packet bytes staged in LDS per lane (header window)
 constexpr int kWinStride = kWin + 4;  // padded per-lane LDS stride: 17 dwords, conflict-free b32
 constexpr int kMaxLdsUops = 4096;     // programs up to this many micro-ops are staged in LDS

@@ -14,8 +14,8 @@ trailer store is bounded by the packet's length, jit.cpp store_mode_no_deopt len
 workspace holds (E - 64) bytes of overflow image per packet. GPU: random programs storing and
 loading through pointers 0 .. ~1500 bytes in (fuzzgen.gen_far_store_program) on 1504-byte slots
 and on unaligned offsets + lens batches of up to 1500-byte packets == the general interpreter ==
-the oracle; the responder over crafted ICMP / IPv4 / other frames with zero lanes deoptimized and
-no deopt pass."""
+the oracle; the responder over crafted ICMP / IPv4 / other frames with zero lanes deoptimized (no
+deopt pass at all on fixed slots)."""
 import random
 import struct
 import zlib
@@ -128,8 +128,10 @@ def _run_checked(oracle_mod, img, pkts, dev, layout, expect_no_deopt=None, tag="
     torch.cuda.synchronize()
     w = ws[:12].cpu().numpy().view(np.uint32)
     assert w[0] == 0, (tag, "the deopt list was left non-empty", w)
-    if expect_no_deopt:
-        assert w[2] == 0xFFFFFFFF, (tag, "the deopt pass ran", w)  # (not launched)
+    if expect_no_deopt is not None:
+        # no lane deoptimized: the pass either not launched (0xFFFFFFFF kept: a proven program on
+        # a batch whose longest packet the host knows) or re-ran nothing
+        assert w[2] == (0xFFFFFFFF if expect_no_deopt == "no pass" else 0), (tag, w)
     gcnt = torch.zeros(8, dtype=torch.int64, device=dev)
     gen = prog.run(frames, r0=True, status=True, generic=True, counters=gcnt, mem_size=MEM,
                    r10=R10, **kw)
@@ -190,8 +192,11 @@ def test_responder_vs_oracle(cuda, oracle_mod, layout):
 
     rng = random.Random(7 + len(layout))
     pkts = _responder_packets(rng, 3000)
+    # (fixed slots: every packet 1504 bytes, below the stack window at 2048 - 4 -- no pass; with
+    # lengths the host cannot bound LEN below mem_size = r10, so the pass runs and re-runs none)
     kid, w = _run_checked(oracle_mod, W.program("responder"), pkts, cuda, layout,
-                          expect_no_deopt=True, tag=layout)
+                          expect_no_deopt="no pass" if layout == "fixed1504" else "empty pass",
+                          tag=layout)
     assert kid == _lib.EBPF_KERNEL_JIT_VARL_STACK
 
 

@@ -445,7 +445,7 @@ def test_no_deopt_proof_fuzz(cuda, oracle_mod, layout):
     from test_stack_tier import VAR_LAYOUTS, _fixed_frames, _images_of, _var_packets
 
     rng = random.Random(zlib.crc32(b"proof" + layout.encode()))
-    done = 0
+    done = nopass = 0
     for it in range(160):
         img = gen_store_program(rng)
         try:
@@ -480,8 +480,10 @@ def test_no_deopt_proof_fuzz(cuda, oracle_mod, layout):
             prog.launch(b, out, torch.cuda.current_stream())
             torch.cuda.synchronize()
             w = ws[:12].cpu().numpy().view(np.uint32)
-            if r10 == 512:  # (the stack window at 512 - k: no pass)
-                assert w[0] == 0 and w[2] == 0xFFFFFFFF, (it, w, img.hex())
+            if r10 == 512:  # (the stack window at 512 - k: no lane deoptimizes; no pass when the
+                            # stores' bound -- or mem_size -- ends before it)
+                assert w[0] == 0 and w[2] in (0, 0xFFFFFFFF), (it, w, img.hex())
+                nopass += w[2] == 0xFFFFFFFF
             else:  # (r10 - k below 128: the pass runs)
                 assert w[0] == 0 and w[2] != 0xFFFFFFFF, (it, w, img.hex())
             gen = prog.run(frames, r0=True, status=True, generic=True, r10=r10, **kw)
@@ -500,4 +502,4 @@ def test_no_deopt_proof_fuzz(cuda, oracle_mod, layout):
         else:
             done += 1
         prog.close()
-    assert done >= 8, done
+    assert done >= 8 and nopass >= 4, (done, nopass)
