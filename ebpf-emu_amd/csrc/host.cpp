@@ -343,7 +343,7 @@ static int jit_compile_locked(ebpf_prog* p) {
                                               p->stack.k ? &p->stack : nullptr, &q.deep)
                            : jit_compile(p->xuops, v == 3 ? p->tuopsk_xdp : v ? p->tuopsk : p->tuops,
                                          q.co, &q.err, &q.text, p->stack.k ? &p->stack : nullptr,
-                                         &q.occ));
+                                         &q.occ, v == 1));
         });
       }
       for (std::thread& t : th) t.join();

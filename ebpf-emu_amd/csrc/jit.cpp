@@ -415,6 +415,7 @@ struct Compiler {
   // out-of-line code in islands between blocks (copy) so that every short branch stays in reach
   bool far_mode = false;
   bool occ_ok = false;  // the occupancy variant's body compiled (compile_into_template)
+  bool main_layout = false;  // the main.rs register layout (variant 1): the ranges hold for it
   mutable uint32_t wcache = 0;  // store mode: window chunks cached in v[64:79] here (ldxk_lds)
   mutable uint32_t far_tag = 0;
   size_t island_from = 0;  // main's length after the last island
@@ -900,12 +901,84 @@ struct Compiler {
   }
 
   // Conditional jump tail: vcc = taken among the active lanes.
+  // The eBPF registers live on entry to each micro-op (bit r; a backward dataflow to a fixpoint,
+  // loops included). Conservative: an exit, a fault or a call reads every register (the final
+  // registers are an output), a load merges into its destination (Q1).
+  mutable std::vector<uint16_t> live_in_;
+  uint16_t live_in(uint32_t pc) const {
+    constexpr uint16_t kAll = 0x7ff;
+    if (pc >= n) return kAll;
+    if (live_in_.empty()) {
+      std::vector<uint16_t> li(n, 0);
+      for (bool ch = true; ch;) {
+        ch = false;
+        for (uint32_t j = n; j-- > 0;) {
+          const Uop& u = uops[j];
+          const uint16_t D = (uint16_t)(u.dst <= 10 ? 1u << u.dst : 0);
+          const uint16_t S = (uint16_t)(u.src <= 10 ? 1u << u.src : 0);
+          const bool reg = (u.aux & F_SRC) != 0;
+          uint16_t use = 0, def = 0, out = 0;
+          auto at = [&](uint32_t q) -> uint16_t { return q >= n ? kAll : li[q]; };
+          bool next = true;
+          if (u.op <= U_ARSH32) {
+            const bool mov = u.op == U_MOV64 || u.op == U_MOV32;
+            use = (uint16_t)((mov ? 0 : D) | (reg ? S : 0));
+            def = D;
+          } else if (u.op <= U_BSWAP64) {
+            use = D, def = u.op == U_NOP ? 0 : D;
+          } else if (u.op == U_JA) {
+            next = false;
+            out = at((uint32_t)u.x);
+          } else if (is_jump(u)) {
+            use = (uint16_t)(D | (reg ? S : 0));
+            out = at((uint32_t)u.x);
+          } else if (u.op == U_LDIMM) {
+            def = D;
+          } else if (u.op == U_LDX) {
+            use = (uint16_t)(S | (u.aux < 8 ? D : 0)), def = D;
+          } else if (u.op == U_ST) {
+            use = D;
+          } else if (u.op == U_STX) {
+            use = (uint16_t)(D | S);
+          } else if (u.op == U_ATOMIC) {
+            use = (uint16_t)(D | S | 1u);
+          } else {  // CALL, EXIT, FAULT
+            use = kAll, next = false;
+          }
+          if (next) out |= at(j + 1);
+          const uint16_t v = (uint16_t)(use | (out & ~def));
+          if (v != li[j]) li[j] = v, ch = true;
+        }
+      }
+      live_in_ = li;
+    }
+    return live_in_[pc];
+  }
+  // A marker for the jump tail's sinking pass (sink_high_zero): the high-half VGPRs of the
+  // registers dead where this jump's leaving lanes go.
+  std::string dead_marker(uint32_t leave) const {
+    if (leave >= n) return "";
+    const uint16_t dead = (uint16_t)(~live_in(leave) & 0x7ff);
+    if (!dead) return "";
+    std::string m = "; dead@leave";
+    for (uint32_t r = 0; r <= 10; r++)
+      if (dead & (1u << r)) m += " v" + std::to_string(2 * r + 1);
+    return m + "\n";
+  }
+
   std::string jtail(uint32_t i, const std::string& P) const {
     if (back_edge(i)) return back_tail(i, P);
     const uint32_t x = t[i].x, np = t[i].npc;
     const bool x_next = x == i + 1, n_next = np == i + 1;
     const bool x_done = x >= n, n_done = np >= n;
     if (x_next && n_next) return "";
+    if (n_next != x_next) return dead_marker(n_next ? x : np) + jtail_code(i);
+    return jtail_code(i);
+  }
+  std::string jtail_code(uint32_t i) const {
+    const uint32_t x = t[i].x, np = t[i].npc;
+    const bool x_next = x == i + 1, n_next = np == i + 1;
+    const bool x_done = x >= n, n_done = np >= n;
     // the leaving lanes' LPC by one select on vcc (the pcs are inline constants, or VGPRs above
     // 64), then exec
     std::string pre;
@@ -1267,9 +1340,9 @@ struct Compiler {
   }
   // The fill routine (one per body, behind its code: ovf_routine; called with s_swappc, return
   // address in s[62:63]): the lanes of exec (some) get block v39 of their overflow image filled
-  // from the packet's dwords (those before LEN; the bytes at or past it zero), 16 bytes at a time
-  // through v[52:55]; bit v39 set in v23, the lanes added to dm. Keeps v36-v39, v42, v43,
-  // s[60:61], s[66:69]; uses v40, v41, v44-v48, v50-v55, s[48:49], s[64:65], vcc.
+  // from the packet's dwords (those before LEN; the bytes at or past it zero), all 16 in flight
+  // through v[64:79]; bit v39 set in v23, the lanes added to dm. Keeps v36-v39, v42, v43,
+  // s[60:61], s[66:69]; uses v40, v41, v44-v48, v50, v51, v64-v79, s[48:49], s[64:65], vcc.
   mutable bool ovf_used = false;
   std::string ovf_label() const { return ".Lovf" + ovl_tag; }
   std::string ovf_routine() const {
@@ -1281,25 +1354,23 @@ struct Compiler {
                     "v_add_u32 v40, 64, v40\n"  // the block's image offset o
                     "v_lshl_add_u64 v[46:47], v[32:33], 0, v[40:41]\n"
                     "v_sub_u32 v48, v31, v40\n";  // LEN - o (signed)
-    for (uint32_t q = 0; q < 4; q++) {
-      for (uint32_t k = 0; k < 4; k++) {
-        const std::string K = std::to_string(16 * q + 4 * k), V = "v" + std::to_string(52 + k);
-        r += "v_mov_b32 " + V + ", 0\n"
-             "v_cmp_lt_i32 vcc, " + K + ", v48\ns_and_b64 exec, s[64:65], vcc\n"
-             "global_load_dword " + V + ", v[46:47], off offset:" + K + "\n"
-             "s_mov_b64 exec, s[64:65]\n";
-      }
-      r += "s_waitcnt vmcnt(0)\n";
-      for (uint32_t k = 0; k < 4; k++)
-        r += "v_subrev_u32 v50, " + std::to_string(16 * q + 4 * k) + ", v48\n"
-             "v_med3_i32 v50, v50, 0, 4\nv_lshlrev_b32 v50, 3, v50\n"
-             "v_lshlrev_b64 v[50:51], v50, 1\nv_add_u32 v50, -1, v50\n"
-             "v_and_b32 v" + std::to_string(52 + k) + ", v50, v" + std::to_string(52 + k) + "\n";
-      // (s_nop 1: a store of more than 64 bits reads its data VGPRs after issue -- the next
-      // round's moves into v[52:55] must wait, cdna_asm_programming.md 4.1)
-      r += "global_store_dwordx4 v[44:45], v[52:55], off offset:" + std::to_string(16 * q) +
-           "\ns_nop 1\n";
-    }
+    // the block's 16 dwords in flight at once, into v[64:79] (free in store mode: the chunk
+    // cache is invalidated around every call, ldxk_lds)
+    for (uint32_t k = 0; k < 16; k++) r += "v_mov_b32 v" + std::to_string(64 + k) + ", 0\n";
+    for (uint32_t k = 0; k < 16; k++)
+      r += "v_cmp_lt_i32 vcc, " + std::to_string(4 * k) + ", v48\ns_and_b64 exec, s[64:65], vcc\n"
+           "global_load_dword v" + std::to_string(64 + k) + ", v[46:47], off offset:" +
+           std::to_string(4 * k) + "\n";
+    r += "s_mov_b64 exec, s[64:65]\ns_waitcnt vmcnt(0)\n";
+    for (uint32_t k = 0; k < 16; k++)
+      r += "v_subrev_u32 v50, " + std::to_string(4 * k) + ", v48\n"
+           "v_med3_i32 v50, v50, 0, 4\nv_lshlrev_b32 v50, 3, v50\n"
+           "v_lshlrev_b64 v[50:51], v50, 1\nv_add_u32 v50, -1, v50\n"
+           "v_and_b32 v" + std::to_string(64 + k) + ", v50, v" + std::to_string(64 + k) + "\n";
+    for (uint32_t c = 0; c < 4; c++)
+      r += "global_store_dwordx4 v[44:45], v[" + std::to_string(64 + 4 * c) + ":" +
+           std::to_string(67 + 4 * c) + "], off offset:" + std::to_string(16 * c) + "\n";
+    // (the wait also covers the stores' reads of their data VGPRs)
     return r + "s_waitcnt vmcnt(0)\nv_lshlrev_b32 v40, v39, 1\nv_or_b32 v23, v23, v40\n"
                "s_setpc_b64 s[62:63]\n";
   }
@@ -1307,6 +1378,7 @@ struct Compiler {
   // `lanes` after).
   std::string ovf_ensure(const std::string& lanes, const std::string& tag) const {
     ovf_used = true;
+    wcache = 0;  // (the routine uses v[64:79])
     const std::string P = ".Lfp" + tag, L = ovf_label(), d = "(" + L + "-" + P + ")";
     return "v_lshrrev_b32 v40, v39, v23\nv_and_b32 v40, 1, v40\nv_cmp_eq_u32 vcc, 0, v40\n"
            "s_and_b64 exec, " + lanes + ", vcc\ns_cbranch_execz .Lfe" + tag + "\n"
@@ -2892,6 +2964,12 @@ struct Compiler {
       err = "bad handler id";
       return false;
     }
+    // (the main.rs layout's forward code: a jump on a register the range analysis bounds below
+    // 2^32 -- its high half zero -- against a constant; narrow_compares takes the marker)
+    if (main_layout && !loops && !ranges.empty() && reached.size() == n && reached[i] &&
+        is_jump(uops[i]) && uops[i].op != U_JA && !(uops[i].aux & F_SRC) &&
+        ranges[i][uops[i].dst].hi < (1ull << 32))
+      main += "; hi0 v" + std::to_string(2 * uops[i].dst + 1) + "\n";
     if (stk && stk->any_dyn) {  // store mode: the header window lives in LDS
       const Uop& o = uops[i];
       if ((o.op == U_ST || o.op == U_STX) && stk->off[i] == kNoStack) {
@@ -3066,6 +3144,7 @@ struct Compiler {
   // otherwise the handlers' copy, with its per-load bounds checks.
   bool body(const Marker& m, std::string& out) {
     if (stk && stk->any_dyn) return body_store(m, out);
+    if (main_layout && !stk && ranges.empty()) prove_loads();  // (no stores: the ranges hold)
     const std::string P = "J" + m.n + "_";
     ovl_tag = m.n;
     overlay_widths = 0;
@@ -3308,11 +3387,65 @@ struct Compiler {
       }
       out += ln[i] + "\n";
     }
-    return narrow_compares(out);
+    return sink_high_zero(narrow_compares(out));
+  }
+
+  // A register's high half zeroed just before a jump (`v_mov_b32 vH, 0` of a fused mov + and,
+  // its compare narrowed to the low half) whose leaving lanes go where the register is dead
+  // (the `; dead@leave` marker of jtail): the move goes after the jump's exec update, so only
+  // the staying lanes run it -- in a rule chain, the rule's first test sends nearly every lane to
+  // the next rule, which overwrites the register, and the move leaves the common path.
+  static std::string sink_high_zero(const std::string& text) {
+    std::vector<std::string> ln;
+    for (size_t p = 0; p < text.size();) {
+      size_t e = text.find('\n', p);
+      if (e == std::string::npos) e = text.size();
+      ln.push_back(text.substr(p, e - p));
+      p = e + 1;
+    }
+    auto names = [](const std::string& l, const std::string& v) {
+      for (size_t q = 0; (q = l.find(v, q)) != std::string::npos; q += v.size()) {
+        const bool lo = q == 0 || !(isalnum((unsigned char)l[q - 1]) || l[q - 1] == '_');
+        const size_t e = q + v.size();
+        const bool hi = e >= l.size() || !isalnum((unsigned char)l[e]);
+        if (lo && hi) return true;
+      }
+      return false;
+    };
+    for (size_t m = 0; m < ln.size(); m++) {
+      if (ln[m].compare(0, 12, "; dead@leave") != 0) continue;
+      size_t x = m + 1;  // the exec update of the jump tail
+      while (x < ln.size() && x <= m + 4 && ln[x].compare(0, 16, "s_and_b64 exec, ") != 0 &&
+             ln[x].compare(0, 18, "s_andn2_b64 exec, ") != 0)
+        x++;
+      if (x >= ln.size() || x > m + 4 || (ln[x] != "s_and_b64 exec, exec, vcc" &&
+                                          ln[x] != "s_andn2_b64 exec, exec, vcc"))
+        continue;
+      for (size_t k = m; k-- > 0 && k + 6 > m;) {
+        uint32_t h;
+        if (sscanf(ln[k].c_str(), "v_mov_b32 v%u, 0", &h) != 1 || ln[k] != "v_mov_b32 v" + std::to_string(h) + ", 0")
+          continue;
+        const std::string vh = "v" + std::to_string(h);
+        if (!names(ln[m], vh)) continue;
+        bool clear = true;  // nothing between the move and the exec update names vH or is a label
+        for (size_t q = k + 1; q <= x && clear; q++)
+          clear = !names(ln[q], vh) || q == m;
+        for (size_t q = k + 1; q <= x && clear; q++) clear = ln[q].empty() || ln[q][0] != '.';
+        if (!clear) continue;
+        ln.insert(ln.begin() + x + 1, ln[k]);
+        ln.erase(ln.begin() + k);
+        m--;
+        x--;
+      }
+    }
+    std::string r;
+    for (const std::string& l : ln) r += l + "\n";
+    return r;
   }
 
   // A 64-bit compare of a register whose high half was just zeroed with a constant below 2^32
-  // (`v_mov_b32 vH, 0`, s[48:49] = {K, 0}, `v_cmp_<op>_[iu]64 vcc, s[48:49], v[L:H]`, in a row):
+  // (`v_mov_b32 vH, 0` -- or the `; hi0 vH` marker of a register the range analysis bounds below
+  // 2^32 -- then s[48:49] = {K, 0}, `v_cmp_<op>_[iu]64 vcc, s[48:49], v[L:H]`, in a row):
   // both sides lie in [0, 2^32), where the signed and unsigned orders agree, so the 32-bit
   // unsigned compare of the low halves gives the same vcc -- with K as the VOPC's literal (the
   // s_movs of s[48:49] go: a micro-op's code sets every field register it reads).
@@ -3329,7 +3462,10 @@ struct Compiler {
       char op[8], sg;
       uint32_t lo, hi, h0;
       if (i >= 3 && ln[i - 1] == "s_mov_b32 s49, 0x0" && ln[i - 2].compare(0, 15, "s_mov_b32 s48, ") == 0 &&
-          sscanf(ln[i - 3].c_str(), "v_mov_b32 v%u, 0", &h0) == 1 && ln[i - 3] == "v_mov_b32 v" + std::to_string(h0) + ", 0" &&
+          ((sscanf(ln[i - 3].c_str(), "v_mov_b32 v%u, 0", &h0) == 1 &&
+            ln[i - 3] == "v_mov_b32 v" + std::to_string(h0) + ", 0") ||
+           (sscanf(ln[i - 3].c_str(), "; hi0 v%u", &h0) == 1 &&
+            ln[i - 3] == "; hi0 v" + std::to_string(h0))) &&
           sscanf(ln[i].c_str(), "v_cmp_%2[a-z]_%c64 vcc, s[48:49], v[%u:%u]", op, &sg, &lo, &hi) == 4 &&
           (sg == 'u' || sg == 'i') && hi == lo + 1 && hi == h0 &&
           ln[i] == std::string("v_cmp_") + op + "_" + sg + "64 vcc, s[48:49], v[" + std::to_string(lo) +
@@ -3736,7 +3872,7 @@ bool store_mode_no_deopt(const std::vector<Uop>& uops, const StackPlan& stk, uin
 
 bool jit_compile(const std::vector<Uop>& uops, const std::vector<TUop>& t,
                  std::vector<char>& code_object, std::string* err, std::string* asm_out,
-                 const StackPlan* stk, bool* occ) {
+                 const StackPlan* stk, bool* occ, bool main_layout) {
   if (uops.empty() || uops.size() > kJitMaxUops || t.size() < uops.size() ||
       (stk && (stk->k == 0 || stk->k > kStackMax || stk->k % 4 || stk->off.size() != uops.size() ||
                stk->pw.size() != uops.size() ||
@@ -3745,6 +3881,7 @@ bool jit_compile(const std::vector<Uop>& uops, const std::vector<TUop>& t,
     return false;
   }
   Compiler c(uops, t, false, false, stk);
+  c.main_layout = main_layout;
   const bool ok = compile_into_template(c, nullptr, code_object, err, asm_out);
   if (occ) *occ = ok && c.occ_ok;
   return ok;

@@ -101,9 +101,11 @@ constexpr uint32_t kStDeopt = 0x80;
 // get its code).
 // *occ (if given): the code also went into ebpf_tile_jit_fixed_occ (an issue-bound program whose
 // code fits that statement's registers).
+// main_layout: the table of the main.rs register layout (variant 1): its compare narrowing may use
+// the load-time value ranges.
 bool jit_compile(const std::vector<Uop>& uops, const std::vector<TUop>& t,
                  std::vector<char>& code_object, std::string* err, std::string* asm_out = nullptr,
-                 const StackPlan* stk = nullptr, bool* occ = nullptr);
+                 const StackPlan* stk = nullptr, bool* occ = nullptr, bool main_layout = false);
 
 // Loop programs (back edges, or budgets that can bind; tile tables of build_tile: `t` the block
 // table, `tx` the exact one-micro-op-per-block table) for ebpf_tile_jit_loop. *deep (if given):
