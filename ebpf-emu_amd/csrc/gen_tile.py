@@ -1385,7 +1385,7 @@ s_cbranch_scc1 .Linitx%=
 ;@@JITINIT@@
 .Linitd%=:
 
-; JIT N=%= fixed=%[fixed] loops=%[loops] aligned=%[aligned] xdp=%[xdpf]""" + (" occ=1" if single else "") + """
+; JIT N=%= fixed=%[fixed] loops=%[loops] aligned=%[aligned] xdp=%[xdpf] pm=1""" + (" occ=1" if single else "") + """
 ;@@JIT@@
 .Ldone%=:
 ; verdict byte, the lane's counter bucket (verdict 0..4, 0xfe -> 5, 0xff -> 6) into %[acc]

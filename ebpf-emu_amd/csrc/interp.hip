@@ -1578,6 +1578,8 @@ constexpr uint32_t kVarlWaveLds = 2 * kWinBytes + 2 * kVarMetaBytes;
           [o_status] "i"(offsetof(LaunchArgs, status)), [o_regs] "i"(offsetof(LaunchArgs, regs_out))
 #define TILE_ASM_CLOBBER "s33", "s34", "s35", "s36", "s37", "s38", "s39", "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53", "s54", "s55", "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71", "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15", "v16", "v17", "v18", "v19", "v20", "v21", "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32", "v33", "v34", "v35", "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", "vcc", "scc", "memory"
 #define TILE_ASM_OPERANDS : TILE_ASM_OUT : TILE_ASM_IN : TILE_ASM_CLOBBER
+// the fixed-slot statements' (marker pm=1) pending masks of compiled forward programs (jit.cpp pm_assign)
+#define TILE_ASM_CLOBBER_PM "s72", "s73", "s74", "s75", "s76", "s77", "s78", "s79"
 // the compiled programs' preloaded window dwords (jit.cpp ldxk_fast): v[64:79]
 // and the stack window of memory tier 0.5 (jit.h kStackVgpr, kStackMax / 4 dwords): v[80:95]
 // compiled loop programs: the next 64 bytes of each lane's packet, prefetched by every window
@@ -1937,12 +1939,12 @@ __device__ __forceinline__ void fixed_body(LaunchArgs& a) {
       asm volatile(
 #include "tile_jit_loop1.inc"
           FIXED_OPERANDS
-          : TILE_ASM_CLOBBER);
+          : TILE_ASM_CLOBBER, TILE_ASM_CLOBBER_PM);
     } else {
       asm volatile(
 #include "tile_jit_loop.inc"
           FIXED_OPERANDS
-          : TILE_ASM_CLOBBER, TILE_ASM_CLOBBER_WINDOW);
+          : TILE_ASM_CLOBBER, TILE_ASM_CLOBBER_WINDOW, TILE_ASM_CLOBBER_PM);
     }
 #undef FIXED_OPERANDS
     // (an asm statement with VGPR outputs is divergent as a whole to the compiler: the scalar

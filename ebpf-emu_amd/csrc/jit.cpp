@@ -66,6 +66,7 @@ struct Marker {
   bool deep = false;   // the deep-prefetch loop kernel's statement
   bool occ = false;    // the fixed-slot kernel's occupancy variant (ebpf_tile_jit_fixed_occ): no
                        // preloaded window, only v[0:55] for the program's code
+  bool pm = false;     // the statement gives the body s[72:79] (the pending masks, pm_assign)
   bool varl = false;   // the var tile loop's statement (ebpf_tile_jit_varl): the var flavour of
                        // loads with the preloaded window, as the stack statement's
   // the var tile loop's store-mode state (gen_tile.py jit_statement_varl): the SGPR pair of
@@ -117,6 +118,7 @@ bool find_markers(const std::string& s, std::vector<Marker>& out) {
     m.deep = field("deep=") == "1";
     m.varl = field("varl=") == "1";
     m.occ = field("occ=") == "1";
+    m.pm = field("pm=") == "1";
     m.ovf = field("ovf=");
     m.tile = field("tile=");
     m.dm = field("dm=");
@@ -417,6 +419,58 @@ struct Compiler {
   bool occ_ok = false;  // the occupancy variant's body compiled (compile_into_template)
   bool main_layout = false;  // the main.rs register layout (variant 1): the ranges hold for it
   mutable uint32_t wcache = 0;  // store mode: window chunks cached in v[64:79] here (ldxk_lds)
+  // pending masks (forward programs, statements with pm=1): pm_of[T] = the SGPR pair s[72+2k:73+2k]
+  // k holding the lanes parked at target T, or -1 (parked through LPC, v28, as everywhere else)
+  std::vector<int> pm_of;
+  static constexpr int kPmPairs = 4;
+
+  // Lanes that jump to a forward target T park in an SGPR mask instead of LPC when every edge into
+  // T is a jump's (jtail, ja) and one of kPmPairs pairs is free over [T's first source, T]: the jump
+  // ORs its leaving lanes into the mask (SALU) where it wrote LPC with a select (VALU), and T's entry
+  // takes exec from the mask where it compared LPC (VALU) -- a rule chain's per-rule VALU chain
+  // loses its select and its re-admission compare. Min-pc order is unchanged: code order is
+  // execution order in a forward program and every empty-exec skip lands on a target entry (the
+  // mask's lanes re-admitted there). A lane's LPC keeps its last parked value, below every later
+  // entry, so no LPC compare re-admits it.
+  void pm_assign(const Marker& m) {
+    pm_of.assign(n + 1, -1);
+    if (!m.pm || loops || stk) return;
+    std::vector<uint32_t> first(n + 1, UINT32_MAX);
+    for (uint32_t i = 0; i < n; i++) {
+      if (!is_jump(uops[i])) continue;
+      const uint32_t x = t[i].x, np = t[i].npc;
+      if ((x <= i && x < n) || (uops[i].op != U_JA && np <= i && np < n)) return;  // (a back edge)
+      if (x < n && x != i + 1) first[x] = std::min(first[x], i);
+      if (uops[i].op != U_JA && np < n && np != i + 1) first[np] = std::min(first[np], i);
+    }
+    std::vector<uint32_t> busy_until(kPmPairs, 0);  // a pair is free after its target's entry
+    std::vector<uint32_t> order;
+    for (uint32_t T = 1; T < n; T++)
+      if (target[T] && first[T] != UINT32_MAX) order.push_back(T);
+    std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return first[a] < first[b]; });
+    for (uint32_t T : order)
+      for (int k = 0; k < kPmPairs; k++)
+        if (busy_until[k] <= first[T]) {
+          busy_until[k] = T;
+          pm_of[T] = k;
+          break;
+        }
+  }
+  std::string pm_reg(uint32_t T) const {
+    if (T >= pm_of.size() || pm_of[T] < 0) return "";
+    const int b = 72 + 2 * pm_of[T];
+    return "s[" + std::to_string(b) + ":" + std::to_string(b + 1) + "]";
+  }
+  std::string pm_zero() const {
+    std::string s;
+    std::vector<char> used(kPmPairs, 0);
+    for (int k : pm_of)
+      if (k >= 0 && !used[k]) {
+        used[k] = 1;
+        s += "s_mov_b64 s[" + std::to_string(72 + 2 * k) + ":" + std::to_string(73 + 2 * k) + "], 0\n";
+      }
+    return s;
+  }
   mutable uint32_t far_tag = 0;
   size_t island_from = 0;  // main's length after the last island
   // A branch whose target may lie past s_branch's reach in far mode: `cond` "" for s_branch, else
@@ -982,6 +1036,24 @@ struct Compiler {
     // the leaving lanes' LPC by one select on vcc (the pcs are inline constants, or VGPRs above
     // 64), then exec
     std::string pre;
+    const std::string mx = x_done ? "" : pm_reg(x), mn = n_done ? "" : pm_reg(np);
+    if (n_next && !mx.empty())  // taken lanes leave into their target's mask
+      return "s_and_b64 vcc, vcc, exec\ns_or_b64 " + mx + ", " + mx + ", vcc\n"
+             "s_andn2_b64 exec, exec, vcc\n";
+    if (x_next && !mn.empty())  // not-taken lanes leave into theirs
+      return "s_andn2_b64 s[64:65], exec, vcc\ns_or_b64 " + mn + ", " + mn + ", s[64:65]\n"
+             "s_and_b64 exec, exec, vcc\n";
+    if (!n_next && !x_next && (!mx.empty() || !mn.empty())) {  // both leave, one or both masked
+      std::string s = "s_and_b64 vcc, vcc, exec\n";
+      if (!mx.empty()) s += "s_or_b64 " + mx + ", " + mx + ", vcc\n";
+      if (!mn.empty()) s += "s_andn2_b64 s[64:65], exec, vcc\ns_or_b64 " + mn + ", " + mn + ", s[64:65]\n";
+      const std::string lx = mx.empty() ? vop3_lpc(lpc_of(x, x_done), "v37", pre) : "",
+                        ln = mn.empty() ? vop3_lpc(lpc_of(np, n_done), "v38", pre) : "";
+      if (!lx.empty() || !ln.empty())
+        s += pre + "v_cndmask_b32_e64 v28, " + (ln.empty() ? "v28" : ln) + ", " +
+             (lx.empty() ? "v28" : lx) + ", vcc\n";
+      return s + "s_mov_b64 exec, 0\n";
+    }
     if (n_next) {  // taken lanes leave
       const std::string lx = vop3_lpc(lpc_of(x, x_done), "v37", pre);
       return pre + (lx.empty() ? "" : "v_cndmask_b32_e64 v28, v28, " + lx + ", vcc\n") +
@@ -1007,6 +1079,8 @@ struct Compiler {
     if (back_edge(i)) return back_tail(i, P);
     const uint32_t x = t[i].x;
     if (x == i + 1) return "";
+    const std::string mx = x >= n ? "" : pm_reg(x);
+    if (!mx.empty()) return "s_or_b64 " + mx + ", " + mx + ", exec\ns_mov_b64 exec, 0\n";
     return park(std::to_string(x), x >= n) + "s_mov_b64 exec, 0\n";
   }
 
@@ -1556,6 +1630,7 @@ struct Compiler {
   // header window's bytes at or past LEN zeroed in LDS once (lanes with LEN < 64 only), so loads
   // and stores address one image; then the program's one (checked) copy.
   bool body_store(const Marker& m, std::string& out) {
+    pm_of.clear();  // (LPC parking only)
     const std::string P = "J" + m.n + "_";
     ovl_tag = m.n;
     overlay_widths = 0;
@@ -2344,7 +2419,12 @@ struct Compiler {
       }
       if (start[i]) {
         main += ".L" + P + "b" + std::to_string(i) + ":\n";
-        if (target[i] && !loops && i > 0 && clears_exec(i - 1))  // (exec is empty here)
+        const std::string pm = pm_reg(i);
+        if (!pm.empty())  // (every lane parked here is in the mask)
+          main += (i > 0 && clears_exec(i - 1) ? "s_mov_b64 exec, " + pm + "\n"
+                                               : "s_or_b64 exec, exec, " + pm + "\n") +
+                  "s_mov_b64 " + pm + ", 0\n";
+        else if (target[i] && !loops && i > 0 && clears_exec(i - 1))  // (exec is empty here)
           main += "s_mov_b64 exec, -1\nv_cmpx_eq_u32 vcc, " + std::to_string(i) + ", v28\n";
         else if (target[i])
           main += "s_or_saveexec_b64 s[64:65], -1\nv_cmp_eq_u32 vcc, " + std::to_string(i) +
@@ -3151,6 +3231,8 @@ struct Compiler {
     island_from = 0;
     std::string main = "; compiled eBPF program: " + std::to_string(n) + " micro-ops\n"
                        "s_mov_b32 s52, s33\ns_mov_b32 s53, 0\n";
+    pm_assign(m);
+    main += pm_zero();
     if (stk) main += stack_zero();
     // xdp_md in place (fixed-slot kernel; the other kernels shift in C++, interp.hip xdp_window):
     // the lane's window holds packet bytes [0, 64), the program reads image bytes [0, 64) =
@@ -3221,6 +3303,7 @@ struct Compiler {
   // ebpf_tile_jit_loop: s70 = 0 runs the block copy, whose budget failure restarts the tile
   // (.Lreinit of the statement's prologue) with s70 = 1, which runs the exact copy.
   bool body_loop(const Marker& m, Compiler& xc, std::string& out) {
+    pm_of.clear();  // (LPC parking only)
     // (compile_into_template may run this twice -- a dry run finds a cooperative sum, then the
     // real one: every piece of state a run writes is reset here, so the two agree)
     for (Compiler* k : {this, &xc}) {
@@ -3410,6 +3493,11 @@ struct Compiler {
         const bool hi = e >= l.size() || !isalnum((unsigned char)l[e]);
         if (lo && hi) return true;
       }
+      // a register range v[a:b] holding it (a 64-bit operand)
+      uint32_t r, a, b;
+      if (sscanf(v.c_str(), "v%u", &r) != 1) return false;
+      for (size_t q = 0; (q = l.find("v[", q)) != std::string::npos; q += 2)
+        if (sscanf(l.c_str() + q, "v[%u:%u]", &a, &b) == 2 && a <= r && r <= b) return true;
       return false;
     };
     for (size_t m = 0; m < ln.size(); m++) {
@@ -3421,6 +3509,37 @@ struct Compiler {
       if (x >= ln.size() || x > m + 4 || (ln[x] != "s_and_b64 exec, exec, vcc" &&
                                           ln[x] != "s_andn2_b64 exec, exec, vcc"))
         continue;
+      // `v_and_b32 vL, 0xff|0xffff, vS` + `v_cmp_<op>_u32 vcc, K, vL` right before the marker, the
+      // register (vL, vL+1) dead where the leaving lanes go: the compare reads vS's low byte / half
+      // itself (SDWA), and the and goes after the exec update with the high half's move
+      {
+        uint32_t L, S, L2;
+        char msk[16], op[8], kv[32];
+        size_t ka = m >= 2 ? m - 2 : 0;  // the and: right before the compare, or before the high
+        uint32_t hz;                      // half's move and the `; hi0` marker
+        while (ka > 0 && ka + 4 >= m &&
+               ((sscanf(ln[ka].c_str(), "v_mov_b32 v%u, 0", &hz) == 1 && ln[ka] == "v_mov_b32 v" + std::to_string(hz) + ", 0") ||
+                ln[ka].compare(0, 6, "; hi0 ") == 0))
+          ka--;
+        if (m >= 2 && sscanf(ln[ka].c_str(), "v_and_b32 v%u, %15[^,], v%u", &L, msk, &S) == 3 &&
+            ln[ka] == "v_and_b32 v" + std::to_string(L) + ", " + msk + ", v" + std::to_string(S) &&
+            (std::string(msk) == "0xff" || std::string(msk) == "0xffff") && S != L && S != L + 1 &&
+            sscanf(ln[m - 1].c_str(), "v_cmp_%2[a-z]_u32 vcc, %31[^,], v%u", op, kv, &L2) == 3 &&
+            L2 == L && ln[m - 1] == std::string("v_cmp_") + op + "_u32 vcc, " + kv + ", v" + std::to_string(L) &&
+            names(ln[m], "v" + std::to_string(L + 1)) && L % 2 == 0 && [&] {
+              for (size_t q = m; q <= x; q++)  // (vL unread, vS unwritten up to the exec update)
+                if (q != m && (names(ln[q], "v" + std::to_string(L)) || names(ln[q], "v" + std::to_string(S))))
+                  return false;
+              return true;
+            }()) {
+          const std::string sel = std::string(msk) == "0xff" ? "BYTE_0" : "WORD_0";
+          const std::string a = ln[ka];
+          ln[ka] = "s_mov_b32 s48, " + std::string(kv);
+          ln[m - 1] = std::string("v_cmp_") + op + "_u32_sdwa vcc, s48, v" + std::to_string(S) +
+                      " src0_sel:DWORD src1_sel:" + sel;
+          ln.insert(ln.begin() + x + 1, a);
+        }
+      }
       for (size_t k = m; k-- > 0 && k + 6 > m;) {
         uint32_t h;
         if (sscanf(ln[k].c_str(), "v_mov_b32 v%u, 0", &h) != 1 || ln[k] != "v_mov_b32 v" + std::to_string(h) + ", 0")
@@ -3429,7 +3548,7 @@ struct Compiler {
         if (!names(ln[m], vh)) continue;
         bool clear = true;  // nothing between the move and the exec update names vH or is a label
         for (size_t q = k + 1; q <= x && clear; q++)
-          clear = !names(ln[q], vh) || q == m;
+          clear = !names(ln[q], vh) || ln[q][0] == ';';  // (markers are comments)
         for (size_t q = k + 1; q <= x && clear; q++) clear = ln[q].empty() || ln[q][0] != '.';
         if (!clear) continue;
         ln.insert(ln.begin() + x + 1, ln[k]);
@@ -3475,6 +3594,19 @@ struct Compiler {
             out.size() >= 2 && out.back() == ln[i - 1] && out[out.size() - 2] == ln[i - 2]) {
           out.resize(out.size() - 2);
           out.push_back("v_cmp_" + o + "_u32 vcc, " + k + ", v" + std::to_string(lo));
+          continue;
+        }
+      }
+      // `; hi0 vH` then `v_cmp_<op>_[iu]64 vcc, K, v[L:H]` with K an inline constant in [0, 64]
+      uint32_t kk;
+      if (i >= 1 && sscanf(ln[i - 1].c_str(), "; hi0 v%u", &h0) == 1 &&
+          sscanf(ln[i].c_str(), "v_cmp_%2[a-z]_%c64 vcc, %u, v[%u:%u]", op, &sg, &kk, &lo, &hi) == 5 &&
+          (sg == 'u' || sg == 'i') && hi == lo + 1 && hi == h0 && kk <= 64 &&
+          ln[i] == std::string("v_cmp_") + op + "_" + sg + "64 vcc, " + std::to_string(kk) + ", v[" +
+                       std::to_string(lo) + ":" + std::to_string(hi) + "]") {
+        const std::string o(op);
+        if (o == "eq" || o == "ne" || o == "gt" || o == "ge" || o == "lt" || o == "le") {
+          out.push_back("v_cmp_" + o + "_u32 vcc, " + std::to_string(kk) + ", v" + std::to_string(lo));
           continue;
         }
       }

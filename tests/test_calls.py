@@ -96,7 +96,8 @@ def test_call_programs_directed(cuda, oracle_mod):
 
     rng = random.Random(1)
     pkts = [gen_packet(rng) for _ in range(130)]
-    fwd = (_lib.EBPF_KERNEL_JIT_VAR, _lib.EBPF_KERNEL_JIT_VARL, _lib.EBPF_KERNEL_JIT_FIXED)
+    fwd = (_lib.EBPF_KERNEL_JIT_VAR, _lib.EBPF_KERNEL_JIT_VARL, _lib.EBPF_KERNEL_JIT_FIXED,
+           _lib.EBPF_KERNEL_JIT_FIXED_OCC)  # (flattened recursion: >= 96 micro-ops, the occ variant)
     for src, kern in ((NESTED, fwd), (RECURSE, fwd), (RECURSE_BIG, fwd),
                       (RECURSE_HUGE, (_lib.EBPF_KERNEL_GENERAL_T1,))):
         img = assemble(src)

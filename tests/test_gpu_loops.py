@@ -222,7 +222,8 @@ def test_fuzz_large_loop_programs(cuda, oracle_mod, seed):
         frames = torch.zeros(len(pkts) * 256, dtype=torch.uint8, device=cuda)
         k = p.batch_kernel(p.make_batch(frames, n=len(pkts), stride=256, max_steps=steps))
         assert k in (_lib.EBPF_KERNEL_JIT_LOOP, _lib.EBPF_KERNEL_JIT_FIXED,
-                     _lib.EBPF_KERNEL_JIT_VAR, _lib.EBPF_KERNEL_JIT_VARL), _lib.KERNEL_NAMES[k]
+                     _lib.EBPF_KERNEL_JIT_FIXED_OCC, _lib.EBPF_KERNEL_JIT_VAR,
+                     _lib.EBPF_KERNEL_JIT_VARL), _lib.KERNEL_NAMES[k]
         p.close()
         prod = _run_prod(img, pkts, cuda, max_steps=steps, **layout)
         _check_prod_against_oracle(oracle_mod, img, pkts, prod, max_steps=steps,

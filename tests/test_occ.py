@@ -69,6 +69,24 @@ def test_occ_code_in_its_registers():
         p.close()
 
 
+def test_pending_masks_in_rule_chains():
+    """jit.cpp pm_assign: in the fixed-slot statements (marker pm=1, s[72:79] clobbered), a
+    rule chain's lanes park in SGPR masks -- every rule's entry takes exec from its mask, no LPC
+    compare re-admits lanes -- and the code names no SGPR past s79."""
+    from ebpf_emu import Program
+    from ebpf_emu import workloads as W
+
+    p = Program(W.program("acl_rules"))
+    p.compile()
+    b = _occ_body(p.jit_asm(1))
+    entries = len(re.findall(r"^s_mov_b64 exec, s\[7[2-9]:7[3-9]\]$", b, re.M))
+    assert entries >= 128, entries  # (one per rule, in each copy)
+    assert not re.search(r"^v_cmpx_eq_u32 vcc, \d+, v28$", b, re.M)
+    sg = [int(x) for x in re.findall(r"(?<![\w.])s\[?(\d+)", b)]
+    assert max(sg) <= 79, max(sg)
+    p.close()
+
+
 def _frames(rng, n):
     from ebpf_emu import workloads as W
 
