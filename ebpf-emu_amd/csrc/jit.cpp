@@ -31,6 +31,7 @@
 #include <cctype>
 #include <cstring>
 #include <set>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -1038,13 +1039,13 @@ struct Compiler {
     std::string pre;
     const std::string mx = x_done ? "" : pm_reg(x), mn = n_done ? "" : pm_reg(np);
     if (n_next && !mx.empty())  // taken lanes leave into their target's mask
-      return "s_and_b64 vcc, vcc, exec\ns_or_b64 " + mx + ", " + mx + ", vcc\n"
+      return "s_or_b64 " + mx + ", " + mx + ", vcc\n"  // (a VOPC result: 0 in inactive lanes)
              "s_andn2_b64 exec, exec, vcc\n";
     if (x_next && !mn.empty())  // not-taken lanes leave into theirs
       return "s_andn2_b64 s[64:65], exec, vcc\ns_or_b64 " + mn + ", " + mn + ", s[64:65]\n"
              "s_and_b64 exec, exec, vcc\n";
     if (!n_next && !x_next && (!mx.empty() || !mn.empty())) {  // both leave, one or both masked
-      std::string s = "s_and_b64 vcc, vcc, exec\n";
+      std::string s;
       if (!mx.empty()) s += "s_or_b64 " + mx + ", " + mx + ", vcc\n";
       if (!mn.empty()) s += "s_andn2_b64 s[64:65], exec, vcc\ns_or_b64 " + mn + ", " + mn + ", s[64:65]\n";
       const std::string lx = mx.empty() ? vop3_lpc(lpc_of(x, x_done), "v37", pre) : "",
@@ -2420,10 +2421,12 @@ struct Compiler {
       if (start[i]) {
         main += ".L" + P + "b" + std::to_string(i) + ":\n";
         const std::string pm = pm_reg(i);
-        if (!pm.empty())  // (every lane parked here is in the mask)
-          main += (i > 0 && clears_exec(i - 1) ? "s_mov_b64 exec, " + pm + "\n"
-                                               : "s_or_b64 exec, exec, " + pm + "\n") +
-                  "s_mov_b64 " + pm + ", 0\n";
+        // (every lane parked here is in the mask; with exec empty, one instruction takes the mask
+        // into exec and clears it: mask = exec = 0, exec = old mask | 0)
+        if (!pm.empty())
+          main += i > 0 && clears_exec(i - 1)
+                      ? "s_or_saveexec_b64 " + pm + ", " + pm + "\n"
+                      : "s_or_b64 exec, exec, " + pm + "\ns_mov_b64 " + pm + ", 0\n";
         else if (target[i] && !loops && i > 0 && clears_exec(i - 1))  // (exec is empty here)
           main += "s_mov_b64 exec, -1\nv_cmpx_eq_u32 vcc, " + std::to_string(i) + ", v28\n";
         else if (target[i])
@@ -3470,7 +3473,7 @@ struct Compiler {
       }
       out += ln[i] + "\n";
     }
-    return sink_high_zero(narrow_compares(out));
+    return negate_leave(sink_high_zero(narrow_compares(out)));
   }
 
   // A register's high half zeroed just before a jump (`v_mov_b32 vH, 0` of a fused mov + and,
@@ -3478,6 +3481,46 @@ struct Compiler {
   // (the `; dead@leave` marker of jtail): the move goes after the jump's exec update, so only
   // the staying lanes run it -- in a rule chain, the rule's first test sends nearly every lane to
   // the next rule, which overwrites the register, and the move leaves the common path.
+  // A jump whose NOT-taken lanes leave into a pending mask (jtail_code: s[64:65] = exec & ~vcc,
+  // OR-ed into the mask, exec &= vcc) after a VOPC compare into vcc: the compare negated, so the
+  // leaving lanes are vcc and the mask takes them directly (two SALU instead of three).
+  static std::string negate_leave(const std::string& text) {
+    std::vector<std::string> ln;
+    for (size_t p = 0; p < text.size();) {
+      size_t e = text.find('\n', p);
+      if (e == std::string::npos) e = text.size();
+      ln.push_back(text.substr(p, e - p));
+      p = e + 1;
+    }
+    static const std::map<std::string, std::string> neg = {
+        {"eq", "ne"}, {"ne", "eq"}, {"gt", "le"}, {"le", "gt"}, {"ge", "lt"}, {"lt", "ge"}};
+    std::vector<std::string> out;
+    out.reserve(ln.size());
+    for (size_t i = 0; i < ln.size(); i++) {
+      char op[8], ty[8], pm[32];
+      if (i + 2 < ln.size() && ln[i] == "s_andn2_b64 s[64:65], exec, vcc" &&
+          sscanf(ln[i + 1].c_str(), "s_or_b64 %31[^,], ", pm) == 1 &&
+          ln[i + 1] == "s_or_b64 " + std::string(pm) + ", " + pm + ", s[64:65]" &&
+          std::string(pm).compare(0, 3, "s[7") == 0 && ln[i + 2] == "s_and_b64 exec, exec, vcc") {
+        size_t c = out.size();  // the compare: the last non-comment line before
+        while (c > 0 && !out[c - 1].empty() && out[c - 1][0] == ';') c--;
+        if (c > 0 && sscanf(out[c - 1].c_str(), "v_cmp_%2[a-z]_%3[a-z0-9] vcc, ", op, ty) == 2 &&
+            neg.count(op) && out[c - 1].find("_e64") == std::string::npos &&
+            out[c - 1].compare(0, 6 + strlen(op) + 1 + strlen(ty), std::string("v_cmp_") + op + "_" + ty) == 0) {
+          out[c - 1] = "v_cmp_" + neg.at(op) + out[c - 1].substr(6 + strlen(op));
+          out.push_back("s_or_b64 " + std::string(pm) + ", " + pm + ", vcc");
+          out.push_back("s_andn2_b64 exec, exec, vcc");
+          i += 2;
+          continue;
+        }
+      }
+      out.push_back(ln[i]);
+    }
+    std::string r;
+    for (const std::string& l : out) r += l + "\n";
+    return r;
+  }
+
   static std::string sink_high_zero(const std::string& text) {
     std::vector<std::string> ln;
     for (size_t p = 0; p < text.size();) {
@@ -3509,6 +3552,13 @@ struct Compiler {
       if (x >= ln.size() || x > m + 4 || (ln[x] != "s_and_b64 exec, exec, vcc" &&
                                           ln[x] != "s_andn2_b64 exec, exec, vcc"))
         continue;
+      // where the sunk code goes: after the exec update -- or, when the next line starts a block
+      // with no entry code (one predecessor, this fall-through) and its empty-exec skip, after
+      // that skip, so that a jump that sent every lane away skips it too
+      size_t ins = x + 1;
+      if (x + 2 < ln.size() && ln[x + 1].size() > 3 && ln[x + 1].compare(0, 2, ".L") == 0 &&
+          ln[x + 1].back() == ':' && ln[x + 2].compare(0, 16, "s_cbranch_execz ") == 0)
+        ins = x + 3;
       // `v_and_b32 vL, 0xff|0xffff, vS` + `v_cmp_<op>_u32 vcc, K, vL` right before the marker, the
       // register (vL, vL+1) dead where the leaving lanes go: the compare reads vS's low byte / half
       // itself (SDWA), and the and goes after the exec update with the high half's move
@@ -3532,12 +3582,24 @@ struct Compiler {
                   return false;
               return true;
             }()) {
-          const std::string sel = std::string(msk) == "0xff" ? "BYTE_0" : "WORD_0";
-          const std::string a = ln[ka];
-          ln[ka] = "s_mov_b32 s48, " + std::string(kv);
-          ln[m - 1] = std::string("v_cmp_") + op + "_u32_sdwa vcc, s48, v" + std::to_string(S) +
-                      " src0_sel:DWORD src1_sel:" + sel;
-          ln.insert(ln.begin() + x + 1, a);
+          // the low half: a 16-bit compare with K as its literal; the low byte: SDWA, whose
+          // operands take inline constants but no literal (a larger K keeps the and)
+          char* ke = nullptr;
+          const unsigned long kn = strtoul(kv, &ke, 0);
+          const bool kok = ke && *ke == 0 && kv[0] != '-';
+          std::string cmp;
+          if (kok && std::string(msk) == "0xffff" && kn <= 0xffff)
+            cmp = std::string("v_cmp_") + op + "_u16 vcc, " + kv + ", v" + std::to_string(S);
+          else if (kok && std::string(msk) == "0xff" && kn <= 64)
+            cmp = std::string("v_cmp_") + op + "_u32_sdwa vcc, " + kv + ", v" + std::to_string(S) +
+                  " src0_sel:DWORD src1_sel:BYTE_0";
+          if (!cmp.empty()) {
+            const std::string a = ln[ka];
+            ln.erase(ln.begin() + ka);
+            m--, x--, ins--;
+            ln[m - 1] = cmp;
+            ln.insert(ln.begin() + ins, a);
+          }
         }
       }
       for (size_t k = m; k-- > 0 && k + 6 > m;) {
@@ -3551,10 +3613,11 @@ struct Compiler {
           clear = !names(ln[q], vh) || ln[q][0] == ';';  // (markers are comments)
         for (size_t q = k + 1; q <= x && clear; q++) clear = ln[q].empty() || ln[q][0] != '.';
         if (!clear) continue;
-        ln.insert(ln.begin() + x + 1, ln[k]);
+        ln.insert(ln.begin() + ins, ln[k]);
         ln.erase(ln.begin() + k);
         m--;
         x--;
+        ins--;
       }
     }
     std::string r;

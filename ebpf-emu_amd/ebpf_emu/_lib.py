@@ -32,7 +32,7 @@ MAX_CALL_DEPTH = 64
 (EBPF_KERNEL_GENERAL_T0, EBPF_KERNEL_GENERAL_T1, EBPF_KERNEL_DAG, EBPF_KERNEL_TILE,
  EBPF_KERNEL_TILE_LOOP, EBPF_KERNEL_JIT_FIXED, EBPF_KERNEL_JIT_VAR, EBPF_KERNEL_JIT_LOOP,
  EBPF_KERNEL_JIT_STACK, EBPF_KERNEL_JIT_VAR_STACK, EBPF_KERNEL_JIT_LOOP_STACK,
- EBPF_KERNEL_JIT_VARL, EBPF_KERNEL_JIT_VARL_STACK) = range(13)
+ EBPF_KERNEL_JIT_VARL, EBPF_KERNEL_JIT_VARL_STACK, EBPF_KERNEL_JIT_FIXED_OCC) = range(14)
 KERNEL_NAMES = ["ebpfemu::interp_kernel<0>", "ebpfemu::interp_kernel<1>", "ebpfemu::dag_kernel",
                 "ebpfemu::tile_kernel<forward>", "ebpfemu::tile_kernel<loops>",
                 "ebpf_tile_jit_fixed (compiled program)", "ebpf_tile_jit_var (compiled program)",

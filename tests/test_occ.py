@@ -79,7 +79,7 @@ def test_pending_masks_in_rule_chains():
     p = Program(W.program("acl_rules"))
     p.compile()
     b = _occ_body(p.jit_asm(1))
-    entries = len(re.findall(r"^s_mov_b64 exec, s\[7[2-9]:7[3-9]\]$", b, re.M))
+    entries = len(re.findall(r"^s_or_saveexec_b64 (s\[7[2-9]:7[3-9]\]), \1$", b, re.M))
     assert entries >= 128, entries  # (one per rule, in each copy)
     assert not re.search(r"^v_cmpx_eq_u32 vcc, \d+, v28$", b, re.M)
     sg = [int(x) for x in re.findall(r"(?<![\w.])s\[?(\d+)", b)]

@@ -10,6 +10,15 @@ mkdir -p "$out"
 cd "$root"
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
   --durations=25 > "$out/suite.log" 2>&1
+# A/B against the build of the previous commit in abA/ (the pending masks, the compare rewrites)
+for rep in 1 2; do
+  for cfg in acl_rules acl 5tuple; do
+    for pkg in ebpf-emu_amd abA/ebpf-emu_amd; do
+      echo "$pkg $cfg" >> "$out/ab.log"
+      timeout -k 10 120 python3 tools/ab_lib.py "$pkg" --fixed --config $cfg --steps 200 >> "$out/ab.log" 2>> "$out/ab.err"
+    done
+  done
+done
 b() {  # tag, bench args
   local tag="$1"; shift
   timeout -k 10 200 python -u bench.py --cpu-seconds 0 "$@" > "$out/$tag.json" 2> "$out/$tag.err"
