@@ -296,6 +296,69 @@ static const bool g_fail_stack_jit = [] {
   return e && e[0] == '1';
 }();
 
+// The compiled variants of recently compiled programs: a program loaded again (the same
+// instructions, the same compile-time switches) takes copies of them instead of compiling.
+// Bounded by the code objects' bytes (oldest out first).
+struct JitRes {
+  bool ok = false, deep = false, occ = false;
+  std::string err, text;
+  std::vector<char> co;
+};
+struct JitCacheEnt {
+  std::string key;
+  std::vector<JitRes> r;
+  size_t bytes = 0;
+};
+static constexpr size_t kJitCacheBytes = 96u << 20;
+static std::mutex g_jit_cache_mu;
+static std::vector<JitCacheEnt> g_jit_cache;  // oldest first
+static size_t g_jit_cache_bytes = 0;
+
+static std::string jit_cache_key(const ebpf_prog* p) {
+  std::string k;
+  k.reserve(p->insns.size() * 16 + 16);
+  for (const RefInsn& i : p->insns) {
+    char b[16];
+    std::memcpy(b, &i.imm64, 8);  // (imm is imm64's low half)
+    std::memcpy(b + 8, &i.imm, 4);
+    std::memcpy(b + 12, &i.off, 2);
+    b[14] = (char)i.code;
+    b[15] = (char)(i.dst | (i.src << 4));
+    k.append(b, 16);
+  }
+  for (int v = 0; v < kJitVariants; v++) k += p->jit_has[v] ? '1' : '0';
+  const char* e = getenv("EBPFEMU_FIXED_OCC");
+  k += std::string("|") + (e ? e : "-") + (g_fail_stack_jit ? "F" : "");
+  return k;
+}
+
+static bool jit_cache_get(const std::string& key, JitRes* r) {
+  std::lock_guard<std::mutex> g(g_jit_cache_mu);
+  for (const JitCacheEnt& c : g_jit_cache)
+    if (c.key == key) {
+      for (int v = 0; v < kJitVariants; v++) r[v] = c.r[v];
+      return true;
+    }
+  return false;
+}
+
+static void jit_cache_put(const std::string& key, const JitRes* r) {
+  JitCacheEnt c;
+  c.key = key;
+  c.r.assign(r, r + kJitVariants);
+  for (const JitRes& q : c.r) c.bytes += q.co.size() + q.text.size();
+  if (c.bytes > kJitCacheBytes / 4) return;
+  std::lock_guard<std::mutex> g(g_jit_cache_mu);
+  for (const JitCacheEnt& o : g_jit_cache)
+    if (o.key == key) return;
+  while (!g_jit_cache.empty() && g_jit_cache_bytes + c.bytes > kJitCacheBytes) {
+    g_jit_cache_bytes -= g_jit_cache.front().bytes;
+    g_jit_cache.erase(g_jit_cache.begin());
+  }
+  g_jit_cache_bytes += c.bytes;
+  g_jit_cache.push_back(std::move(c));
+}
+
 // Compile both table variants (caller holds p->mu). Returns the C ABI code of ebpf_prog_compile.
 static int jit_compile_locked(ebpf_prog* p) {
   if (p->jit_state == 0) {
@@ -320,17 +383,14 @@ static int jit_compile_locked(ebpf_prog* p) {
       p->jit_state = 1;
       // the variants are independent compiles (own Compiler, own code object; the program's
       // tables are read-only here): all at once, one thread each, then their results in order
-      struct Res {
-        bool ok = false, deep = false, occ = false;
-        std::string err, text;
-        std::vector<char> co;
-      };
-      Res r[kJitVariants];
+      JitRes r[kJitVariants];
+      const std::string key = jit_cache_key(p);
+      const bool cached = jit_cache_get(key, r);
       std::vector<std::thread> th;
-      for (int v = 0; v < kJitVariants; v++) {
+      for (int v = 0; v < kJitVariants && !cached; v++) {
         if (!p->jit_has[v]) continue;
         th.emplace_back([p, v, &r] {
-          Res& q = r[v];
+          JitRes& q = r[v];
           if (v == 5 || v == 6)
             q.ok = jit_compile_loop(p->xuops, p->ltuops, p->ltuopsx, q.co, &q.err, &q.text, nullptr,
                                     &q.deep, 0, true, v == 6);
@@ -347,6 +407,7 @@ static int jit_compile_locked(ebpf_prog* p) {
         });
       }
       for (std::thread& t : th) t.join();
+      if (!cached) jit_cache_put(key, r);
       auto take = [&](int v) {
         p->jit_co[v] = std::move(r[v].co);
         p->jit_asm[v] = std::move(r[v].text);
