@@ -50,8 +50,9 @@ constexpr size_t kIslandLines = 3000;
 // far mode: a block entry's empty-exec skip past more micro-ops than this is a long jump
 constexpr uint32_t kFarSkipUops = 48;
 // forward programs of at least this many micro-ops get the fixed-slot kernel's occupancy variant
-// (occ_wanted)
-constexpr uint32_t kOccMinUops = 96;
+// (occ_wanted). 96 until late round 6; 0 since: with two streams its smaller workgroups overlap
+// consecutive launches better, the 5-tuple 98 -> 106 Gpkt/s (profiles/r06_occ_short_programs.log)
+constexpr uint32_t kOccMinUops = 0;
 // store mode's overflow image covers image bytes [64, min(mem_size rounded up to 64, this))
 // (jit.h kOvfEnd)
 
@@ -3797,9 +3798,9 @@ bool occ_regs_ok(const std::string& b) {
 }
 
 // Programs the occupancy variant of the fixed-slot kernel takes (host.cpp routes their
-// fixed-slot batches there): issue-bound ones, judged by length -- a long program's rule chain
-// retires hundreds of steps per packet for the same 64 bytes of HBM. EBPFEMU_FIXED_OCC=0|1 (A/B)
-// turns it off / on for every program it can take.
+// fixed-slot batches there): every forward program it can take (kOccMinUops) -- first meant for
+// issue-bound rule chains, it also runs short programs faster when launches overlap (two
+// streams). EBPFEMU_FIXED_OCC=0|1 (A/B) turns it off / on for every program it can take.
 bool occ_wanted(uint32_t n_uops) {
   static const int force = [] {
     const char* e = getenv("EBPFEMU_FIXED_OCC");

@@ -6,8 +6,8 @@ VGPRs), too few to hide the min-pc scheme's exec / vcc dependency chains. The va
 window buffer per wave (the next tile is claimed and DMA'd when the current one is done,
 gen_tile.py jit_statement_loop(single=True)) and compiles the program without the preloaded
 window (only v[0:55]), so 3 workgroups of 8 waves fit a CU: 6 waves per SIMD.
-Programs of >= 96 micro-ops take it (jit.cpp occ_wanted) when their code fits its registers
-(occ_regs_ok). The reference runs every program through one step() (emu.rs:452-458): outputs
+Every forward program takes it (jit.cpp occ_wanted; programs of >= 96 micro-ops only until late in
+round 6) when its code fits the registers (occ_regs_ok) and the batch is not xdp_md. The reference runs every program through one step() (emu.rs:452-458): outputs
 must not change, only the kernel.
 
 CPU: which programs get the variant's code, and that the code names only the statement's
@@ -39,11 +39,11 @@ def _occ_body(text):
     return head
 
 
-def test_occ_routing_by_length():
+def test_occ_routing():
     from ebpf_emu import Program
     from ebpf_emu import workloads as W
 
-    for name, want in (("acl_rules", True), ("acl", True), ("5tuple", False), ("drop", False),
+    for name, want in (("acl_rules", True), ("acl", True), ("5tuple", True), ("drop", True),
                        ("nat", False), ("5tuple_stack", False)):
         p = Program(W.program(name))
         assert p.compile(), name

@@ -196,9 +196,7 @@ def test_varl_workloads_vs_fixed(cuda, oracle_mod, name):
     _vs_oracle_batch(oracle_mod, W.program(name), buf, n, ref, f"{name} fixed", stride=64)
     stack = name in ("5tuple_stack", "mac_swap_tx")  # (memory tier 0.5: the stack statements)
     assert _route(prog, fr, dict(n=n, stride=64)) == (
-        _lib.EBPF_KERNEL_JIT_STACK if stack
-        else _lib.EBPF_KERNEL_JIT_FIXED_OCC if name == "acl"  # (>= 96 micro-ops, test_occ.py)
-        else _lib.EBPF_KERNEL_JIT_FIXED)
+        _lib.EBPF_KERNEL_JIT_STACK if stack else _lib.EBPF_KERNEL_JIT_FIXED_OCC)  # (test_occ.py)
     # the same frames at offsets: slots of 80 bytes, packet i at 80 i (+3 for some)
     slot = 80
     big = np.zeros((n, slot), dtype=np.uint8)
