@@ -1736,6 +1736,7 @@ static bool xdp_in_place(ebpf_prog* p, const ebpf_batch* b, bool mem_out, int de
   a.stride = b->stride;
   a.n_tiles = (b->n + 63) / 64;
   a.mem_out = mem_out ? (uint8_t*)16 : nullptr;
+  a.xdp = 1;  // (the route of an xdp_md batch in place: not the occupancy variant)
   const int id = launch_kernel_id(kind, a, batch_jit(p, b, kind, stk, device), stk);
   return id == EBPF_KERNEL_JIT_FIXED || id == EBPF_KERNEL_JIT_VAR ||
          id == EBPF_KERNEL_JIT_STACK || id == EBPF_KERNEL_JIT_VAR_STACK ||
