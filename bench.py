@@ -67,6 +67,10 @@ CONFIGS = {
     # xdp_md batch: staged images, compiled with the staged ctx known -- DESIGN 3.17)
     "checksum_xdp": (4, "per-byte checksum as a standard XDP program (xdp_md ctx) over 1Mi mixed "
                         "64B/1500B frames"),
+    # the same with ctx->data_end reloaded in every iteration (the loop reads the ctx: in place
+    # through the loop kernels' ctx-aware refills -- DESIGN 3.17, 3.29)
+    "checksum_xdp_reload": (4, "per-byte checksum as an XDP program reloading ctx->data_end every "
+                               "iteration over 1Mi mixed 64B/1500B frames"),
     # a long program: a 128-rule firewall chain (workloads.acl_rules_source, 1013 insns, ~297 run
     # per packet) -- compiled past the near-branch reach (jit.cpp far mode); issue-bound, not HBM
     "acl_rules": (2, "IPv4 rule-table firewall, 128 rules (1013 insns, ~297 executed per packet) "
@@ -80,6 +84,8 @@ CONFIGS = {
 }
 PROGRAM_OF = {"stack": "5tuple_stack", "tier1": "mac_swap_tx", "xdp": "5tuple_xdp",
               "call": "5tuple_call"}
+MIXED_CONFIGS = ("checksum", "checksum_stack", "checksum_xdp", "checksum_xdp_reload")
+XDP_CONFIGS = ("xdp", "checksum_xdp", "checksum_xdp_reload")
 
 
 def parse():
@@ -230,7 +236,7 @@ def stub_rank(args, world, rank):
         sys.exit(3)
     dist.init_process_group("gloo")
     prog_name = PROGRAM_OF.get(args.config, args.config)
-    mixed = args.config in ("checksum", "checksum_stack", "checksum_xdp")
+    mixed = args.config in MIXED_CONFIGS
     if args.total_packets:
         return stub_rank_strong(args, world, rank)
     with open(PIN_FIXTURE) as f:
@@ -359,7 +365,7 @@ def main():
     if args.layout != "fixed":
         desc += " (offsets + lens batch)" if args.layout == "offsets" else \
             " (a pcap capture indexed in place: offsets + lens into the capture)"
-        assert not args.total_packets and args.config not in ("checksum", "checksum_stack", "checksum_xdp")
+        assert not args.total_packets and args.config not in MIXED_CONFIGS
     n = args.packets
     img = W.program(PROGRAM_OF.get(args.config, args.config))
     prog = Program(img)
@@ -368,7 +374,7 @@ def main():
     # ---- synthetic device-resident batches ----
     from ebpf_emu import dist as D
 
-    mixed = args.config in ("checksum", "checksum_stack", "checksum_xdp")
+    mixed = args.config in MIXED_CONFIGS
     fb = (max(64, args.frame_bytes) + 15) // 16 * 16  # fixed slots: 16-byte aligned, >= 64
     batches = []
     pool_bytes = 0
@@ -449,11 +455,11 @@ def main():
         if mixed:
             bd = prog.make_batch(b["frames"], n=n, offsets=b["offsets"], lens=b["lens"],
                                  mem_size=mem_size, r10=r10, generic=args.generic,
-                                 xdp_md=args.config == "checksum_xdp")
+                                 xdp_md=args.config in XDP_CONFIGS)
         else:
             bd = prog.make_batch(b["frames"], n=n, stride=fb, offsets=b.get("offsets"),
                                  lens=b.get("lens"), mem_size=mem_size, r10=r10,
-                                 generic=args.generic, xdp_md=args.config == "xdp")
+                                 generic=args.generic, xdp_md=args.config in XDP_CONFIGS)
         descs.append(bd)
     # S streams (--streams): step i runs on stream i mod S with that stream's own workspace
     # (counter shards, zeroed once) and verdict buffer; every launch adds into the one counters
@@ -815,7 +821,7 @@ def cpu_baseline(args, img, batch0, mixed, n, mem_size, r10):
 
     def rate(nthreads, seconds):
         kw = dict(mem_size=mem_size, r10=r10, threads=nthreads,
-                  xdp_md=args.config in ("xdp", "checksum_xdp"))
+                  xdp_md=args.config in XDP_CONFIGS)
         # chunks sized to ~0.2 s of work so the time budget is met closely
         chunk = max(4096, min(n, int((1 << 14 if mixed else 1 << 20) * nthreads / 8)))
         done = 0

@@ -108,6 +108,27 @@ done:
     exit
 """
 
+# CHECKSUM_XDP with ctx->data_end reloaded in every iteration (a loop that reads the ctx: run in
+# place, its refilled windows carry the synthesised ctx -- jit.cpp ctx_load). Same verdicts.
+CHECKSUM_XDP_RELOAD = """
+    ldxw r2, [r1+0]           # ctx->data
+    mov r0, 0
+loop:
+    ldxw r3, [r1+4]           # ctx->data_end, every iteration
+    jge r2, r3, done
+    ldxb r5, [r2+0]
+    add r0, r5
+    add r2, 1
+    ja loop
+done:
+    mov r6, r0
+    rsh r6, 8
+    xor r0, r6
+    and r0, 1
+    add r0, 1                 # DROP (1) or PASS (2) by parity
+    exit
+"""
+
 # config 5 with its running sum kept in a stack slot (r10 - 8) instead of a register, the way
 # compiled C keeps a spilled accumulator: memory tier 0.5 with a loop (the loop kernel's stack
 # variant). Same verdicts as CHECKSUM.
@@ -583,6 +604,7 @@ PROGRAMS = {"drop": DROP_ALL, "5tuple": FIVE_TUPLE, "checksum": CHECKSUM,
             "5tuple_stack": FIVE_TUPLE_STACK, "mac_swap_tx": MAC_SWAP_TX, "acl": ACL,
             "5tuple_xdp": FIVE_TUPLE_XDP, "checksum_stack": CHECKSUM_STACK,
             "5tuple_call": FIVE_TUPLE_CALL, "nat": NAT_REWRITE, "checksum_xdp": CHECKSUM_XDP,
+            "checksum_xdp_reload": CHECKSUM_XDP_RELOAD,
             "responder": RESPONDER}
 
 

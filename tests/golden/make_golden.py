@@ -119,7 +119,8 @@ PIN_CHUNKS_64 = 128  # 16 pool batches x 8 ranks
 PIN_CHUNKS_MIXED = 16  # 2 pool batches x 8 ranks (a 1 Mi mixed batch is ~840 MB: one per rank)
 PIN_PROGRAMS_64 = ("5tuple", "drop", "5tuple_stack", "mac_swap_tx", "acl", "5tuple_xdp",
                    "5tuple_call", "nat", "acl_rules", "responder")
-PIN_PROGRAMS_MIXED = ("checksum", "checksum_stack", "checksum_xdp")
+PIN_PROGRAMS_MIXED = ("checksum", "checksum_stack", "checksum_xdp", "checksum_xdp_reload")
+XDP_PROGRAMS = ("5tuple_xdp", "checksum_xdp", "checksum_xdp_reload")
 # 1504-byte slots (bench.py --frame-bytes 1504: rank r's pool is copies of chunk r,
 # workloads.frames_fixed(1Mi, 1504, config_id=3 + 100r), mem_size = r10 = 2048)
 PIN_CHUNKS_1504 = 8
@@ -143,7 +144,7 @@ def _pin_chunk(args):
         for name in PIN_PROGRAMS_MIXED:
             p = oracle.Program(W.program(name))
             _, _, cnt = p.run_batch(buf, D.CHUNK, offsets=offs, lens=lens, mem_size=2048,
-                                    r10=2048, threads=1, xdp_md=name == "checksum_xdp")
+                                    r10=2048, threads=1, xdp_md=name in XDP_PROGRAMS)
             out[name] = [int(x) for x in cnt]
     return kind, c, out
 
@@ -197,7 +198,7 @@ def bench_pins_add(names):
         mixed = name in mixed_names
         rows = sorted((c, o[name]) for kind, c, o in res if (kind == "mixed") == mixed)
         pins["programs"][name] = {"frames": "mixed" if mixed else "fixed64",
-                                  "xdp_md": name in ("5tuple_xdp", "checksum_xdp"),
+                                  "xdp_md": name in XDP_PROGRAMS,
                                   "program": W.program(name).hex(),
                                   "mem_size": 2048 if mixed else 1024,
                                   "r10": 2048 if mixed else 512,
@@ -221,7 +222,7 @@ def bench_pins():
         for _, cnt in rows:
             assert sum(cnt[:7]) == D.CHUNK
         progs[name] = {"frames": "mixed" if mixed else "fixed64",
-                       "xdp_md": name in ("5tuple_xdp", "checksum_xdp"),
+                       "xdp_md": name in XDP_PROGRAMS,
                        "program": W.program(name).hex(),
                        "mem_size": 2048 if mixed else 1024, "r10": 2048 if mixed else 512,
                        "chunk_counters": [cnt for _, cnt in rows]}

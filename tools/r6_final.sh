@@ -17,12 +17,12 @@ b() {  # tag, bench args
   timeout -k 10 300 python -u bench.py "$@" >> "$out/$tag.jsonl" 2>> "$out/$tag.err"
 }
 b default
-for cfg in 5tuple drop stack tier1 acl xdp call nat acl_rules checksum checksum_stack checksum_xdp; do
+for cfg in 5tuple drop stack tier1 acl xdp call nat acl_rules checksum checksum_stack checksum_xdp checksum_xdp_reload; do
   b all --config $cfg --cpu-seconds 0
 done
 b all --config responder --frame-bytes 1504 --cpu-seconds 0
 for i in 1 2 3; do b driver20 --steps 20 --warmup 5; done
-for cfg in 5tuple acl_rules nat; do b s1 --config $cfg --streams 1 --cpu-seconds 0; done
+for cfg in 5tuple acl_rules nat checksum_xdp_reload; do b s1 --config $cfg --streams 1 --cpu-seconds 0; done
 bash tools/prof.sh r6_5tuple_occ_s1 --config 5tuple --steps 200 --warmup 20
 bash tools/pmc.sh 5tuple_occ --config 5tuple --streams 1
 python3 tools/pmc_summary.py gpurun_out/pmc/5tuple_occ ebpf_tile_jit_fixed_occ > gpurun_out/pmc/5tuple_occ.json
