@@ -46,7 +46,8 @@ def test_workloads_compile():
         # variant unless they store into the packet; the ACL, past 62 micro-ops: the forward
         # kernels only, budgets that bind run dag_kernel / interp_kernel)
         # (the NAT rewrite and the responder store through a register: store mode, variant 1 only)
-        variants = ((2,) if name in ("checksum", "checksum_stack", "checksum_xdp")
+        variants = ((2,) if name in ("checksum", "checksum_stack", "checksum_xdp",
+                                     "checksum_xdp_reload")
                     else (1,) if name in ("mac_swap_tx", "nat", "responder")
                     else (1, 2) if name == "5tuple_stack" else (0, 1) if name == "acl"
                     else (0, 1, 2))
