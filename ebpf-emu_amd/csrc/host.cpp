@@ -2045,6 +2045,7 @@ int ebpf_batch_kernel(ebpf_prog* p, const ebpf_batch* bin, const ebpf_batch_out*
   a.lens = staged.lens;
   a.stride = staged.stride;
   a.mem_out = out->mem;
+  a.xdp = (staged.flags & EBPF_BATCH_XDP_MD) && !rb ? 1u : 0u;  // (in place: as ebpf_run_batch)
   return launch_kernel_id(kind, a, rb ? &p->jit_fn[device][6] : batch_jit(p, &staged, kind, stk, device),
                           stk);
 }

@@ -8,7 +8,11 @@
  * reference's process-killing panics.
  *
  * Threading: a loaded program is immutable and may be shared across host threads and
- * devices. Batch launches are asynchronous and ordered on the caller's HIP stream.
+ * devices. Batch launches are asynchronous and ordered on the caller's HIP stream. The library's
+ * per-(device, stream) workspace (counter shards, the deopt list, the overflow images) is found
+ * and grown under a lock and never freed while the library is loaded, so host threads may launch
+ * concurrently; but launches on the SAME stream from two threads must be ordered by the caller
+ * (as any work on one HIP stream): the workspace is reused by every launch on that stream.
  */
 #ifndef EBPF_EMU_H
 #define EBPF_EMU_H
