@@ -1322,6 +1322,47 @@ s_branch .Ld{tag}%=
     return main, ool
 
 
+# The fixed-slot statement's store mode (marker st=1, jit.cpp body_store): lanes that left for the
+# general interpreter (status 0x80, jit.h kStDeopt) produce nothing here; their packet indices go
+# to the deopt list (one returning atomic per wave) -- or, with no pass to follow (%[dfl] bit 1,
+# StackPlan::no_deopt), they fault EBPF_ST_JIT. Other programs: one compare and branch per tile.
+STORE_DEOPT_FIXED = """s_mov_b64 exec, {VM}
+v_cmp_eq_u32 vcc, 0x80, {ST}
+s_cbranch_vccz .Lnodo%=
+s_bitcmp1_b32 %[dfl], 1
+s_cbranch_scc1 .Ldofail%=
+s_andn2_b64 {VM}, {VM}, vcc
+s_mov_b64 {T0}, vcc
+s_mov_b64 exec, vcc
+v_mbcnt_lo_u32_b32 {t5}, {T0L}, 0
+v_mbcnt_hi_u32_b32 {t5}, {T0H}, {t5}
+s_bcnt1_i32_b64 {T3}, {T0}
+s_ff1_i32_b64 {T1L}, {T0}
+s_lshl_b64 {T1}, 1, {T1L}
+s_mov_b64 exec, {T1}
+v_mov_b32 {t6}, {T3}
+v_mov_b64 {T89}, %[k_deopt]
+global_atomic_add {t4}, {T89}, {t6}, off sc0
+s_waitcnt vmcnt(0)
+v_readfirstlane_b32 {T3}, {t4}
+s_mov_b64 exec, {T0}
+v_add_u32 {t10}, {T3}, {t5}
+v_mov_b32 {t11}, 0
+v_lshlrev_b64 {T1011}, 2, {T1011}
+v_lshl_add_u64 {T89}, {T1011}, 0, %[k_dix]
+s_lshl_b32 {T1L}, %[tile], 6
+v_mbcnt_lo_u32_b32 {t4}, -1, 0
+v_mbcnt_hi_u32_b32 {t4}, -1, {t4}
+v_add_u32 {t4}, {T1L}, {t4}
+global_store_dword {T89}, {t4}, off
+s_branch .Lnodo%=
+.Ldofail%=:
+s_mov_b64 exec, vcc
+v_mov_b32 {ST}, 8
+.Lnodo%=:
+"""
+
+
 def jit_statement_loop(single=False):
     """single: the occupancy variant (ebpf_tile_jit_fixed_occ) -- one window buffer per wave, so
     the next tile is claimed and its windows DMA'd only once this tile's code is done with the
@@ -1385,10 +1426,11 @@ s_cbranch_scc1 .Linitx%=
 ;@@JITINIT@@
 .Linitd%=:
 
-; JIT N=%= fixed=%[fixed] loops=%[loops] aligned=%[aligned] xdp=%[xdpf] pm=1""" + (" occ=1" if single else "") + """
+; JIT N=%= fixed=%[fixed] loops=%[loops] aligned=%[aligned] xdp=%[xdpf] pm=1""" + (
+        " occ=1" if single else " st=1 ovf=%[k_ovf] tile=%[tile] dm=s[78:79]") + """
 ;@@JIT@@
 .Ldone%=:
-; verdict byte, the lane's counter bucket (verdict 0..4, 0xfe -> 5, 0xff -> 6) into %[acc]
+""" + ("" if single else STORE_DEOPT_FIXED) + """; verdict byte, the lane's counter bucket (verdict 0..4, 0xfe -> 5, 0xff -> 6) into %[acc]
 s_mov_b64 exec, {VM}
 v_cmp_gt_u64 vcc, 5, {RF}
 v_mov_b32 {t5}, 0xfe

@@ -1541,7 +1541,8 @@ int ebpf_prog_upload(ebpf_prog* p, int device) {
         else if ((v == 2 && p->jit_deep) || (v == 4 && p->pjit_deep) ||
                  (v == 5 && p->xjit_deep) || (v == 6 && p->rjit_deep))  // (the code is in the
           p->jit_fn[device][v].loop = p->jit_fn[device][v].loop_deep;     // deep-prefetch kernel)
-        p->jit_fn[device][v].var_only = p->stack.any_dyn;
+        // (store mode runs on the fixed-slot statement too since round 6: gen_tile.py st=1)
+        p->jit_fn[device][v].var_only = false;
         if (!p->jit_occ[v]) p->jit_fn[device][v].fixed_occ = nullptr;
       }
   }
@@ -1977,7 +1978,8 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* bin, const ebpf_batch_out* ou
   // (the promoted program: lanes whose packet reaches the slots, jit.cpp promo_guard)
   const int kid = jit ? launch_kernel_id(kind, a, jit, stk) : -1;
   const bool deopt = (stk && p->stack.any_dyn && kind == kKindDag && jit &&
-                      (kid == EBPF_KERNEL_JIT_VAR_STACK || kid == EBPF_KERNEL_JIT_VARL_STACK)) ||
+                      (kid == EBPF_KERNEL_JIT_VAR_STACK || kid == EBPF_KERNEL_JIT_VARL_STACK ||
+                       kid == EBPF_KERNEL_JIT_STACK)) ||
                      (promo && jit);
   // store mode on the var tile loop with no lane able to leave (StackPlan::no_deopt: the main.rs
   // registers, the stack window at or past the overflow image's end): no deopt pass
@@ -1987,7 +1989,8 @@ int ebpf_run_batch(ebpf_prog* p, const ebpf_batch* bin, const ebpf_batch_out* ou
   const uint64_t len_max = std::min<uint64_t>(
       b->mem_size, !b->lens && !b->offsets ? b->stride + (a.xdp ? 8 : 0) : b->mem_size);
   // (a store ending past mem_size faults before it could deoptimize: bounded by mem_size too)
-  const bool pass = deopt && !(kid == EBPF_KERNEL_JIT_VARL_STACK && p->stack.no_deopt &&
+  const bool pass = deopt && !((kid == EBPF_KERNEL_JIT_VARL_STACK || kid == EBPF_KERNEL_JIT_STACK) &&
+                               p->stack.no_deopt &&
                                !b->init_regs &&
                                s0 >= std::min<uint64_t>(p->stack.st_bound, b->mem_size) &&
                                (!p->stack.len_bound ||

@@ -1941,9 +1941,12 @@ __device__ __forceinline__ void fixed_body(LaunchArgs& a) {
           FIXED_OPERANDS
           : TILE_ASM_CLOBBER, TILE_ASM_CLOBBER_PM);
     } else {
+      // (+ store mode's deopt list and overflow images: gen_tile.py STORE_DEOPT_FIXED)
+      const uint32_t dfl = rfl((a.deopt ? 1u : 0u) | (a.deopt_pass == 2 ? 2u : 0u));
       asm volatile(
 #include "tile_jit_loop.inc"
-          FIXED_OPERANDS
+          FIXED_OPERANDS, [k_deopt] "s"(a.deopt), [k_dix] "s"(a.deopt_idx), [k_ovf] "s"(a.ovf),
+          [dfl] "s"(dfl)
           : TILE_ASM_CLOBBER, TILE_ASM_CLOBBER_WINDOW, TILE_ASM_CLOBBER_PM);
     }
 #undef FIXED_OPERANDS

@@ -69,6 +69,7 @@ struct Marker {
   bool occ = false;    // the fixed-slot kernel's occupancy variant (ebpf_tile_jit_fixed_occ): no
                        // preloaded window, only v[0:55] for the program's code
   bool pm = false;     // the statement gives the body s[72:79] (the pending masks, pm_assign)
+  bool st = false;     // the fixed-slot statement's store mode (body_store, with ovf / tile / dm)
   bool varl = false;   // the var tile loop's statement (ebpf_tile_jit_varl): the var flavour of
                        // loads with the preloaded window, as the stack statement's
   // the var tile loop's store-mode state (gen_tile.py jit_statement_varl): the SGPR pair of
@@ -121,6 +122,7 @@ bool find_markers(const std::string& s, std::vector<Marker>& out) {
     m.varl = field("varl=") == "1";
     m.occ = field("occ=") == "1";
     m.pm = field("pm=") == "1";
+    m.st = field(" st=") == "1";
     m.ovf = field("ovf=");
     m.tile = field("tile=");
     m.dm = field("dm=");
@@ -914,6 +916,7 @@ struct Compiler {
   // constant-address load and packet-window store ending inside the window (loads past it read
   // HBM directly), at least one. The fixed-slot kernel's window DMA moves only those chunks.
   uint32_t window_chunks() const {
+    if (stk && stk->any_dyn) return 4;  // (store mode reads and writes the whole window)
     uint32_t maxend = 0;
     for (uint32_t i = 0; i < n; i++) {
       const uint32_t id = t[i].hoff / TILE_SLOT;
@@ -1652,15 +1655,16 @@ struct Compiler {
     // (the var tile loop's statement: stores past byte 64 into the overflow image)
     ovf_lo = ovf_hi = tile_s = dm = "";
     unsigned a0 = 0, a1 = 0;
-    if (m.varl && m.stack && !m.tile.empty() && !m.dm.empty() &&
+    if (((m.varl && m.stack) || m.st) && !m.tile.empty() && !m.dm.empty() &&
         sscanf(m.ovf.c_str(), "s[%u:%u]", &a0, &a1) == 2 && a1 == a0 + 1) {
       ovf_lo = "s" + std::to_string(a0);
       ovf_hi = "s" + std::to_string(a1);
       tile_s = m.tile;
       dm = m.dm;
     }
-    if (!m.stack) {
-      out = "s_mov_b64 exec, 0  ; (store mode: the var kernel's stack statement only)\n";
+    if (!m.stack && !m.st) {
+      out = "s_mov_b64 exec, 0  ; (store mode: the var kernels' stack statements and the "
+            "fixed-slot statement only)\n";
       return true;
     }
     std::string ool;
@@ -1672,7 +1676,7 @@ struct Compiler {
               "v_mov_b32 v23, 0\ns_mov_b64 exec, s[64:65]\n";
     // (the var tile loop's windows hold packet bytes [0, 64): the xdp_md ctx shifted in first, as
     // body does; the var kernel's C++ shifts them itself)
-    if (m.varl && !m.xdp.empty())
+    if ((m.varl || m.st) && !m.xdp.empty())
       main += "s_cmp_lg_u32 " + m.xdp + ", 0\ns_cbranch_scc0 .L" + P + "noxdp\n" + xdp_shift() +
               ".L" + P + "noxdp:\n";
     main += stack_zero() + stack_init(P, ool);
@@ -3907,7 +3911,8 @@ bool compile_into_template(Compiler& c, Compiler* xc, std::vector<char>& code_ob
     // (stack-window programs: the fixed-slot kernel and the var kernel's stack statement; other
     // programs: every statement but that one)
     if (loop_marker != (xc != nullptr) || (loop_marker && m.deep != deep) ||
-        (c.stk ? !(m.stack || (!loop_marker && m.fixed == "1" && !c.stk->any_dyn)) : m.stack) ||
+        (c.stk ? !(m.stack || (!loop_marker && m.fixed == "1" && (!c.stk->any_dyn || m.st)))
+               : m.stack) ||
         (m.occ && (c.stk || !occ_wanted(c.n)))) {
       b = "s_mov_b64 exec, 0  ; (not this program's kernel)\n";
       continue;

@@ -431,7 +431,7 @@ def test_stack_window_fuzz_var(cuda, oracle_mod, layout):
         got, xdp = _run_var(img, pkts, cuda, VAR_LAYOUTS[layout])
         assert got["kernel"] in (_lib.EBPF_KERNEL_JIT_VAR_STACK, _lib.EBPF_KERNEL_JIT_VARL_STACK,
                                  _lib.EBPF_KERNEL_JIT_LOOP_STACK, _lib.EBPF_KERNEL_GENERAL_T1)
-        n_stack += got["kernel"] in (_lib.EBPF_KERNEL_JIT_VAR_STACK, _lib.EBPF_KERNEL_JIT_VARL_STACK)
+        n_stack += got["kernel"] in (_lib.EBPF_KERNEL_JIT_VAR_STACK, _lib.EBPF_KERNEL_JIT_VARL_STACK, _lib.EBPF_KERNEL_JIT_STACK)
         ref, _ = _run_var(img, pkts, cuda, VAR_LAYOUTS[layout], generic=True)
         assert ref["kernel"] == _lib.EBPF_KERNEL_GENERAL_T1
         ok = got["status"] != 7  # (ST_BADPKT lanes have no registers: main.rs:20-21 panics)
@@ -458,7 +458,7 @@ def test_stack_workloads_var(cuda, oracle_mod, layout):
         pkts = _var_packets(rng, 150)
         got, xdp = _run_var(img, pkts, cuda, VAR_LAYOUTS[layout])
         # (offsets + lens: the var tile loop's stack statement; stride + lens the var kernel's)
-        assert got["kernel"] in (_lib.EBPF_KERNEL_JIT_VAR_STACK, _lib.EBPF_KERNEL_JIT_VARL_STACK), src
+        assert got["kernel"] in (_lib.EBPF_KERNEL_JIT_VAR_STACK, _lib.EBPF_KERNEL_JIT_VARL_STACK, _lib.EBPF_KERNEL_JIT_STACK), src
         ref, _ = _run_var(img, pkts, cuda, VAR_LAYOUTS[layout], generic=True)
         for key in ("status", "verdict", "counters"):
             assert np.array_equal(got[key], ref[key]), (key, layout, src)
@@ -572,7 +572,7 @@ def test_stack_loop_programs(cuda, oracle_mod, layout):
             got, xdp = _run_var(img, pkts, cuda, VAR_LAYOUTS[layout], max_steps=steps)
             if it == 2 and steps == 3000:  # (forward, budget that cannot bind: forward kernels)
                 assert got["kernel"] in (_lib.EBPF_KERNEL_JIT_VAR_STACK,
-                                         _lib.EBPF_KERNEL_JIT_VARL_STACK), layout
+                                         _lib.EBPF_KERNEL_JIT_VARL_STACK, _lib.EBPF_KERNEL_JIT_STACK), layout
             else:
                 # (the route of the production outputs: a promoted program's own loop kernel,
                 # test_promote.py; every output asked for below runs the stack loop kernel)

@@ -176,7 +176,7 @@ def test_far_store_fuzz(cuda, oracle_mod, layout):
         lens = [0, 14, 60, 64, 65, 127, 128, 200, 700, 1000, 1400, 1499, 1500]
         pkts = [bytes(rng.getrandbits(8) for _ in range(rng.choice(lens))) for _ in range(150)]
         kid, _ = _run_checked(oracle_mod, img, pkts, cuda, layout, tag=f"{layout} {it}")
-        assert kid == _lib.EBPF_KERNEL_JIT_VARL_STACK, (layout, it, kid)
+        assert kid in (_lib.EBPF_KERNEL_JIT_VARL_STACK, _lib.EBPF_KERNEL_JIT_STACK), (layout, it, kid)
         done += 1
     assert done >= 6, done
 
@@ -197,7 +197,7 @@ def test_responder_vs_oracle(cuda, oracle_mod, layout):
     kid, w = _run_checked(oracle_mod, W.program("responder"), pkts, cuda, layout,
                           expect_no_deopt="no pass" if layout == "fixed1504" else "empty pass",
                           tag=layout)
-    assert kid == _lib.EBPF_KERNEL_JIT_VARL_STACK
+    assert kid in (_lib.EBPF_KERNEL_JIT_VARL_STACK, _lib.EBPF_KERNEL_JIT_STACK)
 
 
 @pytest.mark.gpu

@@ -134,7 +134,7 @@ def test_store_mode_fuzz(cuda, oracle_mod, layout):
         if sm:
             # (the var tile loop's stack statement where the layout allows, else the var kernel's)
             assert got["kernel"] in (_lib.EBPF_KERNEL_JIT_VAR_STACK,
-                                     _lib.EBPF_KERNEL_JIT_VARL_STACK), (layout, img.hex())
+                                     _lib.EBPF_KERNEL_JIT_VARL_STACK, _lib.EBPF_KERNEL_JIT_STACK), (layout, img.hex())
             n_sm += 1
         else:
             assert got["kernel"] in (_lib.EBPF_KERNEL_JIT_STACK, _lib.EBPF_KERNEL_JIT_VAR_STACK,
@@ -159,7 +159,7 @@ def test_nat_rewrite_vs_oracle(cuda, oracle_mod, layout):
     rng = random.Random(5150 + len(layout))
     pkts = _nat_packets(rng, 3000)
     got, xdp, pk = _run_layout(img, pkts, cuda, layout)
-    assert got["kernel"] in (_lib.EBPF_KERNEL_JIT_VAR_STACK, _lib.EBPF_KERNEL_JIT_VARL_STACK)
+    assert got["kernel"] in (_lib.EBPF_KERNEL_JIT_VAR_STACK, _lib.EBPF_KERNEL_JIT_VARL_STACK, _lib.EBPF_KERNEL_JIT_STACK)
     ref, _, _ = _run_layout(img, pkts, cuda, layout, generic=True)
     _check(oracle_mod, img, pk, got, ref, xdp, f"nat {layout}")
     # the workload exercised every path: TX (redirected), PASS, DROP (under xdp_md the program,
@@ -234,7 +234,7 @@ def test_nat_long_options_no_deopt(cuda, oracle_mod, layout):
     ws = torch.full((prog.workspace_bytes(b, 0),), 0x55, dtype=torch.uint8, device=cuda)
     ws[:512 + 64 * 8 * 8] = 0  # (launch.h: the deopt words and counter shards start zeroed)
     b = prog.make_batch(frames, xdp_md=xdp, workspace=ws, **kw)
-    assert prog.batch_kernel(b) == _lib.EBPF_KERNEL_JIT_VARL_STACK
+    assert prog.batch_kernel(b) in (_lib.EBPF_KERNEL_JIT_VARL_STACK, _lib.EBPF_KERNEL_JIT_STACK)
     out = _lib.BatchOut()
     r0 = torch.empty(len(pk), dtype=torch.int64, device=cuda)
     st = torch.empty(len(pk), dtype=torch.uint8, device=cuda)
@@ -310,7 +310,7 @@ def test_deopt_list_rerun(cuda, oracle_mod, layout):
         pk = pkts
         frames, kw = _stage(pkts, cuda, **VAR_LAYOUTS[layout])
     b = prog.make_batch(frames, r10=128, **kw)
-    assert prog.batch_kernel(b) == _lib.EBPF_KERNEL_JIT_VARL_STACK
+    assert prog.batch_kernel(b) in (_lib.EBPF_KERNEL_JIT_VARL_STACK, _lib.EBPF_KERNEL_JIT_STACK)
     ws = torch.zeros(prog.workspace_bytes(b, 0), dtype=torch.uint8, device=cuda)
     b = prog.make_batch(frames, r10=128, workspace=ws, **kw)
     gcnt = torch.zeros(8, dtype=torch.int64, device=cuda)
@@ -406,7 +406,7 @@ def test_straddling_loads_no_deopt(cuda, oracle_mod, layout):
     b = prog.make_batch(frames, xdp_md=xdp, **kw)
     ws = torch.zeros(prog.workspace_bytes(b, 0), dtype=torch.uint8, device=cuda)
     b = prog.make_batch(frames, xdp_md=xdp, workspace=ws, **kw)
-    assert prog.batch_kernel(b) == _lib.EBPF_KERNEL_JIT_VARL_STACK
+    assert prog.batch_kernel(b) in (_lib.EBPF_KERNEL_JIT_VARL_STACK, _lib.EBPF_KERNEL_JIT_STACK)
     out = _lib.BatchOut()
     r0 = torch.empty(len(pk), dtype=torch.int64, device=cuda)
     st = torch.empty(len(pk), dtype=torch.uint8, device=cuda)
@@ -468,7 +468,7 @@ def test_no_deopt_proof_fuzz(cuda, oracle_mod, layout):
             frames, kw = _stage(pkts, cuda, **VAR_LAYOUTS[layout])
         for r10 in (512, 100):
             b = prog.make_batch(frames, r10=r10, **kw)
-            if prog.batch_kernel(b) != _lib.EBPF_KERNEL_JIT_VARL_STACK:
+            if prog.batch_kernel(b) not in (_lib.EBPF_KERNEL_JIT_VARL_STACK, _lib.EBPF_KERNEL_JIT_STACK):
                 break
             ws = torch.zeros(prog.workspace_bytes(b, 0), dtype=torch.uint8, device=cuda)
             b = prog.make_batch(frames, r10=r10, workspace=ws, **kw)
