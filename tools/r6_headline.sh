@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 6: the headline (5-tuple, 1 Mi x 64 B, ebpf_tile_jit_fixed) -- one launch's kernel trace
+# Round 6: the headline (5-tuple, 1 Mi x 64 B, ebpf_tile_jit_fixed_occ since late round 6) -- one launch's kernel trace
 # at one stream, the two-stream union (the bench line's per-batch time), the per-wave stamp
 # breakdown (EBPFEMU_TRACE=1: ramp, tiles, last-tile spread, counter tail) with and without the
 # counters, and driver-style 20-step lines. Outputs under gpurun_out/r6_head/. Every GPU step
