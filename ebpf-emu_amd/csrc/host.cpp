@@ -819,6 +819,68 @@ static std::vector<DUop> fold_const_loads(const std::vector<Uop>& uops, std::vec
 // where there is one (then the program is forward-only again), the chain that falls off the end
 // last. Fails (the general interpreter's frame stack runs the program) on recursion, more than
 // kJitMaxUops pairs, or two chains falling off the end.
+// Loop-invariant bound loads peeled (load time, every kernel but the general interpreter's):
+//   H: ldx rN, [rB + off]      H+1: j<cc> rI, rN -> X      B: ...      J: ja H      X: (J + 1)
+// -- a loop testing its bound at the top and reloading it every iteration, as an XDP program
+// re-reading ctx->data_end -- becomes
+//   H: ldx rN, [rB + off]      H+1: j<cc> rI, rN -> X      B: ...      nop      nop
+//   j<!cc> rI, rN -> B         X
+// when B holds no jump, store, call or exit and writes neither rN nor rB (rB != rN), and nothing
+// else jumps into H+1 .. J. The reload rewrote rN with the value it held (same address, memory
+// unchanged; a narrow load keeps rN's high bytes either way), so every step leaves the registers
+// exactly as the original's step did -- the two nops retire the ja and the reload, the back edge
+// the test -- while the loop becomes one block with its test at the bottom: a counted loop for the
+// compiler (jit.cpp counted_entry: byte passes, the cooperative sums). Step counts are unchanged.
+static void peel_invariant_loads(std::vector<Uop>& u) {
+  auto neg = [](uint8_t op) -> int {
+    switch (op) {
+      case U_JGE: return U_JLT; case U_JLT: return U_JGE; case U_JGT: return U_JLE;
+      case U_JLE: return U_JGT; case U_JEQ: return U_JNE; case U_JNE: return U_JEQ;
+      case U_JGE32: return U_JLT32; case U_JLT32: return U_JGE32; case U_JGT32: return U_JLE32;
+      case U_JLE32: return U_JGT32; case U_JEQ32: return U_JNE32; case U_JNE32: return U_JEQ32;
+      default: return -1;
+    }
+  };
+  for (const Uop& o : u)
+    if (o.op == U_CALL) return;
+  for (uint32_t J = 2; J < u.size(); J++) {
+    const uint32_t n = (uint32_t)u.size();
+    if (u[J].op != U_JA || (uint32_t)u[J].x >= J) continue;
+    const uint32_t H = (uint32_t)u[J].x;
+    if (H + 2 > J) continue;
+    const Uop &ld = u[H], &jt = u[H + 1];
+    if (ld.op != U_LDX || ld.dst == ld.src || ld.dst > 10 || ld.src > 10) continue;
+    if (neg(jt.op) < 0 || !(jt.aux & F_SRC) || (uint32_t)jt.x != J + 1) continue;
+    const uint8_t rN = ld.dst, rB = ld.src;
+    if (!((jt.src == rN && jt.dst != rN) || (jt.dst == rN && jt.src != rN))) continue;
+    bool ok = true;
+    for (uint32_t i = H + 2; i < J && ok; i++) {
+      const Uop& b = u[i];
+      const bool writes = (b.op <= U_BSWAP64 && b.op != U_NOP) || b.op == U_LDIMM || b.op == U_LDX;
+      ok = b.op <= U_BSWAP64 || b.op == U_LDIMM || b.op == U_LDX;
+      if (writes && (b.dst == rN || b.dst == rB)) ok = false;
+    }
+    for (uint32_t i = 0; i < n && ok; i++) {  // no other way into H+1 .. J
+      const Uop& b = u[i];
+      if (b.op < U_JA || b.op > U_JLE32 || i == J) continue;
+      const uint32_t x = (uint32_t)b.x;
+      if (x > H && x <= J) ok = false;
+    }
+    if (!ok) continue;
+    // the shift: every jump target past J moves 2 on
+    for (Uop& b : u)
+      if (b.op >= U_JA && b.op <= U_JLE32 && (uint32_t)b.x > J) b.x = (int32_t)((uint32_t)b.x + 2);
+    Uop nop{};
+    nop.op = U_NOP;
+    Uop back = u[H + 1];
+    back.op = (uint8_t)neg(back.op);
+    back.x = (int32_t)(H + 2);
+    u[J] = nop;
+    u.insert(u.begin() + J + 1, {nop, back});
+    J += 2;
+  }
+}
+
 static bool flatten_calls(const std::vector<Uop>& u, std::vector<Uop>& out) {
   const uint32_t n = (uint32_t)u.size();
   if (n == 0) return false;
@@ -1303,6 +1365,7 @@ int ebpf_prog_load(const uint8_t* code, size_t nbytes, ebpf_prog** out, size_t* 
       p->flattened = true;
     }
   }
+  if (p->xuops.size() + 2 <= kJitMaxUops) peel_invariant_loads(p->xuops);
   const std::vector<Uop>& xu = p->xuops;
   for (const Uop& u : xu)
     if (u.op == U_ST || u.op == U_STX || u.op == U_ATOMIC || u.op == U_CALL) p->xtier = 1;
