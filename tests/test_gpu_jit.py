@@ -195,6 +195,23 @@ def test_xdp_ctx_data_folded():
 
 
 # ---------------------------------------------------------------------------------------------
+_PROG = {}  # the last program _run loaded (the compiled, the no-JIT and the production runs of
+# one image share it: one load and module upload instead of three)
+
+
+def _prog(img):
+    from ebpf_emu import Program
+
+    if img not in _PROG:
+        for q in _PROG.values():
+            q.close()
+        _PROG.clear()
+        q = Program(img)
+        assert q.compile()
+        _PROG[img] = q
+    return _PROG[img]
+
+
 def _run(img, pkts, dev, fixed_stride=None, offsets_layout=False, init_regs=None, no_jit=False,
          mem_size=1024, r10=512, prod=False):
     """prod: the production outputs only -- a verdict + counters launch (k_flags = 0) and an r0 +
@@ -202,11 +219,9 @@ def _run(img, pkts, dev, fixed_stride=None, offsets_layout=False, init_regs=None
     register init (;@@JITINIT@@, jit.cpp live_in) instead of initialising every register."""
     import torch
 
-    from ebpf_emu import Program
     from test_gpu_parity import _stage
 
-    prog = Program(img)
-    assert prog.compile()
+    prog = _prog(img)
     if fixed_stride:  # no lens: every packet is `fixed_stride` bytes (the fixed-slot layout)
         buf = np.zeros(len(pkts) * fixed_stride, dtype=np.uint8)
         for i, p in enumerate(pkts):
@@ -228,7 +243,6 @@ def _run(img, pkts, dev, fixed_stride=None, offsets_layout=False, init_regs=None
         torch.cuda.synchronize()
         out = dict(status=rs.status.cpu().numpy(), r0=rs.r0.cpu().numpy().view(np.uint64),
                    verdict=v.verdict.cpu().numpy(), counters=cnt.cpu().numpy().view(np.uint64))
-        prog.close()
         return out
     res = prog.run(frames, mem_size=mem_size, r10=r10, max_steps=STEPS, verdict=True, r0=True,
                    status=True, regs=True, counters=cnt, init_regs=ir, no_jit=no_jit, **kw)
@@ -236,7 +250,6 @@ def _run(img, pkts, dev, fixed_stride=None, offsets_layout=False, init_regs=None
     out = dict(status=res.status.cpu().numpy(), r0=res.r0.cpu().numpy().view(np.uint64),
                verdict=res.verdict.cpu().numpy(), regs=res.regs.cpu().numpy().view(np.uint64),
                counters=cnt.cpu().numpy().view(np.uint64))
-    prog.close()
     return out
 
 
