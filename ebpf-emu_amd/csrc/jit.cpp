@@ -436,8 +436,48 @@ struct Compiler {
   // execution order in a forward program and every empty-exec skip lands on a target entry (the
   // mask's lanes re-admitted there). A lane's LPC keeps its last parked value, below every later
   // entry, so no LPC compare re-admits it.
+  // Complement targets (cm_assign): cm_of[T] = 1 when T's region [R, T) -- R the target before
+  // it -- holds only register ALU work, jumps and exits, and every jump into T comes from inside
+  // it. Then the lanes reaching T are exactly the region's entry set minus the lanes that left it
+  // for elsewhere: kept in P = s[72:73] (set at R's entry, lanes subtracted where they leave for
+  // another target or exit), and a test whose leaving lanes go to T only drops them from exec
+  // (one v_cmpx: cmpx_pass). A rule chain's tests lose their SALU mask updates.
+  std::vector<char> cm_of, cm_start;
+  bool cm_any = false;
+  void cm_assign(const std::vector<uint32_t>& first) {
+    cm_of.assign(n + 1, 0);
+    cm_start.assign(n + 1, 0);
+    cm_any = false;
+    uint32_t R = 0;
+    for (uint32_t T = 1; T < n; T++) {
+      if (!target[T]) continue;
+      bool ok = first[T] != UINT32_MAX && first[T] >= R;
+      for (uint32_t i = R; i < T && ok; i++) {
+        const Uop& u = uops[i];
+        const bool div = u.op == U_DIV64 || u.op == U_MOD64 || u.op == U_DIV32 || u.op == U_MOD32;
+        ok = (u.op <= U_BSWAP64 && !div) || u.op == U_LDIMM || is_jump(u) || u.op == U_EXIT;
+      }
+      if (ok) {
+        cm_of[T] = 1;
+        if (!cm_of[R]) cm_start[R] = 1;
+        cm_any = true;
+      }
+      R = T;
+    }
+  }
+  // micro-op i lies in a complement target's region: that target (else 0)
+  uint32_t cm_region(uint32_t i) const {
+    if (!cm_any || i >= n) return 0;
+    const uint32_t T = next_target(i);
+    return T < n && cm_of[T] ? T : 0;
+  }
+  static constexpr const char* kCmP = "s[72:73]";
+
   void pm_assign(const Marker& m) {
     pm_of.assign(n + 1, -1);
+    cm_of.assign(n + 1, 0);
+    cm_start.assign(n + 1, 0);
+    cm_any = false;
     if (!m.pm || loops || stk) return;
     std::vector<uint32_t> first(n + 1, UINT32_MAX);
     for (uint32_t i = 0; i < n; i++) {
@@ -447,13 +487,14 @@ struct Compiler {
       if (x < n && x != i + 1) first[x] = std::min(first[x], i);
       if (uops[i].op != U_JA && np < n && np != i + 1) first[np] = std::min(first[np], i);
     }
+    cm_assign(first);
     std::vector<uint32_t> busy_until(kPmPairs, 0);  // a pair is free after its target's entry
     std::vector<uint32_t> order;
     for (uint32_t T = 1; T < n; T++)
-      if (target[T] && first[T] != UINT32_MAX) order.push_back(T);
+      if (target[T] && first[T] != UINT32_MAX && !cm_of[T]) order.push_back(T);
     std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return first[a] < first[b]; });
     for (uint32_t T : order)
-      for (int k = 0; k < kPmPairs; k++)
+      for (int k = cm_any ? 1 : 0; k < kPmPairs; k++)
         if (busy_until[k] <= first[T]) {
           busy_until[k] = T;
           pm_of[T] = k;
@@ -1054,6 +1095,28 @@ struct Compiler {
     // 64), then exec
     std::string pre;
     const std::string mx = x_done ? "" : pm_reg(x), mn = n_done ? "" : pm_reg(np);
+    if (const uint32_t CT = cm_region(i)) {
+      // complement region: lanes leaving for CT are only dropped from exec; lanes leaving for
+      // another target or finishing are recorded there (mask or LPC) and taken out of P
+      const bool xl = !x_next, nl = !n_next;  // which side leaves
+      std::string s;
+      if (xl && x != CT) {
+        if (!mx.empty()) s += "s_or_b64 " + mx + ", " + mx + ", vcc\n";
+        s += std::string("s_andn2_b64 ") + kCmP + ", " + kCmP + ", vcc\n";
+      }
+      if (nl && np != CT) {
+        s += "s_andn2_b64 s[64:65], exec, vcc\n";
+        if (!mn.empty()) s += "s_or_b64 " + mn + ", " + mn + ", s[64:65]\n";
+        s += std::string("s_andn2_b64 ") + kCmP + ", " + kCmP + ", s[64:65]\n";
+      }
+      const std::string lx = xl && x != CT && mx.empty() ? vop3_lpc(lpc_of(x, x_done), "v37", pre) : "",
+                        ln = nl && np != CT && mn.empty() ? vop3_lpc(lpc_of(np, n_done), "v38", pre) : "";
+      if (!lx.empty() || !ln.empty())
+        s += pre + "v_cndmask_b32_e64 v28, " + (ln.empty() ? "v28" : ln) + ", " +
+             (lx.empty() ? "v28" : lx) + ", vcc\n";
+      if (xl && nl) return s + "s_mov_b64 exec, 0\n";
+      return s + (xl ? "s_andn2_b64 exec, exec, vcc\n" : "s_and_b64 exec, exec, vcc\n");
+    }
     if (n_next && !mx.empty())  // taken lanes leave into their target's mask
       return "s_or_b64 " + mx + ", " + mx + ", vcc\n"  // (a VOPC result: 0 in inactive lanes)
              "s_andn2_b64 exec, exec, vcc\n";
@@ -1097,8 +1160,13 @@ struct Compiler {
     const uint32_t x = t[i].x;
     if (x == i + 1) return "";
     const std::string mx = x >= n ? "" : pm_reg(x);
-    if (!mx.empty()) return "s_or_b64 " + mx + ", " + mx + ", exec\ns_mov_b64 exec, 0\n";
-    return park(std::to_string(x), x >= n) + "s_mov_b64 exec, 0\n";
+    std::string out = "";
+    if (const uint32_t CT = cm_region(i)) {
+      if (x == CT) return "s_mov_b64 exec, 0\n";
+      out = std::string("s_andn2_b64 ") + kCmP + ", " + kCmP + ", exec\n";
+    }
+    if (!mx.empty()) return out + "s_or_b64 " + mx + ", " + mx + ", exec\ns_mov_b64 exec, 0\n";
+    return out + park(std::to_string(x), x >= n) + "s_mov_b64 exec, 0\n";
   }
 
   // Expand the tokens of one template text for micro-op i.
@@ -1142,7 +1210,10 @@ struct Compiler {
         } else if (tok == "JA") {
           o += ja(i, P);
         } else if (tok == "EXIT") {
-          o += loops ? "v_mov_b32 v28, -1\ns_mov_b64 exec, 0\n" : "s_mov_b64 exec, 0\n";
+          o += loops ? "v_mov_b32 v28, -1\ns_mov_b64 exec, 0\n"
+               : cm_region(i) ? std::string("s_andn2_b64 ") + kCmP + ", " + kCmP +
+                                    ", exec\ns_mov_b64 exec, 0\n"
+                              : "s_mov_b64 exec, 0\n";
         } else if (tok[0] == 'D' || tok[0] == 'S') {
           const uint32_t base = tok[0] == 'D' ? u.dst2 : u.src2;
           if (base > 20) {
@@ -2440,7 +2511,9 @@ struct Compiler {
         const std::string pm = pm_reg(i);
         // (every lane parked here is in the mask; with exec empty, one instruction takes the mask
         // into exec and clears it: mask = exec = 0, exec = old mask | 0)
-        if (!pm.empty())
+        if (i < cm_of.size() && cm_of[i])  // (a complement target: the region's survivors)
+          main += std::string("s_mov_b64 exec, ") + kCmP + "\n";
+        else if (!pm.empty())
           main += i > 0 && clears_exec(i - 1)
                       ? "s_or_saveexec_b64 " + pm + ", " + pm + "\n"
                       : "s_or_b64 exec, exec, " + pm + "\ns_mov_b64 " + pm + ", 0\n";
@@ -2456,7 +2529,9 @@ struct Compiler {
         // (a mask target whose block is register ALU work and a jump runs it with an empty exec
         // instead of skipping: nothing happens, its jump's own skip follows -- one instruction
         // less per rule of a rule chain, whose masks are seldom empty)
-        if (!(pm_reg(i).size() && alu_block(i)))
+        if (i < cm_start.size() && cm_start[i])  // (the start of a complement region)
+          main += std::string("s_mov_b64 ") + kCmP + ", exec\n";
+        if (!((pm_reg(i).size() || (i < cm_of.size() && cm_of[i])) && alu_block(i)))
           main += far_mode && nt - i > kFarSkipUops ? jmp("execz", skip)
                                                     : "s_cbranch_execz " + skip + "\n";
         if (loops && hoist[i] != -2) main += "v_mov_b32 v28, " + std::to_string(hoist[i]) + "\n";
@@ -3494,7 +3569,7 @@ struct Compiler {
       }
       out += ln[i] + "\n";
     }
-    return negate_leave(sink_high_zero(narrow_compares(out)));
+    return cmpx_pass(negate_leave(sink_high_zero(narrow_compares(out))));
   }
 
   // A register's high half zeroed just before a jump (`v_mov_b32 vH, 0` of a fused mov + and,
@@ -3532,6 +3607,42 @@ struct Compiler {
           out.push_back("s_or_b64 " + std::string(pm) + ", " + pm + ", vcc");
           out.push_back("s_andn2_b64 exec, exec, vcc");
           i += 2;
+          continue;
+        }
+      }
+      out.push_back(ln[i]);
+    }
+    std::string r;
+    for (const std::string& l : out) r += l + "\n";
+    return r;
+  }
+
+  // A compare into vcc whose only use is the exec update right after it (comments between):
+  // `v_cmp_<op> vcc, ..` + `s_and_b64 exec, exec, vcc` -> `v_cmpx_<op> vcc, ..`, and with
+  // `s_andn2_b64 exec, exec, vcc` the negated compare -- the tests of a complement region
+  // (cm_assign), one VALU instruction each.
+  static std::string cmpx_pass(const std::string& text) {
+    std::vector<std::string> ln;
+    for (size_t p = 0; p < text.size();) {
+      size_t e = text.find('\n', p);
+      if (e == std::string::npos) e = text.size();
+      ln.push_back(text.substr(p, e - p));
+      p = e + 1;
+    }
+    static const std::map<std::string, std::string> neg = {
+        {"eq", "ne"}, {"ne", "eq"}, {"gt", "le"}, {"le", "gt"}, {"ge", "lt"}, {"lt", "ge"}};
+    std::vector<std::string> out;
+    out.reserve(ln.size());
+    for (size_t i = 0; i < ln.size(); i++) {
+      const bool an = ln[i] == "s_andn2_b64 exec, exec, vcc", a = ln[i] == "s_and_b64 exec, exec, vcc";
+      if (an || a) {
+        size_t c = out.size();
+        while (c > 0 && !out[c - 1].empty() && out[c - 1][0] == ';') c--;
+        char op[8], ty[8];
+        if (c > 0 && sscanf(out[c - 1].c_str(), "v_cmp_%2[a-z]_%3[a-z0-9] vcc, ", op, ty) == 2 &&
+            neg.count(op) && out[c - 1].find("_e64") == std::string::npos &&
+            out[c - 1].compare(0, 6 + strlen(op) + 1 + strlen(ty), std::string("v_cmp_") + op + "_" + ty) == 0) {
+          out[c - 1] = "v_cmpx_" + (an ? neg.at(op) : std::string(op)) + out[c - 1].substr(6 + strlen(op));
           continue;
         }
       }

@@ -79,8 +79,12 @@ def test_pending_masks_in_rule_chains():
     p = Program(W.program("acl_rules"))
     p.compile()
     b = _occ_body(p.jit_asm(1))
+    # (a rule's entry: its mask -- or, its region holding only register work, the region's
+    # survivors in s[72:73], jit.cpp cm_assign; its tests then one v_cmpx each)
     entries = len(re.findall(r"^s_or_saveexec_b64 (s\[7[2-9]:7[3-9]\]), \1$", b, re.M))
+    entries += len(re.findall(r"^s_mov_b64 exec, s\[72:73\]$", b, re.M))
     assert entries >= 128, entries  # (one per rule, in each copy)
+    assert len(re.findall(r"^v_cmpx_", b, re.M)) >= 256
     assert not re.search(r"^v_cmpx_eq_u32 vcc, \d+, v28$", b, re.M)
     sg = [int(x) for x in re.findall(r"(?<![\w.])s\[?(\d+)", b)]
     assert max(sg) <= 79, max(sg)
