@@ -1115,7 +1115,10 @@ struct Compiler {
         s += pre + "v_cndmask_b32_e64 v28, " + (ln.empty() ? "v28" : ln) + ", " +
              (lx.empty() ? "v28" : lx) + ", vcc\n";
       if (xl && nl) return s + "s_mov_b64 exec, 0\n";
-      return s + (xl ? "s_andn2_b64 exec, exec, vcc\n" : "s_and_b64 exec, exec, vcc\n");
+      // (`; cmx`: cmpx_pass may fold the compare and this update into one v_cmpx -- only here,
+      // where nothing reads vcc after it: a negated v_cmpx leaves vcc negated)
+      return s + (s.empty() ? "; cmx\n" : "") +
+             (xl ? "s_andn2_b64 exec, exec, vcc\n" : "s_and_b64 exec, exec, vcc\n");
     }
     if (n_next && !mx.empty())  // taken lanes leave into their target's mask
       return "s_or_b64 " + mx + ", " + mx + ", vcc\n"  // (a VOPC result: 0 in inactive lanes)
@@ -3635,7 +3638,7 @@ struct Compiler {
     out.reserve(ln.size());
     for (size_t i = 0; i < ln.size(); i++) {
       const bool an = ln[i] == "s_andn2_b64 exec, exec, vcc", a = ln[i] == "s_and_b64 exec, exec, vcc";
-      if (an || a) {
+      if ((an || a) && i > 0 && ln[i - 1] == "; cmx") {  // (the marker itself is dropped below)
         size_t c = out.size();
         while (c > 0 && !out[c - 1].empty() && out[c - 1][0] == ';') c--;
         char op[8], ty[8];
@@ -3646,6 +3649,7 @@ struct Compiler {
           continue;
         }
       }
+      if (ln[i] == "; cmx") continue;
       out.push_back(ln[i]);
     }
     std::string r;
