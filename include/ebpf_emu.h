@@ -184,7 +184,7 @@ int ebpf_prog_stack_window(const ebpf_prog* prog);
 
 /* Store mode: ST/STX through a register whose value is not known at load time (a packet pointer
  * behind a variable-length header; reference emu.rs:354-372). Such a program runs on the compiled
- * var kernels with its header window in LDS; a lane whose access leaves the image bytes the kernel
+ * fixed-slot kernel (fixed slots) or the var kernels with its header window in LDS; a lane whose access leaves the image bytes the kernel
  * holds is re-run by the general interpreter after the launch (the deopt pass). 0 = not store
  * mode, 1 = store mode with the deopt pass, 2 = store mode proven at load time to need no pass
  * for main.rs-layout batches (no lane can leave; a lane that did would fault EBPF_ST_JIT); -1 for
@@ -241,7 +241,8 @@ int ebpf_run_batch(ebpf_prog* prog, const ebpf_batch* batch, const ebpf_batch_ou
 #define EBPF_KERNEL_JIT_FIXED  5  /* compiled program, fixed-slot layout (ebpf_tile_jit_fixed) */
 #define EBPF_KERNEL_JIT_VAR    6  /* compiled program, other layouts (ebpf_tile_jit_var) */
 #define EBPF_KERNEL_JIT_LOOP   7  /* compiled loop program (ebpf_tile_jit_loop) */
-#define EBPF_KERNEL_JIT_STACK  8  /* compiled stack-window program (memory tier 0.5, fixed slots) */
+#define EBPF_KERNEL_JIT_STACK  8  /* compiled stack-window program (memory tier 0.5, fixed slots;
+                                    store mode included) */
 #define EBPF_KERNEL_JIT_VAR_STACK 9  /* compiled stack-window program, other layouts
                                         (ebpf_tile_jit_var_stack) */
 #define EBPF_KERNEL_JIT_LOOP_STACK 10 /* compiled stack-window loop program
@@ -250,9 +251,10 @@ int ebpf_run_batch(ebpf_prog* prog, const ebpf_batch* batch, const ebpf_batch_ou
                                     (ebpf_tile_jit_varl; offsets and lens 4-byte aligned, no
                                     final images) */
 #define EBPF_KERNEL_JIT_VARL_STACK 12 /* the var tile loop for stack-window programs
-                                         (ebpf_tile_jit_varl_stack; not store mode) */
-#define EBPF_KERNEL_JIT_FIXED_OCC 13 /* compiled program, fixed-slot layout, occupancy variant for
-                                        issue-bound programs (ebpf_tile_jit_fixed_occ) */
+                                         (ebpf_tile_jit_varl_stack; store mode included) */
+#define EBPF_KERNEL_JIT_FIXED_OCC 13 /* compiled forward program, fixed-slot layout: the kernel's
+                                        occupancy variant (ebpf_tile_jit_fixed_occ; every program
+                                        whose code fits it, not xdp_md, no stack window) */
 int ebpf_batch_kernel(ebpf_prog* prog, const ebpf_batch* batch, const ebpf_batch_out* out,
                       int device);
 
