@@ -1427,7 +1427,7 @@ s_cbranch_scc1 .Linitx%=
 .Linitd%=:
 
 ; JIT N=%= fixed=%[fixed] loops=%[loops] aligned=%[aligned] xdp=%[xdpf] pm=1""" + (
-        " occ=1" if single else " st=1 ovf=%[k_ovf] tile=%[tile] dm=s[78:79]") + """
+        " occ=1 waves=%[wpb]" if single else " st=1 ovf=%[k_ovf] tile=%[tile] dm=s[78:79]") + """
 ;@@JIT@@
 .Ldone%=:
 """ + ("" if single else STORE_DEOPT_FIXED) + """; verdict byte, the lane's counter bucket (verdict 0..4, 0xfe -> 5, 0xff -> 6) into %[acc]

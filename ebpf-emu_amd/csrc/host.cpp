@@ -1606,7 +1606,7 @@ int ebpf_prog_upload(ebpf_prog* p, int device) {
           p->jit_fn[device][v].loop = p->jit_fn[device][v].loop_deep;     // deep-prefetch kernel)
         // (store mode runs on the fixed-slot statement too since round 6: gen_tile.py st=1)
         p->jit_fn[device][v].var_only = false;
-        if (!p->jit_occ[v]) p->jit_fn[device][v].fixed_occ = nullptr;
+        if (!p->jit_occ[v]) p->jit_fn[device][v].fixed_occ = p->jit_fn[device][v].fixed_occw = nullptr;
       }
   }
   TUop* tp = nullptr;

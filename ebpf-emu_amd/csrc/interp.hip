@@ -1992,6 +1992,10 @@ extern "C" __global__ __launch_bounds__(kDbBlock, 1) void ebpf_tile_jit_fixed(La
 extern "C" __global__ __launch_bounds__(kOccBlock, kOccWgsPerCu) void ebpf_tile_jit_fixed_occ(LaunchArgs a) {
   fixed_body<kOccWaves, true>(a);
 }
+extern "C" __global__ __launch_bounds__(kOccWideBlock, kOccWideWgsPerCu) void ebpf_tile_jit_fixed_occw(
+    LaunchArgs a) {
+  fixed_body<kOccWideWaves, true>(a);
+}
 extern "C" __global__ __launch_bounds__(kBlock, 7) void ebpf_tile_jit_var(LaunchArgs a) {
   tile_body<false, false, true>(a);
 }
@@ -2447,11 +2451,13 @@ hipError_t launch_interp(int kind, const LaunchArgs& a, int grid, hipStream_t st
     e = hipModuleLaunchKernel(stack ? jit->varl_stack : jit->varl, grid, 1, 1, kBlock, 1, 1, llds,
                               stream, bargs, nullptr);
   } else if (fixed_occ_ok(kind, a, jit, stack)) {  // one window buffer, 6 waves per SIMD
-    const uint32_t olds = kOccWaves * kWinBytes;
-    e = hipModuleLaunchKernel(jit->fixed_occ,
-                              jit_grid(jit->fixed_occ, olds, a.n_tiles, kOccBlock, true,
-                                       kOccWgsPerCu), 1, 1,
-                              kOccBlock, 1, 1, olds, stream, bargs, nullptr);
+    const bool wide = a.n_uops >= kOccWideUops;  // (jit.cpp compiled the code into that one)
+    hipFunction_t f = wide ? jit->fixed_occw : jit->fixed_occ;
+    const uint32_t ob = wide ? kOccWideBlock : kOccBlock;
+    const uint32_t olds = (wide ? kOccWideWaves : kOccWaves) * kWinBytes;
+    e = hipModuleLaunchKernel(f, jit_grid(f, olds, a.n_tiles, ob, true,
+                                          wide ? kOccWideWgsPerCu : kOccWgsPerCu), 1, 1,
+                              ob, 1, 1, olds, stream, bargs, nullptr);
   } else if (jit && jit->fixed && jit_forward_for(kind, a.n_uops)) {
     if (jit_fixed_layout(&a) && !jit->var_only) {  // double-buffered windows: its own LDS size and grid
       const uint32_t dlds = kDbWaves * kTileWaveLdsDb;

@@ -20,6 +20,7 @@
 // amd_comgr, and loaded with hipModuleLoadData. Results are bit-identical to the interpreter's
 // (the same instruction sequences); tests/test_gpu_jit.py checks both against the oracle.
 #include "jit.h"
+#include "launch.h"  // (kOccWideWaves, kOccWideUops)
 
 #include <amd_comgr/amd_comgr.h>
 
@@ -70,6 +71,7 @@ struct Marker {
                        // preloaded window, only v[0:55] for the program's code
   bool pm = false;     // the statement gives the body s[72:79] (the pending masks, pm_assign)
   bool st = false;     // the fixed-slot statement's store mode (body_store, with ovf / tile / dm)
+  std::string waves;   // the occupancy statements' waves per workgroup (8: _occ, 12: _occw)
   bool varl = false;   // the var tile loop's statement (ebpf_tile_jit_varl): the var flavour of
                        // loads with the preloaded window, as the stack statement's
   // the var tile loop's store-mode state (gen_tile.py jit_statement_varl): the SGPR pair of
@@ -122,6 +124,7 @@ bool find_markers(const std::string& s, std::vector<Marker>& out) {
     m.varl = field("varl=") == "1";
     m.occ = field("occ=") == "1";
     m.pm = field("pm=") == "1";
+    m.waves = field("waves=");
     m.st = field(" st=") == "1";
     m.ovf = field("ovf=");
     m.tile = field("tile=");
@@ -4028,7 +4031,8 @@ bool compile_into_template(Compiler& c, Compiler* xc, std::vector<char>& code_ob
     if (loop_marker != (xc != nullptr) || (loop_marker && m.deep != deep) ||
         (c.stk ? !(m.stack || (!loop_marker && m.fixed == "1" && (!c.stk->any_dyn || m.st)))
                : m.stack) ||
-        (m.occ && (c.stk || !occ_wanted(c.n)))) {
+        (m.occ && (c.stk || !occ_wanted(c.n) ||
+                   (m.waves == std::to_string(kOccWideWaves)) != (c.n >= kOccWideUops)))) {
       b = "s_mov_b64 exec, 0  ; (not this program's kernel)\n";
       continue;
     }
@@ -4268,7 +4272,8 @@ bool jit_load(const std::vector<char>& co, hipModule_t* mod, JitFns* fns) {
       hipModuleGetFunction(&f.loop_deep, m, "ebpf_tile_jit_loop_deep") != hipSuccess ||
       hipModuleGetFunction(&f.varl, m, "ebpf_tile_jit_varl") != hipSuccess ||
       hipModuleGetFunction(&f.varl_stack, m, "ebpf_tile_jit_varl_stack") != hipSuccess ||
-      hipModuleGetFunction(&f.fixed_occ, m, "ebpf_tile_jit_fixed_occ") != hipSuccess) {
+      hipModuleGetFunction(&f.fixed_occ, m, "ebpf_tile_jit_fixed_occ") != hipSuccess ||
+      hipModuleGetFunction(&f.fixed_occw, m, "ebpf_tile_jit_fixed_occw") != hipSuccess) {
     (void)hipModuleUnload(m);
     return false;
   }

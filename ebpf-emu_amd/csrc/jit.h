@@ -25,6 +25,7 @@ struct JitFns {
   // the fixed-slot layout's occupancy variant (ebpf_tile_jit_fixed_occ: issue-bound programs, one
   // window buffer per wave); null unless this program's code went there (jit_compile *occ)
   hipFunction_t fixed_occ = nullptr;
+  hipFunction_t fixed_occw = nullptr;  // its wide form (launch.h kOccWideUops)
   // the program's code exists for the var kernels only (store mode: register-address stores into
   // the packet, StackPlan::any_dyn), whatever the batch layout
   bool var_only = false;

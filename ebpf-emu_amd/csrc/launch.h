@@ -20,6 +20,14 @@ constexpr int kDbBlock = kDbWaves * kWave;
 constexpr int kOccWaves = 8;
 constexpr int kOccBlock = kOccWaves * kWave;
 constexpr int kOccWgsPerCu = 3;
+// its wide form (ebpf_tile_jit_fixed_occw): 2 workgroups of 12 waves per CU -- the same 6 waves per
+// SIMD in fewer, larger workgroups -- for programs of at least kOccWideUops micro-ops (the rule
+// chains: 53 -> 57 Gpkt/s at two streams for acl_rules, while the 5-tuple's line drops 106 -> 101
+// on it: DESIGN 3.35). jit.cpp gives each program's code to the one of the two its length picks.
+constexpr int kOccWideWaves = 12;
+constexpr int kOccWideBlock = kOccWideWaves * kWave;
+constexpr int kOccWideWgsPerCu = 2;
+constexpr uint32_t kOccWideUops = 256;
 constexpr int kWin = 64;              // packet bytes staged in LDS per lane (header window)
 constexpr int kWinStride = kWin + 4;  // padded per-lane LDS stride: 17 dwords, conflict-free b32
 constexpr int kMaxLdsUops = 4096;     // programs up to this many micro-ops are staged in LDS

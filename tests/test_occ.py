@@ -7,8 +7,9 @@ window buffer per wave (the next tile is claimed and DMA'd when the current one 
 gen_tile.py jit_statement_loop(single=True)) and compiles the program without the preloaded
 window (only v[0:55]), so 3 workgroups of 8 waves fit a CU: 6 waves per SIMD.
 Every forward program takes it (jit.cpp occ_wanted; programs of >= 96 micro-ops only until late in
-round 6) when its code fits the registers (occ_regs_ok) and the batch is not xdp_md. The reference runs every program through one step() (emu.rs:452-458): outputs
-must not change, only the kernel.
+round 6) when its code fits the registers (occ_regs_ok) and the batch is not xdp_md; programs of
+>= 256 micro-ops its 12-wave form (ebpf_tile_jit_fixed_occw, same kernel id). The reference runs
+every program through one step() (emu.rs:452-458): outputs must not change, only the kernel.
 
 CPU: which programs get the variant's code, and that the code names only the statement's
 registers. GPU: the route, and every output == the general interpreter == the oracle, including
@@ -25,18 +26,19 @@ NOT_HERE = "(not this program's kernel)"
 
 
 def _occ_body(text):
-    """The occupancy statement's compiled code (None if the program has none there)."""
-    m = re.search(r"; JIT N=(\d+) [^\n]*occ=1\n", text)
-    if not m:
-        return None
-    n = m.group(1)
-    head = text[m.end():text.index(f".Ldone{n}:", m.end())]
-    if NOT_HERE in head or "needs more registers" in head:
-        return None
-    if "out of line" in head:  # far mode: behind the kernel's code
-        k = text.index(f".Lbody{n}:")
-        return text[k:text.index("\n.Lfunc_end", k)]
-    return head
+    """The occupancy statements' compiled code (None if the program has none there): the 8-wave
+    form's (ebpf_tile_jit_fixed_occ) or, for programs of >= launch.h kOccWideUops micro-ops, the
+    12-wave form's (ebpf_tile_jit_fixed_occw)."""
+    for m in re.finditer(r"; JIT N=(\d+) [^\n]*occ=1[^\n]*\n", text):
+        n = m.group(1)
+        head = text[m.end():text.index(f".Ldone{n}:", m.end())]
+        if NOT_HERE in head or "needs more registers" in head:
+            continue
+        if "out of line" in head:  # far mode: behind the kernel's code
+            k = text.index(f".Lbody{n}:")
+            return text[k:text.index("\n.Lfunc_end", k)]
+        return head
+    return None
 
 
 def test_occ_routing():
@@ -132,7 +134,8 @@ def test_occ_vs_oracle(cuda, oracle_mod, name, n):
 
 
 @pytest.mark.gpu
-def test_occ_statement_reentry(cuda, oracle_mod):
+@pytest.mark.parametrize("name", ["acl", "acl_rules"])  # (the 8- and the 12-wave form)
+def test_occ_statement_reentry(cuda, oracle_mod, name):
     """A grid capped to 2 workgroups (EBPFEMU_FIXED_WGS): each wave runs > 511 tiles, so it
     re-enters the statement with its next tile's window already in flight (first = 0)."""
     import subprocess
@@ -145,7 +148,7 @@ def test_occ_statement_reentry(cuda, oracle_mod):
         "from ebpf_emu import Program, _lib, workloads as W\n"
         "n = 16 * 600 * 64 + 5\n"
         "buf = W.frames_fixed(n, 64, 11)\n"
-        "img = W.program('acl')\n"
+        f"img = W.program({name!r})\n"
         "p = Program(img)\n"
         "fr = torch.from_numpy(buf).cuda()\n"
         "assert _lib.KERNEL_NAMES[p.batch_kernel(p.make_batch(fr, n=n, stride=64))].startswith('ebpf_tile_jit_fixed_occ')\n"
