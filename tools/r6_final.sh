@@ -26,6 +26,8 @@ for cfg in 5tuple acl_rules nat checksum_xdp_reload; do b s1 --config $cfg --str
 bash tools/prof.sh r6_5tuple_occ_s1 --config 5tuple --steps 200 --warmup 20
 bash tools/pmc.sh 5tuple_occ --config 5tuple --streams 1
 python3 tools/pmc_summary.py gpurun_out/pmc/5tuple_occ ebpf_tile_jit_fixed_occ > gpurun_out/pmc/5tuple_occ.json
+bash tools/pmc.sh acl_rules_occw --config acl_rules --streams 1
+python3 tools/pmc_summary.py gpurun_out/pmc/acl_rules_occw ebpf_tile_jit_fixed_occw > gpurun_out/pmc/acl_rules_occw.json
 bash tools/pmc.sh drop_occ --config drop --streams 1
 python3 tools/pmc_summary.py gpurun_out/pmc/drop_occ ebpf_tile_jit_fixed_occ > gpurun_out/pmc/drop_occ.json
 echo done
