@@ -51,12 +51,24 @@ def _stage(pkts, dev, stride=None, offsets_layout=False, misalign=0, align=1):
     return frames, dict(n=len(pkts), stride=stride, lens=ln)
 
 
-def _run_full(prog_img, pkts, dev, mem_size=1024, r10=512, max_steps=STEPS, generic=False,
-              **layout):
+_PROG = {}  # the last image's loaded program, shared by its full, generic and production runs
+
+
+def _shared(img):
     from ebpf_emu import Program
 
+    if img not in _PROG:
+        for q in _PROG.values():
+            q.close()
+        _PROG.clear()
+        _PROG[img] = Program(img)
+    return _PROG[img]
+
+
+def _run_full(prog_img, pkts, dev, mem_size=1024, r10=512, max_steps=STEPS, generic=False,
+              **layout):
     torch = _torch()
-    prog = Program(prog_img)
+    prog = _shared(prog_img)
     frames, kw = _stage(pkts, dev, **layout)
     cnt = torch.zeros(8, dtype=torch.int64, device=dev)
     res = prog.run(frames, mem_size=mem_size, r10=r10, max_steps=max_steps, verdict=True, r0=True,
@@ -66,7 +78,6 @@ def _run_full(prog_img, pkts, dev, mem_size=1024, r10=512, max_steps=STEPS, gene
                verdict=res.verdict.cpu().numpy(), regs=res.regs.cpu().numpy().view(np.uint64),
                mem=res.mem.cpu().numpy(), counters=cnt.cpu().numpy().view(np.uint64),
                tier=prog.tier, fast=prog.forward_only and not generic and max_steps >= len(prog))
-    prog.close()
     return out
 
 
@@ -75,10 +86,8 @@ def _run_prod(prog_img, pkts, dev, mem_size=1024, r10=512, max_steps=STEPS, **la
     the kernels take their production paths -- the compiled programs' liveness-pruned register
     init (jit.cpp live_in, ;@@JITINIT@@) and, for a verdict-only launch, the k_flags = 0 epilogue.
     Two launches: verdict + counters only, then r0 + status (still without registers)."""
-    from ebpf_emu import Program
-
     torch = _torch()
-    prog = Program(prog_img)
+    prog = _shared(prog_img)
     frames, kw = _stage(pkts, dev, **layout)
     cnt = torch.zeros(8, dtype=torch.int64, device=dev)
     v = prog.run(frames, mem_size=mem_size, r10=r10, max_steps=max_steps, verdict=True,
@@ -88,7 +97,6 @@ def _run_prod(prog_img, pkts, dev, mem_size=1024, r10=512, max_steps=STEPS, **la
     torch.cuda.synchronize()
     out = dict(verdict=v.verdict.cpu().numpy(), counters=cnt.cpu().numpy().view(np.uint64),
                r0=rs.r0.cpu().numpy().view(np.uint64), status=rs.status.cpu().numpy())
-    prog.close()
     return out
 
 
