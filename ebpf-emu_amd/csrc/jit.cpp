@@ -1525,10 +1525,29 @@ struct Compiler {
     // the block's 16 dwords in flight at once, into v[64:79] (free in store mode: the chunk
     // cache is invalidated around every call, ldxk_lds)
     for (uint32_t k = 0; k < 16; k++) r += "v_mov_b32 v" + std::to_string(64 + k) + ", 0\n";
-    for (uint32_t k = 0; k < 16; k++)
-      r += "v_cmp_lt_i32 vcc, " + std::to_string(4 * k) + ", v48\ns_and_b64 exec, s[64:65], vcc\n"
-           "global_load_dword v" + std::to_string(64 + k) + ", v[46:47], off offset:" +
-           std::to_string(4 * k) + "\n";
+    // a chunk wholly before LEN: one 16-byte load; the chunk LEN falls in: its dwords that start
+    // before LEN (the rest stay 0; nothing at or past the dword holding LEN - 1 is read)
+    for (uint32_t c = 0; c < 4; c++) {
+      const std::string C = std::to_string(c), Q = "v[" + std::to_string(64 + 4 * c) + ":" +
+                                                    std::to_string(67 + 4 * c) + "]";
+      // (every compare under the routine's whole exec: a VOPC result is 0 in inactive lanes)
+      r += "s_mov_b64 exec, s[64:65]\n"
+           "v_cmp_le_i32 vcc, " + std::to_string(16 * c + 16) + ", v48\n"
+           "s_and_b64 exec, s[64:65], vcc\n"
+           "global_load_dwordx4 " + Q + ", v[46:47], off offset:" + std::to_string(16 * c) + "\n"
+           "s_mov_b64 exec, s[64:65]\n"
+           "v_cmp_gt_i32 vcc, " + std::to_string(16 * c + 16) + ", v48\n"
+           "s_and_b64 exec, s[64:65], vcc\n"
+           "v_cmp_lt_i32 vcc, " + std::to_string(16 * c) + ", v48\n"
+           "s_and_b64 exec, exec, vcc\n"
+           "s_cbranch_execz .Lovc" + C + "_" + ovl_tag + "\n"
+           "s_mov_b64 s[48:49], exec\n";  // (s[48:49]: free once ovf_addr has used it)
+      for (uint32_t k = 4 * c; k < 4 * c + 4; k++)
+        r += "v_cmp_lt_i32 vcc, " + std::to_string(4 * k) + ", v48\ns_and_b64 exec, s[48:49], vcc\n"
+             "global_load_dword v" + std::to_string(64 + k) + ", v[46:47], off offset:" +
+             std::to_string(4 * k) + "\n";
+      r += ".Lovc" + C + "_" + ovl_tag + ":\n";
+    }
     r += "s_mov_b64 exec, s[64:65]\ns_waitcnt vmcnt(0)\n";
     for (uint32_t k = 0; k < 16; k++)
       r += "v_subrev_u32 v50, " + std::to_string(4 * k) + ", v48\n"
